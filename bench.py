@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the reference's headline metric on MI355X.
+
+metric : "2D slices/sec fwd+bwd, 256x256x1 batch32 U-Net; Dice vs ref"  (BASELINE.json)
+step   : one training step of PMU/train.py:85-110 on one batch of synthetic 256x256x1 slices:
+         UNet(1,1,[64,128,256,512,1024]) forward -> BCELoss -> backward -> (all-reduce) ->
+         clip_grad_value_(0.1) + SGD(momentum 0.9), all on the HIP path (model.UNet + FusedSGD).
+N GPUs : one process per GPU (torch.distributed.run), 32 slices per GPU (weak scaling), one
+         RCCL all-reduce of the flat gradient buffer per step.
+
+Prints ONE JSON line on rank 0.  `roofline` is the dominant MFMA kernel family timed with HIP
+events on the launch stream during one instrumented step after the timed region;
+`cpu_baseline` times the CPU oracle (oracle/unet_ref.py, a torch-CPU restatement of the
+reference) on a bounded sample, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "probabilistic-multiplanar-unet_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+METRIC = "2D slices/sec fwd+bwd, 256×256×1 batch32 U-Net; Dice vs ref"
+FP32_MFMA_PEAK_TF = 157.3
+FILTERS = [64, 128, 256, 512, 1024]
+
+
+def conv_flops_per_slice(H, W, filters, n_ch=1, n_cls=1):
+    """Algorithmic FLOPs per slice: 2 x MACs x (fwd + dgrad + wgrad) over every conv, convT and
+    the 1x1 head, without the first layer's dgrad."""
+    fl = 0.0
+    h, w = H, W
+    levels = []
+    for i, f in enumerate(filters):
+        cin = n_ch if i == 0 else filters[i - 1]
+        first = 9 * h * w * cin * f * 2          # conv1 fwd
+        fl += first * (2 if i == 0 else 3)
+        fl += 9 * h * w * f * f * 2 * 3           # conv2
+        levels.append((h, w))
+        h, w = h // 2, w // 2
+    for i in reversed(range(len(filters) - 1)):
+        hi, wi = levels[i + 1]
+        cin = filters[i + 1]
+        fl += hi * wi * cin * (cin // 2) * 4 * 2 * 3          # convT 2x2
+        hs, ws = levels[i]
+        fl += 9 * hs * ws * (cin) * filters[i] * 2 * 3        # up conv1 (concat input = cin channels)
+        fl += 9 * hs * ws * filters[i] * filters[i] * 2 * 3   # up conv2
+    fl += H * W * filters[0] * n_cls * 2 * 3                  # outc
+    return fl
+
+
+class KernelTimer:
+    """HIP-event timing of every launch, with algorithmic FLOPs for the MFMA kernels."""
+
+    MFMA = ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad", "pmu_convT2x2_fwd",
+            "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad")
+
+    def __init__(self):
+        self.rec = []
+
+    @staticmethod
+    def _flops(name, args):
+        if name in ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad"):
+            f = args[0]._obj
+            cframe = sum(f.src[i].C for i in range(f.nsrc))
+            if name == "pmu_conv3x3_fwd":
+                cin, cout = cframe, args[3]
+            elif name == "pmu_conv3x3_dgrad":
+                cout, cin = cframe, args[2]
+            else:
+                a = args[1]._obj
+                cin, cout = sum(a.src[i].C for i in range(a.nsrc)), args[2]
+            return 2.0 * f.N * f.H * f.W * cin * cout * 9
+        if name == "pmu_convT2x2_fwd":
+            f = args[0]._obj
+            cin = sum(f.src[i].C for i in range(f.nsrc))
+            return 2.0 * f.N * f.H * f.W * cin * args[3] * 4
+        if name == "pmu_convT2x2_dgrad":
+            N, H, W, cin, cout = args[6], args[7], args[8], args[9], args[10]
+            return 2.0 * N * H * W * cin * cout * 4
+        if name == "pmu_convT2x2_wgrad":
+            a = args[5]._obj
+            cin = sum(a.src[i].C for i in range(a.nsrc))
+            return 2.0 * a.N * a.H * a.W * cin * args[6] * 4
+        return 0.0
+
+    def __call__(self, name, args, e0, e1):
+        self.rec.append((name, self._flops(name, args), e0, e1))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        per = {}
+        for name, fl, e0, e1 in self.rec:
+            t = e0.elapsed_time(e1) * 1e-3
+            d = per.setdefault(name, [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += fl
+            d[2] += t
+        return per
+
+
+def cpu_baseline(max_seconds=25.0):
+    """CPU oracle (torch-CPU restatement of the reference) on a bounded sample: batch 2 of the c2
+    geometry, 1 warm-up + timed steps (fwd+bwd+clip+SGD) until ~max_seconds."""
+    from oracle.unet_ref import unet_train_step
+    from model import UNet
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    sd = {k: v.clone() for k, v in UNet(1, 1, FILTERS).state_dict().items()}
+    g = torch.Generator().manual_seed(1)
+    B = 2
+    x = torch.rand(B, 1, 256, 256, generator=g)
+    t = (torch.rand(B, 1, 256, 256, generator=g) > 0.5).float()
+    from oracle.unet_ref import unet_param_keys
+    bufs = {k: torch.zeros_like(sd[k]) for k in unet_param_keys(sd)}
+    unet_train_step(sd, x, t, 5, 1, lr=1e-3, bufs=bufs)  # warm-up
+    times = []
+    t_end = time.perf_counter() + max_seconds
+    while True:
+        t0 = time.perf_counter()
+        unet_train_step(sd, x, t, 5, 1, lr=1e-3, bufs=bufs)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() > t_end or len(times) >= 5:
+            break
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": round(B / med, 4), "unit": "slices/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/unet_ref.py torch-CPU, c2 geometry (256x256x1, filters {FILTERS}), batch {B}, "
+                      f"median of {len(times)} fwd+bwd+clip+SGD steps after 1 warm-up, {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--classes", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from model import UNet
+    from pmu_hip import _lib as L
+    from pmu_hip.functions import flat_grad_buffer
+    from pmu_hip.optim import FusedSGD
+
+    torch.manual_seed(0)
+    net = UNet(1, args.classes, FILTERS).to(dev).train()
+    if world > 1:  # identical replicas: broadcast rank 0's weights
+        for t in list(net.parameters()) + list(net.buffers()):
+            dist.broadcast(t.data, 0)
+    opt = FusedSGD(net.parameters(), lr=1e-3, momentum=0.9, clip=0.1)
+    g = torch.Generator(device="cpu").manual_seed(1 + rank)
+    B, S = args.batch, args.size
+    x = torch.rand(B, 1, S, S, generator=g).to(dev)
+    if args.classes == 1:
+        tgt = (torch.rand(B, 1, S, S, generator=g) > 0.5).float().to(dev)
+        crit = nn.BCELoss()
+    else:
+        tgt = torch.randint(0, args.classes, (B, S, S), generator=g).to(dev)
+        crit = nn.CrossEntropyLoss()
+    plist = list(net.parameters())
+
+    def step():
+        for p in plist:
+            p.grad = None
+        out = net(x)
+        loss = crit(out, tgt)
+        loss.backward()
+        if world > 1:
+            dist.all_reduce(flat_grad_buffer(net, plist))
+        opt.step(grad_scale=1.0 / world)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt)
+    ms = dt / args.steps * 1e3
+    value = world * B * args.steps / dt
+
+    flops_step = conv_flops_per_slice(S, S, FILTERS, 1, args.classes) * B
+    roof = None
+    kernels = None
+    if not args.no_kernel_timing:
+        timer = KernelTimer()
+        L.set_call_observer(timer)
+        step()
+        L.set_call_observer(None)
+        per = timer.summary()
+        mf = {k: v for k, v in per.items() if k in KernelTimer.MFMA}
+        dom = max(mf, key=lambda k: mf[k][2])
+        n, fl, t = mf[dom]
+        ach = fl / t / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TF,
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+                "launches": n, "avg_launch_ms": round(t / n * 1e3, 4), "flops_per_launch": fl / n}
+        kernels = {k: {"launches": v[0], "ms": round(v[2] * 1e3, 3),
+                       "tflops": (round(v[1] / v[2] / 1e12, 2) if v[1] else None)} for k, v in sorted(per.items())}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": round(value, 3), "unit": "slices/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (x~U[0,1), random binary masks, seeded)",
+            "config": {"workload": "c2: UNet(n_channels=1, n_classes=%d, num_filters=%s), %dx%dx1 slices, "
+                                   "fwd+BCE+bwd+clip(0.1)+SGD(0.9) per step" % (args.classes, FILTERS, S, S),
+                       "global_batch": B * world, "per_gpu_batch": B, "image": [S, S], "parallelism": f"dp{world}"},
+            "step_tflops": round(flops_step / (ms * 1e-3) / 1e12, 2),
+            "step_mfma_frac": round(flops_step / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4),
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "loss": float(loss),
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,180 @@
+/*
+ * pmunet_hip.h — C ABI of libpmunet_hip.so, the MI355X (gfx950) hot path of the
+ * Probabilistic Multi-Planar U-Net.
+ *
+ * The reference (qzs634/Probabilistic-Multiplanar-Unet) has no FFI: its hot path is
+ * PyTorch module code.  Each entry point below replaces the PyTorch operator(s) the
+ * reference calls at the cited line (PMU/ = Probabilistic-Multiplanar-Unet/):
+ *
+ *   pmu_conv3x3_fwd      nn.Conv2d(3x3,pad 1)+bias, with the producer's BatchNorm2d(train/eval)
+ *                        + ReLU (+MaxPool2d(2) | AvgPool2d(2,ceil) | F.pad+torch.cat) fused
+ *                        into the operand load     PMU/model/unet/unet_parts.py:15-20,33,52-66
+ *                                                  PMU/model/probabilistic_unet/probabilistic_unet.py:36-44
+ *   pmu_conv3x3_dgrad    autograd of the above w.r.t. its input (BN-backward fused in the load)
+ *   pmu_conv3x3_wgrad    autograd of the above w.r.t. its weight (split-K, deterministic)
+ *   pmu_conv_first_fwd / _wgrad   the Cin<=4 first layer of UNet / prior / posterior
+ *   pmu_convT2x2_fwd/_dgrad/_wgrad  nn.ConvTranspose2d(k2,s2)        unet_parts.py:52
+ *   pmu_bn_*             BatchNorm2d batch statistics, running-stat update, backward coefficients
+ *   pmu_maxpool2_bwd / pmu_avgpool2_bwd                              unet_parts.py:33, probabilistic_unet.py:36
+ *   pmu_head1x1_fwd/_bwd, pmu_wgrad1x1   OutConv + sigmoid           unet_parts.py:70-76, unet_model.py:48-49
+ *   pmu_sgd_clip         clip_grad_value_(0.1) + SGD(momentum)        PMU/train.py:65,108-110
+ *   pmu_dice_counts      dice_coeff + argmax/one-hot                  PMU/dice_loss.py:5-12, trainer/unet_trainer.py:39-58
+ *   pmu_slice3view       MRI_Dataset.pad_dimensions/sample_slice/preprocess  PMU/utils/mri_dataset.py:70-112
+ *   pmu_fuse3view        eval.py volume fusion                        PMU/eval.py:157-203
+ *   pmu_fcomb_*          Fcomb 1x1 chain with tiled z                 probabilistic_unet.py:116-181
+ *   pmu_spatial_mean / pmu_latent_head   AxisAlignedConvGaussian head probabilistic_unet.py:97-108
+ *
+ * Conventions
+ *   - All tensors are device pointers, fp32, activations stored channels-last (NHWC),
+ *     weights in PyTorch's native layouts ([Cout][Cin][3][3], ConvT [Cin][Cout][2][2]).
+ *   - Every call is asynchronous on the given hipStream_t (passed as void*), never
+ *     allocates, never synchronises, and is safe to capture in a hipGraph.
+ *   - Every call returns 0 on success, PMU_ERR_ARG for an invalid argument (checked
+ *     on the host before any launch), or the hipError_t of a failed launch.
+ *   - Reductions are deterministic: fixed-shape partial slabs, no float atomics.
+ */
+#ifndef PMUNET_HIP_H
+#define PMUNET_HIP_H
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMU_ABI_VERSION 1
+
+enum { PMU_OK = 0, PMU_ERR_ARG = 1001 };
+
+/* How one conv-input source turns stored values into operand values. */
+enum {
+  PMU_SRC_RAW = 0,    /* value = x                                                    */
+  PMU_SRC_BNRELU = 1, /* value = max(0, x*scale[c] + shift[c])        coef = [scale|shift]          */
+  PMU_SRC_BNBWD = 2   /* value = dL/dz of BN+ReLU: g=x*(z*scale+shift>0);
+                         scale*g + kx*(z-mean) + kc                   coef = [scale|shift|mean|kx|kc] */
+};
+enum { PMU_POOL_NONE = 0, PMU_POOL_MAX2 = 1, PMU_POOL_AVG2CEIL = 2 };
+
+typedef struct pmu_src {
+  const float* x;    /* NHWC [N][H][W][C]: raw values, pre-BN z, or upstream gradient */
+  const float* z;    /* PMU_SRC_BNBWD: pre-BN z, same shape as x; else NULL          */
+  const float* coef; /* per-channel coefficient block (see modes)                     */
+  int mode, pool;
+  int C, H, W;       /* stored tensor dims                                            */
+  int off_h, off_w;  /* top/left offset of the (pooled) source inside the frame (F.pad) */
+} pmu_src;
+
+/* A conv operand: one frame of N x H x W pixels whose channels are the concatenation
+ * of up to two sources (torch.cat([skip, up], 1) of unet_parts.py:66). */
+typedef struct pmu_frame {
+  pmu_src src[2];
+  int nsrc;
+  int N, H, W;
+} pmu_frame;
+
+/* ---- 3x3 convolution (implicit GEMM on MFMA, LDS halo tiles) -------------------- */
+/* z[N][H][W][Cout] = conv3x3(frame, w) + bias.  If part != NULL, per-tile BN partial
+ * sums (sum z, sum z^2) are written to part[tile][2][Cout]; pmu_conv3x3_tiles() gives
+ * the tile count. */
+int pmu_conv3x3_fwd(const pmu_frame* in, const float* w, const float* bias, int Cout,
+                    float* z, float* part, void* stream);
+int pmu_conv3x3_tiles(int N, int H, int W);
+/* dx = dL/d(frame) for frame channels [0,Csplit) -> dx0 (NHWC, Csplit ch) and
+ * [Csplit,Cin) -> dx1 (NHWC, Cin-Csplit ch).  dz is a frame whose single source is
+ * normally PMU_SRC_BNBWD. */
+int pmu_conv3x3_dgrad(const pmu_frame* dz, const float* w, int Cin, int Csplit,
+                      float* dx0, float* dx1, void* stream);
+/* dw[Cout][Cin][3][3] = dL/dw; ws must hold pmu_conv3x3_wgrad_ws() bytes. */
+size_t pmu_conv3x3_wgrad_ws(int N, int H, int W, int Cin, int Cout);
+int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int Cout, float* dw,
+                      float* ws, size_t ws_bytes, void* stream);
+
+/* ---- first layer (Cin <= 4, planes given NCHW-style, one pointer per channel) ------ */
+int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,
+                       const float* w, const float* bias, int Cout, float* z, float* part,
+                       void* stream);
+int pmu_conv_first_tiles(int N, int H, int W);
+size_t pmu_conv_first_wgrad_ws(int N, int H, int W, int Cin, int Cout);
+int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* planes, int Cin, int Cout,
+                         float* dw, float* ws, size_t ws_bytes, void* stream);
+
+/* ---- BatchNorm2d ------------------------------------------------------------------- */
+/* Column reduction of fp32 partials part[R][Wd] into fp64 partials out[G][Wd]. */
+int pmu_colsum_f64(const float* part, int R, int Wd, double* out, int G, void* stream);
+int pmu_colsum_groups(int R);
+/* From fp64 sums acc[G][2][C] (sum, sumsq) over count elements: mean, invstd, coef=[scale|shift];
+ * update running stats (unbiased var, momentum) when running_mean != NULL. */
+int pmu_bn_fwd_finalize(const double* acc, int G, int C, double count, const float* gamma,
+                        const float* beta, float eps, float momentum, float* running_mean,
+                        float* running_var, float* mean, float* invstd, float* coef, void* stream);
+/* Eval mode: coef from running stats. */
+int pmu_bn_eval_coef(const float* running_mean, const float* running_var, const float* gamma,
+                     const float* beta, float eps, int C, float* coef, void* stream);
+/* BN+ReLU backward reduction over da (NHWC) and z: part[tile][2][C] = (sum g, sum g*xhat). */
+int pmu_bn_bwd_reduce(const float* da, const float* z, const float* coef, const float* mean,
+                      const float* invstd, int P, int C, float* part, void* stream);
+int pmu_bn_bwd_tiles(int P, int C);
+/* From acc[G][2][C]: dgamma, dbeta, dbias(conv bias feeding BN) and the BNBWD coef block
+ * [scale|shift|mean|kx|kc]. */
+int pmu_bn_bwd_finalize(const double* acc, int G, int C, double count, const float* gamma,
+                        const float* coef, const float* mean, const float* invstd, float* dgamma,
+                        float* dbeta, float* dbias, float* bcoef, void* stream);
+
+/* out[P][C] = max(0, z*scale+shift) (NHWC), coef = [scale|shift]. */
+int pmu_bnrelu_apply(const float* z, const float* coef, long long P, int C, float* out, void* stream);
+
+/* ---- pooling backward ------------------------------------------------------------ */
+/* dx[N][H][W][C] += dpool routed to the first max (row-major) of each 2x2 window of
+ * relu(z*scale+shift).  accumulate=0 overwrites dx (zeros outside windows). */
+int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int N, int H, int W,
+                     int C, float* dx, int accumulate, void* stream);
+/* AvgPool2d(2,2,ceil_mode=True) backward: dx = dpool/count(window), overwrite. */
+int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream);
+
+/* ---- ConvTranspose2d(k=2, s=2) ---------------------------------------------------- */
+/* u[N][2H][2W][Cout] = convT(act(frame)) + bias, frame is N x H x W x Cin. */
+int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float* bias, int Cout, float* u,
+                     void* stream);
+/* dx[N][H][W][Cin] from du (NHWC [N][Hd][Wd][Cout], convT output placed at (off_h,off_w)). */
+int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, int off_w, const float* w,
+                       int N, int H, int W, int Cin, int Cout, float* dx, void* stream);
+size_t pmu_convT2x2_wgrad_ws(int N, int H, int W, int Cin, int Cout);
+int pmu_convT2x2_wgrad(const float* du, int Hd, int Wd, int off_h, int off_w,
+                       const pmu_frame* act, int Cout, float* dw, float* dbias, float* ws,
+                       size_t ws_bytes, void* stream);
+
+/* ---- 1x1 head (OutConv) -------------------------------------------------------------- */
+/* y[N][K][H][W] (NCHW) = w[K][C] . act(frame) + b; sigmoid applied when do_sigmoid. */
+int pmu_head1x1_fwd(const pmu_frame* in, const float* w, const float* b, int K, int do_sigmoid,
+                    float* y, void* stream);
+/* dl = dy * s*(1-s) (do_sigmoid) or dy; da[N][H][W][C] = w^T dl (NHWC); dl written (NCHW). */
+int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
+                    int N, int H, int W, float* dl, float* da, void* stream);
+size_t pmu_wgrad1x1_ws(int P, int K, int C);
+/* dw[K][C] = sum_p dl[p][k] act[p][c], db[k] = sum_p dl[p][k]; dl NCHW [N][K][H][W]. */
+int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float* dw, float* db, float* ws,
+                 size_t ws_bytes, void* stream);
+
+/* ---- optimizer --------------------------------------------------------------------- */
+/* Multi-tensor fused clip_grad_value_ + SGD(momentum, dampening 0, no nesterov):
+ *   g = clamp(gscale*g, -clip, clip) (clip <= 0: no clipping); buf = momentum*buf + g; p -= lr*buf.
+ * (buf starting at zero reproduces torch's first-step buf = g; gscale = 1/world_size turns an
+ * all-reduced gradient sum into the data-parallel mean before clipping.)
+ * ptrs: device array of 3*ntensors pointers (p, g, buf); chunks: device array, one block each. */
+typedef struct pmu_sgd_chunk {
+  int tensor; /* index into ptrs/3 */
+  int len;    /* elements in this chunk (<= 65536) */
+  long long start;
+} pmu_sgd_chunk;
+int pmu_sgd_clip(const pmu_sgd_chunk* chunks, int nchunks, void* const* ptrs, float gscale, float lr,
+                 float momentum, float clip, void* stream);
+
+/* ---- metrics ------------------------------------------------------------------------- */
+/* counts[k][3] = (sum pred_k*t_k, sum pred_k, sum t_k) for k < K, exact (integer-valued fp64).
+ * K==1: pred = (y > 0.5), t = mask.  K>1: pred = onehot(first argmax_c softmax(y)), t = (mask == k).
+ * y NCHW [N][K][H][W], mask [N][H][W]. */
+int pmu_dice_counts(const float* y, const float* mask, int N, int K, int H, int W,
+                    double* counts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,125 @@
+"""CPU oracle: functional restatement of the reference U-Net / Probabilistic U-Net math.
+
+TEST INFRASTRUCTURE ONLY.  Nothing under pmu_hip/, model/, trainer/ or the drivers imports
+this module; only tests/, __graft_entry__.smoke() and bench.py's ``cpu_baseline`` leg do.
+It is written from scratch on torch CPU functional ops and operates on a state_dict (the
+reference's key names), so it needs neither the reference code nor the HIP library.
+
+Parity is pinned: tests/test_oracle_golden.py checks this module against golden vectors that
+tests/golden/make_golden.py produced by importing the reference itself
+(PMU/ = /root/reference/Probabilistic-Multiplanar-Unet/).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def _bn(x, sd, pre, training, momentum=0.1, eps=1e-5):
+    """BatchNorm2d (PMU/model/unet/unet_parts.py:16,19): batch stats in training, running stats in eval.
+    Running stats in ``sd`` are updated in place (unbiased var, momentum 0.1)."""
+    rm, rv = sd[pre + "running_mean"], sd[pre + "running_var"]
+    y = F.batch_norm(x, rm, rv, sd[pre + "weight"], sd[pre + "bias"], training, momentum, eps)
+    if training and (pre + "num_batches_tracked") in sd:
+        sd[pre + "num_batches_tracked"] += 1
+    return y
+
+
+def double_conv(x, sd, pre, training):
+    """(conv3x3 pad1 -> BN -> ReLU) x 2  (unet_parts.py:14-21); Sequential indices 0,1,3,4."""
+    for i in (0, 3):
+        x = F.conv2d(x, sd[f"{pre}double_conv.{i}.weight"], sd[f"{pre}double_conv.{i}.bias"], padding=1)
+        x = F.relu(_bn(x, sd, f"{pre}double_conv.{i + 1}.", training))
+    return x
+
+
+def unet_forward(sd, x, n_levels, n_classes, apply_last_layer=True, training=True):
+    """UNet.forward (PMU/model/unet/unet_model.py:31-54).
+
+    n_levels = len(num_filters).  Down_i = MaxPool2d(2) + DoubleConv (unet_parts.py:31-34);
+    Up = ConvTranspose2d(k2,s2) -> F.pad to the skip size -> cat([skip, up]) -> DoubleConv
+    (unet_parts.py:52,58-66); up_blocks stored deepest-first (unet_model.py:29); skip of up
+    block i is xs[-(2 + 2i)] (:39)."""
+    xs = [double_conv(x, sd, "inc.", training)]
+    for i in range(n_levels - 1):
+        xs.append(double_conv(F.max_pool2d(xs[-1], 2), sd, f"down_blocks.{i}.maxpool_conv.1.", training))
+    for i in range(n_levels - 1):
+        x1, x2 = xs[-1], xs[-(2 + 2 * i)]
+        pre = f"up_blocks.{i}."
+        x1 = F.conv_transpose2d(x1, sd[pre + "up.weight"], sd[pre + "up.bias"], stride=2)
+        dy, dx = x2.shape[2] - x1.shape[2], x2.shape[3] - x1.shape[3]
+        x1 = F.pad(x1, [dx // 2, dx - dx // 2, dy // 2, dy - dy // 2])
+        xs.append(double_conv(torch.cat([x2, x1], dim=1), sd, pre + "conv.", training))
+    feat = xs[-1]
+    if not apply_last_layer:
+        return feat
+    out = F.conv2d(feat, sd["outc.conv.weight"], sd["outc.conv.bias"])
+    if n_classes == 1:
+        out = torch.sigmoid(out)
+    return out
+
+
+def unet_loss(out, target, n_classes):
+    """UNetTrainer.loss (PMU/trainer/unet_trainer.py:23,30-37): BCELoss(mean) on sigmoid
+    output for 1 class, CrossEntropyLoss(mean) with target.squeeze(1) otherwise."""
+    if n_classes == 1:
+        return F.binary_cross_entropy(out, target)
+    return F.cross_entropy(out, target.squeeze(1).long())
+
+
+def sgd_clip_step(params, grads, bufs, lr, momentum=0.9, clip=0.1):
+    """clip_grad_value_(0.1) + SGD(momentum, dampening 0) (PMU/train.py:65,108-110); bufs start at 0."""
+    for k in params:
+        g = grads[k].clamp(-clip, clip)
+        bufs[k] = momentum * bufs[k] + g
+        params[k] = params[k] - lr * bufs[k]
+
+
+def dice_coeff(pred, target):
+    """PMU/dice_loss.py:5-12: whole-batch Dice with smooth 1e-6."""
+    smooth = 0.000001
+    num = pred.size(0)
+    m1 = pred.reshape(num, -1)
+    m2 = target.reshape(num, -1)
+    inter = (m1 * m2).sum()
+    return (2. * inter + smooth) / (m1.sum() + m2.sum() + smooth)
+
+
+def trainer_dice(masks_pred, true_masks, n_classes):
+    """UNetTrainer.eval / ProbUNetTrainer.eval (unet_trainer.py:39-58): per-class Dice of the
+    softmax-argmax one-hot prediction (classes >= 1), or (pred > 0.5) for 1 class."""
+    if n_classes == 1:
+        return [float(dice_coeff((masks_pred > 0.5).float(), true_masks))]
+    probs = F.softmax(masks_pred, dim=1)
+    idx = torch.argmax(probs, 1, keepdim=True)
+    one_hot = torch.zeros_like(probs).scatter_(1, idx, 1)
+    return [float(dice_coeff(one_hot[:, k], (true_masks == k).float().squeeze(1)))
+            for k in range(1, one_hot.shape[1])]
+
+
+def unet_param_keys(sd):
+    """Trainable parameter keys of a U-Net state_dict in module registration order."""
+    return [k for k in sd if not (k.endswith("running_mean") or k.endswith("running_var")
+                                  or k.endswith("num_batches_tracked"))]
+
+
+def unet_train_step(sd, x, target, n_levels, n_classes, lr=None, bufs=None):
+    """One reference training step on CPU: forward, loss, backward (+ optional clip/SGD).
+    Returns (out, loss, grads) and updates sd's running stats (and params if lr)."""
+    keys = unet_param_keys(sd)
+    params = {k: sd[k].detach().clone().requires_grad_(True) for k in keys}
+    work = dict(sd)
+    work.update(params)
+    out = unet_forward(work, x, n_levels, n_classes)
+    loss = unet_loss(out, target, n_classes)
+    loss.backward()
+    grads = {k: params[k].grad.detach().clone() for k in keys}
+    for k in sd:
+        if k not in params:
+            sd[k] = work[k]
+    if lr is not None:
+        cur = {k: sd[k].detach() for k in keys}
+        sgd_clip_step(cur, grads, bufs, lr)
+        for k in keys:
+            sd[k] = cur[k]
+    return out.detach(), loss.detach(), grads

@@ -1,0 +1,612 @@
+// Memory-bound kernels of the hot path:
+//   BatchNorm2d batch statistics / running stats / backward coefficients
+//       (nn.BatchNorm2d in train and eval mode, PMU/model/unet/unet_parts.py:16,19,
+//        PMU/model/probabilistic_unet/probabilistic_unet.py:39,44)
+//   MaxPool2d(2) and AvgPool2d(2, ceil_mode=True) backward (unet_parts.py:33,
+//        probabilistic_unet.py:36)
+//   OutConv 1x1 + sigmoid forward / backward (unet_parts.py:70-76, unet_model.py:48-49)
+//   clip_grad_value_ + SGD(momentum) (PMU/train.py:65,108-110)
+//   dice_coeff counts with argmax/one-hot (PMU/dice_loss.py:5-12, trainer/unet_trainer.py:39-58)
+// All reductions write per-block partial slabs that are summed in a fixed order (fp64).
+#include "pmu_common.h"
+
+namespace {
+
+// ---------------- column sums: part[R][Wd] (f32) -> out[G][Wd] (f64) ----------------
+__global__ __launch_bounds__(256) void colsum_f64_kernel(const float* __restrict__ part, int R, int Wd,
+                                                         double* __restrict__ out, int G) {
+  __shared__ double red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int g = blockIdx.y;
+  const int r0 = (int)(((long long)R * g) / G), r1 = (int)(((long long)R * (g + 1)) / G);
+  double s = 0.0;
+  if (col < Wd)
+    for (int r = r0 + rl; r < r1; r += 4) s += (double)part[(long long)r * Wd + col];
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && col < Wd)
+    out[(long long)g * Wd + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+__global__ void bn_fwd_finalize_kernel(const double* __restrict__ acc, int G, int C, double count,
+                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                       float eps, float momentum, float* running_mean, float* running_var,
+                                       float* mean_out, float* invstd_out, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int g = 0; g < G; ++g) {
+    s1 += acc[((long long)g * 2 + 0) * C + c];
+    s2 += acc[((long long)g * 2 + 1) * C + c];
+  }
+  const double mean = s1 / count;
+  double var = s2 / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const double invstd = 1.0 / sqrt(var + (double)eps);
+  const double gm = gamma ? (double)gamma[c] : 1.0;
+  const double bt = beta ? (double)beta[c] : 0.0;
+  const float scale = (float)(gm * invstd);
+  coef[c] = scale;
+  coef[C + c] = (float)(bt - mean * gm * invstd);
+  mean_out[c] = (float)mean;
+  invstd_out[c] = (float)invstd;
+  if (running_mean) {
+    const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+    running_mean[c] = (float)((1.0 - momentum) * (double)running_mean[c] + momentum * mean);
+    running_var[c] = (float)((1.0 - momentum) * (double)running_var[c] + momentum * unb);
+  }
+}
+
+__global__ void bn_eval_coef_kernel(const float* rm, const float* rv, const float* gamma, const float* beta,
+                                    float eps, int C, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.f / sqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  coef[c] = g * inv;
+  coef[C + c] = b - rm[c] * g * inv;
+}
+
+// ---------------- BN + ReLU backward reduction ----------------
+// part[tile][2][C] = (sum g, sum g*xhat), g = da * (z*scale+shift > 0), xhat = (z-mean)*invstd
+constexpr int BNR_BYTES = 65536;  // bytes of one tensor per block
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ da, const float* __restrict__ z,
+                                                            const float* __restrict__ coef, const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, long long P, int C,
+                                                            int ppb, float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int tid = threadIdx.x;
+  const int CQ = C >> 2;
+  const int npg = CQ >= 256 ? 1 : 256 / CQ;
+  const int qstride = CQ >= 256 ? 256 : CQ;
+  const int pg = tid / qstride;
+  const int q0 = tid % qstride;
+  const long long p0 = (long long)blockIdx.x * ppb;
+  // each thread owns channel quads q0, q0+qstride, ... (only >1 when CQ > 256)
+  for (int q = q0; q < CQ; q += qstride) {
+    const int c = 4 * q;
+    const float4 sc = *reinterpret_cast<const float4*>(coef + c);
+    const float4 sh = *reinterpret_cast<const float4*>(coef + C + c);
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
+    if (pg < npg) {
+      for (int i = pg; i < ppb; i += npg) {
+        const long long p = p0 + i;
+        if (p >= P) break;
+        const float4 d = *reinterpret_cast<const float4*>(da + p * C + c);
+        const float4 zz = *reinterpret_cast<const float4*>(z + p * C + c);
+        const float dv[4] = {d.x, d.y, d.z, d.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
+        const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+        const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float g = fmaf(zv[e], scv[e], shv[e]) > 0.f ? dv[e] : 0.f;
+          sg[e] += g;
+          sgx[e] = fmaf(g, (zv[e] - muv[e]) * isv[e], sgx[e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { red[tid * 8 + e] = sg[e]; red[tid * 8 + 4 + e] = sgx[e]; }
+    __syncthreads();
+    if (pg == 0) {
+      float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
+      for (int l = 0; l < npg; ++l) {
+        const int src = l * qstride + q0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { t1[e] += red[src * 8 + e]; t2[e] += red[src * 8 + 4 + e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        part[((long long)blockIdx.x * 2 + 0) * C + c + e] = t1[e];
+        part[((long long)blockIdx.x * 2 + 1) * C + c + e] = t2[e];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ acc, int G, int C, double count,
+                                       const float* __restrict__ gamma, const float* __restrict__ coef,
+                                       const float* __restrict__ mean, const float* __restrict__ invstd,
+                                       float* dgamma, float* dbeta, float* dbias, float* bcoef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int g = 0; g < G; ++g) {
+    sg += acc[((long long)g * 2 + 0) * C + c];
+    sgx += acc[((long long)g * 2 + 1) * C + c];
+  }
+  const double is = invstd[c];
+  const double gm = gamma ? (double)gamma[c] : 1.0;
+  const double scale = gm * is;
+  const double c2 = sg / count, c3 = sgx / count;
+  const double kx = -scale * is * c3;
+  const double kc = -scale * c2;
+  if (dgamma) dgamma[c] = (float)sgx;
+  if (dbeta) dbeta[c] = (float)sg;
+  // sum_p dz = scale*sum g + kx*(sum z - n*mean) + n*kc ; sum z == n*mean by construction
+  if (dbias) dbias[c] = (float)(scale * sg + count * kc);
+  bcoef[c] = coef[c];
+  bcoef[C + c] = coef[C + c];
+  bcoef[2 * C + c] = mean[c];
+  bcoef[3 * C + c] = (float)kx;
+  bcoef[4 * C + c] = (float)kc;
+}
+
+// ---------------- pooling backward ----------------
+// grid-stride over dx elements in channel quads
+__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restrict__ dpool, const float* __restrict__ z,
+                                                           const float* __restrict__ coef, int N, int H, int W, int C,
+                                                           float* __restrict__ dx, int accumulate) {
+  const int CQ = C >> 2;
+  const int Hp = H / 2, Wp = W / 2;
+  const long long total = (long long)N * H * W * CQ;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(e % CQ);
+    long long p = e / CQ;
+    const int w = (int)(p % W);
+    const int h = (int)((p / W) % H);
+    const int n = (int)(p / ((long long)W * H));
+    const int c = 4 * q;
+    float4 o = accumulate ? *reinterpret_cast<const float4*>(dx + p * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int hp = h >> 1, wp = w >> 1;
+    if (hp < Hp && wp < Wp) {
+      const int me = ((h & 1) << 1) | (w & 1);
+      const float4 sc = *reinterpret_cast<const float4*>(coef + c);
+      const float4 sh = *reinterpret_cast<const float4*>(coef + C + c);
+      const long long b = (((long long)n * H + 2 * hp) * W + 2 * wp) * C + c;
+      const long long off[4] = {0, C, (long long)W * C, (long long)W * C + C};
+      float best[4];
+      int arg[4] = {0, 0, 0, 0};
+      {
+        const float4 v = *reinterpret_cast<const float4*>(z + b);
+        best[0] = fmaxf(0.f, fmaf(v.x, sc.x, sh.x)); best[1] = fmaxf(0.f, fmaf(v.y, sc.y, sh.y));
+        best[2] = fmaxf(0.f, fmaf(v.z, sc.z, sh.z)); best[3] = fmaxf(0.f, fmaf(v.w, sc.w, sh.w));
+      }
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float4 v = *reinterpret_cast<const float4*>(z + b + off[k]);
+        const float a0 = fmaxf(0.f, fmaf(v.x, sc.x, sh.x)), a1 = fmaxf(0.f, fmaf(v.y, sc.y, sh.y));
+        const float a2 = fmaxf(0.f, fmaf(v.z, sc.z, sh.z)), a3 = fmaxf(0.f, fmaf(v.w, sc.w, sh.w));
+        if (a0 > best[0]) { best[0] = a0; arg[0] = k; }
+        if (a1 > best[1]) { best[1] = a1; arg[1] = k; }
+        if (a2 > best[2]) { best[2] = a2; arg[2] = k; }
+        if (a3 > best[3]) { best[3] = a3; arg[3] = k; }
+      }
+      const float4 g = *reinterpret_cast<const float4*>(dpool + (((long long)n * Hp + hp) * Wp + wp) * C + c);
+      if (arg[0] == me) o.x += g.x;
+      if (arg[1] == me) o.y += g.y;
+      if (arg[2] == me) o.z += g.z;
+      if (arg[3] == me) o.w += g.w;
+    }
+    *reinterpret_cast<float4*>(dx + p * C + c) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const float* __restrict__ dpool, int N, int H, int W, int C,
+                                                           float* __restrict__ dx) {
+  const int Hp = (H + 1) / 2, Wp = (W + 1) / 2;
+  const long long total = (long long)N * H * W * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    long long p = e / C;
+    const int w = (int)(p % W);
+    const int h = (int)((p / W) % H);
+    const int n = (int)(p / ((long long)W * H));
+    const int hp = h >> 1, wp = w >> 1;
+    const int cnt = (min(2 * hp + 2, H) - 2 * hp) * (min(2 * wp + 2, W) - 2 * wp);
+    dx[e] = dpool[(((long long)n * Hp + hp) * Wp + wp) * C + c] / (float)cnt;
+  }
+}
+
+// ---------------- 1x1 head ----------------
+constexpr int HEAD_KMAX = 8;
+__global__ __launch_bounds__(256) void head_fwd_kernel(DevFrame f, const float* __restrict__ w, const float* __restrict__ b,
+                                                       int K, int do_sigmoid, float* __restrict__ y) {
+  const long long HW = (long long)f.H * f.W;
+  const long long P = (long long)f.N * HW;
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const int ww = (int)(p % f.W), hh = (int)((p / f.W) % f.H), n = (int)(p / HW);
+  float acc[HEAD_KMAX];
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k) acc[k] = (k < K && b) ? b[k] : 0.f;
+  for (int c = 0; c < f.C; c += 4) {
+    const float4 v = frame_value4(f, n, hh, ww, c);
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (c + e >= f.C) break;
+#pragma unroll
+      for (int k = 0; k < HEAD_KMAX; ++k)
+        if (k < K) acc[k] = fmaf(vv[e], w[k * f.C + c + e], acc[k]);
+    }
+  }
+  const long long pix = p - (long long)n * HW;
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k) {
+    if (k >= K) break;
+    float v = acc[k];
+    if (do_sigmoid) v = 1.f / (1.f + expf(-v));
+    y[((long long)n * K + k) * HW + pix] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                       int do_sigmoid, const float* __restrict__ w, int K, int C,
+                                                       int N, int H, int W, float* __restrict__ dl, float* __restrict__ da) {
+  const long long HW = (long long)H * W;
+  const long long P = (long long)N * HW;
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const int n = (int)(p / HW);
+  const long long pix = p - (long long)n * HW;
+  float g[HEAD_KMAX];
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k) {
+    g[k] = 0.f;
+    if (k < K) {
+      const long long i = ((long long)n * K + k) * HW + pix;
+      float v = dy[i];
+      if (do_sigmoid) { const float s = y[i]; v = v * (s * (1.f - s)); }
+      g[k] = v;
+      dl[i] = v;
+    }
+  }
+  for (int c = 0; c < C; c += 4) {
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float s = 0.f;
+      if (c + e < C) {
+#pragma unroll
+        for (int k = 0; k < HEAD_KMAX; ++k)
+          if (k < K) s = fmaf(g[k], w[k * C + c + e], s);
+      }
+      o[e] = s;
+    }
+    if (c + 3 < C && (C % 4) == 0) {
+      *reinterpret_cast<float4*>(da + p * C + c) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+      for (int e = 0; e < 4 && c + e < C; ++e) da[p * C + c + e] = o[e];
+    }
+  }
+}
+
+// dw[k][c] partial per block: ws[blk][K][C+1] (column C holds the bias grad)
+constexpr int W1_PPB = 1024;
+__global__ __launch_bounds__(256) void wgrad1x1_kernel(const float* __restrict__ dl, DevFrame f, int K,
+                                                       float* __restrict__ ws) {
+  __shared__ float red[256 * 33];
+  const int tid = threadIdx.x;
+  const int C = f.C;
+  const int CQ = (C + 3) >> 2;  // quads (CQ <= 64)
+  const int npg = 256 / CQ;
+  const int q = tid % CQ, pg = tid / CQ;
+  const long long HW = (long long)f.H * f.W;
+  const long long P = (long long)f.N * HW;
+  const long long p0 = (long long)blockIdx.x * W1_PPB;
+  float acc[HEAD_KMAX][4];
+  float accb[HEAD_KMAX];
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k) { accb[k] = 0.f; for (int e = 0; e < 4; ++e) acc[k][e] = 0.f; }
+  if (pg < npg) {
+    for (int i = pg; i < W1_PPB; i += npg) {
+      const long long p = p0 + i;
+      if (p >= P) break;
+      const int n = (int)(p / HW);
+      const long long pix = p - (long long)n * HW;
+      const int ww = (int)(pix % f.W), hh = (int)(pix / f.W);
+      const float4 v = frame_value4(f, n, hh, ww, 4 * q);
+#pragma unroll
+      for (int k = 0; k < HEAD_KMAX; ++k) {
+        if (k >= K) break;
+        const float g = dl[((long long)n * K + k) * HW + pix];
+        acc[k][0] = fmaf(g, v.x, acc[k][0]); acc[k][1] = fmaf(g, v.y, acc[k][1]);
+        acc[k][2] = fmaf(g, v.z, acc[k][2]); acc[k][3] = fmaf(g, v.w, acc[k][3]);
+        if (q == 0) accb[k] += g;
+      }
+    }
+  }
+  const int CW = C + 1;
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[tid * 33 + e] = acc[k][e];
+    red[tid * 33 + 4] = accb[k];
+    __syncthreads();
+    if (pg == 0) {
+      float t[5] = {0, 0, 0, 0, 0};
+      for (int l = 0; l < npg; ++l)
+        for (int e = 0; e < 5; ++e) t[e] += red[(l * CQ + q) * 33 + e];
+      for (int e = 0; e < 4; ++e)
+        if (4 * q + e < C) ws[((long long)blockIdx.x * K + k) * CW + 4 * q + e] = t[e];
+      if (q == 0) ws[((long long)blockIdx.x * K + k) * CW + C] = t[4];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void rows_sum_split_kernel(const float* __restrict__ ws, int R, int K, int C, float* dw, float* db) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;  // k*(C+1) + c
+  const int CW = C + 1;
+  if (o >= K * CW) return;
+  double s = 0.0;
+  for (int r = 0; r < R; ++r) s += ws[(long long)r * K * CW + o];
+  const int k = o / CW, c = o - k * CW;
+  if (c < C) dw[k * C + c] = (float)s;
+  else if (db) db[k] = (float)s;
+}
+
+// ---------------- SGD + clip ----------------
+__global__ __launch_bounds__(256) void sgd_clip_kernel(const pmu_sgd_chunk* __restrict__ chunks, void* const* __restrict__ ptrs,
+                                                       float gscale, float lr, float momentum, float clip) {
+  const pmu_sgd_chunk ck = chunks[blockIdx.x];
+  float* p = (float*)ptrs[3 * ck.tensor + 0];
+  float* g = (float*)ptrs[3 * ck.tensor + 1];
+  float* b = (float*)ptrs[3 * ck.tensor + 2];
+  for (int i = threadIdx.x; i < ck.len; i += blockDim.x) {
+    const long long j = ck.start + i;
+    float gv = g[j] * gscale;
+    if (clip > 0.f) gv = fminf(fmaxf(gv, -clip), clip);
+    const float bv = fmaf(momentum, b[j], gv);
+    b[j] = bv;
+    p[j] = fmaf(-lr, bv, p[j]);
+  }
+}
+
+// ---------------- dice counts ----------------
+__global__ __launch_bounds__(256) void dice_counts_kernel(const float* __restrict__ y, const float* __restrict__ mask,
+                                                          int N, int K, int H, int W, double* __restrict__ out) {
+  __shared__ double red[256];
+  const long long HW = (long long)H * W;
+  const long long P = (long long)N * HW;
+  const int KK = K == 1 ? 1 : K;
+  double loc[3 * HEAD_KMAX];
+#pragma unroll
+  for (int i = 0; i < 3 * HEAD_KMAX; ++i) loc[i] = 0.0;
+  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(p / HW);
+    const long long pix = p - (long long)n * HW;
+    const float t = mask[p];
+    if (K == 1) {
+      const float pr = y[p] > 0.5f ? 1.f : 0.f;
+      loc[0] += (double)(pr * t); loc[1] += (double)pr; loc[2] += (double)t;
+    } else {
+      float m = -INFINITY;
+      for (int k = 0; k < K; ++k) m = fmaxf(m, y[((long long)n * K + k) * HW + pix]);
+      float e[HEAD_KMAX];
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < HEAD_KMAX; ++k) {
+        e[k] = 0.f;
+        if (k < K) { e[k] = expf(y[((long long)n * K + k) * HW + pix] - m); s += e[k]; }
+      }
+      int am = 0;
+      float best = e[0] / s;
+#pragma unroll
+      for (int k = 1; k < HEAD_KMAX; ++k) {
+        if (k < K) { const float pk = e[k] / s; if (pk > best) { best = pk; am = k; } }
+      }
+#pragma unroll
+      for (int k = 0; k < HEAD_KMAX; ++k) {
+        if (k < K) {
+          const double pr = (am == k) ? 1.0 : 0.0;
+          const double tk = (t == (float)k) ? 1.0 : 0.0;
+          loc[3 * k + 0] += pr * tk; loc[3 * k + 1] += pr; loc[3 * k + 2] += tk;
+        }
+      }
+    }
+  }
+  for (int i = 0; i < 3 * KK; ++i) {
+    red[threadIdx.x] = loc[i];
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(out + i, red[0]);  // integer-valued doubles: order-independent
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+extern "C" int pmu_colsum_groups(int R) {
+  int g = R / 64;
+  if (g < 1) g = 1;
+  if (g > 128) g = 128;
+  return g;
+}
+
+extern "C" int pmu_colsum_f64(const float* part, int R, int Wd, double* out, int G, void* stream) {
+  PMU_REQUIRE(part && out && R > 0 && Wd > 0 && G > 0 && G <= R);
+  hipLaunchKernelGGL(colsum_f64_kernel, dim3((unsigned)pmu_cdiv(Wd, 64), (unsigned)G), dim3(256), 0,
+                     (hipStream_t)stream, part, R, Wd, out, G);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_bn_fwd_finalize(const double* acc, int G, int C, double count, const float* gamma,
+                                   const float* beta, float eps, float momentum, float* running_mean,
+                                   float* running_var, float* mean, float* invstd, float* coef, void* stream) {
+  PMU_REQUIRE(acc && G > 0 && C > 0 && count > 0 && mean && invstd && coef);
+  PMU_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)pmu_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream,
+                     acc, G, C, count, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, coef);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_bn_eval_coef(const float* running_mean, const float* running_var, const float* gamma,
+                                const float* beta, float eps, int C, float* coef, void* stream) {
+  PMU_REQUIRE(running_mean && running_var && C > 0 && coef);
+  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((unsigned)pmu_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream,
+                     running_mean, running_var, gamma, beta, eps, C, coef);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+static int bn_bwd_ppb(int C) {
+  int ppb = BNR_BYTES / (C * 4);
+  return ppb < 1 ? 1 : ppb;
+}
+
+extern "C" int pmu_bn_bwd_tiles(int P, int C) { return pmu_cdiv(P, bn_bwd_ppb(C)); }
+
+extern "C" int pmu_bn_bwd_reduce(const float* da, const float* z, const float* coef, const float* mean,
+                                 const float* invstd, int P, int C, float* part, void* stream) {
+  PMU_REQUIRE(da && z && coef && mean && invstd && part && P > 0 && C > 0 && C % 4 == 0);
+  const int ppb = bn_bwd_ppb(C);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0, (hipStream_t)stream,
+                     da, z, coef, mean, invstd, (long long)P, C, ppb, part);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_bn_bwd_finalize(const double* acc, int G, int C, double count, const float* gamma,
+                                   const float* coef, const float* mean, const float* invstd, float* dgamma,
+                                   float* dbeta, float* dbias, float* bcoef, void* stream) {
+  PMU_REQUIRE(acc && G > 0 && C > 0 && count > 0 && coef && mean && invstd && bcoef);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)pmu_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream,
+                     acc, G, C, count, gamma, coef, mean, invstd, dgamma, dbeta, dbias, bcoef);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+static unsigned grid_for(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+extern "C" int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int N, int H, int W,
+                                int C, float* dx, int accumulate, void* stream) {
+  PMU_REQUIRE(dpool && z && coef && dx && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0,
+                     (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream) {
+  PMU_REQUIRE(dpool && dx && N > 0 && H > 0 && W > 0 && C > 0);
+  hipLaunchKernelGGL(avgpool2_bwd_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0,
+                     (hipStream_t)stream, dpool, N, H, W, C, dx);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_head1x1_fwd(const pmu_frame* in, const float* w, const float* b, int K, int do_sigmoid,
+                               float* y, void* stream) {
+  PMU_REQUIRE(valid_frame(in) && w && y && K >= 1 && K <= HEAD_KMAX);
+  const DevFrame f = make_dev_frame(in);
+  const long long P = (long long)in->N * in->H * in->W;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)pmu_cdiv(P, 256)), dim3(256), 0, (hipStream_t)stream,
+                     f, w, b, K, do_sigmoid, y);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
+                               int N, int H, int W, float* dl, float* da, void* stream) {
+  PMU_REQUIRE(dy && w && dl && da && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y));
+  const long long P = (long long)N * H * W;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)pmu_cdiv(P, 256)), dim3(256), 0, (hipStream_t)stream,
+                     dy, y, do_sigmoid, w, K, C, N, H, W, dl, da);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" size_t pmu_wgrad1x1_ws(int P, int K, int C) {
+  return (size_t)pmu_cdiv(P, W1_PPB) * K * (C + 1) * sizeof(float);
+}
+
+extern "C" int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float* dw, float* db, float* ws,
+                            size_t ws_bytes, void* stream) {
+  PMU_REQUIRE(dl && valid_frame(act) && dw && ws && K >= 1 && K <= HEAD_KMAX);
+  const DevFrame f = make_dev_frame(act);
+  PMU_REQUIRE(f.C <= 256);
+  const long long P = (long long)act->N * act->H * act->W;
+  const int R = pmu_cdiv(P, W1_PPB);
+  PMU_REQUIRE(ws_bytes >= (size_t)R * K * (f.C + 1) * sizeof(float));
+  hipLaunchKernelGGL(wgrad1x1_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dl, f, K, ws);
+  PMU_CHECK_LAUNCH();
+  hipLaunchKernelGGL(rows_sum_split_kernel, dim3((unsigned)pmu_cdiv(K * (f.C + 1), 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)ws, R, K, f.C, dw, db);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_sgd_clip(const pmu_sgd_chunk* chunks, int nchunks, void* const* ptrs, float gscale, float lr,
+                            float momentum, float clip, void* stream) {
+  PMU_REQUIRE(chunks && ptrs && nchunks > 0);
+  hipLaunchKernelGGL(sgd_clip_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, chunks, ptrs, gscale,
+                     lr, momentum, clip);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_dice_counts(const float* y, const float* mask, int N, int K, int H, int W, double* counts,
+                               void* stream) {
+  PMU_REQUIRE(y && mask && counts && N > 0 && K >= 1 && K <= HEAD_KMAX && H > 0 && W > 0);
+  if (hipMemsetAsync(counts, 0, sizeof(double) * 3 * K, (hipStream_t)stream) != hipSuccess) return PMU_ERR_ARG;
+  const long long P = (long long)N * H * W;
+  unsigned g = (unsigned)pmu_cdiv(P, 256);
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(dice_counts_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, y, mask, N, K, H, W, counts);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+namespace {
+__global__ __launch_bounds__(256) void bnrelu_apply_kernel(const float* __restrict__ z, const float* __restrict__ coef,
+                                                           long long total4, int C, float* __restrict__ out) {
+  const int CQ = C >> 2;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total4;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % CQ) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(z + 4 * e);
+    const float4 sc = *reinterpret_cast<const float4*>(coef + c);
+    const float4 sh = *reinterpret_cast<const float4*>(coef + C + c);
+    *reinterpret_cast<float4*>(out + 4 * e) =
+        make_float4(fmaxf(0.f, fmaf(v.x, sc.x, sh.x)), fmaxf(0.f, fmaf(v.y, sc.y, sh.y)),
+                    fmaxf(0.f, fmaf(v.z, sc.z, sh.z)), fmaxf(0.f, fmaf(v.w, sc.w, sh.w)));
+  }
+}
+}  // namespace
+
+extern "C" int pmu_bnrelu_apply(const float* z, const float* coef, long long P, int C, float* out, void* stream) {
+  PMU_REQUIRE(z && coef && out && P > 0 && C > 0 && C % 4 == 0);
+  const long long total4 = P * (C / 4);
+  hipLaunchKernelGGL(bnrelu_apply_kernel, dim3(grid_for(total4)), dim3(256), 0, (hipStream_t)stream, z, coef, total4,
+                     C, out);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}

@@ -1,0 +1,193 @@
+// Shared device helpers for libpmunet_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/pmunet_hip.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define PMU_CHECK_LAUNCH()                          \
+  do {                                              \
+    hipError_t e__ = hipGetLastError();             \
+    if (e__ != hipSuccess) return (int)e__;         \
+  } while (0)
+#define PMU_REQUIRE(cond) \
+  do {                    \
+    if (!(cond)) return PMU_ERR_ARG; \
+  } while (0)
+
+static inline int pmu_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+__device__ __forceinline__ int pmu_cdiv_dev(int a, int b) { return (a + b - 1) / b; }
+
+// f32-in / f32-accumulate MFMA: D[32x32] += A[32x2] * B[2x32].
+// Lane l supplies A[l&31][l>>5] and B[l>>5][l&31]; D: col = l&31,
+// row = (r&3) + 8*(r>>2) + 4*(l>>5) for register r.
+__device__ __forceinline__ f32x16 mfma_f32_32x32x2(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// ---------------------------------------------------------------------------------
+// Operand element loader.  A conv operand is a frame (N x H x W) whose channels are
+// the concatenation of up to two sources; each source maps stored values to operand
+// values (raw / BN+ReLU / BN+ReLU backward) and may be 2x2-pooled and offset (F.pad).
+// Positions outside the frame or the source read as 0 (conv zero padding is applied
+// in operand space, i.e. after BN+ReLU, as in the reference).
+// ---------------------------------------------------------------------------------
+struct DevSrc {
+  const float* x;
+  const float* z;
+  const float* coef;
+  int mode, pool, C, H, W, off_h, off_w;
+};
+struct DevFrame {
+  DevSrc s0, s1;
+  int nsrc, N, H, W, C0, C;  // C0 = channels of s0, C = total
+  int vec;                   // 1 if every source has C % 4 == 0 (float4 path legal)
+};
+
+static inline DevFrame make_dev_frame(const pmu_frame* f) {
+  DevFrame d;
+  const pmu_src* a = &f->src[0];
+  d.s0 = DevSrc{a->x, a->z, a->coef, a->mode, a->pool, a->C, a->H, a->W, a->off_h, a->off_w};
+  if (f->nsrc > 1) {
+    const pmu_src* b = &f->src[1];
+    d.s1 = DevSrc{b->x, b->z, b->coef, b->mode, b->pool, b->C, b->H, b->W, b->off_h, b->off_w};
+  } else {
+    d.s1 = DevSrc{nullptr, nullptr, nullptr, 0, 0, 0, 0, 0, 0, 0};
+  }
+  d.nsrc = f->nsrc;
+  d.N = f->N; d.H = f->H; d.W = f->W;
+  d.C0 = a->C;
+  d.C = a->C + (f->nsrc > 1 ? f->src[1].C : 0);
+  d.vec = (a->C % 4 == 0) && (f->nsrc < 2 || f->src[1].C % 4 == 0);
+  return d;
+}
+
+static inline bool valid_src(const pmu_src& s, int N) {
+  if (!s.x || s.C <= 0 || s.H <= 0 || s.W <= 0) return false;
+  if (s.mode == PMU_SRC_BNRELU && !s.coef) return false;
+  if (s.mode == PMU_SRC_BNBWD && (!s.coef || !s.z)) return false;
+  if (s.mode < 0 || s.mode > 2 || s.pool < 0 || s.pool > 2) return false;
+  (void)N;
+  return true;
+}
+static inline bool valid_frame(const pmu_frame* f) {
+  if (!f || f->nsrc < 1 || f->nsrc > 2 || f->N <= 0 || f->H <= 0 || f->W <= 0) return false;
+  for (int i = 0; i < f->nsrc; ++i) {
+    if (!valid_src(f->src[i], f->N)) return false;
+    const pmu_src& s = f->src[i];
+    if (s.pool == PMU_POOL_MAX2 && (s.H / 2 + s.off_h > f->H || s.W / 2 + s.off_w > f->W)) return false;
+  }
+  return true;
+}
+
+// transform of one stored element (index i into x/z, channel c of the source)
+__device__ __forceinline__ float src_xform(const DevSrc& s, long long i, int c) {
+  if (s.mode == PMU_SRC_RAW) return s.x[i];
+  if (s.mode == PMU_SRC_BNRELU) return fmaxf(0.f, fmaf(s.x[i], s.coef[c], s.coef[s.C + c]));
+  // BNBWD
+  const float z = s.z[i];
+  const float sc = s.coef[c];
+  const float g = (fmaf(z, sc, s.coef[s.C + c]) > 0.f) ? s.x[i] : 0.f;
+  return fmaf(sc, g, fmaf(s.coef[3 * s.C + c], z - s.coef[2 * s.C + c], s.coef[4 * s.C + c]));
+}
+__device__ __forceinline__ float4 src_xform4(const DevSrc& s, long long i, int c) {
+  const float4 x = *reinterpret_cast<const float4*>(s.x + i);
+  if (s.mode == PMU_SRC_RAW) return x;
+  const float4 sc = *reinterpret_cast<const float4*>(s.coef + c);
+  const float4 sh = *reinterpret_cast<const float4*>(s.coef + s.C + c);
+  if (s.mode == PMU_SRC_BNRELU) {
+    return make_float4(fmaxf(0.f, fmaf(x.x, sc.x, sh.x)), fmaxf(0.f, fmaf(x.y, sc.y, sh.y)),
+                       fmaxf(0.f, fmaf(x.z, sc.z, sh.z)), fmaxf(0.f, fmaf(x.w, sc.w, sh.w)));
+  }
+  const float4 z = *reinterpret_cast<const float4*>(s.z + i);
+  const float4 mu = *reinterpret_cast<const float4*>(s.coef + 2 * s.C + c);
+  const float4 kx = *reinterpret_cast<const float4*>(s.coef + 3 * s.C + c);
+  const float4 kc = *reinterpret_cast<const float4*>(s.coef + 4 * s.C + c);
+  float4 r;
+  r.x = fmaf(sc.x, fmaf(z.x, sc.x, sh.x) > 0.f ? x.x : 0.f, fmaf(kx.x, z.x - mu.x, kc.x));
+  r.y = fmaf(sc.y, fmaf(z.y, sc.y, sh.y) > 0.f ? x.y : 0.f, fmaf(kx.y, z.y - mu.y, kc.y));
+  r.z = fmaf(sc.z, fmaf(z.z, sc.z, sh.z) > 0.f ? x.z : 0.f, fmaf(kx.z, z.z - mu.z, kc.z));
+  r.w = fmaf(sc.w, fmaf(z.w, sc.w, sh.w) > 0.f ? x.w : 0.f, fmaf(kx.w, z.w - mu.w, kc.w));
+  return r;
+}
+
+// value of source s at source-frame position (hs, ws) (already offset-corrected), channel c
+__device__ __forceinline__ float src_value(const DevSrc& s, int n, int hs, int ws, int c) {
+  if (s.pool == PMU_POOL_NONE) {
+    if (hs < 0 || ws < 0 || hs >= s.H || ws >= s.W) return 0.f;
+    return src_xform(s, (((long long)n * s.H + hs) * s.W + ws) * s.C + c, c);
+  }
+  const int h0 = 2 * hs, w0 = 2 * ws;
+  if (hs < 0 || ws < 0 || h0 >= s.H || w0 >= s.W) return 0.f;
+  if (s.pool == PMU_POOL_MAX2) {  // floor mode: the whole window is inside
+    const long long b = (((long long)n * s.H + h0) * s.W + w0) * s.C + c;
+    const long long rs = (long long)s.W * s.C;
+    float m = src_xform(s, b, c);
+    m = fmaxf(m, src_xform(s, b + s.C, c));
+    m = fmaxf(m, src_xform(s, b + rs, c));
+    m = fmaxf(m, src_xform(s, b + rs + s.C, c));
+    return m;
+  }
+  // avg 2x2, ceil mode, divisor = number of in-bounds elements
+  const int h1 = min(h0 + 2, s.H), w1 = min(w0 + 2, s.W);
+  float acc = 0.f;
+  for (int h = h0; h < h1; ++h)
+    for (int w = w0; w < w1; ++w) acc += src_xform(s, (((long long)n * s.H + h) * s.W + w) * s.C + c, c);
+  return acc / (float)((h1 - h0) * (w1 - w0));
+}
+__device__ __forceinline__ float4 src_value4(const DevSrc& s, int n, int hs, int ws, int c) {
+  if (s.pool == PMU_POOL_NONE) {
+    if (hs < 0 || ws < 0 || hs >= s.H || ws >= s.W) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return src_xform4(s, (((long long)n * s.H + hs) * s.W + ws) * s.C + c, c);
+  }
+  const int h0 = 2 * hs, w0 = 2 * ws;
+  if (hs < 0 || ws < 0 || h0 >= s.H || w0 >= s.W) return make_float4(0.f, 0.f, 0.f, 0.f);
+  if (s.pool == PMU_POOL_MAX2) {
+    const long long b = (((long long)n * s.H + h0) * s.W + w0) * s.C + c;
+    const long long rs = (long long)s.W * s.C;
+    float4 a = src_xform4(s, b, c), t;
+    t = src_xform4(s, b + s.C, c);
+    a.x = fmaxf(a.x, t.x); a.y = fmaxf(a.y, t.y); a.z = fmaxf(a.z, t.z); a.w = fmaxf(a.w, t.w);
+    t = src_xform4(s, b + rs, c);
+    a.x = fmaxf(a.x, t.x); a.y = fmaxf(a.y, t.y); a.z = fmaxf(a.z, t.z); a.w = fmaxf(a.w, t.w);
+    t = src_xform4(s, b + rs + s.C, c);
+    a.x = fmaxf(a.x, t.x); a.y = fmaxf(a.y, t.y); a.z = fmaxf(a.z, t.z); a.w = fmaxf(a.w, t.w);
+    return a;
+  }
+  const int h1 = min(h0 + 2, s.H), w1 = min(w0 + 2, s.W);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int h = h0; h < h1; ++h)
+    for (int w = w0; w < w1; ++w) {
+      const float4 t = src_xform4(s, (((long long)n * s.H + h) * s.W + w) * s.C + c, c);
+      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+    }
+  const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
+  acc.x *= inv; acc.y *= inv; acc.z *= inv; acc.w *= inv;
+  return acc;
+}
+
+// frame element (n, h, w, c); c may be >= C (returns 0)
+__device__ __forceinline__ float frame_value(const DevFrame& f, int n, int h, int w, int c) {
+  if (c >= f.C || h < 0 || w < 0 || h >= f.H || w >= f.W) return 0.f;
+  if (c < f.C0) return src_value(f.s0, n, h - f.s0.off_h, w - f.s0.off_w, c);
+  return src_value(f.s1, n, h - f.s1.off_h, w - f.s1.off_w, c - f.C0);
+}
+// 4 consecutive channels c..c+3 (c % 4 == 0); uses the vector path when legal
+__device__ __forceinline__ float4 frame_value4(const DevFrame& f, int n, int h, int w, int c) {
+  if (h < 0 || w < 0 || h >= f.H || w >= f.W || c >= f.C) return make_float4(0.f, 0.f, 0.f, 0.f);
+  if (f.vec && c + 3 < f.C) {
+    if (c < f.C0) return src_value4(f.s0, n, h - f.s0.off_h, w - f.s0.off_w, c);
+    return src_value4(f.s1, n, h - f.s1.off_h, w - f.s1.off_w, c - f.C0);
+  }
+  return make_float4(frame_value(f, n, h, w, c), frame_value(f, n, h, w, c + 1),
+                     frame_value(f, n, h, w, c + 2), frame_value(f, n, h, w, c + 3));
+}
+
+// wave-level sum over 64 lanes
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

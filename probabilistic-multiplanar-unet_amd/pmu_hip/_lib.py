@@ -1,0 +1,150 @@
+"""ctypes binding of libpmunet_hip.so (the C ABI declared in include/pmunet_hip.h).
+
+The library is loaded after ``import torch`` so that its ``libamdhip64.so.7`` dependency
+binds to the HIP runtime torch already loaded (same SONAME) — one runtime, one set of
+streams.  There is no fallback: if the library or a GPU is missing, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_longlong, c_size_t, c_void_p
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_NAME = "libpmunet_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+HEADER_PATH = os.path.normpath(
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "include", "pmunet_hip.h"))
+
+PMU_OK = 0
+PMU_ERR_ARG = 1001
+SRC_RAW, SRC_BNRELU, SRC_BNBWD = 0, 1, 2
+POOL_NONE, POOL_MAX2, POOL_AVG2CEIL = 0, 1, 2
+
+
+class PmuSrc(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("z", c_void_p), ("coef", c_void_p), ("mode", c_int), ("pool", c_int),
+                ("C", c_int), ("H", c_int), ("W", c_int), ("off_h", c_int), ("off_w", c_int)]
+
+
+class PmuFrame(ctypes.Structure):
+    _fields_ = [("src", PmuSrc * 2), ("nsrc", c_int), ("N", c_int), ("H", c_int), ("W", c_int)]
+
+
+class PmuSgdChunk(ctypes.Structure):
+    _fields_ = [("tensor", c_int), ("len", c_int), ("start", c_longlong)]
+
+
+_FP = POINTER(PmuFrame)
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "pmu_conv3x3_fwd": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_tiles": (c_int, [c_int, c_int, c_int]),
+    "pmu_conv3x3_dgrad": (c_int, [_FP, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_wgrad_ws": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_conv3x3_wgrad": (c_int, [_FP, _FP, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pmu_conv_first_fwd": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                   c_void_p, c_void_p, c_void_p]),
+    "pmu_conv_first_tiles": (c_int, [c_int, c_int, c_int]),
+    "pmu_conv_first_wgrad_ws": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_conv_first_wgrad": (c_int, [_FP, POINTER(c_void_p), c_int, c_int, c_void_p, c_void_p, c_size_t,
+                                     c_void_p]),
+    "pmu_colsum_f64": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "pmu_colsum_groups": (c_int, [c_int]),
+    "pmu_bn_fwd_finalize": (c_int, [c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_float, c_float,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_bn_eval_coef": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p]),
+    "pmu_bn_bwd_reduce": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                  c_void_p]),
+    "pmu_bn_bwd_tiles": (c_int, [c_int, c_int]),
+    "pmu_bn_bwd_finalize": (c_int, [c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_bnrelu_apply": (c_int, [c_void_p, c_void_p, c_longlong, c_int, c_void_p, c_void_p]),
+    "pmu_maxpool2_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                 c_void_p]),
+    "pmu_avgpool2_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_fwd": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_dgrad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                                   c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_wgrad_ws": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_convT2x2_wgrad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, _FP, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_size_t, c_void_p]),
+    "pmu_head1x1_fwd": (c_int, [_FP, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_head1x1_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                c_void_p, c_void_p, c_void_p]),
+    "pmu_wgrad1x1_ws": (c_size_t, [c_int, c_int, c_int]),
+    "pmu_wgrad1x1": (c_int, [c_void_p, _FP, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pmu_sgd_clip": (c_int, [c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_void_p]),
+    "pmu_dice_counts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+}
+
+_LIB = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the shared library and declare every signature (no GPU needed)."""
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{LIB_NAME} not found at {path}: build it with `make -C csrc` (or __graft_entry__.build()). "
+            "There is no CPU fallback for the PMU hot path.")
+    cdll = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(cdll, name)  # AttributeError if the export is missing
+        fn.restype = res
+        fn.argtypes = args
+    return cdll
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library; raises unless a ROCm GPU is present (the product path never runs on CPU)."""
+    global _LIB
+    if _LIB is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError("pmu_hip requires an AMD GPU (gfx950); torch.cuda.is_available() is False. "
+                               "There is no CPU fallback for the PMU hot path.")
+        _LIB = load_library()
+    return _LIB
+
+
+_HIP_ERR = {1: "hipErrorInvalidValue", 2: "hipErrorOutOfMemory", 98: "hipErrorInvalidDeviceFunction",
+            209: "hipErrorNoBinaryForGpu", 700: "hipErrorIllegalAddress"}
+
+
+def check(rc: int, name: str) -> None:
+    if rc != PMU_OK:
+        what = "invalid argument" if rc == PMU_ERR_ARG else _HIP_ERR.get(rc, f"hipError {rc}")
+        raise RuntimeError(f"{name} failed: {what} (code {rc})")
+
+
+_OBSERVER = None
+
+
+def set_call_observer(fn) -> None:
+    """Install fn(name, args, start_event, end_event) around every launch (None to remove).
+    Used by bench.py to time kernels with HIP events on the launch stream."""
+    global _OBSERVER
+    _OBSERVER = fn
+
+
+def call(name: str, *args) -> None:
+    obs = _OBSERVER
+    if obs is None:
+        check(getattr(lib(), name)(*args), name)
+        return
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    check(getattr(lib(), name)(*args), name)
+    e1.record()
+    obs(name, args, e0, e1)
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()

@@ -1,0 +1,395 @@
+"""Forward/backward executor of the U-Net conv stack on libpmunet_hip.
+
+Everything here only enqueues HIP kernels on the current torch stream through the C ABI;
+PyTorch supplies device memory (caching allocator) and the stream.  Activations live
+channels-last (NHWC) between kernels; a layer's output is kept as its *pre-BN* conv result
+``z`` plus per-channel BN coefficients, and the consumer applies BN+ReLU (+pool / +concat)
+while staging its operand, so post-activation tensors are never materialised.
+
+Reference call graph mirrored here (PMU/ = Probabilistic-Multiplanar-Unet/):
+  UNet.forward                 PMU/model/unet/unet_model.py:31-54
+  DoubleConv / Down / Up / OutConv   PMU/model/unet/unet_parts.py:9-76
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib as L
+
+F32 = torch.float32
+
+
+# ----------------------------------------------------------------------------------------
+# operand descriptors
+# ----------------------------------------------------------------------------------------
+@dataclass
+class Src:
+    """One channel source of a conv operand (see pmu_src in include/pmunet_hip.h)."""
+    x: torch.Tensor                  # NHWC [N][H][W][C]
+    mode: int = L.SRC_RAW
+    coef: torch.Tensor | None = None
+    z: torch.Tensor | None = None    # BNBWD only
+    pool: int = L.POOL_NONE
+    off: tuple = (0, 0)
+
+    @property
+    def C(self) -> int:
+        return self.x.shape[3]
+
+    def frame_hw(self):
+        H, W = self.x.shape[1], self.x.shape[2]
+        if self.pool == L.POOL_MAX2:
+            return H // 2, W // 2
+        if self.pool == L.POOL_AVG2CEIL:
+            return (H + 1) // 2, (W + 1) // 2
+        return H, W
+
+
+def make_frame(srcs, N: int, H: int, W: int) -> L.PmuFrame:
+    f = L.PmuFrame()
+    f.nsrc = len(srcs)
+    f.N, f.H, f.W = N, H, W
+    for i, s in enumerate(srcs):
+        t = s.x
+        assert t.is_contiguous() and t.dtype == F32 and t.dim() == 4, "operand must be contiguous NHWC fp32"
+        c = f.src[i]
+        c.x = t.data_ptr()
+        c.z = s.z.data_ptr() if s.z is not None else None
+        c.coef = s.coef.data_ptr() if s.coef is not None else None
+        c.mode, c.pool = s.mode, s.pool
+        c.C, c.H, c.W = t.shape[3], t.shape[1], t.shape[2]
+        c.off_h, c.off_w = s.off
+    return f
+
+
+def frame_of(srcs, N, H, W):
+    return ctypes.byref(make_frame(srcs, N, H, W))
+
+
+def _empty(*shape, dtype=F32, device=None):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+class GradSink(dict):
+    """param -> gradient tensor.  ``new(p)`` hands out the destination a kernel writes: a view
+    of the network's persistent flat gradient buffer when one is attached (stable pointers for
+    the fused optimizer / one-shot all-reduce), else a fresh tensor."""
+
+    def __init__(self, views=None):
+        super().__init__()
+        self.views = views
+
+    def new(self, p):
+        t = self.views.get(p) if self.views is not None else None
+        if t is None:
+            t = torch.empty_like(p)
+        self[p] = t
+        return t
+
+
+# ----------------------------------------------------------------------------------------
+# BatchNorm
+# ----------------------------------------------------------------------------------------
+@dataclass
+class BNState:
+    coef: torch.Tensor      # [scale | shift]
+    mean: torch.Tensor | None = None
+    invstd: torch.Tensor | None = None
+    count: float = 0.0
+
+
+def bn_forward(part, R: int, C: int, count: int, bn: torch.nn.BatchNorm2d, training: bool, dev) -> BNState:
+    """BatchNorm2d statistics (train) or running-stat coefficients (eval)."""
+    s = L.stream()
+    use_batch = training or not bn.track_running_stats or bn.running_mean is None
+    if not use_batch:
+        coef = _empty(2 * C, device=dev)
+        L.call("pmu_bn_eval_coef", bn.running_mean.data_ptr(), bn.running_var.data_ptr(), L.ptr(bn.weight),
+               L.ptr(bn.bias), float(bn.eps), C, coef.data_ptr(), s)
+        return BNState(coef=coef)
+    G = L.lib().pmu_colsum_groups(R)
+    acc = _empty(G, 2 * C, dtype=torch.float64, device=dev)
+    L.call("pmu_colsum_f64", part.data_ptr(), R, 2 * C, acc.data_ptr(), G, s)
+    mean, invstd, coef = _empty(C, device=dev), _empty(C, device=dev), _empty(2 * C, device=dev)
+    update = training and bn.track_running_stats and bn.running_mean is not None
+    momentum = bn.momentum
+    if update:
+        bn.num_batches_tracked.add_(1)
+        if momentum is None:  # cumulative moving average
+            momentum = 1.0 / float(bn.num_batches_tracked.item())
+    L.call("pmu_bn_fwd_finalize", acc.data_ptr(), G, C, float(count), L.ptr(bn.weight), L.ptr(bn.bias),
+           float(bn.eps), float(momentum or 0.0),
+           bn.running_mean.data_ptr() if update else None, bn.running_var.data_ptr() if update else None,
+           mean.data_ptr(), invstd.data_ptr(), coef.data_ptr(), s)
+    return BNState(coef=coef, mean=mean, invstd=invstd, count=float(count))
+
+
+def bn_backward(da: torch.Tensor, z: torch.Tensor, st: BNState, bn: torch.nn.BatchNorm2d, grads, conv_bias=None):
+    """Returns (bcoef, dgamma, dbeta, dbias) for BN+ReLU backward given da = dL/d relu(bn(z))."""
+    s = L.stream()
+    dev = z.device
+    N, H, W, C = z.shape
+    P = N * H * W
+    lb = L.lib()
+    R = lb.pmu_bn_bwd_tiles(P, C)
+    part = _empty(R, 2 * C, device=dev)
+    L.call("pmu_bn_bwd_reduce", da.data_ptr(), z.data_ptr(), st.coef.data_ptr(), st.mean.data_ptr(),
+           st.invstd.data_ptr(), P, C, part.data_ptr(), s)
+    G = lb.pmu_colsum_groups(R)
+    acc = _empty(G, 2 * C, dtype=torch.float64, device=dev)
+    L.call("pmu_colsum_f64", part.data_ptr(), R, 2 * C, acc.data_ptr(), G, s)
+    dgamma = grads.new(bn.weight) if bn.weight is not None else None
+    dbeta = grads.new(bn.bias) if bn.bias is not None else None
+    dbias = grads.new(conv_bias) if conv_bias is not None else _empty(C, device=dev)
+    bcoef = _empty(5 * C, device=dev)
+    L.call("pmu_bn_bwd_finalize", acc.data_ptr(), G, C, float(P), L.ptr(bn.weight), st.coef.data_ptr(),
+           st.mean.data_ptr(), st.invstd.data_ptr(), L.ptr(dgamma), L.ptr(dbeta), dbias.data_ptr(),
+           bcoef.data_ptr(), s)
+    return bcoef, dgamma, dbeta, dbias
+
+
+# ----------------------------------------------------------------------------------------
+# conv + BN layer
+# ----------------------------------------------------------------------------------------
+@dataclass
+class ConvBNOut:
+    z: torch.Tensor       # NHWC pre-BN conv output
+    bn: BNState
+    srcs: list = field(default_factory=list)   # the operand sources it consumed (for wgrad)
+    planes: list | None = None                  # first-layer input planes
+
+    def act(self, pool=L.POOL_NONE) -> Src:
+        return Src(self.z, L.SRC_BNRELU, self.bn.coef, pool=pool)
+
+
+def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H, W, training, dev,
+                    planes=None) -> ConvBNOut:
+    Cout = conv.out_channels
+    s = L.stream()
+    lb = L.lib()
+    z = _empty(N, H, W, Cout, device=dev)
+    need_stats = training or not bn.track_running_stats
+    if planes is not None:
+        R = lb.pmu_conv_first_tiles(N, H, W)
+        part = _empty(R, 2 * Cout, device=dev) if need_stats else None
+        arr = (ctypes.c_void_p * len(planes))(*[p.data_ptr() for p in planes])
+        L.call("pmu_conv_first_fwd", arr, len(planes), N, H, W, conv.weight.data_ptr(), L.ptr(conv.bias), Cout,
+               z.data_ptr(), L.ptr(part), s)
+    else:
+        R = lb.pmu_conv3x3_tiles(N, H, W)
+        part = _empty(R, 2 * Cout, device=dev) if need_stats else None
+        L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), L.ptr(conv.bias), Cout,
+               z.data_ptr(), L.ptr(part), s)
+    st = bn_forward(part, R, Cout, N * H * W, bn, training, dev)
+    return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes)
+
+
+def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, need_dx=True, split=None):
+    """Backward of relu(bn(conv(operand))) given da (NHWC).  Writes conv/bn grads into ``grads``.
+
+    Returns the operand gradient(s): one NHWC tensor, or (dx0, dx1) when ``split`` is given
+    (channel split of a concatenated operand)."""
+    s = L.stream()
+    z = out.z
+    N, H, W, Cout = z.shape
+    dev = z.device
+    bcoef, _, _, _ = bn_backward(da, z, out.bn, bn, grads, conv.bias)
+    dz_src = Src(da, L.SRC_BNBWD, bcoef, z=z)
+    dzf = frame_of([dz_src], N, H, W)
+    dw = grads.new(conv.weight)
+    lb = L.lib()
+    if out.planes is not None:
+        Cin = len(out.planes)
+        wsb = lb.pmu_conv_first_wgrad_ws(N, H, W, Cin, Cout)
+        ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+        arr = (ctypes.c_void_p * Cin)(*[p.data_ptr() for p in out.planes])
+        L.call("pmu_conv_first_wgrad", dzf, arr, Cin, Cout, dw.data_ptr(), ws.data_ptr(), wsb, s)
+    else:
+        Cin = sum(sr.C for sr in out.srcs)
+        wsb = lb.pmu_conv3x3_wgrad_ws(N, H, W, Cin, Cout)
+        ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+        L.call("pmu_conv3x3_wgrad", dzf, frame_of(out.srcs, N, H, W), Cout, dw.data_ptr(), ws.data_ptr(), wsb, s)
+    if not need_dx or out.planes is not None:
+        return None
+    Cin = conv.in_channels
+    if split is None:
+        dx = _empty(N, H, W, Cin, device=dev)
+        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), Cin, Cin, dx.data_ptr(), None, s)
+        return dx
+    dx0 = _empty(N, H, W, split, device=dev)
+    dx1 = _empty(N, H, W, Cin - split, device=dev)
+    L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), Cin, split, dx0.data_ptr(), dx1.data_ptr(), s)
+    return dx0, dx1
+
+
+# ----------------------------------------------------------------------------------------
+# U-Net
+# ----------------------------------------------------------------------------------------
+def _dc_layers(dc):
+    """(conv1, bn1, conv2, bn2) of a DoubleConv (double_conv = [conv, bn, relu, conv, bn, relu])."""
+    s = dc.double_conv
+    return s[0], s[1], s[3], s[4]
+
+
+@dataclass
+class UpState:
+    u: torch.Tensor          # convT output, NHWC [N][2h][2w][Cup]
+    off: tuple               # (pad_top, pad_left) inside the skip frame
+    prev: ConvBNOut          # convT input producer
+    c1: ConvBNOut
+    c2: ConvBNOut
+
+
+class UNetState:
+    """Everything the backward needs from one forward."""
+
+    def __init__(self):
+        self.x = None
+        self.planes = None
+        self.enc: list = []     # per level: (c1, c2) ConvBNOut
+        self.ups: list = []     # per up block: UpState
+        self.y = None           # head output (NCHW)
+        self.feat_src = None    # last DoubleConv output producer
+
+
+def unet_forward(net, x: torch.Tensor, training: bool):
+    """Forward of model.UNet on the HIP path.  Returns (output, state).
+
+    Output: NCHW logits / sigmoid(logits) when net.apply_last_layer, else the last
+    DoubleConv activation as an NCHW-shaped channels-last tensor (unet_model.py:48-54)."""
+    assert x.is_cuda and x.dtype == F32 and x.dim() == 4
+    dev = x.device
+    N, Cin, H, W = x.shape
+    st = UNetState()
+    st.x = x
+    # first layer reads NCHW planes directly (C == 1 is also NHWC)
+    xc = x.contiguous()
+    if Cin <= 4:
+        st.planes = [xc[:, c] for c in range(Cin)]
+        planes = [p if p.is_contiguous() else p.contiguous() for p in st.planes]
+        st.planes = planes
+        first_srcs = []
+    else:
+        planes = None
+        first_srcs = [Src(xc.permute(0, 2, 3, 1).contiguous())]
+    # ---- encoder
+    c1w, b1, c2w, b2 = _dc_layers(net.inc)
+    o1 = conv_bn_forward(first_srcs, c1w, b1, N, H, W, training, dev, planes=planes)
+    o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev)
+    st.enc.append((o1, o2))
+    h, w = H, W
+    for down in net.down_blocks:
+        dc = down.maxpool_conv[1]
+        c1w, b1, c2w, b2 = _dc_layers(dc)
+        prev = st.enc[-1][1]
+        h, w = h // 2, w // 2
+        o1 = conv_bn_forward([prev.act(L.POOL_MAX2)], c1w, b1, N, h, w, training, dev)
+        o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev)
+        st.enc.append((o1, o2))
+    # ---- decoder
+    cur = st.enc[-1][1]
+    nlev = len(st.enc)
+    for j, up in enumerate(net.up_blocks):
+        skip = st.enc[nlev - 2 - j][1]
+        hs, ws_ = skip.z.shape[1], skip.z.shape[2]
+        hi, wi = cur.z.shape[1], cur.z.shape[2]
+        convT = up.up
+        Cup = convT.out_channels
+        u = _empty(N, 2 * hi, 2 * wi, Cup, device=dev)
+        L.call("pmu_convT2x2_fwd", frame_of([cur.act()], N, hi, wi), convT.weight.data_ptr(), L.ptr(convT.bias),
+               Cup, u.data_ptr(), L.stream())
+        dY, dX = hs - 2 * hi, ws_ - 2 * wi
+        assert dY >= 0 and dX >= 0, "decoder feature map larger than skip (unsupported by reference too)"
+        off = (dY // 2, dX // 2)
+        c1w, b1, c2w, b2 = _dc_layers(up.conv)
+        srcs = [skip.act(), Src(u, L.SRC_RAW, off=off)]
+        o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev)
+        o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev)
+        st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2))
+        cur = o2
+    st.feat_src = cur
+    if net.apply_last_layer:
+        K = net.outc.conv.out_channels
+        y = _empty(N, K, H, W, device=dev)
+        L.call("pmu_head1x1_fwd", frame_of([cur.act()], N, H, W), net.outc.conv.weight.data_ptr(),
+               L.ptr(net.outc.conv.bias), K, int(net.n_classes == 1), y.data_ptr(), L.stream())
+        st.y = y
+        return y, st
+    C = cur.z.shape[3]
+    feat = _empty(N, H, W, C, device=dev)
+    L.call("pmu_bnrelu_apply", cur.z.data_ptr(), cur.bn.coef.data_ptr(), N * H * W, C, feat.data_ptr(), L.stream())
+    return feat.permute(0, 3, 1, 2), st
+
+
+def unet_backward(net, st: UNetState, dy: torch.Tensor, sink_views=False) -> dict:
+    """Backward of unet_forward given dL/d(output).  Returns {parameter: grad}."""
+    grads = GradSink(getattr(net, "_pmu_grad_views", None) if sink_views else None)
+    s = L.stream()
+    dev = dy.device
+    x = st.x
+    N, _, H, W = x.shape
+    last = st.feat_src
+    if net.apply_last_layer:
+        K = net.outc.conv.out_channels
+        C = last.z.shape[3]
+        dyc = dy.contiguous()
+        dl = _empty(N, K, H, W, device=dev)
+        da = _empty(N, H, W, C, device=dev)
+        L.call("pmu_head1x1_bwd", dyc.data_ptr(), st.y.data_ptr(), int(net.n_classes == 1),
+               net.outc.conv.weight.data_ptr(), K, C, N, H, W, dl.data_ptr(), da.data_ptr(), s)
+        dwo = grads.new(net.outc.conv.weight)
+        dbo = grads.new(net.outc.conv.bias) if net.outc.conv.bias is not None else _empty(K, device=dev)
+        wsb = L.lib().pmu_wgrad1x1_ws(N * H * W, K, C)
+        ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+        L.call("pmu_wgrad1x1", dl.data_ptr(), frame_of([last.act()], N, H, W), K, dwo.data_ptr(), dbo.data_ptr(),
+               ws.data_ptr(), wsb, s)
+    else:
+        da = dy.permute(0, 2, 3, 1).contiguous()   # NCHW-shaped channels-last view -> NHWC
+
+    nlev = len(st.enc)
+    dskip = [None] * nlev
+    # ---- decoder, last block first
+    for j in reversed(range(len(net.up_blocks))):
+        up = net.up_blocks[j]
+        us: UpState = st.ups[j]
+        c1w, b1, c2w, b2 = _dc_layers(up.conv)
+        da1 = conv_bn_backward(us.c2, da, c2w, b2, grads)
+        Cskip = us.c1.srcs[0].C
+        dsk, dup = conv_bn_backward(us.c1, da1, c1w, b1, grads, split=Cskip)
+        dskip[nlev - 2 - j] = dsk
+        convT = up.up
+        prev = us.prev
+        hi, wi, Cin_t = prev.z.shape[1], prev.z.shape[2], prev.z.shape[3]
+        Hd, Wd = dup.shape[1], dup.shape[2]
+        Cup = convT.out_channels
+        dx = _empty(N, hi, wi, Cin_t, device=dev)
+        L.call("pmu_convT2x2_dgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], convT.weight.data_ptr(), N, hi,
+               wi, Cin_t, Cup, dx.data_ptr(), s)
+        dwt = grads.new(convT.weight)
+        dbt = grads.new(convT.bias) if convT.bias is not None else None
+        wsb = L.lib().pmu_convT2x2_wgrad_ws(N, hi, wi, Cin_t, Cup)
+        ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+        L.call("pmu_convT2x2_wgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], frame_of([prev.act()], N, hi, wi),
+               Cup, dwt.data_ptr(), L.ptr(dbt), ws.data_ptr(), wsb, s)
+        da = dx
+    # ---- encoder, deepest first; da = gradient w.r.t. the deepest encoder output
+    for lev in reversed(range(nlev)):
+        o1, o2 = st.enc[lev]
+        if lev == 0:
+            c1w, b1, c2w, b2 = _dc_layers(net.inc)
+        else:
+            c1w, b1, c2w, b2 = _dc_layers(net.down_blocks[lev - 1].maxpool_conv[1])
+        if lev != nlev - 1:
+            da = dskip[lev]   # skip grad with the pooled path accumulated below
+        da1 = conv_bn_backward(o2, da, c2w, b2, grads)
+        dpool = conv_bn_backward(o1, da1, c1w, b1, grads, need_dx=(lev > 0))
+        if lev > 0:
+            prev = st.enc[lev - 1][1]
+            hp, wp = prev.z.shape[1], prev.z.shape[2]
+            Cp = prev.z.shape[3]
+            L.call("pmu_maxpool2_bwd", dpool.data_ptr(), prev.z.data_ptr(), prev.bn.coef.data_ptr(), N, hp, wp, Cp,
+                   dskip[lev - 1].data_ptr(), 1, s)
+    return grads

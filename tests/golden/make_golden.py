@@ -1,0 +1,208 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE implementation.
+
+Runs only in the build container, where the read-only reference is mounted at
+/root/reference (it never travels to the GPU box).  The reference is imported unmodified
+with in-process shims for the pieces that do not import on this image:
+  - builtins torch/nn/np (probabilistic_unet.py:4-9 uses them without importing),
+  - stub modules utils.dataset (absent file), nibabel (not installed; serves in-memory
+    arrays), torch.utils.tensorboard (not installed).
+Outputs are data only (.npz): inputs, weights, and the reference's outputs/gradients.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import builtins
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+REF = "/root/reference/Probabilistic-Multiplanar-Unet"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def install_shims():
+    builtins.torch, builtins.nn, builtins.np = torch, nn, np
+    ud = types.ModuleType("utils.dataset")
+    ud.BasicDataset = object
+    sys.modules["utils.dataset"] = ud
+    nib = types.ModuleType("nibabel")
+    nib.store = {}
+
+    class _Img:
+        def __init__(self, a):
+            self.a = a
+
+        def get_fdata(self):
+            return self.a
+
+    nib.load = lambda p: _Img(nib.store[os.path.basename(p)])
+    sys.modules["nibabel"] = nib
+    tb = types.ModuleType("torch.utils.tensorboard")
+
+    class SummaryWriter:
+        def __init__(self, *a, **k):
+            pass
+
+        def __getattr__(self, n):
+            return lambda *a, **k: None
+
+    tb.SummaryWriter = SummaryWriter
+    sys.modules["torch.utils.tensorboard"] = tb
+    sys.path.insert(0, REF)
+    return nib
+
+
+def sd_np(prefix, sd):
+    return {f"{prefix}/{k}": v.detach().cpu().numpy() for k, v in sd.items()}
+
+
+def grads_np(prefix, module):
+    return {f"{prefix}/{k}": p.grad.detach().cpu().numpy() for k, p in module.named_parameters()
+            if p.grad is not None}
+
+
+def g1_unet_c1():
+    """Config c1: UNet(1,1,[16,32]), 64x64, batch 4, BCE; one step + 10 SGD steps (train.py:85-110)."""
+    from model import UNet
+    torch.manual_seed(0)
+    net = UNet(1, 1, [16, 32])
+    out = sd_np("init", net.state_dict())
+    g = torch.Generator().manual_seed(1)
+    xs = [torch.rand(4, 1, 64, 64, generator=g) for _ in range(10)]
+    ts = [(torch.rand(4, 1, 64, 64, generator=g) > 0.5).float() for _ in range(10)]
+    for i in range(10):
+        out[f"x{i}"] = xs[i].numpy()
+        out[f"t{i}"] = ts[i].numpy()
+    net.train()
+    crit = nn.BCELoss()
+    opt = torch.optim.SGD(net.parameters(), lr=1e-3, momentum=0.9)
+    losses = []
+    for i in range(10):
+        opt.zero_grad()
+        y = net(xs[i])
+        loss = crit(y, ts[i])
+        loss.backward()
+        if i == 0:
+            out["y0"] = y.detach().numpy()
+            out["loss0"] = np.array(loss.item(), dtype=np.float32)
+            out.update(grads_np("grad0", net))
+            out.update(sd_np("after0", net.state_dict()))
+        nn.utils.clip_grad_value_(net.parameters(), 0.1)
+        opt.step()
+        losses.append(loss.item())
+    out["losses"] = np.array(losses, dtype=np.float32)
+    out.update(sd_np("final", net.state_dict()))
+    np.savez_compressed(os.path.join(OUT, "g1_unet_c1.npz"), **out)
+
+
+def g2_unet_multiclass():
+    """All 5 levels at small width: UNet(1,3,[4,8,16,32,64]) at 64x64 (N=2) and 170x170 (N=1,
+    F.pad branch at 21 and 85), CrossEntropyLoss (unet_trainer.py:23,30-37)."""
+    from model import UNet
+    out = {}
+    for tag, (N, H) in {"s64": (2, 64), "s170": (1, 170)}.items():
+        torch.manual_seed(0)
+        net = UNet(1, 3, [4, 8, 16, 32, 64])
+        out.update(sd_np(f"{tag}/init", net.state_dict()))
+        g = torch.Generator().manual_seed(2)
+        x = torch.rand(N, 1, H, H, generator=g)
+        t = torch.randint(0, 3, (N, 1, H, H), generator=g)
+        net.train()
+        y = net(x)
+        loss = nn.CrossEntropyLoss()(y, t.squeeze(1))
+        loss.backward()
+        out[f"{tag}/x"] = x.numpy()
+        out[f"{tag}/t"] = t.numpy().astype(np.int64)
+        out[f"{tag}/y"] = y.detach().numpy()
+        out[f"{tag}/argmax"] = torch.argmax(torch.softmax(y.detach(), 1), 1).numpy().astype(np.int64)
+        out[f"{tag}/loss"] = np.array(loss.item(), dtype=np.float32)
+        out.update(grads_np(f"{tag}/grad", net))
+        out.update(sd_np(f"{tag}/after", net.state_dict()))
+    np.savez_compressed(os.path.join(OUT, "g2_unet_multiclass.npz"), **out)
+
+
+def g4_dice():
+    """dice_coeff known answers (dice_loss.py:5-12) and trainer-style per-class Dice
+    (unet_trainer.py:39-58) from the reference trainer's eval()."""
+    import dice_loss
+    from trainer import UNetTrainer
+    out = {}
+    g = torch.Generator().manual_seed(4)
+    cases = {
+        "rand": ((torch.rand(3, 20, 20, generator=g) > 0.5).float(), (torch.rand(3, 20, 20, generator=g) > 0.3).float()),
+        "empty": (torch.zeros(2, 8, 8), torch.zeros(2, 8, 8)),
+        "ones": (torch.ones(2, 8, 8), torch.ones(2, 8, 8)),
+        "disjoint": (torch.cat([torch.ones(1, 8, 8), torch.zeros(1, 8, 8)]), torch.cat([torch.zeros(1, 8, 8), torch.ones(1, 8, 8)])),
+    }
+    for k, (p, t) in cases.items():
+        out[f"{k}/pred"], out[f"{k}/target"] = p.numpy(), t.numpy()
+        out[f"{k}/dice"] = np.array(dice_loss.dice_coeff(p, t).item(), dtype=np.float32)
+    # trainer eval, multi-class and binary (constructed on CPU; eval() only uses self.device for one_hot)
+    tr = UNetTrainer.__new__(UNetTrainer)
+    tr.device = torch.device("cpu")
+    tr.net = types.SimpleNamespace(n_classes=3)
+    y = torch.randn(2, 3, 24, 24, generator=g)
+    m = torch.randint(0, 3, (2, 1, 24, 24), generator=g)
+    out["mc/y"], out["mc/mask"] = y.numpy(), m.numpy().astype(np.int64)
+    out["mc/dice"] = tr.eval(None, m, y).astype(np.float64)
+    tr.net = types.SimpleNamespace(n_classes=1)
+    yb = torch.rand(2, 1, 24, 24, generator=g)
+    mb = (torch.rand(2, 1, 24, 24, generator=g) > 0.5).float()
+    out["bin/y"], out["bin/mask"] = yb.numpy(), mb.numpy()
+    out["bin/dice"] = tr.eval(None, mb, yb).astype(np.float64)
+    np.savez_compressed(os.path.join(OUT, "g4_dice.npz"), **out)
+
+
+def g5_slicer(nib):
+    """MRI_Dataset (utils/mri_dataset.py:11-143) on tiny in-memory volumes: non-cube shapes
+    padded at the end of the argmin axis, 3-view slicing, per-slice max-norm, fg filter."""
+    import utils.mri_dataset as md
+    g = np.random.default_rng(5)
+    vols = {"a.nii": (6, 8, 8), "b.nii": (8, 5, 8), "c.nii": (8, 8, 7)}
+    out = {}
+    for name, shp in vols.items():
+        img = g.random(shp) * 100.0
+        img[0] = 0.0  # an all-zero slice (max-norm skipped)
+        lab = np.zeros(shp)
+        lab[1:4, 2:5, 1:6] = 1.0
+        lab[2:3, 3:4, 2:4] = 2.0
+        nib.store["img_" + name] = img
+        nib.store["lab_" + name] = lab
+        out[f"vol/{name}/img"] = img
+        out[f"vol/{name}/lab"] = lab
+    imgs = sorted(vols)
+    md.listdir = lambda d: list(imgs)
+    # the dataset joins dir + file name; route both dirs to the in-memory store by prefix
+    orig_load = nib.load
+    nib.load = lambda p: orig_load(("img_" if "imgs" in p else "lab_") + os.path.basename(p))
+    for filt in (True, False):
+        ds = md.MRI_Dataset("/imgs", "/labs", 3, filter=filt)
+        key = "filt" if filt else "all"
+        out[f"{key}/index_map"] = np.array(ds.index_map, dtype=np.int64)
+        out[f"{key}/image_dims"] = np.array(ds.image_dims, dtype=np.int64)
+        ims = [ds[i]["image"].numpy() for i in range(len(ds))]
+        mks = [ds[i]["mask"].numpy() for i in range(len(ds))]
+        out[f"{key}/images"] = np.stack(ims)
+        out[f"{key}/masks"] = np.stack(mks)
+    nib.load = orig_load
+    np.savez_compressed(os.path.join(OUT, "g5_slicer.npz"), **out)
+
+
+def main():
+    if not os.path.isdir(REF):
+        raise SystemExit(f"reference not found at {REF}: fixtures are generated in the build container only")
+    nib = install_shims()
+    g1_unet_c1()
+    g2_unet_multiclass()
+    g4_dice()
+    g5_slicer(nib)
+    print("golden fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()
