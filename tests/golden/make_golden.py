@@ -58,11 +58,11 @@ def install_shims():
 
 
 def sd_np(prefix, sd):
-    return {f"{prefix}/{k}": v.detach().cpu().numpy() for k, v in sd.items()}
+    return {f"{prefix}/{k}": v.detach().cpu().numpy().copy() for k, v in sd.items()}
 
 
 def grads_np(prefix, module):
-    return {f"{prefix}/{k}": p.grad.detach().cpu().numpy() for k, p in module.named_parameters()
+    return {f"{prefix}/{k}": p.grad.detach().cpu().numpy().copy() for k, p in module.named_parameters()
             if p.grad is not None}
 
 

@@ -1,0 +1,176 @@
+"""CPU-only checks: oracle vs the reference's golden vectors, drop-in surface, C ABI exports.
+
+No GPU compute here: the library is loaded and its symbols resolved, nothing is launched.
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import ACT_TOL, GRAD_TOL, LOSS_RTOL, grad_err, max_abs
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def _sd(z, prefix):
+    pre = prefix + "/"
+    return {k[len(pre):]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith(pre)}
+
+
+# ----------------------------------------------------------------------------- oracle pinning
+def test_oracle_matches_reference_g1_step():
+    """G1 (config c1): one train step of UNet(1,1,[16,32]) — outputs, loss, grads, BN stats."""
+    from oracle.unet_ref import unet_forward, unet_loss, unet_param_keys
+    z = _load("g1_unet_c1.npz")
+    sd = _sd(z, "init")
+    x, t = torch.from_numpy(z["x0"]), torch.from_numpy(z["t0"])
+    keys = unet_param_keys(sd)
+    params = {k: sd[k].clone().requires_grad_(True) for k in keys}
+    work = dict(sd)
+    work.update(params)
+    y = unet_forward(work, x, 2, 1)
+    loss = unet_loss(y, t, 1)
+    loss.backward()
+    assert max_abs(y, torch.from_numpy(z["y0"])) <= 1e-6
+    assert abs(float(loss) - float(z["loss0"])) <= 1e-6
+    gref = _sd(z, "grad0")
+    err, key = grad_err({k: params[k].grad for k in keys}, gref)
+    assert err <= 1e-5, (err, key)
+    after = _sd(z, "after0")
+    for k in after:
+        if "running" in k:
+            assert max_abs(work[k], after[k]) <= 1e-6, k
+
+
+def test_oracle_matches_reference_g1_ten_steps():
+    """G1: params after 10 clip(0.1)+SGD(lr 1e-3, momentum 0.9) steps (train.py:85-110)."""
+    from oracle.unet_ref import unet_param_keys, unet_train_step
+    z = _load("g1_unet_c1.npz")
+    sd = _sd(z, "init")
+    bufs = {k: torch.zeros_like(sd[k]) for k in unet_param_keys(sd)}
+    losses = []
+    for i in range(10):
+        _, loss, _ = unet_train_step(sd, torch.from_numpy(z[f"x{i}"]), torch.from_numpy(z[f"t{i}"]), 2, 1,
+                                     lr=1e-3, bufs=bufs)
+        losses.append(float(loss))
+    assert np.allclose(losses, z["losses"], rtol=1e-5, atol=1e-6)
+    final = _sd(z, "final")
+    for k, v in final.items():
+        assert max_abs(sd[k], v) <= 1e-5, k
+
+
+@pytest.mark.parametrize("tag", ["s64", "s170"])
+def test_oracle_matches_reference_g2(tag):
+    """G2: all 5 levels at small width, CE loss; 170x170 exercises the F.pad branch."""
+    from oracle.unet_ref import unet_forward, unet_loss, unet_param_keys
+    z = _load("g2_unet_multiclass.npz")
+    sd = _sd(z, f"{tag}/init")
+    x, t = torch.from_numpy(z[f"{tag}/x"]), torch.from_numpy(z[f"{tag}/t"])
+    keys = unet_param_keys(sd)
+    params = {k: sd[k].clone().requires_grad_(True) for k in keys}
+    work = dict(sd)
+    work.update(params)
+    y = unet_forward(work, x, 5, 3)
+    loss = unet_loss(y, t, 3)
+    loss.backward()
+    assert max_abs(y, torch.from_numpy(z[f"{tag}/y"])) <= 1e-5
+    assert torch.equal(torch.argmax(torch.softmax(y.detach(), 1), 1), torch.from_numpy(z[f"{tag}/argmax"]))
+    assert abs(float(loss) - float(z[f"{tag}/loss"])) <= 1e-5 * abs(float(z[f"{tag}/loss"]))
+    err, key = grad_err({k: params[k].grad for k in keys}, _sd(z, f"{tag}/grad"))
+    assert err <= 1e-4, (err, key)
+
+
+def test_oracle_dice_matches_reference_g4():
+    from oracle.unet_ref import dice_coeff, trainer_dice
+    z = _load("g4_dice.npz")
+    for case in ("rand", "empty", "ones", "disjoint"):
+        d = dice_coeff(torch.from_numpy(z[f"{case}/pred"]), torch.from_numpy(z[f"{case}/target"]))
+        assert float(d) == pytest.approx(float(z[f"{case}/dice"]), abs=1e-7), case
+    mc = trainer_dice(torch.from_numpy(z["mc/y"]), torch.from_numpy(z["mc/mask"]), 3)
+    assert np.allclose(mc, z["mc/dice"], atol=1e-7)
+    b = trainer_dice(torch.from_numpy(z["bin/y"]), torch.from_numpy(z["bin/mask"]), 1)
+    assert np.allclose(b, z["bin/dice"], atol=1e-7)
+
+
+# ----------------------------------------------------------------------------- drop-in surface
+def test_unet_state_dict_matches_reference_g1():
+    """Same construction order => torch.manual_seed(0) reproduces the reference's weights/keys."""
+    from model import UNet
+    z = _load("g1_unet_c1.npz")
+    ref = _sd(z, "init")
+    torch.manual_seed(0)
+    sd = UNet(1, 1, [16, 32]).state_dict()
+    assert list(sd.keys()) == list(ref.keys())
+    for k in ref:
+        assert torch.equal(sd[k], ref[k]), k
+
+
+def test_unet_state_dict_matches_reference_g2():
+    from model import UNet
+    z = _load("g2_unet_multiclass.npz")
+    ref = _sd(z, "s64/init")
+    torch.manual_seed(0)
+    sd = UNet(1, 3, [4, 8, 16, 32, 64]).state_dict()
+    assert list(sd.keys()) == list(ref.keys())
+    assert all(torch.equal(sd[k], ref[k]) for k in ref)
+
+
+def test_unet_default_is_c2_architecture():
+    from model import UNet
+    net = UNet(1, 1)
+    assert net.num_filters == [64, 128, 256, 512, 1024]
+    assert sum(p.numel() for p in net.parameters()) == 31042369
+    assert len(net.state_dict()) == 136
+
+
+def test_unet_forward_refuses_cpu():
+    """No CPU fallback: the product path must fail loudly without the GPU."""
+    from model import UNet
+    net = UNet(1, 1, [4, 8])
+    with pytest.raises(RuntimeError):
+        net(torch.rand(1, 1, 8, 8))
+
+
+def test_bilinear_up_rejected_like_reference():
+    from model import UNet
+    with pytest.raises(TypeError):
+        UNet(1, 1, [4, 8], bilinear=True)
+
+
+# ----------------------------------------------------------------------------- C ABI
+def _header_functions():
+    from pmu_hip._lib import HEADER_PATH
+    src = open(HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pmu_[A-Za-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from pmu_hip._lib import LIB_PATH, SIGNATURES, load_library
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("libpmunet_hip.so not built (run __graft_entry__.build())")
+    cdll = load_library()
+    names = _header_functions()
+    assert len(names) >= 25
+    for n in names:
+        assert hasattr(cdll, n), f"{n} declared in include/pmunet_hip.h but not exported"
+    assert set(SIGNATURES) == set(names), "ctypes SIGNATURES out of sync with the header"
+
+
+def test_library_rejects_bad_arguments_without_gpu():
+    """Host-side validation returns PMU_ERR_ARG before any launch (safe without a GPU)."""
+    import ctypes
+    from pmu_hip._lib import LIB_PATH, PMU_ERR_ARG, load_library
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("library not built")
+    cdll = load_library()
+    assert cdll.pmu_conv3x3_fwd(None, None, None, 0, None, None, None) == PMU_ERR_ARG
+    assert cdll.pmu_sgd_clip(None, 0, None, ctypes.c_float(1), ctypes.c_float(1), ctypes.c_float(0.9),
+                             ctypes.c_float(0.1), None) == PMU_ERR_ARG
+    assert cdll.pmu_conv3x3_tiles(32, 256, 256) == 32 * 32 * 8
