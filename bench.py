@@ -74,9 +74,9 @@ class KernelTimer:
             f = args[0]._obj
             cframe = sum(f.src[i].C for i in range(f.nsrc))
             if name == "pmu_conv3x3_fwd":
-                cin, cout = cframe, args[3]
+                cin, cout = cframe, args[4]
             elif name == "pmu_conv3x3_dgrad":
-                cout, cin = cframe, args[2]
+                cout, cin = cframe, args[3]
             else:
                 a = args[1]._obj
                 cin, cout = sum(a.src[i].C for i in range(a.nsrc)), args[2]

@@ -75,25 +75,6 @@ struct WT_B {
     return w[(long long)n * Cout * 4 + co * 4 + ab];
   }
 };
-// A[m=ci][k=pixel] = act(frame)
-struct ActColA {
-  static constexpr bool KCONTIG = false;
-  static constexpr bool VEC = false;
-  DevFrame f;
-  PixDecode pd;
-  __device__ float load(long long m, long long k) const {
-    int n, i, j; pd(k, n, i, j);
-    return frame_value(f, n, i, j, (int)m);
-  }
-  __device__ float4 load4(long long, long long) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
-};
-// B[k=pixel][n'=ab*Cout+co] = du gathered
-struct DuGatherB {
-  static constexpr bool KCONTIG = false;
-  DuGatherA g;
-  __device__ float load(long long k, int n) const { return g.load(k, n); }
-};
-
 struct ScatterEp {  // convT forward output
   float* u;
   const float* bias;
@@ -109,13 +90,6 @@ struct RowEp {  // plain row-major store C[m][n]
   float* out;
   int ld;
   __device__ void store(long long m, int col, float v, int) const { out[m * ld + col] = v; }
-};
-struct SlabEp {  // split-K slab ws[split][m][n]
-  float* ws;
-  int M, N;
-  __device__ void store(long long m, int col, float v, int split) const {
-    ws[((long long)split * M + m) * N + col] = v;
-  }
 };
 
 template <class AL, class BL, class EP>
@@ -223,52 +197,124 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(AL al, BL bl, EP ep, long 
   }
 }
 
-// dW[ci][co*4+ab] = sum_s ws[s][ci][ab*Cout+co]
-__global__ void convT_wreduce_kernel(const float* __restrict__ ws, int nsplit, int Cin, int Cout, float* __restrict__ dw) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // ci*(4Cout) + (ab*Cout+co)
-  const long long E = (long long)Cin * 4 * Cout;
-  if (e >= E) return;
-  float s = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) s += ws[(long long)sp * E + e];
-  const int ci = (int)(e / (4 * Cout));
-  const int r = (int)(e - (long long)ci * 4 * Cout);
-  const int ab = r / Cout, co = r - ab * Cout;
-  dw[(long long)ci * 4 * Cout + co * 4 + ab] = s;
-}
+// ---------------------------------------------------------------------------------
+// Weight gradient: dW[ci][co][a][b] = sum_{n,i,j} act[n,i,j,ci] * du[n, oh+2i+a, ow+2j+b, co]
+// Block: 64 ci (M) x 64 co (N) x 4 taps; split-K over 32-pixel tiles of the convT input.
+// LDS: X[32 px][64 ci], D[4 taps][32 px][64 co]; wave w owns (ci frag w>>1, co frag w&1) x 4 taps
+// and reuses its A fragment (act) across the 4 taps.  Blocks of ci-block 0 also accumulate the
+// bias gradient sum du[..][co] from the staged D tile.
+// ---------------------------------------------------------------------------------
+constexpr int TB = 64;    // ci / co per block
+constexpr int TPIX = 32;  // pixels per K tile
 
-// per-block partial bias grads over the convT output region of du: part[blk][Cout]
-constexpr int CB_PPB = 2048;
-__global__ __launch_bounds__(256) void convT_bias_kernel(const float* __restrict__ du, int N, int Hd, int Wd, int off_h,
-                                                         int off_w, int Ho, int Wo, int Cout, float* __restrict__ part) {
-  __shared__ float red[256];
-  const int tid = threadIdx.x;
-  const int cpt = Cout < 256 ? Cout : 256;
-  const int npg = 256 / cpt;
-  const int pg = tid / cpt;
-  const long long P = (long long)N * Ho * Wo;
-  const long long p0 = (long long)blockIdx.x * CB_PPB;
-  for (int c0 = 0; c0 < Cout; c0 += cpt) {
-    const int c = c0 + tid % cpt;
-    float s = 0.f;
-    if (pg < npg && c < Cout) {
-      for (int i = pg; i < CB_PPB; i += npg) {
-        const long long p = p0 + i;
-        if (p >= P) break;
-        const int w = (int)(p % Wo);
-        const int h = (int)((p / Wo) % Ho);
-        const int n = (int)(p / ((long long)Wo * Ho));
-        s += du[(((long long)n * Hd + off_h + h) * Wd + off_w + w) * Cout + c];
-      }
+struct TwArgs {
+  DevFrame act;
+  const float* du;
+  int Hd, Wd, off_h, off_w, Cout, Cin;
+  int twl, tiles_w, tiles_h, ntiles, nsplit;
+  float* ws;   // [split][4][Cin][Cout]
+  float* bws;  // [split][Cout] or null
+};
+
+__global__ __launch_bounds__(256, 2) void convT_wgrad_kernel(TwArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[TPIX * TB + 4 * TPIX * TB];
+  float* Xs = smem;
+  float* Ds = smem + TPIX * TB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int TW = 1 << a.twl, TH = TPIX >> a.twl;
+  const int nci = (a.Cin + TB - 1) / TB;
+  const int ci0 = (blockIdx.x % nci) * TB, co0 = (blockIdx.x / nci) * TB;
+  const int split = blockIdx.y;
+  const int cif = wave >> 1, cof = wave & 1;
+  const bool do_bias = (a.bws != nullptr) && ci0 == 0;
+  const bool vec = (a.Cout & 3) == 0;
+  const DevFrame& X = a.act;
+  const int H = X.H, W = X.W;
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bsum = 0.f;
+
+  const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
+  const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    int t = tile;
+    const int tw = t % a.tiles_w; t /= a.tiles_w;
+    const int th = t % a.tiles_h; t /= a.tiles_h;
+    const int n = t;
+    const int i0 = th * TH, j0 = tw * TW;
+    for (int it = tid; it < TPIX * 16; it += 256) {
+      const int px = it >> 4, cq = it & 15;
+      const float4 v = frame_value4(X, n, i0 + (px >> a.twl), j0 + (px & (TW - 1)), ci0 + 4 * cq);
+      *reinterpret_cast<float4*>(Xs + px * TB + 4 * cq) = v;
     }
-    red[tid] = s;
+    for (int it = tid; it < 4 * TPIX * 16; it += 256) {
+      const int cq = it & 15, px = (it >> 4) & (TPIX - 1), ab = it >> 9;
+      const int i = i0 + (px >> a.twl), j = j0 + (px & (TW - 1));
+      const int co = co0 + 4 * cq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < H && j < W && co < a.Cout) {
+        const long long base = (((long long)n * a.Hd + a.off_h + 2 * i + (ab >> 1)) * a.Wd + a.off_w + 2 * j + (ab & 1)) * a.Cout;
+        if (vec && co + 3 < a.Cout) v = *reinterpret_cast<const float4*>(a.du + base + co);
+        else {
+          v.x = a.du[base + co];
+          v.y = co + 1 < a.Cout ? a.du[base + co + 1] : 0.f;
+          v.z = co + 2 < a.Cout ? a.du[base + co + 2] : 0.f;
+          v.w = co + 3 < a.Cout ? a.du[base + co + 3] : 0.f;
+        }
+      }
+      *reinterpret_cast<float4*>(Ds + (ab * TPIX + px) * TB + 4 * cq) = v;
+    }
     __syncthreads();
-    if (pg == 0 && c < Cout) {
-      float t = 0.f;
-      for (int l = 0; l < npg; ++l) t += red[l * cpt + tid % cpt];
-      part[(long long)blockIdx.x * Cout + c] = t;
+    if (do_bias) {  // thread -> (co = tid & 63, tap = tid >> 6): sum over the tile's pixels
+      const float* d = Ds + (tid >> 6) * TPIX * TB + (tid & 63);
+#pragma unroll 8
+      for (int px = 0; px < TPIX; ++px) bsum += d[px * TB];
+    }
+#pragma unroll 4
+    for (int ks = 0; ks < TPIX / 2; ++ks) {
+      const int px = 2 * ks + (lane >> 5);
+      const float av = Xs[px * TB + cif * 32 + (lane & 31)];
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) {
+        const float bv = Ds[(ab * TPIX + px) * TB + cof * 32 + (lane & 31)];
+        acc[ab] = mfma_f32_32x32x2(av, bv, acc[ab]);
+      }
     }
     __syncthreads();
   }
+  const int co = co0 + cof * 32 + (lane & 31);
+  if (co < a.Cout) {
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = ci0 + cif * 32 + acc_row(r, lane);
+        if (ci < a.Cin) a.ws[(((long long)split * 4 + ab) * a.Cin + ci) * a.Cout + co] = acc[ab][r];
+      }
+  }
+  if (do_bias) {
+    Xs[tid] = bsum;  // LDS no longer read by the MFMA loop (last barrier passed)
+    __syncthreads();
+    if (tid < 64 && co0 + tid < a.Cout)
+      a.bws[(long long)split * a.Cout + co0 + tid] = Xs[tid] + Xs[64 + tid] + Xs[128 + tid] + Xs[192 + tid];
+  }
+}
+
+// dW[ci][co][a][b] = sum_s ws[s][ab][ci][co]
+__global__ void convT_wreduce_kernel(const float* __restrict__ ws, int nsplit, int Cin, int Cout, float* __restrict__ dw) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (ab*Cin + ci)*Cout + co
+  const long long CC = (long long)Cin * Cout;
+  const long long E = 4 * CC;
+  if (e >= E) return;
+  float s = 0.f;
+  for (int sp = 0; sp < nsplit; ++sp) s += ws[(long long)sp * E + e];
+  const int ab = (int)(e / CC);
+  const long long cc = e - ab * CC;  // ci*Cout + co
+  dw[cc * 4 + ab] = s;
 }
 
 __global__ void rows_sum_f32_kernel(const float* __restrict__ ws, int R, int Wd, float* __restrict__ out) {
@@ -279,15 +325,18 @@ __global__ void rows_sum_f32_kernel(const float* __restrict__ ws, int R, int Wd,
   out[o] = (float)s;
 }
 
-static void convT_wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* nsplit, int* cps) {
-  const long long K = (long long)N * H * W;
-  const long long nch = (K + GK - 1) / GK;
-  const int bmn = pmu_cdiv(Cin, GM) * pmu_cdiv(4 * Cout, GN);
-  long long s = 1024 / bmn;
-  if (s < 1) s = 1;
-  if (s > nch) s = nch;
-  *cps = (int)((nch + s - 1) / s);
-  *nsplit = (int)((nch + *cps - 1) / *cps);
+static void convT_wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* twl, int* tiles_w, int* tiles_h,
+                                 int* ntiles, int* nsplit) {
+  *twl = (W > 4) ? 3 : 2;  // 4x8 or 8x4 pixel tiles
+  const int TW = 1 << *twl, TH = TPIX / TW;
+  *tiles_w = pmu_cdiv(W, TW);
+  *tiles_h = pmu_cdiv(H, TH);
+  *ntiles = N * *tiles_w * *tiles_h;
+  const int bmn = pmu_cdiv(Cin, TB) * pmu_cdiv(Cout, TB);
+  int sp = 1024 / bmn;
+  if (sp < 1) sp = 1;
+  if (sp > *ntiles) sp = *ntiles;
+  *nsplit = sp;
 }
 
 }  // namespace
@@ -326,11 +375,9 @@ extern "C" int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, in
 }
 
 extern "C" size_t pmu_convT2x2_wgrad_ws(int N, int H, int W, int Cin, int Cout) {
-  int ns, cps;
-  convT_wgrad_geometry(N, H, W, Cin, Cout, &ns, &cps);
-  const size_t slab = (size_t)ns * Cin * 4 * Cout * sizeof(float);
-  const size_t bias = (size_t)pmu_cdiv((long long)N * 2 * H * 2 * W, CB_PPB) * Cout * sizeof(float);
-  return slab > bias ? slab : bias;
+  int twl, tw, th, nt, ns;
+  convT_wgrad_geometry(N, H, W, Cin, Cout, &twl, &tw, &th, &nt, &ns);
+  return (size_t)ns * (4 * (size_t)Cin * Cout + Cout) * sizeof(float);
 }
 
 extern "C" int pmu_convT2x2_wgrad(const float* du, int Hd, int Wd, int off_h, int off_w, const pmu_frame* act,
@@ -338,31 +385,23 @@ extern "C" int pmu_convT2x2_wgrad(const float* du, int Hd, int Wd, int off_h, in
   PMU_REQUIRE(du && valid_frame(act) && dw && ws && Cout > 0);
   const int N = act->N, H = act->H, W = act->W;
   PMU_REQUIRE(off_h >= 0 && off_w >= 0 && off_h + 2 * H <= Hd && off_w + 2 * W <= Wd);
-  PMU_REQUIRE(ws_bytes >= pmu_convT2x2_wgrad_ws(N, H, W, act->src[0].C + (act->nsrc > 1 ? act->src[1].C : 0), Cout));
-  ActColA al{make_dev_frame(act), PixDecode{H, W}};
-  const int Cin = al.f.C;
-  DuGatherB bl{DuGatherA{du, Hd, Wd, off_h, off_w, Cout, PixDecode{H, W}}};
-  const int NN = 4 * Cout;
-  SlabEp ep{ws, Cin, NN};
-  int ns, cps;
-  convT_wgrad_geometry(N, H, W, Cin, Cout, &ns, &cps);
-  const long long K = (long long)N * H * W;
-  dim3 grid((unsigned)pmu_cdiv(Cin, GM), (unsigned)pmu_cdiv(NN, GN), (unsigned)ns);
-  hipLaunchKernelGGL((gemm_kernel<ActColA, DuGatherB, SlabEp>), grid, dim3(256), 0, (hipStream_t)stream, al, bl, ep,
-                     (long long)Cin, NN, K, cps);
+  TwArgs a;
+  a.act = make_dev_frame(act);
+  a.du = du; a.Hd = Hd; a.Wd = Wd; a.off_h = off_h; a.off_w = off_w; a.Cout = Cout; a.Cin = a.act.C;
+  convT_wgrad_geometry(N, H, W, a.Cin, Cout, &a.twl, &a.tiles_w, &a.tiles_h, &a.ntiles, &a.nsplit);
+  PMU_REQUIRE(ws_bytes >= pmu_convT2x2_wgrad_ws(N, H, W, a.Cin, Cout));
+  a.ws = ws;
+  a.bws = dbias ? ws + (size_t)a.nsplit * 4 * a.Cin * Cout : nullptr;
+  dim3 grid((unsigned)(pmu_cdiv(a.Cin, TB) * pmu_cdiv(Cout, TB)), (unsigned)a.nsplit);
+  hipLaunchKernelGGL(convT_wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   PMU_CHECK_LAUNCH();
-  const long long E = (long long)Cin * NN;
+  const long long E = 4LL * a.Cin * Cout;
   hipLaunchKernelGGL(convT_wreduce_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const float*)ws, ns, Cin, Cout, dw);
+                     (const float*)ws, a.nsplit, a.Cin, Cout, dw);
   PMU_CHECK_LAUNCH();
   if (dbias) {
-    // the slab is consumed; reuse the workspace for the bias partials (same stream => ordered)
-    const int R = pmu_cdiv((long long)N * 2 * H * 2 * W, CB_PPB);
-    hipLaunchKernelGGL(convT_bias_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, du, N, Hd, Wd, off_h,
-                       off_w, 2 * H, 2 * W, Cout, ws);
-    PMU_CHECK_LAUNCH();
     hipLaunchKernelGGL(rows_sum_f32_kernel, dim3((unsigned)pmu_cdiv(Cout, 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const float*)ws, R, Cout, dbias);
+                       (const float*)a.bws, a.nsplit, Cout, dbias);
     PMU_CHECK_LAUNCH();
   }
   return PMU_OK;

@@ -181,8 +181,9 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
     else:
         R = lb.pmu_conv3x3_tiles(N, H, W)
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
-        L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), L.ptr(conv.bias), Cout,
-               z.data_ptr(), L.ptr(part), s)
+        wp = pack_weights(conv.weight, dgrad=False)
+        L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), wp.data_ptr(), L.ptr(conv.bias),
+               Cout, z.data_ptr(), L.ptr(part), s)
     st = bn_forward(part, R, Cout, N * H * W, bn, training, dev)
     return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes)
 
@@ -215,14 +216,26 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     if not need_dx or out.planes is not None:
         return None
     Cin = conv.in_channels
+    wp = pack_weights(conv.weight, dgrad=True)
     if split is None:
         dx = _empty(N, H, W, Cin, device=dev)
-        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), Cin, Cin, dx.data_ptr(), None, s)
+        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, Cin, dx.data_ptr(), None, s)
         return dx
     dx0 = _empty(N, H, W, split, device=dev)
     dx1 = _empty(N, H, W, Cin - split, device=dev)
-    L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), Cin, split, dx0.data_ptr(), dx1.data_ptr(), s)
+    L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, split, dx0.data_ptr(),
+           dx1.data_ptr(), s)
     return dx0, dx1
+
+
+def pack_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """Weights re-laid out as the conv kernel's per-block B tiles (pmu_conv3x3_pack); one launch,
+    ~2x the weight bytes of traffic, so staging inside the conv is a straight copy."""
+    Cout, Cin = w.shape[0], w.shape[1]
+    n = L.lib().pmu_conv3x3_packed_size(Cout, Cin, int(dgrad)) // 4
+    wp = _empty(n, device=w.device)
+    L.call("pmu_conv3x3_pack", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
 
 
 # ----------------------------------------------------------------------------------------

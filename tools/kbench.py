@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Per-shape timing of the conv kernels on the c2 layer shapes (batch 32, 256x256 input).
+
+    python tools/kbench.py [--ops fwd,dgrad,wgrad,convT] [--iters 20]
+
+Prints one line per (op, layer shape) with ms and TFLOP/s (f32 MFMA peak 157.3)."""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "probabilistic-multiplanar-unet_amd"))
+import torch  # noqa: E402
+
+from pmu_hip import _lib as L  # noqa: E402
+from pmu_hip.engine import Src, frame_of  # noqa: E402
+
+# (H, Cin, Cout) of every 3x3 conv of the c2 U-Net (encoder, then decoder)
+SHAPES = [(256, 64, 64), (128, 64, 128), (128, 128, 128), (64, 128, 256), (64, 256, 256), (32, 256, 512),
+          (32, 512, 512), (16, 512, 1024), (16, 1024, 1024),
+          (32, 1024, 512), (64, 512, 256), (128, 256, 128), (256, 128, 64)]
+
+
+def timeit(fn, iters):
+    for _ in range(2):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--N", type=int, default=32)
+    ap.add_argument("--only", default=None, help="H,Cin,Cout of a single shape")
+    ap.add_argument("--unpacked", action="store_true", help="stage weights from the PyTorch layout")
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    N = args.N
+    s = L.stream()
+    tot = {}
+    shapes = SHAPES if args.only is None else [tuple(int(v) for v in args.only.split(","))]
+    for (H, Cin, Cout) in shapes:
+        W = H
+        z = torch.randn(N, H, W, Cin, device=dev)
+        coef = torch.cat([torch.rand(Cin, device=dev) + 0.5, torch.randn(Cin, device=dev) * 0.1])
+        w = torch.randn(Cout, Cin, 3, 3, device=dev) * 0.05
+        b = torch.zeros(Cout, device=dev)
+        out = torch.empty(N, H, W, Cout, device=dev)
+        flops = 2.0 * N * H * W * Cin * Cout * 9
+        R = L.lib().pmu_conv3x3_tiles(N, H, W)
+        part = torch.empty(R, 2 * Cout, device=dev)
+        fin = frame_of([Src(z, L.SRC_BNRELU, coef)], N, H, W)
+        da = torch.randn(N, H, W, Cout, device=dev)
+        zz = torch.randn(N, H, W, Cout, device=dev)
+        bco = torch.cat([torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev) * 0.1,
+                         torch.randn(Cout, device=dev) * 0.1, torch.randn(Cout, device=dev) * 0.01,
+                         torch.randn(Cout, device=dev) * 0.01])
+        fdz = frame_of([Src(da, L.SRC_BNBWD, bco, z=zz)], N, H, W)
+        dx = torch.empty(N, H, W, Cin, device=dev)
+        dw = torch.empty_like(w)
+        wsb = L.lib().pmu_conv3x3_wgrad_ws(N, H, W, Cin, Cout)
+        ws = torch.empty(wsb // 4 + 1, device=dev)
+        from pmu_hip.engine import pack_weights
+        wpf = pack_weights(w, False) if not args.unpacked else None
+        wpd = pack_weights(w, True) if not args.unpacked else None
+        ops = {
+            "fwd": lambda: L.call("pmu_conv3x3_fwd", fin, w.data_ptr(), L.ptr(wpf), b.data_ptr(), Cout,
+                                  out.data_ptr(), part.data_ptr(), s),
+            "dgrad": lambda: L.call("pmu_conv3x3_dgrad", fdz, w.data_ptr(), L.ptr(wpd), Cin, Cin, dx.data_ptr(),
+                                    None, s),
+            "pack": lambda: pack_weights(w, False),
+            "wgrad": lambda: L.call("pmu_conv3x3_wgrad", fdz, fin, Cout, dw.data_ptr(), ws.data_ptr(), wsb, s),
+        }
+        for op in args.ops.split(","):
+            if op not in ops:
+                continue
+            ms = timeit(ops[op], args.iters)
+            tf = flops / (ms * 1e-3) / 1e12
+            tot.setdefault(op, [0.0, 0.0])
+            tot[op][0] += ms
+            tot[op][1] += flops
+            print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / 157.3 * 100:5.1f}%)",
+                  flush=True)
+    for op, (ms, fl) in tot.items():
+        print(f"TOTAL {op:6s} {ms:8.3f} ms  {fl / (ms * 1e-3) / 1e12:7.2f} TF")
+
+
+if __name__ == "__main__":
+    main()
