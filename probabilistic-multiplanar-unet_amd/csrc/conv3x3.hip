@@ -8,20 +8,18 @@
 // GEMM view (forward):  M = output pixels, N = Cout, K = 9 * Cin.
 //   Per K chunk of BK input channels ONE (TH+2) x (TW+2) halo tile of the transformed input is
 //   staged in LDS; all 9 taps read shifted windows of it (im2col-free).  Weights of the chunk
-//   are staged as B[tap][cout][k].
+//   are staged as B[tap][cout][k] from a pre-packed copy (pmu_conv3x3_pack) by straight copy.
 // GEMM view (input gradient, "dgrad"): the same kernel with the roles of Cin/Cout swapped and
 //   the taps flipped: dx[p][ci] = sum_{tap,co} dz[p + d(tap)][co] * w[co][ci][8 - tap].
 //
-// Block = 8 waves, warp-specialised: waves 0-3 are MFMA consumers, waves 4-7 are producers that
-// stage chunk c+1 (global -> VGPR -> BN/ReLU/pool/concat transform -> LDS) into the other half
-// of a double-buffered LDS ring while the consumers run chunk c.  One barrier per chunk.
-// Tile: 256 pixels (TH x TW, TW in {32,16,8}) x 64 output channels; consumer wave w owns pixels
-// [64w, 64w+64) x all 64 channels = 2 x 2 32x32 accumulators.
+// Block: 256 threads (4 waves), 2 blocks per CU (73 KB LDS each) so one block's staging overlaps
+// the other's MFMAs.  Tile: 256 pixels (TH x TW, TW in {32,16,8}) x 64 output channels; wave w
+// owns pixels [64w, 64w+64) x 64 channels = 2 x 2 32x32 accumulators.
 // LDS rows are k-contiguous (BK = 16 floats + 4 pad): lane half h reads k = 8h..8h+7 with two
 // ds_read_b128 and feeds one k per MFMA step (the K order inside a chunk is free as long as A
-// and B agree), conflict-free for 16 consecutive rows.
-#include "pmu_common.h"
-#include <stdlib.h>
+// and B agree), conflict-free for 16 consecutive rows.  The next tap's 8 reads are issued ahead
+// of the current tap's 32 MFMAs.
+#include "pmu_stage.h"
 
 namespace {
 
@@ -31,8 +29,8 @@ constexpr int BK = 16;      // reduction channels per chunk
 constexpr int LS = BK + 4;  // LDS row stride (floats)
 constexpr int MAX_HP = 340; // max halo pixels: (8+2)*(32+2) = (32+2)*(8+2) = 340, (16+2)^2 = 324
 constexpr int A_FLOATS = MAX_HP * LS;
-constexpr int STAGE = A_FLOATS + 9 * BN * LS;  // floats per ring slot
-constexpr int A_ITEMS_MAX = 6;                 // ceil(340*4 / 256)
+constexpr int STAGE = A_FLOATS + 9 * BN * LS;
+constexpr int NI = 6;       // A items per thread: ceil(340*4 / 256)
 
 struct ConvArgs {
   DevFrame in;       // operand frame (fwd: activation; dgrad: dz)
@@ -46,7 +44,6 @@ struct ConvArgs {
   int split;         // dgrad channel split
   int twl;           // log2(TW)
   int tiles_w, tiles_h;
-  int dgrad;
 };
 
 // Packed weights: wp[jb][ch][tap][jl][kl] (jb = N block of BN, ch = K chunk of BK), zero padded,
@@ -73,173 +70,40 @@ __global__ __launch_bounds__(256) void pack_w_kernel(const float* __restrict__ w
   }
 }
 
-// producer: copy chunk ch of the packed B operand (9 taps x BN x BK) into padded LDS rows
-__device__ __forceinline__ void stage_B_packed(const float* wp, int jb, int ch, int nch, float* Bs, int ptid, int nthr) {
-  const float4* src = reinterpret_cast<const float4*>(wp + ((long long)jb * nch + ch) * (9 * BN * BK));
-  constexpr int NV = 9 * BN * BK / 4;  // 2304 float4
-#pragma unroll 3
-  for (int it = ptid; it < NV; it += nthr) {
-    const int row = it >> 2, q = it & 3;
-    *reinterpret_cast<float4*>(Bs + row * LS + 4 * q) = src[it];
-  }
-}
-
-// producer: stage chunk k0 of the B operand (9 taps x BN x BK) into Bs
+// stage chunk k0 of the B operand (9 taps x BN x BK) into Bs
 template <bool DGRAD>
-__device__ __forceinline__ void stage_B(const ConvArgs& a, int j0, int k0, bool bvec, float* Bs, int ptid) {
-  if (a.wp) {
-    stage_B_packed(a.wp, j0 / BN, k0 / BK, (a.KC + BK - 1) / BK, Bs, ptid, 256);
+__device__ __forceinline__ void stage_B(const ConvArgs& a, int j0, int k0, float* Bs, int tid) {
+  if (a.wp) {  // straight copy of the packed tile into padded rows
+    const int nch = (a.KC + BK - 1) / BK;
+    const float4* src = reinterpret_cast<const float4*>(a.wp + ((long long)(j0 / BN) * nch + k0 / BK) * (9 * BN * BK));
+#pragma unroll 3
+    for (int it = tid; it < 9 * BN * BK / 4; it += 256) {
+      const int row = it >> 2, q = it & 3;
+      *reinterpret_cast<float4*>(Bs + row * LS + 4 * q) = src[it];
+    }
     return;
   }
-  if (bvec) {
-    if (!DGRAD) {
-      // per output channel co: w[co][k0..k0+16][0..9) is 144 contiguous floats
-#pragma unroll 3
-      for (int it = ptid; it < BN * 36; it += 256) {
-        const int jl = it / 36, q = it - jl * 36;
-        const float4 v = *reinterpret_cast<const float4*>(a.w + ((long long)(j0 + jl) * a.KC + k0) * 9 + 4 * q);
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int idx = 4 * q + e, kl = idx / 9, tap = idx - kl * 9;
-          Bs[(tap * BN + jl) * LS + kl] = vv[e];
-        }
-      }
-    } else {
-      // per reduction channel co (= k): w[co][j0..j0+64][0..9) is 576 contiguous floats
-#pragma unroll 3
-      for (int it = ptid; it < BK * 144; it += 256) {
-        const int kl = it / 144, q = it - kl * 144;
-        const float4 v = *reinterpret_cast<const float4*>(a.w + ((long long)(k0 + kl) * a.NOUT + j0) * 9 + 4 * q);
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int idx = 4 * q + e, jl = idx / 9, tap = idx - jl * 9;
-          Bs[((8 - tap) * BN + jl) * LS + kl] = vv[e];
-        }
-      }
-    }
-  } else {
-    for (int it = ptid; it < 9 * BN * BK; it += 256) {
-      const int kl = it % BK;
-      const int jl = (it / BK) % BN;
-      const int tap = it / (BK * BN);
-      const int j = j0 + jl, k = k0 + kl;
-      float v = 0.f;
-      if (j < a.NOUT && k < a.KC) {
-        v = DGRAD ? a.w[((long long)k * a.NOUT + j) * 9 + (8 - tap)] : a.w[((long long)j * a.KC + k) * 9 + tap];
-      }
-      Bs[(tap * BN + jl) * LS + kl] = v;
-    }
+  for (int it = tid; it < 9 * BN * BK; it += 256) {  // from the PyTorch layout (no pack)
+    const int kl = it % BK;
+    const int jl = (it / BK) % BN;
+    const int tap = it / (BK * BN);
+    const int j = j0 + jl, k = k0 + kl;
+    float v = 0.f;
+    if (j < a.NOUT && k < a.KC)
+      v = DGRAD ? a.w[((long long)k * a.NOUT + j) * 9 + (8 - tap)] : a.w[((long long)j * a.KC + k) * 9 + tap];
+    Bs[(tap * BN + jl) * LS + kl] = v;
   }
 }
 
-// ---------------------------------------------------------------------------------
-// Fast A staging for a chunk lying entirely in one source with C % 4 == 0.  Every item of a
-// producer thread uses the same 4 channels (item index = ptid + 256 i, channel quad = ptid & 3),
-// so the per-channel coefficients are loaded once per chunk; addresses are clamped and masked
-// so that all loads of the chunk are issued before the first wait.
-// ---------------------------------------------------------------------------------
-__device__ __forceinline__ float4 bnrelu4(float4 x, float4 sc, float4 sh) {
-  return make_float4(fmaxf(0.f, fmaf(x.x, sc.x, sh.x)), fmaxf(0.f, fmaf(x.y, sc.y, sh.y)),
-                     fmaxf(0.f, fmaf(x.z, sc.z, sh.z)), fmaxf(0.f, fmaf(x.w, sc.w, sh.w)));
-}
-__device__ __forceinline__ float bnbwd1(float d, float z, float sc, float sh, float mu, float kx, float kc) {
-  return fmaf(sc, fmaf(z, sc, sh) > 0.f ? d : 0.f, fmaf(kx, z - mu, kc));
-}
-__device__ __forceinline__ float4 max4(float4 a, float4 b) {
-  return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
-}
-
-template <int MODE, int POOL>
-__device__ __forceinline__ void stage_A_fast(const DevSrc& s, int c, int n, const int (&ih)[A_ITEMS_MAX],
-                                             const int (&iw)[A_ITEMS_MAX], const int (&icq)[A_ITEMS_MAX], float* As) {
-  float4 sc = make_float4(0, 0, 0, 0), sh = sc, mu = sc, kx = sc, kc = sc;
-  if (MODE != PMU_SRC_RAW) {
-    sc = *reinterpret_cast<const float4*>(s.coef + c);
-    sh = *reinterpret_cast<const float4*>(s.coef + s.C + c);
-  }
-  if (MODE == PMU_SRC_BNBWD) {
-    mu = *reinterpret_cast<const float4*>(s.coef + 2 * s.C + c);
-    kx = *reinterpret_cast<const float4*>(s.coef + 3 * s.C + c);
-    kc = *reinterpret_cast<const float4*>(s.coef + 4 * s.C + c);
-  }
-  constexpr int NL = (POOL == PMU_POOL_MAX2) ? 4 : 1;
-  float4 xv[A_ITEMS_MAX][NL];
-  float4 zv[A_ITEMS_MAX];
-  bool ok[A_ITEMS_MAX];
-  const long long rs = (long long)s.W * s.C;
-#pragma unroll
-  for (int i = 0; i < A_ITEMS_MAX; ++i) {
-    int hs = ih[i] - s.off_h, ws = iw[i] - s.off_w;
-    if (POOL == PMU_POOL_MAX2) { hs *= 2; ws *= 2; }
-    const int lim_h = (POOL == PMU_POOL_MAX2) ? s.H - 1 : s.H;
-    const int lim_w = (POOL == PMU_POOL_MAX2) ? s.W - 1 : s.W;
-    ok[i] = (ih[i] != -0x4000) && hs >= 0 && ws >= 0 && hs < lim_h && ws < lim_w;
-    const long long idx = ok[i] ? (((long long)n * s.H + hs) * s.W + ws) * s.C + c : (long long)c;
-    xv[i][0] = *reinterpret_cast<const float4*>(s.x + idx);
-    if (POOL == PMU_POOL_MAX2) {
-      xv[i][1] = *reinterpret_cast<const float4*>(s.x + idx + s.C);
-      xv[i][2] = *reinterpret_cast<const float4*>(s.x + idx + rs);
-      xv[i][3] = *reinterpret_cast<const float4*>(s.x + idx + rs + s.C);
-    }
-    if (MODE == PMU_SRC_BNBWD) zv[i] = *reinterpret_cast<const float4*>(s.z + idx);
-  }
-#pragma unroll
-  for (int i = 0; i < A_ITEMS_MAX; ++i) {
-    if (ih[i] == -0x4000) continue;
-    float4 v;
-    if (MODE == PMU_SRC_RAW) {
-      v = xv[i][0];
-    } else if (MODE == PMU_SRC_BNRELU) {
-      v = bnrelu4(xv[i][0], sc, sh);
-      if (POOL == PMU_POOL_MAX2) {
-        v = max4(v, bnrelu4(xv[i][1], sc, sh));
-        v = max4(v, bnrelu4(xv[i][2], sc, sh));
-        v = max4(v, bnrelu4(xv[i][3], sc, sh));
-      }
-    } else {
-      const float4 d = xv[i][0], z = zv[i];
-      v = make_float4(bnbwd1(d.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x), bnbwd1(d.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y),
-                      bnbwd1(d.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z), bnbwd1(d.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w));
-    }
-    if (!ok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(As + icq[i]) = v;
-  }
-}
-
-// stage the A operand of chunk k0 (BK channels): fast paths when the chunk lies in one source
-__device__ __forceinline__ void stage_A(const DevFrame& F, int n, int k0, int cq, const int (&ih)[A_ITEMS_MAX],
-                                        const int (&iw)[A_ITEMS_MAX], const int (&icq)[A_ITEMS_MAX], float* As) {
-  const bool in0 = k0 + BK <= F.C0;
-  const bool in1 = F.nsrc > 1 && k0 >= F.C0 && k0 + BK <= F.C;
-  if (F.vec && (in0 || in1)) {
-    const DevSrc& s = in0 ? F.s0 : F.s1;
-    const int c = (in0 ? k0 : k0 - F.C0) + 4 * cq;
-    if (s.pool == PMU_POOL_NONE) {
-      if (s.mode == PMU_SRC_BNRELU) return stage_A_fast<PMU_SRC_BNRELU, PMU_POOL_NONE>(s, c, n, ih, iw, icq, As);
-      if (s.mode == PMU_SRC_BNBWD) return stage_A_fast<PMU_SRC_BNBWD, PMU_POOL_NONE>(s, c, n, ih, iw, icq, As);
-      return stage_A_fast<PMU_SRC_RAW, PMU_POOL_NONE>(s, c, n, ih, iw, icq, As);
-    }
-    if (s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU)
-      return stage_A_fast<PMU_SRC_BNRELU, PMU_POOL_MAX2>(s, c, n, ih, iw, icq, As);
-  }
-  // generic path (avg pool, mixed-source chunk, tiny channel counts)
-#pragma unroll
-  for (int i = 0; i < A_ITEMS_MAX; ++i)
-    if (ih[i] != -0x4000) *reinterpret_cast<float4*>(As + icq[i]) = frame_value4(F, n, ih[i], iw[i], k0 + 4 * cq);
-}
-
-// SPEC: 8 waves, warp-specialised producer/consumer over a 2-slot LDS ring (1 block per CU);
-// otherwise 4 waves that all stage and all compute over one LDS slot (2 blocks per CU).
-template <bool DGRAD, bool SPEC, bool PIN>
-__global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 2 : 2) void conv3x3_kernel(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[SPEC ? 2 * STAGE : STAGE];
+template <bool DGRAD>
+__global__ __launch_bounds__(256, 2) void conv3x3_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[STAGE];
+  float* As = smem;
+  float* Bs = smem + A_FLOATS;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const bool producer = SPEC ? (wave >= 4) : true;
   const int TW = 1 << a.twl;
   const int TH = BM >> a.twl;
   const int HW2 = TW + 2;
@@ -253,28 +117,25 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 2 : 2) void conv3x3_kernel
   const int j0 = blockIdx.y * BN;
   const DevFrame& F = a.in;
   const int nchunks = (a.KC + BK - 1) / BK;
-  const bool bvec = ((a.KC % BK) == 0) && ((a.NOUT % 4) == 0) && (j0 + BN <= a.NOUT);
 
-  // ---------------- producer state: chunk-independent halo coordinates of its A items
-  const int ptid = SPEC ? tid - 256 : tid;
-  int ih[A_ITEMS_MAX], iw[A_ITEMS_MAX], icq[A_ITEMS_MAX];
+  // staging items (chunk-independent): halo pixel of item i and its LDS row; quad = tid & 3
+  int ih[NI], iw[NI], dst[NI];
 #pragma unroll
-  for (int i = 0; i < A_ITEMS_MAX; ++i) {
-    const int it = ptid + 256 * i;
+  for (int i = 0; i < NI; ++i) {
+    const int it = tid + 256 * i;
     const int hp = it >> 2;
     const int hr = hp / HW2, hc = hp - hr * HW2;
-    ih[i] = (it < HP * 4) ? h0 - 1 + hr : -0x4000;  // -0x4000 marks "no item"
+    ih[i] = (it < HP * 4) ? h0 - 1 + hr : PMU_NO_ITEM;
     iw[i] = w0 - 1 + hc;
-    icq[i] = (hp * LS) + 4 * (it & 3);
+    dst[i] = hp * LS + 4 * (it & 3);
   }
 
-  // ---------------- consumer state
+  // MFMA operand addressing
   const int hsel = (lane >> 5) * 8;
   int abase[2], bbase[2];
-  const int cw = wave & 3;
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm) {
-    const int q = cw * 64 + fm * 32 + (lane & 31);
+    const int q = wave * 64 + fm * 32 + (lane & 31);
     const int r = q >> a.twl, c = q & (TW - 1);
     abase[fm] = (r * HW2 + c) * LS + hsel;
   }
@@ -289,15 +150,13 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 2 : 2) void conv3x3_kernel
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  auto stage = [&](int ch, float* As) {
-    stage_A(F, n, ch * BK, ptid & 3, ih, iw, icq, As);
-    stage_B<DGRAD>(a, j0, ch * BK, bvec, As + A_FLOATS, ptid);
-  };
-  auto compute = [&](const float* As) {
-    const float* Bs = As + A_FLOATS;
-    // operand registers double-buffered across taps: tap t+1's ds_reads are issued ahead of
-    // tap t's 32 MFMAs (pinned below with sched_group_barrier)
-    float4 op[2][8];
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int k0 = ch * BK;
+    stage_items<NI>(F, n, k0, BK, tid & 3, ih, iw, dst, As);
+    stage_B<DGRAD>(a, j0, k0, Bs, tid);
+    __syncthreads();
+
+    float4 op[2][8];  // operand registers double-buffered across taps
     auto load_ops = [&](int tap, float4 (&o)[8]) {
       const int toff = ((tap / 3) * HW2 + (tap % 3)) * LS;
 #pragma unroll
@@ -330,76 +189,45 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 2 : 2) void conv3x3_kernel
       if (tap + 1 < 9) load_ops(tap + 1, op[(tap + 1) & 1]);
       mfmas(op[tap & 1]);
     }
-    if constexpr (PIN) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        if (tap + 1 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);
-      }
-    }
-  };
-
-  if constexpr (SPEC) {
-    if (producer) stage(0, smem);
     __syncthreads();
-    for (int ch = 0; ch < nchunks; ++ch) {
-      if (producer) {
-        if (ch + 1 < nchunks) stage(ch + 1, smem + ((ch + 1) & 1) * STAGE);
-      } else {
-        compute(smem + (ch & 1) * STAGE);
-      }
-      __syncthreads();
-    }
-  } else {
-    for (int ch = 0; ch < nchunks; ++ch) {
-      stage(ch, smem);
-      __syncthreads();
-      compute(smem);
-      __syncthreads();
-    }
   }
 
-  // ---------------- epilogue (consumers)
-  float* red = smem;  // [4 waves][64 ch][2], ring no longer read
+  // ---------------- epilogue
+  float* red = smem;  // [4 waves][64 ch][2]
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
-  if (!SPEC || !producer) {
 #pragma unroll
-    for (int fn = 0; fn < 2; ++fn) {
-      const int j = j0 + fn * 32 + (lane & 31);
-      const bool jok = j < a.NOUT;
-      const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+  for (int fn = 0; fn < 2; ++fn) {
+    const int j = j0 + fn * 32 + (lane & 31);
+    const bool jok = j < a.NOUT;
+    const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
 #pragma unroll
-      for (int fm = 0; fm < 2; ++fm) {
+    for (int fm = 0; fm < 2; ++fm) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int q = cw * 64 + fm * 32 + acc_row(r, lane);
-          const int h = h0 + (q >> a.twl), w = w0 + (q & (TW - 1));
-          if (!jok || h >= F.H || w >= F.W) continue;
-          const long long pix = ((long long)n * F.H + h) * F.W + w;
-          const float v = acc[fm][fn][r] + b;
-          if (!DGRAD) {
-            a.out0[pix * a.NOUT + j] = v;
-            s1[fn] += v;
-            s2[fn] = fmaf(v, v, s2[fn]);
-          } else {
-            if (j < a.split) a.out0[pix * a.split + j] = v;
-            else a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
-          }
+      for (int r = 0; r < 16; ++r) {
+        const int q = wave * 64 + fm * 32 + acc_row(r, lane);
+        const int h = h0 + (q >> a.twl), w = w0 + (q & (TW - 1));
+        if (!jok || h >= F.H || w >= F.W) continue;
+        const long long pix = ((long long)n * F.H + h) * F.W + w;
+        const float v = acc[fm][fn][r] + b;
+        if (!DGRAD) {
+          a.out0[pix * a.NOUT + j] = v;
+          s1[fn] += v;
+          s2[fn] = fmaf(v, v, s2[fn]);
+        } else {
+          if (j < a.split) a.out0[pix * a.split + j] = v;
+          else a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
         }
       }
     }
   }
   if (!DGRAD && a.part) {
-    if (!SPEC || !producer) {
 #pragma unroll
-      for (int fn = 0; fn < 2; ++fn) {
-        s1[fn] += __shfl_xor(s1[fn], 32, 64);
-        s2[fn] += __shfl_xor(s2[fn], 32, 64);
-        if (lane < 32) {
-          red[(cw * 64 + fn * 32 + lane) * 2 + 0] = s1[fn];
-          red[(cw * 64 + fn * 32 + lane) * 2 + 1] = s2[fn];
-        }
+    for (int fn = 0; fn < 2; ++fn) {
+      s1[fn] += __shfl_xor(s1[fn], 32, 64);
+      s2[fn] += __shfl_xor(s2[fn], 32, 64);
+      if (lane < 32) {
+        red[(wave * 64 + fn * 32 + lane) * 2 + 0] = s1[fn];
+        red[(wave * 64 + fn * 32 + lane) * 2 + 1] = s2[fn];
       }
     }
     __syncthreads();
@@ -419,17 +247,6 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 2 : 2) void conv3x3_kernel
   }
 }
 
-// kernel schedule variant (bit 0: warp-specialised, bit 1: pinned consumer schedule);
-// PMU_CONV_VARIANT overrides the default for A/B measurements.
-static int conv_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PMU_CONV_VARIANT");
-    v = e ? atoi(e) : 2;
-  }
-  return v;
-}
-
 static int pick_twl(int W) {
   if (W > 16) return 5;
   if (W > 8) return 4;
@@ -441,25 +258,16 @@ static int launch_conv(const pmu_frame* in, const float* w, const float* wp, con
   ConvArgs a;
   a.in = make_dev_frame(in);
   a.w = w; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
-  a.NOUT = NOUT; a.KC = KC; a.split = split; a.dgrad = dgrad;
+  a.NOUT = NOUT; a.KC = KC; a.split = split;
   a.twl = pick_twl(in->W);
   const int TW = 1 << a.twl, TH = BM / TW;
   a.tiles_w = pmu_cdiv(in->W, TW);
   a.tiles_h = pmu_cdiv(in->H, TH);
   dim3 grid((unsigned)(a.tiles_w * a.tiles_h * in->N), (unsigned)pmu_cdiv(NOUT, BN));
-  const int v = conv_variant();
-  const bool spec = (v & 1) != 0, pin = (v & 2) != 0;
-  const dim3 blk(spec ? 512 : 256);
-  hipStream_t st = (hipStream_t)stream;
-#define PMU_LAUNCH(D, S, P) hipLaunchKernelGGL((conv3x3_kernel<D, S, P>), grid, blk, 0, st, a)
-  if (dgrad) {
-    if (spec) { if (pin) PMU_LAUNCH(true, true, true); else PMU_LAUNCH(true, true, false); }
-    else { if (pin) PMU_LAUNCH(true, false, true); else PMU_LAUNCH(true, false, false); }
-  } else {
-    if (spec) { if (pin) PMU_LAUNCH(false, true, true); else PMU_LAUNCH(false, true, false); }
-    else { if (pin) PMU_LAUNCH(false, false, true); else PMU_LAUNCH(false, false, false); }
-  }
-#undef PMU_LAUNCH
+  if (dgrad)
+    hipLaunchKernelGGL(conv3x3_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(conv3x3_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

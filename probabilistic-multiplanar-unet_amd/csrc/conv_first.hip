@@ -1,0 +1,190 @@
+// First layer of the U-Net / prior / posterior (Cin <= 4 input planes): conv3x3 forward with BN
+// partial sums, and its weight gradient, on the VALU (K = 9*Cin is too short for MFMA tiles).
+// Reference: the first DoubleConv conv of PMU/model/unet/unet_parts.py:15 and Encoder conv of
+// PMU/model/probabilistic_unet/probabilistic_unet.py:38 (posterior input = cat(image, mask), :88).
+#include "pmu_common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------
+// First layer: Cin <= 4 input planes (NCHW-style, one pointer per channel), VALU.
+// ---------------------------------------------------------------------------------
+constexpr int FPIX = 256;  // pixels per block
+
+struct FirstArgs {
+  const float* planes[4];
+  int Cin, N, H, W, Cout;
+  const float* w;
+  const float* bias;
+  float* z;
+  float* part;
+};
+
+// thread = (channel quad cq, pixel lane pl); 256 / (Cout/4) pixel lanes per block step
+__global__ __launch_bounds__(256) void conv_first_fwd_kernel(FirstArgs a) {
+  __shared__ float wl[4 * 9 * 256];  // [ci*9+tap][co], Cout <= 256
+  __shared__ float red[256 * 8];
+  const int tid = threadIdx.x;
+  const int CQ = a.Cout >> 2;
+  const int npl = 256 / CQ;
+  const int cq = tid % CQ, pl = tid / CQ;
+  const int K9 = a.Cin * 9;
+  for (int i = tid; i < K9 * a.Cout; i += 256) {
+    const int co = i % a.Cout, k = i / a.Cout;
+    wl[k * a.Cout + co] = a.w[co * K9 + k];  // w[co][ci][kh][kw] -> k = ci*9+tap
+  }
+  __syncthreads();
+  const long long P = (long long)a.N * a.H * a.W;
+  const long long p0 = (long long)blockIdx.x * FPIX;
+  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.bias) bias = *reinterpret_cast<const float4*>(a.bias + 4 * cq);
+  float s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  if (pl < npl) {
+    for (int i = pl; i < FPIX; i += npl) {
+      const long long p = p0 + i;
+      if (p >= P) break;
+      const int w = (int)(p % a.W);
+      const int h = (int)((p / a.W) % a.H);
+      const int n = (int)(p / ((long long)a.W * a.H));
+      float o[4] = {bias.x, bias.y, bias.z, bias.w};
+      for (int ci = 0; ci < a.Cin; ++ci) {
+        const float* pl_ = a.planes[ci] + (long long)n * a.H * a.W;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+          const float x = (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) ? pl_[hh * a.W + ww] : 0.f;
+          const float4 wv = *reinterpret_cast<const float4*>(wl + (ci * 9 + tap) * a.Cout + 4 * cq);
+          o[0] = fmaf(x, wv.x, o[0]); o[1] = fmaf(x, wv.y, o[1]);
+          o[2] = fmaf(x, wv.z, o[2]); o[3] = fmaf(x, wv.w, o[3]);
+        }
+      }
+      *reinterpret_cast<float4*>(a.z + p * a.Cout + 4 * cq) = make_float4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { s1[e] += o[e]; s2[e] = fmaf(o[e], o[e], s2[e]); }
+    }
+  }
+  if (!a.part) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { red[tid * 8 + e] = s1[e]; red[tid * 8 + 4 + e] = s2[e]; }
+  __syncthreads();
+  if (tid < CQ) {
+    float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
+    for (int l = 0; l < npl; ++l) {
+      const int src = l * CQ + tid;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { t1[e] += red[src * 8 + e]; t2[e] += red[src * 8 + 4 + e]; }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a.part[((long long)blockIdx.x * 2 + 0) * a.Cout + 4 * tid + e] = t1[e];
+      a.part[((long long)blockIdx.x * 2 + 1) * a.Cout + 4 * tid + e] = t2[e];
+    }
+  }
+}
+
+struct FirstWgArgs {
+  DevFrame dz;
+  const float* planes[4];
+  int Cin, Cout;
+  float* ws;  // [blocks][Cout][Cin*9]
+};
+
+constexpr int FWPIX = 1024;  // pixels per block
+
+// thread = (co, pixel group); accumulates Cin*9 products over its pixels
+__global__ __launch_bounds__(256) void conv_first_wgrad_kernel(FirstWgArgs a) {
+  __shared__ float red[256 * 36];
+  const int tid = threadIdx.x;
+  const int npg = 256 / a.Cout;
+  const int co = tid % a.Cout, pg = tid / a.Cout;
+  const DevFrame& D = a.dz;
+  const int H = D.H, W = D.W;
+  const long long P = (long long)D.N * H * W;
+  const long long p0 = (long long)blockIdx.x * FWPIX;
+  const int K9 = a.Cin * 9;
+  float acc[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) acc[k] = 0.f;
+  for (int i = pg; i < FWPIX; i += npg) {
+    const long long p = p0 + i;
+    if (p >= P) break;
+    const int w = (int)(p % W);
+    const int h = (int)((p / W) % H);
+    const int n = (int)(p / ((long long)W * H));
+    const float g = frame_value(D, n, h, w, co);
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+      if (ci >= a.Cin) break;
+      const float* pl_ = a.planes[ci] + (long long)n * H * W;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+        const float x = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? pl_[hh * W + ww] : 0.f;
+        acc[ci * 9 + tap] = fmaf(g, x, acc[ci * 9 + tap]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 36; ++k) red[tid * 36 + k] = acc[k];
+  __syncthreads();
+  for (int o = tid; o < a.Cout * K9; o += 256) {
+    const int c = o / K9, k = o - c * K9;
+    float s = 0.f;
+    for (int l = 0; l < npg; ++l) s += red[(l * a.Cout + c) * 36 + k];
+    a.ws[(long long)blockIdx.x * a.Cout * K9 + o] = s;
+  }
+}
+
+// dw[o] = sum_b ws[b][o]
+__global__ void rows_sum_kernel(const float* __restrict__ ws, int R, int Wd, float* __restrict__ out) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= Wd) return;
+  double s = 0.0;
+  for (int r = 0; r < R; ++r) s += ws[(long long)r * Wd + o];
+  out[o] = (float)s;
+}
+
+}  // namespace
+
+extern "C" int pmu_conv_first_tiles(int N, int H, int W) {
+  return pmu_cdiv((long long)N * H * W, FPIX);
+}
+
+extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,
+                                  const float* w, const float* bias, int Cout, float* z, float* part,
+                                  void* stream) {
+  PMU_REQUIRE(planes && Cin >= 1 && Cin <= 4 && N > 0 && H > 0 && W > 0 && w && z);
+  PMU_REQUIRE(Cout >= 4 && Cout <= 256 && Cout % 4 == 0 && 256 % (Cout / 4) == 0);
+  FirstArgs a;
+  for (int i = 0; i < 4; ++i) a.planes[i] = i < Cin ? planes[i] : nullptr;
+  for (int i = 0; i < Cin; ++i) PMU_REQUIRE(planes[i]);
+  a.Cin = Cin; a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.w = w; a.bias = bias; a.z = z; a.part = part;
+  hipLaunchKernelGGL(conv_first_fwd_kernel, dim3((unsigned)pmu_conv_first_tiles(N, H, W)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" size_t pmu_conv_first_wgrad_ws(int N, int H, int W, int Cin, int Cout) {
+  return (size_t)pmu_cdiv((long long)N * H * W, FWPIX) * Cout * Cin * 9 * sizeof(float);
+}
+
+extern "C" int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* planes, int Cin, int Cout,
+                                    float* dw, float* ws, size_t ws_bytes, void* stream) {
+  PMU_REQUIRE(valid_frame(dz) && dz->nsrc == 1 && dz->src[0].C == Cout && planes && dw && ws);
+  PMU_REQUIRE(Cin >= 1 && Cin <= 4 && Cout >= 1 && Cout <= 256 && 256 % Cout == 0);
+  const int nb = pmu_cdiv((long long)dz->N * dz->H * dz->W, FWPIX);
+  PMU_REQUIRE(ws_bytes >= (size_t)nb * Cout * Cin * 9 * sizeof(float));
+  FirstWgArgs a;
+  a.dz = make_dev_frame(dz);
+  for (int i = 0; i < 4; ++i) a.planes[i] = i < Cin ? planes[i] : nullptr;
+  for (int i = 0; i < Cin; ++i) PMU_REQUIRE(planes[i]);
+  a.Cin = Cin; a.Cout = Cout; a.ws = ws;
+  hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, a);
+  PMU_CHECK_LAUNCH();
+  const int Wd = Cout * Cin * 9;
+  hipLaunchKernelGGL(rows_sum_kernel, dim3((unsigned)pmu_cdiv(Wd, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)ws, nb, Wd, dw);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}

@@ -1,0 +1,103 @@
+// Branch-free operand staging shared by the conv kernels.
+//
+// A thread stages NI items of one frame into LDS: item i is the float4 of channels
+// c..c+3 at frame pixel (ih[i], iw[i]) of image n, written to lds + dst[i].  All items of a
+// thread use the same 4 channels, so the per-channel BN coefficients are loaded once; item
+// addresses are clamped and masked so every load is issued before the first wait (the
+// generic frame_value4 path branches per item and serialises one memory round trip per item).
+#pragma once
+#include "pmu_common.h"
+
+constexpr int PMU_NO_ITEM = -0x4000;  // ih[i] marker: thread has no item i
+
+__device__ __forceinline__ float4 pmu_bnrelu4(float4 x, float4 sc, float4 sh) {
+  return make_float4(fmaxf(0.f, fmaf(x.x, sc.x, sh.x)), fmaxf(0.f, fmaf(x.y, sc.y, sh.y)),
+                     fmaxf(0.f, fmaf(x.z, sc.z, sh.z)), fmaxf(0.f, fmaf(x.w, sc.w, sh.w)));
+}
+__device__ __forceinline__ float pmu_bnbwd1(float d, float z, float sc, float sh, float mu, float kx, float kc) {
+  return fmaf(sc, fmaf(z, sc, sh) > 0.f ? d : 0.f, fmaf(kx, z - mu, kc));
+}
+__device__ __forceinline__ float4 pmu_max4(float4 a, float4 b) {
+  return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
+}
+
+template <int MODE, int POOL, int NI>
+__device__ __forceinline__ void stage_items_fast(const DevSrc& s, int c, int n, const int (&ih)[NI],
+                                                 const int (&iw)[NI], const int (&dst)[NI], float* lds) {
+  float4 sc = make_float4(0, 0, 0, 0), sh = sc, mu = sc, kx = sc, kc = sc;
+  if (MODE != PMU_SRC_RAW) {
+    sc = *reinterpret_cast<const float4*>(s.coef + c);
+    sh = *reinterpret_cast<const float4*>(s.coef + s.C + c);
+  }
+  if (MODE == PMU_SRC_BNBWD) {
+    mu = *reinterpret_cast<const float4*>(s.coef + 2 * s.C + c);
+    kx = *reinterpret_cast<const float4*>(s.coef + 3 * s.C + c);
+    kc = *reinterpret_cast<const float4*>(s.coef + 4 * s.C + c);
+  }
+  constexpr int NL = (POOL == PMU_POOL_MAX2) ? 4 : 1;
+  float4 xv[NI][NL];
+  float4 zv[NI];
+  bool ok[NI];
+  const long long rs = (long long)s.W * s.C;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    int hs = ih[i] - s.off_h, ws = iw[i] - s.off_w;
+    if (POOL == PMU_POOL_MAX2) { hs *= 2; ws *= 2; }
+    const int lim_h = (POOL == PMU_POOL_MAX2) ? s.H - 1 : s.H;
+    const int lim_w = (POOL == PMU_POOL_MAX2) ? s.W - 1 : s.W;
+    ok[i] = (ih[i] != PMU_NO_ITEM) && hs >= 0 && ws >= 0 && hs < lim_h && ws < lim_w;
+    const long long idx = ok[i] ? (((long long)n * s.H + hs) * s.W + ws) * s.C + c : (long long)c;
+    xv[i][0] = *reinterpret_cast<const float4*>(s.x + idx);
+    if (POOL == PMU_POOL_MAX2) {
+      xv[i][1] = *reinterpret_cast<const float4*>(s.x + idx + s.C);
+      xv[i][2] = *reinterpret_cast<const float4*>(s.x + idx + rs);
+      xv[i][3] = *reinterpret_cast<const float4*>(s.x + idx + rs + s.C);
+    }
+    if (MODE == PMU_SRC_BNBWD) zv[i] = *reinterpret_cast<const float4*>(s.z + idx);
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    if (ih[i] == PMU_NO_ITEM) continue;
+    float4 v;
+    if (MODE == PMU_SRC_RAW) {
+      v = xv[i][0];
+    } else if (MODE == PMU_SRC_BNRELU) {
+      v = pmu_bnrelu4(xv[i][0], sc, sh);
+      if (POOL == PMU_POOL_MAX2) {
+        v = pmu_max4(v, pmu_bnrelu4(xv[i][1], sc, sh));
+        v = pmu_max4(v, pmu_bnrelu4(xv[i][2], sc, sh));
+        v = pmu_max4(v, pmu_bnrelu4(xv[i][3], sc, sh));
+      }
+    } else {
+      const float4 d = xv[i][0], z = zv[i];
+      v = make_float4(pmu_bnbwd1(d.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x), pmu_bnbwd1(d.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y),
+                      pmu_bnbwd1(d.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z), pmu_bnbwd1(d.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w));
+    }
+    if (!ok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(lds + dst[i]) = v;
+  }
+}
+
+// Stage NI items of frame channels [cbase, cbase + span) — this thread's quad is cbase + 4*cq.
+// Fast when the span lies inside one source (C % 4 == 0, no avg pool); generic otherwise.
+template <int NI>
+__device__ __forceinline__ void stage_items(const DevFrame& F, int n, int cbase, int span, int cq,
+                                            const int (&ih)[NI], const int (&iw)[NI], const int (&dst)[NI],
+                                            float* lds) {
+  const bool in0 = cbase + span <= F.C0;
+  const bool in1 = F.nsrc > 1 && cbase >= F.C0 && cbase + span <= F.C;
+  if (F.vec && (in0 || in1)) {
+    const DevSrc& s = in0 ? F.s0 : F.s1;
+    const int c = (in0 ? cbase : cbase - F.C0) + 4 * cq;
+    if (s.pool == PMU_POOL_NONE) {
+      if (s.mode == PMU_SRC_BNRELU) return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_NONE, NI>(s, c, n, ih, iw, dst, lds);
+      if (s.mode == PMU_SRC_BNBWD) return stage_items_fast<PMU_SRC_BNBWD, PMU_POOL_NONE, NI>(s, c, n, ih, iw, dst, lds);
+      return stage_items_fast<PMU_SRC_RAW, PMU_POOL_NONE, NI>(s, c, n, ih, iw, dst, lds);
+    }
+    if (s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU)
+      return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_MAX2, NI>(s, c, n, ih, iw, dst, lds);
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    if (ih[i] != PMU_NO_ITEM) *reinterpret_cast<float4*>(lds + dst[i]) = frame_value4(F, n, ih[i], iw[i], cbase + 4 * cq);
+}

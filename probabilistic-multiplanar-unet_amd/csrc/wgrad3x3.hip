@@ -1,23 +1,30 @@
-// Weight gradient of the 3x3 / pad 1 convolution (autograd of unet_parts.py:15,18 and
-// probabilistic_unet.py:38,43 w.r.t. weight) on f32 MFMA, plus the Cin <= 4 first layer.
+// Weight gradient of the 3x3 / pad 1 convolution on f32 MFMA (autograd of nn.Conv2d w.r.t. its
+// weight at PMU/model/unet/unet_parts.py:15,18 and PMU/model/probabilistic_unet/probabilistic_unet.py:38,43).
 //
-//   dw[co][ci][tap] = sum_{n,h,w} dz[n,h,w,co] * act[n, h+dy-1, w+dx-1, ci]
+//   dw[co][ci][kh][kw] = sum_{n,h,w} dz[n,h,w,co] * act[n, h+kh-1, w+kw-1, ci]
 //
-// GEMM view: M = Cout (64 per block), N = Cin (64 per block), 9 taps, K = pixels.
-// K is split across blocks (split-K over TH x TW pixel tiles); every block writes its own
-// fp32 slab ws[split][tap][co][ci] and pmu_wgrad_reduce sums slabs in a fixed order, so the
-// result is bitwise reproducible (no float atomics).
-// Per pixel tile the block stages dz[64 px][64 co] and the (TH+2)x(TW+2) activation halo
-// [px][64 ci] in LDS; wave w owns (co frag w>>1, ci frag w&1) x 9 taps = 9 accumulators and
-// reuses one A fragment (dz) across the 9 taps.
-#include "pmu_common.h"
+// GEMM view: M = Cout (64 per block), N = Cin (64 per block), 9 taps, K = pixels, split over
+// blocks (split-K); each block writes an fp32 slab ws[split][tap][co][ci] and wgrad_reduce sums
+// the slabs in a fixed order (bitwise reproducible, no float atomics).
+//
+// Block: 12 waves = 4 (co frag, ci frag) pairs x 3 kernel rows (kh); each wave keeps only the 3
+// accumulators of its row (48 VGPRs), so the block can keep a whole tile of global loads in flight.
+// Per K tile (64 output pixels, TH x TW) the block stages dz[64 px][64 co] (BN+ReLU backward applied
+// on the fly) and the (TH+2) x (TW+2) halo of the BN+ReLU(+max-pool)(+concat) activation into a
+// double-buffered LDS ring: the next tile's global loads are issued before the current tile's MFMAs
+// and transformed/stored after them (1 block per CU, 88 KB LDS).
+#include "pmu_stage.h"
 
 namespace {
 
-constexpr int WB = 64;          // co and ci per block
-constexpr int WPIX = 64;        // pixels per K tile
-constexpr int MAX_HPX = 108;    // (4+2)*(16+2) = 108, (8+2)*(8+2) = 100
-constexpr int WLS = 64;         // LDS row stride (b32 reads, lanes consecutive)
+constexpr int WB = 64;        // co and ci per block
+constexpr int WPIX = 64;      // pixels per K tile
+constexpr int MAX_HPX = 108;  // (4+2)*(16+2) = 108, (8+2)*(8+2) = 100
+constexpr int WLS = 64;       // LDS row stride (b32 reads, lanes consecutive)
+constexpr int SLOT = WPIX * WLS + MAX_HPX * WLS;
+constexpr int NT = 768;       // threads per block
+constexpr int ND = 2;         // dz items per thread: ceil(64*16 / 768)
+constexpr int NX = 3;         // halo items per thread: ceil(108*16 / 768)
 
 struct WgArgs {
   DevFrame dz, act;
@@ -26,60 +33,205 @@ struct WgArgs {
   int twl, tiles_w, tiles_h, ntiles, nsplit;
 };
 
-__global__ __launch_bounds__(256, 2) void wgrad3x3_kernel(WgArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[WPIX * WLS + MAX_HPX * WLS];
-  float* Ds = smem;
-  float* Xs = smem + WPIX * WLS;
+// in-flight raw loads of one tile for this thread
+struct TileRegs {
+  float4 d[ND], dz[ND];
+  float4 x[NX][4];
+  bool dok[ND], xok[NX];
+};
+
+// fast-path descriptor: the block's 64 dz channels and 64 act channels each lie in one source
+struct FastOps {
+  DevSrc ds, xs;
+  int dc, xc;  // this thread's channel quad inside each source
+};
+
+__device__ __forceinline__ void tile_load(const FastOps& f, int n, int h0, int w0, int twl, int HW2, int HP, int tid,
+                                          TileRegs& r) {
+  const int TW = 1 << twl;
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const int it = tid + NT * i;
+    const int px = it >> 4;
+    const int h = h0 + (px >> twl), w = w0 + (px & (TW - 1));
+    r.dok[i] = it < WPIX * 16 && h < f.ds.H && w < f.ds.W;
+    const long long idx = r.dok[i] ? (((long long)n * f.ds.H + h) * f.ds.W + w) * f.ds.C + f.dc : (long long)f.dc;
+    r.d[i] = *reinterpret_cast<const float4*>(f.ds.x + idx);
+    r.dz[i] = *reinterpret_cast<const float4*>(f.ds.z + idx);
+  }
+  const DevSrc& s = f.xs;
+  const bool mp = s.pool == PMU_POOL_MAX2;
+  const long long rs = (long long)s.W * s.C;
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int it = tid + NT * i;
+    const int hp = it >> 4;
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    int hs = h0 - 1 + hr - s.off_h, ws = w0 - 1 + hc - s.off_w;
+    if (mp) { hs *= 2; ws *= 2; }
+    const int lh = mp ? s.H - 1 : s.H, lw = mp ? s.W - 1 : s.W;
+    r.xok[i] = it < HP * 16 && hs >= 0 && ws >= 0 && hs < lh && ws < lw;
+    const long long idx = r.xok[i] ? (((long long)n * s.H + hs) * s.W + ws) * s.C + f.xc : (long long)f.xc;
+    r.x[i][0] = *reinterpret_cast<const float4*>(s.x + idx);
+    if (mp) {
+      r.x[i][1] = *reinterpret_cast<const float4*>(s.x + idx + s.C);
+      r.x[i][2] = *reinterpret_cast<const float4*>(s.x + idx + rs);
+      r.x[i][3] = *reinterpret_cast<const float4*>(s.x + idx + rs + s.C);
+    }
+  }
+}
+
+__device__ __forceinline__ void tile_store(const FastOps& f, const TileRegs& r, int HP, int tid, float* slot) {
+  float* Ds = slot;
+  float* Xs = slot + WPIX * WLS;
+  const int cq = tid & 15;
+  // coefficients re-read per tile (L1/L2 hits) rather than held in 28 VGPRs across the MFMA loop
+  const float* dco = f.ds.coef + f.dc;
+  const int dC = f.ds.C;
+  const float4 dsc = *reinterpret_cast<const float4*>(dco), dsh = *reinterpret_cast<const float4*>(dco + dC);
+  const float4 dmu = *reinterpret_cast<const float4*>(dco + 2 * dC), dkx = *reinterpret_cast<const float4*>(dco + 3 * dC);
+  const float4 dkc = *reinterpret_cast<const float4*>(dco + 4 * dC);
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const int it = tid + NT * i;
+    if (it >= WPIX * 16) continue;
+    const float4 d = r.d[i], z = r.dz[i];
+    float4 v = make_float4(pmu_bnbwd1(d.x, z.x, dsc.x, dsh.x, dmu.x, dkx.x, dkc.x),
+                           pmu_bnbwd1(d.y, z.y, dsc.y, dsh.y, dmu.y, dkx.y, dkc.y),
+                           pmu_bnbwd1(d.z, z.z, dsc.z, dsh.z, dmu.z, dkx.z, dkc.z),
+                           pmu_bnbwd1(d.w, z.w, dsc.w, dsh.w, dmu.w, dkx.w, dkc.w));
+    if (!r.dok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(Ds + (it >> 4) * WLS + 4 * cq) = v;
+  }
+  const bool mp = f.xs.pool == PMU_POOL_MAX2;
+  const bool raw = f.xs.mode == PMU_SRC_RAW;
+  float4 xsc = make_float4(0.f, 0.f, 0.f, 0.f), xsh = xsc;
+  if (!raw) {
+    xsc = *reinterpret_cast<const float4*>(f.xs.coef + f.xc);
+    xsh = *reinterpret_cast<const float4*>(f.xs.coef + f.xs.C + f.xc);
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int it = tid + NT * i;
+    if (it >= HP * 16) continue;
+    float4 v;
+    if (raw) {
+      v = r.x[i][0];
+    } else {
+      v = pmu_bnrelu4(r.x[i][0], xsc, xsh);
+      if (mp) {
+        v = pmu_max4(v, pmu_bnrelu4(r.x[i][1], xsc, xsh));
+        v = pmu_max4(v, pmu_bnrelu4(r.x[i][2], xsc, xsh));
+        v = pmu_max4(v, pmu_bnrelu4(r.x[i][3], xsc, xsh));
+      }
+    }
+    if (!r.xok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(Xs + (it >> 4) * WLS + 4 * cq) = v;
+  }
+}
+
+// generic synchronous staging (mixed-source blocks, avg pool, channel counts not multiple of 4)
+__device__ __forceinline__ void tile_stage_generic(const DevFrame& D, const DevFrame& X, int n, int h0, int w0, int twl, int HW2,
+                                   int HP, int co0, int ci0, int tid, float* slot) {
+  float* Ds = slot;
+  float* Xs = slot + WPIX * WLS;
+  const int TW = 1 << twl;
+  for (int it = tid; it < WPIX * 16; it += NT) {
+    const int px = it >> 4, cq = it & 15;
+    *reinterpret_cast<float4*>(Ds + px * WLS + 4 * cq) =
+        frame_value4(D, n, h0 + (px >> twl), w0 + (px & (TW - 1)), co0 + 4 * cq);
+  }
+  for (int it = tid; it < HP * 16; it += NT) {
+    const int hp = it >> 4, cq = it & 15;
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    *reinterpret_cast<float4*>(Xs + hp * WLS + 4 * cq) = frame_value4(X, n, h0 - 1 + hr, w0 - 1 + hc, ci0 + 4 * cq);
+  }
+}
+
+// FAST: every block's 64 dz channels / 64 act channels lie in one source each (host-checked);
+// the generic instantiation stages synchronously through frame_value4.
+template <bool FAST>
+__global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int TW = 1 << a.twl, TH = WPIX >> a.twl, HW2 = TW + 2, HP = (TH + 2) * HW2;
   const int nco = pmu_cdiv_dev(a.Cout, WB);
-  const int bid = blockIdx.x;
+  const int co0 = (blockIdx.x % nco) * WB, ci0 = (blockIdx.x / nco) * WB;
   const int split = blockIdx.y;
-  const int co0 = (bid % nco) * WB, ci0 = (bid / nco) * WB;
-  const int cof = wave >> 1, cif = wave & 1;
+  const int pair = wave & 3, kh = wave >> 2;
+  const int cof = pair >> 1, cif = pair & 1;
+  const DevFrame& D = a.dz;
+  const DevFrame& X = a.act;
 
-  f32x16 acc[9];
+  // fast path if both 64-channel blocks sit inside one source each
+  const bool d_fast = D.vec && D.nsrc == 1 && D.s0.mode == PMU_SRC_BNBWD && D.s0.pool == PMU_POOL_NONE &&
+                      co0 + WB <= D.C0;
+  const bool x_in0 = ci0 + WB <= X.C0, x_in1 = X.nsrc > 1 && ci0 >= X.C0 && ci0 + WB <= X.C;
+  const DevSrc& xsrc = x_in0 ? X.s0 : X.s1;
+  const bool x_fast = X.vec && (x_in0 || x_in1) && xsrc.mode != PMU_SRC_BNBWD &&
+                      (xsrc.pool == PMU_POOL_NONE || (xsrc.pool == PMU_POOL_MAX2 && xsrc.mode == PMU_SRC_BNRELU));
+  const bool fast = FAST && d_fast && x_fast;
+  (void)fast;
+  FastOps f;
+  if constexpr (FAST) {
+    const int cq = tid & 15;
+    f.ds = D.s0;
+    f.dc = co0 + 4 * cq;
+    f.xs = xsrc;
+    f.xc = (x_in0 ? ci0 : ci0 - X.C0) + 4 * cq;
+  }
+
+  f32x16 acc[3];
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int t = 0; t < 3; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
   const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
   const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);
-  const DevFrame& D = a.dz;
-  const DevFrame& X = a.act;
-
-  for (int tile = t_beg; tile < t_end; ++tile) {
+  auto origin = [&](int tile, int& n, int& h0, int& w0) {
     int t = tile;
     const int tw = t % a.tiles_w; t /= a.tiles_w;
     const int th = t % a.tiles_h; t /= a.tiles_h;
-    const int n = t;
-    const int h0 = th * TH, w0 = tw * TW;
-    // dz tile: WPIX pixels x 64 co
-    for (int it = tid; it < WPIX * 16; it += 256) {
-      const int px = it >> 4, cq = it & 15;
-      const float4 v = frame_value4(D, n, h0 + (px >> a.twl), w0 + (px & (TW - 1)), co0 + 4 * cq);
-      *reinterpret_cast<float4*>(Ds + px * WLS + 4 * cq) = v;
+    n = t; h0 = th * TH; w0 = tw * TW;
+  };
+
+  TileRegs regs;
+  {
+    int n, h0, w0;
+    origin(t_beg, n, h0, w0);
+    if constexpr (FAST) {
+      tile_load(f, n, h0, w0, a.twl, HW2, HP, tid, regs);
+      tile_store(f, regs, HP, tid, smem);
+    } else {
+      tile_stage_generic(D, X, n, h0, w0, a.twl, HW2, HP, co0, ci0, tid, smem);
     }
-    // activation halo: HP pixels x 64 ci
-    for (int it = tid; it < HP * 16; it += 256) {
-      const int hp = it >> 4, cq = it & 15;
-      const int hr = hp / HW2, hc = hp - hr * HW2;
-      const float4 v = frame_value4(X, n, h0 - 1 + hr, w0 - 1 + hc, ci0 + 4 * cq);
-      *reinterpret_cast<float4*>(Xs + hp * WLS + 4 * cq) = v;
+  }
+  __syncthreads();
+
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    const int cur = (tile - t_beg) & 1;
+    const bool more = tile + 1 < t_end;
+    int nn = 0, nh0 = 0, nw0 = 0;
+    if (more) {
+      origin(tile + 1, nn, nh0, nw0);
+      if constexpr (FAST) tile_load(f, nn, nh0, nw0, a.twl, HW2, HP, tid, regs);  // in flight during the MFMAs
     }
-    __syncthreads();
-#pragma unroll 2
+    const float* Ds = smem + cur * SLOT;
+    const float* Xs = Ds + WPIX * WLS;
+#pragma unroll 4
     for (int ks = 0; ks < WPIX / 2; ++ks) {
       const int px = 2 * ks + (lane >> 5);
       const int r = px >> a.twl, c = px & (TW - 1);
       const float av = Ds[px * WLS + cof * 32 + (lane & 31)];
-      const float* xb = Xs + (r * HW2 + c) * WLS + cif * 32 + (lane & 31);
+      const float* xb = Xs + ((r + kh) * HW2 + c) * WLS + cif * 32 + (lane & 31);
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const float bv = xb[((tap / 3) * HW2 + (tap % 3)) * WLS];
-        acc[tap] = mfma_f32_32x32x2(av, bv, acc[tap]);
-      }
+      for (int kw = 0; kw < 3; ++kw) acc[kw] = mfma_f32_32x32x2(av, xb[kw * WLS], acc[kw]);
+    }
+    if (more) {
+      float* nxt = smem + (cur ^ 1) * SLOT;
+      if constexpr (FAST) tile_store(f, regs, HP, tid, nxt);
+      else tile_stage_generic(D, X, nn, nh0, nw0, a.twl, HW2, HP, co0, ci0, tid, nxt);
     }
     __syncthreads();
   }
@@ -88,12 +240,12 @@ __global__ __launch_bounds__(256, 2) void wgrad3x3_kernel(WgArgs a) {
   const int ci = ci0 + cif * 32 + (lane & 31);
   if (ci < a.Cin) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
+    for (int kw = 0; kw < 3; ++kw) {
+      const int tap = kh * 3 + kw;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int co = co0 + cof * 32 + acc_row(r, lane);
-        if (co < a.Cout)
-          a.ws[(((long long)split * 9 + tap) * a.Cout + co) * a.Cin + ci] = acc[tap][r];
+        if (co < a.Cout) a.ws[(((long long)split * 9 + tap) * a.Cout + co) * a.Cin + ci] = acc[kw][r];
       }
     }
   }
@@ -113,156 +265,18 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, in
   dw[cc * 9 + tap] = s;
 }
 
-static void wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* twl, int* tiles_w,
-                           int* tiles_h, int* ntiles, int* nsplit) {
+static void wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* twl, int* tiles_w, int* tiles_h,
+                           int* ntiles, int* nsplit) {
   *twl = (W > 8) ? 4 : 3;
   const int TW = 1 << *twl, TH = WPIX / TW;
   *tiles_w = pmu_cdiv(W, TW);
   *tiles_h = pmu_cdiv(H, TH);
   *ntiles = N * *tiles_w * *tiles_h;
   const int blocks_mn = pmu_cdiv(Cout, WB) * pmu_cdiv(Cin, WB);
-  int s = 1024 / blocks_mn;
+  int s = 512 / blocks_mn;  // ~2 blocks per CU over the launch
   if (s < 1) s = 1;
   if (s > *ntiles) s = *ntiles;
   *nsplit = s;
-}
-
-// ---------------------------------------------------------------------------------
-// First layer: Cin <= 4 input planes (NCHW-style, one pointer per channel), VALU.
-// ---------------------------------------------------------------------------------
-constexpr int FPIX = 256;  // pixels per block
-
-struct FirstArgs {
-  const float* planes[4];
-  int Cin, N, H, W, Cout;
-  const float* w;
-  const float* bias;
-  float* z;
-  float* part;
-};
-
-// thread = (channel quad cq, pixel lane pl); 256 / (Cout/4) pixel lanes per block step
-__global__ __launch_bounds__(256) void conv_first_fwd_kernel(FirstArgs a) {
-  __shared__ float wl[4 * 9 * 256];  // [ci*9+tap][co], Cout <= 256
-  __shared__ float red[256 * 8];
-  const int tid = threadIdx.x;
-  const int CQ = a.Cout >> 2;
-  const int npl = 256 / CQ;
-  const int cq = tid % CQ, pl = tid / CQ;
-  const int K9 = a.Cin * 9;
-  for (int i = tid; i < K9 * a.Cout; i += 256) {
-    const int co = i % a.Cout, k = i / a.Cout;
-    wl[k * a.Cout + co] = a.w[co * K9 + k];  // w[co][ci][kh][kw] -> k = ci*9+tap
-  }
-  __syncthreads();
-  const long long P = (long long)a.N * a.H * a.W;
-  const long long p0 = (long long)blockIdx.x * FPIX;
-  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.bias) bias = *reinterpret_cast<const float4*>(a.bias + 4 * cq);
-  float s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
-  if (pl < npl) {
-    for (int i = pl; i < FPIX; i += npl) {
-      const long long p = p0 + i;
-      if (p >= P) break;
-      const int w = (int)(p % a.W);
-      const int h = (int)((p / a.W) % a.H);
-      const int n = (int)(p / ((long long)a.W * a.H));
-      float o[4] = {bias.x, bias.y, bias.z, bias.w};
-      for (int ci = 0; ci < a.Cin; ++ci) {
-        const float* pl_ = a.planes[ci] + (long long)n * a.H * a.W;
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
-          const float x = (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) ? pl_[hh * a.W + ww] : 0.f;
-          const float4 wv = *reinterpret_cast<const float4*>(wl + (ci * 9 + tap) * a.Cout + 4 * cq);
-          o[0] = fmaf(x, wv.x, o[0]); o[1] = fmaf(x, wv.y, o[1]);
-          o[2] = fmaf(x, wv.z, o[2]); o[3] = fmaf(x, wv.w, o[3]);
-        }
-      }
-      *reinterpret_cast<float4*>(a.z + p * a.Cout + 4 * cq) = make_float4(o[0], o[1], o[2], o[3]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { s1[e] += o[e]; s2[e] = fmaf(o[e], o[e], s2[e]); }
-    }
-  }
-  if (!a.part) return;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) { red[tid * 8 + e] = s1[e]; red[tid * 8 + 4 + e] = s2[e]; }
-  __syncthreads();
-  if (tid < CQ) {
-    float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
-    for (int l = 0; l < npl; ++l) {
-      const int src = l * CQ + tid;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { t1[e] += red[src * 8 + e]; t2[e] += red[src * 8 + 4 + e]; }
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      a.part[((long long)blockIdx.x * 2 + 0) * a.Cout + 4 * tid + e] = t1[e];
-      a.part[((long long)blockIdx.x * 2 + 1) * a.Cout + 4 * tid + e] = t2[e];
-    }
-  }
-}
-
-struct FirstWgArgs {
-  DevFrame dz;
-  const float* planes[4];
-  int Cin, Cout;
-  float* ws;  // [blocks][Cout][Cin*9]
-};
-
-constexpr int FWPIX = 1024;  // pixels per block
-
-// thread = (co, pixel group); accumulates Cin*9 products over its pixels
-__global__ __launch_bounds__(256) void conv_first_wgrad_kernel(FirstWgArgs a) {
-  __shared__ float red[256 * 36];
-  const int tid = threadIdx.x;
-  const int npg = 256 / a.Cout;
-  const int co = tid % a.Cout, pg = tid / a.Cout;
-  const DevFrame& D = a.dz;
-  const int H = D.H, W = D.W;
-  const long long P = (long long)D.N * H * W;
-  const long long p0 = (long long)blockIdx.x * FWPIX;
-  const int K9 = a.Cin * 9;
-  float acc[36];
-#pragma unroll
-  for (int k = 0; k < 36; ++k) acc[k] = 0.f;
-  for (int i = pg; i < FWPIX; i += npg) {
-    const long long p = p0 + i;
-    if (p >= P) break;
-    const int w = (int)(p % W);
-    const int h = (int)((p / W) % H);
-    const int n = (int)(p / ((long long)W * H));
-    const float g = frame_value(D, n, h, w, co);
-#pragma unroll
-    for (int ci = 0; ci < 4; ++ci) {
-      if (ci >= a.Cin) break;
-      const float* pl_ = a.planes[ci] + (long long)n * H * W;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
-        const float x = (hh >= 0 && hh < H && ww >= 0 && ww < W) ? pl_[hh * W + ww] : 0.f;
-        acc[ci * 9 + tap] = fmaf(g, x, acc[ci * 9 + tap]);
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 36; ++k) red[tid * 36 + k] = acc[k];
-  __syncthreads();
-  for (int o = tid; o < a.Cout * K9; o += 256) {
-    const int c = o / K9, k = o - c * K9;
-    float s = 0.f;
-    for (int l = 0; l < npg; ++l) s += red[(l * a.Cout + c) * 36 + k];
-    a.ws[(long long)blockIdx.x * a.Cout * K9 + o] = s;
-  }
-}
-
-// dw[o] = sum_b ws[b][o]
-__global__ void rows_sum_kernel(const float* __restrict__ ws, int R, int Wd, float* __restrict__ out) {
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= Wd) return;
-  double s = 0.0;
-  for (int r = 0; r < R; ++r) s += ws[(long long)r * Wd + o];
-  out[o] = (float)s;
 }
 
 }  // namespace
@@ -273,8 +287,8 @@ extern "C" size_t pmu_conv3x3_wgrad_ws(int N, int H, int W, int Cin, int Cout) {
   return (size_t)ns * 9 * Cout * Cin * sizeof(float);
 }
 
-extern "C" int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int Cout, float* dw,
-                                 float* ws, size_t ws_bytes, void* stream) {
+extern "C" int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int Cout, float* dw, float* ws,
+                                 size_t ws_bytes, void* stream) {
   PMU_REQUIRE(valid_frame(dz) && valid_frame(act) && dw && ws);
   PMU_REQUIRE(dz->N == act->N && dz->H == act->H && dz->W == act->W);
   const int Cin = act->src[0].C + (act->nsrc > 1 ? act->src[1].C : 0);
@@ -286,54 +300,23 @@ extern "C" int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int 
   wgrad_geometry(dz->N, dz->H, dz->W, Cin, Cout, &a.twl, &a.tiles_w, &a.tiles_h, &a.ntiles, &a.nsplit);
   PMU_REQUIRE(ws_bytes >= (size_t)a.nsplit * 9 * Cout * Cin * sizeof(float));
   dim3 grid((unsigned)(pmu_cdiv(Cout, WB) * pmu_cdiv(Cin, WB)), (unsigned)a.nsplit);
-  hipLaunchKernelGGL(wgrad3x3_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  // fast kernel only if every (co block, ci block) lies inside one source of each frame
+  const pmu_src& d0 = dz->src[0];
+  bool fast = a.dz.vec && d0.mode == PMU_SRC_BNBWD && d0.pool == PMU_POOL_NONE && Cout % WB == 0;
+  fast = fast && a.act.vec && (a.act.C0 % WB == 0) && (Cin % WB == 0);
+  for (int i = 0; i < act->nsrc; ++i) {
+    const pmu_src& s = act->src[i];
+    fast = fast && s.mode != PMU_SRC_BNBWD &&
+           (s.pool == PMU_POOL_NONE || (s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU));
+  }
+  if (fast)
+    hipLaunchKernelGGL(wgrad3x3_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(wgrad3x3_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, a);
   PMU_CHECK_LAUNCH();
   const long long E = 9LL * Cout * Cin;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0,
-                     (hipStream_t)stream, (const float*)ws, a.nsplit, Cout, Cin, dw);
-  PMU_CHECK_LAUNCH();
-  return PMU_OK;
-}
-
-extern "C" int pmu_conv_first_tiles(int N, int H, int W) {
-  return pmu_cdiv((long long)N * H * W, FPIX);
-}
-
-extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,
-                                  const float* w, const float* bias, int Cout, float* z, float* part,
-                                  void* stream) {
-  PMU_REQUIRE(planes && Cin >= 1 && Cin <= 4 && N > 0 && H > 0 && W > 0 && w && z);
-  PMU_REQUIRE(Cout >= 4 && Cout <= 256 && Cout % 4 == 0 && 256 % (Cout / 4) == 0);
-  FirstArgs a;
-  for (int i = 0; i < 4; ++i) a.planes[i] = i < Cin ? planes[i] : nullptr;
-  for (int i = 0; i < Cin; ++i) PMU_REQUIRE(planes[i]);
-  a.Cin = Cin; a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.w = w; a.bias = bias; a.z = z; a.part = part;
-  hipLaunchKernelGGL(conv_first_fwd_kernel, dim3((unsigned)pmu_conv_first_tiles(N, H, W)), dim3(256), 0,
-                     (hipStream_t)stream, a);
-  PMU_CHECK_LAUNCH();
-  return PMU_OK;
-}
-
-extern "C" size_t pmu_conv_first_wgrad_ws(int N, int H, int W, int Cin, int Cout) {
-  return (size_t)pmu_cdiv((long long)N * H * W, FWPIX) * Cout * Cin * 9 * sizeof(float);
-}
-
-extern "C" int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* planes, int Cin, int Cout,
-                                    float* dw, float* ws, size_t ws_bytes, void* stream) {
-  PMU_REQUIRE(valid_frame(dz) && dz->nsrc == 1 && dz->src[0].C == Cout && planes && dw && ws);
-  PMU_REQUIRE(Cin >= 1 && Cin <= 4 && Cout >= 1 && Cout <= 256 && 256 % Cout == 0);
-  const int nb = pmu_cdiv((long long)dz->N * dz->H * dz->W, FWPIX);
-  PMU_REQUIRE(ws_bytes >= (size_t)nb * Cout * Cin * 9 * sizeof(float));
-  FirstWgArgs a;
-  a.dz = make_dev_frame(dz);
-  for (int i = 0; i < 4; ++i) a.planes[i] = i < Cin ? planes[i] : nullptr;
-  for (int i = 0; i < Cin; ++i) PMU_REQUIRE(planes[i]);
-  a.Cin = Cin; a.Cout = Cout; a.ws = ws;
-  hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, a);
-  PMU_CHECK_LAUNCH();
-  const int Wd = Cout * Cin * 9;
-  hipLaunchKernelGGL(rows_sum_kernel, dim3((unsigned)pmu_cdiv(Wd, 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const float*)ws, nb, Wd, dw);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)ws, a.nsplit, Cout, Cin, dw);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
