@@ -19,10 +19,8 @@
  *   pmu_head1x1_fwd/_bwd, pmu_wgrad1x1   OutConv + sigmoid           unet_parts.py:70-76, unet_model.py:48-49
  *   pmu_sgd_clip         clip_grad_value_(0.1) + SGD(momentum)        PMU/train.py:65,108-110
  *   pmu_dice_counts      dice_coeff + argmax/one-hot                  PMU/dice_loss.py:5-12, trainer/unet_trainer.py:39-58
- *   pmu_slice3view       MRI_Dataset.pad_dimensions/sample_slice/preprocess  PMU/utils/mri_dataset.py:70-112
- *   pmu_fuse3view        eval.py volume fusion                        PMU/eval.py:157-203
  *   pmu_fcomb_*          Fcomb 1x1 chain with tiled z                 probabilistic_unet.py:116-181
- *   pmu_spatial_mean / pmu_latent_head   AxisAlignedConvGaussian head probabilistic_unet.py:97-108
+ *   pmu_spatial_mean(_bwd) / pmu_linear_*   AxisAlignedConvGaussian head  probabilistic_unet.py:95-108
  *
  * Conventions
  *   - All tensors are device pointers, fp32, activations stored channels-last (NHWC),
@@ -178,6 +176,42 @@ int pmu_sgd_clip(const pmu_sgd_chunk* chunks, int nchunks, void* const* ptrs, fl
  * y NCHW [N][K][H][W], mask [N][H][W]. */
 int pmu_dice_counts(const float* y, const float* mask, int N, int K, int H, int W,
                     double* counts, void* stream);
+
+/* ---- probabilistic path: latent head of AxisAlignedConvGaussian ---------------------------
+ * probabilistic_unet.py:95-108: encoding = mean_{h,w} relu(bn(z_last)); mu_log_sigma = conv1x1(encoding). */
+/* out[N][C] = (1/(H*W)) sum_{h,w} max(0, z*scale+shift), z NHWC, coef = [scale|shift]. */
+int pmu_spatial_mean(const float* z, const float* coef, int N, int H, int W, int C, float* out,
+                     void* stream);
+/* da[N][H][W][C] = dmean[N][C] / (H*W). */
+int pmu_spatial_mean_bwd(const float* dmean, int N, int H, int W, int C, float* da, void* stream);
+/* y[N][M] = x[N][K] . w[M][K]^T + b  (a 1x1 conv on a 1x1 map, probabilistic_unet.py:72,101). */
+int pmu_linear_fwd(const float* x, const float* w, const float* b, int N, int K, int M, float* y,
+                   void* stream);
+/* dx = dy.w (dx may be NULL), dw = dy^T.x, db = sum_n dy (db may be NULL); M <= 256. */
+int pmu_linear_bwd(const float* x, const float* w, const float* dy, int N, int K, int M, float* dx,
+                   float* dw, float* db, void* stream);
+
+/* ---- probabilistic path: Fcomb (probabilistic_unet.py:116-181) ----------------------------
+ * logits = W_last . relu(W_NH ... relu(W_1 . cat(f, tile(z)) + b_1) ...) + b_last per pixel,
+ * NH = no_convs_fcomb - 1 hidden 1x1 convs (1..3), F = feature width (<= 64), L = latent dim,
+ * K = classes (<= 32).  w[l], b[l]: PyTorch layouts (w[0] = W_1 [F][F+L], w[l>0] = [F][F]),
+ * wl = W_last [K][F].  The tiled z is never built: zb = W_1z . z + b_1 is a per-(sample,image)
+ * bias from pmu_fcomb_zbias. */
+/* zb[SN][F] = w1[:, F:F+L] . z[SN][L] + b1. */
+int pmu_fcomb_zbias(const float* z, const float* w1, const float* b1, int SN, int F, int L,
+                    float* zb, void* stream);
+/* feat NHWC [N][H][W][F]; zb [S][N][F]; y NCHW [S][N][K][H][W] (S samples in one pass). */
+int pmu_fcomb_fwd(const float* feat, const float* zb, const float* const* w, const float* const* b,
+                  const float* wl, const float* bl, int F, int L, int K, int NH, int S, int N, int H,
+                  int W, float* y, void* stream);
+size_t pmu_fcomb_bwd_ws(int N, int H, int W);
+/* One sample: dl = dL/dlogits NCHW [N][K][H][W] -> dfeat NHWC, dz [N][L] (may be NULL),
+ * dw[l], db[l] (PyTorch layouts, overwritten), dwl, dbl.  z [N][L] and zb [N][F] as in forward. */
+int pmu_fcomb_bwd(const float* feat, const float* z, const float* zb, const float* dl,
+                  const float* const* w, const float* const* b, const float* wl, const float* bl,
+                  int F, int L, int K, int NH, int N, int H, int W, float* dfeat, float* dz,
+                  float* const* dw, float* const* db, float* dwl, float* dbl, float* ws,
+                  size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

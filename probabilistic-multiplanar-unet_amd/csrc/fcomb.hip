@@ -1,0 +1,629 @@
+// Fcomb (PMU/model/probabilistic_unet/probabilistic_unet.py:116-181) and the latent head of
+// AxisAlignedConvGaussian (probabilistic_unet.py:95-108) on gfx950.
+//
+// Fcomb: logits = W_last . relu(W_NH ... relu(W_1 . [f ; tile(z)] + b_1) ...) + b_last per pixel.
+// The tiled z is never materialised: W_1 . [f ; z] = W_1f . f + (W_1z . z + b_1), the second term
+// being a per-(sample, image) bias zb computed once (pmu_fcomb_zbias).  One launch evaluates S
+// samples: the feature tile is staged and W_1f . f computed once, then each sample adds its own zb.
+// Per-pixel layers are 64-wide GEMMs on f32 MFMA (32x32x2); activations stay in LDS.
+// Backward recomputes the forward for its tile in LDS and back-propagates through the chain,
+// accumulating weight gradients in registers across the tiles of a persistent block and writing
+// one fp32 partial slab per block (fixed-order reduction, no atomics).
+#include "pmu_common.h"
+
+namespace {
+
+constexpr int FW = 64;         // padded feature / hidden width
+constexpr int KP = 32;         // padded output classes
+constexpr int RS = FW + 1;     // LDS row stride (b32 reads: consecutive lanes -> distinct banks)
+constexpr int MAXNH = 3;       // hidden layers supported (no_convs_fcomb <= 4)
+
+struct FcombW {
+  const float* w[MAXNH];  // w[0] = W_1 [F][F+L] (feature part used), w[l] = [F][F]
+  const float* b[MAXNH];  // b[0] unused in-kernel (folded into zb)
+  const float* wl;        // W_last [K][F]
+  const float* bl;        // [K]
+  int F, L, K, NH;
+};
+
+// stage all weights into LDS: Ws[l][o][c] (padded to 64x64, stride RS), Wl[o][c] (32 x 64)
+__device__ __forceinline__ void stage_weights(const FcombW& p, float* Ws, float* Wl) {
+  for (int e = threadIdx.x; e < MAXNH * FW * FW; e += blockDim.x) {
+    const int l = e / (FW * FW), r = e % (FW * FW), o = r / FW, c = r % FW;
+    float v = 0.f;
+    if (l < p.NH && o < p.F && c < p.F) v = p.w[l][(long long)o * (l == 0 ? p.F + p.L : p.F) + c];
+    Ws[(l * FW + o) * RS + c] = v;
+  }
+  for (int e = threadIdx.x; e < KP * FW; e += blockDim.x) {
+    const int o = e / FW, c = e % FW;
+    Wl[o * RS + c] = (o < p.K && c < p.F) ? p.wl[o * p.F + c] : 0.f;
+  }
+}
+
+// acc[fn] (32 px x 32 out, out = fn*32 + lane&31) = sum_k A[px][k] * W[o][k] over k < 64.
+// A rows are this wave's 32 pixels (row base pa), W rows o (stride RS).
+template <int NF>
+__device__ __forceinline__ void mm64(const float* A, const float* W, int lane, f32x16 (&acc)[NF]) {
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[f][r] = 0.f;
+  const float* pa = A + (lane & 31) * RS + (lane >> 5);
+#pragma unroll 4
+  for (int k = 0; k < FW; k += 2) {
+    const float av = pa[k];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[f] = mfma_f32_32x32x2(av, W[(f * 32 + (lane & 31)) * RS + k + (lane >> 5)], acc[f]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward: y[s][n][k][h][w]; feat NHWC [P][F]; zb [S][N][F]
+// block = 4 waves, tile = 128 pixels (wave w: pixels 32w..32w+31), persistent over tiles
+// ------------------------------------------------------------------------------------------
+constexpr int FT = 128;
+
+__global__ __launch_bounds__(256) void fcomb_fwd_kernel(const float* __restrict__ feat, const float* __restrict__ zb,
+                                                        FcombW p, int S, int N, long long HW, float* __restrict__ y,
+                                                        long long ntiles) {
+  __shared__ __attribute__((aligned(16))) float sm[MAXNH * FW * RS + KP * RS + 2 * FT * RS];
+  float* Ws = sm;                       // MAXNH*64*RS
+  float* Wl = Ws + MAXNH * FW * RS;     // 32*RS
+  float* U1 = Wl + KP * RS;             // [128][RS]  W_1f . f (sample independent)
+  float* Hb = U1 + FT * RS;             // [128][RS]  working activations
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  stage_weights(p, Ws, Wl);
+  const long long P = (long long)N * HW;
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long long p0 = tile * FT;
+    __syncthreads();  // weights staged / previous tile's LDS reads done
+    for (int e = tid; e < FT * FW; e += 256) {
+      const int r = e / FW, c = e % FW;
+      const long long px = p0 + r;
+      Hb[r * RS + c] = (px < P && c < p.F) ? feat[px * p.F + c] : 0.f;
+    }
+    __syncthreads();
+    const float* A = Hb + wave * 32 * RS;
+    float* U = U1 + wave * 32 * RS;
+    float* Hw = Hb + wave * 32 * RS;
+    {  // u1 = W_1f . f
+      f32x16 acc[2];
+      mm64<2>(A, Ws, lane, acc);
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) U[acc_row(r, lane) * RS + f * 32 + (lane & 31)] = acc[f][r];
+    }
+    for (int s = 0; s < S; ++s) {
+      // h1 = relu(u1 + zb[s][n])
+#pragma unroll 4
+      for (int e = lane; e < 32 * FW; e += 64) {
+        const int r = e / FW, c = e % FW;
+        const long long px = p0 + wave * 32 + r;
+        const int n = (int)((px < P ? px : P - 1) / HW);
+        const float b = c < p.F ? zb[((long long)s * N + n) * p.F + c] : 0.f;
+        Hw[r * RS + c] = fmaxf(0.f, U[r * RS + c] + b);
+      }
+      for (int l = 1; l < p.NH; ++l) {
+        f32x16 acc[2];
+        mm64<2>(Hw, Ws + l * FW * RS, lane, acc);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int o = f * 32 + (lane & 31);
+          const float b = o < p.F ? p.b[l][o] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) Hw[acc_row(r, lane) * RS + o] = fmaxf(0.f, acc[f][r] + b);
+        }
+      }
+      f32x16 acc[1];
+      mm64<1>(Hw, Wl, lane, acc);
+      const int k = lane & 31;
+      if (k < p.K) {
+        const float b = p.bl[k];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long px = p0 + wave * 32 + acc_row(r, lane);
+          if (px < P) {
+            const long long n = px / HW, pix = px - n * HW;
+            y[(((long long)s * N + n) * p.K + k) * HW + pix] = acc[0][r] + b;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward (one sample): given dl = dL/dy [N][K][HW], recompute the chain per 64-pixel tile
+// and produce dfeat NHWC [P][F], per-block partial slabs of dW_l, db_l, dW_last, db_last and
+// per-image dzb[n][F] (= dL/d(zb), summed over the image's pixels).
+// block = 4 waves; GEMMs over 64 px x 64 out are split 2x2 over waves.
+// ------------------------------------------------------------------------------------------
+constexpr int BT = 64;
+
+struct FcombG {
+  float* dfeat;  // [P][F]
+  float* ws;     // per block: NH*64*64 (dW_l, [o][c]) + 32*64 (dW_last) + NH*64 (db_l) + 32 (db_last)
+  float* dzb;    // per block: [N][64]  (zeroed by the kernel, block-partial)
+};
+
+constexpr int WS_BLOCK = MAXNH * FW * FW + KP * FW + MAXNH * FW + KP;
+
+// C[px][o] += sum_k A[px][k] * B[k][o]  for a 32x32 fragment: A row stride RS, B given as
+// element accessor (k, o).  Lane supplies A[px = lane&31][k] and B[k][o = lane&31].
+template <class BF>
+__device__ __forceinline__ void frag_mm(const float* A, int arow0, int K, const BF& bf, int ocol0, int lane,
+                                        f32x16& acc) {
+  const float* pa = A + (arow0 + (lane & 31)) * RS + (lane >> 5);
+#pragma unroll 4
+  for (int k = 0; k < K; k += 2)
+    acc = mfma_f32_32x32x2(pa[k], bf(k + (lane >> 5), ocol0 + (lane & 31)), acc);
+}
+
+__global__ __launch_bounds__(256) void fcomb_bwd_kernel(const float* __restrict__ feat, const float* __restrict__ zb,
+                                                        const float* __restrict__ dl, FcombW p, int N, long long HW,
+                                                        FcombG g, long long ntiles) {
+  __shared__ __attribute__((aligned(16))) float sm[MAXNH * FW * RS + KP * RS + BT * RS + MAXNH * BT * RS + BT * RS + BT * 33];
+  float* Ws = sm;                     // [NH][64 o][RS]
+  float* Wl = Ws + MAXNH * FW * RS;   // [32][RS]
+  float* Fb = Wl + KP * RS;           // features [64][RS]
+  float* Hb = Fb + BT * RS;           // H1..H3 [3][64][RS]
+  float* Xb = Hb + MAXNH * BT * RS;   // scratch dU [64][RS]
+  float* Db = Xb + BT * RS;           // dl [64][33]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fm = wave >> 1, fn = wave & 1;  // 2x2 split of 64x64 GEMMs
+  const int NH = p.NH;
+  stage_weights(p, Ws, Wl);
+  float* myws = g.ws + (long long)blockIdx.x * WS_BLOCK;
+  float* mydzb = g.dzb + (long long)blockIdx.x * N * FW;
+  for (int e = tid; e < N * FW; e += 256) mydzb[e] = 0.f;
+
+  // weight-gradient accumulators (register-resident across tiles): dW_l[o][c] frag (fm, fn)
+  f32x16 dW[MAXNH];
+  f32x16 dWl;
+#pragma unroll
+  for (int l = 0; l < MAXNH; ++l)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dW[l][r] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dWl[r] = 0.f;
+  float dbl = 0.f, db[MAXNH] = {0.f, 0.f, 0.f};  // thread tid < 64 owns column tid
+  const long long P = (long long)N * HW;
+
+  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long long p0 = tile * BT;
+    __syncthreads();
+    for (int e = tid; e < BT * FW; e += 256) {
+      const int r = e / FW, c = e % FW;
+      const long long px = p0 + r;
+      Fb[r * RS + c] = (px < P && c < p.F) ? feat[px * p.F + c] : 0.f;
+    }
+    for (int e = tid; e < BT * KP; e += 256) {
+      const int r = e / KP, k = e % KP;
+      const long long px = p0 + r;
+      float v = 0.f;
+      if (px < P && k < p.K) {
+        const long long n = px / HW, pix = px - n * HW;
+        v = dl[(n * p.K + k) * HW + pix];
+      }
+      Db[r * 33 + k] = v;
+    }
+    __syncthreads();
+    // ---- recompute H_l = relu(U_l)
+    for (int l = 0; l < NH; ++l) {
+      const float* A = l == 0 ? Fb : Hb + (l - 1) * BT * RS;
+      const float* W = Ws + l * FW * RS;
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      frag_mm(A, fm * 32, FW, [&](int k, int o) { return W[o * RS + k]; }, fn * 32, lane, acc);
+      float* H = Hb + l * BT * RS;
+      const int o = fn * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = fm * 32 + acc_row(r, lane);
+        float b;
+        if (l == 0) {
+          const long long px = p0 + rr;
+          const int n = (int)((px < P ? px : P - 1) / HW);
+          b = o < p.F ? zb[(long long)n * p.F + o] : 0.f;
+        } else {
+          b = o < p.F ? p.b[l][o] : 0.f;
+        }
+        H[rr * RS + o] = fmaxf(0.f, acc[r] + b);
+      }
+      __syncthreads();
+    }
+    // ---- last layer: dU_NH = (dl . W_last) * [H_NH > 0];  dW_last += dl^T H_NH;  db_last += sum dl
+    {
+      const float* Hn = Hb + (NH - 1) * BT * RS;
+      if (wave < 2) {  // dW_last [32 o][64 c]: frag (o 0..31, c = wave*32..)
+        const float* pd = Db + (lane >> 5) * 33;
+#pragma unroll 4
+        for (int k = 0; k < BT; k += 2) {  // k = pixel
+          const float av = pd[(k) * 33 + (lane & 31)];          // A[o][px] = dl[px][o]
+          const float bv = Hn[(k + (lane >> 5)) * RS + wave * 32 + (lane & 31)];  // B[px][c]
+          dWl = mfma_f32_32x32x2(av, bv, dWl);
+        }
+      }
+      if (tid < KP) {
+        float s = 0.f;
+        for (int r = 0; r < BT; ++r) s += Db[r * 33 + tid];
+        dbl += s;
+      }
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      // dH[px][c] = sum_o dl[px][o] W_last[o][c]  (A = Db rows (stride 33), K = 32 classes)
+      {
+        const float* pa = Db + (fm * 32 + (lane & 31)) * 33 + (lane >> 5);
+#pragma unroll 4
+        for (int k = 0; k < KP; k += 2)
+          acc = mfma_f32_32x32x2(pa[k], Wl[(k + (lane >> 5)) * RS + fn * 32 + (lane & 31)], acc);
+      }
+      const int c = fn * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = fm * 32 + acc_row(r, lane);
+        Xb[rr * RS + c] = Hn[rr * RS + c] > 0.f ? acc[r] : 0.f;
+      }
+      __syncthreads();
+    }
+    // ---- hidden layers l = NH-1 .. 0:  dU_l in Xb
+    for (int l = NH - 1; l >= 0; --l) {
+      const float* Hin = l == 0 ? Fb : Hb + (l - 1) * BT * RS;  // input of layer l
+      // dW_l[o][c] += sum_px dU[px][o] * Hin[px][c]   (frag: o = fm*32.., c = fn*32..)
+      {
+        const float* pa = Xb + (lane >> 5) * RS + fm * 32 + (lane & 31);  // A[o][px] = dU[px][o]
+        const float* pb = Hin + (lane >> 5) * RS + fn * 32 + (lane & 31);
+        f32x16 acc = dW[0];
+        if (l == 1) acc = dW[1];
+        if (l == 2) acc = dW[2];
+#pragma unroll 4
+        for (int k = 0; k < BT; k += 2) acc = mfma_f32_32x32x2(pa[k * RS], pb[k * RS], acc);
+        if (l == 0) dW[0] = acc;
+        if (l == 1) dW[1] = acc;
+        if (l == 2) dW[2] = acc;
+      }
+      if (tid < FW) {  // db_l (l >= 1) or per-image dzb (l == 0)
+        if (l > 0) {
+          float s = 0.f;
+          for (int r = 0; r < BT; ++r) s += Xb[r * RS + tid];
+          if (l == 1) db[1] += s;
+          if (l == 2) db[2] += s;
+        } else {
+          // group the tile's pixels by image
+          int r = 0;
+          while (r < BT && p0 + r < P) {
+            const long long n = (p0 + r) / HW;
+            const long long end = (n + 1) * HW - p0;
+            const int r1 = (int)(end < BT ? end : BT);
+            float s = 0.f;
+            for (int q = r; q < r1 && p0 + q < P; ++q) s += Xb[q * RS + tid];
+            mydzb[n * FW + tid] += s;
+            r = r1;
+          }
+        }
+      }
+      // dX[px][c] = sum_o dU[px][o] W_l[o][c]
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const float* W = Ws + l * FW * RS;
+      {
+        const float* pa = Xb + (fm * 32 + (lane & 31)) * RS + (lane >> 5);
+#pragma unroll 4
+        for (int k = 0; k < FW; k += 2)
+          acc = mfma_f32_32x32x2(pa[k], W[(k + (lane >> 5)) * RS + fn * 32 + (lane & 31)], acc);
+      }
+      __syncthreads();  // everyone done reading Xb / Hin
+      const int c = fn * 32 + (lane & 31);
+      if (l > 0) {
+        const float* Hm = Hb + (l - 1) * BT * RS;  // relu mask of layer l-1's output
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rr = fm * 32 + acc_row(r, lane);
+          Xb[rr * RS + c] = Hm[rr * RS + c] > 0.f ? acc[r] : 0.f;
+        }
+      } else if (c < p.F) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long px = p0 + fm * 32 + acc_row(r, lane);
+          if (px < P) g.dfeat[px * p.F + c] = acc[r];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // ---- write the block's partial slab
+#pragma unroll
+  for (int l = 0; l < MAXNH; ++l) {
+    if (l >= NH) break;
+    const int c = fn * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) myws[(l * FW + fm * 32 + acc_row(r, lane)) * FW + c] = dW[l][r];
+  }
+  if (wave < 2) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) myws[MAXNH * FW * FW + acc_row(r, lane) * FW + wave * 32 + (lane & 31)] = dWl[r];
+  }
+  if (tid < FW) {
+    for (int l = 1; l < MAXNH; ++l) myws[MAXNH * FW * FW + KP * FW + l * FW + tid] = db[l];
+    myws[MAXNH * FW * FW + KP * FW + tid] = 0.f;
+  }
+  if (tid < KP) myws[MAXNH * FW * FW + KP * FW + MAXNH * FW + tid] = dbl;
+}
+
+struct FcombOut {
+  float* dw[MAXNH];  // dw[0] = dW_1 [F][F+L]
+  float* db[MAXNH];
+  float* dwl;
+  float* dbl;
+  float* dz;  // [N][L] or null
+};
+
+// sum the per-block slabs (fixed order) and scatter to the PyTorch-layout gradients;
+// entries past WS_BLOCK reduce the per-image dzb slabs into dzb_out [N][64]
+__global__ void fcomb_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ dzb_slab, int nblk, int N,
+                                    FcombW p, FcombOut o, float* __restrict__ dzb_out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= WS_BLOCK) {
+    const int q = e - WS_BLOCK;
+    if (q >= N * FW) return;
+    float s = 0.f;
+    for (int b = 0; b < nblk; ++b) s += dzb_slab[(long long)b * N * FW + q];
+    dzb_out[q] = s;
+    return;
+  }
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += ws[(long long)b * WS_BLOCK + e];
+  if (e < MAXNH * FW * FW) {
+    const int l = e / (FW * FW), r = e % (FW * FW), oo = r / FW, c = r % FW;
+    if (l < p.NH && oo < p.F && c < p.F) o.dw[l][(long long)oo * (l == 0 ? p.F + p.L : p.F) + c] = s;
+    return;
+  }
+  int r = e - MAXNH * FW * FW;
+  if (r < KP * FW) {
+    const int oo = r / FW, c = r % FW;
+    if (oo < p.K && c < p.F) o.dwl[oo * p.F + c] = s;
+    return;
+  }
+  r -= KP * FW;
+  if (r < MAXNH * FW) {
+    const int l = r / FW, c = r % FW;
+    if (l >= 1 && l < p.NH && c < p.F) o.db[l][c] = s;
+    return;
+  }
+  r -= MAXNH * FW;
+  if (r < p.K) o.dbl[r] = s;
+}
+
+// the z side of layer 1 from dzb[n][o] = dL/d(zb[n][o]):
+//   db_1[o] = sum_n dzb[n][o];  dW_1[o][F+l] = sum_n dzb[n][o] z[n][l];  dz[n][l] = sum_o dzb[n][o] W_1[o][F+l]
+__global__ void fcomb_zgrad_kernel(const float* __restrict__ dzb, const float* __restrict__ z, int N, FcombW p,
+                                   FcombOut o) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int F = p.F, L = p.L;
+  if (e < F) {
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += dzb[n * FW + e];
+    o.db[0][e] = s;
+    return;
+  }
+  int r = e - F;
+  if (r < F * L) {
+    const int oo = r / L, l = r % L;
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s = fmaf(dzb[n * FW + oo], z[(long long)n * L + l], s);
+    o.dw[0][(long long)oo * (F + L) + F + l] = s;
+    return;
+  }
+  r -= F * L;
+  if (o.dz && r < N * L) {
+    const int n = r / L, l = r % L;
+    float s = 0.f;
+    for (int oo = 0; oo < F; ++oo) s = fmaf(dzb[n * FW + oo], p.w[0][(long long)oo * (F + L) + F + l], s);
+    o.dz[r] = s;
+  }
+}
+
+// zb[s][n][o] = sum_l W_1[o][F+l] z[s][n][l] + b_1[o]
+__global__ void fcomb_zbias_kernel(const float* __restrict__ z, const float* __restrict__ w1, const float* __restrict__ b1,
+                                   int SN, int F, int L, float* __restrict__ zb) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= SN * F) return;
+  const int sn = e / F, o = e % F;
+  float acc = b1 ? b1[o] : 0.f;
+  for (int l = 0; l < L; ++l) acc = fmaf(w1[(long long)o * (F + L) + F + l], z[(long long)sn * L + l], acc);
+  zb[e] = acc;
+}
+
+// ---------------- latent head of AxisAlignedConvGaussian ----------------
+// mean[n][c] = (1/HW) sum_p relu(z*scale+shift)  (torch.mean over dim 2 then 3, :97-98)
+__global__ __launch_bounds__(256) void spatial_mean_kernel(const float* __restrict__ z, const float* __restrict__ coef,
+                                                           int N, int HW, int C, float* __restrict__ out) {
+  __shared__ float red[256];
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int pg = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < C) {
+    const float sc = coef[c], sh = coef[C + c];
+    for (int p = pg; p < HW; p += 4) s += fmaxf(0.f, fmaf(z[((long long)n * HW + p) * C + c], sc, sh));
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (pg == 0 && c < C) out[(long long)n * C + c] = (red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] +
+                                                      red[threadIdx.x + 192]) / (float)HW;
+}
+
+// da[n][p][c] = dmean[n][c] / HW  (backward of the spatial mean)
+__global__ void spatial_mean_bwd_kernel(const float* __restrict__ dmean, int N, int HW, int C, float* __restrict__ da) {
+  const long long total = (long long)N * HW * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long n = e / ((long long)HW * C);
+    da[e] = dmean[n * C + c] / (float)HW;
+  }
+}
+
+// y[n][m] = sum_k x[n][k] w[m][k] + b[m]   (the 1x1 conv of a 1x1 map, :72,101)
+__global__ void linear_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                                  int N, int K, int M, float* __restrict__ y) {
+  __shared__ float red[256];
+  const int n = blockIdx.y, m = blockIdx.x;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) s = fmaf(x[(long long)n * K + k], w[(long long)m * K + k], s);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) y[(long long)n * M + m] = red[0] + (b ? b[m] : 0.f);
+}
+
+// dx[n][k] = sum_m dy[n][m] w[m][k];  dw[m][k] = sum_n dy[n][m] x[n][k];  db[m] = sum_n dy[n][m]
+__global__ void linear_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ dy,
+                                  int N, int K, int M, float* __restrict__ dx, float* __restrict__ dw,
+                                  float* __restrict__ db) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < K) {
+    for (int n = 0; n < N; ++n) {
+      float s = 0.f;
+      for (int m = 0; m < M; ++m) s = fmaf(dy[(long long)n * M + m], w[(long long)m * K + k], s);
+      if (dx) dx[(long long)n * K + k] = s;
+    }
+    for (int m = 0; m < M; ++m) {
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s = fmaf(dy[(long long)n * M + m], x[(long long)n * K + k], s);
+      dw[(long long)m * K + k] = s;
+    }
+  }
+  if (db && blockIdx.x == 0 && threadIdx.x < M) {
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += dy[(long long)n * M + threadIdx.x];
+    db[threadIdx.x] = s;
+  }
+}
+
+static int fcomb_bwd_blocks(long long ntiles) {
+  long long b = ntiles < 512 ? ntiles : 512;
+  return (int)(b < 1 ? 1 : b);
+}
+
+static bool make_w(FcombW& p, const float* const* w, const float* const* b, const float* wl, const float* bl, int F,
+                   int L, int K, int NH) {
+  if (F < 1 || F > FW || L < 0 || K < 1 || K > KP || NH < 1 || NH > MAXNH || !w || !b || !wl || !bl) return false;
+  for (int l = 0; l < MAXNH; ++l) {
+    p.w[l] = l < NH ? w[l] : nullptr;
+    p.b[l] = l < NH ? b[l] : nullptr;
+    if (l < NH && (!w[l] || !b[l])) return false;
+  }
+  p.wl = wl; p.bl = bl; p.F = F; p.L = L; p.K = K; p.NH = NH;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int pmu_fcomb_zbias(const float* z, const float* w1, const float* b1, int SN, int F, int L, float* zb,
+                               void* stream) {
+  PMU_REQUIRE(z && w1 && b1 && zb && SN > 0 && F > 0 && F <= FW && L >= 0);
+  hipLaunchKernelGGL(fcomb_zbias_kernel, dim3((unsigned)pmu_cdiv((long long)SN * F, 256)), dim3(256), 0,
+                     (hipStream_t)stream, z, w1, b1, SN, F, L, zb);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_fcomb_fwd(const float* feat, const float* zb, const float* const* w, const float* const* b,
+                             const float* wl, const float* bl, int F, int L, int K, int NH, int S, int N, int H, int W,
+                             float* y, void* stream) {
+  FcombW p;
+  PMU_REQUIRE(feat && zb && y && S > 0 && N > 0 && H > 0 && W > 0 && make_w(p, w, b, wl, bl, F, L, K, NH));
+  const long long HW = (long long)H * W;
+  const long long ntiles = ((long long)N * HW + FT - 1) / FT;
+  const long long g = ntiles < 1024 ? ntiles : 1024;
+  hipLaunchKernelGGL(fcomb_fwd_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, feat, zb, p, S, N, HW, y,
+                     ntiles);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" size_t pmu_fcomb_bwd_ws(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return 0;
+  const long long ntiles = ((long long)N * H * W + BT - 1) / BT;
+  const int nb = fcomb_bwd_blocks(ntiles);
+  return ((size_t)nb * WS_BLOCK + (size_t)nb * N * FW + (size_t)N * FW) * sizeof(float);
+}
+
+extern "C" int pmu_fcomb_bwd(const float* feat, const float* z, const float* zb, const float* dl,
+                             const float* const* w, const float* const* b, const float* wl, const float* bl, int F,
+                             int L, int K, int NH, int N, int H, int W, float* dfeat, float* dz, float* const* dw,
+                             float* const* db, float* dwl, float* dbl, float* ws, size_t ws_bytes, void* stream) {
+  FcombW p;
+  PMU_REQUIRE(feat && z && zb && dl && dfeat && dw && db && dwl && dbl && ws);
+  PMU_REQUIRE(N > 0 && H > 0 && W > 0 && make_w(p, w, b, wl, bl, F, L, K, NH));
+  PMU_REQUIRE(ws_bytes >= pmu_fcomb_bwd_ws(N, H, W));
+  FcombOut o;
+  for (int l = 0; l < MAXNH; ++l) {
+    o.dw[l] = l < NH ? dw[l] : nullptr;
+    o.db[l] = l < NH ? db[l] : nullptr;
+    if (l < NH) PMU_REQUIRE(dw[l] && db[l]);
+  }
+  o.dwl = dwl; o.dbl = dbl; o.dz = dz;
+  const long long HW = (long long)H * W;
+  const long long ntiles = ((long long)N * HW + BT - 1) / BT;
+  const int nb = fcomb_bwd_blocks(ntiles);
+  FcombG gg;
+  gg.dfeat = dfeat;
+  gg.ws = ws;
+  gg.dzb = ws + (size_t)nb * WS_BLOCK;
+  float* dzb = gg.dzb + (size_t)nb * N * FW;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(fcomb_bwd_kernel, dim3((unsigned)nb), dim3(256), 0, st, feat, zb, dl, p, N, HW, gg, ntiles);
+  PMU_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fcomb_reduce_kernel, dim3((unsigned)pmu_cdiv(WS_BLOCK + (long long)N * FW, 256)), dim3(256), 0, st,
+                     ws, gg.dzb, nb, N, p, o, dzb);
+  PMU_CHECK_LAUNCH();
+  hipLaunchKernelGGL(fcomb_zgrad_kernel, dim3((unsigned)pmu_cdiv(F + F * L + (long long)N * L, 256)), dim3(256), 0, st,
+                     dzb, z, N, p, o);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_spatial_mean(const float* z, const float* coef, int N, int H, int W, int C, float* out,
+                                void* stream) {
+  PMU_REQUIRE(z && coef && out && N > 0 && H > 0 && W > 0 && C > 0);
+  hipLaunchKernelGGL(spatial_mean_kernel, dim3((unsigned)pmu_cdiv(C, 64), (unsigned)N), dim3(256), 0,
+                     (hipStream_t)stream, z, coef, N, H * W, C, out);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_spatial_mean_bwd(const float* dmean, int N, int H, int W, int C, float* da, void* stream) {
+  PMU_REQUIRE(dmean && da && N > 0 && H > 0 && W > 0 && C > 0);
+  const long long total = (long long)N * H * W * C;
+  const long long g = total / 256 + 1 < 4096 ? total / 256 + 1 : 4096;
+  hipLaunchKernelGGL(spatial_mean_bwd_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, dmean, N, H * W, C,
+                     da);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_linear_fwd(const float* x, const float* w, const float* b, int N, int K, int M, float* y,
+                              void* stream) {
+  PMU_REQUIRE(x && w && y && N > 0 && K > 0 && M > 0 && N <= 65535);
+  hipLaunchKernelGGL(linear_fwd_kernel, dim3((unsigned)M, (unsigned)N), dim3(256), 0, (hipStream_t)stream, x, w, b, N,
+                     K, M, y);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_linear_bwd(const float* x, const float* w, const float* dy, int N, int K, int M, float* dx, float* dw,
+                              float* db, void* stream) {
+  PMU_REQUIRE(x && w && dy && dw && N > 0 && K > 0 && M > 0 && M <= 256);
+  hipLaunchKernelGGL(linear_bwd_kernel, dim3((unsigned)pmu_cdiv(K, 256)), dim3(256), 0, (hipStream_t)stream, x, w, dy,
+                     N, K, M, dx, dw, db);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}

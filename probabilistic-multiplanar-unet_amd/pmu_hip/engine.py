@@ -337,9 +337,9 @@ def unet_forward(net, x: torch.Tensor, training: bool):
     return feat.permute(0, 3, 1, 2), st
 
 
-def unet_backward(net, st: UNetState, dy: torch.Tensor, sink_views=False) -> dict:
+def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None = None) -> dict:
     """Backward of unet_forward given dL/d(output).  Returns {parameter: grad}."""
-    grads = GradSink(getattr(net, "_pmu_grad_views", None) if sink_views else None)
+    grads = grads if grads is not None else GradSink()
     s = L.stream()
     dev = dy.device
     x = st.x

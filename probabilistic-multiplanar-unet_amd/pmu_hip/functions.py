@@ -1,67 +1,107 @@
-"""Autograd bridge: one torch.autograd.Function per fused network, backed by pmu_hip.engine.
+"""Autograd bridge: one torch.autograd.Function per fused network part, backed by the HIP executors.
 
 The reference builds one autograd node per PyTorch op (~90 for the 5-level U-Net); here the
 whole U-Net forward is a single node whose backward replays the stack in reverse on the HIP
-kernels and returns every parameter gradient at once.
+kernels and returns every parameter gradient at once.  The Probabilistic U-Net adds two more
+node kinds: the prior/posterior AxisAlignedConvGaussian (encoder + latent head) and Fcomb.
+
+Gradients: when every ``.grad`` of a node's parameters is None (zero_grad(set_to_none=True)),
+the kernels write straight into fresh views of one persistent flat buffer owned by the root
+module (the U-Net, or the ProbabilisticUnet that contains it); autograd adopts those views as
+``.grad``, so all gradients are contiguous for one all-reduce and pointer-stable for FusedSGD.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
-from . import engine
+from . import engine, prob_engine
+from .engine import GradSink
+
+_NO_CPU = "runs on the MI355X HIP path only: move the model and inputs to the GPU (there is no CPU fallback)"
 
 
-class UNetFunction(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, net, x, *params):
-        out, st = engine.unet_forward(net, x, net.training)
-        ctx.net = net
-        ctx.st = st
-        ctx.nparams = len(params)
-        return out
+# ----------------------------------------------------------------------------------------
+# flat gradient buffer
+# ----------------------------------------------------------------------------------------
+def set_grad_root(module, root):
+    """Make ``module``'s gradient views live in ``root``'s flat buffer (not a submodule link)."""
+    module.__dict__["_pmu_root_ref"] = weakref.ref(root)
 
-    @staticmethod
-    def backward(ctx, dy):
-        net = ctx.net
-        plist = list(net.parameters())
-        # When every .grad is None (zero_grad(set_to_none=True)), the kernels write straight into
-        # fresh views of one persistent flat buffer; autograd then adopts those views as .grad,
-        # so gradients are contiguous for one all-reduce and pointer-stable for the fused SGD.
-        use_flat = all(p.grad is None for p in plist)
-        if use_flat:
-            attach_flat_grad_views(net, plist)
-        grads = engine.unet_backward(net, ctx.st, dy, sink_views=use_flat)
-        net._pmu_grad_views = None
-        ctx.st = None
-        return (None, None) + tuple(grads.get(p) for p in plist)
+
+def grad_root(module):
+    ref = module.__dict__.get("_pmu_root_ref")
+    root = ref() if ref is not None else None
+    return root if root is not None else module
 
 
 def flat_grad_buffer(net, plist=None):
     """The persistent flat fp32 gradient buffer of ``net`` (registration order), created on demand."""
     plist = plist if plist is not None else list(net.parameters())
     total = sum(p.numel() for p in plist)
-    buf = getattr(net, "_pmu_grad_flat", None)
+    buf = net.__dict__.get("_pmu_grad_flat")
     dev = plist[0].device
     if buf is None or buf.numel() != total or buf.device != dev:
         buf = torch.zeros(total, dtype=torch.float32, device=dev)
-        net._pmu_grad_flat = buf
+        net.__dict__["_pmu_grad_flat"] = buf
+        net.__dict__["_pmu_grad_offsets"] = None
     return buf
 
 
-def attach_flat_grad_views(net, plist):
-    buf = flat_grad_buffer(net, plist)
-    views, off = {}, 0
-    for p in plist:
-        n = p.numel()
-        views[p] = buf[off:off + n].view_as(p)
-        off += n
-    net._pmu_grad_views = views
+def _offsets(root, plist):
+    cached = root.__dict__.get("_pmu_grad_offsets")
+    key = tuple(id(p) for p in plist)
+    if cached is None or cached[0] != key:
+        offs, o = {}, 0
+        for p in plist:
+            offs[id(p)] = o
+            o += p.numel()
+        cached = (key, offs)
+        root.__dict__["_pmu_grad_offsets"] = cached
+    return cached[1]
+
+
+def grad_sink_for(module, params) -> GradSink:
+    """Destination of this node's parameter gradients (fresh flat-buffer views, see module doc).
+    The views are created per backward and not retained, so autograd can adopt them as .grad."""
+    if not all(p.grad is None for p in params):
+        return GradSink()
+    root = grad_root(module)
+    plist = list(root.parameters())
+    buf = flat_grad_buffer(root, plist)
+    offs = _offsets(root, plist)
+    views = {}
+    for p in params:
+        o = offs.get(id(p))
+        if o is not None:
+            views[p] = buf[o:o + p.numel()].view_as(p)
+    return GradSink(views)
+
+
+# ----------------------------------------------------------------------------------------
+# U-Net
+# ----------------------------------------------------------------------------------------
+class UNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, net, x, *params):
+        out, st = engine.unet_forward(net, x, net.training)
+        ctx.net = net
+        ctx.st = st
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        net = ctx.net
+        plist = list(net.parameters())
+        grads = engine.unet_backward(net, ctx.st, dy, grad_sink_for(net, plist))
+        ctx.st = None
+        return (None, None) + tuple(grads.get(p) for p in plist)
 
 
 def unet_apply(net, x):
     if not isinstance(x, torch.Tensor) or not x.is_cuda:
-        raise RuntimeError("UNet.forward runs on the MI355X HIP path only: move the model and input to the GPU "
-                           "(there is no CPU fallback)")
+        raise RuntimeError("UNet.forward " + _NO_CPU)
     if x.dtype != torch.float32:
         x = x.float()
     params = list(net.parameters())
@@ -70,3 +110,88 @@ def unet_apply(net, x):
     with torch.no_grad():
         out, _ = engine.unet_forward(net, x, net.training)
     return out
+
+
+# ----------------------------------------------------------------------------------------
+# AxisAlignedConvGaussian: input planes -> mu_log_sigma (N, 2L)
+# ----------------------------------------------------------------------------------------
+def _planes(x, segm):
+    ps = [x[:, c] for c in range(x.shape[1])]
+    if segm is not None:
+        ps += [segm[:, c] for c in range(segm.shape[1])]
+    return [p.contiguous().float() for p in ps]
+
+
+class GaussianFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, x, segm, *params):
+        mls, st = prob_engine.gaussian_forward(g, _planes(x, segm), g.training)
+        ctx.g, ctx.st = g, st
+        return mls
+
+    @staticmethod
+    def backward(ctx, dmls):
+        g = ctx.g
+        plist = list(g.parameters())
+        grads = prob_engine.gaussian_backward(g, ctx.st, dmls, grad_sink_for(g, plist))
+        ctx.st = None
+        return (None, None, None) + tuple(grads.get(p) for p in plist)
+
+
+def gaussian_apply(g, x, segm=None):
+    """mu_log_sigma (N, 2L) of AxisAlignedConvGaussian.forward (probabilistic_unet.py:82-105)."""
+    for t in (x, segm):
+        if t is not None and (not isinstance(t, torch.Tensor) or not t.is_cuda):
+            raise RuntimeError("AxisAlignedConvGaussian.forward " + _NO_CPU)
+    params = list(g.parameters())
+    if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+        return GaussianFunction.apply(g, x, segm, *params)
+    with torch.no_grad():
+        mls, _ = prob_engine.gaussian_forward(g, _planes(x, segm), g.training)
+    return mls
+
+
+# ----------------------------------------------------------------------------------------
+# Fcomb: (features, z) -> logits
+# ----------------------------------------------------------------------------------------
+class FcombFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fc, feat, z, *params):
+        y, fh, zc, zb = prob_engine.fcomb_forward(fc, feat, z.unsqueeze(0))
+        ctx.fc = fc
+        ctx.save = (fh, zc[0], zb)
+        return y[0]
+
+    @staticmethod
+    def backward(ctx, dy):
+        fc = ctx.fc
+        fh, zc, zb = ctx.save
+        plist = list(fc.parameters())
+        grads = grad_sink_for(fc, plist)
+        dfeat, dz = prob_engine.fcomb_backward(fc, fh, zc, zb, dy, grads)
+        ctx.save = None
+        # dfeat is NHWC storage; hand it back with the (N,F,H,W) shape of the features input
+        return (None, dfeat.permute(0, 3, 1, 2), dz) + tuple(grads.get(p) for p in plist)
+
+
+def fcomb_apply(fc, feat, z):
+    """Fcomb.forward (probabilistic_unet.py:167-181): feat (N,F,H,W), z (N,L) -> logits (N,K,H,W)."""
+    for t in (feat, z):
+        if not isinstance(t, torch.Tensor) or not t.is_cuda:
+            raise RuntimeError("Fcomb.forward " + _NO_CPU)
+    params = list(fc.parameters())
+    needs = torch.is_grad_enabled() and (feat.requires_grad or z.requires_grad or any(p.requires_grad for p in params))
+    if needs:
+        return FcombFunction.apply(fc, feat, z, *params)
+    with torch.no_grad():
+        y, _, _, _ = prob_engine.fcomb_forward(fc, feat, z.unsqueeze(0))
+    return y[0]
+
+
+def fcomb_samples(fc, feat, zs):
+    """S samples in one pass (features read once): zs (S,N,L) -> (S,N,K,H,W).  No autograd."""
+    if not feat.is_cuda or not zs.is_cuda:
+        raise RuntimeError("Fcomb sampling " + _NO_CPU)
+    with torch.no_grad():
+        y, _, _, _ = prob_engine.fcomb_forward(fc, feat, zs)
+    return y

@@ -126,6 +126,65 @@ def g2_unet_multiclass():
     np.savez_compressed(os.path.join(OUT, "g2_unet_multiclass.npz"), **out)
 
 
+def _inject(dist, eps, method):
+    """Make a torch Independent(Normal) return loc + scale * eps from rsample()/sample() — what
+    Normal.rsample computes for that eps, so gradients still flow through loc and scale."""
+    def draw(sample_shape=torch.Size()):
+        v = dist.base_dist.loc + dist.base_dist.scale * eps
+        return v if method == "rsample" else v.detach()
+    setattr(dist, method, draw)
+
+
+def g3_probunet():
+    """ProbabilisticUnet(1,3,[4,8,16,32,64],latent_dim=6,no_convs_fcomb=4,beta=10) — the
+    ProbUNetTrainer configuration (probunet_trainer.py:16) at small width — with injected latent
+    noise: one training forward + elbo + backward (probabilistic_unet.py:215-308), 8 prior
+    samples through Fcomb, and an eval-mode pass (training=False, sample(testing=True))."""
+    from model import ProbabilisticUnet
+    out = {}
+    for tag, (N, H, W, S) in {"s64": (2, 64, 64, 8), "s45": (3, 45, 37, 2)}.items():
+        torch.manual_seed(0)
+        net = ProbabilisticUnet(input_channels=1, num_classes=3, num_filters=[4, 8, 16, 32, 64], latent_dim=6,
+                                no_convs_fcomb=4, beta=10.0)
+        if tag == "s64":  # same seed and architecture for both cases: one copy of the initial weights
+            out.update(sd_np("init", net.state_dict()))
+        g = torch.Generator().manual_seed(3)
+        x = torch.rand(N, 1, H, W, generator=g)
+        segm = torch.randint(0, 3, (N, 1, H, W), generator=g).float()
+        eps_post = torch.randn(N, 6, generator=g)
+        eps_prior = torch.randn(S, N, 6, generator=g)
+        eps_eval = torch.randn(N, 6, generator=g)
+        out[f"{tag}/x"], out[f"{tag}/segm"] = x.numpy(), segm.numpy()
+        out[f"{tag}/eps_post"], out[f"{tag}/eps_prior"], out[f"{tag}/eps_eval"] = (
+            eps_post.numpy(), eps_prior.numpy(), eps_eval.numpy())
+        net.train()
+        net.forward(x, segm, training=True)
+        _inject(net.posterior_latent_space, eps_post, "rsample")
+        elbo = net.elbo(segm)
+        loss = -elbo
+        loss.backward()
+        for name, d in (("post", net.posterior_latent_space), ("prior", net.prior_latent_space)):
+            out[f"{tag}/{name}_mu"] = d.base_dist.loc.detach().numpy().copy()
+            out[f"{tag}/{name}_sigma"] = d.base_dist.scale.detach().numpy().copy()
+        out[f"{tag}/feat"] = net.unet_features.detach().numpy().copy()
+        out[f"{tag}/kl"] = np.array(net.kl.item(), dtype=np.float32)
+        out[f"{tag}/ce"] = np.array(net.reconstruction_loss.item(), dtype=np.float32)
+        out[f"{tag}/elbo"] = np.array(elbo.item(), dtype=np.float32)
+        out[f"{tag}/rec"] = net.reconstruction.detach().numpy().copy()
+        out.update(grads_np(f"{tag}/grad", net))
+        out.update(sd_np(f"{tag}/after", dict(net.named_buffers())))   # BN running statistics
+        with torch.no_grad():
+            mu_p, sd_p = net.prior_latent_space.base_dist.loc, net.prior_latent_space.base_dist.scale
+            out[f"{tag}/samples"] = torch.stack(
+                [net.fcomb.forward(net.unet_features, mu_p + sd_p * eps_prior[s]) for s in range(S)]).numpy()
+            net.eval()
+            net.forward(x, segm, training=False)
+            _inject(net.prior_latent_space, eps_eval, "sample")
+            out[f"{tag}/eval_sample"] = net.sample(testing=True).numpy().copy()
+            out[f"{tag}/eval_prior_mu"] = net.prior_latent_space.base_dist.loc.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "g3_probunet.npz"), **out)
+
+
 def g4_dice():
     """dice_coeff known answers (dice_loss.py:5-12) and trainer-style per-class Dice
     (unet_trainer.py:39-58) from the reference trainer's eval()."""
@@ -197,10 +256,17 @@ def main():
     if not os.path.isdir(REF):
         raise SystemExit(f"reference not found at {REF}: fixtures are generated in the build container only")
     nib = install_shims()
-    g1_unet_c1()
-    g2_unet_multiclass()
-    g4_dice()
-    g5_slicer(nib)
+    which = set(sys.argv[1:]) or {"g1", "g2", "g3", "g4", "g5"}
+    if "g1" in which:
+        g1_unet_c1()
+    if "g2" in which:
+        g2_unet_multiclass()
+    if "g3" in which:
+        g3_probunet()
+    if "g4" in which:
+        g4_dice()
+    if "g5" in which:
+        g5_slicer(nib)
     print("golden fixtures written to", OUT)
 
 

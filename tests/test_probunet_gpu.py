@@ -1,0 +1,184 @@
+"""GPU parity of the probabilistic path (rows a9-a12): the HIP ProbabilisticUnet vs the reference's
+own G3 golden vectors (tests/golden/g3_probunet.npz, produced by importing the reference) and vs
+the CPU oracle on larger seeded cases.
+
+Tolerances: outputs |d| <= 1e-3, losses rel <= 1e-3, gradients max|dg|/max|g| <= 1e-3,
+BN running stats |d| <= 1e-3.  Latent noise is injected (mu + sigma * eps), which is exactly what
+Normal.rsample computes, so the comparison is deterministic.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import ACT_TOL, GRAD_TOL, LOSS_RTOL, grad_err, max_abs
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _g3():
+    return np.load(os.path.join(GOLD, "g3_probunet.npz"), allow_pickle=False)
+
+
+def _sd(z, prefix):
+    pre = prefix + "/"
+    return {k[len(pre):]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith(pre)}
+
+
+def _inject(dist, eps, method):
+    def draw(sample_shape=torch.Size()):
+        v = dist.base_dist.loc + dist.base_dist.scale * eps
+        return v if method == "rsample" else v.detach()
+    setattr(dist, method, draw)
+
+
+def _net(dev, num_filters=(4, 8, 16, 32, 64), n_classes=3, seed=0, init=None):
+    """The G3 network.  With ``init`` the reference's initial weights are loaded: the orthogonal
+    Fcomb init goes through LAPACK QR, whose last bits depend on the host CPU (bit-equality of the
+    seeded init is checked in the build container, tests/test_probunet_cpu.py)."""
+    from model import ProbabilisticUnet
+    torch.manual_seed(seed)
+    net = ProbabilisticUnet(input_channels=1, num_classes=n_classes, num_filters=list(num_filters), latent_dim=6,
+                            no_convs_fcomb=4, beta=10.0)
+    if init is not None:
+        net.load_state_dict(_sd(init, "init"))
+    return net.to(dev)
+
+
+@pytest.mark.parametrize("tag", ["s64", "s45"])
+def test_probunet_train_step_matches_reference_g3(tag, dev):
+    z = _g3()
+    net = _net(dev, init=z).train()
+    x = torch.from_numpy(z[f"{tag}/x"]).to(dev)
+    segm = torch.from_numpy(z[f"{tag}/segm"]).to(dev)
+    eps = torch.from_numpy(z[f"{tag}/eps_post"]).to(dev)
+    net.forward(x, segm, training=True)
+    _inject(net.posterior_latent_space, eps, "rsample")
+    elbo = net.elbo(segm)
+    (-elbo).backward()
+    torch.cuda.synchronize()
+    for name, d in (("post", net.posterior_latent_space), ("prior", net.prior_latent_space)):
+        assert max_abs(d.base_dist.loc, torch.from_numpy(z[f"{tag}/{name}_mu"])) <= ACT_TOL, name
+        assert max_abs(d.base_dist.scale, torch.from_numpy(z[f"{tag}/{name}_sigma"])) <= ACT_TOL, name
+    assert max_abs(net.unet_features, torch.from_numpy(z[f"{tag}/feat"])) <= ACT_TOL
+    assert max_abs(net.reconstruction, torch.from_numpy(z[f"{tag}/rec"])) <= ACT_TOL
+    for q, ref in (("kl", net.kl), ("ce", net.reconstruction_loss), ("elbo", elbo)):
+        r = float(z[f"{tag}/{q}"])
+        assert abs(float(ref) - r) <= LOSS_RTOL * max(1.0, abs(r)), (q, float(ref), r)
+    named = dict(net.named_parameters())
+    gref = _sd(z, f"{tag}/grad")
+    missing = [k for k in gref if named[k].grad is None]
+    assert not missing, missing[:4]
+    err, key = grad_err({k: named[k].grad for k in gref}, gref)
+    assert err <= GRAD_TOL, (err, key)
+    # the discarded unet.outc gets no gradient, as in the reference
+    assert set(gref) == {k for k, p in named.items() if p.grad is not None}
+    bufs = dict(net.named_buffers())
+    for k, v in _sd(z, f"{tag}/after").items():
+        assert max_abs(bufs[k].float(), v.float()) <= ACT_TOL, k
+
+
+@pytest.mark.parametrize("tag", ["s64", "s45"])
+def test_probunet_samples_and_eval_match_reference_g3(tag, dev):
+    z = _g3()
+    net = _net(dev, init=z).train()
+    x = torch.from_numpy(z[f"{tag}/x"]).to(dev)
+    segm = torch.from_numpy(z[f"{tag}/segm"]).to(dev)
+    net.forward(x, segm, training=True)
+    eps_prior = torch.from_numpy(z[f"{tag}/eps_prior"]).to(dev)
+    ref = torch.from_numpy(z[f"{tag}/samples"])
+    with torch.no_grad():
+        d = net.prior_latent_space
+        zs = d.base_dist.loc + d.base_dist.scale * eps_prior           # (S, N, L)
+        one = torch.stack([net.fcomb.forward(net.unet_features, zs[s]) for s in range(zs.shape[0])])
+        many = net.fcomb.forward_samples(net.unet_features, zs)      # fused S-sample pass
+    assert max_abs(one, ref) <= ACT_TOL
+    assert max_abs(many, ref) <= ACT_TOL
+    # eval mode: BN running statistics, sample(testing=True)
+    with torch.no_grad():
+        net.eval()
+        net.forward(x, segm, training=False)
+        _inject(net.prior_latent_space, torch.from_numpy(z[f"{tag}/eps_eval"]).to(dev), "sample")
+        y = net.sample(testing=True)
+    assert max_abs(net.prior_latent_space.base_dist.loc, torch.from_numpy(z[f"{tag}/eval_prior_mu"])) <= ACT_TOL
+    assert max_abs(y, torch.from_numpy(z[f"{tag}/eval_sample"])) <= ACT_TOL
+
+
+@pytest.mark.parametrize("N,H,W,F,K,NH", [(2, 64, 64, 64, 3, 3), (3, 45, 37, 64, 3, 3), (1, 20, 13, 32, 1, 2),
+                                          (2, 16, 16, 8, 5, 1)])
+def test_fcomb_fwd_bwd_vs_fp64_oracle(N, H, W, F, K, NH, dev):
+    """Fcomb alone at trainer width (F=64, 3 hidden layers) and at other legal shapes, including
+    pixel counts that are not tile multiples; forward and every gradient vs float64 torch."""
+    from model.probabilistic_unet.probabilistic_unet import Fcomb
+    torch.manual_seed(5)
+    fc = Fcomb([F], 6, 1, K, NH + 1, {"w": "orthogonal", "b": "normal"}).to(dev)
+    with torch.no_grad():
+        for p in fc.parameters():
+            if p.dim() == 1:
+                p.normal_(0, 0.1)
+    g = torch.Generator().manual_seed(6)
+    feat = torch.relu(torch.randn(N, F, H, W, generator=g)).to(dev).contiguous(memory_format=torch.channels_last)
+    zl = torch.randn(N, 6, generator=g).to(dev)
+    feat.requires_grad_(True)
+    zl.requires_grad_(True)
+    y = fc.forward(feat, zl)
+    dy = torch.randn(y.shape, generator=g).to(dev)
+    (y * dy).sum().backward()
+    torch.cuda.synchronize()
+    # float64 reference on the CPU with autograd
+    from oracle.probunet_ref import fcomb_forward
+    sd = {"fcomb." + k: v.detach().cpu().double().requires_grad_(True) for k, v in fc.state_dict().items()}
+    f64 = feat.detach().cpu().double().requires_grad_(True)
+    z64 = zl.detach().cpu().double().requires_grad_(True)
+    yr = fcomb_forward(sd, f64, z64, NH + 1)
+    (yr * dy.cpu().double()).sum().backward()
+    assert max_abs(y, yr) <= 1e-4 * max(1.0, float(yr.abs().max()))
+    assert max_abs(feat.grad, f64.grad) <= 1e-4 * max(1.0, float(f64.grad.abs().max()))
+    assert max_abs(zl.grad, z64.grad) <= 1e-4 * max(1.0, float(z64.grad.abs().max()))
+    got = {k: p.grad for k, p in fc.named_parameters()}
+    ref = {k[6:]: v.grad for k, v in sd.items()}
+    err, key = grad_err(got, ref)
+    assert err <= 1e-4, (err, key)
+
+
+def test_probunet_full_width_vs_oracle(dev):
+    """ProbUNetTrainer architecture ([64..1024], 3 classes, no_convs_fcomb=4, beta=10) at 64x48, N=2:
+    loss and all 68.78M gradients vs the fp32 CPU oracle."""
+    from oracle.probunet_ref import probunet_param_keys, probunet_train_step
+    torch.manual_seed(0)
+    net = _net(dev, num_filters=(64, 128, 256, 512, 1024)).train()
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    g = torch.Generator().manual_seed(7)
+    N, H, W = 2, 64, 48
+    x = torch.rand(N, 1, H, W, generator=g)
+    segm = torch.randint(0, 3, (N, 1, H, W), generator=g).float()
+    eps = torch.randn(N, 6, generator=g)
+    res, gref = probunet_train_step(sd, x, segm, eps, 5, 6, 3, 4, 10.0)
+    net.forward(x.to(dev), segm.to(dev), training=True)
+    _inject(net.posterior_latent_space, eps.to(dev), "rsample")
+    elbo = net.elbo(segm.to(dev))
+    (-elbo).backward()
+    torch.cuda.synchronize()
+    assert abs(float(-elbo) - float(res["loss"])) <= LOSS_RTOL * abs(float(res["loss"]))
+    assert max_abs(net.reconstruction, res["rec"]) <= 5 * ACT_TOL
+    named = dict(net.named_parameters())
+    keys = [k for k in probunet_param_keys(sd) if not k.startswith("unet.outc")]
+    err, key = grad_err({k: named[k].grad for k in keys}, {k: gref[k] for k in keys})
+    assert err <= 2 * GRAD_TOL, (err, key)
+
+
+def test_probunet_flat_grad_buffer(dev):
+    """All gradients of one backward land in the model's single flat buffer (one all-reduce)."""
+    from pmu_hip.functions import flat_grad_buffer
+    net = _net(dev).train()
+    x = torch.rand(2, 1, 32, 32, device=dev)
+    segm = torch.randint(0, 3, (2, 1, 32, 32), device=dev).float()
+    net.forward(x, segm, training=True)
+    (-net.elbo(segm)).backward()
+    buf = flat_grad_buffer(net)
+    lo, hi = buf.data_ptr(), buf.data_ptr() + buf.numel() * 4
+    for k, p in net.named_parameters():
+        if p.grad is not None:
+            assert lo <= p.grad.data_ptr() < hi, k
