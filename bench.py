@@ -63,7 +63,7 @@ class KernelTimer:
     """HIP-event timing of every launch, with algorithmic FLOPs for the MFMA kernels."""
 
     MFMA = ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad", "pmu_convT2x2_fwd",
-            "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad")
+            "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd")
 
     def __init__(self):
         self.rec = []
@@ -92,7 +92,7 @@ class KernelTimer:
             a = args[5]._obj
             cin = sum(a.src[i].C for i in range(a.nsrc))
             return 2.0 * a.N * a.H * a.W * cin * args[6] * 4
-        return 0.0
+        return fcomb_flops(name, args)
 
     def __call__(self, name, args, e0, e1):
         self.rec.append((name, self._flops(name, args), e0, e1))
@@ -109,63 +109,71 @@ class KernelTimer:
         return per
 
 
-def cpu_baseline(max_seconds=25.0):
-    """CPU oracle (torch-CPU restatement of the reference) on a bounded sample: batch 2 of the c2
-    geometry, 1 warm-up + timed steps (fwd+bwd+clip+SGD) until ~max_seconds."""
-    from oracle.unet_ref import unet_train_step
-    from model import UNet
+def cpu_baseline(max_seconds=25.0, workload="unet"):
+    """CPU oracle (torch-CPU restatement of the reference) on a bounded sample: batch 2 of the
+    bench geometry, 1 warm-up + timed steps until ~max_seconds (at most 5)."""
+    from oracle.unet_ref import unet_param_keys, unet_train_step
+    from oracle.probunet_ref import probunet_train_step
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    sd = {k: v.clone() for k, v in UNet(1, 1, FILTERS).state_dict().items()}
     g = torch.Generator().manual_seed(1)
     B = 2
     x = torch.rand(B, 1, 256, 256, generator=g)
-    t = (torch.rand(B, 1, 256, 256, generator=g) > 0.5).float()
-    from oracle.unet_ref import unet_param_keys
-    bufs = {k: torch.zeros_like(sd[k]) for k in unet_param_keys(sd)}
-    unet_train_step(sd, x, t, 5, 1, lr=1e-3, bufs=bufs)  # warm-up
+    if workload == "unet":
+        from model import UNet
+        sd = {k: v.clone() for k, v in UNet(1, 1, FILTERS).state_dict().items()}
+        t = (torch.rand(B, 1, 256, 256, generator=g) > 0.5).float()
+        bufs = {k: torch.zeros_like(sd[k]) for k in unet_param_keys(sd)}
+
+        def one():
+            unet_train_step(sd, x, t, 5, 1, lr=1e-3, bufs=bufs)
+        what = "fwd+bwd+clip+SGD steps"
+    else:
+        from model import ProbabilisticUnet
+        net = ProbabilisticUnet(1, 3, FILTERS, latent_dim=6, no_convs_fcomb=4, beta=10.0)
+        sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+        del net
+        segm = torch.randint(0, 3, (B, 1, 256, 256), generator=g).float()
+        eps = torch.randn(B, 6, generator=g)
+
+        def one():
+            probunet_train_step(sd, x, segm, eps, 5, 6, 3, 4, 10.0)
+        what = "ProbabilisticUnet fwd+elbo+bwd steps (no optimizer, no eval samples)"
+    one()  # warm-up
     times = []
     t_end = time.perf_counter() + max_seconds
     while True:
         t0 = time.perf_counter()
-        unet_train_step(sd, x, t, 5, 1, lr=1e-3, bufs=bufs)
+        one()
         times.append(time.perf_counter() - t0)
         if time.perf_counter() > t_end or len(times) >= 5:
             break
     times.sort()
     med = times[len(times) // 2]
     return {"value": round(B / med, 4), "unit": "slices/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/unet_ref.py torch-CPU, c2 geometry (256x256x1, filters {FILTERS}), batch {B}, "
-                      f"median of {len(times)} fwd+bwd+clip+SGD steps after 1 warm-up, {threads} threads"}
+            "sample": f"oracle/{'unet' if workload == 'unet' else 'probunet'}_ref.py torch-CPU, 256x256x1, "
+                      f"filters {FILTERS}, batch {B}, median of {len(times)} {what} after 1 warm-up, "
+                      f"{threads} threads"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--classes", type=int, default=1)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true")
-    args = ap.parse_args()
+def fcomb_flops(name, args):
+    """MACs the fused Fcomb kernels execute (z folded into a bias, so layer 1 is F x F per pixel)."""
+    if name == "pmu_fcomb_fwd":
+        F_, K, NH, S, N, H, W = args[6], args[8], args[9], args[10], args[11], args[12], args[13]
+        return 2.0 * N * H * W * (F_ * F_ + S * ((NH - 1) * F_ * F_ + F_ * K))
+    if name == "pmu_fcomb_bwd":
+        F_, K, NH, N, H, W = args[8], args[10], args[11], args[12], args[13], args[14]
+        return 2.0 * N * H * W * (3 * NH * F_ * F_ + 2 * F_ * K)
+    return 0.0
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
 
+def build_unet(args, dev, world, rank):
+    """c2: UNet fwd + loss + bwd + (all-reduce) + fused clip/SGD on one batch of slices."""
     from model import UNet
-    from pmu_hip import _lib as L
     from pmu_hip.functions import flat_grad_buffer
     from pmu_hip.optim import FusedSGD
-
+    import torch.distributed as dist
     torch.manual_seed(0)
     net = UNet(1, args.classes, FILTERS).to(dev).train()
     if world > 1:  # identical replicas: broadcast rank 0's weights
@@ -194,6 +202,91 @@ def main():
         opt.step(grad_scale=1.0 / world)
         return loss
 
+    flops = conv_flops_per_slice(S, S, FILTERS, 1, args.classes) * B
+    config = {"workload": "c2: UNet(n_channels=1, n_classes=%d, num_filters=%s), %dx%dx1 slices, "
+                          "fwd+BCE+bwd+clip(0.1)+SGD(0.9) per step" % (args.classes, FILTERS, S, S),
+              "global_batch": B * world, "per_gpu_batch": B, "image": [S, S], "parallelism": f"dp{world}"}
+    data = "synthetic (x~U[0,1), random binary masks, seeded)"
+    return step, flops, config, data
+
+
+def build_probunet(args, dev, world, rank):
+    """c4: one ProbUNetTrainer training step (probunet_trainer.py:27-39 + train.py:85-110):
+    forward(training=True) -> sample() (the trainer's predict) -> -elbo (CE-sum + beta*KL) ->
+    backward -> (all-reduce) -> clip+SGD, then the evaluation sweep: 16 prior samples through
+    Fcomb in one fused pass + per-class Dice counts of every sample."""
+    from model import ProbabilisticUnet
+    from pmu_hip.functions import flat_grad_buffer
+    from pmu_hip.metrics import dice_counts
+    from pmu_hip.optim import FusedSGD
+    import torch.distributed as dist
+    torch.manual_seed(0)
+    n_cls = 3
+    net = ProbabilisticUnet(input_channels=1, num_classes=n_cls, num_filters=FILTERS, latent_dim=6,
+                            no_convs_fcomb=4, beta=10.0).to(dev).train()
+    if world > 1:
+        for t in list(net.parameters()) + list(net.buffers()):
+            dist.broadcast(t.data, 0)
+    opt = FusedSGD(net.parameters(), lr=1e-3, momentum=0.9, clip=0.1)
+    g = torch.Generator(device="cpu").manual_seed(1 + rank)
+    B, S = args.batch, args.size
+    x = torch.rand(B, 1, S, S, generator=g).to(dev)
+    segm = torch.randint(0, n_cls, (B, 1, S, S), generator=g).float().to(dev)
+    plist = list(net.parameters())
+    n_samples = 16
+
+    def step():
+        for p in plist:
+            p.grad = None
+        net.forward(x, segm, training=True)
+        net.sample(testing=False)
+        loss = -net.elbo(segm)
+        loss.backward()
+        if world > 1:
+            dist.all_reduce(flat_grad_buffer(net, plist))
+        opt.step(grad_scale=1.0 / world)
+        with torch.no_grad():
+            ys = net.sample_many(n_samples)                  # (16, B, 3, S, S)
+            for s_ in range(n_samples):
+                dice_counts(ys[s_], segm, n_cls)
+        return loss
+
+    config = {"workload": "c4: ProbabilisticUnet(1, 3, %s, latent_dim=6, no_convs_fcomb=4, beta=10), %dx%dx1 "
+                          "slices; train step (fwd, prior sample, -elbo, bwd, clip+SGD) + 16 fcomb samples + Dice"
+                          % (FILTERS, S, S),
+              "global_batch": B * world, "per_gpu_batch": B, "image": [S, S], "parallelism": f"dp{world}"}
+    data = "synthetic (x~U[0,1), random 3-class masks, seeded)"
+    return step, None, config, data
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--classes", type=int, default=1)
+    ap.add_argument("--workload", choices=["unet", "probunet"], default="unet")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from pmu_hip import _lib as L
+
+    build = build_unet if args.workload == "unet" else build_probunet
+    step, flops_step, config, data = build(args, dev, world, rank)
+    B = args.batch
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -215,7 +308,6 @@ def main():
     ms = dt / args.steps * 1e3
     value = world * B * args.steps / dt
 
-    flops_step = conv_flops_per_slice(S, S, FILTERS, 1, args.classes) * B
     roof = None
     kernels = None
     if not args.no_kernel_timing:
@@ -233,19 +325,18 @@ def main():
                 "launches": n, "avg_launch_ms": round(t / n * 1e3, 4), "flops_per_launch": fl / n}
         kernels = {k: {"launches": v[0], "ms": round(v[2] * 1e3, 3),
                        "tflops": (round(v[1] / v[2] / 1e12, 2) if v[1] else None)} for k, v in sorted(per.items())}
+        if flops_step is None:   # algorithmic FLOPs of the step = those of the MFMA kernels it launches
+            flops_step = sum(v[1] for v in per.values())
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline()
+        cpu = cpu_baseline(workload=args.workload)
     if rank == 0:
         res = {
             "metric": METRIC, "value": round(value, 3), "unit": "slices/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (x~U[0,1), random binary masks, seeded)",
-            "config": {"workload": "c2: UNet(n_channels=1, n_classes=%d, num_filters=%s), %dx%dx1 slices, "
-                                   "fwd+BCE+bwd+clip(0.1)+SGD(0.9) per step" % (args.classes, FILTERS, S, S),
-                       "global_batch": B * world, "per_gpu_batch": B, "image": [S, S], "parallelism": f"dp{world}"},
-            "step_tflops": round(flops_step / (ms * 1e-3) / 1e12, 2),
-            "step_mfma_frac": round(flops_step / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4),
+            "vs_baseline": None, "dtype": "fp32", "data": data, "config": config,
+            "step_tflops": round(flops_step / (ms * 1e-3) / 1e12, 2) if flops_step else None,
+            "step_mfma_frac": round(flops_step / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4) if flops_step else None,
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "loss": float(loss),
         }
         print(json.dumps(res), flush=True)
