@@ -177,6 +177,34 @@ int pmu_sgd_clip(const pmu_sgd_chunk* chunks, int nchunks, void* const* ptrs, fl
 int pmu_dice_counts(const float* y, const float* mask, int N, int K, int H, int W,
                     double* counts, void* stream);
 
+/* (sum a*b, sum a, sum b) over n elements into out[3] (fp64): dice_coeff's three sums
+ * (PMU/dice_loss.py:5-12) for arbitrary pred/target tensors. */
+int pmu_dice_sums(const float* a, const float* b, long long n, double* out, void* stream);
+
+/* ---- multi-planar slicer (PMU/utils/mri_dataset.py:11-143) --------------------------------
+ * A scan vol [d0][d1][d2] (f64) is re-laid out per view into a padded p0 x p1 x p2 frame
+ * (pad_dimensions :85-98 = zeros at the end of the argmin axis) so each slice is contiguous:
+ *   view 0: out[i][j][k] (slice = image[i,:,:]),  view 1: out[j][i][k] (image[:,j,:]),
+ *   view 2: out[k][i][j] (image[:,:,k])            (sample_slice :70-82). */
+int pmu_slice_view_layout(const double* vol, int d0, int d1, int d2, int p0, int p1, int p2, int view,
+                          double* out, void* stream);
+/* out[s] = max over the px elements of slice s (preprocess' max :109-110, index-map filter :45-46). */
+int pmu_slice_max(const double* slices, int nslices, long long px, double* out, void* stream);
+/* Batch assembly from a device slice table: addr[g] = device address of f64 slice g (px elements),
+ * maxv[g] its max.  out[b][:] = float(slice[ids[b]] / maxv[ids[b]]) when normalize and the max is
+ * non-zero, else float(value) (preprocess :101-112 then .float() :142).  ids: device [B]. */
+int pmu_gather_slices(const long long* addr, const double* maxv, const int* ids, int B, long long px,
+                      int normalize, float* out, void* stream);
+
+/* ---- 3-view volume fusion (PMU/eval.py:157-203) --------------------------------------------
+ * v0 [D0][C][D1][D2], v1 [D1][C][D0][D2], v2 [D2][C][D0][D1]: the per-view stacks of slice
+ * predictions (probabilities; logits=1 applies softmax over C first).  In the view-0 frame:
+ * avg = (p0 + p1 + p2) / 3 (optional output, [D0][C][D1][D2]), label = first argmax of avg
+ * (optional, int32 [D0][D1][D2]), and counts[4][C][3] = exact (intersection, |pred|, |truth|) of the
+ * one-hot argmax of view 0, view 1, view 2 and avg vs truth [D0][D1][D2] == c.  C <= 8. */
+int pmu_fuse3view(const float* v0, const float* v1, const float* v2, const float* truth, int D0, int D1,
+                  int D2, int C, int logits, float* avg, int* label, double* counts, void* stream);
+
 /* ---- probabilistic path: latent head of AxisAlignedConvGaussian ---------------------------
  * probabilistic_unet.py:95-108: encoding = mean_{h,w} relu(bn(z_last)); mu_log_sigma = conv1x1(encoding). */
 /* out[N][C] = (1/(H*W)) sum_{h,w} max(0, z*scale+shift), z NHWC, coef = [scale|shift]. */

@@ -79,6 +79,13 @@ SIGNATURES = {
     "pmu_wgrad1x1": (c_int, [c_void_p, _FP, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_sgd_clip": (c_int, [c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_void_p]),
     "pmu_dice_counts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_dice_sums": (c_int, [c_void_p, c_void_p, c_longlong, c_void_p, c_void_p]),
+    "pmu_slice_view_layout": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                      c_void_p]),
+    "pmu_slice_max": (c_int, [c_void_p, c_int, c_longlong, c_void_p, c_void_p]),
+    "pmu_gather_slices": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_longlong, c_int, c_void_p, c_void_p]),
+    "pmu_fuse3view": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                              c_void_p, c_void_p, c_void_p]),
     "pmu_spatial_mean": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_spatial_mean_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_linear_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -1,0 +1,41 @@
+"""UNetTrainer — drop-in for PMU/trainer/unet_trainer.py:10-129.
+
+Same constructor, attributes (device, name, mask_type, net, criterion) and methods.  The net runs
+on the HIP path (model.UNet); the loss is the reference's own nn.BCELoss / nn.CrossEntropyLoss
+(row a6); eval's per-class Dice comes from one fused argmax+count kernel (pmu_hip.metrics).
+"""
+import torch
+import torch.nn as nn
+
+from model import UNet
+from pmu_hip.metrics import trainer_dice
+
+from .trainer import Trainer, load_checkpoint, masks_to_rgb
+
+
+class UNetTrainer(Trainer):
+
+    def __init__(self, device, n_channels=1, n_classes=1, load_model=None):
+        self.device = device
+        self.name = "unet"
+        self.mask_type = torch.float32 if n_classes == 1 else torch.long
+        self.net = UNet(n_channels=n_channels, n_classes=n_classes)
+        if load_model is not None:
+            load_checkpoint(self.net, load_model, device)
+        self.net = self.net.to(device)
+        self.criterion = nn.BCELoss() if self.net.n_classes == 1 else nn.CrossEntropyLoss()
+
+    def predict(self, imgs, true_masks):
+        return self.net(imgs)
+
+    def loss(self, imgs, true_masks, masks_pred):
+        if self.net.n_classes > 1:
+            return self.criterion(masks_pred, true_masks.squeeze(1))
+        return self.criterion(masks_pred, true_masks)
+
+    def eval(self, imgs, true_masks, masks_pred):
+        """[dice] for 1 class, else Dice of classes 1..K-1 of the softmax-argmax one-hot (:52-98)."""
+        return trainer_dice(masks_pred, true_masks, self.net.n_classes)
+
+    def mask_to_image(self, masks, prediction=False):
+        return masks_to_rgb(masks, self.net.n_classes, prediction)

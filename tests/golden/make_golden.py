@@ -252,11 +252,65 @@ def g5_slicer(nib):
     np.savez_compressed(os.path.join(OUT, "g5_slicer.npz"), **out)
 
 
+def g6_fusion():
+    """3-view fusion (eval.py:157-203).  eval.py does not parse (:137-138); the fixture comes from
+    the build's own restatement of its flow (oracle/data_ref.py: per-slice softmax :157, per-view
+    volumes with the :182/:188 permutes, 3-view average :193, per-class Dice of the argmax one-hot
+    :42-49), with the Dice itself computed by the reference's importable dice_loss.dice_coeff.
+    Parity of this row is therefore pinned by the restatement, not by running eval.py."""
+    import dice_loss
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from oracle.data_ref import fuse
+    out = {}
+    g = torch.Generator().manual_seed(6)
+    for tag, (D0, D1, D2) in {"cube": (16, 16, 16), "box": (10, 12, 9)}.items():
+        C = 3
+        truth = torch.randint(0, C, (D0, D1, D2), generator=g).float()
+        logits = [torch.randn(n, C, a, b, generator=g) * 2.0 for n, a, b in ((D0, D1, D2), (D1, D0, D2), (D2, D0, D1))]
+        probs = [torch.softmax(lg, dim=1) for lg in logits]          # per-slice softmax over C
+        vols = fuse(*probs)
+        out[f"{tag}/truth"] = truth.numpy()
+        for v in range(3):
+            out[f"{tag}/logits{v}"] = logits[v].numpy()
+            out[f"{tag}/probs{v}"] = probs[v].numpy()
+        out[f"{tag}/avg"] = vols[3].numpy()
+        out[f"{tag}/label"] = torch.argmax(vols[3], 1).numpy().astype(np.int32)
+
+        def class_dice(vol, k):
+            idx = torch.argmax(vol, 1, keepdim=True)
+            one_hot = torch.zeros(vol.shape).scatter_(1, idx, 1)   # contiguous, as eval.py:44-46
+            return dice_loss.dice_coeff(one_hot[:, k], (truth == k).float()).item()
+        out[f"{tag}/dice"] = np.array([[class_dice(vol, k) for k in (1, 2)] for vol in vols])
+    np.savez_compressed(os.path.join(OUT, "g6_fusion.npz"), **out)
+
+
+def g7_dp_accumulation():
+    """Gradient accumulation of train.py:85-110 on config c1: UNet(1,1,[16,32]), 8 micro-batches
+    of 4 slices at 64x64, loss / 8 per micro-batch, summed into one gradient — what data-parallel
+    ranks must reproduce with a SUM all-reduce."""
+    from model import UNet
+    torch.manual_seed(0)
+    net = UNet(1, 1, [16, 32])
+    out = sd_np("init", net.state_dict())
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(32, 1, 64, 64, generator=g)
+    t = (torch.rand(32, 1, 64, 64, generator=g) > 0.5).float()
+    out["x"], out["t"] = x.numpy(), t.numpy()
+    net.train()
+    crit = nn.BCELoss()
+    acc = 8
+    for i in range(acc):
+        loss = crit(net(x[4 * i:4 * i + 4]), t[4 * i:4 * i + 4]) / acc
+        loss.backward()
+    out.update(grads_np("grad", net))
+    np.savez_compressed(os.path.join(OUT, "g7_dp.npz"), **out)
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit(f"reference not found at {REF}: fixtures are generated in the build container only")
     nib = install_shims()
-    which = set(sys.argv[1:]) or {"g1", "g2", "g3", "g4", "g5"}
+    which = set(sys.argv[1:]) or {"g1", "g2", "g3", "g4", "g5", "g6", "g7"}
     if "g1" in which:
         g1_unet_c1()
     if "g2" in which:
@@ -267,6 +321,10 @@ def main():
         g4_dice()
     if "g5" in which:
         g5_slicer(nib)
+    if "g6" in which:
+        g6_fusion()
+    if "g7" in which:
+        g7_dp_accumulation()
     print("golden fixtures written to", OUT)
 
 

@@ -1,0 +1,176 @@
+"""GPU parity of the data-side rows and the drop-in loops.
+
+  * slicer (a13): MRI_Dataset on resident scans vs the reference's G5 items — bit-exact;
+    at 256^3 vs the oracle restatement on the same volume — bit-exact;
+  * Dice (a8): dice_coeff and the trainers' eval vs the reference's G4 — bit-exact;
+  * fusion (a14): pmu_fuse3view vs G6 (probabilities in: average, label map and Dice bit-exact;
+    logits in: softmax inside the kernel, labels equal up to fp32 ties) and at 128^3 vs the
+    restatement;
+  * train_net / predict_volume run end to end on a synthetic scan set.
+"""
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def _g5_dataset(filt, dev):
+    from utils.mri_dataset import MRI_Dataset
+    z = _load("g5_slicer.npz")
+    names = sorted({k.split("/")[1] for k in z.files if k.startswith("vol/")})
+    store = {n: (z[f"vol/{n}/img"], z[f"vol/{n}/lab"]) for n in names}
+
+    def loader(p):
+        return store[os.path.basename(p)][0 if "imgs" in p else 1]
+    return z, MRI_Dataset("/imgs", "/labs", 3, filter=filt, loader=loader, files=names, device=dev)
+
+
+@pytest.mark.parametrize("filt", [True, False])
+def test_slicer_matches_reference_g5(filt, dev):
+    z, ds = _g5_dataset(filt, dev)
+    key = "filt" if filt else "all"
+    assert tuple(ds.image_dims) == tuple(z[f"{key}/image_dims"])
+    assert np.array_equal(np.array(ds.index_map), z[f"{key}/index_map"])
+    assert len(ds) == len(z[f"{key}/images"])
+    imgs = np.stack([ds[i]["image"].cpu().numpy() for i in range(len(ds))])
+    masks = np.stack([ds[i]["mask"].cpu().numpy() for i in range(len(ds))])
+    assert np.array_equal(imgs, z[f"{key}/images"])      # bit-exact, incl. the f64 max normalisation
+    assert np.array_equal(masks, z[f"{key}/masks"])
+    # a batched gather equals the items
+    b = ds.get_batch(list(range(min(5, len(ds)))))
+    assert np.array_equal(b["image"].cpu().numpy(), imgs[:5])
+
+
+def test_slicer_full_size_vs_oracle(dev):
+    """A 256x256x200 scan (padded along axis 2) with a spherical mask: every 7th slice of every
+    view, gathered in batches, vs the numpy restatement — bit-exact."""
+    from oracle.data_ref import build_dataset
+    from utils.mri_dataset import MRI_Dataset
+    g = np.random.default_rng(11)
+    img = g.random((256, 256, 200)) * 1000.0
+    ii, jj, kk = np.meshgrid(np.arange(256), np.arange(256), np.arange(200), indexing="ij")
+    lab = ((ii - 128) ** 2 + (jj - 120) ** 2 + (kk - 90) ** 2 < 60 ** 2).astype(np.float64)
+    lab[(ii - 128) ** 2 + (jj - 120) ** 2 + (kk - 90) ** 2 < 25 ** 2] = 2.0
+    ds = MRI_Dataset("/imgs", "/labs", 3, filter=True, loader=lambda p: img if "imgs" in p else lab, files=["s"],
+                     device=dev)
+    dims, imap, items = build_dataset([(img, lab)], True)
+    assert ds.index_map == [tuple(t) for t in imap] and tuple(ds.image_dims) == tuple(dims)
+    sel = list(range(0, len(ds), 7))
+    for s0 in range(0, len(sel), 16):
+        chunk = sel[s0:s0 + 16]
+        b = ds.get_batch(chunk)
+        want_i = np.stack([items[i][0] for i in chunk])
+        want_m = np.stack([items[i][1] for i in chunk])
+        assert np.array_equal(b["image"].cpu().numpy(), want_i)
+        assert np.array_equal(b["mask"].cpu().numpy(), want_m)
+
+
+def test_dice_matches_reference_g4(dev):
+    from dice_loss import dice_coeff
+    from trainer import UNetTrainer
+    z = _load("g4_dice.npz")
+    for k in ("rand", "empty", "ones", "disjoint"):
+        d = dice_coeff(torch.from_numpy(z[f"{k}/pred"]).to(dev), torch.from_numpy(z[f"{k}/target"]).to(dev))
+        assert np.float32(d.item()) == np.float32(z[f"{k}/dice"]), k
+    tr = UNetTrainer.__new__(UNetTrainer)
+    tr.device = dev
+    tr.net = types.SimpleNamespace(n_classes=3)
+    got = tr.eval(None, torch.from_numpy(z["mc/mask"]).to(dev), torch.from_numpy(z["mc/y"]).to(dev))
+    assert np.array_equal(got.astype(np.float32), z["mc/dice"].astype(np.float32))
+    tr.net = types.SimpleNamespace(n_classes=1)
+    got = tr.eval(None, torch.from_numpy(z["bin/mask"]).to(dev), torch.from_numpy(z["bin/y"]).to(dev))
+    assert np.array_equal(got.astype(np.float32), z["bin/dice"].astype(np.float32))
+
+
+@pytest.mark.parametrize("tag", ["cube", "box"])
+def test_fusion_matches_g6(tag, dev):
+    from pmu_hip.fusion import fuse_views
+    z = _load("g6_fusion.npz")
+    truth = torch.from_numpy(z[f"{tag}/truth"]).to(dev)
+    probs = [torch.from_numpy(z[f"{tag}/probs{v}"]).to(dev) for v in range(3)]
+    r = fuse_views(*probs, truth)
+    assert np.array_equal(r["avg"].cpu().numpy(), z[f"{tag}/avg"])              # bit-exact average
+    assert np.array_equal(r["label"].cpu().numpy(), z[f"{tag}/label"])          # bit-exact label map
+    assert np.array_equal(r["dice"][:, 1:3].cpu().numpy(), z[f"{tag}/dice"].astype(np.float32))
+    logits = [torch.from_numpy(z[f"{tag}/logits{v}"]).to(dev) for v in range(3)]
+    r2 = fuse_views(*logits, truth, logits=True)
+    assert float((r2["avg"] - r["avg"]).abs().max()) <= 1e-6
+    mism = int((r2["label"] != r["label"]).sum())
+    assert mism <= 1, mism      # softmax inside the kernel: identical up to fp32 near-ties
+
+
+def test_fusion_large_vs_restatement(dev):
+    """128 x 120 x 100 volume, 3 classes, probabilities in: vs the torch restatement on the CPU (the
+    reference's arithmetic: torch's GPU `/ 3.0` multiplies by the reciprocal instead of dividing)."""
+    from oracle.data_ref import fuse
+    from pmu_hip.fusion import fuse_views
+    g = torch.Generator(device="cpu").manual_seed(12)
+    D0, D1, D2, C = 128, 120, 100, 3
+    st = [torch.softmax(torch.randn(n, C, a, b, generator=g), 1).to(dev)
+          for n, a, b in ((D0, D1, D2), (D1, D0, D2), (D2, D0, D1))]
+    truth = torch.randint(0, C, (D0, D1, D2), generator=g).float().to(dev)
+    r = fuse_views(*st, truth)
+    vols = [v.to(dev) for v in fuse(*[t.cpu() for t in st])]
+    assert torch.equal(r["avg"], vols[3])
+    lab = torch.argmax(vols[3], 1).int()
+    assert torch.equal(r["label"], lab)
+    for v in range(4):
+        am = torch.argmax(vols[v], 1)
+        for c in range(C):
+            inter = float(((am == c) & (truth == c)).sum())
+            assert float(r["counts"][v, c, 0]) == inter
+            assert float(r["counts"][v, c, 1]) == float((am == c).sum())
+            assert float(r["counts"][v, c, 2]) == float((truth == c).sum())
+
+
+def _synthetic_scans(n, shape, seed):
+    g = np.random.default_rng(seed)
+    out = {}
+    for s in range(n):
+        img = g.random(shape) * 100.0
+        ii, jj, kk = np.meshgrid(*[np.arange(d) for d in shape], indexing="ij")
+        r2 = (ii - shape[0] / 2) ** 2 + (jj - shape[1] / 2) ** 2 + (kk - shape[2] / 2) ** 2
+        lab = np.zeros(shape)
+        lab[r2 < (min(shape) / 3) ** 2] = 1.0
+        lab[r2 < (min(shape) / 6) ** 2] = 2.0
+        out[f"scan{s}.nii"] = (img, lab)
+    return out
+
+
+def test_train_net_and_predict_volume_end_to_end(dev, tmp_path):
+    """train.py's train_net (1 epoch, batch 8 -> 4 micro-batches of 2, clip+SGD, validation Dice,
+    checkpoints) and predict_volume + fusion on a synthetic 16^3 scan set."""
+    import train as train_mod
+    from predict import predict_volume
+    from trainer import UNetTrainer
+    from utils.mri_dataset import MRI_Dataset
+    scans = _synthetic_scans(2, (16, 16, 16), 3)
+    ds = MRI_Dataset("/imgs", "/labs", 3, filter=True, files=sorted(scans),
+                     loader=lambda p: scans[os.path.basename(p)][0 if "imgs" in p else 1], device=dev)
+    torch.manual_seed(0)
+    tr = UNetTrainer(dev, n_channels=1, n_classes=3)
+    train_mod.dir_checkpoint = str(tmp_path) + "/"
+    before = {k: v.clone() for k, v in tr.net.state_dict().items()}
+    train_mod.train_net(tr, dev, epochs=1, batch_size=8, lr=1e-3, val_percent=0.2, dataset=ds)
+    after = tr.net.state_dict()
+    assert any(not torch.equal(before[k], after[k]) for k in before)
+    assert all(torch.isfinite(v.float()).all() for v in after.values())
+    assert os.path.exists(os.path.join(str(tmp_path), "unet_checkpoint0.pt"))
+    res = predict_volume(tr.net, ds, 0, batch_size=8)
+    from oracle.data_ref import class_dice, fuse
+    probs = [torch.softmax(s, 1) for s in res["stacks"]]
+    vols = fuse(*probs)
+    truth = res["truth"]
+    for v in range(4):
+        for k in (1, 2):
+            ref = class_dice(vols[v].cpu(), truth.cpu(), k)
+            assert abs(float(res["dice"][v, k]) - ref) <= 5e-3   # softmax in-kernel: a few fp32 near-ties may flip

@@ -1,0 +1,99 @@
+"""Data-parallel host logic on CPU with the gloo backend, world size 2 (row e).
+
+Each rank computes its round-robin share of the 8 micro-batches of G7 (c1, 4 slices each) with
+loss / (micro-batches per step), as train.py's loop does, and train.allreduce_grads sums them.
+The result must equal the reference's single-process accumulation (tests/golden/g7_dp.npz).
+Both all-reduce paths are exercised: the flat gradient buffer (grads are views of it, as the HIP
+autograd nodes produce them) and the flattened-bucket fallback.  The per-rank gradients here come
+from the CPU oracle: the HIP forward/backward needs a GPU, the all-reduce logic under test does not.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, flat, q):
+    import sys
+    for p in (os.path.join(ROOT, "probabilistic-multiplanar-unet_amd"), ROOT, os.path.dirname(__file__)):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(2)
+        from model import UNet
+        from oracle.unet_ref import unet_forward, unet_loss
+        from pmu_hip.functions import grad_sink_for
+        from train import allreduce_grads, dp_micro_batches, shared_generator
+        z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
+        net = UNet(1, 1, [16, 32])
+        sd = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("init/")}
+        net.load_state_dict(sd)
+        x, t = torch.from_numpy(z["x"]), torch.from_numpy(z["t"])
+        # the 32 samples in order; train.py deals micro-batches of 4 round-robin, 4 per rank per step
+        steps, per_rank = dp_micro_batches(list(range(32)), 4, 8, world, rank)
+        assert len(steps) == 1 and per_rank == 4
+        named = dict(net.named_parameters())
+        plist = list(net.parameters())
+        keys = list(named)
+        params = {k: named[k].detach().clone().requires_grad_(True) for k in keys}
+        work = dict(sd)
+        work.update(params)
+        for mb in steps[0]:
+            idx = torch.tensor(mb)
+            (unet_loss(unet_forward(work, x[idx], 2, 1), t[idx], 1) / (per_rank * world)).backward()
+        if flat:
+            sink = grad_sink_for(net, plist)      # views of the flat buffer, as the HIP nodes write them
+            for k, p in named.items():
+                g = sink.new(p)
+                g.copy_(params[k].grad)
+                p.grad = g
+        else:
+            for k, p in named.items():
+                p.grad = params[k].grad.clone()
+        allreduce_grads(net, plist)
+        # every rank must agree on the generator the loop shuffles with
+        seed = shared_generator().initial_seed()
+        out = {k: p.grad.detach().numpy().copy() for k, p in named.items()}
+        q.put((rank, out, seed, [i for st in steps for mb in st for i in mb]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("flat", [True, False])
+def test_dp_allreduce_matches_reference_accumulation(flat):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, flat, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
+    ref = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("grad/")}
+    from helpers import grad_err
+    for rank, out, _, _ in res:
+        err, key = grad_err({k: torch.from_numpy(out[k]) for k in ref}, ref)
+        assert err <= 1e-5, (rank, err, key)
+    assert res[0][2] == res[1][2]                          # shared shuffle seed
+    assert sorted(res[0][3] + res[1][3]) == list(range(32)) and not set(res[0][3]) & set(res[1][3])
