@@ -84,9 +84,9 @@ class KernelTimer:
         if name == "pmu_convT2x2_fwd":
             f = args[0]._obj
             cin = sum(f.src[i].C for i in range(f.nsrc))
-            return 2.0 * f.N * f.H * f.W * cin * args[3] * 4
+            return 2.0 * f.N * f.H * f.W * cin * args[4] * 4
         if name == "pmu_convT2x2_dgrad":
-            N, H, W, cin, cout = args[6], args[7], args[8], args[9], args[10]
+            N, H, W, cin, cout = args[7], args[8], args[9], args[10], args[11]
             return 2.0 * N * H * W * cin * cout * 4
         if name == "pmu_convT2x2_wgrad":
             a = args[5]._obj
@@ -155,6 +155,35 @@ def cpu_baseline(max_seconds=25.0, workload="unet"):
             "sample": f"oracle/{'unet' if workload == 'unet' else 'probunet'}_ref.py torch-CPU, 256x256x1, "
                       f"filters {FILTERS}, batch {B}, median of {len(times)} {what} after 1 warm-up, "
                       f"{threads} threads"}
+
+
+# C-ABI entry -> device kernel family it launches (rocprof kernel names), for the PMC traffic lookup
+KERNEL_FAMILY = {
+    "pmu_conv3x3_fwd": "conv3x3_kernel<false>", "pmu_conv3x3_dgrad": "conv3x3_kernel<true>",
+    "pmu_conv3x3_wgrad": "wgrad3x3_kernel", "pmu_convT2x2_fwd": "ActRowA", "pmu_convT2x2_dgrad": "DuGatherA",
+    "pmu_convT2x2_wgrad": "convT_wgrad_kernel", "pmu_fcomb_fwd": "fcomb_fwd_kernel", "pmu_fcomb_bwd": "fcomb_bwd_kernel",
+}
+
+
+def pmc_traffic(workload, api):
+    """HBM bytes per launch of ``api``'s kernel family from the newest committed PMC summary
+    (profiles/r*/pmc_traffic_<workload>.json, written by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE passes of this bench command).  None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{workload}.json")))
+    fam = KERNEL_FAMILY.get(api)
+    if not files or fam is None:
+        return None, None
+    data = json.load(open(files[-1]))["kernels"]
+    tot, n = 0.0, 0
+    for k, v in data.items():
+        if fam in k:
+            d = v["dispatches_fetch_pass"]
+            tot += v["hbm_bytes_per_dispatch"] * d
+            n += d
+    if n == 0:
+        return None, None
+    return tot / n, os.path.relpath(files[-1], ROOT)
 
 
 def fcomb_flops(name, args):
@@ -320,9 +349,12 @@ def main():
         dom = max(mf, key=lambda k: mf[k][2])
         n, fl, t = mf[dom]
         ach = fl / t / 1e12
+        traffic, tsrc = pmc_traffic(args.workload, dom)
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TF,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": None,
-                "launches": n, "avg_launch_ms": round(t / n * 1e3, 4), "flops_per_launch": fl / n}
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4),
+                "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "bytes/launch (HBM)",
+                "traffic_source": tsrc, "launches": n, "avg_launch_ms": round(t / n * 1e3, 4),
+                "flops_per_launch": fl / n}
         kernels = {k: {"launches": v[0], "ms": round(v[2] * 1e3, 3),
                        "tflops": (round(v[1] / v[2] / 1e12, 2) if v[1] else None)} for k, v in sorted(per.items())}
         if flops_step is None:   # algorithmic FLOPs of the step = those of the MFMA kernels it launches

@@ -133,12 +133,17 @@ int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int 
 int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream);
 
 /* ---- ConvTranspose2d(k=2, s=2) ---------------------------------------------------- */
-/* u[N][2H][2W][Cout] = convT(act(frame)) + bias, frame is N x H x W x Cin. */
-int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float* bias, int Cout, float* u,
-                     void* stream);
+/* Optional packed weights (wp, pmu_convT2x2_packed_size bytes): k-contiguous B operands for the
+ * pipelined GEMMs (dgrad=0: [ab][co][ci] for the forward, dgrad=1: [ci][ab][co] for dgrad). */
+size_t pmu_convT2x2_packed_size(int Cin, int Cout);
+int pmu_convT2x2_pack(const float* w, int Cin, int Cout, int dgrad, float* wp, void* stream);
+/* u[N][2H][2W][Cout] = convT(act(frame)) + bias, frame is N x H x W x Cin.  wp (nullable) = packed
+ * forward weights; used when the frame is one unpooled BN+ReLU source and Cin%16 == Cout%32 == 0. */
+int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout,
+                     float* u, void* stream);
 /* dx[N][H][W][Cin] from du (NHWC [N][Hd][Wd][Cout], convT output placed at (off_h,off_w)). */
 int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, int off_w, const float* w,
-                       int N, int H, int W, int Cin, int Cout, float* dx, void* stream);
+                       const float* wp, int N, int H, int W, int Cin, int Cout, float* dx, void* stream);
 size_t pmu_convT2x2_wgrad_ws(int N, int H, int W, int Cin, int Cout);
 int pmu_convT2x2_wgrad(const float* du, int Hd, int Wd, int off_h, int off_w,
                        const pmu_frame* act, int Cout, float* dw, float* dbias, float* ws,

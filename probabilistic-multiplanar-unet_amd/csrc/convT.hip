@@ -325,6 +325,177 @@ __global__ void rows_sum_f32_kernel(const float* __restrict__ ws, int R, int Wd,
   out[o] = (float)s;
 }
 
+// ---------------------------------------------------------------------------------
+// Pipelined ConvT forward / dgrad GEMM (the common case: Cin, Cout multiples of 16, the forward
+// operand a single unpooled BN+ReLU source).  128x128x16 tiles, 4 waves of 64x64, double-buffered
+// LDS: the next chunk's global loads are issued before the current chunk's MFMAs and written to
+// the other buffer afterwards, so one barrier per chunk and the load latency hides under MFMAs.
+// Both B operands come pre-packed k-contiguous (pmu_convT2x2_pack):
+//   forward: Bp[n = ab*Cout + co][ci] = W[ci][co][ab]   (N ordered (ab, co): the scatter epilogue
+//            writes 32 consecutive channels of one output pixel per fragment column block)
+//   dgrad  : Bp[ci][k' = ab*Cout + co] = W[ci][co][ab]
+// ---------------------------------------------------------------------------------
+constexpr int PM = 128, PN = 128, PK = 16, PLS = 20;
+
+struct PipeArgs {
+  const float* a;      // fwd: z [M][Cin] (pre-BN);  dgrad: du [N][Hd][Wd][Cout]
+  const float* coef;   // fwd: [scale|shift] of the BN feeding the convT
+  const float* bp;     // packed B [Ncols][K]
+  const float* bias;   // fwd: [Cout]
+  float* out;          // fwd: u [N][2H][2W][Cout];  dgrad: dx [M][Cin]
+  long long M;
+  int Ncols, K;        // GEMM N and K
+  int H, W, Cin, Cout;
+  int Hd, Wd, off_h, off_w;
+};
+
+template <bool DGRAD>
+__global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
+  __shared__ __attribute__((aligned(16))) float As[2][PM * PLS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][PN * PLS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const long long m0 = (long long)blockIdx.x * PM;
+  const int n0 = blockIdx.y * PN;
+  const int hsel = (lane >> 5) * 8;
+  // this thread's two A rows and two B rows (fixed over the K loop), 4 consecutive k each
+  const int kq = (tid & 3) * 4;
+  const int rl0 = tid >> 2, rl1 = rl0 + 64;
+  const bool rok0 = m0 + rl0 < p.M, rok1 = m0 + rl1 < p.M;
+  // A row base: fwd = row start of z; dgrad = du element of (2i, 2j) of the row's pixel, ab added per chunk
+  auto row_base = [&](long long m) -> long long {
+    if constexpr (DGRAD) {
+      const int j = (int)(m % p.W);
+      const long long t = m / p.W;
+      const int i = (int)(t % p.H);
+      const long long n = t / p.H;
+      return ((n * p.Hd + p.off_h + 2 * i) * p.Wd + p.off_w + 2 * j) * p.Cout;
+    } else {
+      return m * p.Cin;
+    }
+  };
+  const long long ab0 = row_base(rok0 ? m0 + rl0 : 0), ab1 = row_base(rok1 ? m0 + rl1 : 0);
+  const float* br0 = p.bp + (long long)(n0 + rl0) * p.K + kq;
+  const float* br1 = p.bp + (long long)(n0 + rl1) * p.K + kq;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float4 ra0, ra1, rb0, rb1;
+  auto load = [&](int k0) {
+    long long off = k0 + kq;
+    if constexpr (DGRAD) {
+      const int ab = k0 / p.Cout;
+      off = ((long long)(ab >> 1) * p.Wd + (ab & 1)) * p.Cout + (k0 - ab * p.Cout) + kq;
+    }
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    ra0 = rok0 ? *reinterpret_cast<const float4*>(p.a + ab0 + off) : z4;
+    ra1 = rok1 ? *reinterpret_cast<const float4*>(p.a + ab1 + off) : z4;
+    rb0 = *reinterpret_cast<const float4*>(br0 + k0);
+    rb1 = *reinterpret_cast<const float4*>(br1 + k0);
+  };
+  auto store = [&](int buf, int k0) {
+    if constexpr (!DGRAD) {  // BN + ReLU of the producer, in registers (rows past M stay zero)
+      const float4 sc = *reinterpret_cast<const float4*>(p.coef + k0 + kq);
+      const float4 sh = *reinterpret_cast<const float4*>(p.coef + p.Cin + k0 + kq);
+      auto f = [&](float4 v) {
+        return make_float4(fmaxf(0.f, fmaf(v.x, sc.x, sh.x)), fmaxf(0.f, fmaf(v.y, sc.y, sh.y)),
+                           fmaxf(0.f, fmaf(v.z, sc.z, sh.z)), fmaxf(0.f, fmaf(v.w, sc.w, sh.w)));
+      };
+      if (rok0) ra0 = f(ra0);
+      if (rok1) ra1 = f(ra1);
+    }
+    *reinterpret_cast<float4*>(&As[buf][rl0 * PLS + kq]) = ra0;
+    *reinterpret_cast<float4*>(&As[buf][rl1 * PLS + kq]) = ra1;
+    *reinterpret_cast<float4*>(&Bs[buf][rl0 * PLS + kq]) = rb0;
+    *reinterpret_cast<float4*>(&Bs[buf][rl1 * PLS + kq]) = rb1;
+  };
+
+  const int nch = p.K / PK;
+  load(0);
+  store(0, 0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nch) load((c + 1) * PK);
+    float av[2][8], bv[2][8];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const float* pa = &As[cur][(wm * 64 + f * 32 + (lane & 31)) * PLS + hsel];
+      const float4 x0 = *reinterpret_cast<const float4*>(pa), x1 = *reinterpret_cast<const float4*>(pa + 4);
+      av[f][0] = x0.x; av[f][1] = x0.y; av[f][2] = x0.z; av[f][3] = x0.w;
+      av[f][4] = x1.x; av[f][5] = x1.y; av[f][6] = x1.z; av[f][7] = x1.w;
+      const float* pb = &Bs[cur][(wn * 64 + f * 32 + (lane & 31)) * PLS + hsel];
+      const float4 y0 = *reinterpret_cast<const float4*>(pb), y1 = *reinterpret_cast<const float4*>(pb + 4);
+      bv[f][0] = y0.x; bv[f][1] = y0.y; bv[f][2] = y0.z; bv[f][3] = y0.w;
+      bv[f][4] = y1.x; bv[f][5] = y1.y; bv[f][6] = y1.z; bv[f][7] = y1.w;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma_f32_32x32x2(av[fm][s], bv[fn][s], acc[fm][fn]);
+    if (c + 1 < nch) store(cur ^ 1, (c + 1) * PK);
+    __syncthreads();
+  }
+  // epilogue
+#pragma unroll
+  for (int fn = 0; fn < 2; ++fn) {
+    const int col = n0 + wn * 64 + fn * 32 + (lane & 31);
+    if constexpr (DGRAD) {
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long m = m0 + wm * 64 + fm * 32 + acc_row(r, lane);
+          if (m < p.M) p.out[m * p.Cin + col] = acc[fm][fn][r];
+        }
+    } else {
+      const int ab = col / p.Cout, co = col - ab * p.Cout;
+      const float b = p.bias ? p.bias[co] : 0.f;
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long m = m0 + wm * 64 + fm * 32 + acc_row(r, lane);
+          if (m < p.M) {
+            const int j = (int)(m % p.W);
+            const long long t = m / p.W;
+            const int i = (int)(t % p.H);
+            const long long n = t / p.H;
+            p.out[((n * 2 * p.H + 2 * i + (ab >> 1)) * (2 * p.W) + 2 * j + (ab & 1)) * p.Cout + co] = acc[fm][fn][r] + b;
+          }
+        }
+    }
+  }
+}
+
+// packed B operands (see above); e over Cin*Cout*4
+__global__ void convT_pack_kernel(const float* __restrict__ w, int Cin, int Cout, int dgrad, float* __restrict__ wp) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long E = 4LL * Cin * Cout;
+  if (e >= E) return;
+  // read-coalesced: e = (ci*Cout + co)*4 + ab
+  const int ab = (int)(e & 3);
+  const long long cc = e >> 2;
+  const int co = (int)(cc % Cout), ci = (int)(cc / Cout);
+  const float v = w[e];
+  if (dgrad) wp[(long long)ci * 4 * Cout + ab * Cout + co] = v;
+  else wp[((long long)ab * Cout + co) * Cin + ci] = v;
+}
+
+static bool pipe_ok_fwd(const pmu_frame* in, int Cout) {
+  const pmu_src& s = in->src[0];
+  return in->nsrc == 1 && s.mode == PMU_SRC_BNRELU && s.pool == PMU_POOL_NONE && s.off_h == 0 && s.off_w == 0 &&
+         s.H == in->H && s.W == in->W && s.C % PK == 0 && Cout % PK == 0 && (4 * Cout) % PN == 0;
+}
+
 static void convT_wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* twl, int* tiles_w, int* tiles_h,
                                  int* ntiles, int* nsplit) {
   *twl = (W > 4) ? 3 : 2;  // 4x8 or 8x4 pixel tiles
@@ -341,14 +512,37 @@ static void convT_wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* tw
 
 }  // namespace
 
-extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float* bias, int Cout, float* u,
-                                void* stream) {
+extern "C" size_t pmu_convT2x2_packed_size(int Cin, int Cout) {
+  return (Cin > 0 && Cout > 0) ? (size_t)4 * Cin * Cout * sizeof(float) : 0;
+}
+
+extern "C" int pmu_convT2x2_pack(const float* w, int Cin, int Cout, int dgrad, float* wp, void* stream) {
+  PMU_REQUIRE(w && wp && Cin > 0 && Cout > 0);
+  const long long E = 4LL * Cin * Cout;
+  hipLaunchKernelGGL(convT_pack_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0, (hipStream_t)stream, w, Cin,
+                     Cout, dgrad, wp);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout,
+                                float* u, void* stream) {
   PMU_REQUIRE(valid_frame(in) && w && u && Cout > 0);
+  const long long M = (long long)in->N * in->H * in->W;
+  if (wp && pipe_ok_fwd(in, Cout)) {
+    PipeArgs p{};
+    p.a = in->src[0].x; p.coef = in->src[0].coef; p.bp = wp; p.bias = bias; p.out = u;
+    p.M = M; p.Ncols = 4 * Cout; p.K = in->src[0].C;
+    p.H = in->H; p.W = in->W; p.Cin = in->src[0].C; p.Cout = Cout;
+    dim3 grid((unsigned)pmu_cdiv(M, PM), (unsigned)(p.Ncols / PN));
+    hipLaunchKernelGGL(convT_pipe_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   ActRowA al{make_dev_frame(in), PixDecode{in->H, in->W}};
   const int Cin = al.f.C;
   WKN_B bl{w, 4 * Cout};
   ScatterEp ep{u, bias, in->H, in->W, Cout, PixDecode{in->H, in->W}};
-  const long long M = (long long)in->N * in->H * in->W;
   const int N = 4 * Cout;
   const long long nch = (Cin + GK - 1) / GK;
   dim3 grid((unsigned)pmu_cdiv(M, GM), (unsigned)pmu_cdiv(N, GN), 1);
@@ -358,14 +552,25 @@ extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float
   return PMU_OK;
 }
 
-extern "C" int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, int off_w, const float* w, int N,
-                                  int H, int W, int Cin, int Cout, float* dx, void* stream) {
+extern "C" int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, int off_w, const float* w,
+                                  const float* wp, int N, int H, int W, int Cin, int Cout, float* dx, void* stream) {
   PMU_REQUIRE(du && w && dx && N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0);
   PMU_REQUIRE(off_h >= 0 && off_w >= 0 && off_h + 2 * H <= Hd && off_w + 2 * W <= Wd);
+  const long long M = (long long)N * H * W;
+  if (wp && Cout % PK == 0 && Cin % PN == 0) {
+    PipeArgs p{};
+    p.a = du; p.bp = wp; p.out = dx;
+    p.M = M; p.Ncols = Cin; p.K = 4 * Cout;
+    p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
+    p.Hd = Hd; p.Wd = Wd; p.off_h = off_h; p.off_w = off_w;
+    dim3 grid((unsigned)pmu_cdiv(M, PM), (unsigned)(Cin / PN));
+    hipLaunchKernelGGL(convT_pipe_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, p);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   DuGatherA al{du, Hd, Wd, off_h, off_w, Cout, PixDecode{H, W}};
   WT_B bl{w, Cout};
   RowEp ep{dx, Cin};
-  const long long M = (long long)N * H * W;
   const long long K = 4LL * Cout;
   dim3 grid((unsigned)pmu_cdiv(M, GM), (unsigned)pmu_cdiv(Cin, GN), 1);
   hipLaunchKernelGGL((gemm_kernel<DuGatherA, WT_B, RowEp>), grid, dim3(256), 0, (hipStream_t)stream, al, bl, ep, M,

@@ -66,9 +66,11 @@ SIGNATURES = {
     "pmu_maxpool2_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                  c_void_p]),
     "pmu_avgpool2_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
-    "pmu_convT2x2_fwd": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
-    "pmu_convT2x2_dgrad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
-                                   c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_packed_size": (c_size_t, [c_int, c_int]),
+    "pmu_convT2x2_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_fwd": (c_int, [_FP, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_dgrad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                   c_int, c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_wgrad_ws": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_convT2x2_wgrad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, _FP, c_int, c_void_p, c_void_p,
                                    c_void_p, c_size_t, c_void_p]),

@@ -238,6 +238,14 @@ def pack_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wp
 
 
+def pack_convT_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """ConvT weights [Cin][Cout][2][2] re-laid out k-contiguous for the pipelined GEMMs (pmu_convT2x2_pack)."""
+    Cin, Cout = w.shape[0], w.shape[1]
+    wp = _empty(L.lib().pmu_convT2x2_packed_size(Cin, Cout) // 4, device=w.device)
+    L.call("pmu_convT2x2_pack", w.data_ptr(), Cin, Cout, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
 # ----------------------------------------------------------------------------------------
 # U-Net
 # ----------------------------------------------------------------------------------------
@@ -312,8 +320,9 @@ def unet_forward(net, x: torch.Tensor, training: bool):
         convT = up.up
         Cup = convT.out_channels
         u = _empty(N, 2 * hi, 2 * wi, Cup, device=dev)
-        L.call("pmu_convT2x2_fwd", frame_of([cur.act()], N, hi, wi), convT.weight.data_ptr(), L.ptr(convT.bias),
-               Cup, u.data_ptr(), L.stream())
+        wpt = pack_convT_weights(convT.weight, dgrad=False)
+        L.call("pmu_convT2x2_fwd", frame_of([cur.act()], N, hi, wi), convT.weight.data_ptr(), wpt.data_ptr(),
+               L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
         dY, dX = hs - 2 * hi, ws_ - 2 * wi
         assert dY >= 0 and dX >= 0, "decoder feature map larger than skip (unsupported by reference too)"
         off = (dY // 2, dX // 2)
@@ -379,8 +388,9 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         Hd, Wd = dup.shape[1], dup.shape[2]
         Cup = convT.out_channels
         dx = _empty(N, hi, wi, Cin_t, device=dev)
-        L.call("pmu_convT2x2_dgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], convT.weight.data_ptr(), N, hi,
-               wi, Cin_t, Cup, dx.data_ptr(), s)
+        wpt = pack_convT_weights(convT.weight, dgrad=True)
+        L.call("pmu_convT2x2_dgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], convT.weight.data_ptr(),
+               wpt.data_ptr(), N, hi, wi, Cin_t, Cup, dx.data_ptr(), s)
         dwt = grads.new(convT.weight)
         dbt = grads.new(convT.bias) if convT.bias is not None else None
         wsb = L.lib().pmu_convT2x2_wgrad_ws(N, hi, wi, Cin_t, Cup)
