@@ -19,8 +19,12 @@
  *   pmu_head1x1_fwd/_bwd, pmu_wgrad1x1   OutConv + sigmoid           unet_parts.py:70-76, unet_model.py:48-49
  *   pmu_sgd_clip         clip_grad_value_(0.1) + SGD(momentum)        PMU/train.py:65,108-110
  *   pmu_dice_counts      dice_coeff + argmax/one-hot                  PMU/dice_loss.py:5-12, trainer/unet_trainer.py:39-58
+ *   pmu_dice_sums        dice_coeff's three sums for arbitrary tensors PMU/dice_loss.py:5-12
  *   pmu_fcomb_*          Fcomb 1x1 chain with tiled z                 probabilistic_unet.py:116-181
  *   pmu_spatial_mean(_bwd) / pmu_linear_*   AxisAlignedConvGaussian head  probabilistic_unet.py:95-108
+ *   pmu_slice_view_layout / pmu_slice_max / pmu_gather_slices
+ *                        MRI_Dataset pad_dimensions/sample_slice/preprocess  PMU/utils/mri_dataset.py:70-112
+ *   pmu_fuse3view        eval.py 3-view volume fusion + per-class Dice PMU/eval.py:42-65,157-203
  *
  * Conventions
  *   - All tensors are device pointers, fp32, activations stored channels-last (NHWC),
@@ -29,7 +33,9 @@
  *     allocates, never synchronises, and is safe to capture in a hipGraph.
  *   - Every call returns 0 on success, PMU_ERR_ARG for an invalid argument (checked
  *     on the host before any launch), or the hipError_t of a failed launch.
- *   - Reductions are deterministic: fixed-shape partial slabs, no float atomics.
+ *   - Reductions are deterministic: fixed-shape partial slabs, no float atomics — except the
+ *     metric counters (pmu_dice_counts, pmu_fuse3view: fp64 atomics of integer values, exact) and
+ *     pmu_dice_sums (fp64 atomics; exact for the 0/1 inputs the reference feeds it).
  */
 #ifndef PMUNET_HIP_H
 #define PMUNET_HIP_H
