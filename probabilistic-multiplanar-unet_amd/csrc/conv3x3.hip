@@ -19,6 +19,9 @@
 // ds_read_b128 and feeds one k per MFMA step (the K order inside a chunk is free as long as A
 // and B agree), conflict-free for 16 consecutive rows.  The next tap's 8 reads are issued ahead
 // of the current tap's 32 MFMAs.
+#include <cstdlib>
+#include <cstring>
+
 #include "pmu_stage.h"
 
 namespace {
@@ -92,6 +95,68 @@ __device__ __forceinline__ void stage_B(const ConvArgs& a, int j0, int k0, float
     if (j < a.NOUT && k < a.KC)
       v = DGRAD ? a.w[((long long)k * a.NOUT + j) * 9 + (8 - tap)] : a.w[((long long)j * a.KC + k) * 9 + tap];
     Bs[(tap * BN + jl) * LS + kl] = v;
+  }
+}
+
+// Epilogue shared by both conv kernels: fwd writes z (+bias) and per-tile BN partial sums
+// (sum, sum of squares per channel, reduced over the block through LDS); dgrad writes dx split
+// into the two concat halves.
+template <bool DGRAD>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2][2], float* smem, int n, int h0,
+                                              int w0, int j0, int TW) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const DevFrame& F = a.in;
+  float* red = smem;  // [4 waves][64 ch][2]
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+#pragma unroll
+  for (int fn = 0; fn < 2; ++fn) {
+    const int j = j0 + fn * 32 + (lane & 31);
+    const bool jok = j < a.NOUT;
+    const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = wave * 64 + fm * 32 + acc_row(r, lane);
+        const int h = h0 + (q >> a.twl), w = w0 + (q & (TW - 1));
+        if (!jok || h >= F.H || w >= F.W) continue;
+        const long long pix = ((long long)n * F.H + h) * F.W + w;
+        const float v = acc[fm][fn][r] + b;
+        if (!DGRAD) {
+          a.out0[pix * a.NOUT + j] = v;
+          s1[fn] += v;
+          s2[fn] = fmaf(v, v, s2[fn]);
+        } else {
+          if (j < a.split) a.out0[pix * a.split + j] = v;
+          else a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+        }
+      }
+    }
+  }
+  if (!DGRAD && a.part) {
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn) {
+      s1[fn] += __shfl_xor(s1[fn], 32, 64);
+      s2[fn] += __shfl_xor(s2[fn], 32, 64);
+      if (lane < 32) {
+        red[(wave * 64 + fn * 32 + lane) * 2 + 0] = s1[fn];
+        red[(wave * 64 + fn * 32 + lane) * 2 + 1] = s2[fn];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const int j = j0 + tid;
+      if (j < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < 4; ++wv) {
+          t1 += red[(wv * 64 + tid) * 2 + 0];
+          t2 += red[(wv * 64 + tid) * 2 + 1];
+        }
+        a.part[((long long)blockIdx.x * 2 + 0) * a.NOUT + j] = t1;
+        a.part[((long long)blockIdx.x * 2 + 1) * a.NOUT + j] = t2;
+      }
+    }
   }
 }
 
@@ -192,65 +257,185 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---------------- epilogue
-  float* red = smem;  // [4 waves][64 ch][2]
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  conv_epilogue<DGRAD>(a, acc, smem, n, h0, w0, j0, TW);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Software-pipelined variant (1 block/CU, LDS double-buffered): the next chunk's A items and B
+// tile are loaded into registers before the current chunk's 9 x 32 MFMAs, transformed and written
+// to the other LDS buffer after them, with one barrier per chunk.  The operand modes are template
+// parameters (M1 < 0: single source), so the staging has no runtime dispatch.  Used when every
+// source is a fast-path source whose channel count is a multiple of BK and packed weights exist.
+// ---------------------------------------------------------------------------------------------
+constexpr int PIPE_NB = 9 * BN * BK / 4 / 256;  // packed-B float4 per thread per chunk
+static_assert(PIPE_NB == 9, "PipeB holds 9 float4");
+
+// the packed-B prefetch registers as named members: an indexed array here is kept in scratch
+struct PipeB {
+  float4 v0, v1, v2, v3, v4, v5, v6, v7, v8;
+};
+template <int R>
+__device__ __forceinline__ float4& pipe_b(PipeB& b) {
+  if constexpr (R == 0) return b.v0;
+  else if constexpr (R == 1) return b.v1;
+  else if constexpr (R == 2) return b.v2;
+  else if constexpr (R == 3) return b.v3;
+  else if constexpr (R == 4) return b.v4;
+  else if constexpr (R == 5) return b.v5;
+  else if constexpr (R == 6) return b.v6;
+  else if constexpr (R == 7) return b.v7;
+  else return b.v8;
+}
+template <int R>
+__device__ __forceinline__ void pipe_load_b_r(const float4* src, int tid, PipeB& b) {
+  pipe_b<R>(b) = src[tid + 256 * R];
+  if constexpr (R + 1 < PIPE_NB) pipe_load_b_r<R + 1>(src, tid, b);
+}
+template <int R>
+__device__ __forceinline__ void pipe_store_b_r(float* bs, int tid, PipeB& b) {
+  const int it = tid + 256 * R;
+  *reinterpret_cast<float4*>(bs + (it >> 2) * LS + 4 * (it & 3)) = pipe_b<R>(b);
+  if constexpr (R + 1 < PIPE_NB) pipe_store_b_r<R + 1>(bs, tid, b);
+}
+__device__ __forceinline__ void pipe_load_b(const float4* src, int tid, PipeB& b) { pipe_load_b_r<0>(src, tid, b); }
+__device__ __forceinline__ void pipe_store_b(float* bs, int tid, PipeB& b) { pipe_store_b_r<0>(bs, tid, b); }
+
+template <bool DGRAD, int POOL>
+__global__ __launch_bounds__(256, 1) void conv3x3_pipe_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int TW = 1 << a.twl;
+  const int TH = BM >> a.twl;
+  const int HW2 = TW + 2;
+  const int HP = (TH + 2) * HW2;
+
+  int t = blockIdx.x;
+  const int tw = t % a.tiles_w; t /= a.tiles_w;
+  const int th = t % a.tiles_h; t /= a.tiles_h;
+  const int n = t;
+  const int h0 = th * TH, w0 = tw * TW;
+  const int j0 = blockIdx.y * BN;
+  const DevFrame& F = a.in;
+  const int nchunks = (a.KC + BK - 1) / BK;
+  const int cq4 = 4 * (tid & 3);
+
+  int ih[NI], iw[NI], dst[NI];
 #pragma unroll
-  for (int fn = 0; fn < 2; ++fn) {
-    const int j = j0 + fn * 32 + (lane & 31);
-    const bool jok = j < a.NOUT;
-    const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
-#pragma unroll
-    for (int fm = 0; fm < 2; ++fm) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = wave * 64 + fm * 32 + acc_row(r, lane);
-        const int h = h0 + (q >> a.twl), w = w0 + (q & (TW - 1));
-        if (!jok || h >= F.H || w >= F.W) continue;
-        const long long pix = ((long long)n * F.H + h) * F.W + w;
-        const float v = acc[fm][fn][r] + b;
-        if (!DGRAD) {
-          a.out0[pix * a.NOUT + j] = v;
-          s1[fn] += v;
-          s2[fn] = fmaf(v, v, s2[fn]);
-        } else {
-          if (j < a.split) a.out0[pix * a.split + j] = v;
-          else a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
-        }
-      }
-    }
+  for (int i = 0; i < NI; ++i) {
+    const int it = tid + 256 * i;
+    const int hp = it >> 2;
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    ih[i] = (it < HP * 4) ? h0 - 1 + hr : PMU_NO_ITEM;
+    iw[i] = w0 - 1 + hc;
+    dst[i] = hp * LS + 4 * (it & 3);
   }
-  if (!DGRAD && a.part) {
+  const int hsel = (lane >> 5) * 8;
+  int abase[2], bbase[2];
 #pragma unroll
-    for (int fn = 0; fn < 2; ++fn) {
-      s1[fn] += __shfl_xor(s1[fn], 32, 64);
-      s2[fn] += __shfl_xor(s2[fn], 32, 64);
-      if (lane < 32) {
-        red[(wave * 64 + fn * 32 + lane) * 2 + 0] = s1[fn];
-        red[(wave * 64 + fn * 32 + lane) * 2 + 1] = s2[fn];
+  for (int fm = 0; fm < 2; ++fm) {
+    const int q = wave * 64 + fm * 32 + (lane & 31);
+    const int r = q >> a.twl, c = q & (TW - 1);
+    abase[fm] = (r * HW2 + c) * LS + hsel;
+  }
+#pragma unroll
+  for (int fn = 0; fn < 2; ++fn) bbase[fn] = (fn * 32 + (lane & 31)) * LS + hsel;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  PmuPref<POOL, DGRAD, NI> pf;
+  PipeB pb;
+  const float4* wpk = reinterpret_cast<const float4*>(a.wp + (long long)(j0 / BN) * nchunks * (9 * BN * BK));
+#define PMU_PREFETCH(CH)                                                                      \
+  {                                                                                           \
+    const int k0_ = (CH) * BK;                                                                \
+    if (F.nsrc < 2 || k0_ < F.C0) pmu_prefetch<POOL, DGRAD, NI>(F.s0, k0_ + cq4, n, ih, iw, pf); \
+    else pmu_prefetch<POOL, DGRAD, NI>(F.s1, k0_ - F.C0 + cq4, n, ih, iw, pf);                \
+    pipe_load_b(wpk + (long long)(CH) * (9 * BN * BK / 4), tid, pb);                          \
+  }
+#define PMU_COMMIT(BUF)                                                                       \
+  {                                                                                           \
+    pmu_commit<POOL, DGRAD, NI>(pf, ih, dst, (BUF));                                          \
+    pipe_store_b((BUF) + A_FLOATS, tid, pb);                                                  \
+  }
+
+  PMU_PREFETCH(0)
+  PMU_COMMIT(smem)
+  __syncthreads();
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const float* As = smem + (ch & 1) * STAGE;
+    const float* Bs = As + A_FLOATS;
+    if (ch + 1 < nchunks) PMU_PREFETCH(ch + 1)
+    float4 op[2][8];
+    auto load_ops = [&](int tap, float4 (&o)[8]) {
+      const int toff = ((tap / 3) * HW2 + (tap % 3)) * LS;
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm) {
+        o[2 * fm + 0] = *reinterpret_cast<const float4*>(As + abase[fm] + toff);
+        o[2 * fm + 1] = *reinterpret_cast<const float4*>(As + abase[fm] + toff + 4);
       }
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn) {
+        o[4 + 2 * fn + 0] = *reinterpret_cast<const float4*>(Bs + tap * BN * LS + bbase[fn]);
+        o[4 + 2 * fn + 1] = *reinterpret_cast<const float4*>(Bs + tap * BN * LS + bbase[fn] + 4);
+      }
+    };
+    auto mfmas = [&](const float4 (&o)[8]) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < 2; ++fn) {
+            const float4 va = o[2 * fm + (s >> 2)], vb = o[4 + 2 * fn + (s >> 2)];
+            const float x = (s & 3) == 0 ? va.x : (s & 3) == 1 ? va.y : (s & 3) == 2 ? va.z : va.w;
+            const float y = (s & 3) == 0 ? vb.x : (s & 3) == 1 ? vb.y : (s & 3) == 2 ? vb.z : vb.w;
+            acc[fm][fn] = mfma_f32_32x32x2(x, y, acc[fm][fn]);
+          }
+    };
+    load_ops(0, op[0]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) load_ops(tap + 1, op[(tap + 1) & 1]);
+      mfmas(op[tap & 1]);
     }
+    if (ch + 1 < nchunks) PMU_COMMIT(smem + ((ch + 1) & 1) * STAGE)
     __syncthreads();
-    if (tid < 64) {
-      const int j = j0 + tid;
-      if (j < a.NOUT) {
-        float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-        for (int wv = 0; wv < 4; ++wv) {
-          t1 += red[(wv * 64 + tid) * 2 + 0];
-          t2 += red[(wv * 64 + tid) * 2 + 1];
-        }
-        a.part[((long long)blockIdx.x * 2 + 0) * a.NOUT + j] = t1;
-        a.part[((long long)blockIdx.x * 2 + 1) * a.NOUT + j] = t2;
-      }
-    }
   }
+#undef PMU_PREFETCH
+#undef PMU_COMMIT
+  conv_epilogue<DGRAD>(a, acc, smem, n, h0, w0, j0, TW);
 }
 
 static int pick_twl(int W) {
   if (W > 16) return 5;
   if (W > 8) return 4;
   return 3;
+}
+
+// PMU_CONV_IMPL=pipe selects the software-pipelined 1-block/CU kernel where it applies.  Default:
+// the 2-blocks/CU kernel, measured ~10% faster on every c2 shape (the pipelined variant's 9-float4
+// B prefetch ends up in scratch and one wave per SIMD exposes the staging).
+static bool use_pipe() {
+  static const int v = [] {
+    const char* e = getenv("PMU_CONV_IMPL");
+    return (e && strcmp(e, "pipe") == 0) ? 1 : 0;
+  }();
+  return v != 0;
+}
+
+// a source the pipelined staging handles: float4 channels, chunks never straddle sources
+static bool pipe_src_ok(const pmu_src& s) {
+  if (s.C % BK != 0) return false;
+  if (s.pool == PMU_POOL_NONE) return true;
+  return s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU;
 }
 
 static int launch_conv(const pmu_frame* in, const float* w, const float* wp, const float* bias, int NOUT, int KC,
@@ -264,10 +449,35 @@ static int launch_conv(const pmu_frame* in, const float* w, const float* wp, con
   a.tiles_w = pmu_cdiv(in->W, TW);
   a.tiles_h = pmu_cdiv(in->H, TH);
   dim3 grid((unsigned)(a.tiles_w * a.tiles_h * in->N), (unsigned)pmu_cdiv(NOUT, BN));
+  hipStream_t st = (hipStream_t)stream;
+  if (wp && use_pipe()) {
+    const pmu_src& s0 = in->src[0];
+    const bool two = in->nsrc > 1;
+    const pmu_src& s1 = in->src[1];
+    const bool ok = pipe_src_ok(s0) && (!two || pipe_src_ok(s1));
+    // one pool mode for the whole frame; the BN-backward source only for dgrad (single source)
+    const int pool = s0.pool;
+    const bool same_pool = !two || s1.pool == pool;
+    const bool modes_ok = dgrad ? (!two && s0.mode == PMU_SRC_BNBWD)
+                                : (s0.mode != PMU_SRC_BNBWD && (!two || s1.mode != PMU_SRC_BNBWD));
+    const bool c0_ok = !two || s0.C % BK == 0;
+#define PMU_PIPE(DG, PL)                                                                           \
+  if (dgrad == DG && pool == PL) {                                                                 \
+    hipLaunchKernelGGL((conv3x3_pipe_kernel<DG, PL>), grid, dim3(256), 0, st, a);                  \
+    PMU_CHECK_LAUNCH();                                                                            \
+    return PMU_OK;                                                                                 \
+  }
+    if (ok && same_pool && modes_ok && c0_ok) {
+      PMU_PIPE(false, PMU_POOL_NONE)
+      PMU_PIPE(false, PMU_POOL_MAX2)
+      PMU_PIPE(true, PMU_POOL_NONE)
+    }
+#undef PMU_PIPE
+  }
   if (dgrad)
-    hipLaunchKernelGGL(conv3x3_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(conv3x3_kernel<true>, grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(conv3x3_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(conv3x3_kernel<false>, grid, dim3(256), 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -101,3 +101,84 @@ __device__ __forceinline__ void stage_items(const DevFrame& F, int n, int cbase,
   for (int i = 0; i < NI; ++i)
     if (ih[i] != PMU_NO_ITEM) *reinterpret_cast<float4*>(lds + dst[i]) = frame_value4(F, n, ih[i], iw[i], cbase + 4 * cq);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Split staging for software-pipelined kernels: pmu_prefetch() issues every global load of a
+// thread's NI items (and the chunk's BN coefficients) into registers; pmu_commit() applies the
+// transform and writes LDS.  Between the two the caller runs MFMAs on the previous chunk, so the
+// load latency is hidden inside the wave instead of relying on a second resident block.
+// POOL and BWD (= BN-backward source) are compile-time; RAW vs BN+ReLU is a uniform runtime field
+// so both halves of a concat frame share one register set.
+// ---------------------------------------------------------------------------------------------
+template <int POOL, bool BWD, int NI>
+struct PmuPref {
+  static constexpr int NL = (POOL == PMU_POOL_MAX2) ? 4 : 1;
+  float4 x[NI][NL];
+  float4 z[BWD ? NI : 1];
+  float4 sc, sh, mu, kx, kc;
+  unsigned okmask;
+  int raw;
+};
+
+template <int POOL, bool BWD, int NI>
+__device__ __forceinline__ void pmu_prefetch(const DevSrc& s, int c, int n, const int (&ih)[NI], const int (&iw)[NI],
+                                             PmuPref<POOL, BWD, NI>& p) {
+  p.raw = (s.mode == PMU_SRC_RAW);
+  if (!p.raw) {
+    p.sc = *reinterpret_cast<const float4*>(s.coef + c);
+    p.sh = *reinterpret_cast<const float4*>(s.coef + s.C + c);
+  }
+  if (BWD) {
+    p.mu = *reinterpret_cast<const float4*>(s.coef + 2 * s.C + c);
+    p.kx = *reinterpret_cast<const float4*>(s.coef + 3 * s.C + c);
+    p.kc = *reinterpret_cast<const float4*>(s.coef + 4 * s.C + c);
+  }
+  const long long rs = (long long)s.W * s.C;
+  unsigned m = 0u;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    int hs = ih[i] - s.off_h, ws = iw[i] - s.off_w;
+    if (POOL == PMU_POOL_MAX2) { hs *= 2; ws *= 2; }
+    const int lim_h = (POOL == PMU_POOL_MAX2) ? s.H - 1 : s.H;
+    const int lim_w = (POOL == PMU_POOL_MAX2) ? s.W - 1 : s.W;
+    const bool ok = (ih[i] != PMU_NO_ITEM) && hs >= 0 && ws >= 0 && hs < lim_h && ws < lim_w;
+    m |= ok ? (1u << i) : 0u;
+    const long long idx = ok ? (((long long)n * s.H + hs) * s.W + ws) * s.C + c : (long long)c;
+    p.x[i][0] = *reinterpret_cast<const float4*>(s.x + idx);
+    if (POOL == PMU_POOL_MAX2) {
+      p.x[i][1] = *reinterpret_cast<const float4*>(s.x + idx + s.C);
+      p.x[i][2] = *reinterpret_cast<const float4*>(s.x + idx + rs);
+      p.x[i][3] = *reinterpret_cast<const float4*>(s.x + idx + rs + s.C);
+    }
+    if (BWD) p.z[i] = *reinterpret_cast<const float4*>(s.z + idx);
+  }
+  p.okmask = m;
+}
+
+template <int POOL, bool BWD, int NI>
+__device__ __forceinline__ void pmu_commit(const PmuPref<POOL, BWD, NI>& p, const int (&ih)[NI], const int (&dst)[NI],
+                                           float* lds) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    if (ih[i] == PMU_NO_ITEM) continue;
+    float4 v;
+    if (BWD) {
+      const float4 d = p.x[i][0], z = p.z[i];
+      v = make_float4(pmu_bnbwd1(d.x, z.x, p.sc.x, p.sh.x, p.mu.x, p.kx.x, p.kc.x),
+                      pmu_bnbwd1(d.y, z.y, p.sc.y, p.sh.y, p.mu.y, p.kx.y, p.kc.y),
+                      pmu_bnbwd1(d.z, z.z, p.sc.z, p.sh.z, p.mu.z, p.kx.z, p.kc.z),
+                      pmu_bnbwd1(d.w, z.w, p.sc.w, p.sh.w, p.mu.w, p.kx.w, p.kc.w));
+    } else if (p.raw) {
+      v = p.x[i][0];
+    } else {
+      v = pmu_bnrelu4(p.x[i][0], p.sc, p.sh);
+      if (POOL == PMU_POOL_MAX2) {
+        v = pmu_max4(v, pmu_bnrelu4(p.x[i][1], p.sc, p.sh));
+        v = pmu_max4(v, pmu_bnrelu4(p.x[i][2], p.sc, p.sh));
+        v = pmu_max4(v, pmu_bnrelu4(p.x[i][3], p.sc, p.sh));
+      }
+    }
+    if (!((p.okmask >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(lds + dst[i]) = v;
+  }
+}
