@@ -2,7 +2,7 @@
 // partial sums, and its weight gradient, on the VALU (K = 9*Cin is too short for MFMA tiles).
 // Reference: the first DoubleConv conv of PMU/model/unet/unet_parts.py:15 and Encoder conv of
 // PMU/model/probabilistic_unet/probabilistic_unet.py:38 (posterior input = cat(image, mask), :88).
-#include "pmu_common.h"
+#include "pmu_stage.h"
 
 namespace {
 
@@ -135,6 +135,107 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(FirstWgArgs a) {
   }
 }
 
+// Fast path (dz = one unpooled BN-backward source, Cout % 4 == 0): thread = (channel quad, pixel
+// group); float4 loads of da and z with the quad's BN-backward coefficients in registers; the
+// 3x3 x CIN input neighbourhood read once per pixel; partial dW reduced over the pixel groups of
+// a wave by shuffles, over the 4 waves through LDS, and over blocks by rows_sum4_kernel.
+constexpr int FWP2 = 4096;  // pixels per block (fast path)
+
+template <int CIN>
+__global__ __launch_bounds__(256) void conv_first_wgrad_fast_kernel(FirstWgArgs a) {
+  constexpr int K9 = CIN * 9;
+  __shared__ float red[512 * K9];  // [slot][Cout][K9]: 4 slots x Cout <= 128, or 1 slot x Cout = 256
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const DevSrc& s = a.dz.s0;
+  const int Cout = a.Cout, CQ = Cout >> 2, PG = 256 / CQ;
+  const int cq = tid % CQ, pg = tid / CQ;
+  const int H = a.dz.H, W = a.dz.W;
+  const long long P = (long long)a.dz.N * H * W;
+  const int c = 4 * cq;
+  const float4 sc = *reinterpret_cast<const float4*>(s.coef + c);
+  const float4 sh = *reinterpret_cast<const float4*>(s.coef + Cout + c);
+  const float4 mu = *reinterpret_cast<const float4*>(s.coef + 2 * Cout + c);
+  const float4 kx = *reinterpret_cast<const float4*>(s.coef + 3 * Cout + c);
+  const float4 kc = *reinterpret_cast<const float4*>(s.coef + 4 * Cout + c);
+  float acc[4][K9];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int k = 0; k < K9; ++k) acc[e][k] = 0.f;
+  long long p = (long long)blockIdx.x * FWP2 + pg;
+  const long long pend = min(P, (long long)(blockIdx.x + 1) * FWP2);
+  // incremental (n, h, w) of p
+  int w = (int)(p % W);
+  long long t = p / W;
+  int h = (int)(t % H);
+  long long n = t / H;
+  for (; p < pend; p += PG) {
+    const float4 d = *reinterpret_cast<const float4*>(s.x + p * Cout + c);
+    const float4 z = *reinterpret_cast<const float4*>(s.z + p * Cout + c);
+    float g[4];
+    g[0] = pmu_bnbwd1(d.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x);
+    g[1] = pmu_bnbwd1(d.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y);
+    g[2] = pmu_bnbwd1(d.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z);
+    g[3] = pmu_bnbwd1(d.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w);
+#pragma unroll
+    for (int ci = 0; ci < CIN; ++ci) {
+      const float* pl = a.planes[ci] + n * H * W;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+        const bool in = hh >= 0 && hh < H && ww >= 0 && ww < W;
+        const float x = in ? pl[hh * W + ww] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e][ci * 9 + tap] = fmaf(g[e], x, acc[e][ci * 9 + tap]);
+      }
+    }
+    w += PG;
+    while (w >= W) {
+      w -= W;
+      if (++h == H) { h = 0; ++n; }
+    }
+  }
+  // reduce over the pixel groups inside the wave (lanes with equal cq are CQ apart)
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int k = 0; k < K9; ++k) {
+      float v = acc[e][k];
+      for (int off = CQ; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+      acc[e][k] = v;
+    }
+  const int cq_per_wave = CQ < 64 ? CQ : 64;
+  const int nwr = CQ < 64 ? 4 : 1;  // waves holding distinct partials of the same channels
+  if (lane < cq_per_wave) {
+    const int slot = CQ < 64 ? wave : 0;
+    const int ch0 = 4 * cq;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int k = 0; k < K9; ++k) red[(slot * Cout + ch0 + e) * K9 + k] = acc[e][k];
+  }
+  __syncthreads();
+  for (int o = tid; o < Cout * K9; o += 256) {
+    float v = 0.f;
+    for (int wv = 0; wv < nwr; ++wv) v += red[wv * Cout * K9 + o];
+    a.ws[(long long)blockIdx.x * Cout * K9 + o] = v;
+  }
+}
+
+// out[o] = sum_r ws[r][o]: block = 64 outputs x 4 row phases (fixed order), fp64 accumulation
+__global__ __launch_bounds__(256) void rows_sum4_kernel(const float* __restrict__ ws, int R, int Wd,
+                                                        float* __restrict__ out) {
+  __shared__ double red[256];
+  const int o = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  double s = 0.0;
+  if (o < Wd)
+    for (int r = ph; r < R; r += 4) s += ws[(long long)r * Wd + o];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && o < Wd) out[o] = (float)(red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] +
+                                                   red[threadIdx.x + 192]);
+}
+
 // dw[o] = sum_b ws[b][o]
 __global__ void rows_sum_kernel(const float* __restrict__ ws, int R, int Wd, float* __restrict__ out) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
@@ -165,26 +266,48 @@ extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, in
   return PMU_OK;
 }
 
+static bool first_wgrad_fast(const pmu_frame* dz, int Cout) {
+  const pmu_src& s = dz->src[0];
+  return s.mode == PMU_SRC_BNBWD && s.pool == PMU_POOL_NONE && s.off_h == 0 && s.off_w == 0 && s.H == dz->H &&
+         s.W == dz->W && Cout % 4 == 0 && Cout <= 256 && 256 % (Cout / 4) == 0;
+}
+
 extern "C" size_t pmu_conv_first_wgrad_ws(int N, int H, int W, int Cin, int Cout) {
-  return (size_t)pmu_cdiv((long long)N * H * W, FWPIX) * Cout * Cin * 9 * sizeof(float);
+  const long long P = (long long)N * H * W;
+  const size_t slow = (size_t)pmu_cdiv(P, FWPIX) * Cout * Cin * 9 * sizeof(float);
+  const size_t fast = (size_t)pmu_cdiv(P, FWP2) * Cout * Cin * 9 * sizeof(float);
+  return slow > fast ? slow : fast;
 }
 
 extern "C" int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* planes, int Cin, int Cout,
                                     float* dw, float* ws, size_t ws_bytes, void* stream) {
   PMU_REQUIRE(valid_frame(dz) && dz->nsrc == 1 && dz->src[0].C == Cout && planes && dw && ws);
   PMU_REQUIRE(Cin >= 1 && Cin <= 4 && Cout >= 1 && Cout <= 256 && 256 % Cout == 0);
-  const int nb = pmu_cdiv((long long)dz->N * dz->H * dz->W, FWPIX);
-  PMU_REQUIRE(ws_bytes >= (size_t)nb * Cout * Cin * 9 * sizeof(float));
+  PMU_REQUIRE(ws_bytes >= pmu_conv_first_wgrad_ws(dz->N, dz->H, dz->W, Cin, Cout));
   FirstWgArgs a;
   a.dz = make_dev_frame(dz);
   for (int i = 0; i < 4; ++i) a.planes[i] = i < Cin ? planes[i] : nullptr;
   for (int i = 0; i < Cin; ++i) PMU_REQUIRE(planes[i]);
   a.Cin = Cin; a.Cout = Cout; a.ws = ws;
-  hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, a);
+  hipStream_t st = (hipStream_t)stream;
+  const long long P = (long long)dz->N * dz->H * dz->W;
+  int nb;
+  if (first_wgrad_fast(dz, Cout)) {
+    nb = pmu_cdiv(P, FWP2);
+    switch (Cin) {
+      case 1: hipLaunchKernelGGL(conv_first_wgrad_fast_kernel<1>, dim3((unsigned)nb), dim3(256), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(conv_first_wgrad_fast_kernel<2>, dim3((unsigned)nb), dim3(256), 0, st, a); break;
+      case 3: hipLaunchKernelGGL(conv_first_wgrad_fast_kernel<3>, dim3((unsigned)nb), dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL(conv_first_wgrad_fast_kernel<4>, dim3((unsigned)nb), dim3(256), 0, st, a); break;
+    }
+  } else {
+    nb = pmu_cdiv(P, FWPIX);
+    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, a);
+  }
   PMU_CHECK_LAUNCH();
   const int Wd = Cout * Cin * 9;
-  hipLaunchKernelGGL(rows_sum_kernel, dim3((unsigned)pmu_cdiv(Wd, 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const float*)ws, nb, Wd, dw);
+  hipLaunchKernelGGL(rows_sum4_kernel, dim3((unsigned)pmu_cdiv(Wd, 64)), dim3(256), 0, st, (const float*)ws, nb, Wd,
+                     dw);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
