@@ -304,11 +304,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; rank -> device modulo the visible count so a multi-rank run can be
+    # rehearsed on fewer GPUs (PMU_DIST_BACKEND=gloo: RCCL needs distinct devices per rank)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(1, ndev))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        backend = os.environ.get("PMU_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from pmu_hip import _lib as L
 

@@ -160,7 +160,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x16 (&acc)[2
   }
 }
 
-template <bool DGRAD>
+// TWL = log2 of the tile width (compile-time, so every tap's LDS offset is an immediate)
+template <bool DGRAD, int TWL>
 __global__ __launch_bounds__(256, 2) void conv3x3_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[STAGE];
   float* As = smem;
@@ -169,10 +170,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(ConvArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int TW = 1 << a.twl;
-  const int TH = BM >> a.twl;
-  const int HW2 = TW + 2;
-  const int HP = (TH + 2) * HW2;
+  constexpr int TW = 1 << TWL;
+  constexpr int TH = BM >> TWL;
+  constexpr int HW2 = TW + 2;
+  constexpr int HP = (TH + 2) * HW2;
 
   int t = blockIdx.x;
   const int tw = t % a.tiles_w; t /= a.tiles_w;
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(ConvArgs a) {
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm) {
     const int q = wave * 64 + fm * 32 + (lane & 31);
-    const int r = q >> a.twl, c = q & (TW - 1);
+    const int r = q >> TWL, c = q & (TW - 1);
     abase[fm] = (r * HW2 + c) * LS + hsel;
   }
 #pragma unroll
@@ -474,10 +475,16 @@ static int launch_conv(const pmu_frame* in, const float* w, const float* wp, con
     }
 #undef PMU_PIPE
   }
-  if (dgrad)
-    hipLaunchKernelGGL(conv3x3_kernel<true>, grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(conv3x3_kernel<false>, grid, dim3(256), 0, st, a);
+#define PMU_CLASSIC(DG, T)                                                                         \
+  if (dgrad == DG && a.twl == T) {                                                                 \
+    hipLaunchKernelGGL((conv3x3_kernel<DG, T>), grid, dim3(256), 0, st, a);                        \
+    PMU_CHECK_LAUNCH();                                                                            \
+    return PMU_OK;                                                                                 \
+  }
+  PMU_CLASSIC(false, 3) PMU_CLASSIC(false, 4) PMU_CLASSIC(false, 5)
+  PMU_CLASSIC(true, 3) PMU_CLASSIC(true, 4) PMU_CLASSIC(true, 5)
+#undef PMU_CLASSIC
+  return PMU_ERR_ARG;
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

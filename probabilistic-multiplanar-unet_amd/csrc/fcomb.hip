@@ -59,74 +59,150 @@ __device__ __forceinline__ void mm64(const float* A, const float* W, int lane, f
 
 // ------------------------------------------------------------------------------------------
 // forward: y[s][n][k][h][w]; feat NHWC [P][F]; zb [S][N][F]
-// block = 4 waves, tile = 128 pixels (wave w: pixels 32w..32w+31), persistent over tiles
+// Register-resident: a wave owns 32 pixels and computes every layer transposed,
+//   out^T[o][px] = sum_k W[o][k] * in^T[k][px]     (MFMA A = weight rows, B = activations)
+// so the accumulator of one layer IS the B operand of the next: lane (px = lane&31, half h) holds
+// channels o = acc_row(r) = (r&3) + 8(r>>2) + 4h in register r, and k-step s of a 32-channel block
+// feeds channel acc_row(s) of that block (the K order inside a block is free as long as A and B
+// agree).  The matching weight values W[o][8q+4h .. 8q+4h+3] of 4 consecutive k-steps are one
+// ds_read_b128 of the LDS weight row.  Activations never touch LDS; weights are staged once per
+// block (persistent over 32-pixel groups).
 // ------------------------------------------------------------------------------------------
-constexpr int FT = 128;
+constexpr int RRS = 68;  // LDS weight row stride: b128 reads of 8 rows hit distinct bank groups
 
-__global__ __launch_bounds__(256) void fcomb_fwd_kernel(const float* __restrict__ feat, const float* __restrict__ zb,
-                                                        FcombW p, int S, int N, long long HW, float* __restrict__ y,
-                                                        long long ntiles) {
-  __shared__ __attribute__((aligned(16))) float sm[MAXNH * FW * RS + KP * RS + 2 * FT * RS];
-  float* Ws = sm;                       // MAXNH*64*RS
-  float* Wl = Ws + MAXNH * FW * RS;     // 32*RS
-  float* U1 = Wl + KP * RS;             // [128][RS]  W_1f . f (sample independent)
-  float* Hb = U1 + FT * RS;             // [128][RS]  working activations
+__global__ __launch_bounds__(256, 2) void fcomb_fwd_kernel(const float* __restrict__ feat, const float* __restrict__ zb,
+                                                           FcombW p, int S, int N, long long HW, float* __restrict__ y,
+                                                           long long ngroups) {
+  __shared__ __attribute__((aligned(16))) float Wsh[(MAXNH * FW + KP) * RRS + MAXNH * FW + KP];
+  float* Bsh = Wsh + (MAXNH * FW + KP) * RRS;  // biases: [l][64] for l >= 1, then last [32]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  stage_weights(p, Ws, Wl);
+  for (int e = tid; e < MAXNH * FW * FW; e += 256) {
+    const int l = e / (FW * FW), r = e % (FW * FW), o = r / FW, c = r % FW;
+    float v = 0.f;
+    if (l < p.NH && o < p.F && c < p.F) v = p.w[l][(long long)o * (l == 0 ? p.F + p.L : p.F) + c];
+    Wsh[(l * FW + o) * RRS + c] = v;
+  }
+  for (int e = tid; e < KP * FW; e += 256) {
+    const int o = e / FW, c = e % FW;
+    Wsh[(MAXNH * FW + o) * RRS + c] = (o < p.K && c < p.F) ? p.wl[o * p.F + c] : 0.f;
+  }
+  for (int e = tid; e < MAXNH * FW + KP; e += 256) {
+    float v = 0.f;
+    if (e < MAXNH * FW) {
+      const int l = e / FW, o = e % FW;
+      if (l >= 1 && l < p.NH && o < p.F) v = p.b[l][o];
+    } else if (e - MAXNH * FW < p.K) {
+      v = p.bl[e - MAXNH * FW];
+    }
+    Bsh[e] = v;
+  }
+  __syncthreads();
+
+  const int h = lane >> 5;
   const long long P = (long long)N * HW;
-  for (long long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const long long p0 = tile * FT;
-    __syncthreads();  // weights staged / previous tile's LDS reads done
-    for (int e = tid; e < FT * FW; e += 256) {
-      const int r = e / FW, c = e % FW;
-      const long long px = p0 + r;
-      Hb[r * RS + c] = (px < P && c < p.F) ? feat[px * p.F + c] : 0.f;
-    }
-    __syncthreads();
-    const float* A = Hb + wave * 32 * RS;
-    float* U = U1 + wave * 32 * RS;
-    float* Hw = Hb + wave * 32 * RS;
-    {  // u1 = W_1f . f
-      f32x16 acc[2];
-      mm64<2>(A, Ws, lane, acc);
+  const float* wrow = Wsh + (lane & 31) * RRS + 4 * h;  // + (row block)*RRS + kb*32 + 8q
+  for (long long g = (long long)blockIdx.x * 4 + wave; g < ngroups; g += (long long)gridDim.x * 4) {
+    const long long px = g * 32 + (lane & 31);
+    const bool valid = px < P;
+    const long long pxc = valid ? px : P - 1;
+    const long long n = pxc / HW, pix = pxc - n * HW;
+    // ---- layer 1 feature part (sample independent): u[ob] = W_1f . f
+    f32x16 u[2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f)
+    for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) U[acc_row(r, lane) * RS + f * 32 + (lane & 31)] = acc[f][r];
-    }
+      for (int r = 0; r < 16; ++r) u[ob][r] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c0 = kb * 32 + 8 * q + 4 * h;
+        float4 fv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (valid && c0 < p.F) fv = *reinterpret_cast<const float4*>(feat + pxc * p.F + c0);
+        const float fa[4] = {fv.x, fv.y, fv.z, fv.w};
+        float4 w4[2];
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob) w4[ob] = *reinterpret_cast<const float4*>(wrow + (ob * 32) * RRS + kb * 32 + 8 * q);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int ob = 0; ob < 2; ++ob) {
+            const float wa = s4 == 0 ? w4[ob].x : s4 == 1 ? w4[ob].y : s4 == 2 ? w4[ob].z : w4[ob].w;
+            u[ob] = mfma_f32_32x32x2(wa, fa[s4], u[ob]);
+          }
+      }
     for (int s = 0; s < S; ++s) {
-      // h1 = relu(u1 + zb[s][n])
-#pragma unroll 4
-      for (int e = lane; e < 32 * FW; e += 64) {
-        const int r = e / FW, c = e % FW;
-        const long long px = p0 + wave * 32 + r;
-        const int n = (int)((px < P ? px : P - 1) / HW);
-        const float b = c < p.F ? zb[((long long)s * N + n) * p.F + c] : 0.f;
-        Hw[r * RS + c] = fmaxf(0.f, U[r * RS + c] + b);
-      }
-      for (int l = 1; l < p.NH; ++l) {
-        f32x16 acc[2];
-        mm64<2>(Hw, Ws + l * FW * RS, lane, acc);
+      // ---- h1 = relu(u + zb[s][n])
+      f32x16 hc[2];
+      const float* zr = zb + ((long long)s * N + n) * p.F;
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          const int o = f * 32 + (lane & 31);
-          const float b = o < p.F ? p.b[l][o] : 0.f;
+      for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) Hw[acc_row(r, lane) * RS + o] = fmaxf(0.f, acc[f][r] + b);
+        for (int q = 0; q < 4; ++q) {
+          const int c0 = ob * 32 + 8 * q + 4 * h;
+          const float4 zv = c0 < p.F ? *reinterpret_cast<const float4*>(zr + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+          hc[ob][4 * q + 0] = fmaxf(0.f, u[ob][4 * q + 0] + zv.x);
+          hc[ob][4 * q + 1] = fmaxf(0.f, u[ob][4 * q + 1] + zv.y);
+          hc[ob][4 * q + 2] = fmaxf(0.f, u[ob][4 * q + 2] + zv.z);
+          hc[ob][4 * q + 3] = fmaxf(0.f, u[ob][4 * q + 3] + zv.w);
         }
+      // ---- hidden layers 2..NH
+      for (int l = 1; l < p.NH; ++l) {
+        f32x16 na[2];
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) na[ob][r] = 0.f;
+        const float* wl = wrow + (l * FW) * RRS;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float4 w4[2];
+#pragma unroll
+            for (int ob = 0; ob < 2; ++ob) w4[ob] = *reinterpret_cast<const float4*>(wl + (ob * 32) * RRS + kb * 32 + 8 * q);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+              for (int ob = 0; ob < 2; ++ob) {
+                const float wa = s4 == 0 ? w4[ob].x : s4 == 1 ? w4[ob].y : s4 == 2 ? w4[ob].z : w4[ob].w;
+                na[ob] = mfma_f32_32x32x2(wa, hc[kb][4 * q + s4], na[ob]);
+              }
+          }
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 bv = *reinterpret_cast<const float4*>(Bsh + l * FW + ob * 32 + 8 * q + 4 * h);
+            hc[ob][4 * q + 0] = fmaxf(0.f, na[ob][4 * q + 0] + bv.x);
+            hc[ob][4 * q + 1] = fmaxf(0.f, na[ob][4 * q + 1] + bv.y);
+            hc[ob][4 * q + 2] = fmaxf(0.f, na[ob][4 * q + 2] + bv.z);
+            hc[ob][4 * q + 3] = fmaxf(0.f, na[ob][4 * q + 3] + bv.w);
+          }
       }
-      f32x16 acc[1];
-      mm64<1>(Hw, Wl, lane, acc);
-      const int k = lane & 31;
-      if (k < p.K) {
-        const float b = p.bl[k];
+      // ---- last layer (K <= 32 rows); two accumulators (one per input block) to break the chain
+      f32x16 la[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) la[kb][r] = 0.f;
+      const float* wlast = wrow + (MAXNH * FW) * RRS;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const float4 w4 = *reinterpret_cast<const float4*>(wlast + kb * 32 + 8 * q);
+          la[kb] = mfma_f32_32x32x2(w4.x, hc[kb][4 * q + 0], la[kb]);
+          la[kb] = mfma_f32_32x32x2(w4.y, hc[kb][4 * q + 1], la[kb]);
+          la[kb] = mfma_f32_32x32x2(w4.z, hc[kb][4 * q + 2], la[kb]);
+          la[kb] = mfma_f32_32x32x2(w4.w, hc[kb][4 * q + 3], la[kb]);
+        }
+      if (valid) {
+        float* yo = y + ((long long)s * N + n) * p.K * HW + pix;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const long long px = p0 + wave * 32 + acc_row(r, lane);
-          if (px < P) {
-            const long long n = px / HW, pix = px - n * HW;
-            y[(((long long)s * N + n) * p.K + k) * HW + pix] = acc[0][r] + b;
-          }
+          const int k = acc_row(r, lane);
+          if (k < p.K) yo[(long long)k * HW] = la[0][r] + la[1][r] + Bsh[MAXNH * FW + k];
         }
       }
     }
@@ -540,11 +616,13 @@ extern "C" int pmu_fcomb_fwd(const float* feat, const float* zb, const float* co
                              float* y, void* stream) {
   FcombW p;
   PMU_REQUIRE(feat && zb && y && S > 0 && N > 0 && H > 0 && W > 0 && make_w(p, w, b, wl, bl, F, L, K, NH));
+  PMU_REQUIRE(F % 4 == 0);
   const long long HW = (long long)H * W;
-  const long long ntiles = ((long long)N * HW + FT - 1) / FT;
-  const long long g = ntiles < 1024 ? ntiles : 1024;
+  const long long ngroups = ((long long)N * HW + 31) / 32;
+  long long g = (ngroups + 3) / 4;
+  if (g > 512) g = 512;  // persistent: 2 blocks per CU
   hipLaunchKernelGGL(fcomb_fwd_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, feat, zb, p, S, N, HW, y,
-                     ntiles);
+                     ngroups);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

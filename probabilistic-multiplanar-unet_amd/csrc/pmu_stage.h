@@ -21,6 +21,18 @@ __device__ __forceinline__ float4 pmu_max4(float4 a, float4 b) {
   return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
 }
 
+// AvgPool2d(2, 2, ceil_mode=True) of BN+ReLU values: v00 already transformed; the divisor is the
+// number of window elements inside the input (the reference's ceil-mode windows at the edge)
+__device__ __forceinline__ float4 pmu_avg4(float4 v00, const float4 (&x)[4], unsigned em, float4 sc, float4 sh) {
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 a = (em & 1u) ? pmu_bnrelu4(x[1], sc, sh) : z;
+  const float4 b = (em & 2u) ? pmu_bnrelu4(x[2], sc, sh) : z;
+  const float4 d = (em & 4u) ? pmu_bnrelu4(x[3], sc, sh) : z;
+  const float cnt = (float)((1 + (em & 1u)) * (1 + ((em >> 1) & 1u)));
+  return make_float4((((v00.x + a.x) + b.x) + d.x) / cnt, (((v00.y + a.y) + b.y) + d.y) / cnt,
+                     (((v00.z + a.z) + b.z) + d.z) / cnt, (((v00.w + a.w) + b.w) + d.w) / cnt);
+}
+
 template <int MODE, int POOL, int NI>
 __device__ __forceinline__ void stage_items_fast(const DevSrc& s, int c, int n, const int (&ih)[NI],
                                                  const int (&iw)[NI], const int (&dst)[NI], float* lds) {
@@ -34,15 +46,18 @@ __device__ __forceinline__ void stage_items_fast(const DevSrc& s, int c, int n, 
     kx = *reinterpret_cast<const float4*>(s.coef + 3 * s.C + c);
     kc = *reinterpret_cast<const float4*>(s.coef + 4 * s.C + c);
   }
-  constexpr int NL = (POOL == PMU_POOL_MAX2) ? 4 : 1;
+  constexpr bool P4 = POOL == PMU_POOL_MAX2 || POOL == PMU_POOL_AVG2CEIL;
+  constexpr int NL = P4 ? 4 : 1;
   float4 xv[NI][NL];
   float4 zv[NI];
   bool ok[NI];
+  unsigned em[NI];  // AvgPool2d(ceil): which of the window's (0,1), (1,0), (1,1) elements exist
   const long long rs = (long long)s.W * s.C;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     int hs = ih[i] - s.off_h, ws = iw[i] - s.off_w;
-    if (POOL == PMU_POOL_MAX2) { hs *= 2; ws *= 2; }
+    if (P4) { hs *= 2; ws *= 2; }
+    // max pool (floor) needs the whole window inside; avg pool (ceil) only its first element
     const int lim_h = (POOL == PMU_POOL_MAX2) ? s.H - 1 : s.H;
     const int lim_w = (POOL == PMU_POOL_MAX2) ? s.W - 1 : s.W;
     ok[i] = (ih[i] != PMU_NO_ITEM) && hs >= 0 && ws >= 0 && hs < lim_h && ws < lim_w;
@@ -52,6 +67,13 @@ __device__ __forceinline__ void stage_items_fast(const DevSrc& s, int c, int n, 
       xv[i][1] = *reinterpret_cast<const float4*>(s.x + idx + s.C);
       xv[i][2] = *reinterpret_cast<const float4*>(s.x + idx + rs);
       xv[i][3] = *reinterpret_cast<const float4*>(s.x + idx + rs + s.C);
+    }
+    if constexpr (POOL == PMU_POOL_AVG2CEIL) {
+      const bool e01 = ok[i] && ws + 1 < s.W, e10 = ok[i] && hs + 1 < s.H;
+      em[i] = (e01 ? 1u : 0u) | (e10 ? 2u : 0u) | ((e01 && e10) ? 4u : 0u);
+      xv[i][1] = *reinterpret_cast<const float4*>(s.x + idx + (e01 ? s.C : 0));
+      xv[i][2] = *reinterpret_cast<const float4*>(s.x + idx + (e10 ? rs : 0));
+      xv[i][3] = *reinterpret_cast<const float4*>(s.x + idx + ((e01 && e10) ? rs + s.C : 0));
     }
     if (MODE == PMU_SRC_BNBWD) zv[i] = *reinterpret_cast<const float4*>(s.z + idx);
   }
@@ -68,6 +90,7 @@ __device__ __forceinline__ void stage_items_fast(const DevSrc& s, int c, int n, 
         v = pmu_max4(v, pmu_bnrelu4(xv[i][2], sc, sh));
         v = pmu_max4(v, pmu_bnrelu4(xv[i][3], sc, sh));
       }
+      if constexpr (POOL == PMU_POOL_AVG2CEIL) v = pmu_avg4(v, xv[i], em[i], sc, sh);
     } else {
       const float4 d = xv[i][0], z = zv[i];
       v = make_float4(pmu_bnbwd1(d.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x), pmu_bnbwd1(d.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y),
@@ -79,7 +102,7 @@ __device__ __forceinline__ void stage_items_fast(const DevSrc& s, int c, int n, 
 }
 
 // Stage NI items of frame channels [cbase, cbase + span) — this thread's quad is cbase + 4*cq.
-// Fast when the span lies inside one source (C % 4 == 0, no avg pool); generic otherwise.
+// Fast when the span lies inside one source (C % 4 == 0); generic otherwise.
 template <int NI>
 __device__ __forceinline__ void stage_items(const DevFrame& F, int n, int cbase, int span, int cq,
                                             const int (&ih)[NI], const int (&iw)[NI], const int (&dst)[NI],
@@ -96,6 +119,8 @@ __device__ __forceinline__ void stage_items(const DevFrame& F, int n, int cbase,
     }
     if (s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU)
       return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_MAX2, NI>(s, c, n, ih, iw, dst, lds);
+    if (s.pool == PMU_POOL_AVG2CEIL && s.mode == PMU_SRC_BNRELU)
+      return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_AVG2CEIL, NI>(s, c, n, ih, iw, dst, lds);
   }
 #pragma unroll
   for (int i = 0; i < NI; ++i)

@@ -38,6 +38,7 @@ struct TileRegs {
   float4 d[ND], dz[ND];
   float4 x[NX][4];
   bool dok[ND], xok[NX];
+  unsigned xem[NX];  // avg pool (ceil): window elements present
 };
 
 // fast-path descriptor: the block's 64 dz channels and 64 act channels each lie in one source
@@ -60,7 +61,7 @@ __device__ __forceinline__ void tile_load(const FastOps& f, int n, int h0, int w
     r.dz[i] = *reinterpret_cast<const float4*>(f.ds.z + idx);
   }
   const DevSrc& s = f.xs;
-  const bool mp = s.pool == PMU_POOL_MAX2;
+  const bool mp = s.pool == PMU_POOL_MAX2, ap = s.pool == PMU_POOL_AVG2CEIL;
   const long long rs = (long long)s.W * s.C;
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
@@ -68,7 +69,7 @@ __device__ __forceinline__ void tile_load(const FastOps& f, int n, int h0, int w
     const int hp = it >> 4;
     const int hr = hp / HW2, hc = hp - hr * HW2;
     int hs = h0 - 1 + hr - s.off_h, ws = w0 - 1 + hc - s.off_w;
-    if (mp) { hs *= 2; ws *= 2; }
+    if (mp || ap) { hs *= 2; ws *= 2; }
     const int lh = mp ? s.H - 1 : s.H, lw = mp ? s.W - 1 : s.W;
     r.xok[i] = it < HP * 16 && hs >= 0 && ws >= 0 && hs < lh && ws < lw;
     const long long idx = r.xok[i] ? (((long long)n * s.H + hs) * s.W + ws) * s.C + f.xc : (long long)f.xc;
@@ -77,6 +78,13 @@ __device__ __forceinline__ void tile_load(const FastOps& f, int n, int h0, int w
       r.x[i][1] = *reinterpret_cast<const float4*>(s.x + idx + s.C);
       r.x[i][2] = *reinterpret_cast<const float4*>(s.x + idx + rs);
       r.x[i][3] = *reinterpret_cast<const float4*>(s.x + idx + rs + s.C);
+    }
+    if (ap) {
+      const bool e01 = r.xok[i] && ws + 1 < s.W, e10 = r.xok[i] && hs + 1 < s.H;
+      r.xem[i] = (e01 ? 1u : 0u) | (e10 ? 2u : 0u) | ((e01 && e10) ? 4u : 0u);
+      r.x[i][1] = *reinterpret_cast<const float4*>(s.x + idx + (e01 ? s.C : 0));
+      r.x[i][2] = *reinterpret_cast<const float4*>(s.x + idx + (e10 ? rs : 0));
+      r.x[i][3] = *reinterpret_cast<const float4*>(s.x + idx + ((e01 && e10) ? rs + s.C : 0));
     }
   }
 }
@@ -103,7 +111,7 @@ __device__ __forceinline__ void tile_store(const FastOps& f, const TileRegs& r, 
     if (!r.dok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
     *reinterpret_cast<float4*>(Ds + (it >> 4) * WLS + 4 * cq) = v;
   }
-  const bool mp = f.xs.pool == PMU_POOL_MAX2;
+  const bool mp = f.xs.pool == PMU_POOL_MAX2, ap = f.xs.pool == PMU_POOL_AVG2CEIL;
   const bool raw = f.xs.mode == PMU_SRC_RAW;
   float4 xsc = make_float4(0.f, 0.f, 0.f, 0.f), xsh = xsc;
   if (!raw) {
@@ -124,6 +132,7 @@ __device__ __forceinline__ void tile_store(const FastOps& f, const TileRegs& r, 
         v = pmu_max4(v, pmu_bnrelu4(r.x[i][2], xsc, xsh));
         v = pmu_max4(v, pmu_bnrelu4(r.x[i][3], xsc, xsh));
       }
+      if (ap) v = pmu_avg4(v, r.x[i], r.xem[i], xsc, xsh);
     }
     if (!r.xok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
     *reinterpret_cast<float4*>(Xs + (it >> 4) * WLS + 4 * cq) = v;
@@ -150,11 +159,13 @@ __device__ __forceinline__ void tile_stage_generic(const DevFrame& D, const DevF
 
 // FAST: every block's 64 dz channels / 64 act channels lie in one source each (host-checked);
 // the generic instantiation stages synchronously through frame_value4.
-template <bool FAST>
+// TWL = log2 of the pixel-tile width (compile-time: with the K loop fully unrolled every LDS
+// operand address is the wave's base plus an immediate offset, no per-step VALU).
+template <bool FAST, int TWL>
 __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int TW = 1 << a.twl, TH = WPIX >> a.twl, HW2 = TW + 2, HP = (TH + 2) * HW2;
+  constexpr int TW = 1 << TWL, TH = WPIX >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
   const int nco = pmu_cdiv_dev(a.Cout, WB);
   const int co0 = (blockIdx.x % nco) * WB, ci0 = (blockIdx.x / nco) * WB;
   const int split = blockIdx.y;
@@ -169,7 +180,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
   const bool x_in0 = ci0 + WB <= X.C0, x_in1 = X.nsrc > 1 && ci0 >= X.C0 && ci0 + WB <= X.C;
   const DevSrc& xsrc = x_in0 ? X.s0 : X.s1;
   const bool x_fast = X.vec && (x_in0 || x_in1) && xsrc.mode != PMU_SRC_BNBWD &&
-                      (xsrc.pool == PMU_POOL_NONE || (xsrc.pool == PMU_POOL_MAX2 && xsrc.mode == PMU_SRC_BNRELU));
+                      (xsrc.pool == PMU_POOL_NONE || xsrc.mode == PMU_SRC_BNRELU);
   const bool fast = FAST && d_fast && x_fast;
   (void)fast;
   FastOps f;
@@ -201,10 +212,10 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
     int n, h0, w0;
     origin(t_beg, n, h0, w0);
     if constexpr (FAST) {
-      tile_load(f, n, h0, w0, a.twl, HW2, HP, tid, regs);
+      tile_load(f, n, h0, w0, TWL, HW2, HP, tid, regs);
       tile_store(f, regs, HP, tid, smem);
     } else {
-      tile_stage_generic(D, X, n, h0, w0, a.twl, HW2, HP, co0, ci0, tid, smem);
+      tile_stage_generic(D, X, n, h0, w0, TWL, HW2, HP, co0, ci0, tid, smem);
     }
   }
   __syncthreads();
@@ -215,23 +226,27 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
     int nn = 0, nh0 = 0, nw0 = 0;
     if (more) {
       origin(tile + 1, nn, nh0, nw0);
-      if constexpr (FAST) tile_load(f, nn, nh0, nw0, a.twl, HW2, HP, tid, regs);  // in flight during the MFMAs
+      if constexpr (FAST) tile_load(f, nn, nh0, nw0, TWL, HW2, HP, tid, regs);  // in flight during the MFMAs
     }
     const float* Ds = smem + cur * SLOT;
     const float* Xs = Ds + WPIX * WLS;
-#pragma unroll 4
+    // lane half h takes pixels 2ks+h; TW is even, so both halves of a step share the row
+    const int h = lane >> 5;
+    const float* da = Ds + h * WLS + cof * 32 + (lane & 31);
+    const float* xa = Xs + (kh * HW2 + h) * WLS + cif * 32 + (lane & 31);
+#pragma unroll 8
     for (int ks = 0; ks < WPIX / 2; ++ks) {
-      const int px = 2 * ks + (lane >> 5);
-      const int r = px >> a.twl, c = px & (TW - 1);
-      const float av = Ds[px * WLS + cof * 32 + (lane & 31)];
-      const float* xb = Xs + ((r + kh) * HW2 + c) * WLS + cif * 32 + (lane & 31);
+      const int px0 = 2 * ks;  // constant within an unrolled group: immediate LDS offsets
+      const int r = px0 >> TWL, c = px0 & (TW - 1);
+      const float av = da[px0 * WLS];
+      const float* xb = xa + (r * HW2 + c) * WLS;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) acc[kw] = mfma_f32_32x32x2(av, xb[kw * WLS], acc[kw]);
     }
     if (more) {
       float* nxt = smem + (cur ^ 1) * SLOT;
       if constexpr (FAST) tile_store(f, regs, HP, tid, nxt);
-      else tile_stage_generic(D, X, nn, nh0, nw0, a.twl, HW2, HP, co0, ci0, tid, nxt);
+      else tile_stage_generic(D, X, nn, nh0, nw0, TWL, HW2, HP, co0, ci0, tid, nxt);
     }
     __syncthreads();
   }
@@ -306,13 +321,16 @@ extern "C" int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int 
   fast = fast && a.act.vec && (a.act.C0 % WB == 0) && (Cin % WB == 0);
   for (int i = 0; i < act->nsrc; ++i) {
     const pmu_src& s = act->src[i];
-    fast = fast && s.mode != PMU_SRC_BNBWD &&
-           (s.pool == PMU_POOL_NONE || (s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU));
+    fast = fast && s.mode != PMU_SRC_BNBWD && (s.pool == PMU_POOL_NONE || s.mode == PMU_SRC_BNRELU);
   }
-  if (fast)
-    hipLaunchKernelGGL(wgrad3x3_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(wgrad3x3_kernel<false>, grid, dim3(NT), 0, (hipStream_t)stream, a);
+  hipStream_t st = (hipStream_t)stream;
+  if (a.twl == 4) {
+    if (fast) hipLaunchKernelGGL((wgrad3x3_kernel<true, 4>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((wgrad3x3_kernel<false, 4>), grid, dim3(NT), 0, st, a);
+  } else {
+    if (fast) hipLaunchKernelGGL((wgrad3x3_kernel<true, 3>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((wgrad3x3_kernel<false, 3>), grid, dim3(NT), 0, st, a);
+  }
   PMU_CHECK_LAUNCH();
   const long long E = 9LL * Cout * Cin;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0, (hipStream_t)stream,
