@@ -8,7 +8,7 @@
 //   clip_grad_value_ + SGD(momentum) (PMU/train.py:65,108-110)
 //   dice_coeff counts with argmax/one-hot (PMU/dice_loss.py:5-12, trainer/unet_trainer.py:39-58)
 // All reductions write per-block partial slabs that are summed in a fixed order (fp64).
-#include "pmu_common.h"
+#include "pmu_stage.h"
 
 namespace {
 
@@ -352,6 +352,116 @@ __global__ __launch_bounds__(256) void wgrad1x1_kernel(const float* __restrict__
   }
 }
 
+// ---- channel-quad x pixel-group fast paths of the 1x1 head (single unpooled BN+ReLU source,
+// C = 4*CQ with CQ a power of two <= 64): a wave reads CQ consecutive quads of 64/CQ pixels, i.e.
+// contiguous runs of NHWC rows, instead of one strided row per thread.
+__device__ __forceinline__ bool head_fast_frame(const DevFrame& f) {
+  const int CQ = f.C >> 2;
+  return f.nsrc == 1 && f.s0.mode == PMU_SRC_BNRELU && f.s0.pool == PMU_POOL_NONE && f.s0.off_h == 0 &&
+         f.s0.off_w == 0 && f.s0.H == f.H && f.s0.W == f.W && (f.C & 3) == 0 && CQ <= 64 && (CQ & (CQ - 1)) == 0;
+}
+
+constexpr int HPPB = 2048;  // pixels per block in the fast head kernels
+
+__global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                            int do_sigmoid, const float* __restrict__ w, int K, int C,
+                                                            long long HW, long long P, float* __restrict__ dl,
+                                                            float* __restrict__ da) {
+  const int tid = threadIdx.x;
+  const int CQ = C >> 2, PG = 256 / CQ;
+  const int cq = tid & (CQ - 1), pg = tid / CQ;
+  float4 wq[HEAD_KMAX];
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k)
+    wq[k] = k < K ? *reinterpret_cast<const float4*>(w + k * C + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const long long pend = min(P, (long long)(blockIdx.x + 1) * HPPB);
+  for (long long p = (long long)blockIdx.x * HPPB + pg; p < pend; p += PG) {
+    const long long n = p / HW, pix = p - n * HW;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < HEAD_KMAX; ++k) {
+      if (k >= K) break;
+      const long long i = (n * K + k) * HW + pix;
+      float g = dy[i];
+      if (do_sigmoid) { const float sg = y[i]; g = g * (sg * (1.f - sg)); }
+      if (cq == 0) dl[i] = g;
+      o.x = fmaf(g, wq[k].x, o.x); o.y = fmaf(g, wq[k].y, o.y);
+      o.z = fmaf(g, wq[k].z, o.z); o.w = fmaf(g, wq[k].w, o.w);
+    }
+    *reinterpret_cast<float4*>(da + p * C + 4 * cq) = o;
+  }
+}
+
+// dw[k][c] / db[k] partials per block: ws[block][k][C+1]; shuffles over the wave's pixel groups,
+// LDS over the 4 waves (fixed order)
+__global__ __launch_bounds__(256) void wgrad1x1_fast_kernel(const float* __restrict__ dl, DevFrame f, int K,
+                                                            float* __restrict__ ws) {
+  __shared__ float red[4 * HEAD_KMAX * 260];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = f.C, CQ = C >> 2, PG = 256 / CQ;
+  const int cq = tid & (CQ - 1), pg = tid / CQ;
+  const long long HW = (long long)f.H * f.W, P = (long long)f.N * HW;
+  const float4 sc = *reinterpret_cast<const float4*>(f.s0.coef + 4 * cq);
+  const float4 sh = *reinterpret_cast<const float4*>(f.s0.coef + C + 4 * cq);
+  float4 acc[HEAD_KMAX];
+  float accb[HEAD_KMAX];
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k) { acc[k] = make_float4(0.f, 0.f, 0.f, 0.f); accb[k] = 0.f; }
+  const long long pend = min(P, (long long)(blockIdx.x + 1) * HPPB);
+  for (long long p = (long long)blockIdx.x * HPPB + pg; p < pend; p += PG) {
+    const long long n = p / HW, pix = p - n * HW;
+    const float4 a = pmu_bnrelu4(*reinterpret_cast<const float4*>(f.s0.x + p * C + 4 * cq), sc, sh);
+#pragma unroll
+    for (int k = 0; k < HEAD_KMAX; ++k) {
+      if (k >= K) break;
+      const float g = dl[(n * K + k) * HW + pix];
+      acc[k].x = fmaf(g, a.x, acc[k].x); acc[k].y = fmaf(g, a.y, acc[k].y);
+      acc[k].z = fmaf(g, a.z, acc[k].z); acc[k].w = fmaf(g, a.w, acc[k].w);
+      accb[k] += g;
+    }
+  }
+  const int CW = C + 1;
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k) {
+    if (k >= K) break;
+    float v[5] = {acc[k].x, acc[k].y, acc[k].z, acc[k].w, accb[k]};
+#pragma unroll
+    for (int e = 0; e < 5; ++e)
+      for (int o = CQ; o < 64; o <<= 1) v[e] += __shfl_xor(v[e], o, 64);
+    if (lane < CQ) {  // after the shuffles these lanes hold the wave's sums (all lanes when CQ == 64)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[(wave * HEAD_KMAX + k) * 260 + 4 * cq + e] = v[e];
+      if (cq == 0) red[(wave * HEAD_KMAX + k) * 260 + C] = v[4];
+    }
+  }
+  __syncthreads();
+  for (int o = tid; o < K * CW; o += 256) {
+    const int k = o / CW, c = o - k * CW;
+    float t = 0.f;
+    for (int wv = 0; wv < 4; ++wv) t += red[(wv * HEAD_KMAX + k) * 260 + c];
+    ws[(long long)blockIdx.x * K * CW + o] = t;
+  }
+}
+
+// out[o] = sum_r ws[r][o] for o < K*(C+1), split into dw[k][c] and db[k]; 64 outputs x 4 row phases
+__global__ __launch_bounds__(256) void rows_sum_split4_kernel(const float* __restrict__ ws, int R, int K, int C,
+                                                              float* dw, float* db) {
+  __shared__ double red[256];
+  const int CW = C + 1, Wd = K * CW;
+  const int o = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  double s = 0.0;
+  if (o < Wd)
+    for (int r = ph; r < R; r += 4) s += ws[(long long)r * Wd + o];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && o < Wd) {
+    const double t = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+    const int k = o / CW, c = o - k * CW;
+    if (c < C) dw[k * C + c] = (float)t;
+    else if (db) db[k] = (float)t;
+  }
+}
+
 __global__ void rows_sum_split_kernel(const float* __restrict__ ws, int R, int K, int C, float* dw, float* db) {
   const int o = blockIdx.x * blockDim.x + threadIdx.x;  // k*(C+1) + c
   const int CW = C + 1;
@@ -523,6 +633,13 @@ extern "C" int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, 
   return PMU_OK;
 }
 
+static bool host_head_fast(const pmu_frame* in) {
+  const pmu_src& s = in->src[0];
+  const int CQ = s.C >> 2;
+  return in->nsrc == 1 && s.mode == PMU_SRC_BNRELU && s.pool == PMU_POOL_NONE && s.off_h == 0 && s.off_w == 0 &&
+         s.H == in->H && s.W == in->W && (s.C & 3) == 0 && CQ <= 64 && (CQ & (CQ - 1)) == 0;
+}
+
 extern "C" int pmu_head1x1_fwd(const pmu_frame* in, const float* w, const float* b, int K, int do_sigmoid,
                                float* y, void* stream) {
   PMU_REQUIRE(valid_frame(in) && w && y && K >= 1 && K <= HEAD_KMAX);
@@ -538,6 +655,13 @@ extern "C" int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, 
                                int N, int H, int W, float* dl, float* da, void* stream) {
   PMU_REQUIRE(dy && w && dl && da && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y));
   const long long P = (long long)N * H * W;
+  const int CQ = C >> 2;
+  if ((C & 3) == 0 && CQ <= 64 && (CQ & (CQ - 1)) == 0) {
+    hipLaunchKernelGGL(head_bwd_fast_kernel, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
+                       dy, y, do_sigmoid, w, K, C, (long long)H * W, P, dl, da);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)pmu_cdiv(P, 256)), dim3(256), 0, (hipStream_t)stream,
                      dy, y, do_sigmoid, w, K, C, N, H, W, dl, da);
   PMU_CHECK_LAUNCH();
@@ -545,7 +669,8 @@ extern "C" int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, 
 }
 
 extern "C" size_t pmu_wgrad1x1_ws(int P, int K, int C) {
-  return (size_t)pmu_cdiv(P, W1_PPB) * K * (C + 1) * sizeof(float);
+  const int R = pmu_cdiv(P, W1_PPB) > pmu_cdiv(P, HPPB) ? pmu_cdiv(P, W1_PPB) : pmu_cdiv(P, HPPB);
+  return (size_t)R * K * (C + 1) * sizeof(float);
 }
 
 extern "C" int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float* dw, float* db, float* ws,
@@ -554,11 +679,15 @@ extern "C" int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float*
   const DevFrame f = make_dev_frame(act);
   PMU_REQUIRE(f.C <= 256);
   const long long P = (long long)act->N * act->H * act->W;
-  const int R = pmu_cdiv(P, W1_PPB);
+  const bool fast = host_head_fast(act);
+  const int R = fast ? pmu_cdiv(P, HPPB) : pmu_cdiv(P, W1_PPB);
   PMU_REQUIRE(ws_bytes >= (size_t)R * K * (f.C + 1) * sizeof(float));
-  hipLaunchKernelGGL(wgrad1x1_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dl, f, K, ws);
+  if (fast)
+    hipLaunchKernelGGL(wgrad1x1_fast_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dl, f, K, ws);
+  else
+    hipLaunchKernelGGL(wgrad1x1_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dl, f, K, ws);
   PMU_CHECK_LAUNCH();
-  hipLaunchKernelGGL(rows_sum_split_kernel, dim3((unsigned)pmu_cdiv(K * (f.C + 1), 256)), dim3(256), 0,
+  hipLaunchKernelGGL(rows_sum_split4_kernel, dim3((unsigned)pmu_cdiv(K * (f.C + 1), 64)), dim3(256), 0,
                      (hipStream_t)stream, (const float*)ws, R, K, f.C, dw, db);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
