@@ -8,7 +8,7 @@
 // du is the gradient of the concat's "up" half in the skip's frame; the convT output sits at
 // (off_h, off_w) inside it (F.pad, unet_parts.py:58-62).
 // Tile 128x128x16, 4 waves (2x2), wave tile 64x64 = 2x2 32x32 accumulators, LDS rows k-contiguous.
-#include "pmu_common.h"
+#include "pmu_stage.h"
 
 namespace {
 
@@ -304,6 +304,140 @@ __global__ __launch_bounds__(256, 2) void convT_wgrad_kernel(TwArgs a) {
   }
 }
 
+// registers of one in-flight tile of convT_wgrad_pipe_kernel (a struct passed by reference to
+// inlined functions stays in VGPRs; captured by a lambda it was placed in scratch)
+struct TwRegs {
+  float4 rx0, rx1, rd[8];
+  bool ox0, ox1;
+  unsigned od;
+};
+
+__device__ __forceinline__ void tw_load(const TwArgs& a, int tile, int ci0, int co0, int tid, TwRegs& g) {
+  const DevSrc& xs = a.act.s0;
+  const int H = a.act.H, W = a.act.W;
+  const int TW = 1 << a.twl, TH = TPIX >> a.twl;
+  const int cq = tid & 15;
+  int t = tile;
+  const int tw = t % a.tiles_w; t /= a.tiles_w;
+  const int th = t % a.tiles_h; t /= a.tiles_h;
+  const long long n = t;
+  const int i0 = th * TH, j0 = tw * TW;
+  const int px = tid >> 4;  // act items tid and tid + 256: pixels px and px + 16
+  const int i = i0 + (px >> a.twl), j = j0 + (px & (TW - 1));
+  g.ox0 = i < H && j < W;
+  g.rx0 = *reinterpret_cast<const float4*>(xs.x + (g.ox0 ? ((n * H + i) * W + j) * xs.C : 0) + ci0 + 4 * cq);
+  const int px1 = px + 16;
+  const int i1 = i0 + (px1 >> a.twl), j1 = j0 + (px1 & (TW - 1));
+  g.ox1 = i1 < H && j1 < W;
+  g.rx1 = *reinterpret_cast<const float4*>(xs.x + (g.ox1 ? ((n * H + i1) * W + j1) * xs.C : 0) + ci0 + 4 * cq);
+  unsigned od = 0u;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int it = tid + 256 * r;
+    const int p = (it >> 4) & (TPIX - 1), ab = it >> 9;
+    const int ii = i0 + (p >> a.twl), jj = j0 + (p & (TW - 1));
+    const bool ok = ii < H && jj < W;
+    od |= ok ? (1u << r) : 0u;
+    const long long base =
+        ok ? ((n * a.Hd + a.off_h + 2 * ii + (ab >> 1)) * a.Wd + a.off_w + 2 * jj + (ab & 1)) * a.Cout : 0;
+    g.rd[r] = *reinterpret_cast<const float4*>(a.du + base + co0 + 4 * cq);
+  }
+  g.od = od;
+}
+
+__device__ __forceinline__ void tw_store(const TwRegs& g, int tid, float4 xsc, float4 xsh, float* buf) {
+  float* Xs = buf;
+  float* Ds = buf + TPIX * TB;
+  const int cq = tid & 15, px = tid >> 4;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 x0 = pmu_bnrelu4(g.rx0, xsc, xsh), x1 = pmu_bnrelu4(g.rx1, xsc, xsh);
+  if (!g.ox0) x0 = z4;
+  if (!g.ox1) x1 = z4;
+  *reinterpret_cast<float4*>(Xs + px * TB + 4 * cq) = x0;
+  *reinterpret_cast<float4*>(Xs + (px + 16) * TB + 4 * cq) = x1;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int it = tid + 256 * r;
+    const int p = (it >> 4) & (TPIX - 1), ab = it >> 9;
+    float4 v = g.rd[r];  // value select (a select of the two lvalues becomes an address select -> scratch)
+    if (!((g.od >> r) & 1u)) v = z4;
+    *reinterpret_cast<float4*>(Ds + (ab * TPIX + p) * TB + 4 * cq) = v;
+  }
+}
+
+// Pipelined variant (act = one unpooled BN+ReLU source, Cin and Cout multiples of TB): the next
+// tile's 2 act float4 and 8 du float4 per thread are loaded into registers before the current
+// tile's 64 MFMAs per wave and written to the other half of a double-buffered LDS ring after them
+// (2 x 40 KB: still 2 blocks per CU), one barrier per tile.
+__global__ __launch_bounds__(256, 2) void convT_wgrad_pipe_kernel(TwArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * (TPIX * TB + 4 * TPIX * TB)];
+  constexpr int SL = TPIX * TB + 4 * TPIX * TB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nci = a.Cin / TB;
+  const int ci0 = (blockIdx.x % nci) * TB, co0 = (blockIdx.x / nci) * TB;
+  const int split = blockIdx.y;
+  const int cif = wave >> 1, cof = wave & 1;
+  const bool do_bias = (a.bws != nullptr) && ci0 == 0;
+  const DevSrc& xs = a.act.s0;
+  const int cq = tid & 15;
+  const float4 xsc = *reinterpret_cast<const float4*>(xs.coef + ci0 + 4 * cq);
+  const float4 xsh = *reinterpret_cast<const float4*>(xs.coef + xs.C + ci0 + 4 * cq);
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bsum = 0.f;
+
+  TwRegs rg;
+
+  const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
+  const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);
+  if (t_beg < t_end) {
+    tw_load(a, t_beg, ci0, co0, tid, rg);
+    tw_store(rg, tid, xsc, xsh, smem);
+  }
+  __syncthreads();
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    const int cur = (tile - t_beg) & 1;
+    const bool more = tile + 1 < t_end;
+    if (more) tw_load(a, tile + 1, ci0, co0, tid, rg);
+    const float* Xs = smem + cur * SL;
+    const float* Ds = Xs + TPIX * TB;
+    if (do_bias) {  // thread -> (co = tid & 63, tap = tid >> 6): sum over the tile's pixels
+      const float* d = Ds + (tid >> 6) * TPIX * TB + (tid & 63);
+#pragma unroll 8
+      for (int px = 0; px < TPIX; ++px) bsum += d[px * TB];
+    }
+#pragma unroll
+    for (int ks = 0; ks < TPIX / 2; ++ks) {
+      const int px = 2 * ks + (lane >> 5);
+      const float av = Xs[px * TB + cif * 32 + (lane & 31)];
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) {
+        const float bv = Ds[(ab * TPIX + px) * TB + cof * 32 + (lane & 31)];
+        acc[ab] = mfma_f32_32x32x2(av, bv, acc[ab]);
+      }
+    }
+    if (more) tw_store(rg, tid, xsc, xsh, smem + (cur ^ 1) * SL);
+    __syncthreads();
+  }
+  const int co = co0 + cof * 32 + (lane & 31);
+#pragma unroll
+  for (int ab = 0; ab < 4; ++ab)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = ci0 + cif * 32 + acc_row(r, lane);
+      a.ws[(((long long)split * 4 + ab) * a.Cin + ci) * a.Cout + co] = acc[ab][r];
+    }
+  if (do_bias) {
+    smem[tid] = bsum;  // LDS no longer read by the MFMA loop (last barrier passed)
+    __syncthreads();
+    if (tid < 64) a.bws[(long long)split * a.Cout + co0 + tid] = smem[tid] + smem[64 + tid] + smem[128 + tid] + smem[192 + tid];
+  }
+}
+
 // dW[ci][co][a][b] = sum_s ws[s][ab][ci][co]
 __global__ void convT_wreduce_kernel(const float* __restrict__ ws, int nsplit, int Cin, int Cout, float* __restrict__ dw) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (ab*Cin + ci)*Cout + co
@@ -459,17 +593,17 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
     } else {
       const int ab = col / p.Cout, co = col - ab * p.Cout;
       const float b = p.bias ? p.bias[co] : 0.f;
+      const unsigned Wu = (unsigned)p.W, Hu = (unsigned)p.H;  // 32-bit decode (M < 2^31, host-checked)
+      float* outc = p.out + (long long)(ab >> 1) * 2 * p.W * p.Cout + (ab & 1) * p.Cout + co;
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const long long m = m0 + wm * 64 + fm * 32 + acc_row(r, lane);
-          if (m < p.M) {
-            const int j = (int)(m % p.W);
-            const long long t = m / p.W;
-            const int i = (int)(t % p.H);
-            const long long n = t / p.H;
-            p.out[((n * 2 * p.H + 2 * i + (ab >> 1)) * (2 * p.W) + 2 * j + (ab & 1)) * p.Cout + co] = acc[fm][fn][r] + b;
+          const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
+          if (m < (unsigned)p.M) {
+            const unsigned t = m / Wu, j = m - t * Wu;
+            const unsigned n = t / Hu, i = t - n * Hu;
+            outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * p.Cout] = acc[fm][fn][r] + b;
           }
         }
     }
@@ -529,7 +663,7 @@ extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float
                                 float* u, void* stream) {
   PMU_REQUIRE(valid_frame(in) && w && u && Cout > 0);
   const long long M = (long long)in->N * in->H * in->W;
-  if (wp && pipe_ok_fwd(in, Cout)) {
+  if (wp && pipe_ok_fwd(in, Cout) && M < (1LL << 31)) {
     PipeArgs p{};
     p.a = in->src[0].x; p.coef = in->src[0].coef; p.bp = wp; p.bias = bias; p.out = u;
     p.M = M; p.Ncols = 4 * Cout; p.K = in->src[0].C;
@@ -598,7 +732,13 @@ extern "C" int pmu_convT2x2_wgrad(const float* du, int Hd, int Wd, int off_h, in
   a.ws = ws;
   a.bws = dbias ? ws + (size_t)a.nsplit * 4 * a.Cin * Cout : nullptr;
   dim3 grid((unsigned)(pmu_cdiv(a.Cin, TB) * pmu_cdiv(Cout, TB)), (unsigned)a.nsplit);
-  hipLaunchKernelGGL(convT_wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  const pmu_src& xs = act->src[0];
+  const bool pipe = act->nsrc == 1 && xs.mode == PMU_SRC_BNRELU && xs.pool == PMU_POOL_NONE && xs.off_h == 0 &&
+                    xs.off_w == 0 && xs.H == act->H && xs.W == act->W && a.Cin % TB == 0 && Cout % TB == 0;
+  if (pipe)
+    hipLaunchKernelGGL(convT_wgrad_pipe_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(convT_wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   PMU_CHECK_LAUNCH();
   const long long E = 4LL * a.Cin * Cout;
   hipLaunchKernelGGL(convT_wreduce_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0, (hipStream_t)stream,
