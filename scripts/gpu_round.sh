@@ -1,12 +1,19 @@
-# Round evidence: GPU tests, full bench (with CPU baseline), rocprofv3 kernel trace + stats.
+# Round evidence in one call: all GPU tests, smoke, both bench lines (with CPU baseline),
+# rocprofv3 kernel-trace stats of the c2 bench command, and the FETCH/WRITE PMC passes.
 set -u
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/round; mkdir -p $O
 cd $R
-timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > $O/tests_gpu.log 2>&1; rc=$?
+timeout -k 10 700 python -m pytest tests -q -m gpu -p no:cacheprovider > $O/tests_gpu.log 2>&1; rc=$?
 echo "tests exit=$rc" >> $O/tests_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+tail -2 $O/tests_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+tail -2 $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
+timeout -k 10 600 python bench.py --workload probunet > $O/bench_c4.json 2> $O/bench_c4.err || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing > $O/prof.log 2>&1 || exit $?
+cd $R
+WL=unet bash scripts/gpu_pmc_bench.sh > $O/pmc.log 2>&1 || exit $?
+cut -c 1-200 $O/bench.json; cut -c 1-200 $O/bench_c4.json
 echo round-done
