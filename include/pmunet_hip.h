@@ -127,7 +127,7 @@ int pmu_bn_bwd_finalize(const double* acc, int G, int C, double count, const flo
                         const float* coef, const float* mean, const float* invstd, float* dgamma,
                         float* dbeta, float* dbias, float* bcoef, void* stream);
 
-/* out[P][C] = max(0, z*scale+shift) (NHWC), coef = [scale|shift]. */
+/* out[P][C] = max(0, z*scale+shift) (NHWC), coef = [scale|shift]; any C (float4 path when C % 4 == 0). */
 int pmu_bnrelu_apply(const float* z, const float* coef, long long P, int C, float* out, void* stream);
 
 /* ---- pooling backward ------------------------------------------------------------ */

@@ -157,6 +157,59 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ acc, int G, in
   bcoef[4 * C + c] = (float)kc;
 }
 
+// Scalar variant for channel counts that are not a multiple of 4 (any num_filters is legal in the
+// reference): thread t owns channels t, t+256, ... and walks the block's pixels in order.
+__global__ __launch_bounds__(256) void bn_bwd_reduce1_kernel(const float* __restrict__ da, const float* __restrict__ z,
+                                                             const float* __restrict__ coef, const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, long long P, int C,
+                                                             int ppb, float* __restrict__ part) {
+  const long long p0 = (long long)blockIdx.x * ppb;
+  const long long p1 = min(P, p0 + ppb);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float sc = coef[c], sh = coef[C + c], mu = mean[c], is = invstd[c];
+    float sg = 0.f, sgx = 0.f;
+    for (long long p = p0; p < p1; ++p) {
+      const float zz = z[p * C + c];
+      const float g = fmaf(zz, sc, sh) > 0.f ? da[p * C + c] : 0.f;
+      sg += g;
+      sgx = fmaf(g, (zz - mu) * is, sgx);
+    }
+    part[((long long)blockIdx.x * 2 + 0) * C + c] = sg;
+    part[((long long)blockIdx.x * 2 + 1) * C + c] = sgx;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool2_bwd1_kernel(const float* __restrict__ dpool, const float* __restrict__ z,
+                                                            const float* __restrict__ coef, int N, int H, int W, int C,
+                                                            float* __restrict__ dx, int accumulate) {
+  const int Hp = H / 2, Wp = W / 2;
+  const long long total = (long long)N * H * W * C;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long p = e / C;
+    const int w = (int)(p % W), h = (int)((p / W) % H);
+    const long long n = p / ((long long)W * H);
+    float o = accumulate ? dx[e] : 0.f;
+    const int hp = h >> 1, wp = w >> 1;
+    if (hp < Hp && wp < Wp) {
+      const int me = ((h & 1) << 1) | (w & 1);
+      const float sc = coef[c], sh = coef[C + c];
+      const long long b = ((n * H + 2 * hp) * W + 2 * wp) * C + c;
+      const long long off[4] = {0, C, (long long)W * C, (long long)W * C + C};
+      float best = fmaxf(0.f, fmaf(z[b], sc, sh));
+      int arg = 0;
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float v = fmaxf(0.f, fmaf(z[b + off[k]], sc, sh));
+        if (v > best) { best = v; arg = k; }
+      }
+      if (arg == me) o += dpool[((n * Hp + hp) * Wp + wp) * C + c];
+    }
+    dx[e] = o;
+  }
+}
+
 // ---------------- pooling backward ----------------
 // grid-stride over dx elements in channel quads
 __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restrict__ dpool, const float* __restrict__ z,
@@ -591,8 +644,14 @@ extern "C" int pmu_bn_bwd_tiles(int P, int C) { return pmu_cdiv(P, bn_bwd_ppb(C)
 
 extern "C" int pmu_bn_bwd_reduce(const float* da, const float* z, const float* coef, const float* mean,
                                  const float* invstd, int P, int C, float* part, void* stream) {
-  PMU_REQUIRE(da && z && coef && mean && invstd && part && P > 0 && C > 0 && C % 4 == 0);
+  PMU_REQUIRE(da && z && coef && mean && invstd && part && P > 0 && C > 0);
   const int ppb = bn_bwd_ppb(C);
+  if (C % 4 != 0) {
+    hipLaunchKernelGGL(bn_bwd_reduce1_kernel, dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0, (hipStream_t)stream, da,
+                       z, coef, mean, invstd, (long long)P, C, ppb, part);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0, (hipStream_t)stream,
                      da, z, coef, mean, invstd, (long long)P, C, ppb, part);
   PMU_CHECK_LAUNCH();
@@ -618,7 +677,13 @@ static unsigned grid_for(long long n) {
 
 extern "C" int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int N, int H, int W,
                                 int C, float* dx, int accumulate, void* stream) {
-  PMU_REQUIRE(dpool && z && coef && dx && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
+  PMU_REQUIRE(dpool && z && coef && dx && N > 0 && H > 1 && W > 1 && C > 0);
+  if (C % 4 != 0) {
+    hipLaunchKernelGGL(maxpool2_bwd1_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0,
+                       (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0,
                      (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
   PMU_CHECK_LAUNCH();
@@ -731,8 +796,25 @@ __global__ __launch_bounds__(256) void bnrelu_apply_kernel(const float* __restri
 }
 }  // namespace
 
+namespace {
+__global__ __launch_bounds__(256) void bnrelu_apply1_kernel(const float* __restrict__ z, const float* __restrict__ coef,
+                                                            long long total, int C, float* __restrict__ out) {
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    out[e] = fmaxf(0.f, fmaf(z[e], coef[c], coef[C + c]));
+  }
+}
+}  // namespace
+
 extern "C" int pmu_bnrelu_apply(const float* z, const float* coef, long long P, int C, float* out, void* stream) {
-  PMU_REQUIRE(z && coef && out && P > 0 && C > 0 && C % 4 == 0);
+  PMU_REQUIRE(z && coef && out && P > 0 && C > 0);
+  if (C % 4 != 0) {  // any channel count (scalar path)
+    hipLaunchKernelGGL(bnrelu_apply1_kernel, dim3(grid_for(P * C)), dim3(256), 0, (hipStream_t)stream, z, coef, P * C,
+                       C, out);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   const long long total4 = P * (C / 4);
   hipLaunchKernelGGL(bnrelu_apply_kernel, dim3(grid_for(total4)), dim3(256), 0, (hipStream_t)stream, z, coef, total4,
                      C, out);

@@ -70,6 +70,14 @@ __device__ __forceinline__ void mm64(const float* A, const float* W, int lane, f
 // ------------------------------------------------------------------------------------------
 constexpr int RRS = 68;  // LDS weight row stride: b128 reads of 8 rows hit distinct bank groups
 
+// channels c0..c0+3 of a row of F floats: one float4 when rows are 16-B aligned (F % 4 == 0),
+// else guarded scalar loads (any num_filters[0] <= 64 is legal in the reference)
+__device__ __forceinline__ float4 ld4_row(const float* row, int c0, int F, bool f4) {
+  if (f4) return c0 < F ? *reinterpret_cast<const float4*>(row + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  return make_float4(c0 < F ? row[c0] : 0.f, c0 + 1 < F ? row[c0 + 1] : 0.f, c0 + 2 < F ? row[c0 + 2] : 0.f,
+                     c0 + 3 < F ? row[c0 + 3] : 0.f);
+}
+
 __global__ __launch_bounds__(256, 2) void fcomb_fwd_kernel(const float* __restrict__ feat, const float* __restrict__ zb,
                                                            FcombW p, int S, int N, long long HW, float* __restrict__ y,
                                                            long long ngroups) {
@@ -99,6 +107,7 @@ __global__ __launch_bounds__(256, 2) void fcomb_fwd_kernel(const float* __restri
   __syncthreads();
 
   const int h = lane >> 5;
+  const bool f4 = (p.F & 3) == 0;
   const long long P = (long long)N * HW;
   const float* wrow = Wsh + (lane & 31) * RRS + 4 * h;  // + (row block)*RRS + kb*32 + 8q
   for (long long g = (long long)blockIdx.x * 4 + wave; g < ngroups; g += (long long)gridDim.x * 4) {
@@ -118,7 +127,7 @@ __global__ __launch_bounds__(256, 2) void fcomb_fwd_kernel(const float* __restri
       for (int q = 0; q < 4; ++q) {
         const int c0 = kb * 32 + 8 * q + 4 * h;
         float4 fv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (valid && c0 < p.F) fv = *reinterpret_cast<const float4*>(feat + pxc * p.F + c0);
+        if (valid) fv = ld4_row(feat + pxc * p.F, c0, p.F, f4);
         const float fa[4] = {fv.x, fv.y, fv.z, fv.w};
         float4 w4[2];
 #pragma unroll
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void fcomb_fwd_kernel(const float* __restri
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c0 = ob * 32 + 8 * q + 4 * h;
-          const float4 zv = c0 < p.F ? *reinterpret_cast<const float4*>(zr + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 zv = ld4_row(zr, c0, p.F, f4);
           hc[ob][4 * q + 0] = fmaxf(0.f, u[ob][4 * q + 0] + zv.x);
           hc[ob][4 * q + 1] = fmaxf(0.f, u[ob][4 * q + 1] + zv.y);
           hc[ob][4 * q + 2] = fmaxf(0.f, u[ob][4 * q + 2] + zv.z);
@@ -616,7 +625,6 @@ extern "C" int pmu_fcomb_fwd(const float* feat, const float* zb, const float* co
                              float* y, void* stream) {
   FcombW p;
   PMU_REQUIRE(feat && zb && y && S > 0 && N > 0 && H > 0 && W > 0 && make_w(p, w, b, wl, bl, F, L, K, NH));
-  PMU_REQUIRE(F % 4 == 0);
   const long long HW = (long long)H * W;
   const long long ngroups = ((long long)N * HW + 31) / 32;
   long long g = (ngroups + 3) / 4;

@@ -165,6 +165,11 @@ class ConvBNOut:
         return Src(self.z, L.SRC_BNRELU, self.bn.coef, pool=pool)
 
 
+def first_layer_ok(cin: int, cout: int) -> bool:
+    """Shapes pmu_conv_first_fwd/_wgrad take (include/pmunet_hip.h): Cin <= 4, Cout = 4q with 256 % q == 0."""
+    return 1 <= cin <= 4 and cout % 4 == 0 and 4 <= cout <= 1024 and 256 % (cout // 4) == 0 and cout <= 256
+
+
 def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H, W, training, dev,
                     planes=None) -> ConvBNOut:
     Cout = conv.out_channels
@@ -172,6 +177,10 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
     lb = L.lib()
     z = _empty(N, H, W, Cout, device=dev)
     need_stats = training or not bn.track_running_stats
+    if planes is not None and not first_layer_ok(len(planes), Cout):
+        # channel counts outside the first-layer kernel: the generic 3x3 path on a raw NHWC frame
+        srcs = [Src(torch.stack(planes, dim=-1).contiguous())]
+        planes = None
     if planes is not None:
         R = lb.pmu_conv_first_tiles(N, H, W)
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None

@@ -107,7 +107,7 @@ def test_probunet_samples_and_eval_match_reference_g3(tag, dev):
 
 
 @pytest.mark.parametrize("N,H,W,F,K,NH", [(2, 64, 64, 64, 3, 3), (3, 45, 37, 64, 3, 3), (1, 20, 13, 32, 1, 2),
-                                          (2, 16, 16, 8, 5, 1)])
+                                          (2, 16, 16, 8, 5, 1), (2, 24, 20, 30, 2, 2)])
 def test_fcomb_fwd_bwd_vs_fp64_oracle(N, H, W, F, K, NH, dev):
     """Fcomb alone at trainer width (F=64, 3 hidden layers) and at other legal shapes, including
     pixel counts that are not tile multiples; forward and every gradient vs float64 torch."""
@@ -182,3 +182,30 @@ def test_probunet_flat_grad_buffer(dev):
     for k, p in net.named_parameters():
         if p.grad is not None:
             assert lo <= p.grad.data_ptr() < hi, k
+
+
+def test_probunet_odd_filters_vs_oracle(dev):
+    """num_filters not multiples of 4 (any count is legal in the reference): every generic/scalar
+    path of the encoders, U-Net and Fcomb at once, vs the fp32 CPU oracle."""
+    from oracle.probunet_ref import probunet_train_step
+    from model import ProbabilisticUnet
+    torch.manual_seed(0)
+    net = ProbabilisticUnet(1, 3, [6, 12, 24], latent_dim=5, no_convs_fcomb=3, beta=10.0).to(dev).train()
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    g = torch.Generator().manual_seed(9)
+    N, H, W = 2, 33, 29
+    x = torch.rand(N, 1, H, W, generator=g)
+    segm = torch.randint(0, 3, (N, 1, H, W), generator=g).float()
+    eps = torch.randn(N, 5, generator=g)
+    res, gref = probunet_train_step(sd, x, segm, eps, 3, 5, 3, 3, 10.0)
+    net.forward(x.to(dev), segm.to(dev), training=True)
+    _inject(net.posterior_latent_space, eps.to(dev), "rsample")
+    elbo = net.elbo(segm.to(dev))
+    (-elbo).backward()
+    torch.cuda.synchronize()
+    assert abs(float(-elbo) - float(res["loss"])) <= LOSS_RTOL * abs(float(res["loss"]))
+    assert max_abs(net.reconstruction, res["rec"]) <= ACT_TOL
+    named = dict(net.named_parameters())
+    keys = [k for k in gref if not k.startswith("unet.outc")]
+    err, key = grad_err({k: named[k].grad for k in keys}, {k: gref[k] for k in keys})
+    assert err <= GRAD_TOL, (err, key)

@@ -18,6 +18,7 @@ CASES = [
     ([64, 128, 256], 1, 2, 64, 64),      # vector fast paths
     ([64, 128, 256, 512, 1024], 1, 2, 64, 48),  # full c2 architecture, small batch, non-square
     ([64, 128, 256, 512, 1024], 3, 2, 37, 45),  # full depth, odd sizes, CE
+    ([6, 12, 24], 3, 2, 40, 36),         # 6 channels (not a multiple of 4): scalar/generic paths
 ]
 
 
