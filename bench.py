@@ -211,16 +211,24 @@ def build_unet(args, dev, world, rank):
     opt = FusedSGD(net.parameters(), lr=1e-3, momentum=0.9, clip=0.1)
     g = torch.Generator(device="cpu").manual_seed(1 + rank)
     B, S = args.batch, args.size
-    x = torch.rand(B, 1, S, S, generator=g).to(dev)
-    if args.classes == 1:
-        tgt = (torch.rand(B, 1, S, S, generator=g) > 0.5).float().to(dev)
-        crit = nn.BCELoss()
+    crit = nn.BCELoss() if args.classes == 1 else nn.CrossEntropyLoss()
+    batches = None
+    if args.data == "phantom":
+        batches = phantom_batches(S, B, rank, world, dev)
     else:
-        tgt = torch.randint(0, args.classes, (B, S, S), generator=g).to(dev)
-        crit = nn.CrossEntropyLoss()
+        x = torch.rand(B, 1, S, S, generator=g).to(dev)
+        if args.classes == 1:
+            tgt = (torch.rand(B, 1, S, S, generator=g) > 0.5).float().to(dev)
+        else:
+            tgt = torch.randint(0, args.classes, (B, S, S), generator=g).to(dev)
     plist = list(net.parameters())
 
     def step():
+        nonlocal x, tgt
+        if batches is not None:  # multi-planar batch gathered on the GPU (one launch per tensor)
+            b = next(batches)
+            x = b["image"]
+            tgt = (b["mask"] > 0).float() if args.classes == 1 else b["mask"][:, 0].long()
         for p in plist:
             p.grad = None
         out = net(x)
@@ -236,7 +244,38 @@ def build_unet(args, dev, world, rank):
                           "fwd+BCE+bwd+clip(0.1)+SGD(0.9) per step" % (args.classes, FILTERS, S, S),
               "global_batch": B * world, "per_gpu_batch": B, "image": [S, S], "parallelism": f"dp{world}"}
     data = "synthetic (x~U[0,1), random binary masks, seeded)"
+    if args.data == "phantom":
+        config["workload"] = ("c3: " + config["workload"][4:] + "; batches of axial/coronal/sagittal slices "
+                              "gathered on the GPU from a resident %d^3 phantom (MRI_Dataset)" % S)
+        data = "synthetic seeded %d^3 ellipsoid phantom (nested-shell classes), 3-view slices, rank-sharded" % S
     return step, flops, config, data
+
+
+def phantom_batches(S, B, rank, world, dev):
+    """Endless per-rank batches of multi-planar slices (config c3): a seeded S^3 phantom with two
+    nested ellipsoid shells (classes 1, 2) resident on the GPU through MRI_Dataset; the shuffled
+    3-view index map is dealt round-robin over the ranks."""
+    import numpy as np
+    from utils.mri_dataset import MRI_Dataset
+    rng = np.random.default_rng(11)
+    ax = np.arange(S) - S / 2
+    ii, jj, kk = np.meshgrid(ax, ax, ax, indexing="ij", sparse=True)
+    r2 = (ii / (0.40 * S)) ** 2 + (jj / (0.35 * S)) ** 2 + (kk / (0.30 * S)) ** 2
+    lab = np.where(r2 < 1.0, 1.0, 0.0) + np.where(r2 < 0.35, 1.0, 0.0)
+    img = (rng.random((S, S, S)) * 200.0 + lab * 300.0).astype(np.float64)
+    ds = MRI_Dataset("/imgs", "/labs", 3, filter=True, loader=lambda p: img if "imgs" in p else lab,
+                     files=["phantom"], device=dev)
+    del img
+    order = np.random.default_rng(7).permutation(len(ds))[rank::world]
+
+    def gen():
+        i = 0
+        while True:
+            if i + B > len(order):
+                i = 0
+            yield ds.get_batch(order[i:i + B])
+            i += B
+    return gen()
 
 
 def build_probunet(args, dev, world, rank):
@@ -297,6 +336,8 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--classes", type=int, default=1)
     ap.add_argument("--workload", choices=["unet", "probunet"], default="unet")
+    ap.add_argument("--data", choices=["synthetic", "phantom"], default="synthetic",
+                    help="phantom: multi-planar slices gathered on the GPU from a resident phantom (c3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
@@ -376,7 +417,7 @@ def main():
             "vs_baseline": None, "dtype": "fp32", "data": data, "config": config,
             "step_tflops": round(flops_step / (ms * 1e-3) / 1e12, 2) if flops_step else None,
             "step_mfma_frac": round(flops_step / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4) if flops_step else None,
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "loss": float(loss),
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "loss": float(loss.detach()),
         }
         print(json.dumps(res), flush=True)
     if world > 1:

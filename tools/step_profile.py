@@ -42,7 +42,8 @@ def main():
     args = ap.parse_args()
     import bench
     from pmu_hip import _lib as L
-    ns = argparse.Namespace(batch=args.batch, size=args.size, classes=1, workload=args.workload)
+    ns = argparse.Namespace(batch=args.batch, size=args.size, classes=1, workload=args.workload,
+                            data="synthetic")
     build = bench.build_unet if args.workload == "unet" else bench.build_probunet
     step, _, _, _ = build(ns, torch.device("cuda", 0), 1, 0)
     for _ in range(2):
