@@ -96,6 +96,20 @@ size_t pmu_conv3x3_wgrad_ws(int N, int H, int W, int Cin, int Cout);
 int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int Cout, float* dw,
                       float* ws, size_t ws_bytes, void* stream);
 
+/* ---- bf16-MFMA variants (config c5, BASELINE.json configs[4]: "... bf16") --------------
+ * torch.autocast(bfloat16) arithmetic for the same operators: the operand (after the fused fp32
+ * BN/ReLU/pool/concat transform) and the weights are rounded to bf16 (RNE), products are summed in
+ * fp32 on v_mfma_f32_32x32x16_bf16, and every output (z, BN partials, dx, dw) stays fp32, so all
+ * the fp32 BN / pool / head / optimizer kernels above consume them unchanged.
+ * Weights are always pre-packed (bf16, [row block of 64][chunk of 16][tap][64][16]). */
+size_t pmu_conv3x3_packed_size_bf16(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_bf16(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream);
+/* as pmu_conv3x3_fwd / _dgrad (part uses the same pmu_conv3x3_tiles() tile count) */
+int pmu_conv3x3_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int Cout,
+                         float* z, float* part, void* stream);
+int pmu_conv3x3_dgrad_bf16(const pmu_frame* dz, const unsigned short* wp, int Cin, int Csplit,
+                           float* dx0, float* dx1, void* stream);
+
 /* ---- first layer (Cin <= 4, planes given NCHW-style, one pointer per channel) ------ */
 int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,
                        const float* w, const float* bias, int Cout, float* z, float* part,

@@ -1,0 +1,287 @@
+// 3x3 / pad 1 convolution on gfx950 bf16 MFMA (v_mfma_f32_32x32x16_bf16): config c5's precision
+// (BASELINE.json configs[4]: "5-level U-Net base=64ch bf16").
+//
+// Same operator and fusion as conv3x3.hip (nn.Conv2d(k=3, padding=1) of DoubleConv / Encoder,
+// PMU/model/unet/unet_parts.py:15,18, PMU/model/probabilistic_unet/probabilistic_unet.py:38,43,
+// with the producer's BatchNorm2d + ReLU (+ MaxPool2d(2) | AvgPool2d(2, ceil) | F.pad + torch.cat)
+// applied while the operand is staged), with the arithmetic split as torch.autocast(bfloat16) does
+// it: operands rounded to bf16 (RNE) after the fp32 BN/ReLU/pool transform, products summed in
+// fp32, outputs (pre-BN z, BN partial sums, dx) written in fp32.
+//
+// GEMM view as conv3x3.hip (M = pixels, N = output channels, K = 9 x input channels).
+// Block: 256 threads = 4 waves, 2 blocks per CU (<= 72 KB LDS each).  Tile: 256 pixels (TH x TW)
+// x BNT output channels (64 or 128); per chunk of BK = 16 input channels one (TH+2) x (TW+2) bf16
+// halo tile and 9 taps x BNT x 16 bf16 weights are staged, then every tap is ONE k-step of 16:
+// lane half h reads k = 8h..8h+7 of its row with one ds_read_b128 (48-B rows: conflict-free for
+// any 16 consecutive rows).  Wave layout: BNT = 128 -> 2 (pixels) x 2 (channels) waves of 128 px x
+// 64 ch = 4 x 2 accumulators; BNT = 64 -> 4 x 1 waves of 64 px x 64 ch = 2 x 2 accumulators.
+#include "pmu_stage.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BM = 256;      // pixels per tile
+constexpr int BK = 16;       // reduction channels per chunk (= one MFMA k-step per tap)
+constexpr int LSB = 24;      // LDS row stride in bf16 (32 B of data + 16 B pad)
+constexpr int MAX_HP = 340;  // max halo pixels: (8+2)*(32+2) = 340
+constexpr int NI = 6;        // A items per thread: ceil(340*4 / 256)
+constexpr int PJ = 64;       // packed-weight row block
+constexpr int A_ELEMS = MAX_HP * LSB;
+
+struct ConvArgsB {
+  DevFrame in;
+  const unsigned short* wp;  // packed bf16 weights [jb][ch][tap][PJ][BK]
+  const float* bias;
+  float* out0;
+  float* out1;
+  float* part;
+  int NOUT, KC, split, tiles_w, tiles_h;
+};
+
+__device__ __forceinline__ unsigned short bf16_bits(float v) {
+  return __builtin_bit_cast(unsigned short, (__bf16)v);
+}
+
+// wp[jb][ch][tap][jl][kl] = B[tap][j = jb*PJ + jl][k = ch*BK + kl] (zero padded), bf16 RNE.
+//   forward: B[tap][co][ci] = w[co][ci][tap];  dgrad: B[tap][ci][co] = w[co][ci][8 - tap]
+__global__ __launch_bounds__(256) void pack_w_bf16_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
+                                                          int njb, unsigned short* __restrict__ wp) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  const int nch = (KC + BK - 1) / BK;
+  const long long total = (long long)njb * nch * 9 * PJ * BK;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int kl = (int)(e % BK);
+    long long r = e / BK;
+    const int jl = (int)(r % PJ); r /= PJ;
+    const int tap = (int)(r % 9); r /= 9;
+    const int ch = (int)(r % nch);
+    const int jb = (int)(r / nch);
+    const int j = jb * PJ + jl, k = ch * BK + kl;
+    float v = 0.f;
+    if (j < NOUT && k < KC)
+      v = dgrad ? w[((long long)k * Cin + j) * 9 + (8 - tap)] : w[((long long)j * Cin + k) * 9 + tap];
+    wp[e] = bf16_bits(v);
+  }
+}
+
+static int packed_row_blocks(int NOUT) { return 2 * pmu_cdiv(NOUT, 2 * PJ); }
+
+template <int TWL, int BNT, bool DGRAD>
+__global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(ConvArgsB a) {
+  constexpr int FM = (BNT == 128) ? 4 : 2;  // pixel fragments per wave
+  constexpr int FN = 2;                     // channel fragments per wave
+  constexpr int WM = BM / (32 * FM);        // waves along pixels
+  constexpr int TW = 1 << TWL, TH = BM >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
+  constexpr int B_ELEMS = 9 * BNT * LSB;
+  __shared__ __attribute__((aligned(16))) unsigned short smem[A_ELEMS + B_ELEMS];
+  unsigned short* As = smem;
+  unsigned short* Bs = smem + A_ELEMS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  int t = blockIdx.x;
+  const int tw = t % a.tiles_w; t /= a.tiles_w;
+  const int th = t % a.tiles_h; t /= a.tiles_h;
+  const int n = t;
+  const int h0 = th * TH, w0 = tw * TW;
+  const int j0 = blockIdx.y * BNT;
+  const DevFrame& F = a.in;
+  const int nch = (a.KC + BK - 1) / BK;
+
+  int ih[NI], iw[NI], dst[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int it = tid + 256 * i;
+    const int hp = it >> 2;
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    ih[i] = (it < HP * 4) ? h0 - 1 + hr : PMU_NO_ITEM;
+    iw[i] = w0 - 1 + hc;
+    dst[i] = hp * LSB + 4 * (it & 3);
+  }
+  const int hsel = (lane >> 5) * 8;
+  int abase[FM], bbase[FN];
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int q = wm * 32 * FM + fm * 32 + (lane & 31);
+    abase[fm] = ((q >> TWL) * HW2 + (q & (TW - 1))) * LSB + hsel;
+  }
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) bbase[fn] = (wn * 64 + fn * 32 + (lane & 31)) * LSB + hsel;
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // packed B: this block's BNT/PJ row blocks of one chunk, 16-B units (2 per row)
+  constexpr int UNITS = 9 * BNT * 2;
+  const uint4* wsrc = reinterpret_cast<const uint4*>(a.wp);
+  const long long tile_units = 9LL * PJ * BK / 8;
+  const int jb0 = j0 / PJ;
+
+  for (int ch = 0; ch < nch; ++ch) {
+    stage_items<NI, true>(F, n, ch * BK, BK, tid & 3, ih, iw, dst, As);
+#pragma unroll
+    for (int i = 0; i < (UNITS + 255) / 256; ++i) {
+      const int u = tid + 256 * i;
+      if (UNITS % 256 == 0 || u < UNITS) {
+        const int hh = u / (9 * PJ * 2);        // row block inside the block
+        const int uu = u - hh * (9 * PJ * 2);
+        const int row = uu >> 1, qq = uu & 1;   // row = tap*PJ + jl
+        const int tap = row / PJ, jl = row - tap * PJ;
+        const uint4 v = wsrc[((long long)(jb0 + hh) * nch + ch) * tile_units + uu];
+        *reinterpret_cast<uint4*>(Bs + (tap * BNT + hh * PJ + jl) * LSB + 8 * qq) = v;
+      }
+    }
+    __syncthreads();
+
+    // BNT = 64: the next tap's operands are read ahead of the current tap's MFMAs; BNT = 128 has
+    // no registers for a second set (the partner wave on the SIMD covers the read latency)
+    constexpr int NB = (BNT == 128) ? 1 : 2;
+    bf16x8 op[NB][FM + FN];
+    auto load_ops = [&](int tap, bf16x8 (&o)[FM + FN]) {
+      const int toff = ((tap / 3) * HW2 + (tap % 3)) * LSB;
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) o[fm] = *reinterpret_cast<const bf16x8*>(As + abase[fm] + toff);
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) o[FM + fn] = *reinterpret_cast<const bf16x8*>(Bs + tap * BNT * LSB + bbase[fn]);
+    };
+    if (NB == 2) load_ops(0, op[0]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (NB == 1) load_ops(tap, op[0]);
+      else if (tap + 1 < 9) load_ops(tap + 1, op[(tap + 1) % NB]);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[tap % NB][fm], op[tap % NB][FM + fn], acc[fm][fn], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: fwd writes z (+bias) and per-tile BN partials; dgrad writes dx split in two
+  float* red = reinterpret_cast<float*>(smem);  // [WM][BNT][2]
+  float s1[FN], s2[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    s1[fn] = 0.f; s2[fn] = 0.f;
+    const int j = j0 + wn * 64 + fn * 32 + (lane & 31);
+    const bool jok = j < a.NOUT;
+    const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = wm * 32 * FM + fm * 32 + acc_row(r, lane);
+        const int h = h0 + (q >> TWL), w = w0 + (q & (TW - 1));
+        if (!jok || h >= F.H || w >= F.W) continue;
+        const long long pix = ((long long)n * F.H + h) * F.W + w;
+        const float v = acc[fm][fn][r] + b;
+        if (!DGRAD) {
+          a.out0[pix * a.NOUT + j] = v;
+          s1[fn] += v;
+          s2[fn] = fmaf(v, v, s2[fn]);
+        } else if (j < a.split) {
+          a.out0[pix * a.split + j] = v;
+        } else {
+          a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+        }
+      }
+    }
+  }
+  if (!DGRAD && a.part) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] += __shfl_xor(s1[fn], 32, 64);
+      s2[fn] += __shfl_xor(s2[fn], 32, 64);
+      if (lane < 32) {
+        const int jj = wn * 64 + fn * 32 + lane;
+        red[(wm * BNT + jj) * 2 + 0] = s1[fn];
+        red[(wm * BNT + jj) * 2 + 1] = s2[fn];
+      }
+    }
+    __syncthreads();
+    if (tid < BNT) {
+      const int j = j0 + tid;
+      if (j < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < WM; ++v) {
+          t1 += red[(v * BNT + tid) * 2 + 0];
+          t2 += red[(v * BNT + tid) * 2 + 1];
+        }
+        a.part[((long long)blockIdx.x * 2 + 0) * a.NOUT + j] = t1;
+        a.part[((long long)blockIdx.x * 2 + 1) * a.NOUT + j] = t2;
+      }
+    }
+  }
+}
+
+static int pick_twl(int W) {
+  if (W > 16) return 5;
+  if (W > 8) return 4;
+  return 3;
+}
+
+static int launch_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int NOUT, int KC, float* out0,
+                       float* out1, int split, float* part, bool dgrad, void* stream) {
+  ConvArgsB a;
+  a.in = make_dev_frame(in);
+  a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
+  a.NOUT = NOUT; a.KC = KC; a.split = split;
+  const int twl = pick_twl(in->W);
+  const int TW = 1 << twl, TH = BM / TW;
+  a.tiles_w = pmu_cdiv(in->W, TW);
+  a.tiles_h = pmu_cdiv(in->H, TH);
+  const int bnt = 64;  // BNT = 128 needs the 1-block/CU pipelined variant (register budget)
+  dim3 grid((unsigned)(a.tiles_w * a.tiles_h * in->N), (unsigned)pmu_cdiv(NOUT, bnt));
+  hipStream_t st = (hipStream_t)stream;
+#define PMU_BF(T, B, D)                                                                 \
+  if (twl == T && bnt == B && dgrad == D) {                                            \
+    hipLaunchKernelGGL((conv3x3_bf16_kernel<T, B, D>), grid, dim3(256), 0, st, a);     \
+    PMU_CHECK_LAUNCH();                                                                \
+    return PMU_OK;                                                                     \
+  }
+  PMU_BF(3, 64, false) PMU_BF(4, 64, false) PMU_BF(5, 64, false)
+  PMU_BF(3, 64, true) PMU_BF(4, 64, true) PMU_BF(5, 64, true)
+#undef PMU_BF
+  return PMU_ERR_ARG;
+}
+
+}  // namespace
+
+extern "C" size_t pmu_conv3x3_packed_size_bf16(int Cout, int Cin, int dgrad) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  return (size_t)packed_row_blocks(NOUT) * pmu_cdiv(KC, BK) * 9 * PJ * BK * sizeof(unsigned short);
+}
+
+extern "C" int pmu_conv3x3_pack_bf16(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream) {
+  PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
+  const int NOUT = dgrad ? Cin : Cout;
+  const long long total = (long long)(pmu_conv3x3_packed_size_bf16(Cout, Cin, dgrad) / sizeof(unsigned short));
+  long long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(pack_w_bf16_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad,
+                     packed_row_blocks(NOUT), wp);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_conv3x3_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int Cout,
+                                    float* z, float* part, void* stream) {
+  PMU_REQUIRE(valid_frame(in) && wp && z && Cout > 0);
+  const int Cin = in->src[0].C + (in->nsrc > 1 ? in->src[1].C : 0);
+  return launch_bf16(in, wp, bias, Cout, Cin, z, nullptr, Cout, part, false, stream);
+}
+
+extern "C" int pmu_conv3x3_dgrad_bf16(const pmu_frame* dz, const unsigned short* wp, int Cin, int Csplit, float* dx0,
+                                      float* dx1, void* stream) {
+  PMU_REQUIRE(valid_frame(dz) && dz->nsrc == 1 && wp && dx0 && Cin > 0);
+  PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
+  return launch_bf16(dz, wp, nullptr, Cin, dz->src[0].C, dx0, dx1, Csplit, nullptr, true, stream);
+}

@@ -17,6 +17,21 @@ __device__ __forceinline__ float4 pmu_bnrelu4(float4 x, float4 sc, float4 sh) {
 __device__ __forceinline__ float pmu_bnbwd1(float d, float z, float sc, float sh, float mu, float kx, float kc) {
   return fmaf(sc, fmaf(z, sc, sh) > 0.f ? d : 0.f, fmaf(kx, z - mu, kc));
 }
+// 4 operand values to LDS: fp32 (16 B at ((float*)lds)[dst]) or, for the bf16-MFMA kernels, rounded
+// to bf16 (RNE, v_cvt_pk_bf16_f32) as 8 B at ((bf16*)lds)[dst]
+typedef __bf16 pmu_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pmu_pk_bf16(float lo, float hi) {
+  const pmu_bf16x2 r = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, r);
+}
+template <bool BF>
+__device__ __forceinline__ void pmu_lds_store4(void* lds, int dst, float4 v) {
+  if constexpr (BF) {
+    *reinterpret_cast<uint2*>(reinterpret_cast<unsigned short*>(lds) + dst) = make_uint2(pmu_pk_bf16(v.x, v.y), pmu_pk_bf16(v.z, v.w));
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(lds) + dst) = v;
+  }
+}
 __device__ __forceinline__ float4 pmu_max4(float4 a, float4 b) {
   return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
 }
@@ -33,9 +48,9 @@ __device__ __forceinline__ float4 pmu_avg4(float4 v00, const float4 (&x)[4], uns
                      (((v00.z + a.z) + b.z) + d.z) / cnt, (((v00.w + a.w) + b.w) + d.w) / cnt);
 }
 
-template <int MODE, int POOL, int NI>
+template <int MODE, int POOL, int NI, bool BF = false>
 __device__ __forceinline__ void stage_items_fast(const DevSrc& s, int c, int n, const int (&ih)[NI],
-                                                 const int (&iw)[NI], const int (&dst)[NI], float* lds) {
+                                                 const int (&iw)[NI], const int (&dst)[NI], void* lds) {
   float4 sc = make_float4(0, 0, 0, 0), sh = sc, mu = sc, kx = sc, kc = sc;
   if (MODE != PMU_SRC_RAW) {
     sc = *reinterpret_cast<const float4*>(s.coef + c);
@@ -97,34 +112,34 @@ __device__ __forceinline__ void stage_items_fast(const DevSrc& s, int c, int n, 
                       pmu_bnbwd1(d.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z), pmu_bnbwd1(d.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w));
     }
     if (!ok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(lds + dst[i]) = v;
+    pmu_lds_store4<BF>(lds, dst[i], v);
   }
 }
 
 // Stage NI items of frame channels [cbase, cbase + span) — this thread's quad is cbase + 4*cq.
 // Fast when the span lies inside one source (C % 4 == 0); generic otherwise.
-template <int NI>
+template <int NI, bool BF = false>
 __device__ __forceinline__ void stage_items(const DevFrame& F, int n, int cbase, int span, int cq,
                                             const int (&ih)[NI], const int (&iw)[NI], const int (&dst)[NI],
-                                            float* lds) {
+                                            void* lds) {
   const bool in0 = cbase + span <= F.C0;
   const bool in1 = F.nsrc > 1 && cbase >= F.C0 && cbase + span <= F.C;
   if (F.vec && (in0 || in1)) {
     const DevSrc& s = in0 ? F.s0 : F.s1;
     const int c = (in0 ? cbase : cbase - F.C0) + 4 * cq;
     if (s.pool == PMU_POOL_NONE) {
-      if (s.mode == PMU_SRC_BNRELU) return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_NONE, NI>(s, c, n, ih, iw, dst, lds);
-      if (s.mode == PMU_SRC_BNBWD) return stage_items_fast<PMU_SRC_BNBWD, PMU_POOL_NONE, NI>(s, c, n, ih, iw, dst, lds);
-      return stage_items_fast<PMU_SRC_RAW, PMU_POOL_NONE, NI>(s, c, n, ih, iw, dst, lds);
+      if (s.mode == PMU_SRC_BNRELU) return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_NONE, NI, BF>(s, c, n, ih, iw, dst, lds);
+      if (s.mode == PMU_SRC_BNBWD) return stage_items_fast<PMU_SRC_BNBWD, PMU_POOL_NONE, NI, BF>(s, c, n, ih, iw, dst, lds);
+      return stage_items_fast<PMU_SRC_RAW, PMU_POOL_NONE, NI, BF>(s, c, n, ih, iw, dst, lds);
     }
     if (s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU)
-      return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_MAX2, NI>(s, c, n, ih, iw, dst, lds);
+      return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_MAX2, NI, BF>(s, c, n, ih, iw, dst, lds);
     if (s.pool == PMU_POOL_AVG2CEIL && s.mode == PMU_SRC_BNRELU)
-      return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_AVG2CEIL, NI>(s, c, n, ih, iw, dst, lds);
+      return stage_items_fast<PMU_SRC_BNRELU, PMU_POOL_AVG2CEIL, NI, BF>(s, c, n, ih, iw, dst, lds);
   }
 #pragma unroll
   for (int i = 0; i < NI; ++i)
-    if (ih[i] != PMU_NO_ITEM) *reinterpret_cast<float4*>(lds + dst[i]) = frame_value4(F, n, ih[i], iw[i], cbase + 4 * cq);
+    if (ih[i] != PMU_NO_ITEM) pmu_lds_store4<BF>(lds, dst[i], frame_value4(F, n, ih[i], iw[i], cbase + 4 * cq));
 }
 
 // ---------------------------------------------------------------------------------------------

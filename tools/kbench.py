@@ -3,7 +3,8 @@
 
     python tools/kbench.py [--ops fwd,dgrad,wgrad,convT] [--iters 20]
 
-Prints one line per (op, layer shape) with ms and TFLOP/s (f32 MFMA peak 157.3)."""
+Prints one line per (op, layer shape) with ms and TFLOP/s (% of the f32 MFMA peak 157.3, or of the
+bf16 peak 2516 for the *_bf16 ops)."""
 import argparse
 import ctypes
 import os
@@ -71,7 +72,18 @@ def main():
         from pmu_hip.engine import pack_weights
         wpf = pack_weights(w, False) if not args.unpacked else None
         wpd = pack_weights(w, True) if not args.unpacked else None
+        def packb(wt, dg):
+            n = L.lib().pmu_conv3x3_packed_size_bf16(wt.shape[0], wt.shape[1], int(dg)) // 2
+            t = torch.empty(n, dtype=torch.int16, device=dev)
+            L.call("pmu_conv3x3_pack_bf16", wt.data_ptr(), wt.shape[0], wt.shape[1], int(dg), t.data_ptr(), s)
+            return t
+        wbf = packb(w, False)
+        wbd = packb(w, True)
         ops = {
+            "fwd_bf16": lambda: L.call("pmu_conv3x3_fwd_bf16", fin, wbf.data_ptr(), b.data_ptr(), Cout,
+                                       out.data_ptr(), part.data_ptr(), s),
+            "dgrad_bf16": lambda: L.call("pmu_conv3x3_dgrad_bf16", fdz, wbd.data_ptr(), Cin, Cin, dx.data_ptr(),
+                                         None, s),
             "fwd": lambda: L.call("pmu_conv3x3_fwd", fin, w.data_ptr(), L.ptr(wpf), b.data_ptr(), Cout,
                                   out.data_ptr(), part.data_ptr(), s),
             "dgrad": lambda: L.call("pmu_conv3x3_dgrad", fdz, w.data_ptr(), L.ptr(wpd), Cin, Cin, dx.data_ptr(),
@@ -87,7 +99,8 @@ def main():
             tot.setdefault(op, [0.0, 0.0])
             tot[op][0] += ms
             tot[op][1] += flops
-            print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / 157.3 * 100:5.1f}%)",
+            peak = 2516.0 if op.endswith("bf16") else 157.3
+            print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / peak * 100:5.1f}%)",
                   flush=True)
     for op, (ms, fl) in tot.items():
         print(f"TOTAL {op:6s} {ms:8.3f} ms  {fl / (ms * 1e-3) / 1e12:7.2f} TF")
