@@ -32,6 +32,7 @@ import torch.nn as nn  # noqa: E402
 
 METRIC = "2D slices/sec fwd+bwd, 256×256×1 batch32 U-Net; Dice vs ref"
 FP32_MFMA_PEAK_TF = 157.3
+BF16_MFMA_PEAK_TF = 2516.0   # dense bf16 MFMA (MI355X_MICROARCH.md; 2.5 PF, no sparsity)
 FILTERS = [64, 128, 256, 512, 1024]
 
 
@@ -63,13 +64,23 @@ class KernelTimer:
     """HIP-event timing of every launch, with algorithmic FLOPs for the MFMA kernels."""
 
     MFMA = ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad", "pmu_convT2x2_fwd",
-            "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd")
+            "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd",
+            "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16")
 
     def __init__(self):
         self.rec = []
 
     @staticmethod
     def _flops(name, args):
+        if name == "pmu_conv3x3_fwd_bf16":
+            f = args[0]._obj
+            return 2.0 * f.N * f.H * f.W * sum(f.src[i].C for i in range(f.nsrc)) * args[3] * 9
+        if name == "pmu_conv3x3_dgrad_bf16":
+            f = args[0]._obj
+            return 2.0 * f.N * f.H * f.W * f.src[0].C * args[2] * 9
+        if name == "pmu_conv3x3_wgrad_bf16":
+            N, H, W, cout, cin = args[2], args[3], args[4], args[5], args[6]
+            return 2.0 * N * H * W * cin * cout * 9
         if name in ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad"):
             f = args[0]._obj
             cframe = sum(f.src[i].C for i in range(f.nsrc))
@@ -109,9 +120,10 @@ class KernelTimer:
         return per
 
 
-def cpu_baseline(max_seconds=25.0, workload="unet"):
+def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classes=1):
     """CPU oracle (torch-CPU restatement of the reference) on a bounded sample: batch 2 of the
-    bench geometry, 1 warm-up + timed steps until ~max_seconds (at most 5)."""
+    bench geometry, 1 warm-up + timed steps until ~max_seconds (at most 5).  The reference's CPU
+    path is fp32 only, so the c5 (bf16) sample is timed in fp32."""
     from oracle.unet_ref import unet_param_keys, unet_train_step
     from oracle.probunet_ref import probunet_train_step
     threads = min(16, os.cpu_count() or 1)
@@ -119,15 +131,18 @@ def cpu_baseline(max_seconds=25.0, workload="unet"):
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(1)
     B = 2
-    x = torch.rand(B, 1, 256, 256, generator=g)
+    x = torch.rand(B, channels, size, size, generator=g)
     if workload == "unet":
         from model import UNet
-        sd = {k: v.clone() for k, v in UNet(1, 1, FILTERS).state_dict().items()}
-        t = (torch.rand(B, 1, 256, 256, generator=g) > 0.5).float()
+        sd = {k: v.clone() for k, v in UNet(channels, classes, FILTERS).state_dict().items()}
+        if classes == 1:
+            t = (torch.rand(B, 1, size, size, generator=g) > 0.5).float()
+        else:
+            t = torch.randint(0, classes, (B, 1, size, size), generator=g)
         bufs = {k: torch.zeros_like(sd[k]) for k in unet_param_keys(sd)}
 
         def one():
-            unet_train_step(sd, x, t, 5, 1, lr=1e-3, bufs=bufs)
+            unet_train_step(sd, x, t, 5, classes, lr=1e-3, bufs=bufs)
         what = "fwd+bwd+clip+SGD steps"
     else:
         from model import ProbabilisticUnet
@@ -152,7 +167,8 @@ def cpu_baseline(max_seconds=25.0, workload="unet"):
     times.sort()
     med = times[len(times) // 2]
     return {"value": round(B / med, 4), "unit": "slices/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/{'unet' if workload == 'unet' else 'probunet'}_ref.py torch-CPU, 256x256x1, "
+            "sample": f"oracle/{'unet' if workload == 'unet' else 'probunet'}_ref.py torch-CPU fp32, "
+                      f"{size}x{size}x{channels}, {classes} class(es), "
                       f"filters {FILTERS}, batch {B}, median of {len(times)} {what} after 1 warm-up, "
                       f"{threads} threads"}
 
@@ -204,7 +220,7 @@ def build_unet(args, dev, world, rank):
     from pmu_hip.optim import FusedSGD
     import torch.distributed as dist
     torch.manual_seed(0)
-    net = UNet(1, args.classes, FILTERS).to(dev).train()
+    net = UNet(args.channels, args.classes, FILTERS).to(dev).train()
     if world > 1:  # identical replicas: broadcast rank 0's weights
         for t in list(net.parameters()) + list(net.buffers()):
             dist.broadcast(t.data, 0)
@@ -216,7 +232,7 @@ def build_unet(args, dev, world, rank):
     if args.data == "phantom":
         batches = phantom_batches(S, B, rank, world, dev)
     else:
-        x = torch.rand(B, 1, S, S, generator=g).to(dev)
+        x = torch.rand(B, args.channels, S, S, generator=g).to(dev)
         if args.classes == 1:
             tgt = (torch.rand(B, 1, S, S, generator=g) > 0.5).float().to(dev)
         else:
@@ -231,7 +247,10 @@ def build_unet(args, dev, world, rank):
             tgt = (b["mask"] > 0).float() if args.classes == 1 else b["mask"][:, 0].long()
         for p in plist:
             p.grad = None
-        out = net(x)
+        # bf16: the reference's model code under torch.autocast(bfloat16), the PyTorch idiom for
+        # config c5; the engine runs every 3x3 conv (fwd, dgrad, wgrad) on bf16 MFMA
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.precision == "bf16"):
+            out = net(x)
         loss = crit(out, tgt)
         loss.backward()
         if world > 1:
@@ -239,11 +258,16 @@ def build_unet(args, dev, world, rank):
         opt.step(grad_scale=1.0 / world)
         return loss
 
-    flops = conv_flops_per_slice(S, S, FILTERS, 1, args.classes) * B
-    config = {"workload": "c2: UNet(n_channels=1, n_classes=%d, num_filters=%s), %dx%dx1 slices, "
-                          "fwd+BCE+bwd+clip(0.1)+SGD(0.9) per step" % (args.classes, FILTERS, S, S),
+    flops = conv_flops_per_slice(S, S, FILTERS, args.channels, args.classes) * B
+    lossn = "BCE" if args.classes == 1 else "CE"
+    tag = "c5" if args.workload == "c5" else "c2"
+    config = {"workload": "%s: UNet(n_channels=%d, n_classes=%d, num_filters=%s), %dx%dx%d slices, "
+                          "fwd+%s+bwd+clip(0.1)+SGD(0.9) per step, %s" % (tag, args.channels, args.classes, FILTERS,
+                                                                         S, S, args.channels, lossn,
+                                                                         args.precision),
               "global_batch": B * world, "per_gpu_batch": B, "image": [S, S], "parallelism": f"dp{world}"}
-    data = "synthetic (x~U[0,1), random binary masks, seeded)"
+    data = "synthetic (x~U[0,1), random %s masks, seeded)" % ("binary" if args.classes == 1 else
+                                                              "%d-class" % args.classes)
     if args.data == "phantom":
         config["workload"] = ("c3: " + config["workload"][4:] + "; batches of axial/coronal/sagittal slices "
                               "gathered on the GPU from a resident %d^3 phantom (MRI_Dataset)" % S)
@@ -335,12 +359,28 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--classes", type=int, default=1)
-    ap.add_argument("--workload", choices=["unet", "probunet"], default="unet")
+    ap.add_argument("--workload", choices=["unet", "probunet", "c5"], default="unet",
+                    help="unet: c2 (default); probunet: c4; c5: UNet(3,3) on 512x512x3 slices, batch 16, bf16")
+    ap.add_argument("--channels", type=int, default=None)
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
+                    help="bf16: 3x3 convs on bf16 MFMA (torch.autocast(bfloat16) arithmetic)")
     ap.add_argument("--data", choices=["synthetic", "phantom"], default="synthetic",
                     help="phantom: multi-planar slices gathered on the GPU from a resident phantom (c3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     args = ap.parse_args()
+    c5 = args.workload == "c5"
+    if args.channels is None:
+        args.channels = 3 if c5 else 1
+    if args.precision is None:
+        args.precision = "bf16" if c5 else "fp32"
+    if c5:
+        if "--batch" not in sys.argv:
+            args.batch = 16
+        if "--size" not in sys.argv:
+            args.size = 512
+        if "--classes" not in sys.argv:
+            args.classes = 3
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -360,7 +400,7 @@ def main():
 
     from pmu_hip import _lib as L
 
-    build = build_unet if args.workload == "unet" else build_probunet
+    build = build_probunet if args.workload == "probunet" else build_unet
     step, flops_step, config, data = build(args, dev, world, rank)
     B = args.batch
 
@@ -398,8 +438,9 @@ def main():
         n, fl, t = mf[dom]
         ach = fl / t / 1e12
         traffic, tsrc = pmc_traffic(args.workload, dom)
-        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TF,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4),
+        peak = BF16_MFMA_PEAK_TF if dom.endswith("_bf16") else FP32_MFMA_PEAK_TF
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "bytes/launch (HBM)",
                 "traffic_source": tsrc, "launches": n, "avg_launch_ms": round(t / n * 1e3, 4),
                 "flops_per_launch": fl / n}
@@ -409,14 +450,18 @@ def main():
             flops_step = sum(v[1] for v in per.values())
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(workload=args.workload)
+        cpu = cpu_baseline(workload="probunet" if args.workload == "probunet" else "unet", size=args.size,
+                           channels=args.channels, classes=args.classes)
     if rank == 0:
         res = {
             "metric": METRIC, "value": round(value, 3), "unit": "slices/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": data, "config": config,
+            "vs_baseline": None, "dtype": args.precision if args.workload != "probunet" else "fp32",
+            "data": data, "config": config,
             "step_tflops": round(flops_step / (ms * 1e-3) / 1e12, 2) if flops_step else None,
-            "step_mfma_frac": round(flops_step / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4) if flops_step else None,
+            "step_mfma_frac": round(flops_step / (ms * 1e-3) / 1e12 /
+                                    (BF16_MFMA_PEAK_TF if args.precision == "bf16" else FP32_MFMA_PEAK_TF), 4)
+            if flops_step else None,
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "loss": float(loss.detach()),
         }
         print(json.dumps(res), flush=True)

@@ -110,6 +110,16 @@ int pmu_conv3x3_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const fl
 int pmu_conv3x3_dgrad_bf16(const pmu_frame* dz, const unsigned short* wp, int Cin, int Csplit,
                            float* dx0, float* dx1, void* stream);
 
+/* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels
+ * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz
+ * that pmu_conv3x3_wgrad_bf16 multiplies. */
+int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* out, void* stream);
+/* dw[Cout][Cin][3][3] from dzt [N][H][W][pad8(Cout)] and xt [N][H][W][pad8(Cin)] (bf16, pad8(c) =
+ * c rounded up to a multiple of 8); ws must hold pmu_conv3x3_wgrad_ws_bf16() bytes. */
+size_t pmu_conv3x3_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);
+int pmu_conv3x3_wgrad_bf16(const unsigned short* dzt, const unsigned short* xt, int N, int H, int W,
+                           int Cout, int Cin, float* dw, float* ws, size_t ws_bytes, void* stream);
+
 /* ---- first layer (Cin <= 4, planes given NCHW-style, one pointer per channel) ------ */
 int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,
                        const float* w, const float* bias, int Cout, float* z, float* part,

@@ -25,31 +25,66 @@ def _bn(x, sd, pre, training, momentum=0.1, eps=1e-5):
     return y
 
 
-def double_conv(x, sd, pre, training):
-    """(conv3x3 pad1 -> BN -> ReLU) x 2  (unet_parts.py:14-21); Sequential indices 0,1,3,4."""
+def _rb(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class Bf16Conv3x3(torch.autograd.Function):
+    """conv3x3(pad 1) with torch.autocast(bfloat16) arithmetic as the HIP bf16 kernels implement it
+    (include/pmunet_hip.h, bf16 section): the operand x and the weights are rounded to bf16, the
+    exact products summed in the ambient dtype; backward rounds the incoming gradient dy to bf16
+    once and forms dx = conv2d_input(rb(w), rb(dy)), dw = conv2d_weight(rb(x), rb(dy)), db = sum dy."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xr, wr = _rb(x), _rb(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.has_b = b is not None
+        return F.conv2d(xr, wr, b, padding=1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xr, wr = ctx.saved_tensors
+        dyr = _rb(dy)
+        dx = torch.nn.grad.conv2d_input(xr.shape, wr, dyr, padding=1)
+        dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dyr, padding=1)
+        db = dy.sum((0, 2, 3)) if ctx.has_b else None
+        return dx, dw, db
+
+
+def _conv3x3(x, w, b, bf16):
+    return Bf16Conv3x3.apply(x, w, b) if bf16 else F.conv2d(x, w, b, padding=1)
+
+
+def double_conv(x, sd, pre, training, bf16=False, first_fp32=False):
+    """(conv3x3 pad1 -> BN -> ReLU) x 2  (unet_parts.py:14-21); Sequential indices 0,1,3,4.
+    bf16: the autocast arithmetic of Bf16Conv3x3 (first_fp32 keeps the first conv in fp32, as the
+    HIP path's Cin <= 4 first-layer kernel)."""
     for i in (0, 3):
-        x = F.conv2d(x, sd[f"{pre}double_conv.{i}.weight"], sd[f"{pre}double_conv.{i}.bias"], padding=1)
+        use = bf16 and not (first_fp32 and i == 0)
+        x = _conv3x3(x, sd[f"{pre}double_conv.{i}.weight"], sd[f"{pre}double_conv.{i}.bias"], use)
         x = F.relu(_bn(x, sd, f"{pre}double_conv.{i + 1}.", training))
     return x
 
 
-def unet_forward(sd, x, n_levels, n_classes, apply_last_layer=True, training=True):
+def unet_forward(sd, x, n_levels, n_classes, apply_last_layer=True, training=True, bf16=False):
     """UNet.forward (PMU/model/unet/unet_model.py:31-54).
 
     n_levels = len(num_filters).  Down_i = MaxPool2d(2) + DoubleConv (unet_parts.py:31-34);
     Up = ConvTranspose2d(k2,s2) -> F.pad to the skip size -> cat([skip, up]) -> DoubleConv
     (unet_parts.py:52,58-66); up_blocks stored deepest-first (unet_model.py:29); skip of up
-    block i is xs[-(2 + 2i)] (:39)."""
-    xs = [double_conv(x, sd, "inc.", training)]
+    block i is xs[-(2 + 2i)] (:39).  bf16: every 3x3 conv but a Cin <= 4 first one in Bf16Conv3x3
+    arithmetic (the HIP path's autocast mode)."""
+    xs = [double_conv(x, sd, "inc.", training, bf16, first_fp32=x.shape[1] <= 4)]
     for i in range(n_levels - 1):
-        xs.append(double_conv(F.max_pool2d(xs[-1], 2), sd, f"down_blocks.{i}.maxpool_conv.1.", training))
+        xs.append(double_conv(F.max_pool2d(xs[-1], 2), sd, f"down_blocks.{i}.maxpool_conv.1.", training, bf16))
     for i in range(n_levels - 1):
         x1, x2 = xs[-1], xs[-(2 + 2 * i)]
         pre = f"up_blocks.{i}."
         x1 = F.conv_transpose2d(x1, sd[pre + "up.weight"], sd[pre + "up.bias"], stride=2)
         dy, dx = x2.shape[2] - x1.shape[2], x2.shape[3] - x1.shape[3]
         x1 = F.pad(x1, [dx // 2, dx - dx // 2, dy // 2, dy - dy // 2])
-        xs.append(double_conv(torch.cat([x2, x1], dim=1), sd, pre + "conv.", training))
+        xs.append(double_conv(torch.cat([x2, x1], dim=1), sd, pre + "conv.", training, bf16))
     feat = xs[-1]
     if not apply_last_layer:
         return feat

@@ -160,6 +160,7 @@ class ConvBNOut:
     bn: BNState
     srcs: list = field(default_factory=list)   # the operand sources it consumed (for wgrad)
     planes: list | None = None                  # first-layer input planes
+    bf16: bool = False                          # computed on the bf16-MFMA kernels
 
     def act(self, pool=L.POOL_NONE) -> Src:
         return Src(self.z, L.SRC_BNRELU, self.bn.coef, pool=pool)
@@ -171,7 +172,7 @@ def first_layer_ok(cin: int, cout: int) -> bool:
 
 
 def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H, W, training, dev,
-                    planes=None) -> ConvBNOut:
+                    planes=None, bf16=False) -> ConvBNOut:
     Cout = conv.out_channels
     s = L.stream()
     lb = L.lib()
@@ -187,6 +188,12 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         arr = (ctypes.c_void_p * len(planes))(*[p.data_ptr() for p in planes])
         L.call("pmu_conv_first_fwd", arr, len(planes), N, H, W, conv.weight.data_ptr(), L.ptr(conv.bias), Cout,
                z.data_ptr(), L.ptr(part), s)
+    elif bf16:
+        R = lb.pmu_conv3x3_tiles(N, H, W)
+        part = _empty(R, 2 * Cout, device=dev) if need_stats else None
+        wp = pack_weights_bf16(conv.weight, dgrad=False)
+        L.call("pmu_conv3x3_fwd_bf16", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout, z.data_ptr(),
+               L.ptr(part), s)
     else:
         R = lb.pmu_conv3x3_tiles(N, H, W)
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
@@ -194,7 +201,7 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), wp.data_ptr(), L.ptr(conv.bias),
                Cout, z.data_ptr(), L.ptr(part), s)
     st = bn_forward(part, R, Cout, N * H * W, bn, training, dev)
-    return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes)
+    return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes, bf16=bf16 and planes is None)
 
 
 def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, need_dx=True, split=None):
@@ -211,6 +218,8 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     dzf = frame_of([dz_src], N, H, W)
     dw = grads.new(conv.weight)
     lb = L.lib()
+    if out.bf16:
+        return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split)
     if out.planes is not None:
         Cin = len(out.planes)
         wsb = lb.pmu_conv_first_wgrad_ws(N, H, W, Cin, Cout)
@@ -235,6 +244,53 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, split, dx0.data_ptr(),
            dx1.data_ptr(), s)
     return dx0, dx1
+
+
+def _pad8(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def frame_to_bf16(srcs, N, H, W) -> torch.Tensor:
+    """The bf16 operand of a frame, NHWC with channels padded to a multiple of 8 (pmu_frame_to_bf16)."""
+    C = sum(sr.C for sr in srcs)
+    out = torch.empty(N, H, W, _pad8(C), dtype=torch.int16, device=srcs[0].x.device)
+    L.call("pmu_frame_to_bf16", frame_of(srcs, N, H, W), _pad8(C), out.data_ptr(), L.stream())
+    return out
+
+
+def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split):
+    """bf16-MFMA backward of one conv layer (torch.autocast(bfloat16) arithmetic): the weight
+    gradient multiplies the materialised bf16 operands (dz after the BN+ReLU backward, and the
+    layer's BN+ReLU(+pool)(+concat) input); the input gradient stages dz's frame directly."""
+    s = L.stream()
+    N, H, W, Cout = out.z.shape
+    dev = out.z.device
+    Cin = conv.in_channels
+    dzt = frame_to_bf16([dz_src], N, H, W)
+    xt = frame_to_bf16(out.srcs, N, H, W)
+    wsb = L.lib().pmu_conv3x3_wgrad_ws_bf16(N, H, W, Cin, Cout)
+    ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+    L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(), ws.data_ptr(),
+           wsb, s)
+    del dzt, xt
+    if not need_dx:
+        return None
+    wp = pack_weights_bf16(conv.weight, dgrad=True)
+    dzf = frame_of([dz_src], N, H, W)
+    sp = Cin if split is None else split
+    dx0 = _empty(N, H, W, sp, device=dev)
+    dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin else None
+    L.call("pmu_conv3x3_dgrad_bf16", dzf, wp.data_ptr(), Cin, sp, dx0.data_ptr(), L.ptr(dx1), s)
+    return dx0 if split is None else (dx0, dx1)
+
+
+def pack_weights_bf16(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """Weights rounded to bf16 and laid out as the bf16 conv kernel's B tiles (pmu_conv3x3_pack_bf16)."""
+    Cout, Cin = w.shape[0], w.shape[1]
+    n = L.lib().pmu_conv3x3_packed_size_bf16(Cout, Cin, int(dgrad)) // 2
+    wp = torch.empty(n, dtype=torch.int16, device=w.device)
+    L.call("pmu_conv3x3_pack_bf16", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
 
 
 def pack_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
@@ -285,11 +341,13 @@ class UNetState:
         self.feat_src = None    # last DoubleConv output producer
 
 
-def unet_forward(net, x: torch.Tensor, training: bool):
+def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False):
     """Forward of model.UNet on the HIP path.  Returns (output, state).
 
     Output: NCHW logits / sigmoid(logits) when net.apply_last_layer, else the last
-    DoubleConv activation as an NCHW-shaped channels-last tensor (unet_model.py:48-54)."""
+    DoubleConv activation as an NCHW-shaped channels-last tensor (unet_model.py:48-54).
+    bf16: the 3x3 convs (except the Cin <= 4 first layer) run on the bf16-MFMA kernels
+    (autocast arithmetic; see include/pmunet_hip.h), their backward too."""
     assert x.is_cuda and x.dtype == F32 and x.dim() == 4
     dev = x.device
     N, Cin, H, W = x.shape
@@ -307,8 +365,8 @@ def unet_forward(net, x: torch.Tensor, training: bool):
         first_srcs = [Src(xc.permute(0, 2, 3, 1).contiguous())]
     # ---- encoder
     c1w, b1, c2w, b2 = _dc_layers(net.inc)
-    o1 = conv_bn_forward(first_srcs, c1w, b1, N, H, W, training, dev, planes=planes)
-    o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev)
+    o1 = conv_bn_forward(first_srcs, c1w, b1, N, H, W, training, dev, planes=planes, bf16=bf16)
+    o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev, bf16=bf16)
     st.enc.append((o1, o2))
     h, w = H, W
     for down in net.down_blocks:
@@ -316,8 +374,8 @@ def unet_forward(net, x: torch.Tensor, training: bool):
         c1w, b1, c2w, b2 = _dc_layers(dc)
         prev = st.enc[-1][1]
         h, w = h // 2, w // 2
-        o1 = conv_bn_forward([prev.act(L.POOL_MAX2)], c1w, b1, N, h, w, training, dev)
-        o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev)
+        o1 = conv_bn_forward([prev.act(L.POOL_MAX2)], c1w, b1, N, h, w, training, dev, bf16=bf16)
+        o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev, bf16=bf16)
         st.enc.append((o1, o2))
     # ---- decoder
     cur = st.enc[-1][1]
@@ -337,8 +395,8 @@ def unet_forward(net, x: torch.Tensor, training: bool):
         off = (dY // 2, dX // 2)
         c1w, b1, c2w, b2 = _dc_layers(up.conv)
         srcs = [skip.act(), Src(u, L.SRC_RAW, off=off)]
-        o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev)
-        o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev)
+        o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev, bf16=bf16)
+        o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev, bf16=bf16)
         st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2))
         cur = o2
     st.feat_src = cur

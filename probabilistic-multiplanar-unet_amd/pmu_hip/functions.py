@@ -82,10 +82,18 @@ def grad_sink_for(module, params) -> GradSink:
 # ----------------------------------------------------------------------------------------
 # U-Net
 # ----------------------------------------------------------------------------------------
+def use_bf16(net) -> bool:
+    """bf16-MFMA arithmetic for this call: inside torch.autocast("cuda", dtype=torch.bfloat16) —
+    the PyTorch idiom for the reference's config c5 — or when ``net.pmu_precision == "bf16"``."""
+    if getattr(net, "pmu_precision", None) == "bf16":
+        return True
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
 class UNetFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, net, x, *params):
-        out, st = engine.unet_forward(net, x, net.training)
+    def forward(ctx, net, x, bf16, *params):
+        out, st = engine.unet_forward(net, x, net.training, bf16=bf16)
         ctx.net = net
         ctx.st = st
         return out
@@ -96,7 +104,7 @@ class UNetFunction(torch.autograd.Function):
         plist = list(net.parameters())
         grads = engine.unet_backward(net, ctx.st, dy, grad_sink_for(net, plist))
         ctx.st = None
-        return (None, None) + tuple(grads.get(p) for p in plist)
+        return (None, None, None) + tuple(grads.get(p) for p in plist)
 
 
 def unet_apply(net, x):
@@ -105,10 +113,11 @@ def unet_apply(net, x):
     if x.dtype != torch.float32:
         x = x.float()
     params = list(net.parameters())
+    bf16 = use_bf16(net)
     if torch.is_grad_enabled() and any(p.requires_grad for p in params):
-        return UNetFunction.apply(net, x, *params)
+        return UNetFunction.apply(net, x, bf16, *params)
     with torch.no_grad():
-        out, _ = engine.unet_forward(net, x, net.training)
+        out, _ = engine.unet_forward(net, x, net.training, bf16=bf16)
     return out
 
 

@@ -129,3 +129,114 @@ def test_conv3x3_dgrad_bf16(dev, N, H, W, Cin, Cout, split):
                                      padding=1).permute(0, 2, 3, 1)
     got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
     assert _rel(got, ref) <= TOL
+
+
+def _to_bf16(srcs, N, H, W, C):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import frame_of
+    Cp = (C + 7) // 8 * 8
+    out = torch.empty(N, H, W, Cp, dtype=torch.int16, device=srcs[0].x.device)
+    L.call("pmu_frame_to_bf16", frame_of(srcs, N, H, W), Cp, out.data_ptr(), L.stream())
+    return out
+
+
+def _bf16_values(t16, C):
+    return t16.view(torch.bfloat16)[..., :C].float()
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 32, 32, 64, 64), (2, 24, 40, 64, 128), (3, 9, 13, 32, 64),
+                                            (2, 16, 16, 128, 192), (1, 11, 7, 12, 20)])
+def test_conv3x3_wgrad_bf16(dev, N, H, W, Cin, Cout):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    g = torch.Generator().manual_seed(3 + H + Cout)
+    x = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    dz = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    xt = _to_bf16([Src(x)], N, H, W, Cin)
+    dzt = _to_bf16([Src(dz)], N, H, W, Cout)
+    # the materialised operands are exactly the RNE bf16 roundings
+    assert torch.equal(_bf16_values(xt, Cin), _rb(x))
+    assert torch.equal(_bf16_values(dzt, Cout), _rb(dz))
+    wsb = L.lib().pmu_conv3x3_wgrad_ws_bf16(N, H, W, Cin, Cout)
+    ws = torch.empty(wsb // 4 + 1, device=dev)
+    dw = torch.empty(Cout, Cin, 3, 3, device=dev)
+    L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(), ws.data_ptr(),
+           wsb, L.stream())
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(_nchw(_rb(x)).double().cpu(), (Cout, Cin, 3, 3),
+                                      _nchw(_rb(dz)).double().cpu(), padding=1)
+    assert _rel(dw, ref) <= TOL
+
+
+def test_frame_to_bf16_bnbwd_pool_concat(dev):
+    """The materialised operand equals the fp32 transform rounded to bf16 (BN+ReLU+max-pool, concat)."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    N, H, W, C0, C1 = 2, 10, 12, 8, 12
+    g = torch.Generator().manual_seed(9)
+    z0 = torch.randn(N, 2 * H, 2 * W, C0, generator=g).to(dev)
+    coef = torch.cat([torch.rand(C0, generator=g) + 0.5, torch.randn(C0, generator=g) * 0.2]).to(dev)
+    u = torch.randn(N, H, W - 2, C1, generator=g).to(dev)
+    t = _to_bf16([Src(z0, L.SRC_BNRELU, coef, pool=L.POOL_MAX2), Src(u, off=(0, 1))], N, H, W, C0 + C1)
+    a = TF.max_pool2d(_nchw(_bnrelu(z0, coef)), 2).permute(0, 2, 3, 1)
+    up = torch.zeros(N, H, W, C1, device=dev)
+    up[:, :, 1:W - 1] = u
+    ref = _rb(torch.cat([a, up], dim=3))
+    got = _bf16_values(t, C0 + C1)
+    assert float((got - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+    assert torch.equal(t.view(torch.bfloat16)[..., C0 + C1:].float(), torch.zeros_like(t[..., C0 + C1:], dtype=torch.float))
+
+
+@pytest.mark.parametrize("filters,n_cls,N,H,W,C", [([16, 32, 64], 3, 2, 64, 64, 1),
+                                                   ([64, 128, 256], 1, 2, 48, 40, 3),
+                                                   ([8, 16, 32, 64, 128], 3, 2, 37, 45, 1)])
+def test_unet_autocast_bf16(dev, filters, n_cls, N, H, W, C):
+    """model.UNet under torch.autocast(bfloat16) vs the oracle's Bf16Conv3x3 arithmetic in fp64:
+    outputs, loss, every gradient (max|d| / max|ref| over all parameters) and BN running stats.
+
+    bf16 rounding turns the last-bit differences of any fp32 evaluation order into occasional
+    one-ulp operand flips, which BN over a small batch amplifies: the same oracle evaluated in fp32
+    is itself ~1e-3..4e-3 away from its fp64 evaluation.  Tolerance: max(2e-3, 2 x that floor)."""
+    from helpers import grad_err
+    from model import UNet
+    from oracle.unet_ref import unet_forward, unet_loss, unet_param_keys
+    torch.manual_seed(0)
+    net = UNet(C, n_cls, filters)
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    g = torch.Generator().manual_seed(2)
+    x = torch.rand(N, C, H, W, generator=g)
+    tgt = ((torch.rand(N, 1, H, W, generator=g) > 0.5).float() if n_cls == 1
+           else torch.randint(0, n_cls, (N, 1, H, W), generator=g))
+    keys = unet_param_keys(sd)
+
+    def oracle(dt):
+        sdd = {k: (v.to(dt) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+        params = {k: sdd[k].clone().requires_grad_(True) for k in keys}
+        work = dict(sdd)
+        work.update(params)
+        o = unet_forward(work, x.to(dt), len(filters), n_cls, bf16=True)
+        lo = unet_loss(o, tgt.to(dt) if n_cls == 1 else tgt, n_cls)
+        lo.backward()
+        return o.detach(), float(lo), {k: params[k].grad for k in keys}, work
+
+    ref, lref, gref, work = oracle(torch.float64)
+    o32, l32, g32, _ = oracle(torch.float32)
+    tol_out = max(2e-3, 2 * _rel(o32, ref))
+    tol_loss = max(2e-3, 2 * abs(l32 - lref) / abs(lref))
+    tol_g = max(2e-3, 2 * grad_err(g32, gref)[0])
+
+    net = net.to(dev).train()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = net(x.to(dev))
+    assert out.dtype == torch.float32
+    loss = unet_loss(out, tgt.to(dev), n_cls)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert _rel(out, ref) <= tol_out, (_rel(out, ref), tol_out)
+    assert abs(float(loss) - lref) <= tol_loss * abs(lref)
+    named = dict(net.named_parameters())
+    err, worst = grad_err({k: named[k].grad for k in keys}, gref)
+    assert err <= tol_g, (err, worst, tol_g)
+    for k, v in net.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            assert float((v.double().cpu() - work[k]).abs().max()) <= 2e-3 * max(1.0, float(work[k].abs().max())), k

@@ -79,7 +79,18 @@ def main():
             return t
         wbf = packb(w, False)
         wbd = packb(w, True)
+        cpo, cpi = (Cout + 7) // 8 * 8, (Cin + 7) // 8 * 8
+        dzt = torch.empty(N, H, W, cpo, dtype=torch.int16, device=dev)
+        xt = torch.empty(N, H, W, cpi, dtype=torch.int16, device=dev)
+        L.call("pmu_frame_to_bf16", fdz, cpo, dzt.data_ptr(), s)
+        L.call("pmu_frame_to_bf16", fin, cpi, xt.data_ptr(), s)
+        wsbb = L.lib().pmu_conv3x3_wgrad_ws_bf16(N, H, W, Cin, Cout)
+        wsb16 = torch.empty(wsbb // 4 + 1, device=dev)
         ops = {
+            "wgrad_bf16": lambda: L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin,
+                                         dw.data_ptr(), wsb16.data_ptr(), wsbb, s),
+            "mat_bf16": lambda: (L.call("pmu_frame_to_bf16", fdz, cpo, dzt.data_ptr(), s),
+                                 L.call("pmu_frame_to_bf16", fin, cpi, xt.data_ptr(), s)),
             "fwd_bf16": lambda: L.call("pmu_conv3x3_fwd_bf16", fin, wbf.data_ptr(), b.data_ptr(), Cout,
                                        out.data_ptr(), part.data_ptr(), s),
             "dgrad_bf16": lambda: L.call("pmu_conv3x3_dgrad_bf16", fdz, wbd.data_ptr(), Cin, Cin, dx.data_ptr(),
