@@ -15,6 +15,8 @@
 // lane half h reads k = 8h..8h+7 of its row with one ds_read_b128 (48-B rows: conflict-free for
 // any 16 consecutive rows).  Wave layout: BNT = 128 -> 2 (pixels) x 2 (channels) waves of 128 px x
 // 64 ch = 4 x 2 accumulators; BNT = 64 -> 4 x 1 waves of 64 px x 64 ch = 2 x 2 accumulators.
+#include <cstdlib>
+
 #include "pmu_stage.h"
 
 namespace {
@@ -222,6 +224,184 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(ConvArgsB a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Software-pipelined variant (2 blocks/CU, BNT = 64): chunk c+1's global loads (A items and the
+// packed B tile) are issued into registers before chunk c's 9 x 4 MFMAs and transformed/written
+// to LDS after them.  At bf16 rates a chunk's MFMAs last ~1 us, so the synchronous kernel above
+// pays the full global-load latency per chunk; here it hides under the MFMAs, and the partner
+// block's MFMAs cover this block's commit phase.  Operand modes are template parameters.
+// ---------------------------------------------------------------------------------------------
+constexpr int PB_UNITS = 9 * 64 * 2;               // 16-B units of a BNT = 64 B tile
+constexpr int PB_N = (PB_UNITS + 255) / 256;       // 5 (the last one for tid < 128)
+
+template <bool DGRAD, int POOL, int TWL>
+__global__ __launch_bounds__(256, 2) void conv3x3_bf16_pipe_kernel(ConvArgsB a) {
+  constexpr int BNT = 64, FM = 2, FN = 2, WM = 4;
+  constexpr int TW = 1 << TWL, TH = BM >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
+  __shared__ __attribute__((aligned(16))) unsigned short smem[A_ELEMS + 9 * BNT * LSB];
+  unsigned short* As = smem;
+  unsigned short* Bs = smem + A_ELEMS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave;
+  int t = blockIdx.x;
+  const int tw = t % a.tiles_w; t /= a.tiles_w;
+  const int th = t % a.tiles_h; t /= a.tiles_h;
+  const int n = t;
+  const int h0 = th * TH, w0 = tw * TW;
+  const int j0 = blockIdx.y * BNT;
+  const DevFrame& F = a.in;
+  const int nch = (a.KC + BK - 1) / BK;
+  const int cq4 = 4 * (tid & 3);
+
+  int ih[NI], iw[NI], dst[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int it = tid + 256 * i;
+    const int hp = it >> 2;
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    ih[i] = (it < HP * 4) ? h0 - 1 + hr : PMU_NO_ITEM;
+    iw[i] = w0 - 1 + hc;
+    dst[i] = hp * LSB + 4 * (it & 3);
+  }
+  const int hsel = (lane >> 5) * 8;
+  int abase[FM], bbase[FN];
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int q = wm * 32 * FM + fm * 32 + (lane & 31);
+    abase[fm] = ((q >> TWL) * HW2 + (q & (TW - 1))) * LSB + hsel;
+  }
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) bbase[fn] = (fn * 32 + (lane & 31)) * LSB + hsel;
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  PmuPref<POOL, DGRAD, NI> pf;
+  uint4 pb0, pb1, pb2, pb3, pb4;  // packed-B prefetch (plain locals: a struct or array here lands in scratch)
+  const uint4* wtile = reinterpret_cast<const uint4*>(a.wp) + (long long)(j0 / PJ) * nch * (9 * PJ * BK / 8);
+  const bool b4 = tid < PB_UNITS - 4 * 256;
+  static_assert(PB_N == 5, "five B units per thread");
+#define PMU_PREFETCH(CH)                                                                                    \
+  {                                                                                                        \
+    const int k0_ = (CH) * BK;                                                                             \
+    const bool second_ = F.nsrc > 1 && k0_ >= F.C0;                                                        \
+    pmu_prefetch<POOL, DGRAD, NI>(pmu_pick_src(F, second_), k0_ - (second_ ? F.C0 : 0) + cq4, n, ih, iw, pf); \
+    const uint4* src_ = wtile + (long long)(CH) * (9 * PJ * BK / 8) + tid;                               \
+    pb0 = src_[0]; pb1 = src_[256]; pb2 = src_[512]; pb3 = src_[768];                                      \
+    pb4 = src_[b4 ? 1024 : 0];                                                                             \
+  }
+#define PMU_COMMIT()                                                                                        \
+  {                                                                                                        \
+    pmu_commit<POOL, DGRAD, NI, true>(pf, ih, dst, As);                                                    \
+    *reinterpret_cast<uint4*>(Bs + ((tid) >> 1) * LSB + 8 * ((tid) & 1)) = pb0;                            \
+    *reinterpret_cast<uint4*>(Bs + ((tid + 256) >> 1) * LSB + 8 * ((tid) & 1)) = pb1;                      \
+    *reinterpret_cast<uint4*>(Bs + ((tid + 512) >> 1) * LSB + 8 * ((tid) & 1)) = pb2;                      \
+    *reinterpret_cast<uint4*>(Bs + ((tid + 768) >> 1) * LSB + 8 * ((tid) & 1)) = pb3;                      \
+    if (b4) *reinterpret_cast<uint4*>(Bs + ((tid + 1024) >> 1) * LSB + 8 * ((tid) & 1)) = pb4;             \
+  }
+
+  PMU_PREFETCH(0)
+  PMU_COMMIT()
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const bool more = ch + 1 < nch;
+    if (more) PMU_PREFETCH(ch + 1)  // in flight during the MFMAs below
+    bf16x8 op[2][FM + FN];
+    auto load_ops = [&](int tap, bf16x8 (&o)[FM + FN]) {
+      const int toff = ((tap / 3) * HW2 + (tap % 3)) * LSB;
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) o[fm] = *reinterpret_cast<const bf16x8*>(As + abase[fm] + toff);
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) o[FM + fn] = *reinterpret_cast<const bf16x8*>(Bs + tap * BNT * LSB + bbase[fn]);
+    };
+    load_ops(0, op[0]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) load_ops(tap + 1, op[(tap + 1) & 1]);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[tap & 1][fm], op[tap & 1][FM + fn], acc[fm][fn], 0, 0, 0);
+    }
+    __syncthreads();
+    if (more) {
+      PMU_COMMIT()
+      __syncthreads();
+    }
+  }
+#undef PMU_PREFETCH
+#undef PMU_COMMIT
+
+  // epilogue (as conv3x3_bf16_kernel with WN = 1)
+  float* red = reinterpret_cast<float*>(smem);
+  float s1[FN], s2[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    s1[fn] = 0.f; s2[fn] = 0.f;
+    const int j = j0 + fn * 32 + (lane & 31);
+    const bool jok = j < a.NOUT;
+    const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = wm * 32 * FM + fm * 32 + acc_row(r, lane);
+        const int h = h0 + (q >> TWL), w = w0 + (q & (TW - 1));
+        if (!jok || h >= F.H || w >= F.W) continue;
+        const long long pix = ((long long)n * F.H + h) * F.W + w;
+        const float v = acc[fm][fn][r] + b;
+        if (!DGRAD) {
+          a.out0[pix * a.NOUT + j] = v;
+          s1[fn] += v;
+          s2[fn] = fmaf(v, v, s2[fn]);
+        } else if (j < a.split) {
+          a.out0[pix * a.split + j] = v;
+        } else {
+          a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+        }
+      }
+    }
+  }
+  if (!DGRAD && a.part) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] += __shfl_xor(s1[fn], 32, 64);
+      s2[fn] += __shfl_xor(s2[fn], 32, 64);
+      if (lane < 32) {
+        red[(wm * BNT + fn * 32 + lane) * 2 + 0] = s1[fn];
+        red[(wm * BNT + fn * 32 + lane) * 2 + 1] = s2[fn];
+      }
+    }
+    __syncthreads();
+    if (tid < BNT) {
+      const int j = j0 + tid;
+      if (j < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < WM; ++v) {
+          t1 += red[(v * BNT + tid) * 2 + 0];
+          t2 += red[(v * BNT + tid) * 2 + 1];
+        }
+        a.part[((long long)blockIdx.x * 2 + 0) * a.NOUT + j] = t1;
+        a.part[((long long)blockIdx.x * 2 + 1) * a.NOUT + j] = t2;
+      }
+    }
+  }
+}
+
+// sources the pipelined staging handles: float4 channels, chunks never straddle sources
+static bool pipe_src_ok(const pmu_src& s) {
+  if (s.C % BK != 0) return false;
+  if (s.pool == PMU_POOL_NONE) return true;
+  return s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU;
+}
+
 static int pick_twl(int W) {
   if (W > 16) return 5;
   if (W > 8) return 4;
@@ -241,7 +421,28 @@ static int launch_bf16(const pmu_frame* in, const unsigned short* wp, const floa
   const int bnt = 64;  // BNT = 128 needs the 1-block/CU pipelined variant (register budget)
   dim3 grid((unsigned)(a.tiles_w * a.tiles_h * in->N), (unsigned)pmu_cdiv(NOUT, bnt));
   hipStream_t st = (hipStream_t)stream;
-#define PMU_BF(T, B, D)                                                                 \
+  {
+    const pmu_src& s0 = in->src[0];
+    const bool two = in->nsrc > 1;
+    const pmu_src& s1 = in->src[1];
+    const int pool = s0.pool;
+    const bool ok = pipe_src_ok(s0) && (!two || (pipe_src_ok(s1) && s1.pool == pool));
+    const bool modes_ok = dgrad ? (!two && s0.mode == PMU_SRC_BNBWD)
+                                : (s0.mode != PMU_SRC_BNBWD && (!two || s1.mode != PMU_SRC_BNBWD));
+    if (ok && modes_ok && !getenv("PMU_BF16_NOPIPE")) {
+#define PMU_BP(D, P, T)                                                                    \
+  if (dgrad == D && pool == P && twl == T) {                                               \
+    hipLaunchKernelGGL((conv3x3_bf16_pipe_kernel<D, P, T>), grid, dim3(256), 0, st, a);    \
+    PMU_CHECK_LAUNCH();                                                                    \
+    return PMU_OK;                                                                         \
+  }
+      PMU_BP(false, PMU_POOL_NONE, 3) PMU_BP(false, PMU_POOL_NONE, 4) PMU_BP(false, PMU_POOL_NONE, 5)
+      PMU_BP(false, PMU_POOL_MAX2, 3) PMU_BP(false, PMU_POOL_MAX2, 4) PMU_BP(false, PMU_POOL_MAX2, 5)
+      PMU_BP(true, PMU_POOL_NONE, 3) PMU_BP(true, PMU_POOL_NONE, 4) PMU_BP(true, PMU_POOL_NONE, 5)
+#undef PMU_BP
+    }
+  }
+#define PMU_BF(T, B, D)                                                              \
   if (twl == T && bnt == B && dgrad == D) {                                            \
     hipLaunchKernelGGL((conv3x3_bf16_kernel<T, B, D>), grid, dim3(256), 0, st, a);     \
     PMU_CHECK_LAUNCH();                                                                \

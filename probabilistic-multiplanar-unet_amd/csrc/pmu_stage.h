@@ -150,6 +150,23 @@ __device__ __forceinline__ void stage_items(const DevFrame& F, int n, int cbase,
 // POOL and BWD (= BN-backward source) are compile-time; RAW vs BN+ReLU is a uniform runtime field
 // so both halves of a concat frame share one register set.
 // ---------------------------------------------------------------------------------------------
+// F.s0 or F.s1 as a value, selected field by field (a select of the whole struct, or a call in each
+// branch of an if, keeps the prefetch registers of the pipelined kernels in scratch)
+__device__ __forceinline__ DevSrc pmu_pick_src(const DevFrame& F, bool second) {
+  DevSrc r;
+  r.x = second ? F.s1.x : F.s0.x;
+  r.z = second ? F.s1.z : F.s0.z;
+  r.coef = second ? F.s1.coef : F.s0.coef;
+  r.mode = second ? F.s1.mode : F.s0.mode;
+  r.pool = second ? F.s1.pool : F.s0.pool;
+  r.C = second ? F.s1.C : F.s0.C;
+  r.H = second ? F.s1.H : F.s0.H;
+  r.W = second ? F.s1.W : F.s0.W;
+  r.off_h = second ? F.s1.off_h : F.s0.off_h;
+  r.off_w = second ? F.s1.off_w : F.s0.off_w;
+  return r;
+}
+
 template <int POOL, bool BWD, int NI>
 struct PmuPref {
   static constexpr int NL = (POOL == PMU_POOL_MAX2) ? 4 : 1;
@@ -195,9 +212,9 @@ __device__ __forceinline__ void pmu_prefetch(const DevSrc& s, int c, int n, cons
   p.okmask = m;
 }
 
-template <int POOL, bool BWD, int NI>
+template <int POOL, bool BWD, int NI, bool BF = false>
 __device__ __forceinline__ void pmu_commit(const PmuPref<POOL, BWD, NI>& p, const int (&ih)[NI], const int (&dst)[NI],
-                                           float* lds) {
+                                           void* lds) {
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     if (ih[i] == PMU_NO_ITEM) continue;
@@ -219,6 +236,6 @@ __device__ __forceinline__ void pmu_commit(const PmuPref<POOL, BWD, NI>& p, cons
       }
     }
     if (!((p.okmask >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(lds + dst[i]) = v;
+    pmu_lds_store4<BF>(lds, dst[i], v);
   }
 }
