@@ -262,44 +262,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Software-pipelined variant (1 block/CU, LDS double-buffered): the next chunk's A items and B
-// tile are loaded into registers before the current chunk's 9 x 32 MFMAs, transformed and written
-// to the other LDS buffer after them, with one barrier per chunk.  The operand modes are template
+// Software-pipelined variant (1 block/CU, LDS double-buffered; the default): the next chunk's A
+// items and B tile are loaded into registers before the current chunk's 9 x 32 MFMAs, transformed
+// and written to the other LDS buffer after them, with one barrier per chunk.  The operand modes are template
 // parameters (M1 < 0: single source), so the staging has no runtime dispatch.  Used when every
 // source is a fast-path source whose channel count is a multiple of BK and packed weights exist.
 // ---------------------------------------------------------------------------------------------
 constexpr int PIPE_NB = 9 * BN * BK / 4 / 256;  // packed-B float4 per thread per chunk
 static_assert(PIPE_NB == 9, "PipeB holds 9 float4");
-
-// the packed-B prefetch registers as named members: an indexed array here is kept in scratch
-struct PipeB {
-  float4 v0, v1, v2, v3, v4, v5, v6, v7, v8;
-};
-template <int R>
-__device__ __forceinline__ float4& pipe_b(PipeB& b) {
-  if constexpr (R == 0) return b.v0;
-  else if constexpr (R == 1) return b.v1;
-  else if constexpr (R == 2) return b.v2;
-  else if constexpr (R == 3) return b.v3;
-  else if constexpr (R == 4) return b.v4;
-  else if constexpr (R == 5) return b.v5;
-  else if constexpr (R == 6) return b.v6;
-  else if constexpr (R == 7) return b.v7;
-  else return b.v8;
-}
-template <int R>
-__device__ __forceinline__ void pipe_load_b_r(const float4* src, int tid, PipeB& b) {
-  pipe_b<R>(b) = src[tid + 256 * R];
-  if constexpr (R + 1 < PIPE_NB) pipe_load_b_r<R + 1>(src, tid, b);
-}
-template <int R>
-__device__ __forceinline__ void pipe_store_b_r(float* bs, int tid, PipeB& b) {
-  const int it = tid + 256 * R;
-  *reinterpret_cast<float4*>(bs + (it >> 2) * LS + 4 * (it & 3)) = pipe_b<R>(b);
-  if constexpr (R + 1 < PIPE_NB) pipe_store_b_r<R + 1>(bs, tid, b);
-}
-__device__ __forceinline__ void pipe_load_b(const float4* src, int tid, PipeB& b) { pipe_load_b_r<0>(src, tid, b); }
-__device__ __forceinline__ void pipe_store_b(float* bs, int tid, PipeB& b) { pipe_store_b_r<0>(bs, tid, b); }
 
 template <bool DGRAD, int POOL>
 __global__ __launch_bounds__(256, 1) void conv3x3_pipe_kernel(ConvArgs a) {
@@ -352,19 +322,25 @@ __global__ __launch_bounds__(256, 1) void conv3x3_pipe_kernel(ConvArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   PmuPref<POOL, DGRAD, NI> pf;
-  PipeB pb;
+  // packed-B prefetch as plain locals (a struct passed by reference or an array here is kept in scratch)
+  float4 pb0, pb1, pb2, pb3, pb4, pb5, pb6, pb7, pb8;
   const float4* wpk = reinterpret_cast<const float4*>(a.wp + (long long)(j0 / BN) * nchunks * (9 * BN * BK));
-#define PMU_PREFETCH(CH)                                                                      \
-  {                                                                                           \
-    const int k0_ = (CH) * BK;                                                                \
-    if (F.nsrc < 2 || k0_ < F.C0) pmu_prefetch<POOL, DGRAD, NI>(F.s0, k0_ + cq4, n, ih, iw, pf); \
-    else pmu_prefetch<POOL, DGRAD, NI>(F.s1, k0_ - F.C0 + cq4, n, ih, iw, pf);                \
-    pipe_load_b(wpk + (long long)(CH) * (9 * BN * BK / 4), tid, pb);                          \
+#define PMU_PB_ST(R, V) *reinterpret_cast<float4*>(bs_ + ((tid + 256 * (R)) >> 2) * LS + 4 * (tid & 3)) = (V);
+#define PMU_PREFETCH(CH)                                                                                    \
+  {                                                                                                        \
+    const int k0_ = (CH) * BK;                                                                             \
+    const bool second_ = F.nsrc > 1 && k0_ >= F.C0;                                                        \
+    pmu_prefetch<POOL, DGRAD, NI>(pmu_pick_src(F, second_), k0_ - (second_ ? F.C0 : 0) + cq4, n, ih, iw, pf); \
+    const float4* src_ = wpk + (long long)(CH) * (9 * BN * BK / 4) + tid;                                  \
+    pb0 = src_[0]; pb1 = src_[256]; pb2 = src_[512]; pb3 = src_[768]; pb4 = src_[1024];                    \
+    pb5 = src_[1280]; pb6 = src_[1536]; pb7 = src_[1792]; pb8 = src_[2048];                                \
   }
-#define PMU_COMMIT(BUF)                                                                       \
-  {                                                                                           \
-    pmu_commit<POOL, DGRAD, NI>(pf, ih, dst, (BUF));                                          \
-    pipe_store_b((BUF) + A_FLOATS, tid, pb);                                                  \
+#define PMU_COMMIT(BUF)                                                                                     \
+  {                                                                                                        \
+    pmu_commit<POOL, DGRAD, NI>(pf, ih, dst, (BUF));                                                       \
+    float* bs_ = (BUF) + A_FLOATS;                                                                         \
+    PMU_PB_ST(0, pb0) PMU_PB_ST(1, pb1) PMU_PB_ST(2, pb2) PMU_PB_ST(3, pb3) PMU_PB_ST(4, pb4)              \
+    PMU_PB_ST(5, pb5) PMU_PB_ST(6, pb6) PMU_PB_ST(7, pb7) PMU_PB_ST(8, pb8)                                \
   }
 
   PMU_PREFETCH(0)
@@ -412,6 +388,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_pipe_kernel(ConvArgs a) {
   }
 #undef PMU_PREFETCH
 #undef PMU_COMMIT
+#undef PMU_PB_ST
   conv_epilogue<DGRAD>(a, acc, smem, n, h0, w0, j0, TW);
 }
 
@@ -421,13 +398,13 @@ static int pick_twl(int W) {
   return 3;
 }
 
-// PMU_CONV_IMPL=pipe selects the software-pipelined 1-block/CU kernel where it applies.  Default:
-// the 2-blocks/CU kernel, measured ~10% faster on every c2 shape (the pipelined variant's 9-float4
-// B prefetch ends up in scratch and one wave per SIMD exposes the staging).
+// Default: the software-pipelined 1-block/CU kernel wherever its staging applies (measured 3-15%
+// faster than the 2-blocks/CU kernel on the c2 dgrad shapes and on par for fwd, once its prefetch
+// registers were kept out of scratch); PMU_CONV_IMPL=sync selects the 2-blocks/CU kernel.
 static bool use_pipe() {
   static const int v = [] {
     const char* e = getenv("PMU_CONV_IMPL");
-    return (e && strcmp(e, "pipe") == 0) ? 1 : 0;
+    return (e && strcmp(e, "sync") == 0) ? 0 : 1;
   }();
   return v != 0;
 }
