@@ -120,6 +120,17 @@ size_t pmu_conv3x3_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);
 int pmu_conv3x3_wgrad_bf16(const unsigned short* dzt, const unsigned short* xt, int N, int H, int W,
                            int Cout, int Cin, float* dw, float* ws, size_t ws_bytes, void* stream);
 
+/* ConvTranspose2d(k2,s2) forward / input gradient with bf16 operands (fp32 sums and outputs), weights
+ * packed as pmu_convT2x2_pack's layouts in bf16 (4*Cin*Cout elements).  The forward takes one unpooled
+ * BN+ReLU source with Cin % 32 == 0, Cout % 32 == 0 (pmu_convT2x2_bf16_ok), dgrad Cin % 128 == 0 and
+ * Cout % 32 == 0. */
+int pmu_convT2x2_pack_bf16(const float* w, int Cin, int Cout, int dgrad, unsigned short* wp, void* stream);
+int pmu_convT2x2_bf16_ok(const pmu_frame* in, int Cout);
+int pmu_convT2x2_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int Cout,
+                          float* u, void* stream);
+int pmu_convT2x2_dgrad_bf16(const float* du, int Hd, int Wd, int off_h, int off_w, const unsigned short* wp,
+                            int N, int H, int W, int Cin, int Cout, float* dx, void* stream);
+
 /* ---- first layer (Cin <= 4, planes given NCHW-style, one pointer per channel) ------ */
 int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,
                        const float* w, const float* bias, int Cout, float* z, float* part,

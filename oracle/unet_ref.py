@@ -52,6 +52,27 @@ class Bf16Conv3x3(torch.autograd.Function):
         return dx, dw, db
 
 
+class Bf16ConvT2x2(torch.autograd.Function):
+    """ConvTranspose2d(k2, s2) with the HIP bf16 path's arithmetic: the forward rounds the operand
+    and the weights to bf16 (when ``fwd``), the input gradient rounds dy and the weights (when
+    ``dgrad``); the weight gradient stays in the ambient precision (pmu_convT2x2_wgrad is fp32)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, fwd, dgrad):
+        ctx.save_for_backward(x, w)
+        ctx.dgrad, ctx.has_b = dgrad, b is not None
+        return F.conv_transpose2d(_rb(x) if fwd else x, _rb(w) if fwd else w, b, stride=2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = F.conv2d(_rb(dy) if ctx.dgrad else dy, _rb(w) if ctx.dgrad else w, stride=2)
+        n, k = dy.shape[0], dy.shape[1]
+        dw = torch.einsum("ncij,nkiajb->ckab", x, dy.reshape(n, k, x.shape[2], 2, x.shape[3], 2))
+        db = dy.sum((0, 2, 3)) if ctx.has_b else None
+        return dx, dw, db, None, None
+
+
 def _conv3x3(x, w, b, bf16):
     return Bf16Conv3x3.apply(x, w, b) if bf16 else F.conv2d(x, w, b, padding=1)
 
@@ -81,7 +102,13 @@ def unet_forward(sd, x, n_levels, n_classes, apply_last_layer=True, training=Tru
     for i in range(n_levels - 1):
         x1, x2 = xs[-1], xs[-(2 + 2 * i)]
         pre = f"up_blocks.{i}."
-        x1 = F.conv_transpose2d(x1, sd[pre + "up.weight"], sd[pre + "up.bias"], stride=2)
+        wt = sd[pre + "up.weight"]
+        if bf16:  # the HIP path's bf16 convT where its kernels take the shapes (pmu_convT2x2_bf16_ok)
+            cin, cout = wt.shape[0], wt.shape[1]
+            fwd_b = cin % 32 == 0 and cout % 32 == 0 and (4 * cout) % 128 == 0
+            x1 = Bf16ConvT2x2.apply(x1, wt, sd[pre + "up.bias"], fwd_b, cin % 128 == 0 and cout % 32 == 0)
+        else:
+            x1 = F.conv_transpose2d(x1, wt, sd[pre + "up.bias"], stride=2)
         dy, dx = x2.shape[2] - x1.shape[2], x2.shape[3] - x1.shape[3]
         x1 = F.pad(x1, [dx // 2, dx - dx // 2, dy // 2, dy - dy // 2])
         xs.append(double_conv(torch.cat([x2, x1], dim=1), sd, pre + "conv.", training, bf16))

@@ -303,6 +303,14 @@ def pack_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wp
 
 
+def pack_convT_weights_bf16(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """ConvT weights rounded to bf16 in pmu_convT2x2_pack's layouts (pmu_convT2x2_pack_bf16)."""
+    Cin, Cout = w.shape[0], w.shape[1]
+    wp = torch.empty(4 * Cin * Cout, dtype=torch.int16, device=w.device)
+    L.call("pmu_convT2x2_pack_bf16", w.data_ptr(), Cin, Cout, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
 def pack_convT_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     """ConvT weights [Cin][Cout][2][2] re-laid out k-contiguous for the pipelined GEMMs (pmu_convT2x2_pack)."""
     Cin, Cout = w.shape[0], w.shape[1]
@@ -327,6 +335,7 @@ class UpState:
     prev: ConvBNOut          # convT input producer
     c1: ConvBNOut
     c2: ConvBNOut
+    bf16: bool = False       # convT input gradient on bf16 MFMA where its shapes allow
 
 
 class UNetState:
@@ -346,8 +355,9 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False):
 
     Output: NCHW logits / sigmoid(logits) when net.apply_last_layer, else the last
     DoubleConv activation as an NCHW-shaped channels-last tensor (unet_model.py:48-54).
-    bf16: the 3x3 convs (except the Cin <= 4 first layer) run on the bf16-MFMA kernels
-    (autocast arithmetic; see include/pmunet_hip.h), their backward too."""
+    bf16: the 3x3 convs (except the Cin <= 4 first layer) and the ConvTranspose2d forward / input
+    gradient (where their shapes allow) run on the bf16-MFMA kernels (autocast arithmetic; see
+    include/pmunet_hip.h), the 3x3 weight gradients too."""
     assert x.is_cuda and x.dtype == F32 and x.dim() == 4
     dev = x.device
     N, Cin, H, W = x.shape
@@ -387,9 +397,14 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False):
         convT = up.up
         Cup = convT.out_channels
         u = _empty(N, 2 * hi, 2 * wi, Cup, device=dev)
-        wpt = pack_convT_weights(convT.weight, dgrad=False)
-        L.call("pmu_convT2x2_fwd", frame_of([cur.act()], N, hi, wi), convT.weight.data_ptr(), wpt.data_ptr(),
-               L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
+        fin = frame_of([cur.act()], N, hi, wi)
+        if bf16 and L.lib().pmu_convT2x2_bf16_ok(fin, Cup):
+            wpt = pack_convT_weights_bf16(convT.weight, dgrad=False)
+            L.call("pmu_convT2x2_fwd_bf16", fin, wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
+        else:
+            wpt = pack_convT_weights(convT.weight, dgrad=False)
+            L.call("pmu_convT2x2_fwd", fin, convT.weight.data_ptr(), wpt.data_ptr(), L.ptr(convT.bias), Cup,
+                   u.data_ptr(), L.stream())
         dY, dX = hs - 2 * hi, ws_ - 2 * wi
         assert dY >= 0 and dX >= 0, "decoder feature map larger than skip (unsupported by reference too)"
         off = (dY // 2, dX // 2)
@@ -397,7 +412,7 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False):
         srcs = [skip.act(), Src(u, L.SRC_RAW, off=off)]
         o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev, bf16=bf16)
         o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev, bf16=bf16)
-        st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2))
+        st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2, bf16=bf16))
         cur = o2
     st.feat_src = cur
     if net.apply_last_layer:
@@ -455,9 +470,14 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         Hd, Wd = dup.shape[1], dup.shape[2]
         Cup = convT.out_channels
         dx = _empty(N, hi, wi, Cin_t, device=dev)
-        wpt = pack_convT_weights(convT.weight, dgrad=True)
-        L.call("pmu_convT2x2_dgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], convT.weight.data_ptr(),
-               wpt.data_ptr(), N, hi, wi, Cin_t, Cup, dx.data_ptr(), s)
+        if us.bf16 and Cin_t % 128 == 0 and Cup % 32 == 0:
+            wpt = pack_convT_weights_bf16(convT.weight, dgrad=True)
+            L.call("pmu_convT2x2_dgrad_bf16", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], wpt.data_ptr(), N, hi, wi,
+                   Cin_t, Cup, dx.data_ptr(), s)
+        else:
+            wpt = pack_convT_weights(convT.weight, dgrad=True)
+            L.call("pmu_convT2x2_dgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], convT.weight.data_ptr(),
+                   wpt.data_ptr(), N, hi, wi, Cin_t, Cup, dx.data_ptr(), s)
         dwt = grads.new(convT.weight)
         dbt = grads.new(convT.bias) if convT.bias is not None else None
         wsb = L.lib().pmu_convT2x2_wgrad_ws(N, hi, wi, Cin_t, Cup)

@@ -189,7 +189,8 @@ def test_frame_to_bf16_bnbwd_pool_concat(dev):
 
 @pytest.mark.parametrize("filters,n_cls,N,H,W,C", [([16, 32, 64], 3, 2, 64, 64, 1),
                                                    ([64, 128, 256], 1, 2, 48, 40, 3),
-                                                   ([8, 16, 32, 64, 128], 3, 2, 37, 45, 1)])
+                                                   ([8, 16, 32, 64, 128], 3, 2, 37, 45, 1),
+                                                   ([32, 64, 128, 256], 3, 2, 40, 36, 3)])
 def test_unet_autocast_bf16(dev, filters, n_cls, N, H, W, C):
     """model.UNet under torch.autocast(bfloat16) vs the oracle's Bf16Conv3x3 arithmetic in fp64:
     outputs, loss, every gradient (max|d| / max|ref| over all parameters) and BN running stats.
@@ -240,3 +241,46 @@ def test_unet_autocast_bf16(dev, filters, n_cls, N, H, W, C):
     for k, v in net.state_dict().items():
         if k.endswith("running_mean") or k.endswith("running_var"):
             assert float((v.double().cpu() - work[k]).abs().max()) <= 2e-3 * max(1.0, float(work[k].abs().max())), k
+
+
+def _packT(w, dgrad):
+    from pmu_hip import _lib as L
+    wp = torch.empty(w.numel(), dtype=torch.int16, device=w.device)
+    L.call("pmu_convT2x2_pack_bf16", w.data_ptr(), w.shape[0], w.shape[1], int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 16, 16, 128, 64), (3, 9, 7, 64, 32), (1, 32, 24, 256, 128)])
+def test_convT_fwd_bf16(dev, N, H, W, Cin, Cout):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_of
+    g = torch.Generator().manual_seed(21 + H)
+    z = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    coef = torch.cat([torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.2]).to(dev)
+    w = (torch.randn(Cin, Cout, 2, 2, generator=g) * 0.1).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    fin = frame_of([Src(z, L.SRC_BNRELU, coef)], N, H, W)
+    assert L.lib().pmu_convT2x2_bf16_ok(fin, Cout) == 1
+    u = torch.empty(N, 2 * H, 2 * W, Cout, device=dev)
+    L.call("pmu_convT2x2_fwd_bf16", fin, _packT(w, False).data_ptr(), b.data_ptr(), Cout, u.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = TF.conv_transpose2d(_nchw(_rb(_bnrelu(z, coef))).double().cpu(), _rb(w).double().cpu(), b.double().cpu(),
+                              stride=2).permute(0, 2, 3, 1)
+    assert _rel(u, ref) <= TOL
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,oh,ow", [(2, 16, 16, 128, 64, 0, 0), (2, 10, 9, 256, 32, 1, 0),
+                                                  (1, 8, 12, 128, 128, 0, 1)])
+def test_convT_dgrad_bf16(dev, N, H, W, Cin, Cout, oh, ow):
+    from pmu_hip import _lib as L
+    g = torch.Generator().manual_seed(31 + H)
+    Hd, Wd = 2 * H + oh + (1 if oh else 0), 2 * W + ow + (1 if ow else 0)
+    du = torch.randn(N, Hd, Wd, Cout, generator=g).to(dev)
+    w = (torch.randn(Cin, Cout, 2, 2, generator=g) * 0.1).to(dev)
+    dx = torch.empty(N, H, W, Cin, device=dev)
+    L.call("pmu_convT2x2_dgrad_bf16", du.data_ptr(), Hd, Wd, oh, ow, _packT(w, True).data_ptr(), N, H, W, Cin, Cout,
+           dx.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    dui = du[:, oh:oh + 2 * H, ow:ow + 2 * W]
+    ref = TF.conv2d(_nchw(_rb(dui)).double().cpu(), _rb(w).double().cpu(), stride=2).permute(0, 2, 3, 1)
+    assert _rel(dx, ref) <= TOL
