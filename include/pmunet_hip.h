@@ -104,11 +104,13 @@ int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int Cout, float
  * Weights are always pre-packed (bf16, [row block of 64][chunk of 16][tap][64][16]). */
 size_t pmu_conv3x3_packed_size_bf16(int Cout, int Cin, int dgrad);
 int pmu_conv3x3_pack_bf16(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream);
-/* as pmu_conv3x3_fwd / _dgrad (part uses the same pmu_conv3x3_tiles() tile count) */
+/* as pmu_conv3x3_fwd / _dgrad (part uses the same pmu_conv3x3_tiles() tile count).  tee (nullable):
+ * receives the bf16 operand the kernel multiplied, [N][H][W][pad8(K channels)] as pmu_frame_to_bf16
+ * would write it (padding channels untouched) — the input of pmu_conv3x3_wgrad_bf16, for free. */
 int pmu_conv3x3_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int Cout,
-                         float* z, float* part, void* stream);
+                         float* z, float* part, unsigned short* tee, void* stream);
 int pmu_conv3x3_dgrad_bf16(const pmu_frame* dz, const unsigned short* wp, int Cin, int Csplit,
-                           float* dx0, float* dx1, void* stream);
+                           float* dx0, float* dx1, unsigned short* tee, void* stream);
 
 /* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels
  * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz

@@ -38,8 +38,32 @@ struct ConvArgsB {
   float* out0;
   float* out1;
   float* part;
+  unsigned short* tee;       // optional bf16 copy of the operand [N][H][W][pad8(KC)] (blockIdx.y == 0 writes)
   int NOUT, KC, split, tiles_w, tiles_h;
 };
+
+// Copy the staged chunk's interior pixels (the operand itself, already transformed and rounded to
+// bf16) from LDS to the tee tensor: the weight-gradient kernel reads these instead of
+// re-materialising the operand (pmu_frame_to_bf16).  512 units of 8 channels per chunk.
+template <int TWL>
+__device__ __forceinline__ void tee_chunk(const ConvArgsB& a, const unsigned short* As, int k0, int n, int h0, int w0,
+                                          int tid) {
+  constexpr int TW = 1 << TWL, HW2 = TW + 2;
+  const int Cp = (a.KC + 7) & ~7;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int u = tid + 256 * i;
+    const int q = u >> 1, half = u & 1;
+    const int r = q >> TWL, c = q & (TW - 1);
+    const int h = h0 + r, w = w0 + c, ch = k0 + 8 * half;
+    if (h < a.in.H && w < a.in.W && ch < a.KC) {
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = *reinterpret_cast<const u32x4*>(As + ((r + 1) * HW2 + c + 1) * LSB + 8 * half);
+      // streamed past the caches: read back only by the backward's weight-gradient kernel
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(a.tee + (((long long)n * a.in.H + h) * a.in.W + w) * Cp + ch));
+    }
+  }
+}
 
 __device__ __forceinline__ unsigned short bf16_bits(float v) {
   return __builtin_bit_cast(unsigned short, (__bf16)v);
@@ -140,6 +164,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(ConvArgsB a) {
       }
     }
     __syncthreads();
+    if (a.tee && blockIdx.y == 0) tee_chunk<TWL>(a, As, ch * BK, n, h0, w0, tid);
 
     // BNT = 64: the next tap's operands are read ahead of the current tap's MFMAs; BNT = 128 has
     // no registers for a second set (the partner wave on the SIMD covers the read latency)
@@ -305,12 +330,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_pipe_kernel(ConvArgsB a) 
     if (b4) *reinterpret_cast<uint4*>(Bs + ((tid + 1024) >> 1) * LSB + 8 * ((tid) & 1)) = pb4;             \
   }
 
+  const bool tee = a.tee && blockIdx.y == 0;
   PMU_PREFETCH(0)
   PMU_COMMIT()
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
     const bool more = ch + 1 < nch;
     if (more) PMU_PREFETCH(ch + 1)  // in flight during the MFMAs below
+    if (tee) tee_chunk<TWL>(a, As, ch * BK, n, h0, w0, tid);
     bf16x8 op[2][FM + FN];
     auto load_ops = [&](int tap, bf16x8 (&o)[FM + FN]) {
       const int toff = ((tap / 3) * HW2 + (tap % 3)) * LSB;
@@ -409,10 +436,10 @@ static int pick_twl(int W) {
 }
 
 static int launch_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int NOUT, int KC, float* out0,
-                       float* out1, int split, float* part, bool dgrad, void* stream) {
+                       float* out1, int split, float* part, unsigned short* tee, bool dgrad, void* stream) {
   ConvArgsB a;
   a.in = make_dev_frame(in);
-  a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
+  a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part; a.tee = tee;
   a.NOUT = NOUT; a.KC = KC; a.split = split;
   const int twl = pick_twl(in->W);
   const int TW = 1 << twl, TH = BM / TW;
@@ -474,15 +501,15 @@ extern "C" int pmu_conv3x3_pack_bf16(const float* w, int Cout, int Cin, int dgra
 }
 
 extern "C" int pmu_conv3x3_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int Cout,
-                                    float* z, float* part, void* stream) {
+                                    float* z, float* part, unsigned short* tee, void* stream) {
   PMU_REQUIRE(valid_frame(in) && wp && z && Cout > 0);
   const int Cin = in->src[0].C + (in->nsrc > 1 ? in->src[1].C : 0);
-  return launch_bf16(in, wp, bias, Cout, Cin, z, nullptr, Cout, part, false, stream);
+  return launch_bf16(in, wp, bias, Cout, Cin, z, nullptr, Cout, part, tee, false, stream);
 }
 
 extern "C" int pmu_conv3x3_dgrad_bf16(const pmu_frame* dz, const unsigned short* wp, int Cin, int Csplit, float* dx0,
-                                      float* dx1, void* stream) {
+                                      float* dx1, unsigned short* tee, void* stream) {
   PMU_REQUIRE(valid_frame(dz) && dz->nsrc == 1 && wp && dx0 && Cin > 0);
   PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
-  return launch_bf16(dz, wp, nullptr, Cin, dz->src[0].C, dx0, dx1, Csplit, nullptr, true, stream);
+  return launch_bf16(dz, wp, nullptr, Cin, dz->src[0].C, dx0, dx1, Csplit, nullptr, tee, true, stream);
 }

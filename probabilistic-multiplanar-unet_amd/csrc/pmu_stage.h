@@ -212,9 +212,14 @@ __device__ __forceinline__ void pmu_prefetch(const DevSrc& s, int c, int n, cons
   p.okmask = m;
 }
 
-template <int POOL, bool BWD, int NI, bool BF = false>
+struct PmuNoTee {
+  __device__ __forceinline__ void operator()(int, float4) const {}
+};
+
+// tee(i, v) sees every committed item's operand value (e.g. to keep a bf16 copy for the backward)
+template <int POOL, bool BWD, int NI, bool BF = false, class TEE = PmuNoTee>
 __device__ __forceinline__ void pmu_commit(const PmuPref<POOL, BWD, NI>& p, const int (&ih)[NI], const int (&dst)[NI],
-                                           void* lds) {
+                                           void* lds, const TEE& tee = TEE()) {
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     if (ih[i] == PMU_NO_ITEM) continue;
@@ -237,5 +242,6 @@ __device__ __forceinline__ void pmu_commit(const PmuPref<POOL, BWD, NI>& p, cons
     }
     if (!((p.okmask >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
     pmu_lds_store4<BF>(lds, dst[i], v);
+    tee(i, v);
   }
 }

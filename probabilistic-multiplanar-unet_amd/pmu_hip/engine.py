@@ -161,6 +161,7 @@ class ConvBNOut:
     srcs: list = field(default_factory=list)   # the operand sources it consumed (for wgrad)
     planes: list | None = None                  # first-layer input planes
     bf16: bool = False                          # computed on the bf16-MFMA kernels
+    xt: torch.Tensor | None = None              # bf16: the operand copy the forward kernel wrote (for wgrad)
 
     def act(self, pool=L.POOL_NONE) -> Src:
         return Src(self.z, L.SRC_BNRELU, self.bn.coef, pool=pool)
@@ -172,11 +173,12 @@ def first_layer_ok(cin: int, cout: int) -> bool:
 
 
 def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H, W, training, dev,
-                    planes=None, bf16=False) -> ConvBNOut:
+                    planes=None, bf16=False, keep=False) -> ConvBNOut:
     Cout = conv.out_channels
     s = L.stream()
     lb = L.lib()
     z = _empty(N, H, W, Cout, device=dev)
+    xt = None
     need_stats = training or not bn.track_running_stats
     if planes is not None and not first_layer_ok(len(planes), Cout):
         # channel counts outside the first-layer kernel: the generic 3x3 path on a raw NHWC frame
@@ -192,8 +194,11 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         R = lb.pmu_conv3x3_tiles(N, H, W)
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
         wp = pack_weights_bf16(conv.weight, dgrad=False)
+        Cin = sum(sr.C for sr in srcs)
+        xt = (torch.empty(N, H, W, _pad8(Cin), dtype=torch.int16, device=dev)
+              if keep else None)   # the weight gradient's operand, written for free (backward follows)
         L.call("pmu_conv3x3_fwd_bf16", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout, z.data_ptr(),
-               L.ptr(part), s)
+               L.ptr(part), L.ptr(xt), s)
     else:
         R = lb.pmu_conv3x3_tiles(N, H, W)
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
@@ -201,7 +206,8 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), wp.data_ptr(), L.ptr(conv.bias),
                Cout, z.data_ptr(), L.ptr(part), s)
     st = bn_forward(part, R, Cout, N * H * W, bn, training, dev)
-    return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes, bf16=bf16 and planes is None)
+    bfl = bf16 and planes is None
+    return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes, bf16=bfl, xt=xt if bfl else None)
 
 
 def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, need_dx=True, split=None):
@@ -259,29 +265,33 @@ def frame_to_bf16(srcs, N, H, W) -> torch.Tensor:
 
 
 def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split):
-    """bf16-MFMA backward of one conv layer (torch.autocast(bfloat16) arithmetic): the weight
-    gradient multiplies the materialised bf16 operands (dz after the BN+ReLU backward, and the
-    layer's BN+ReLU(+pool)(+concat) input); the input gradient stages dz's frame directly."""
+    """bf16-MFMA backward of one conv layer (torch.autocast(bfloat16) arithmetic).  The input
+    gradient stages dz's BN+ReLU-backward frame and tees the bf16 dz it multiplied; the weight
+    gradient then multiplies that copy with the forward's operand copy (out.xt), so neither operand
+    is materialised by a separate pass (pmu_frame_to_bf16 only when a copy is missing)."""
     s = L.stream()
     N, H, W, Cout = out.z.shape
     dev = out.z.device
     Cin = conv.in_channels
-    dzt = frame_to_bf16([dz_src], N, H, W)
-    xt = frame_to_bf16(out.srcs, N, H, W)
+    dzt = torch.empty(N, H, W, _pad8(Cout), dtype=torch.int16, device=dev)
+    res = None
+    if need_dx:
+        wp = pack_weights_bf16(conv.weight, dgrad=True)
+        dzf = frame_of([dz_src], N, H, W)
+        sp = Cin if split is None else split
+        dx0 = _empty(N, H, W, sp, device=dev)
+        dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin else None
+        L.call("pmu_conv3x3_dgrad_bf16", dzf, wp.data_ptr(), Cin, sp, dx0.data_ptr(), L.ptr(dx1), dzt.data_ptr(), s)
+        res = dx0 if split is None else (dx0, dx1)
+    else:
+        dzt = frame_to_bf16([dz_src], N, H, W)
+    xt = out.xt if out.xt is not None else frame_to_bf16(out.srcs, N, H, W)
+    out.xt = None
     wsb = L.lib().pmu_conv3x3_wgrad_ws_bf16(N, H, W, Cin, Cout)
     ws = _empty(max(1, (wsb + 3) // 4), device=dev)
     L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(), ws.data_ptr(),
            wsb, s)
-    del dzt, xt
-    if not need_dx:
-        return None
-    wp = pack_weights_bf16(conv.weight, dgrad=True)
-    dzf = frame_of([dz_src], N, H, W)
-    sp = Cin if split is None else split
-    dx0 = _empty(N, H, W, sp, device=dev)
-    dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin else None
-    L.call("pmu_conv3x3_dgrad_bf16", dzf, wp.data_ptr(), Cin, sp, dx0.data_ptr(), L.ptr(dx1), s)
-    return dx0 if split is None else (dx0, dx1)
+    return res
 
 
 def pack_weights_bf16(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
@@ -350,14 +360,15 @@ class UNetState:
         self.feat_src = None    # last DoubleConv output producer
 
 
-def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False):
+def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep: bool = False):
     """Forward of model.UNet on the HIP path.  Returns (output, state).
 
     Output: NCHW logits / sigmoid(logits) when net.apply_last_layer, else the last
     DoubleConv activation as an NCHW-shaped channels-last tensor (unet_model.py:48-54).
     bf16: the 3x3 convs (except the Cin <= 4 first layer) and the ConvTranspose2d forward / input
     gradient (where their shapes allow) run on the bf16-MFMA kernels (autocast arithmetic; see
-    include/pmunet_hip.h), the 3x3 weight gradients too."""
+    include/pmunet_hip.h), the 3x3 weight gradients too.  keep: a backward follows (bf16 convs keep
+    their operand copies for the weight gradient)."""
     assert x.is_cuda and x.dtype == F32 and x.dim() == 4
     dev = x.device
     N, Cin, H, W = x.shape
@@ -375,8 +386,8 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False):
         first_srcs = [Src(xc.permute(0, 2, 3, 1).contiguous())]
     # ---- encoder
     c1w, b1, c2w, b2 = _dc_layers(net.inc)
-    o1 = conv_bn_forward(first_srcs, c1w, b1, N, H, W, training, dev, planes=planes, bf16=bf16)
-    o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev, bf16=bf16)
+    o1 = conv_bn_forward(first_srcs, c1w, b1, N, H, W, training, dev, planes=planes, bf16=bf16, keep=keep)
+    o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev, bf16=bf16, keep=keep)
     st.enc.append((o1, o2))
     h, w = H, W
     for down in net.down_blocks:
@@ -384,8 +395,8 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False):
         c1w, b1, c2w, b2 = _dc_layers(dc)
         prev = st.enc[-1][1]
         h, w = h // 2, w // 2
-        o1 = conv_bn_forward([prev.act(L.POOL_MAX2)], c1w, b1, N, h, w, training, dev, bf16=bf16)
-        o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev, bf16=bf16)
+        o1 = conv_bn_forward([prev.act(L.POOL_MAX2)], c1w, b1, N, h, w, training, dev, bf16=bf16, keep=keep)
+        o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev, bf16=bf16, keep=keep)
         st.enc.append((o1, o2))
     # ---- decoder
     cur = st.enc[-1][1]
@@ -410,8 +421,8 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False):
         off = (dY // 2, dX // 2)
         c1w, b1, c2w, b2 = _dc_layers(up.conv)
         srcs = [skip.act(), Src(u, L.SRC_RAW, off=off)]
-        o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev, bf16=bf16)
-        o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev, bf16=bf16)
+        o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev, bf16=bf16, keep=keep)
+        o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev, bf16=bf16, keep=keep)
         st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2, bf16=bf16))
         cur = o2
     st.feat_src = cur

@@ -93,7 +93,7 @@ def use_bf16(net) -> bool:
 class UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, net, x, bf16, *params):
-        out, st = engine.unet_forward(net, x, net.training, bf16=bf16)
+        out, st = engine.unet_forward(net, x, net.training, bf16=bf16, keep=True)
         ctx.net = net
         ctx.st = st
         return out

@@ -49,9 +49,13 @@ def _fwd(srcs, N, H, W, w, bias, dev):
     R = L.lib().pmu_conv3x3_tiles(N, H, W)
     part = torch.empty(R, 2 * Cout, device=dev)
     wp = _pack(w, False)
+    C = sum(sr.C for sr in srcs)
+    tee = torch.zeros(N, H, W, (C + 7) // 8 * 8, dtype=torch.int16, device=dev)
     L.call("pmu_conv3x3_fwd_bf16", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(bias), Cout, z.data_ptr(),
-           part.data_ptr(), L.stream())
+           part.data_ptr(), tee.data_ptr(), L.stream())
     torch.cuda.synchronize()
+    # the operand copy equals the materialised operand bit for bit
+    assert torch.equal(tee[..., :C], _to_bf16(srcs, N, H, W, C)[..., :C])
     return z, part
 
 
@@ -122,9 +126,11 @@ def test_conv3x3_dgrad_bf16(dev, N, H, W, Cin, Cout, split):
     wp = _pack(w, True)
     dx0 = torch.empty(N, H, W, split, device=dev)
     dx1 = torch.empty(N, H, W, Cin - split, device=dev) if split < Cin else None
+    tee = torch.zeros(N, H, W, (Cout + 7) // 8 * 8, dtype=torch.int16, device=dev)
     L.call("pmu_conv3x3_dgrad_bf16", frame_of([Src(dz)], N, H, W), wp.data_ptr(), Cin, split, dx0.data_ptr(),
-           L.ptr(dx1), L.stream())
+           L.ptr(dx1), tee.data_ptr(), L.stream())
     torch.cuda.synchronize()
+    assert torch.equal(tee[..., :Cout], _to_bf16([Src(dz)], N, H, W, Cout)[..., :Cout])
     ref = torch.nn.grad.conv2d_input((N, Cin, H, W), _rb(w).double().cpu(), _nchw(_rb(dz)).double().cpu(),
                                      padding=1).permute(0, 2, 3, 1)
     got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)

@@ -92,9 +92,9 @@ def main():
             "mat_bf16": lambda: (L.call("pmu_frame_to_bf16", fdz, cpo, dzt.data_ptr(), s),
                                  L.call("pmu_frame_to_bf16", fin, cpi, xt.data_ptr(), s)),
             "fwd_bf16": lambda: L.call("pmu_conv3x3_fwd_bf16", fin, wbf.data_ptr(), b.data_ptr(), Cout,
-                                       out.data_ptr(), part.data_ptr(), s),
+                                       out.data_ptr(), part.data_ptr(), xt.data_ptr(), s),
             "dgrad_bf16": lambda: L.call("pmu_conv3x3_dgrad_bf16", fdz, wbd.data_ptr(), Cin, Cin, dx.data_ptr(),
-                                         None, s),
+                                         None, dzt.data_ptr(), s),
             "fwd": lambda: L.call("pmu_conv3x3_fwd", fin, w.data_ptr(), L.ptr(wpf), b.data_ptr(), Cout,
                                   out.data_ptr(), part.data_ptr(), s),
             "dgrad": lambda: L.call("pmu_conv3x3_dgrad", fdz, w.data_ptr(), L.ptr(wpd), Cin, Cin, dx.data_ptr(),
