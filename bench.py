@@ -31,6 +31,7 @@ import torch  # noqa: E402
 import torch.nn as nn  # noqa: E402
 
 METRIC = "2D slices/sec fwd+bwd, 256×256×1 batch32 U-Net; Dice vs ref"
+METRIC_C5 = "2D slices/sec fwd+bwd, 512×512×3 batch16 U-Net bf16 (BASELINE.json configs[4])"
 FP32_MFMA_PEAK_TF = 157.3
 BF16_MFMA_PEAK_TF = 2516.0   # dense bf16 MFMA (MI355X_MICROARCH.md; 2.5 PF, no sparsity)
 FILTERS = [64, 128, 256, 512, 1024]
@@ -65,7 +66,8 @@ class KernelTimer:
 
     MFMA = ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad", "pmu_convT2x2_fwd",
             "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd",
-            "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16")
+            "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16", "pmu_convT2x2_fwd_bf16",
+            "pmu_convT2x2_dgrad_bf16")
 
     def __init__(self):
         self.rec = []
@@ -81,6 +83,12 @@ class KernelTimer:
         if name == "pmu_conv3x3_wgrad_bf16":
             N, H, W, cout, cin = args[2], args[3], args[4], args[5], args[6]
             return 2.0 * N * H * W * cin * cout * 9
+        if name == "pmu_convT2x2_fwd_bf16":
+            f = args[0]._obj
+            return 2.0 * f.N * f.H * f.W * f.src[0].C * args[3] * 4
+        if name == "pmu_convT2x2_dgrad_bf16":
+            N, H, W, cin, cout = args[6], args[7], args[8], args[9], args[10]
+            return 2.0 * N * H * W * cin * cout * 4
         if name in ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad"):
             f = args[0]._obj
             cframe = sum(f.src[i].C for i in range(f.nsrc))
@@ -173,11 +181,17 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
                       f"{threads} threads"}
 
 
-# C-ABI entry -> device kernel family it launches (rocprof kernel names), for the PMC traffic lookup
+# C-ABI entry -> regex over the device kernels it launches (rocprof kernel names), for the PMC traffic lookup
 KERNEL_FAMILY = {
-    "pmu_conv3x3_fwd": "conv3x3_kernel<false>", "pmu_conv3x3_dgrad": "conv3x3_kernel<true>",
-    "pmu_conv3x3_wgrad": "wgrad3x3_kernel", "pmu_convT2x2_fwd": "ActRowA", "pmu_convT2x2_dgrad": "DuGatherA",
-    "pmu_convT2x2_wgrad": "convT_wgrad_kernel", "pmu_fcomb_fwd": "fcomb_fwd_kernel", "pmu_fcomb_bwd": "fcomb_bwd_kernel",
+    "pmu_conv3x3_fwd": r"conv3x3_(pipe_)?kernel<false", "pmu_conv3x3_dgrad": r"conv3x3_(pipe_)?kernel<true",
+    "pmu_conv3x3_wgrad": r"wgrad3x3_kernel<", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
+    "pmu_convT2x2_dgrad": r"convT_pipe_kernel<true>|DuGatherA",
+    "pmu_convT2x2_wgrad": r"convT_wgrad_(pipe_)?kernel", "pmu_fcomb_fwd": r"fcomb_fwd_kernel",
+    "pmu_fcomb_bwd": r"fcomb_bwd_kernel",
+    "pmu_conv3x3_fwd_bf16": r"conv3x3_bf16_pipe_kernel<false|conv3x3_bf16_kernel<\d, \d+, false>",
+    "pmu_conv3x3_dgrad_bf16": r"conv3x3_bf16_pipe_kernel<true|conv3x3_bf16_kernel<\d, \d+, true>",
+    "pmu_conv3x3_wgrad_bf16": r"wgrad3x3_bf16_kernel<", "pmu_convT2x2_fwd_bf16": r"convT_bf16_kernel<false>",
+    "pmu_convT2x2_dgrad_bf16": r"convT_bf16_kernel<true>",
 }
 
 
@@ -187,13 +201,14 @@ def pmc_traffic(workload, api):
     FETCH_SIZE / WRITE_SIZE passes of this bench command).  None when absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{workload}.json")))
+    import re
     fam = KERNEL_FAMILY.get(api)
     if not files or fam is None:
         return None, None
     data = json.load(open(files[-1]))["kernels"]
     tot, n = 0.0, 0
     for k, v in data.items():
-        if fam in k:
+        if re.search(fam, k):
             d = v["dispatches_fetch_pass"]
             tot += v["hbm_bytes_per_dispatch"] * d
             n += d
@@ -454,7 +469,7 @@ def main():
                            channels=args.channels, classes=args.classes)
     if rank == 0:
         res = {
-            "metric": METRIC, "value": round(value, 3), "unit": "slices/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC_C5 if args.workload == "c5" else METRIC, "value": round(value, 3), "unit": "slices/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.precision if args.workload != "probunet" else "fp32",
             "data": data, "config": config,
