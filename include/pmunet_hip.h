@@ -116,6 +116,8 @@ int pmu_conv3x3_dgrad_bf16(const pmu_frame* dz, const unsigned short* wp, int Ci
  * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz
  * that pmu_conv3x3_wgrad_bf16 multiplies. */
 int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* out, void* stream);
+/* out[N][H][W][C] = the frame's fp32 operand values (e.g. MaxPool2d of BN+ReLU, unet_parts.py:33). */
+int pmu_frame_to_f32(const pmu_frame* f, float* out, void* stream);
 /* dw[Cout][Cin][3][3] from dzt [N][H][W][pad8(Cout)] and xt [N][H][W][pad8(Cin)] (bf16, pad8(c) =
  * c rounded up to a multiple of 8); ws must hold pmu_conv3x3_wgrad_ws_bf16() bytes. */
 size_t pmu_conv3x3_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);

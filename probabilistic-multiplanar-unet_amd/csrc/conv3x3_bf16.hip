@@ -259,8 +259,31 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_kernel(ConvArgsB a) {
 constexpr int PB_UNITS = 9 * 64 * 2;               // 16-B units of a BNT = 64 B tile
 constexpr int PB_N = (PB_UNITS + 255) / 256;       // 5 (the last one for tid < 128)
 
+// Lean staging for the pipelined kernel: the items' pixel offsets inside the current source are
+// tile constants, computed once per source (32-bit element offsets: the host routes tensors of
+// >= 2^31 elements to the synchronous kernel), so a chunk's prefetch is NI (x2 for BN-backward)
+// float4 loads at offset + channel and its commit one transform per item — no per-item 64-bit
+// index arithmetic or divergent bounds branches in the pipelined loop.
+template <int TWL>
+__device__ __forceinline__ void item_offsets(const DevSrc& s, int n, int h0, int w0, int tid, int (&eo)[NI],
+                                             unsigned& okm) {
+  constexpr int TW = 1 << TWL, TH = BM >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
+  okm = 0u;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int it = tid + 256 * i;
+    const int hp = it >> 2;
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    const int hs = h0 - 1 + hr - s.off_h, ws = w0 - 1 + hc - s.off_w;
+    const bool ok = it < HP * 4 && hs >= 0 && ws >= 0 && hs < s.H && ws < s.W;
+    okm |= ok ? (1u << i) : 0u;
+    eo[i] = ok ? ((n * s.H + hs) * s.W + ws) * s.C : 0;
+  }
+}
+
 template <bool DGRAD, int POOL, int TWL>
 __global__ __launch_bounds__(256, 2) void conv3x3_bf16_pipe_kernel(ConvArgsB a) {
+  static_assert(POOL == PMU_POOL_NONE, "pooled sources are materialised (pmu_frame_to_f32) in bf16 mode");
   constexpr int BNT = 64, FM = 2, FN = 2, WM = 4;
   constexpr int TW = 1 << TWL, TH = BM >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
   __shared__ __attribute__((aligned(16))) unsigned short smem[A_ELEMS + 9 * BNT * LSB];
@@ -278,15 +301,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_pipe_kernel(ConvArgsB a) 
   const int nch = (a.KC + BK - 1) / BK;
   const int cq4 = 4 * (tid & 3);
 
-  int ih[NI], iw[NI], dst[NI];
+  int dst[NI];
+  unsigned vm = 0u;  // items this thread stages at all
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int it = tid + 256 * i;
-    const int hp = it >> 2;
-    const int hr = hp / HW2, hc = hp - hr * HW2;
-    ih[i] = (it < HP * 4) ? h0 - 1 + hr : PMU_NO_ITEM;
-    iw[i] = w0 - 1 + hc;
-    dst[i] = hp * LSB + 4 * (it & 3);
+    dst[i] = (it >> 2) * LSB + 4 * (it & 3);
+    vm |= (it < HP * 4) ? (1u << i) : 0u;
   }
   const int hsel = (lane >> 5) * 8;
   int abase[FM], bbase[FN];
@@ -306,28 +327,72 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_pipe_kernel(ConvArgsB a) 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  PmuPref<POOL, DGRAD, NI> pf;
-  uint4 pb0, pb1, pb2, pb3, pb4;  // packed-B prefetch (plain locals: a struct or array here lands in scratch)
+  // current source (s0 first, then s1 of a concat frame) and its tile-constant item offsets
+  int eo[NI];
+  unsigned okm;
+  int second = 0;
+  const float* sx = F.s0.x;
+  const float* sz = F.s0.z;
+  const float* sco = F.s0.coef;
+  int sC = F.s0.C, sraw = F.s0.mode == PMU_SRC_RAW;
+  item_offsets<TWL>(F.s0, n, h0, w0, tid, eo, okm);
+
+  float4 px0, px1, px2, px3, px4, px5;  // prefetched operand items (plain locals: no scratch)
+  float4 pz0, pz1, pz2, pz3, pz4, pz5;  // BN-backward: z of the same items
+  float4 psc, psh, pmu, pkx, pkc;
+  uint4 pb0, pb1, pb2, pb3, pb4;
   const uint4* wtile = reinterpret_cast<const uint4*>(a.wp) + (long long)(j0 / PJ) * nch * (9 * PJ * BK / 8);
   const bool b4 = tid < PB_UNITS - 4 * 256;
-  static_assert(PB_N == 5, "five B units per thread");
-#define PMU_PREFETCH(CH)                                                                                    \
-  {                                                                                                        \
-    const int k0_ = (CH) * BK;                                                                             \
-    const bool second_ = F.nsrc > 1 && k0_ >= F.C0;                                                        \
-    pmu_prefetch<POOL, DGRAD, NI>(pmu_pick_src(F, second_), k0_ - (second_ ? F.C0 : 0) + cq4, n, ih, iw, pf); \
-    const uint4* src_ = wtile + (long long)(CH) * (9 * PJ * BK / 8) + tid;                               \
-    pb0 = src_[0]; pb1 = src_[256]; pb2 = src_[512]; pb3 = src_[768];                                      \
-    pb4 = src_[b4 ? 1024 : 0];                                                                             \
+  static_assert(PB_N == 5 && NI == 6, "staging register layout");
+#define PMU_X(I) (*reinterpret_cast<const float4*>(sx + (unsigned)(eo[I] + c_)))
+#define PMU_Z(I) (*reinterpret_cast<const float4*>(sz + (unsigned)(eo[I] + c_)))
+#define PMU_PREFETCH(CH)                                                                         \
+  {                                                                                             \
+    const int k0_ = (CH) * BK;                                                                  \
+    if (F.nsrc > 1 && !second && k0_ >= F.C0) { /* uniform: switch to the concat's 2nd source */ \
+      second = 1;                                                                               \
+      sx = F.s1.x; sz = F.s1.z; sco = F.s1.coef; sC = F.s1.C; sraw = F.s1.mode == PMU_SRC_RAW;  \
+      item_offsets<TWL>(F.s1, n, h0, w0, tid, eo, okm);                                         \
+    }                                                                                           \
+    const int c_ = k0_ - (second ? F.C0 : 0) + cq4;                                             \
+    px0 = PMU_X(0); px1 = PMU_X(1); px2 = PMU_X(2); px3 = PMU_X(3); px4 = PMU_X(4); px5 = PMU_X(5); \
+    if (DGRAD) {                                                                                \
+      pz0 = PMU_Z(0); pz1 = PMU_Z(1); pz2 = PMU_Z(2); pz3 = PMU_Z(3); pz4 = PMU_Z(4); pz5 = PMU_Z(5); \
+      pmu = *reinterpret_cast<const float4*>(sco + 2 * sC + c_);                                \
+      pkx = *reinterpret_cast<const float4*>(sco + 3 * sC + c_);                                \
+      pkc = *reinterpret_cast<const float4*>(sco + 4 * sC + c_);                                \
+    }                                                                                           \
+    if (DGRAD || !sraw) {                                                                       \
+      psc = *reinterpret_cast<const float4*>(sco + c_);                                         \
+      psh = *reinterpret_cast<const float4*>(sco + sC + c_);                                    \
+    }                                                                                           \
+    const uint4* src_ = wtile + (long long)(CH) * (9 * PJ * BK / 8) + tid;                      \
+    pb0 = src_[0]; pb1 = src_[256]; pb2 = src_[512]; pb3 = src_[768];                           \
+    pb4 = src_[b4 ? 1024 : 0];                                                                  \
   }
-#define PMU_COMMIT()                                                                                        \
-  {                                                                                                        \
-    pmu_commit<POOL, DGRAD, NI, true>(pf, ih, dst, As);                                                    \
-    *reinterpret_cast<uint4*>(Bs + ((tid) >> 1) * LSB + 8 * ((tid) & 1)) = pb0;                            \
-    *reinterpret_cast<uint4*>(Bs + ((tid + 256) >> 1) * LSB + 8 * ((tid) & 1)) = pb1;                      \
-    *reinterpret_cast<uint4*>(Bs + ((tid + 512) >> 1) * LSB + 8 * ((tid) & 1)) = pb2;                      \
-    *reinterpret_cast<uint4*>(Bs + ((tid + 768) >> 1) * LSB + 8 * ((tid) & 1)) = pb3;                      \
-    if (b4) *reinterpret_cast<uint4*>(Bs + ((tid + 1024) >> 1) * LSB + 8 * ((tid) & 1)) = pb4;             \
+#define PMU_ITEM(I, X, Z)                                                                        \
+  if ((vm >> (I)) & 1u) {                                                                       \
+    float4 v_;                                                                                  \
+    if (DGRAD) {                                                                                \
+      v_ = make_float4(pmu_bnbwd1(X.x, Z.x, psc.x, psh.x, pmu.x, pkx.x, pkc.x),                 \
+                       pmu_bnbwd1(X.y, Z.y, psc.y, psh.y, pmu.y, pkx.y, pkc.y),                 \
+                       pmu_bnbwd1(X.z, Z.z, psc.z, psh.z, pmu.z, pkx.z, pkc.z),                 \
+                       pmu_bnbwd1(X.w, Z.w, psc.w, psh.w, pmu.w, pkx.w, pkc.w));                \
+    } else {                                                                                    \
+      v_ = sraw ? X : pmu_bnrelu4(X, psc, psh);                                                 \
+    }                                                                                           \
+    if (!((okm >> (I)) & 1u)) v_ = make_float4(0.f, 0.f, 0.f, 0.f);                             \
+    pmu_lds_store4<true>(As, dst[I], v_);                                                       \
+  }
+#define PMU_COMMIT()                                                                             \
+  {                                                                                             \
+    PMU_ITEM(0, px0, pz0) PMU_ITEM(1, px1, pz1) PMU_ITEM(2, px2, pz2)                           \
+    PMU_ITEM(3, px3, pz3) PMU_ITEM(4, px4, pz4) PMU_ITEM(5, px5, pz5)                           \
+    *reinterpret_cast<uint4*>(Bs + ((tid) >> 1) * LSB + 8 * ((tid) & 1)) = pb0;                 \
+    *reinterpret_cast<uint4*>(Bs + ((tid + 256) >> 1) * LSB + 8 * ((tid) & 1)) = pb1;           \
+    *reinterpret_cast<uint4*>(Bs + ((tid + 512) >> 1) * LSB + 8 * ((tid) & 1)) = pb2;           \
+    *reinterpret_cast<uint4*>(Bs + ((tid + 768) >> 1) * LSB + 8 * ((tid) & 1)) = pb3;           \
+    if (b4) *reinterpret_cast<uint4*>(Bs + ((tid + 1024) >> 1) * LSB + 8 * ((tid) & 1)) = pb4;  \
   }
 
   const bool tee = a.tee && blockIdx.y == 0;
@@ -364,33 +429,42 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16_pipe_kernel(ConvArgsB a) 
   }
 #undef PMU_PREFETCH
 #undef PMU_COMMIT
+#undef PMU_ITEM
+#undef PMU_X
+#undef PMU_Z
 
-  // epilogue (as conv3x3_bf16_kernel with WN = 1)
+  // epilogue (as conv3x3_bf16_kernel with WN = 1).  Per channel block of 32 the destination
+  // (z, or the dx half the channels fall in: split % 32 == 0, host-checked) is uniform; in a full
+  // tile every element is stored without bounds tests, addressed from one 32-bit pixel base per
+  // fragment row plus compile-time pixel offsets.
   float* red = reinterpret_cast<float*>(smem);
   float s1[FN], s2[FN];
+  const bool full = h0 + TH <= F.H && w0 + TW <= F.W && j0 + BNT <= a.NOUT;
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
     s1[fn] = 0.f; s2[fn] = 0.f;
-    const int j = j0 + fn * 32 + (lane & 31);
+    const int jb = j0 + fn * 32;
+    const int j = jb + (lane & 31);
     const bool jok = j < a.NOUT;
     const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+    float* dstp;
+    int ld;
+    if (!DGRAD) { dstp = a.out0 + j; ld = a.NOUT; }
+    else if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
+    else { dstp = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int q = wm * 32 * FM + fm * 32 + acc_row(r, lane);
         const int h = h0 + (q >> TWL), w = w0 + (q & (TW - 1));
-        if (!jok || h >= F.H || w >= F.W) continue;
-        const long long pix = ((long long)n * F.H + h) * F.W + w;
+        if (!full && (!jok || h >= F.H || w >= F.W)) continue;
+        const unsigned pix = (unsigned)((n * F.H + h) * F.W + w);
         const float v = acc[fm][fn][r] + b;
+        dstp[(size_t)pix * (unsigned)ld] = v;
         if (!DGRAD) {
-          a.out0[pix * a.NOUT + j] = v;
           s1[fn] += v;
           s2[fn] = fmaf(v, v, s2[fn]);
-        } else if (j < a.split) {
-          a.out0[pix * a.split + j] = v;
-        } else {
-          a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
         }
       }
     }
@@ -456,7 +530,12 @@ static int launch_bf16(const pmu_frame* in, const unsigned short* wp, const floa
     const bool ok = pipe_src_ok(s0) && (!two || (pipe_src_ok(s1) && s1.pool == pool));
     const bool modes_ok = dgrad ? (!two && s0.mode == PMU_SRC_BNBWD)
                                 : (s0.mode != PMU_SRC_BNBWD && (!two || s1.mode != PMU_SRC_BNBWD));
-    if (ok && modes_ok && !getenv("PMU_BF16_NOPIPE")) {
+    // 32-bit item offsets inside every source, 32-bit pixel indices of the output
+    const bool small = (long long)s0.C * s0.H * s0.W * in->N < (1LL << 31) &&
+                       (!two || (long long)s1.C * s1.H * s1.W * in->N < (1LL << 31)) &&
+                       (long long)in->N * in->H * in->W < (1LL << 31);
+    const bool split_ok = !dgrad || split % 32 == 0 || split == NOUT;
+    if (ok && modes_ok && small && split_ok && pool == PMU_POOL_NONE && !getenv("PMU_BF16_NOPIPE")) {
 #define PMU_BP(D, P, T)                                                                    \
   if (dgrad == D && pool == P && twl == T) {                                               \
     hipLaunchKernelGGL((conv3x3_bf16_pipe_kernel<D, P, T>), grid, dim3(256), 0, st, a);    \
@@ -464,7 +543,6 @@ static int launch_bf16(const pmu_frame* in, const unsigned short* wp, const floa
     return PMU_OK;                                                                         \
   }
       PMU_BP(false, PMU_POOL_NONE, 3) PMU_BP(false, PMU_POOL_NONE, 4) PMU_BP(false, PMU_POOL_NONE, 5)
-      PMU_BP(false, PMU_POOL_MAX2, 3) PMU_BP(false, PMU_POOL_MAX2, 4) PMU_BP(false, PMU_POOL_MAX2, 5)
       PMU_BP(true, PMU_POOL_NONE, 3) PMU_BP(true, PMU_POOL_NONE, 4) PMU_BP(true, PMU_POOL_NONE, 5)
 #undef PMU_BP
     }

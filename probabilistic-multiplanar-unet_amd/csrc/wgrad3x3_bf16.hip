@@ -240,6 +240,29 @@ __global__ __launch_bounds__(256) void frame_to_bf16_kernel(DevFrame f, int Cpad
   }
 }
 
+// operand materialisation in fp32: out[p][c] = frame value (e.g. a max-pooled BN+ReLU activation,
+// consumed as a RAW source so the conv kernels need no pooled staging variant)
+__global__ __launch_bounds__(256) void frame_to_f32_kernel(DevFrame f, float* __restrict__ out) {
+  const int nq = (f.C + 3) / 4;
+  const long long total = (long long)f.N * f.H * f.W * nq;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int cq = (int)(e % nq);
+    long long pix = e / nq;
+    const int w = (int)(pix % f.W);
+    long long t = pix / f.W;
+    const int h = (int)(t % f.H);
+    const int n = (int)(t / f.H);
+    const float4 v = frame_value4(f, n, h, w, 4 * cq);
+    float* o = out + pix * f.C + 4 * cq;
+    if (f.C % 4 == 0) {
+      *reinterpret_cast<float4*>(o) = v;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int k = 0; k < 4 && 4 * cq + k < f.C; ++k) o[k] = vv[k];
+    }
+  }
+}
+
 static int pad8(int c) { return (c + 7) & ~7; }
 
 static void geometry(int N, int H, int W, int Cin, int Cout, int* wco, int* twl, int* tiles_w, int* tiles_h,
@@ -268,6 +291,17 @@ extern "C" int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* o
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(frame_to_bf16_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, make_dev_frame(f),
                      Cpad, out);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_frame_to_f32(const pmu_frame* f, float* out, void* stream) {
+  PMU_REQUIRE(valid_frame(f) && out);
+  const DevFrame d = make_dev_frame(f);
+  const long long total = (long long)d.N * d.H * d.W * ((d.C + 3) / 4);
+  long long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(frame_to_f32_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, d, out);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -395,7 +395,15 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         c1w, b1, c2w, b2 = _dc_layers(dc)
         prev = st.enc[-1][1]
         h, w = h // 2, w // 2
-        o1 = conv_bn_forward([prev.act(L.POOL_MAX2)], c1w, b1, N, h, w, training, dev, bf16=bf16, keep=keep)
+        if bf16:
+            # bf16 mode: the max-pooled activation is materialised once (1/4 of the producer's bytes) and
+            # every column block of the conv reads it raw instead of re-pooling
+            pooled = _empty(N, h, w, prev.z.shape[3], device=dev)
+            L.call("pmu_frame_to_f32", frame_of([prev.act(L.POOL_MAX2)], N, h, w), pooled.data_ptr(), L.stream())
+            srcs = [Src(pooled)]
+        else:
+            srcs = [prev.act(L.POOL_MAX2)]
+        o1 = conv_bn_forward(srcs, c1w, b1, N, h, w, training, dev, bf16=bf16, keep=keep)
         o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev, bf16=bf16, keep=keep)
         st.enc.append((o1, o2))
     # ---- decoder
