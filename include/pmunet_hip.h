@@ -112,6 +112,16 @@ int pmu_conv3x3_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const fl
 int pmu_conv3x3_dgrad_bf16(const pmu_frame* dz, const unsigned short* wp, int Cin, int Csplit,
                            float* dx0, float* dx1, unsigned short* tee, void* stream);
 
+/* The bf16-mode main path: a conv whose operand was materialised once by pmu_frame_to_bf16
+ * (xt / dzt: [N][H][W][Cp] bf16, Cp % 8 == 0), weights packed per 64 output rows x 32 channels
+ * (pmu_conv3x3_pack_raw).  Outputs as pmu_conv3x3_fwd / _dgrad; dgrad needs Csplit % 32 == 0 when
+ * Csplit < Cin; N*H*W*Cp < 2^31. */
+size_t pmu_conv3x3_packed_size_raw(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_raw(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream);
+int pmu_conv3x3_fwd_raw(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
+                        const float* bias, int Cout, float* z, float* part, void* stream);
+int pmu_conv3x3_dgrad_raw(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                          int Cin, int Csplit, float* dx0, float* dx1, void* stream);
 /* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels
  * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz
  * that pmu_conv3x3_wgrad_bf16 multiplies. */

@@ -1,0 +1,299 @@
+// 3x3 / pad 1 convolution of a materialised bf16 operand on bf16 MFMA (config c5's main path).
+//
+// nn.Conv2d(k=3, padding=1) of DoubleConv (PMU/model/unet/unet_parts.py:15,18) forward, and its
+// input gradient, with torch.autocast(bfloat16) arithmetic.  In bf16 mode every conv operand is
+// first written once as a dense bf16 NHWC tensor by one streaming pass (pmu_frame_to_bf16: the
+// producer's BatchNorm + ReLU, the max-pool, the F.pad + torch.cat of the skip connection, or
+// the BN+ReLU backward of dz), which the weight gradient needs anyway.  The GEMM kernel then only
+// copies 16-B units into LDS: half the bytes of the fp32 sources (a quarter for dz), no transform
+// arithmetic and half the prefetch registers of the fused-staging kernel (conv3x3_bf16.hip).
+//
+// GEMM view: M = 256 output pixels (TH x TW tile), N = 64 output channels, K = 9 taps x channels,
+// chunks of 32 channels: the (TH+2) x (TW+2) halo tile (80-B rows) and 9 x 64 x 32 packed weights
+// are staged per chunk, each tap is two 32x32x16 k-steps.  4 waves of 64 px x 64 ch (2 x 2
+// accumulators), 2 blocks per CU (73 KB LDS), the next chunk's 15 units per thread in registers
+// under the current chunk's 72 MFMAs per wave.
+#include <cstdlib>
+
+#include "pmu_stage.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BM = 256, BNT = 64, BK = 32;
+constexpr int LS = 40;       // LDS row stride (bf16): 64 B of data + 16 B pad, ds_read_b128 conflict-free
+constexpr int MAX_HP = 340;  // (8+2)*(32+2)
+constexpr int NA = 6;        // A units per thread: ceil(340 * 4 / 256)
+constexpr int NB = 9;        // B units per thread: 9 * 64 * 4 / 256
+constexpr int A_EL = MAX_HP * LS, B_EL = 9 * BNT * LS;
+
+struct RawArgs {
+  const unsigned short* x;   // operand [N][H][W][Cp] bf16
+  const unsigned short* wp;  // packed [jb][ch][tap][64][32] bf16
+  const float* bias;
+  float* out0;
+  float* out1;
+  float* part;
+  int N, H, W, Cp, NOUT, split, tiles_w, tiles_h, nch;
+};
+
+__device__ __forceinline__ unsigned short bf16_bits(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
+
+// wp[jb][ch][tap][jl][kl] = B[tap][j = 64 jb + jl][k = 32 ch + kl], zero padded, bf16 RNE
+//   forward: B[tap][co][ci] = w[co][ci][tap];  dgrad: B[tap][ci][co] = w[co][ci][8 - tap]
+__global__ __launch_bounds__(256) void pack_raw_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
+                                                       unsigned short* __restrict__ wp) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  const int nch = (KC + BK - 1) / BK, njb = (NOUT + BNT - 1) / BNT;
+  const long long total = (long long)njb * nch * 9 * BNT * BK;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int kl = (int)(e % BK);
+    long long r = e / BK;
+    const int jl = (int)(r % BNT); r /= BNT;
+    const int tap = (int)(r % 9); r /= 9;
+    const int ch = (int)(r % nch);
+    const int jb = (int)(r / nch);
+    const int j = jb * BNT + jl, k = ch * BK + kl;
+    float v = 0.f;
+    if (j < NOUT && k < KC)
+      v = dgrad ? w[((long long)k * Cin + j) * 9 + (8 - tap)] : w[((long long)j * Cin + k) * 9 + tap];
+    wp[e] = bf16_bits(v);
+  }
+}
+
+template <bool DGRAD, int TWL>
+__global__ __launch_bounds__(256, 2) void conv3x3_raw_kernel(RawArgs a) {
+  constexpr int FM = 2, FN = 2;
+  constexpr int TW = 1 << TWL, TH = BM >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
+  __shared__ __attribute__((aligned(16))) unsigned short smem[A_EL + B_EL];
+  unsigned short* As = smem;
+  unsigned short* Bs = smem + A_EL;
+  const int tid = threadIdx.x, lane = tid & 63, wm = tid >> 6;
+  int t = blockIdx.x;
+  const int tw = t % a.tiles_w; t /= a.tiles_w;
+  const int th = t % a.tiles_h; t /= a.tiles_h;
+  const int n = t;
+  const int h0 = th * TH, w0 = tw * TW;
+  const int j0 = blockIdx.y * BNT;
+
+  // A units: halo pixel hp = it >> 2, 8-channel unit q = it & 3; tile-constant 32-bit offsets
+  int eo[NA], dsta[NA];
+  unsigned okm = 0u, vm = 0u;
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int it = tid + 256 * i;
+    const int hp = it >> 2, q = it & 3;
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    const int h = h0 - 1 + hr, w = w0 - 1 + hc;
+    const bool v = it < HP * 4;
+    const bool ok = v && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    vm |= v ? (1u << i) : 0u;
+    okm |= ok ? (1u << i) : 0u;
+    eo[i] = ok ? ((n * a.H + h) * a.W + w) * a.Cp + 8 * q : 0;
+    dsta[i] = hp * LS + 8 * q;
+  }
+  const int hsel = (lane >> 5) * 8;
+  int abase[FM], bbase[FN];
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int q = wm * 64 + fm * 32 + (lane & 31);
+    abase[fm] = ((q >> TWL) * HW2 + (q & (TW - 1))) * LS + hsel;
+  }
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) bbase[fn] = (fn * 32 + (lane & 31)) * LS + hsel;
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const uint4* wt = reinterpret_cast<const uint4*>(a.wp) + (long long)(j0 / BNT) * a.nch * (9 * BNT * BK / 8) + tid;
+  uint4 ra0, ra1, ra2, ra3, ra4, ra5;                     // plain locals (no scratch)
+  uint4 rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7, rb8;
+  static_assert(NA == 6 && NB == 9, "staging register layout");
+  // channel units past Cp (a partial last chunk) read as zero
+#define PMU_RA(I, R)                                                                               \
+  {                                                                                               \
+    const bool k_ = ((okm >> (I)) & 1u) && k0_ + 8 * ((tid + 256 * (I)) & 3) < a.Cp;              \
+    const uint4 v_ = *reinterpret_cast<const uint4*>(a.x + (k_ ? (unsigned)(eo[I] + k0_) : 0u));  \
+    R = make_uint4(k_ ? v_.x : 0u, k_ ? v_.y : 0u, k_ ? v_.z : 0u, k_ ? v_.w : 0u);               \
+  }
+#define PMU_PREFETCH(CH)                                                                           \
+  {                                                                                               \
+    const int k0_ = (CH) * BK;                                                                    \
+    PMU_RA(0, ra0) PMU_RA(1, ra1) PMU_RA(2, ra2) PMU_RA(3, ra3) PMU_RA(4, ra4) PMU_RA(5, ra5)    \
+    const uint4* s_ = wt + (long long)(CH) * (9 * BNT * BK / 8);                                  \
+    rb0 = s_[0]; rb1 = s_[256]; rb2 = s_[512]; rb3 = s_[768]; rb4 = s_[1024];                    \
+    rb5 = s_[1280]; rb6 = s_[1536]; rb7 = s_[1792]; rb8 = s_[2048];                              \
+  }
+#define PMU_WA(I, R) \
+  if ((vm >> (I)) & 1u) *reinterpret_cast<uint4*>(As + dsta[I]) = R;
+#define PMU_WB(I, R) *reinterpret_cast<uint4*>(Bs + ((tid + 256 * (I)) >> 2) * LS + 8 * (tid & 3)) = R;
+#define PMU_COMMIT()                                                                               \
+  {                                                                                               \
+    PMU_WA(0, ra0) PMU_WA(1, ra1) PMU_WA(2, ra2) PMU_WA(3, ra3) PMU_WA(4, ra4) PMU_WA(5, ra5)    \
+    PMU_WB(0, rb0) PMU_WB(1, rb1) PMU_WB(2, rb2) PMU_WB(3, rb3) PMU_WB(4, rb4)                    \
+    PMU_WB(5, rb5) PMU_WB(6, rb6) PMU_WB(7, rb7) PMU_WB(8, rb8)                                   \
+  }
+
+  PMU_PREFETCH(0)
+  PMU_COMMIT()
+  __syncthreads();
+  for (int ch = 0; ch < a.nch; ++ch) {
+    const bool more = ch + 1 < a.nch;
+    if (more) PMU_PREFETCH(ch + 1)  // in flight during the MFMAs below
+    bf16x8 op[2][FM + FN];
+    auto load_ops = [&](int tap, int s, bf16x8 (&o)[FM + FN]) {
+      const int toff = ((tap / 3) * HW2 + (tap % 3)) * LS + 16 * s;
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) o[fm] = *reinterpret_cast<const bf16x8*>(As + abase[fm] + toff);
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+        o[FM + fn] = *reinterpret_cast<const bf16x8*>(Bs + tap * BNT * LS + bbase[fn] + 16 * s);
+    };
+    load_ops(0, 0, op[0]);
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {  // 9 taps x 2 k-steps
+      if (st + 1 < 18) load_ops((st + 1) >> 1, (st + 1) & 1, op[(st + 1) & 1]);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st & 1][fm], op[st & 1][FM + fn], acc[fm][fn], 0, 0, 0);
+    }
+    __syncthreads();
+    if (more) {
+      PMU_COMMIT()
+      __syncthreads();
+    }
+  }
+#undef PMU_RA
+#undef PMU_PREFETCH
+#undef PMU_WA
+#undef PMU_WB
+#undef PMU_COMMIT
+
+  // epilogue: per 32-channel block the destination is uniform (split % 32 == 0, host-checked);
+  // full tiles store without bounds tests
+  float* red = reinterpret_cast<float*>(smem);
+  float s1[FN], s2[FN];
+  const bool full = h0 + TH <= a.H && w0 + TW <= a.W && j0 + BNT <= a.NOUT;
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    s1[fn] = 0.f; s2[fn] = 0.f;
+    const int jb = j0 + fn * 32;
+    const int j = jb + (lane & 31);
+    const bool jok = j < a.NOUT;
+    const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+    float* dstp;
+    int ld;
+    if (!DGRAD) { dstp = a.out0 + j; ld = a.NOUT; }
+    else if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
+    else { dstp = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = wm * 64 + fm * 32 + acc_row(r, lane);
+        const int h = h0 + (q >> TWL), w = w0 + (q & (TW - 1));
+        if (!full && (!jok || h >= a.H || w >= a.W)) continue;
+        const unsigned pix = (unsigned)((n * a.H + h) * a.W + w);
+        const float v = acc[fm][fn][r] + b;
+        dstp[(size_t)pix * (unsigned)ld] = v;
+        if (!DGRAD) {
+          s1[fn] += v;
+          s2[fn] = fmaf(v, v, s2[fn]);
+        }
+      }
+    }
+  }
+  if (!DGRAD && a.part) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] += __shfl_xor(s1[fn], 32, 64);
+      s2[fn] += __shfl_xor(s2[fn], 32, 64);
+      if (lane < 32) {
+        red[(wm * BNT + fn * 32 + lane) * 2 + 0] = s1[fn];
+        red[(wm * BNT + fn * 32 + lane) * 2 + 1] = s2[fn];
+      }
+    }
+    __syncthreads();
+    if (tid < BNT) {
+      const int j = j0 + tid;
+      if (j < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          t1 += red[(v * BNT + tid) * 2 + 0];
+          t2 += red[(v * BNT + tid) * 2 + 1];
+        }
+        a.part[((long long)blockIdx.x * 2 + 0) * a.NOUT + j] = t1;
+        a.part[((long long)blockIdx.x * 2 + 1) * a.NOUT + j] = t2;
+      }
+    }
+  }
+}
+
+static int pick_twl(int W) {
+  if (W > 16) return 5;
+  if (W > 8) return 4;
+  return 3;
+}
+
+static int launch_raw(const unsigned short* x, int Cp, int N, int H, int W, const unsigned short* wp,
+                      const float* bias, int NOUT, float* out0, float* out1, int split, float* part, bool dgrad,
+                      void* stream) {
+  PMU_REQUIRE(x && wp && out0 && N > 0 && H > 0 && W > 0 && Cp > 0 && Cp % 8 == 0 && NOUT > 0);
+  PMU_REQUIRE((long long)N * H * W * Cp < (1LL << 31));
+  PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && out1));
+  RawArgs a;
+  a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
+  a.N = N; a.H = H; a.W = W; a.Cp = Cp; a.NOUT = NOUT; a.split = dgrad ? split : NOUT;
+  const int twl = pick_twl(W);
+  const int TW = 1 << twl, TH = BM / TW;
+  a.tiles_w = pmu_cdiv(W, TW);
+  a.tiles_h = pmu_cdiv(H, TH);
+  a.nch = pmu_cdiv(Cp, BK);
+  dim3 grid((unsigned)(a.tiles_w * a.tiles_h * N), (unsigned)pmu_cdiv(NOUT, BNT));
+  hipStream_t st = (hipStream_t)stream;
+#define PMU_RK(D, T)                                                                  \
+  if (dgrad == D && twl == T) {                                                       \
+    hipLaunchKernelGGL((conv3x3_raw_kernel<D, T>), grid, dim3(256), 0, st, a);        \
+    PMU_CHECK_LAUNCH();                                                               \
+    return PMU_OK;                                                                    \
+  }
+  PMU_RK(false, 3) PMU_RK(false, 4) PMU_RK(false, 5) PMU_RK(true, 3) PMU_RK(true, 4) PMU_RK(true, 5)
+#undef PMU_RK
+  return PMU_ERR_ARG;
+}
+
+}  // namespace
+
+extern "C" size_t pmu_conv3x3_packed_size_raw(int Cout, int Cin, int dgrad) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  return (size_t)pmu_cdiv(NOUT, BNT) * pmu_cdiv(KC, BK) * 9 * BNT * BK * sizeof(unsigned short);
+}
+
+extern "C" int pmu_conv3x3_pack_raw(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream) {
+  PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
+  const long long total = (long long)(pmu_conv3x3_packed_size_raw(Cout, Cin, dgrad) / sizeof(unsigned short));
+  long long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(pack_raw_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_conv3x3_fwd_raw(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                   const float* bias, int Cout, float* z, float* part, void* stream) {
+  return launch_raw(xt, Cp, N, H, W, wp, bias, Cout, z, nullptr, Cout, part, false, stream);
+}
+
+extern "C" int pmu_conv3x3_dgrad_raw(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                     int Cin, int Csplit, float* dx0, float* dx1, void* stream) {
+  return launch_raw(dzt, Cp, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
+}

@@ -193,12 +193,22 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
     elif bf16:
         R = lb.pmu_conv3x3_tiles(N, H, W)
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
-        wp = pack_weights_bf16(conv.weight, dgrad=False)
-        Cin = sum(sr.C for sr in srcs)
-        xt = (torch.empty(N, H, W, _pad8(Cin), dtype=torch.int16, device=dev)
-              if keep else None)   # the weight gradient's operand, written for free (backward follows)
-        L.call("pmu_conv3x3_fwd_bf16", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout, z.data_ptr(),
-               L.ptr(part), L.ptr(xt), s)
+        Cp = _pad8(sum(sr.C for sr in srcs))
+        if raw_ok(N, H, W, Cp):
+            # the operand (BN+ReLU / max-pool / F.pad+cat applied) written once in bf16; the GEMM
+            # streams it, and the weight gradient reuses it
+            xt = frame_to_bf16(srcs, N, H, W)
+            wp = pack_weights_raw(conv.weight, dgrad=False)
+            L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), Cp, N, H, W, wp.data_ptr(), L.ptr(conv.bias), Cout,
+                   z.data_ptr(), L.ptr(part), s)
+            if not keep:
+                xt = None
+        else:
+            wp = pack_weights_bf16(conv.weight, dgrad=False)
+            xt = (torch.empty(N, H, W, Cp, dtype=torch.int16, device=dev)
+                  if keep else None)   # the weight gradient's operand, teed by the fused kernel
+            L.call("pmu_conv3x3_fwd_bf16", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout,
+                   z.data_ptr(), L.ptr(part), L.ptr(xt), s)
     else:
         R = lb.pmu_conv3x3_tiles(N, H, W)
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
@@ -264,27 +274,35 @@ def frame_to_bf16(srcs, N, H, W) -> torch.Tensor:
     return out
 
 
+def raw_ok(N, H, W, Cp) -> bool:
+    """Shapes the materialised-operand bf16 conv takes (pmu_conv3x3_fwd_raw / _dgrad_raw)."""
+    return N * H * W * Cp < 2 ** 31
+
+
 def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split):
-    """bf16-MFMA backward of one conv layer (torch.autocast(bfloat16) arithmetic).  The input
-    gradient stages dz's BN+ReLU-backward frame and tees the bf16 dz it multiplied; the weight
-    gradient then multiplies that copy with the forward's operand copy (out.xt), so neither operand
-    is materialised by a separate pass (pmu_frame_to_bf16 only when a copy is missing)."""
+    """bf16-MFMA backward of one conv layer (torch.autocast(bfloat16) arithmetic).  dz after the
+    BN+ReLU backward is written once in bf16 (dzt); the input gradient streams it (or, for a concat
+    split that is not a multiple of 32, stages dz's frame in the fused kernel) and the weight
+    gradient multiplies it with the forward's bf16 operand (out.xt)."""
     s = L.stream()
     N, H, W, Cout = out.z.shape
     dev = out.z.device
     Cin = conv.in_channels
-    dzt = torch.empty(N, H, W, _pad8(Cout), dtype=torch.int16, device=dev)
+    dzt = frame_to_bf16([dz_src], N, H, W)
     res = None
     if need_dx:
-        wp = pack_weights_bf16(conv.weight, dgrad=True)
-        dzf = frame_of([dz_src], N, H, W)
         sp = Cin if split is None else split
         dx0 = _empty(N, H, W, sp, device=dev)
         dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin else None
-        L.call("pmu_conv3x3_dgrad_bf16", dzf, wp.data_ptr(), Cin, sp, dx0.data_ptr(), L.ptr(dx1), dzt.data_ptr(), s)
+        if raw_ok(N, H, W, dzt.shape[3]) and (sp == Cin or sp % 32 == 0):
+            wp = pack_weights_raw(conv.weight, dgrad=True)
+            L.call("pmu_conv3x3_dgrad_raw", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
+                   dx0.data_ptr(), L.ptr(dx1), s)
+        else:
+            wp = pack_weights_bf16(conv.weight, dgrad=True)
+            L.call("pmu_conv3x3_dgrad_bf16", frame_of([dz_src], N, H, W), wp.data_ptr(), Cin, sp, dx0.data_ptr(),
+                   L.ptr(dx1), None, s)
         res = dx0 if split is None else (dx0, dx1)
-    else:
-        dzt = frame_to_bf16([dz_src], N, H, W)
     xt = out.xt if out.xt is not None else frame_to_bf16(out.srcs, N, H, W)
     out.xt = None
     wsb = L.lib().pmu_conv3x3_wgrad_ws_bf16(N, H, W, Cin, Cout)
@@ -292,6 +310,15 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split):
     L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(), ws.data_ptr(),
            wsb, s)
     return res
+
+
+def pack_weights_raw(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """Weights rounded to bf16 in the materialised-operand conv's B tiles (pmu_conv3x3_pack_raw)."""
+    Cout, Cin = w.shape[0], w.shape[1]
+    n = L.lib().pmu_conv3x3_packed_size_raw(Cout, Cin, int(dgrad)) // 2
+    wp = torch.empty(n, dtype=torch.int16, device=w.device)
+    L.call("pmu_conv3x3_pack_raw", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
 
 
 def pack_weights_bf16(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
@@ -395,14 +422,13 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         c1w, b1, c2w, b2 = _dc_layers(dc)
         prev = st.enc[-1][1]
         h, w = h // 2, w // 2
-        if bf16:
-            # bf16 mode: the max-pooled activation is materialised once (1/4 of the producer's bytes) and
-            # every column block of the conv reads it raw instead of re-pooling
+        srcs = [prev.act(L.POOL_MAX2)]
+        if bf16 and not raw_ok(N, h, w, _pad8(prev.z.shape[3])):
+            # fused bf16 fallback: the max-pooled activation materialised once, read raw by every
+            # column block (the pipelined fused kernel has no pooled staging)
             pooled = _empty(N, h, w, prev.z.shape[3], device=dev)
-            L.call("pmu_frame_to_f32", frame_of([prev.act(L.POOL_MAX2)], N, h, w), pooled.data_ptr(), L.stream())
+            L.call("pmu_frame_to_f32", frame_of(srcs, N, h, w), pooled.data_ptr(), L.stream())
             srcs = [Src(pooled)]
-        else:
-            srcs = [prev.act(L.POOL_MAX2)]
         o1 = conv_bn_forward(srcs, c1w, b1, N, h, w, training, dev, bf16=bf16, keep=keep)
         o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev, bf16=bf16, keep=keep)
         st.enc.append((o1, o2))

@@ -290,3 +290,54 @@ def test_convT_dgrad_bf16(dev, N, H, W, Cin, Cout, oh, ow):
     dui = du[:, oh:oh + 2 * H, ow:ow + 2 * W]
     ref = TF.conv2d(_nchw(_rb(dui)).double().cpu(), _rb(w).double().cpu(), stride=2).permute(0, 2, 3, 1)
     assert _rel(dx, ref) <= TOL
+
+
+def _pack_raw(w, dgrad):
+    from pmu_hip import _lib as L
+    n = L.lib().pmu_conv3x3_packed_size_raw(w.shape[0], w.shape[1], int(dgrad)) // 2
+    wp = torch.empty(n, dtype=torch.int16, device=w.device)
+    L.call("pmu_conv3x3_pack_raw", w.data_ptr(), w.shape[0], w.shape[1], int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 40, 40, 64, 96), (1, 33, 17, 40, 64), (3, 12, 20, 128, 128),
+                                            (2, 9, 7, 8, 10)])
+def test_conv3x3_fwd_raw(dev, N, H, W, Cin, Cout):
+    """Conv of a materialised bf16 operand (BN+ReLU source) == conv of the rounded operand."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    g = torch.Generator().manual_seed(41 + H)
+    z0 = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    coef = torch.cat([torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.2]).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    xt = _to_bf16([Src(z0, L.SRC_BNRELU, coef)], N, H, W, Cin)
+    z = torch.empty(N, H, W, Cout, device=dev)
+    part = torch.empty(L.lib().pmu_conv3x3_tiles(N, H, W), 2 * Cout, device=dev)
+    L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), xt.shape[3], N, H, W, _pack_raw(w, False).data_ptr(), b.data_ptr(),
+           Cout, z.data_ptr(), part.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = _ref_conv(_bf16_values(xt, Cin), w, b)
+    assert _rel(z, ref) <= TOL
+    s = part.view(-1, 2, Cout).double().sum(0).cpu()
+    assert _rel(s[0], z.double().cpu().reshape(-1, Cout).sum(0)) <= 1e-4
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 40, 36, 64, 32, 64), (2, 17, 33, 128, 64, 64),
+                                                  (1, 8, 8, 96, 128, 32), (2, 20, 12, 64, 40, 64)])
+def test_conv3x3_dgrad_raw(dev, N, H, W, Cin, Cout, split):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    g = torch.Generator().manual_seed(51 + H)
+    dz = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    dzt = _to_bf16([Src(dz)], N, H, W, Cout)
+    dx0 = torch.empty(N, H, W, split, device=dev)
+    dx1 = torch.empty(N, H, W, Cin - split, device=dev) if split < Cin else None
+    L.call("pmu_conv3x3_dgrad_raw", dzt.data_ptr(), dzt.shape[3], N, H, W, _pack_raw(w, True).data_ptr(), Cin, split,
+           dx0.data_ptr(), L.ptr(dx1), L.stream())
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, W), _rb(w).double().cpu(), _nchw(_rb(dz)).double().cpu(),
+                                     padding=1).permute(0, 2, 3, 1)
+    got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
+    assert _rel(got, ref) <= TOL

@@ -86,7 +86,18 @@ def main():
         L.call("pmu_frame_to_bf16", fin, cpi, xt.data_ptr(), s)
         wsbb = L.lib().pmu_conv3x3_wgrad_ws_bf16(N, H, W, Cin, Cout)
         wsb16 = torch.empty(wsbb // 4 + 1, device=dev)
+        def packr(wt, dg):
+            n = L.lib().pmu_conv3x3_packed_size_raw(wt.shape[0], wt.shape[1], int(dg)) // 2
+            t = torch.empty(n, dtype=torch.int16, device=dev)
+            L.call("pmu_conv3x3_pack_raw", wt.data_ptr(), wt.shape[0], wt.shape[1], int(dg), t.data_ptr(), s)
+            return t
+        wrf = packr(w, False)
+        wrd = packr(w, True)
         ops = {
+            "fwd_raw": lambda: L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), cpi, N, H, W, wrf.data_ptr(), b.data_ptr(),
+                                      Cout, out.data_ptr(), part.data_ptr(), s),
+            "dgrad_raw": lambda: L.call("pmu_conv3x3_dgrad_raw", dzt.data_ptr(), cpo, N, H, W, wrd.data_ptr(), Cin, Cin,
+                                        dx.data_ptr(), None, s),
             "wgrad_bf16": lambda: L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin,
                                          dw.data_ptr(), wsb16.data_ptr(), wsbb, s),
             "mat_bf16": lambda: (L.call("pmu_frame_to_bf16", fdz, cpo, dzt.data_ptr(), s),
@@ -110,7 +121,7 @@ def main():
             tot.setdefault(op, [0.0, 0.0])
             tot[op][0] += ms
             tot[op][1] += flops
-            peak = 2516.0 if op.endswith("bf16") else 157.3
+            peak = 2516.0 if (op.endswith("bf16") or op.endswith("raw")) else 157.3
             print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / peak * 100:5.1f}%)",
                   flush=True)
     for op, (ms, fl) in tot.items():
