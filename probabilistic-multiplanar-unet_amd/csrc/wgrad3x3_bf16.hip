@@ -240,6 +240,30 @@ __global__ __launch_bounds__(256) void frame_to_bf16_kernel(DevFrame f, int Cpad
   }
 }
 
+// Fast path: one 16-B unit (8 channels) per thread, 32-bit pixel decode; every source's channel
+// count is a multiple of 8 (a unit never straddles the concat) and the output has < 2^31 units.
+__global__ __launch_bounds__(256) void frame_to_bf16_fast_kernel(DevFrame f, int Cpad, unsigned total,
+                                                                 unsigned short* __restrict__ out) {
+  const unsigned nu = (unsigned)Cpad / 8u, Wu = (unsigned)f.W, Hu = (unsigned)f.H;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const unsigned pix = e / nu, cu = e - pix * nu;
+    const unsigned t = pix / Wu, w = pix - t * Wu;
+    const unsigned n = t / Hu, h = t - n * Hu;
+    const int c = 8 * (int)cu;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (c < f.C) {
+      const bool second = f.nsrc > 1 && c >= f.C0;
+      const DevSrc& s = second ? f.s1 : f.s0;
+      const int cs = c - (second ? f.C0 : 0);
+      const int hs = (int)h - s.off_h, ws = (int)w - s.off_w;
+      a = src_value4(s, (int)n, hs, ws, cs);
+      b = src_value4(s, (int)n, hs, ws, cs + 4);
+    }
+    *reinterpret_cast<uint4*>(out + (size_t)pix * Cpad + c) =
+        make_uint4(pmu_pk_bf16(a.x, a.y), pmu_pk_bf16(a.z, a.w), pmu_pk_bf16(b.x, b.y), pmu_pk_bf16(b.z, b.w));
+  }
+}
+
 // operand materialisation in fp32: out[p][c] = frame value (e.g. a max-pooled BN+ReLU activation,
 // consumed as a RAW source so the conv kernels need no pooled staging variant)
 __global__ __launch_bounds__(256) void frame_to_f32_kernel(DevFrame f, float* __restrict__ out) {
@@ -286,6 +310,17 @@ extern "C" int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* o
   PMU_REQUIRE(valid_frame(f) && out && Cpad % 4 == 0);
   const int C = f->src[0].C + (f->nsrc > 1 ? f->src[1].C : 0);
   PMU_REQUIRE(Cpad >= C);
+  const long long units = (long long)f->N * f->H * f->W * (Cpad / 8);
+  bool fast = Cpad % 8 == 0 && units < (1LL << 31);
+  for (int i = 0; i < f->nsrc; ++i) fast = fast && f->src[i].C % 8 == 0;
+  if (fast) {
+    long long g = (units + 255) / 256;
+    if (g > 16384) g = 16384;
+    hipLaunchKernelGGL(frame_to_bf16_fast_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
+                       make_dev_frame(f), Cpad, (unsigned)units, out);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   const long long total = (long long)f->N * f->H * f->W * (Cpad / 4);
   long long g = (total + 255) / 256;
   if (g > 8192) g = 8192;
