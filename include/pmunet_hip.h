@@ -120,6 +120,8 @@ size_t pmu_conv3x3_packed_size_raw(int Cout, int Cin, int dgrad);
 int pmu_conv3x3_pack_raw(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream);
 int pmu_conv3x3_fwd_raw(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
                         const float* bias, int Cout, float* z, float* part, void* stream);
+/* rows of pmu_conv3x3_fwd_raw's part[tile][2][Cout] (its pixel tiles are 256 or 512 pixels) */
+int pmu_conv3x3_tiles_raw(int N, int H, int W, int Cout);
 int pmu_conv3x3_dgrad_raw(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                           int Cin, int Csplit, float* dx0, float* dx1, void* stream);
 /* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels

@@ -21,12 +21,21 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int BM = 256, BNT = 64, BK = 32;
+constexpr int BNT = 64, BK = 32;
 constexpr int LS = 40;       // LDS row stride (bf16): 64 B of data + 16 B pad, ds_read_b128 conflict-free
-constexpr int MAX_HP = 340;  // (8+2)*(32+2)
-constexpr int NA = 6;        // A units per thread: ceil(340 * 4 / 256)
-constexpr int NB = 9;        // B units per thread: 9 * 64 * 4 / 256
-constexpr int A_EL = MAX_HP * LS, B_EL = 9 * BNT * LS;
+constexpr int B_UNITS = 9 * BNT * BK / 8;  // 2304 16-B units of packed weights per chunk
+constexpr int B_EL = 9 * BNT * LS;
+
+// Tile of BMT pixels (= threads: one wave per 64 pixels).  BMT = 512 halves the weight bytes per
+// FLOP of BMT = 256: the per-CU vector-memory path (64 B/clk) bounds the 256-pixel tile at ~1/3 of
+// the MFMA rate (58 KB per chunk per block), the 512-pixel tile needs 16.5 B/clk at full rate.
+template <int BMT>
+struct RawGeo {
+  static constexpr int MAX_HP = BMT == 512 ? 660 : 340;  // (TH+2)*(TW+2) over TW in {8,16,32}
+  static constexpr int A_EL = MAX_HP * LS;
+  static constexpr int NA = (MAX_HP * 4 + BMT - 1) / BMT;  // A units per thread
+  static constexpr int NB = (B_UNITS + BMT - 1) / BMT;     // B units per thread
+};
 
 struct RawArgs {
   const unsigned short* x;   // operand [N][H][W][Cp] bf16
@@ -62,13 +71,15 @@ __global__ __launch_bounds__(256) void pack_raw_kernel(const float* __restrict__
   }
 }
 
-template <bool DGRAD, int TWL>
-__global__ __launch_bounds__(256, 2) void conv3x3_raw_kernel(RawArgs a) {
-  constexpr int FM = 2, FN = 2;
-  constexpr int TW = 1 << TWL, TH = BM >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
-  __shared__ __attribute__((aligned(16))) unsigned short smem[A_EL + B_EL];
+template <bool DGRAD, int TWL, int BMT>
+__global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
+  using G = RawGeo<BMT>;
+  constexpr int FM = 2, FN = 2, NA = G::NA, NB = G::NB, NWV = BMT / 64;
+  constexpr int TW = 1 << TWL, TH = BMT >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
+  static_assert(HP <= G::MAX_HP, "halo tile fits");
+  __shared__ __attribute__((aligned(16))) unsigned short smem[G::A_EL + B_EL];
   unsigned short* As = smem;
-  unsigned short* Bs = smem + A_EL;
+  unsigned short* Bs = smem + G::A_EL;
   const int tid = threadIdx.x, lane = tid & 63, wm = tid >> 6;
   int t = blockIdx.x;
   const int tw = t % a.tiles_w; t /= a.tiles_w;
@@ -82,11 +93,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_raw_kernel(RawArgs a) {
   unsigned okm = 0u, vm = 0u;
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int it = tid + 256 * i;
-    const int hp = it >> 2, q = it & 3;
+    // unit -> (halo pixel, 8-channel unit) so that each 8-lane ds_write_b128 group covers 8 rows of
+    // one unit column: conflict-free on the 80-B rows (row-major pairs of rows would be 2-way)
+    const int it = tid + BMT * i;
+    const int hp = (it >> 5) * 8 + (it & 7), q = (it >> 3) & 3;
     const int hr = hp / HW2, hc = hp - hr * HW2;
     const int h = h0 - 1 + hr, w = w0 - 1 + hc;
-    const bool v = it < HP * 4;
+    const bool v = hp < HP;
     const bool ok = v && h >= 0 && w >= 0 && h < a.H && w < a.W;
     vm |= v ? (1u << i) : 0u;
     okm |= ok ? (1u << i) : 0u;
@@ -111,28 +124,35 @@ __global__ __launch_bounds__(256, 2) void conv3x3_raw_kernel(RawArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const uint4* wt = reinterpret_cast<const uint4*>(a.wp) + (long long)(j0 / BNT) * a.nch * (9 * BNT * BK / 8) + tid;
+  const int bq = (tid >> 3) & 3;  // B unit of this thread within its row (BMT is a multiple of 32)
+  const uint4* wt = reinterpret_cast<const uint4*>(a.wp) + (long long)(j0 / BNT) * a.nch * B_UNITS +
+                    ((tid >> 5) * 8 + (tid & 7)) * 4 + bq;
   uint4 ra0, ra1, ra2, ra3, ra4, ra5;                     // plain locals (no scratch)
   uint4 rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7, rb8;
-  static_assert(NA == 6 && NB == 9, "staging register layout");
+  static_assert(NA <= 6 && NB <= 9, "staging register layout");
   // channel units past Cp (a partial last chunk) read as zero
 #define PMU_RA(I, R)                                                                               \
-  {                                                                                               \
-    const bool k_ = ((okm >> (I)) & 1u) && k0_ + 8 * ((tid + 256 * (I)) & 3) < a.Cp;              \
+  if ((I) < NA) {                                                                                 \
+    const bool k_ = ((okm >> (I)) & 1u) && k0_ + 8 * ((tid >> 3) & 3) < a.Cp;              \
     const uint4 v_ = *reinterpret_cast<const uint4*>(a.x + (k_ ? (unsigned)(eo[I] + k0_) : 0u));  \
     R = make_uint4(k_ ? v_.x : 0u, k_ ? v_.y : 0u, k_ ? v_.z : 0u, k_ ? v_.w : 0u);               \
   }
+#define PMU_RB(I, R) \
+  if ((I) < NB) R = s_[(B_UNITS % BMT == 0 || (I) + 1 < NB || tid + BMT * (I) < B_UNITS) ? BMT * (I) : 0];
+  // (B units use the same row-interleaved order as A: see wt and PMU_WB)
 #define PMU_PREFETCH(CH)                                                                           \
   {                                                                                               \
     const int k0_ = (CH) * BK;                                                                    \
     PMU_RA(0, ra0) PMU_RA(1, ra1) PMU_RA(2, ra2) PMU_RA(3, ra3) PMU_RA(4, ra4) PMU_RA(5, ra5)    \
-    const uint4* s_ = wt + (long long)(CH) * (9 * BNT * BK / 8);                                  \
-    rb0 = s_[0]; rb1 = s_[256]; rb2 = s_[512]; rb3 = s_[768]; rb4 = s_[1024];                    \
-    rb5 = s_[1280]; rb6 = s_[1536]; rb7 = s_[1792]; rb8 = s_[2048];                              \
+    const uint4* s_ = wt + (long long)(CH) * B_UNITS;                                             \
+    PMU_RB(0, rb0) PMU_RB(1, rb1) PMU_RB(2, rb2) PMU_RB(3, rb3) PMU_RB(4, rb4)                    \
+    PMU_RB(5, rb5) PMU_RB(6, rb6) PMU_RB(7, rb7) PMU_RB(8, rb8)                                   \
   }
 #define PMU_WA(I, R) \
-  if ((vm >> (I)) & 1u) *reinterpret_cast<uint4*>(As + dsta[I]) = R;
-#define PMU_WB(I, R) *reinterpret_cast<uint4*>(Bs + ((tid + 256 * (I)) >> 2) * LS + 8 * (tid & 3)) = R;
+  if ((I) < NA && ((vm >> (I)) & 1u)) *reinterpret_cast<uint4*>(As + dsta[I]) = R;
+#define PMU_WB(I, R)                                                                               \
+  if ((I) < NB && (B_UNITS % BMT == 0 || (I) + 1 < NB || tid + BMT * (I) < B_UNITS))               \
+    *reinterpret_cast<uint4*>(Bs + (((tid + BMT * (I)) >> 5) * 8 + (tid & 7)) * LS + 8 * bq) = R;
 #define PMU_COMMIT()                                                                               \
   {                                                                                               \
     PMU_WA(0, ra0) PMU_WA(1, ra1) PMU_WA(2, ra2) PMU_WA(3, ra3) PMU_WA(4, ra4) PMU_WA(5, ra5)    \
@@ -172,6 +192,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_raw_kernel(RawArgs a) {
     }
   }
 #undef PMU_RA
+#undef PMU_RB
 #undef PMU_PREFETCH
 #undef PMU_WA
 #undef PMU_WB
@@ -179,7 +200,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_raw_kernel(RawArgs a) {
 
   // epilogue: per 32-channel block the destination is uniform (split % 32 == 0, host-checked);
   // full tiles store without bounds tests
-  float* red = reinterpret_cast<float*>(smem);
+  float* red = reinterpret_cast<float*>(smem);  // [NWV][64][2]
   float s1[FN], s2[FN];
   const bool full = h0 + TH <= a.H && w0 + TW <= a.W && j0 + BNT <= a.NOUT;
 #pragma unroll
@@ -227,7 +248,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_raw_kernel(RawArgs a) {
       if (j < a.NOUT) {
         float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < NWV; ++v) {
           t1 += red[(v * BNT + tid) * 2 + 0];
           t2 += red[(v * BNT + tid) * 2 + 1];
         }
@@ -244,6 +265,17 @@ static int pick_twl(int W) {
   return 3;
 }
 
+// pixels per tile: PMU_RAW_BMT=256|512 forces one (A/B measurements); default 256
+static int raw_bmt(int N, int H, int W, int TW, int ncb) {
+  static const int forced = [] {
+    const char* e = getenv("PMU_RAW_BMT");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 256 || forced == 512) return forced;
+  (void)N; (void)H; (void)W; (void)TW; (void)ncb;
+  return 256;
+}
+
 static int launch_raw(const unsigned short* x, int Cp, int N, int H, int W, const unsigned short* wp,
                       const float* bias, int NOUT, float* out0, float* out1, int split, float* part, bool dgrad,
                       void* stream) {
@@ -253,25 +285,42 @@ static int launch_raw(const unsigned short* x, int Cp, int N, int H, int W, cons
   RawArgs a;
   a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
   a.N = N; a.H = H; a.W = W; a.Cp = Cp; a.NOUT = NOUT; a.split = dgrad ? split : NOUT;
+  a.nch = pmu_cdiv(Cp, BK);
   const int twl = pick_twl(W);
-  const int TW = 1 << twl, TH = BM / TW;
+  const int TW = 1 << twl;
+  const int ncb = pmu_cdiv(NOUT, BNT);
+  // 512-pixel tiles when they still give the chip >= 2 blocks per CU; part (BN partials) is then
+  // indexed by the 512-pixel tile (pmu_conv3x3_tiles_raw)
+  const int bmt = raw_bmt(N, H, W, TW, ncb);
+  const int TH = bmt / TW;
   a.tiles_w = pmu_cdiv(W, TW);
   a.tiles_h = pmu_cdiv(H, TH);
-  a.nch = pmu_cdiv(Cp, BK);
-  dim3 grid((unsigned)(a.tiles_w * a.tiles_h * N), (unsigned)pmu_cdiv(NOUT, BNT));
+  dim3 grid((unsigned)(a.tiles_w * a.tiles_h * N), (unsigned)ncb);
   hipStream_t st = (hipStream_t)stream;
-#define PMU_RK(D, T)                                                                  \
-  if (dgrad == D && twl == T) {                                                       \
-    hipLaunchKernelGGL((conv3x3_raw_kernel<D, T>), grid, dim3(256), 0, st, a);        \
-    PMU_CHECK_LAUNCH();                                                               \
-    return PMU_OK;                                                                    \
+#define PMU_RK(D, T, B)                                                                 \
+  if (dgrad == D && twl == T && bmt == B) {                                             \
+    hipLaunchKernelGGL((conv3x3_raw_kernel<D, T, B>), grid, dim3(B), 0, st, a);         \
+    PMU_CHECK_LAUNCH();                                                                 \
+    return PMU_OK;                                                                      \
   }
-  PMU_RK(false, 3) PMU_RK(false, 4) PMU_RK(false, 5) PMU_RK(true, 3) PMU_RK(true, 4) PMU_RK(true, 5)
+  PMU_RK(false, 3, 256) PMU_RK(false, 4, 256) PMU_RK(false, 5, 256)
+  PMU_RK(true, 3, 256) PMU_RK(true, 4, 256) PMU_RK(true, 5, 256)
+  PMU_RK(false, 3, 512) PMU_RK(false, 4, 512) PMU_RK(false, 5, 512)
+  PMU_RK(true, 3, 512) PMU_RK(true, 4, 512) PMU_RK(true, 5, 512)
 #undef PMU_RK
   return PMU_ERR_ARG;
 }
 
+static int raw_tiles(int N, int H, int W, int NOUT) {
+  const int TW = 1 << pick_twl(W);
+  const int ncb = pmu_cdiv(NOUT, BNT);
+  const int bmt = raw_bmt(N, H, W, TW, ncb);
+  return N * pmu_cdiv(H, bmt / TW) * pmu_cdiv(W, TW);
+}
+
 }  // namespace
+
+extern "C" int pmu_conv3x3_tiles_raw(int N, int H, int W, int Cout) { return raw_tiles(N, H, W, Cout); }
 
 extern "C" size_t pmu_conv3x3_packed_size_raw(int Cout, int Cin, int dgrad) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;

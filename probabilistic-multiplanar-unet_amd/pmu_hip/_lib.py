@@ -51,6 +51,7 @@ SIGNATURES = {
     "pmu_conv3x3_fwd_bf16": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_bf16": (c_int, [_FP, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_packed_size_raw": (c_size_t, [c_int, c_int, c_int]),
+    "pmu_conv3x3_tiles_raw": (c_int, [c_int, c_int, c_int, c_int]),
     "pmu_conv3x3_pack_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_fwd_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p]),

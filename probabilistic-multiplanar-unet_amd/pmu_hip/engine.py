@@ -191,10 +191,11 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         L.call("pmu_conv_first_fwd", arr, len(planes), N, H, W, conv.weight.data_ptr(), L.ptr(conv.bias), Cout,
                z.data_ptr(), L.ptr(part), s)
     elif bf16:
-        R = lb.pmu_conv3x3_tiles(N, H, W)
-        part = _empty(R, 2 * Cout, device=dev) if need_stats else None
         Cp = _pad8(sum(sr.C for sr in srcs))
-        if raw_ok(N, H, W, Cp):
+        use_raw = raw_ok(N, H, W, Cp)
+        R = lb.pmu_conv3x3_tiles_raw(N, H, W, Cout) if use_raw else lb.pmu_conv3x3_tiles(N, H, W)
+        part = _empty(R, 2 * Cout, device=dev) if need_stats else None
+        if use_raw:
             # the operand (BN+ReLU / max-pool / F.pad+cat applied) written once in bf16; the GEMM
             # streams it, and the weight gradient reuses it
             xt = frame_to_bf16(srcs, N, H, W)

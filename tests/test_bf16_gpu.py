@@ -301,7 +301,7 @@ def _pack_raw(w, dgrad):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 40, 40, 64, 96), (1, 33, 17, 40, 64), (3, 12, 20, 128, 128),
-                                            (2, 9, 7, 8, 10)])
+                                            (2, 9, 7, 8, 10), (8, 96, 80, 64, 64), (16, 32, 40, 32, 128)])
 def test_conv3x3_fwd_raw(dev, N, H, W, Cin, Cout):
     """Conv of a materialised bf16 operand (BN+ReLU source) == conv of the rounded operand."""
     from pmu_hip import _lib as L
@@ -313,7 +313,7 @@ def test_conv3x3_fwd_raw(dev, N, H, W, Cin, Cout):
     b = torch.randn(Cout, generator=g).to(dev)
     xt = _to_bf16([Src(z0, L.SRC_BNRELU, coef)], N, H, W, Cin)
     z = torch.empty(N, H, W, Cout, device=dev)
-    part = torch.empty(L.lib().pmu_conv3x3_tiles(N, H, W), 2 * Cout, device=dev)
+    part = torch.full((L.lib().pmu_conv3x3_tiles_raw(N, H, W, Cout), 2 * Cout), float("nan"), device=dev)
     L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), xt.shape[3], N, H, W, _pack_raw(w, False).data_ptr(), b.data_ptr(),
            Cout, z.data_ptr(), part.data_ptr(), L.stream())
     torch.cuda.synchronize()
@@ -324,7 +324,8 @@ def test_conv3x3_fwd_raw(dev, N, H, W, Cin, Cout):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 40, 36, 64, 32, 64), (2, 17, 33, 128, 64, 64),
-                                                  (1, 8, 8, 96, 128, 32), (2, 20, 12, 64, 40, 64)])
+                                                  (1, 8, 8, 96, 128, 32), (2, 20, 12, 64, 40, 64),
+                                                  (8, 64, 72, 128, 64, 64)])
 def test_conv3x3_dgrad_raw(dev, N, H, W, Cin, Cout, split):
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src

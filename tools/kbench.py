@@ -92,10 +92,11 @@ def main():
             L.call("pmu_conv3x3_pack_raw", wt.data_ptr(), wt.shape[0], wt.shape[1], int(dg), t.data_ptr(), s)
             return t
         wrf = packr(w, False)
+        partr = torch.empty(L.lib().pmu_conv3x3_tiles_raw(N, H, W, Cout), 2 * Cout, device=dev)
         wrd = packr(w, True)
         ops = {
             "fwd_raw": lambda: L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), cpi, N, H, W, wrf.data_ptr(), b.data_ptr(),
-                                      Cout, out.data_ptr(), part.data_ptr(), s),
+                                      Cout, out.data_ptr(), partr.data_ptr(), s),
             "dgrad_raw": lambda: L.call("pmu_conv3x3_dgrad_raw", dzt.data_ptr(), cpo, N, H, W, wrd.data_ptr(), Cin, Cin,
                                         dx.data_ptr(), None, s),
             "wgrad_bf16": lambda: L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin,
