@@ -185,6 +185,37 @@ __device__ __forceinline__ float4 frame_value4(const DevFrame& f, int n, int h, 
                      frame_value(f, n, h, w, c + 2), frame_value(f, n, h, w, c + 3));
 }
 
+// Split-K slab reduction shared by the weight-gradient kernels: dw[cc*9 + tap] = sum over sp of
+// ws[sp][tap][cc] (E = 9*CC elements per slab).  A 256-thread block owns 64 consecutive elements;
+// its 4 waves each sum the splits sp = g, g+4, ... (4 independent accumulators, combined in a fixed
+// order) and wave 0 adds the 4 partials in order: deterministic, 4x the loads in flight of one
+// thread per element walking all splits.
+static __global__ __launch_bounds__(256) void pmu_splitk_reduce9_kernel(const float* __restrict__ ws, int nsplit,
+                                                                       long long CC, float* __restrict__ dw) {
+  __shared__ float red[4][64];
+  const long long E = 9 * CC;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (e < E) {
+    int sp = g;
+    for (; sp + 12 < nsplit; sp += 16) {
+      s0 += ws[(long long)sp * E + e];
+      s1 += ws[(long long)(sp + 4) * E + e];
+      s2 += ws[(long long)(sp + 8) * E + e];
+      s3 += ws[(long long)(sp + 12) * E + e];
+    }
+    for (; sp < nsplit; sp += 4) s0 += ws[(long long)sp * E + e];
+  }
+  red[g][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && e < E) {
+    const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    const int tap = (int)(e / CC);
+    dw[(e - tap * CC) * 9 + tap] = t;
+  }
+}
+
 // wave-level sum over 64 lanes
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

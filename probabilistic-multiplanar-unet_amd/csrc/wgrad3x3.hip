@@ -266,19 +266,6 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
   }
 }
 
-// dw[co][ci][tap] = sum_s ws[s][tap][co][ci]  (one thread per slab element, fixed split order)
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, int Cout, int Cin,
-                                    float* __restrict__ dw) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (tap*Cout + co)*Cin + ci
-  const long long CC = (long long)Cout * Cin;
-  const long long E = 9 * CC;
-  if (e >= E) return;
-  float s = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) s += ws[(long long)sp * E + e];
-  const int tap = (int)(e / CC);
-  const long long cc = e - tap * CC;  // co*Cin + ci
-  dw[cc * 9 + tap] = s;
-}
 
 static void wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* twl, int* tiles_w, int* tiles_h,
                            int* ntiles, int* nsplit) {
@@ -333,8 +320,8 @@ extern "C" int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int 
   }
   PMU_CHECK_LAUNCH();
   const long long E = 9LL * Cout * Cin;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const float*)ws, a.nsplit, Cout, Cin, dw);
+  hipLaunchKernelGGL(pmu_splitk_reduce9_kernel, dim3((unsigned)pmu_cdiv(E, 64)), dim3(256), 0, st, (const float*)ws,
+                     a.nsplit, (long long)Cout * Cin, dw);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -210,19 +210,6 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_bf16_kernel(WgbArgs a) {
   }
 }
 
-// dw[co][ci][tap] = sum_s ws[s][tap][co][ci]  (fixed split order)
-__global__ void wgrad_bf16_reduce_kernel(const float* __restrict__ ws, int nsplit, int Cout, int Cin,
-                                         float* __restrict__ dw) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long CC = (long long)Cout * Cin;
-  const long long E = 9 * CC;
-  if (e >= E) return;
-  float s = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) s += ws[(long long)sp * E + e];
-  const int tap = (int)(e / CC);
-  const long long cc = e - tap * CC;
-  dw[cc * 9 + tap] = s;
-}
 
 // operand materialisation: out[p][c] = bf16(frame value), channels [C, Cpad) zero
 __global__ __launch_bounds__(256) void frame_to_bf16_kernel(DevFrame f, int Cpad, unsigned short* __restrict__ out) {
@@ -298,7 +285,7 @@ static void geometry(int N, int H, int W, int Cin, int Cout, int* wco, int* twl,
   *tiles_h = pmu_cdiv(H, TH);
   *ntiles = N * *tiles_w * *tiles_h;
   const int blocks_mn = pmu_cdiv(Cout, *wco) * pmu_cdiv(Cin, WCI);
-  int s = 768 / blocks_mn;  // ~3 waves of one block per CU over the launch
+  int s = 512 / blocks_mn;  // ~2 rounds of one block per CU (fewer splits: smaller slabs to reduce)
   if (s < 1) s = 1;
   if (s > *ntiles) s = *ntiles;
   *nsplit = s;
@@ -367,8 +354,8 @@ extern "C" int pmu_conv3x3_wgrad_bf16(const unsigned short* dzt, const unsigned 
   }
   PMU_CHECK_LAUNCH();
   const long long E = 9LL * Cout * Cin;
-  hipLaunchKernelGGL(wgrad_bf16_reduce_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0, st, (const float*)ws,
-                     a.nsplit, Cout, Cin, dw);
+  hipLaunchKernelGGL(pmu_splitk_reduce9_kernel, dim3((unsigned)pmu_cdiv(E, 64)), dim3(256), 0, st, (const float*)ws,
+                     a.nsplit, (long long)Cout * Cin, dw);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
