@@ -277,6 +277,7 @@ def build_unet(args, dev, world, rank):
         opt.step(grad_scale=1.0 / world)
         return loss
 
+    step.net = net
     flops = conv_flops_per_slice(S, S, FILTERS, args.channels, args.classes) * B
     lossn = "BCE" if args.classes == 1 else "CE"
     tag = "c5" if args.workload == "c5" else "c2"
@@ -319,6 +320,53 @@ def phantom_batches(S, B, rank, world, dev):
             yield ds.get_batch(order[i:i + B])
             i += B
     return gen()
+
+
+@torch.no_grad()
+def c5_eval(net, dev, D, batch, precision):
+    """Config c5's evaluation (PMU/eval.py:131-203 via predict.predict_volume's batching): predict all
+    3 x D slices (D x D x 3 channels) of a seeded D^3 phantom along the axial/coronal/sagittal views
+    with the network in eval mode, then fuse the three views with pmu_fuse3view (softmax, average,
+    argmax label map, per-class Dice of every volume).  Returns timings and the fused Dice."""
+    from pmu_hip.fusion import fuse_views
+    C = net.n_classes
+    g = torch.Generator(device=dev).manual_seed(5)
+    ax = torch.arange(D, dtype=torch.float32, device=dev) - D / 2
+    r2 = ((ax[:, None, None] / (0.40 * D)) ** 2 + (ax[None, :, None] / (0.35 * D)) ** 2 +
+          (ax[None, None, :] / (0.30 * D)) ** 2)
+    lab = (r2 < 1.0).float() + (r2 < 0.35).float()
+    del r2
+    vol = torch.empty(3, D, D, D, device=dev)
+    for c in range(3):  # three "modalities": the label-driven contrast under different seeded noise
+        vol[c] = 0.6 * torch.rand(D, D, D, generator=g, device=dev) + 0.2 * (c + 1) * lab
+    net.eval()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stacks = []
+    for v in range(3):
+        out = torch.empty(D, C, D, D, device=dev)
+        for s0 in range(0, D, batch):
+            s1 = min(D, s0 + batch)
+            if v == 0:
+                xb = vol[:, s0:s1].permute(1, 0, 2, 3)
+            elif v == 1:
+                xb = vol[:, :, s0:s1].permute(2, 0, 1, 3)
+            else:
+                xb = vol[:, :, :, s0:s1].permute(3, 0, 1, 2)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=precision == "bf16"):
+                out[s0:s1] = net(xb.contiguous())
+        stacks.append(out)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    res = fuse_views(stacks[0], stacks[1], stacks[2], lab, logits=True)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    net.train()
+    dice = res["dice"].tolist()
+    return {"volume": [D, D, D], "channels": 3, "slices": 3 * D, "batch": batch, "predict_s": round(t1 - t0, 4),
+            "predict_slices_per_s": round(3 * D / (t1 - t0), 2), "fuse_ms": round((t2 - t1) * 1e3, 3),
+            "dice_average_volume": [round(x, 4) for x in dice[3]],
+            "note": "random-init weights: the Dice values only show the pipeline runs end to end"}
 
 
 def build_probunet(args, dev, world, rank):
@@ -387,6 +435,8 @@ def main():
                     help="phantom: multi-planar slices gathered on the GPU from a resident phantom (c3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-eval", action="store_true", help="c5: skip the 3-view volume-fusion evaluation")
+    ap.add_argument("--eval-size", type=int, default=512, help="c5 evaluation volume edge (D^3 voxels)")
     args = ap.parse_args()
     c5 = args.workload == "c5"
     if args.channels is None:
@@ -467,6 +517,9 @@ def main():
                        "tflops": (round(v[1] / v[2] / 1e12, 2) if v[1] else None)} for k, v in sorted(per.items())}
         if flops_step is None:   # algorithmic FLOPs of the step = those of the MFMA kernels it launches
             flops_step = sum(v[1] for v in per.values())
+    evalres = None
+    if args.workload == "c5" and not args.no_eval and rank == 0:
+        evalres = c5_eval(step.net, dev, args.eval_size, B, args.precision)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(workload="probunet" if args.workload == "probunet" else "unet", size=args.size,
@@ -483,6 +536,8 @@ def main():
             if flops_step else None,
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "loss": float(loss.detach()),
         }
+        if evalres is not None:
+            res["c5_volume_fusion_eval"] = evalres
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
