@@ -146,20 +146,16 @@ __device__ __forceinline__ void softmax_inplace(float (&p)[FUSE_CMAX], int C) {
 }
 
 __global__ __launch_bounds__(256) void fuse3view_kernel(FuseArgs a) {
-  // block: plane i, tile of 32 (j) x 32 (k); v2 is read [k][j] coalesced in j and transposed in LDS
+  // block: plane i, row of 32 j, walking every 32-wide k tile; v2 is read [k][j] coalesced in j and
+  // transposed in LDS.  The integer counts accumulate in registers over the whole row, are summed
+  // over the block in LDS and leave as one exact fp64 atomic per counter per block (per-wave
+  // atomics on the same 4*C*3 addresses serialised the kernel).
   __shared__ float t2[FUSE_CMAX][TT][TT + 1];
-  const int i = blockIdx.z, j0 = blockIdx.y * TT, k0 = blockIdx.x * TT;
+  __shared__ int red[4][4 * FUSE_CMAX * 2 + FUSE_CMAX];
+  const int i = blockIdx.z, j0 = blockIdx.y * TT;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int C = a.C;
   const long long P01 = (long long)a.D0 * a.D1, P02 = (long long)a.D0 * a.D2, P12 = (long long)a.D1 * a.D2;
-  for (int r = ty; r < TT; r += 8) {
-    const int k = k0 + r, j = j0 + tx;
-#pragma unroll
-    for (int c = 0; c < FUSE_CMAX; ++c)
-      if (c < C)
-        t2[c][r][tx] = (k < a.D2 && j < a.D1) ? a.v2[((long long)k * C + c) * P01 + (long long)i * a.D1 + j] : 0.f;
-  }
-  __syncthreads();
   int cI[4][FUSE_CMAX], cP[4][FUSE_CMAX], cT[FUSE_CMAX];
 #pragma unroll
   for (int c = 0; c < FUSE_CMAX; ++c) {
@@ -167,65 +163,84 @@ __global__ __launch_bounds__(256) void fuse3view_kernel(FuseArgs a) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) { cI[v][c] = 0; cP[v][c] = 0; }
   }
-  for (int r = ty; r < TT; r += 8) {
-    const int j = j0 + r, k = k0 + tx;
-    if (j >= a.D1 || k >= a.D2) continue;
-    float p0[FUSE_CMAX], p1[FUSE_CMAX], p2[FUSE_CMAX], pa[FUSE_CMAX];
-#pragma unroll
-    for (int c = 0; c < FUSE_CMAX; ++c) {
-      p0[c] = p1[c] = p2[c] = 0.f;
-      if (c < C) {
-        p0[c] = a.v0[((long long)i * C + c) * P12 + (long long)j * a.D2 + k];
-        p1[c] = a.v1[((long long)j * C + c) * P02 + (long long)i * a.D2 + k];
-        p2[c] = t2[c][tx][r];
-      }
-    }
-    if (a.logits) {
-      softmax_inplace(p0, C);
-      softmax_inplace(p1, C);
-      softmax_inplace(p2, C);
-    }
-#pragma unroll
-    for (int c = 0; c < FUSE_CMAX; ++c) pa[c] = (p0[c] + p1[c] + p2[c]) / 3.0f;
-    const long long vox = ((long long)i * a.D1 + j) * a.D2 + k;
-    const int t = (int)a.truth[vox];
-    const int m0 = argmax_first(p0, C), m1 = argmax_first(p1, C), m2 = argmax_first(p2, C), ma = argmax_first(pa, C);
-#pragma unroll
-    for (int c = 0; c < FUSE_CMAX; ++c) {
-      if (c >= C) break;
-      const int tc = (t == c);
-      cT[c] += tc;
-      cP[0][c] += (m0 == c); cI[0][c] += (m0 == c) & tc;
-      cP[1][c] += (m1 == c); cI[1][c] += (m1 == c) & tc;
-      cP[2][c] += (m2 == c); cI[2][c] += (m2 == c) & tc;
-      cP[3][c] += (ma == c); cI[3][c] += (ma == c) & tc;
-    }
-    if (a.avg) {
+  for (int k0 = 0; k0 < a.D2; k0 += TT) {
+    __syncthreads();  // previous tile's t2 reads done
+    for (int r = ty; r < TT; r += 8) {
+      const int k = k0 + r, j = j0 + tx;
 #pragma unroll
       for (int c = 0; c < FUSE_CMAX; ++c)
-        if (c < C) a.avg[((long long)i * C + c) * P12 + (long long)j * a.D2 + k] = pa[c];
+        if (c < C)
+          t2[c][r][tx] = (k < a.D2 && j < a.D1) ? a.v2[((long long)k * C + c) * P01 + (long long)i * a.D1 + j] : 0.f;
     }
-    if (a.label) a.label[vox] = ma;
+    __syncthreads();
+    for (int r = ty; r < TT; r += 8) {
+      const int j = j0 + r, k = k0 + tx;
+      if (j >= a.D1 || k >= a.D2) continue;
+      float p0[FUSE_CMAX], p1[FUSE_CMAX], p2[FUSE_CMAX], pa[FUSE_CMAX];
+#pragma unroll
+      for (int c = 0; c < FUSE_CMAX; ++c) {
+        p0[c] = p1[c] = p2[c] = 0.f;
+        if (c < C) {
+          p0[c] = a.v0[((long long)i * C + c) * P12 + (long long)j * a.D2 + k];
+          p1[c] = a.v1[((long long)j * C + c) * P02 + (long long)i * a.D2 + k];
+          p2[c] = t2[c][tx][r];
+        }
+      }
+      if (a.logits) {
+        softmax_inplace(p0, C);
+        softmax_inplace(p1, C);
+        softmax_inplace(p2, C);
+      }
+#pragma unroll
+      for (int c = 0; c < FUSE_CMAX; ++c) pa[c] = (p0[c] + p1[c] + p2[c]) / 3.0f;
+      const long long vox = ((long long)i * a.D1 + j) * a.D2 + k;
+      const int t = (int)a.truth[vox];
+      const int m0 = argmax_first(p0, C), m1 = argmax_first(p1, C), m2 = argmax_first(p2, C), ma = argmax_first(pa, C);
+#pragma unroll
+      for (int c = 0; c < FUSE_CMAX; ++c) {
+        if (c >= C) break;
+        const int tc = (t == c);
+        cT[c] += tc;
+        cP[0][c] += (m0 == c); cI[0][c] += (m0 == c) & tc;
+        cP[1][c] += (m1 == c); cI[1][c] += (m1 == c) & tc;
+        cP[2][c] += (m2 == c); cI[2][c] += (m2 == c) & tc;
+        cP[3][c] += (ma == c); cI[3][c] += (ma == c) & tc;
+      }
+      if (a.avg) {
+#pragma unroll
+        for (int c = 0; c < FUSE_CMAX; ++c)
+          if (c < C) a.avg[((long long)i * C + c) * P12 + (long long)j * a.D2 + k] = pa[c];
+      }
+      if (a.label) a.label[vox] = ma;
+    }
   }
-  // wave-reduce the integer counts, one fp64 atomic (exact) per wave and counter
-  const bool lead = (threadIdx.x & 63) == 0;
+  // wave sums -> LDS -> block sums -> one atomic per counter (exact: integer values in fp64)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < FUSE_CMAX; ++c) {
     if (c >= C) break;
     int v = cT[c];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lead && v) for (int w = 0; w < 4; ++w) atomicAdd(a.counts + (w * C + c) * 3 + 2, (double)v);
+    if (lane == 0) red[wv][8 * FUSE_CMAX + c] = v;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       int x = cI[w][c], y = cP[w][c];
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) { x += __shfl_xor(x, o, 64); y += __shfl_xor(y, o, 64); }
-      if (lead) {
-        if (x) atomicAdd(a.counts + (w * C + c) * 3 + 0, (double)x);
-        if (y) atomicAdd(a.counts + (w * C + c) * 3 + 1, (double)y);
+      if (lane == 0) {
+        red[wv][(w * FUSE_CMAX + c) * 2 + 0] = x;
+        red[wv][(w * FUSE_CMAX + c) * 2 + 1] = y;
       }
     }
+  }
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid < 4 * C * 3) {
+    const int w = tid / (3 * C), rem = tid - w * 3 * C, c = rem / 3, k = rem - c * 3;
+    const int slot = (k == 2) ? 8 * FUSE_CMAX + c : (w * FUSE_CMAX + c) * 2 + k;
+    const int v = red[0][slot] + red[1][slot] + red[2][slot] + red[3][slot];
+    if (v) atomicAdd(a.counts + (w * C + c) * 3 + k, (double)v);
   }
 }
 
@@ -284,8 +299,7 @@ extern "C" int pmu_fuse3view(const float* v0, const float* v1, const float* v2, 
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(counts, 0, sizeof(double) * 4 * C * 3, st) != hipSuccess) return PMU_ERR_ARG;
   FuseArgs a{v0, v1, v2, truth, D0, D1, D2, C, logits, avg, label, counts};
-  hipLaunchKernelGGL(fuse3view_kernel, dim3((unsigned)pmu_cdiv(D2, TT), (unsigned)pmu_cdiv(D1, TT), (unsigned)D0),
-                     dim3(256), 0, st, a);
+  hipLaunchKernelGGL(fuse3view_kernel, dim3(1u, (unsigned)pmu_cdiv(D1, TT), (unsigned)D0), dim3(256), 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
