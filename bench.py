@@ -67,7 +67,7 @@ class KernelTimer:
     MFMA = ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad", "pmu_convT2x2_fwd",
             "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd",
             "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16", "pmu_convT2x2_fwd_bf16",
-            "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw")
+            "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16")
 
     def __init__(self):
         self.rec = []
@@ -86,6 +86,9 @@ class KernelTimer:
         if name in ("pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw"):
             cp, N, H, W, nout = args[1], args[2], args[3], args[4], args[7] if name.endswith("fwd_raw") else args[6]
             return 2.0 * N * H * W * cp * nout * 9
+        if name == "pmu_convT2x2_wgrad_bf16":
+            N, H, W, cin, cout = args[3], args[4], args[5], args[10], args[11]
+            return 2.0 * N * H * W * cin * cout * 4
         if name == "pmu_convT2x2_fwd_bf16":
             f = args[0]._obj
             return 2.0 * f.N * f.H * f.W * f.src[0].C * args[3] * 4
@@ -195,7 +198,7 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_dgrad_bf16": r"conv3x3_bf16_pipe_kernel<true|conv3x3_bf16_kernel<\d, \d+, true>",
     "pmu_conv3x3_wgrad_bf16": r"wgrad3x3_bf16_kernel<", "pmu_conv3x3_fwd_raw": r"conv3x3_raw_kernel<false",
     "pmu_conv3x3_dgrad_raw": r"conv3x3_raw_kernel<true", "pmu_convT2x2_fwd_bf16": r"convT_bf16_kernel<false>",
-    "pmu_convT2x2_dgrad_bf16": r"convT_bf16_kernel<true>",
+    "pmu_convT2x2_dgrad_bf16": r"convT_bf16_kernel<true>", "pmu_convT2x2_wgrad_bf16": r"convT_wgrad_bf16_kernel",
 }
 
 

@@ -146,6 +146,12 @@ int pmu_convT2x2_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const f
                           float* u, void* stream);
 int pmu_convT2x2_dgrad_bf16(const float* du, int Hd, int Wd, int off_h, int off_w, const unsigned short* wp,
                             int N, int H, int W, int Cin, int Cout, float* dx, void* stream);
+/* Weight gradient from materialised bf16 operands: xt [N][H][W][pad8(Cin)] (the convT input after BN+ReLU)
+ * and dut [N][Hd][Wd][pad8(Cout)] (du); dbias (nullable) sums the fp32 du over the output region. */
+size_t pmu_convT2x2_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);
+int pmu_convT2x2_wgrad_bf16(const unsigned short* xt, const unsigned short* dut, const float* du, int N, int H,
+                            int W, int Hd, int Wd, int off_h, int off_w, int Cin, int Cout, float* dw,
+                            float* dbias, float* ws, size_t ws_bytes, void* stream);
 
 /* ---- first layer (Cin <= 4, planes given NCHW-style, one pointer per channel) ------ */
 int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,

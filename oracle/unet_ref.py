@@ -55,7 +55,8 @@ class Bf16Conv3x3(torch.autograd.Function):
 class Bf16ConvT2x2(torch.autograd.Function):
     """ConvTranspose2d(k2, s2) with the HIP bf16 path's arithmetic: the forward rounds the operand
     and the weights to bf16 (when ``fwd``), the input gradient rounds dy and the weights (when
-    ``dgrad``); the weight gradient stays in the ambient precision (pmu_convT2x2_wgrad is fp32)."""
+    ``dgrad``); the weight gradient multiplies the rounded input and dy (pmu_convT2x2_wgrad_bf16),
+    the bias gradient sums the unrounded dy."""
 
     @staticmethod
     def forward(ctx, x, w, b, fwd, dgrad):
@@ -68,7 +69,7 @@ class Bf16ConvT2x2(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx = F.conv2d(_rb(dy) if ctx.dgrad else dy, _rb(w) if ctx.dgrad else w, stride=2)
         n, k = dy.shape[0], dy.shape[1]
-        dw = torch.einsum("ncij,nkiajb->ckab", x, dy.reshape(n, k, x.shape[2], 2, x.shape[3], 2))
+        dw = torch.einsum("ncij,nkiajb->ckab", _rb(x), _rb(dy).reshape(n, k, x.shape[2], 2, x.shape[3], 2))
         db = dy.sum((0, 2, 3)) if ctx.has_b else None
         return dx, dw, db, None, None
 

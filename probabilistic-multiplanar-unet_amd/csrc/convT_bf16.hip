@@ -173,6 +173,249 @@ __global__ __launch_bounds__(256, 2) void convT_bf16_kernel(TArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Weight gradient on bf16 MFMA: dW[ci][co][a][b] = sum_p xt[p][ci] * dut[pix_ab(p)][co]
+// (xt = bf16 of the BN+ReLU input, dut = bf16 of du, both materialised by pmu_frame_to_bf16).
+// K = convT-input pixels, 64 per tile in flat (n, i, j) order; the MFMA takes 8 consecutive pixels
+// per lane half, so both operands are read with ds_read_b64_tr_b16 from channel-contiguous LDS rows
+// (as wgrad3x3_bf16): the tap only changes which du pixel a row holds.  Block = 128 ci x 64 co x 4
+// taps, 4 waves (one 32-ci fragment each) x (2 co fragments x 4 taps) = 8 accumulators; the next
+// tile's 12 units per thread are in registers under the current tile's 32 MFMAs per wave.
+// Split-K slabs ws[split][ab][ci][co] are reduced in a fixed order.
+// ---------------------------------------------------------------------------------------------
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+constexpr int WCI = 128, WCO = 64, WPX = 64;
+constexpr int XSW = WCI + 32;  // 320-B rows: 64 mod 256, transposed reads conflict-free
+constexpr int DSW = WCO + 32;  // 192-B rows
+constexpr int XU = WPX * WCI / 8 / 256;      // 4 X units per thread
+constexpr int DU = 4 * WPX * WCO / 8 / 256;  // 8 D units per thread
+
+struct TwbArgs {
+  const unsigned short* xt;   // [N][H][W][Cip]
+  const unsigned short* dut;  // [N][Hd][Wd][Cop]
+  float* ws;
+  int N, H, W, Hd, Wd, oh, ow, Cin, Cout, Cip, Cop, ntiles, nsplit;
+};
+
+__device__ __forceinline__ s16x4 tr_read(const unsigned short* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+__device__ __forceinline__ uint4 keep_if(bool ok, uint4 v) {
+  return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
+}
+
+__global__ __launch_bounds__(256, 2) void convT_wgrad_bf16_kernel(TwbArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[WPX * XSW];
+  __shared__ __attribute__((aligned(16))) unsigned short Ds[4 * WPX * DSW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nco = pmu_cdiv_dev(a.Cout, WCO);
+  const int co0 = (blockIdx.x % nco) * WCO, ci0 = (blockIdx.x / nco) * WCI;
+  const int split = blockIdx.y;
+  const long long P = (long long)a.N * a.H * a.W;
+  const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
+  const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[f][t][r] = 0.f;
+
+  uint4 rx0, rx1, rx2, rx3, rd0, rd1, rd2, rd3, rd4, rd5, rd6, rd7;  // plain locals (no scratch)
+  static_assert(XU == 4 && DU == 8, "staging register layout");
+  // X unit u = tid + 256 i: pixel u >> 4, 8-channel unit u & 15; D unit: tap u >> 9, pixel (u >> 3) & 63, unit u & 7
+#define PMU_XL(I, R)                                                                                \
+  {                                                                                                \
+    const int u_ = tid + 256 * (I);                                                                \
+    const long long p_ = (long long)tile_ * WPX + (u_ >> 4);                                       \
+    const int c_ = ci0 + 8 * (u_ & 15);                                                            \
+    const bool ok_ = p_ < P && c_ < a.Cip;                                                         \
+    R = keep_if(ok_, *reinterpret_cast<const uint4*>(a.xt + (ok_ ? p_ * a.Cip + c_ : 0)));        \
+  }
+#define PMU_DL(I, R)                                                                                \
+  {                                                                                                \
+    const int u_ = tid + 256 * (I);                                                                \
+    const int tap_ = u_ >> 9;                                                                      \
+    const long long p_ = (long long)tile_ * WPX + ((u_ >> 3) & 63);                                \
+    const int c_ = co0 + 8 * (u_ & 7);                                                             \
+    const bool ok_ = p_ < P && c_ < a.Cop;                                                         \
+    long long q_ = 0;                                                                              \
+    if (ok_) {                                                                                     \
+      const int j_ = (int)(p_ % a.W);                                                              \
+      const long long t2_ = p_ / a.W;                                                              \
+      const int i_ = (int)(t2_ % a.H);                                                             \
+      const long long n_ = t2_ / a.H;                                                              \
+      q_ = ((n_ * a.Hd + a.oh + 2 * i_ + (tap_ >> 1)) * a.Wd + a.ow + 2 * j_ + (tap_ & 1)) * a.Cop + c_; \
+    }                                                                                              \
+    R = keep_if(ok_, *reinterpret_cast<const uint4*>(a.dut + q_));                                 \
+  }
+#define PMU_LOAD(T)                                                                                 \
+  {                                                                                                \
+    const int tile_ = (T);                                                                         \
+    PMU_XL(0, rx0) PMU_XL(1, rx1) PMU_XL(2, rx2) PMU_XL(3, rx3)                                    \
+    PMU_DL(0, rd0) PMU_DL(1, rd1) PMU_DL(2, rd2) PMU_DL(3, rd3)                                    \
+    PMU_DL(4, rd4) PMU_DL(5, rd5) PMU_DL(6, rd6) PMU_DL(7, rd7)                                    \
+  }
+#define PMU_XS(I, R) { const int u_ = tid + 256 * (I); *reinterpret_cast<uint4*>(Xs + (u_ >> 4) * XSW + 8 * (u_ & 15)) = R; }
+#define PMU_DS(I, R) { const int u_ = tid + 256 * (I); *reinterpret_cast<uint4*>(Ds + ((u_ >> 9) * WPX + ((u_ >> 3) & 63)) * DSW + 8 * (u_ & 7)) = R; }
+#define PMU_STORE()                                                                                 \
+  {                                                                                                \
+    PMU_XS(0, rx0) PMU_XS(1, rx1) PMU_XS(2, rx2) PMU_XS(3, rx3)                                    \
+    PMU_DS(0, rd0) PMU_DS(1, rd1) PMU_DS(2, rd2) PMU_DS(3, rd3)                                    \
+    PMU_DS(4, rd4) PMU_DS(5, rd5) PMU_DS(6, rd6) PMU_DS(7, rd7)                                    \
+  }
+
+  // transposed-read lane roles (see wgrad3x3_bf16.hip)
+  const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+  const int xcol = wave * 32 + 16 * g + 4 * p;
+  const int dcol = 16 * g + 4 * p;
+  if (t_beg < t_end) {
+    PMU_LOAD(t_beg)
+    PMU_STORE()
+  }
+  __syncthreads();
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    const bool more = tile + 1 < t_end;
+    if (more) PMU_LOAD(tile + 1)  // in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < WPX / 16; ++ks) {
+      const int pk0 = 16 * ks + 8 * h + q, pk1 = pk0 + 4;
+      const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(tr_read(Xs + pk0 * XSW + xcol),
+                                                                             tr_read(Xs + pk1 * XSW + xcol), 0, 1, 2,
+                                                                             3, 4, 5, 6, 7));
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const unsigned short* d = Ds + (tap * WPX) * DSW + 32 * f + dcol;
+          const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(tr_read(d + pk0 * DSW),
+                                                                                  tr_read(d + pk1 * DSW), 0, 1, 2, 3,
+                                                                                  4, 5, 6, 7));
+          acc[f][tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[f][tap], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (more) {
+      PMU_STORE()
+      __syncthreads();
+    }
+  }
+#undef PMU_XL
+#undef PMU_DL
+#undef PMU_LOAD
+#undef PMU_XS
+#undef PMU_DS
+#undef PMU_STORE
+  // slab ws[split][ab][ci][co]: accumulator rows = ci (A rows), columns = co (lanes)
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int co = co0 + 32 * f + (lane & 31);
+    if (co >= a.Cout) continue;
+#pragma unroll
+    for (int tap = 0; tap < 4; ++tap)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = ci0 + wave * 32 + acc_row(r, lane);
+        if (ci < a.Cin) a.ws[(((long long)split * 4 + tap) * a.Cin + ci) * a.Cout + co] = acc[f][tap][r];
+      }
+  }
+}
+
+// dW[ci][co][ab] = sum_s ws[s][ab][ci][co] (4 split groups per element, fixed order)
+__global__ __launch_bounds__(256) void convT_wreduce_bf16_kernel(const float* __restrict__ ws, int nsplit, int Cin,
+                                                                 int Cout, float* __restrict__ dw) {
+  __shared__ float red[4][64];
+  const long long CC = (long long)Cin * Cout, E = 4 * CC;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + lane;  // (ab * Cin + ci) * Cout + co
+  float s0 = 0.f, s1 = 0.f;
+  if (e < E) {
+    int sp = g;
+    for (; sp + 4 < nsplit; sp += 8) {
+      s0 += ws[(long long)sp * E + e];
+      s1 += ws[(long long)(sp + 4) * E + e];
+    }
+    for (; sp < nsplit; sp += 4) s0 += ws[(long long)sp * E + e];
+  }
+  red[g][lane] = s0 + s1;
+  __syncthreads();
+  if (g == 0 && e < E) {
+    const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    const int ab = (int)(e / CC);
+    const long long cc = e - ab * CC;  // ci * Cout + co
+    dw[cc * 4 + ab] = t;
+  }
+}
+
+// dbias[co] = sum of du over the convT output region, fp32 (the unrounded gradient), fixed order.
+// Block b: PL = 256 / (Cout/4) pixel lanes x Cout/4 channel quads; lane pl sums pixels
+// b*PL + pl + k*G*PL as float4, the lanes are added in order through LDS into part[b][Cout].
+__global__ __launch_bounds__(256) void convT_dbias_part_kernel(const float* __restrict__ du, int N, int H2, int W2,
+                                                               int Hd, int Wd, int oh, int ow, int Cout,
+                                                               float* __restrict__ part) {
+  __shared__ float4 red[256];
+  const int nq = Cout / 4, PL = 256 / nq;
+  const int t = threadIdx.x, qd = t % nq, pl = t / nq;
+  const long long npx = (long long)N * H2 * W2;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (pl < PL) {
+    for (long long r = (long long)blockIdx.x * PL + pl; r < npx; r += (long long)gridDim.x * PL) {
+      const long long row = r / W2;
+      const int x = (int)(r - row * W2);
+      const long long n = row / H2;
+      const int y = (int)(row - n * H2);
+      const float4 v = *reinterpret_cast<const float4*>(du + ((n * Hd + oh + y) * Wd + ow + x) * Cout + 4 * qd);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[t] = acc;
+  __syncthreads();
+  if (pl == 0) {
+    float4 s = red[qd];
+    for (int l = 1; l < PL; ++l) {
+      const float4 v = red[l * nq + qd];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    *reinterpret_cast<float4*>(part + (long long)blockIdx.x * Cout + 4 * qd) = s;
+  }
+}
+// scalar variant for Cout not a multiple of 4 (or > 1024)
+__global__ __launch_bounds__(256) void convT_dbias_part1_kernel(const float* __restrict__ du, int N, int H2, int W2,
+                                                                int Hd, int Wd, int oh, int ow, int Cout,
+                                                                float* __restrict__ part) {
+  const long long rows = (long long)N * H2;
+  for (int c = threadIdx.x; c < Cout; c += 256) {
+    float s = 0.f;
+    for (long long r = blockIdx.x; r < rows; r += gridDim.x) {
+      const long long n = r / H2;
+      const int y = (int)(r - n * H2);
+      const float* row = du + ((n * Hd + oh + y) * Wd + ow) * Cout + c;
+      for (int x = 0; x < W2; ++x) s += row[(long long)x * Cout];
+    }
+    part[(long long)blockIdx.x * Cout + c] = s;
+  }
+}
+__global__ void convT_dbias_sum_kernel(const float* __restrict__ part, int G, int Cout, float* __restrict__ db) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= Cout) return;
+  float s = 0.f;
+  for (int gidx = 0; gidx < G; ++gidx) s += part[(long long)gidx * Cout + c];
+  db[c] = s;
+}
+
+static void twb_geometry(int N, int H, int W, int Cin, int Cout, int* ntiles, int* nsplit) {
+  *ntiles = (int)(((long long)N * H * W + WPX - 1) / WPX);
+  const int bmn = pmu_cdiv(Cin, WCI) * pmu_cdiv(Cout, WCO);
+  int sp = 512 / bmn;
+  if (sp < 1) sp = 1;
+  if (sp > *ntiles) sp = *ntiles;
+  *nsplit = sp;
+}
+constexpr int DB_G = 256;  // dbias partial rows
+
 }  // namespace
 
 extern "C" int pmu_convT2x2_pack_bf16(const float* w, int Cin, int Cout, int dgrad, unsigned short* wp, void* stream) {
@@ -216,5 +459,46 @@ extern "C" int pmu_convT2x2_dgrad_bf16(const float* du, int Hd, int Wd, int off_
   dim3 grid((unsigned)pmu_cdiv(p.M, TM), (unsigned)(Cin / TN));
   hipLaunchKernelGGL(convT_bf16_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, p);
   PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" size_t pmu_convT2x2_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout) {
+  int nt, ns;
+  twb_geometry(N, H, W, Cin, Cout, &nt, &ns);
+  return ((size_t)ns * 4 * Cin * Cout + (size_t)DB_G * Cout) * sizeof(float);
+}
+
+extern "C" int pmu_convT2x2_wgrad_bf16(const unsigned short* xt, const unsigned short* dut, const float* du, int N, int H,
+                                       int W, int Hd, int Wd, int off_h, int off_w, int Cin, int Cout, float* dw,
+                                       float* dbias, float* ws, size_t ws_bytes, void* stream) {
+  PMU_REQUIRE(xt && dut && dw && ws && N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0);
+  PMU_REQUIRE(off_h >= 0 && off_w >= 0 && off_h + 2 * H <= Hd && off_w + 2 * W <= Wd && (!dbias || du));
+  PMU_REQUIRE(ws_bytes >= pmu_convT2x2_wgrad_ws_bf16(N, H, W, Cin, Cout));
+  TwbArgs a;
+  a.xt = xt; a.dut = dut; a.ws = ws;
+  a.N = N; a.H = H; a.W = W; a.Hd = Hd; a.Wd = Wd; a.oh = off_h; a.ow = off_w; a.Cin = Cin; a.Cout = Cout;
+  a.Cip = (Cin + 7) & ~7; a.Cop = (Cout + 7) & ~7;
+  twb_geometry(N, H, W, Cin, Cout, &a.ntiles, &a.nsplit);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)(pmu_cdiv(Cin, WCI) * pmu_cdiv(Cout, WCO)), (unsigned)a.nsplit);
+  hipLaunchKernelGGL(convT_wgrad_bf16_kernel, grid, dim3(256), 0, st, a);
+  PMU_CHECK_LAUNCH();
+  const long long E = 4LL * Cin * Cout;
+  hipLaunchKernelGGL(convT_wreduce_bf16_kernel, dim3((unsigned)pmu_cdiv(E, 64)), dim3(256), 0, st, (const float*)ws,
+                     a.nsplit, Cin, Cout, dw);
+  PMU_CHECK_LAUNCH();
+  if (dbias) {
+    float* part = ws + (size_t)a.nsplit * 4 * Cin * Cout;
+    if (Cout % 4 == 0 && Cout <= 1024)
+      hipLaunchKernelGGL(convT_dbias_part_kernel, dim3(DB_G), dim3(256), 0, st, du, N, 2 * H, 2 * W, Hd, Wd, off_h,
+                         off_w, Cout, part);
+    else
+      hipLaunchKernelGGL(convT_dbias_part1_kernel, dim3(DB_G), dim3(256), 0, st, du, N, 2 * H, 2 * W, Hd, Wd, off_h,
+                         off_w, Cout, part);
+    PMU_CHECK_LAUNCH();
+    hipLaunchKernelGGL(convT_dbias_sum_kernel, dim3((unsigned)pmu_cdiv(Cout, 256)), dim3(256), 0, st, (const float*)part,
+                       DB_G, Cout, dbias);
+    PMU_CHECK_LAUNCH();
+  }
   return PMU_OK;
 }

@@ -67,6 +67,9 @@ SIGNATURES = {
     "pmu_convT2x2_fwd_bf16": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_dgrad_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                         c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_wgrad_ws_bf16": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_convT2x2_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                                        c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_conv_first_fwd": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p, c_void_p]),
     "pmu_conv_first_tiles": (c_int, [c_int, c_int, c_int]),

@@ -526,10 +526,20 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
                    wpt.data_ptr(), N, hi, wi, Cin_t, Cup, dx.data_ptr(), s)
         dwt = grads.new(convT.weight)
         dbt = grads.new(convT.bias) if convT.bias is not None else None
-        wsb = L.lib().pmu_convT2x2_wgrad_ws(N, hi, wi, Cin_t, Cup)
-        ws = _empty(max(1, (wsb + 3) // 4), device=dev)
-        L.call("pmu_convT2x2_wgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], frame_of([prev.act()], N, hi, wi),
-               Cup, dwt.data_ptr(), L.ptr(dbt), ws.data_ptr(), wsb, s)
+        if us.bf16:
+            # bf16 operands materialised (the convT input after BN+ReLU, du); the bias gradient sums fp32 du
+            xt = frame_to_bf16([prev.act()], N, hi, wi)
+            dut = frame_to_bf16([Src(dup)], N, Hd, Wd)
+            wsb = L.lib().pmu_convT2x2_wgrad_ws_bf16(N, hi, wi, Cin_t, Cup)
+            ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+            L.call("pmu_convT2x2_wgrad_bf16", xt.data_ptr(), dut.data_ptr(), dup.data_ptr(), N, hi, wi, Hd, Wd,
+                   us.off[0], us.off[1], Cin_t, Cup, dwt.data_ptr(), L.ptr(dbt), ws.data_ptr(), wsb, s)
+            del xt, dut
+        else:
+            wsb = L.lib().pmu_convT2x2_wgrad_ws(N, hi, wi, Cin_t, Cup)
+            ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+            L.call("pmu_convT2x2_wgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1],
+                   frame_of([prev.act()], N, hi, wi), Cup, dwt.data_ptr(), L.ptr(dbt), ws.data_ptr(), wsb, s)
         da = dx
     # ---- encoder, deepest first; da = gradient w.r.t. the deepest encoder output
     for lev in reversed(range(nlev)):

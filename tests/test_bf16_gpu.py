@@ -342,3 +342,30 @@ def test_conv3x3_dgrad_raw(dev, N, H, W, Cin, Cout, split):
                                      padding=1).permute(0, 2, 3, 1)
     got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
     assert _rel(got, ref) <= TOL
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,oh,ow", [(2, 16, 16, 128, 64, 0, 0), (2, 10, 9, 256, 32, 1, 0),
+                                                  (1, 8, 12, 64, 128, 0, 1), (3, 5, 7, 40, 24, 1, 1)])
+def test_convT_wgrad_bf16(dev, N, H, W, Cin, Cout, oh, ow):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    g = torch.Generator().manual_seed(61 + H)
+    Hd, Wd = 2 * H + oh + (1 if oh else 0), 2 * W + ow + (1 if ow else 0)
+    z = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    coef = torch.cat([torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.2]).to(dev)
+    du = torch.randn(N, Hd, Wd, Cout, generator=g).to(dev)
+    xt = _to_bf16([Src(z, L.SRC_BNRELU, coef)], N, H, W, Cin)
+    dut = _to_bf16([Src(du)], N, Hd, Wd, Cout)
+    wsb = L.lib().pmu_convT2x2_wgrad_ws_bf16(N, H, W, Cin, Cout)
+    ws = torch.empty(wsb // 4 + 1, device=dev)
+    dw = torch.empty(Cin, Cout, 2, 2, device=dev)
+    db = torch.empty(Cout, device=dev)
+    L.call("pmu_convT2x2_wgrad_bf16", xt.data_ptr(), dut.data_ptr(), du.data_ptr(), N, H, W, Hd, Wd, oh, ow, Cin, Cout,
+           dw.data_ptr(), db.data_ptr(), ws.data_ptr(), wsb, L.stream())
+    torch.cuda.synchronize()
+    x = _bf16_values(xt, Cin).double().cpu()                       # (N,H,W,Cin)
+    dui = du[:, oh:oh + 2 * H, ow:ow + 2 * W].double().cpu()
+    dr = _rb(du[:, oh:oh + 2 * H, ow:ow + 2 * W]).double().cpu().reshape(N, H, 2, W, 2, Cout)
+    ref = torch.einsum("nijc,niajbk->ckab", x, dr)
+    assert _rel(dw, ref) <= TOL
+    assert _rel(db, dui.sum((0, 1, 2))) <= 1e-5
