@@ -309,6 +309,11 @@ int pmu_fcomb_bwd(const float* feat, const float* z, const float* zb, const floa
                   float* const* dw, float* const* db, float* dwl, float* dbl, float* ws,
                   size_t ws_bytes, void* stream);
 
+/* ---- diagnostics: resident blocks per CU of the main GEMM kernels (hipOccupancy API) ---- */
+int pmu_occupancy_conv3x3_raw(int* blocks_per_cu);
+int pmu_occupancy_wgrad3x3_bf16(int* blocks_per_cu);
+int pmu_occupancy_conv3x3_pipe(int* blocks_per_cu);
+
 #ifdef __cplusplus
 }
 #endif

@@ -503,3 +503,13 @@ extern "C" int pmu_conv3x3_dgrad(const pmu_frame* dz, const float* w, const floa
   const int Cout = dz->src[0].C;
   return launch_conv(dz, w, wp, nullptr, Cin, Cout, dx0, dx1, Csplit, nullptr, true, stream);
 }
+
+// Diagnostic: resident blocks per CU of the main kernel of this file (hipOccupancy API).
+extern "C" int pmu_occupancy_conv3x3_pipe(int* blocks_per_cu) {
+  PMU_REQUIRE(blocks_per_cu);
+  int n = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(conv3x3_pipe_kernel<false, PMU_POOL_NONE>), 256, 0);
+  if (e != hipSuccess) return (int)e;
+  *blocks_per_cu = n;
+  return PMU_OK;
+}

@@ -166,24 +166,35 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
   for (int ch = 0; ch < a.nch; ++ch) {
     const bool more = ch + 1 < a.nch;
     if (more) PMU_PREFETCH(ch + 1)  // in flight during the MFMAs below
-    bf16x8 op[2][FM + FN];
-    auto load_ops = [&](int tap, int s, bf16x8 (&o)[FM + FN]) {
-      const int toff = ((tap / 3) * HW2 + (tap % 3)) * LS + 16 * s;
+    // Operands move a whole tap (both k-steps: 8 x ds_read_b128) ahead of its 8 MFMAs; the
+    // scheduling barriers keep the compiler from sinking each read next to its first use (it did:
+    // one LDS round trip exposed every two MFMAs).
+    bf16x8 op[2][2][FM + FN];
+    auto load_tap = [&](int tap, bf16x8 (&o)[2][FM + FN]) {
+      const int toff = ((tap / 3) * HW2 + (tap % 3)) * LS;
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm) o[fm] = *reinterpret_cast<const bf16x8*>(As + abase[fm] + toff);
+      for (int s = 0; s < 2; ++s) {
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn)
-        o[FM + fn] = *reinterpret_cast<const bf16x8*>(Bs + tap * BNT * LS + bbase[fn] + 16 * s);
-    };
-    load_ops(0, 0, op[0]);
-#pragma unroll
-    for (int st = 0; st < 18; ++st) {  // 9 taps x 2 k-steps
-      if (st + 1 < 18) load_ops((st + 1) >> 1, (st + 1) & 1, op[(st + 1) & 1]);
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
+        for (int fm = 0; fm < FM; ++fm) o[s][fm] = *reinterpret_cast<const bf16x8*>(As + abase[fm] + toff + 16 * s);
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st & 1][fm], op[st & 1][FM + fn], acc[fm][fn], 0, 0, 0);
+          o[s][FM + fn] = *reinterpret_cast<const bf16x8*>(Bs + tap * BNT * LS + bbase[fn] + 16 * s);
+      }
+    };
+    load_tap(0, op[0]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) load_tap(tap + 1, op[(tap + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn)
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[tap & 1][s][fm], op[tap & 1][s][FM + fn],
+                                                                   acc[fm][fn], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
     if (more) {
@@ -345,4 +356,14 @@ extern "C" int pmu_conv3x3_fwd_raw(const unsigned short* xt, int Cp, int N, int 
 extern "C" int pmu_conv3x3_dgrad_raw(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                                      int Cin, int Csplit, float* dx0, float* dx1, void* stream) {
   return launch_raw(dzt, Cp, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
+}
+
+// Diagnostic: resident blocks per CU of the main kernel of this file (hipOccupancy API).
+extern "C" int pmu_occupancy_conv3x3_raw(int* blocks_per_cu) {
+  PMU_REQUIRE(blocks_per_cu);
+  int n = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(conv3x3_raw_kernel<false, 5, 256>), 256, 0);
+  if (e != hipSuccess) return (int)e;
+  *blocks_per_cu = n;
+  return PMU_OK;
 }

@@ -359,3 +359,13 @@ extern "C" int pmu_conv3x3_wgrad_bf16(const unsigned short* dzt, const unsigned 
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
+
+// Diagnostic: resident blocks per CU of the main kernel of this file (hipOccupancy API).
+extern "C" int pmu_occupancy_wgrad3x3_bf16(int* blocks_per_cu) {
+  PMU_REQUIRE(blocks_per_cu);
+  int n = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(wgrad3x3_bf16_kernel<128, 4>), 768, 0);
+  if (e != hipSuccess) return (int)e;
+  *blocks_per_cu = n;
+  return PMU_OK;
+}

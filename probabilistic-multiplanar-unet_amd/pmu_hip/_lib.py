@@ -70,6 +70,9 @@ SIGNATURES = {
     "pmu_convT2x2_wgrad_ws_bf16": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_convT2x2_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                         c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pmu_occupancy_conv3x3_raw": (c_int, [POINTER(c_int)]),
+    "pmu_occupancy_wgrad3x3_bf16": (c_int, [POINTER(c_int)]),
+    "pmu_occupancy_conv3x3_pipe": (c_int, [POINTER(c_int)]),
     "pmu_conv_first_fwd": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p, c_void_p]),
     "pmu_conv_first_tiles": (c_int, [c_int, c_int, c_int]),
