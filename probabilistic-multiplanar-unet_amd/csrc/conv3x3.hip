@@ -271,9 +271,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(ConvArgs a) {
 constexpr int PIPE_NB = 9 * BN * BK / 4 / 256;  // packed-B float4 per thread per chunk
 static_assert(PIPE_NB == 9, "PipeB holds 9 float4");
 
-template <bool DGRAD, int POOL>
-__global__ __launch_bounds__(256, 1) void conv3x3_pipe_kernel(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+// SB (single buffer): one LDS stage and 2 blocks per CU — the commit waits behind a barrier, but the
+// partner block's MFMAs cover it.
+template <bool DGRAD, int POOL, bool SB = false>
+__global__ __launch_bounds__(256, SB ? 2 : 1) void conv3x3_pipe_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[(SB ? 1 : 2) * STAGE];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -347,7 +349,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_pipe_kernel(ConvArgs a) {
   PMU_COMMIT(smem)
   __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
-    const float* As = smem + (ch & 1) * STAGE;
+    const float* As = smem + (SB ? 0 : (ch & 1) * STAGE);
     const float* Bs = As + A_FLOATS;
     if (ch + 1 < nchunks) PMU_PREFETCH(ch + 1)
     float4 op[2][8];
@@ -383,8 +385,16 @@ __global__ __launch_bounds__(256, 1) void conv3x3_pipe_kernel(ConvArgs a) {
       if (tap + 1 < 9) load_ops(tap + 1, op[(tap + 1) & 1]);
       mfmas(op[tap & 1]);
     }
-    if (ch + 1 < nchunks) PMU_COMMIT(smem + ((ch + 1) & 1) * STAGE)
-    __syncthreads();
+    if (SB) {
+      __syncthreads();
+      if (ch + 1 < nchunks) {
+        PMU_COMMIT(smem)
+        __syncthreads();
+      }
+    } else {
+      if (ch + 1 < nchunks) PMU_COMMIT(smem + ((ch + 1) & 1) * STAGE)
+      __syncthreads();
+    }
   }
 #undef PMU_PREFETCH
 #undef PMU_COMMIT
@@ -398,16 +408,19 @@ static int pick_twl(int W) {
   return 3;
 }
 
-// Default: the software-pipelined 1-block/CU kernel wherever its staging applies (measured 3-15%
-// faster than the 2-blocks/CU kernel on the c2 dgrad shapes and on par for fwd, once its prefetch
-// registers were kept out of scratch); PMU_CONV_IMPL=sync selects the 2-blocks/CU kernel.
-static bool use_pipe() {
+// 0: sync kernel, 1: pipelined double-buffered (1 block/CU), 2 (default): pipelined single-buffered,
+// 2 blocks/CU — measured fwd 117 -> 128 TF, dgrad 113 -> 122 TF on the c2 shapes (the partner block's
+// MFMAs cover each block's commit phase).  PMU_CONV_IMPL=sync|pipe1 selects the others.
+static int pipe_mode() {
   static const int v = [] {
     const char* e = getenv("PMU_CONV_IMPL");
-    return (e && strcmp(e, "sync") == 0) ? 0 : 1;
+    if (e && strcmp(e, "sync") == 0) return 0;
+    if (e && strcmp(e, "pipe1") == 0) return 1;
+    return 2;
   }();
-  return v != 0;
+  return v;
 }
+static bool use_pipe() { return pipe_mode() != 0; }
 
 // a source the pipelined staging handles: float4 channels, chunks never straddle sources
 static bool pipe_src_ok(const pmu_src& s) {
@@ -441,7 +454,10 @@ static int launch_conv(const pmu_frame* in, const float* w, const float* wp, con
     const bool c0_ok = !two || s0.C % BK == 0;
 #define PMU_PIPE(DG, PL)                                                                           \
   if (dgrad == DG && pool == PL) {                                                                 \
-    hipLaunchKernelGGL((conv3x3_pipe_kernel<DG, PL>), grid, dim3(256), 0, st, a);                  \
+    if (pipe_mode() == 2)                                                                          \
+      hipLaunchKernelGGL((conv3x3_pipe_kernel<DG, PL, true>), grid, dim3(256), 0, st, a);          \
+    else                                                                                           \
+      hipLaunchKernelGGL((conv3x3_pipe_kernel<DG, PL, false>), grid, dim3(256), 0, st, a);         \
     PMU_CHECK_LAUNCH();                                                                            \
     return PMU_OK;                                                                                 \
   }
@@ -508,7 +524,7 @@ extern "C" int pmu_conv3x3_dgrad(const pmu_frame* dz, const float* w, const floa
 extern "C" int pmu_occupancy_conv3x3_pipe(int* blocks_per_cu) {
   PMU_REQUIRE(blocks_per_cu);
   int n = 0;
-  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(conv3x3_pipe_kernel<false, PMU_POOL_NONE>), 256, 0);
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(conv3x3_pipe_kernel<false, PMU_POOL_NONE, false>), 256, 0);
   if (e != hipSuccess) return (int)e;
   *blocks_per_cu = n;
   return PMU_OK;

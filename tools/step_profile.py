@@ -20,6 +20,10 @@ MODE = {0: "raw", 1: "bnrelu", 2: "bnbwd"}
 
 def describe(name, args):
     try:
+        if name in ("pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw"):
+            return f"{args[3]}x{args[4]} Cp{args[1]} -> {args[7] if name.endswith('fwd_raw') else args[6]}"
+        if name == "pmu_conv3x3_wgrad_bf16":
+            return f"{args[3]}x{args[4]} {args[5]}x{args[6]}"
         if name in ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad", "pmu_convT2x2_fwd"):
             f = args[0]._obj
             srcs = "+".join(f"{MODE[f.src[i].mode]}{POOL[f.src[i].pool]}{f.src[i].C}" for i in range(f.nsrc))
@@ -38,12 +42,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--workload", default="unet")
+    ap.add_argument("--workload", default="unet", help="unet (c2), c5 or probunet")
+    ap.add_argument("--precision", default=None)
     args = ap.parse_args()
     import bench
     from pmu_hip import _lib as L
-    ns = argparse.Namespace(batch=args.batch, size=args.size, classes=1, workload=args.workload,
-                            data="synthetic")
+    c5 = args.workload == "c5"
+    ns = argparse.Namespace(batch=16 if c5 else args.batch, size=512 if c5 else args.size, classes=3 if c5 else 1,
+                            workload=args.workload, data="synthetic", channels=3 if c5 else 1,
+                            precision=args.precision or ("bf16" if c5 else "fp32"))
     build = bench.build_unet if args.workload == "unet" else bench.build_probunet
     step, _, _, _ = build(ns, torch.device("cuda", 0), 1, 0)
     for _ in range(2):
