@@ -77,9 +77,10 @@ typedef struct pmu_frame {
 /* ---- 3x3 convolution (implicit GEMM on MFMA, LDS halo tiles) -------------------- */
 /* z[N][H][W][Cout] = conv3x3(frame, w) + bias.  If part != NULL, per-tile BN partial
  * sums (sum z, sum z^2) are written to part[tile][2][Cout]; pmu_conv3x3_tiles() gives
- * the tile count. */
+ * the tile count.  tee (nullable): receives the operand the kernel multiplied (the frame after
+ * BN+ReLU / pooling / concatenation), [N][H][W][Cin] fp32 — a RAW source for pmu_conv3x3_wgrad. */
 int pmu_conv3x3_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias,
-                    int Cout, float* z, float* part, void* stream);
+                    int Cout, float* z, float* part, float* tee, void* stream);
 int pmu_conv3x3_tiles(int N, int H, int W);
 /* Optional pre-packed weights (wp != NULL replaces w): the per-block/chunk B tiles laid out
  * contiguously in LDS order, so staging is a straight copy.  dgrad=1 packs the flipped,
@@ -90,7 +91,7 @@ int pmu_conv3x3_pack(const float* w, int Cout, int Cin, int dgrad, float* wp, vo
  * [Csplit,Cin) -> dx1 (NHWC, Cin-Csplit ch).  dz is a frame whose single source is
  * normally PMU_SRC_BNBWD. */
 int pmu_conv3x3_dgrad(const pmu_frame* dz, const float* w, const float* wp, int Cin, int Csplit,
-                      float* dx0, float* dx1, void* stream);
+                      float* dx0, float* dx1, float* tee, void* stream);  /* tee: dz after BN backward, [N][H][W][Cout] */
 /* dw[Cout][Cin][3][3] = dL/dw; ws must hold pmu_conv3x3_wgrad_ws() bytes. */
 size_t pmu_conv3x3_wgrad_ws(int N, int H, int W, int Cin, int Cout);
 int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int Cout, float* dw,

@@ -43,6 +43,7 @@ struct ConvArgs {
   float* out0;       // fwd: z [N][H][W][NOUT]; dgrad: dx channels [0, split)
   float* out1;       // dgrad: dx channels [split, NOUT)
   float* part;       // fwd BN partials [tiles][2][NOUT] or null
+  float* tee;        // optional copy of the staged operand [N][H][W][KC] (blockIdx.y == 0 writes)
   int NOUT, KC;      // GEMM N (output channels) and reduction channels
   int split;         // dgrad channel split
   int twl;           // log2(TW)
@@ -95,6 +96,24 @@ __device__ __forceinline__ void stage_B(const ConvArgs& a, int j0, int k0, float
     if (j < a.NOUT && k < a.KC)
       v = DGRAD ? a.w[((long long)k * a.NOUT + j) * 9 + (8 - tap)] : a.w[((long long)j * a.KC + k) * 9 + tap];
     Bs[(tap * BN + jl) * LS + kl] = v;
+  }
+}
+
+// Copy a staged chunk's interior pixels (the transformed operand: BN+ReLU, pooled, concatenated, or
+// the BN+ReLU backward of dz) to the tee tensor, from which the weight gradient stages a plain copy
+// instead of re-deriving it.  1024 float4 per chunk.
+__device__ __forceinline__ void tee_chunk32(const ConvArgs& a, const float* As, int k0, int n, int h0, int w0, int twl,
+                                            int tid) {
+  const int TW = 1 << twl, HW2 = TW + 2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = tid + 256 * i;
+    const int q = u >> 2, qq = u & 3;
+    const int r = q >> twl, c = q & (TW - 1);
+    const int h = h0 + r, w = w0 + c, ch = k0 + 4 * qq;
+    if (h < a.in.H && w < a.in.W && ch < a.KC)
+      *reinterpret_cast<float4*>(a.tee + (((long long)n * a.in.H + h) * a.in.W + w) * a.KC + ch) =
+          *reinterpret_cast<const float4*>(As + ((r + 1) * HW2 + c + 1) * LS + 4 * qq);
   }
 }
 
@@ -221,6 +240,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(ConvArgs a) {
     stage_items<NI>(F, n, k0, BK, tid & 3, ih, iw, dst, As);
     stage_B<DGRAD>(a, j0, k0, Bs, tid);
     __syncthreads();
+    if (a.tee && blockIdx.y == 0) tee_chunk32(a, As, k0, n, h0, w0, TWL, tid);
 
     float4 op[2][8];  // operand registers double-buffered across taps
     auto load_ops = [&](int tap, float4 (&o)[8]) {
@@ -352,6 +372,7 @@ __global__ __launch_bounds__(256, SB ? 2 : 1) void conv3x3_pipe_kernel(ConvArgs 
     const float* As = smem + (SB ? 0 : (ch & 1) * STAGE);
     const float* Bs = As + A_FLOATS;
     if (ch + 1 < nchunks) PMU_PREFETCH(ch + 1)
+    if (a.tee && blockIdx.y == 0) tee_chunk32(a, As, ch * BK, n, h0, w0, a.twl, tid);
     float4 op[2][8];
     auto load_ops = [&](int tap, float4 (&o)[8]) {
       const int toff = ((tap / 3) * HW2 + (tap % 3)) * LS;
@@ -430,10 +451,10 @@ static bool pipe_src_ok(const pmu_src& s) {
 }
 
 static int launch_conv(const pmu_frame* in, const float* w, const float* wp, const float* bias, int NOUT, int KC,
-                       float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
+                       float* out0, float* out1, int split, float* part, float* tee, bool dgrad, void* stream) {
   ConvArgs a;
   a.in = make_dev_frame(in);
-  a.w = w; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
+  a.w = w; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part; a.tee = tee;
   a.NOUT = NOUT; a.KC = KC; a.split = split;
   a.twl = pick_twl(in->W);
   const int TW = 1 << a.twl, TH = BM / TW;
@@ -506,18 +527,20 @@ extern "C" int pmu_conv3x3_pack(const float* w, int Cout, int Cin, int dgrad, fl
 }
 
 extern "C" int pmu_conv3x3_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout,
-                               float* z, float* part, void* stream) {
+                               float* z, float* part, float* tee, void* stream) {
   PMU_REQUIRE(valid_frame(in) && (w || wp) && z && Cout > 0);
   const int Cin = in->src[0].C + (in->nsrc > 1 ? in->src[1].C : 0);
-  return launch_conv(in, w, wp, bias, Cout, Cin, z, nullptr, Cout, part, false, stream);
+  PMU_REQUIRE(!tee || Cin % 4 == 0);
+  return launch_conv(in, w, wp, bias, Cout, Cin, z, nullptr, Cout, part, tee, false, stream);
 }
 
 extern "C" int pmu_conv3x3_dgrad(const pmu_frame* dz, const float* w, const float* wp, int Cin, int Csplit,
-                                 float* dx0, float* dx1, void* stream) {
+                                 float* dx0, float* dx1, float* tee, void* stream) {
   PMU_REQUIRE(valid_frame(dz) && dz->nsrc == 1 && (w || wp) && dx0 && Cin > 0);
   PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
   const int Cout = dz->src[0].C;
-  return launch_conv(dz, w, wp, nullptr, Cin, Cout, dx0, dx1, Csplit, nullptr, true, stream);
+  PMU_REQUIRE(!tee || Cout % 4 == 0);
+  return launch_conv(dz, w, wp, nullptr, Cin, Cout, dx0, dx1, Csplit, nullptr, tee, true, stream);
 }
 
 // Diagnostic: resident blocks per CU of the main kernel of this file (hipOccupancy API).

@@ -47,6 +47,7 @@ struct FastOps {
   int dc, xc;  // this thread's channel quad inside each source
 };
 
+template <bool RAW>
 __device__ __forceinline__ void tile_load(const FastOps& f, int n, int h0, int w0, int twl, int HW2, int HP, int tid,
                                           TileRegs& r) {
   const int TW = 1 << twl;
@@ -58,10 +59,10 @@ __device__ __forceinline__ void tile_load(const FastOps& f, int n, int h0, int w
     r.dok[i] = it < WPIX * 16 && h < f.ds.H && w < f.ds.W;
     const long long idx = r.dok[i] ? (((long long)n * f.ds.H + h) * f.ds.W + w) * f.ds.C + f.dc : (long long)f.dc;
     r.d[i] = *reinterpret_cast<const float4*>(f.ds.x + idx);
-    r.dz[i] = *reinterpret_cast<const float4*>(f.ds.z + idx);
+    if constexpr (!RAW) r.dz[i] = *reinterpret_cast<const float4*>(f.ds.z + idx);
   }
   const DevSrc& s = f.xs;
-  const bool mp = s.pool == PMU_POOL_MAX2, ap = s.pool == PMU_POOL_AVG2CEIL;
+  const bool mp = !RAW && s.pool == PMU_POOL_MAX2, ap = !RAW && s.pool == PMU_POOL_AVG2CEIL;
   const long long rs = (long long)s.W * s.C;
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
@@ -89,10 +90,30 @@ __device__ __forceinline__ void tile_load(const FastOps& f, int n, int h0, int w
   }
 }
 
+template <bool RAW>
 __device__ __forceinline__ void tile_store(const FastOps& f, const TileRegs& r, int HP, int tid, float* slot) {
   float* Ds = slot;
   float* Xs = slot + WPIX * WLS;
   const int cq = tid & 15;
+  if constexpr (RAW) {  // both operands already materialised (teed by the fwd / dgrad kernels)
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int it = tid + NT * i;
+      if (it >= WPIX * 16) continue;
+      float4 v = r.d[i];
+      if (!r.dok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(Ds + (it >> 4) * WLS + 4 * cq) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int it = tid + NT * i;
+      if (it >= HP * 16) continue;
+      float4 v = r.x[i][0];
+      if (!r.xok[i]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(Xs + (it >> 4) * WLS + 4 * cq) = v;
+    }
+    return;
+  }
   // coefficients re-read per tile (L1/L2 hits) rather than held in 28 VGPRs across the MFMA loop
   const float* dco = f.ds.coef + f.dc;
   const int dC = f.ds.C;
@@ -157,12 +178,14 @@ __device__ __forceinline__ void tile_stage_generic(const DevFrame& D, const DevF
   }
 }
 
-// FAST: every block's 64 dz channels / 64 act channels lie in one source each (host-checked);
-// the generic instantiation stages synchronously through frame_value4.
+// MODE 1 (fast): every block's 64 dz channels / 64 act channels lie in one source each (host-checked);
+// MODE 2 (raw): additionally both frames are single RAW sources (the operands the conv kernels teed);
+// MODE 0 stages synchronously through frame_value4.
 // TWL = log2 of the pixel-tile width (compile-time: with the K loop fully unrolled every LDS
 // operand address is the wave's base plus an immediate offset, no per-step VALU).
-template <bool FAST, int TWL>
+template <int MODE, int TWL>
 __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
+  constexpr bool FAST = MODE > 0, RAW = MODE == 2;
   __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int TW = 1 << TWL, TH = WPIX >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
@@ -175,14 +198,8 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
   const DevFrame& X = a.act;
 
   // fast path if both 64-channel blocks sit inside one source each
-  const bool d_fast = D.vec && D.nsrc == 1 && D.s0.mode == PMU_SRC_BNBWD && D.s0.pool == PMU_POOL_NONE &&
-                      co0 + WB <= D.C0;
-  const bool x_in0 = ci0 + WB <= X.C0, x_in1 = X.nsrc > 1 && ci0 >= X.C0 && ci0 + WB <= X.C;
+  const bool x_in0 = ci0 + WB <= X.C0;
   const DevSrc& xsrc = x_in0 ? X.s0 : X.s1;
-  const bool x_fast = X.vec && (x_in0 || x_in1) && xsrc.mode != PMU_SRC_BNBWD &&
-                      (xsrc.pool == PMU_POOL_NONE || xsrc.mode == PMU_SRC_BNRELU);
-  const bool fast = FAST && d_fast && x_fast;
-  (void)fast;
   FastOps f;
   if constexpr (FAST) {
     const int cq = tid & 15;
@@ -212,8 +229,8 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
     int n, h0, w0;
     origin(t_beg, n, h0, w0);
     if constexpr (FAST) {
-      tile_load(f, n, h0, w0, TWL, HW2, HP, tid, regs);
-      tile_store(f, regs, HP, tid, smem);
+      tile_load<RAW>(f, n, h0, w0, TWL, HW2, HP, tid, regs);
+      tile_store<RAW>(f, regs, HP, tid, smem);
     } else {
       tile_stage_generic(D, X, n, h0, w0, TWL, HW2, HP, co0, ci0, tid, smem);
     }
@@ -226,7 +243,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
     int nn = 0, nh0 = 0, nw0 = 0;
     if (more) {
       origin(tile + 1, nn, nh0, nw0);
-      if constexpr (FAST) tile_load(f, nn, nh0, nw0, TWL, HW2, HP, tid, regs);  // in flight during the MFMAs
+      if constexpr (FAST) tile_load<RAW>(f, nn, nh0, nw0, TWL, HW2, HP, tid, regs);  // in flight during the MFMAs
     }
     const float* Ds = smem + cur * SLOT;
     const float* Xs = Ds + WPIX * WLS;
@@ -245,7 +262,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_kernel(WgArgs a) {
     }
     if (more) {
       float* nxt = smem + (cur ^ 1) * SLOT;
-      if constexpr (FAST) tile_store(f, regs, HP, tid, nxt);
+      if constexpr (FAST) tile_store<RAW>(f, regs, HP, tid, nxt);
       else tile_stage_generic(D, X, nn, nh0, nw0, TWL, HW2, HP, co0, ci0, tid, nxt);
     }
     __syncthreads();
@@ -310,14 +327,18 @@ extern "C" int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int 
     const pmu_src& s = act->src[i];
     fast = fast && s.mode != PMU_SRC_BNBWD && (s.pool == PMU_POOL_NONE || s.mode == PMU_SRC_BNRELU);
   }
+  const bool raw = a.dz.vec && d0.mode == PMU_SRC_RAW && d0.pool == PMU_POOL_NONE && Cout % WB == 0 &&
+                   a.act.vec && act->nsrc == 1 && act->src[0].mode == PMU_SRC_RAW &&
+                   act->src[0].pool == PMU_POOL_NONE && Cin % WB == 0;
+  const int mode = raw ? 2 : fast ? 1 : 0;
   hipStream_t st = (hipStream_t)stream;
+#define PMU_WG_LAUNCH(M, T) hipLaunchKernelGGL((wgrad3x3_kernel<M, T>), grid, dim3(NT), 0, st, a)
   if (a.twl == 4) {
-    if (fast) hipLaunchKernelGGL((wgrad3x3_kernel<true, 4>), grid, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((wgrad3x3_kernel<false, 4>), grid, dim3(NT), 0, st, a);
+    if (mode == 2) PMU_WG_LAUNCH(2, 4); else if (mode == 1) PMU_WG_LAUNCH(1, 4); else PMU_WG_LAUNCH(0, 4);
   } else {
-    if (fast) hipLaunchKernelGGL((wgrad3x3_kernel<true, 3>), grid, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((wgrad3x3_kernel<false, 3>), grid, dim3(NT), 0, st, a);
+    if (mode == 2) PMU_WG_LAUNCH(2, 3); else if (mode == 1) PMU_WG_LAUNCH(1, 3); else PMU_WG_LAUNCH(0, 3);
   }
+#undef PMU_WG_LAUNCH
   PMU_CHECK_LAUNCH();
   const long long E = 9LL * Cout * Cin;
   hipLaunchKernelGGL(pmu_splitk_reduce9_kernel, dim3((unsigned)pmu_cdiv(E, 64)), dim3(256), 0, st, (const float*)ws,

@@ -39,11 +39,11 @@ class PmuSgdChunk(ctypes.Structure):
 _FP = POINTER(PmuFrame)
 # name -> (restype, argtypes)
 SIGNATURES = {
-    "pmu_conv3x3_fwd": (c_int, [_FP, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_fwd": (c_int, [_FP, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_packed_size": (c_size_t, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_tiles": (c_int, [c_int, c_int, c_int]),
-    "pmu_conv3x3_dgrad": (c_int, [_FP, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad": (c_int, [_FP, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_wgrad_ws": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_conv3x3_wgrad": (c_int, [_FP, _FP, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_conv3x3_packed_size_bf16": (c_size_t, [c_int, c_int, c_int]),

@@ -162,6 +162,7 @@ class ConvBNOut:
     planes: list | None = None                  # first-layer input planes
     bf16: bool = False                          # computed on the bf16-MFMA kernels
     xt: torch.Tensor | None = None              # bf16: the operand copy the forward kernel wrote (for wgrad)
+    xt32: torch.Tensor | None = None            # fp32: the same, teed by pmu_conv3x3_fwd (RAW wgrad operand)
 
     def act(self, pool=L.POOL_NONE) -> Src:
         return Src(self.z, L.SRC_BNRELU, self.bn.coef, pool=pool)
@@ -214,11 +215,20 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         R = lb.pmu_conv3x3_tiles(N, H, W)
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
         wp = pack_weights(conv.weight, dgrad=False)
+        Cin = sum(sr.C for sr in srcs)
+        # the weight gradient reads the operand the kernel staged (RAW) instead of re-deriving it
+        xt32 = _empty(N, H, W, Cin, device=dev) if keep and tee32_ok(Cin, Cout) else None
         L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), wp.data_ptr(), L.ptr(conv.bias),
-               Cout, z.data_ptr(), L.ptr(part), s)
+               Cout, z.data_ptr(), L.ptr(part), L.ptr(xt32), s)
     st = bn_forward(part, R, Cout, N * H * W, bn, training, dev)
     bfl = bf16 and planes is None
-    return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes, bf16=bfl, xt=xt if bfl else None)
+    return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes, bf16=bfl, xt=xt if bfl else None,
+                     xt32=None if (bf16 or planes is not None) else xt32)
+
+
+def tee32_ok(cin: int, cout: int) -> bool:
+    """Channel counts for which the fp32 weight gradient runs on teed RAW operands (its 64x64 blocks)."""
+    return cin % 64 == 0 and cout % 64 == 0
 
 
 def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, need_dx=True, split=None):
@@ -237,6 +247,8 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     lb = L.lib()
     if out.bf16:
         return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split)
+    if out.xt32 is not None and need_dx:
+        return _conv_backward_tee32(out, dzf, conv, dw, split)
     if out.planes is not None:
         Cin = len(out.planes)
         wsb = lb.pmu_conv_first_wgrad_ws(N, H, W, Cin, Cout)
@@ -254,13 +266,44 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     wp = pack_weights(conv.weight, dgrad=True)
     if split is None:
         dx = _empty(N, H, W, Cin, device=dev)
-        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, Cin, dx.data_ptr(), None, s)
+        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, Cin, dx.data_ptr(), None,
+               None, s)
         return dx
     dx0 = _empty(N, H, W, split, device=dev)
     dx1 = _empty(N, H, W, Cin - split, device=dev)
     L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, split, dx0.data_ptr(),
-           dx1.data_ptr(), s)
+           dx1.data_ptr(), None, s)
     return dx0, dx1
+
+
+def _conv_backward_tee32(out: ConvBNOut, dzf, conv, dw, split):
+    """fp32 backward with materialised operands: the input-gradient kernel tees dz (BN+ReLU backward
+    applied) as it stages it, and the weight gradient multiplies that with the operand the forward
+    teed — both RAW frames, so its staging is a plain copy."""
+    s = L.stream()
+    lb = L.lib()
+    N, H, W, Cout = out.z.shape
+    dev = out.z.device
+    Cin = conv.in_channels
+    wp = pack_weights(conv.weight, dgrad=True)
+    dzt = _empty(N, H, W, Cout, device=dev)
+    if split is None:
+        dx = _empty(N, H, W, Cin, device=dev)
+        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, Cin, dx.data_ptr(), None,
+               dzt.data_ptr(), s)
+        res = dx
+    else:
+        dx0 = _empty(N, H, W, split, device=dev)
+        dx1 = _empty(N, H, W, Cin - split, device=dev)
+        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, split, dx0.data_ptr(),
+               dx1.data_ptr(), dzt.data_ptr(), s)
+        res = (dx0, dx1)
+    wsb = lb.pmu_conv3x3_wgrad_ws(N, H, W, Cin, Cout)
+    ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+    L.call("pmu_conv3x3_wgrad", frame_of([Src(dzt)], N, H, W), frame_of([Src(out.xt32)], N, H, W), Cout,
+           dw.data_ptr(), ws.data_ptr(), wsb, s)
+    out.xt32 = None
+    return res
 
 
 def _pad8(c: int) -> int:

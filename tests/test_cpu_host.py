@@ -170,7 +170,7 @@ def test_library_rejects_bad_arguments_without_gpu():
     if not os.path.exists(LIB_PATH):
         pytest.skip("library not built")
     cdll = load_library()
-    assert cdll.pmu_conv3x3_fwd(None, None, None, None, 0, None, None, None) == PMU_ERR_ARG
+    assert cdll.pmu_conv3x3_fwd(None, None, None, None, 0, None, None, None, None) == PMU_ERR_ARG
     assert cdll.pmu_sgd_clip(None, 0, None, ctypes.c_float(1), ctypes.c_float(1), ctypes.c_float(0.9),
                              ctypes.c_float(0.1), None) == PMU_ERR_ARG
     assert cdll.pmu_conv3x3_tiles(32, 256, 256) == 32 * 32 * 8

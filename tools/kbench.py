@@ -94,6 +94,8 @@ def main():
         wrf = packr(w, False)
         partr = torch.empty(L.lib().pmu_conv3x3_tiles_raw(N, H, W, Cout), 2 * Cout, device=dev)
         wrd = packr(w, True)
+        xt32 = torch.empty(N, H, W, Cin, device=dev)
+        dzt32 = torch.empty(N, H, W, Cout, device=dev)
         ops = {
             "fwd_raw": lambda: L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), cpi, N, H, W, wrf.data_ptr(), b.data_ptr(),
                                       Cout, out.data_ptr(), partr.data_ptr(), s),
@@ -108,9 +110,15 @@ def main():
             "dgrad_bf16": lambda: L.call("pmu_conv3x3_dgrad_bf16", fdz, wbd.data_ptr(), Cin, Cin, dx.data_ptr(),
                                          None, dzt.data_ptr(), s),
             "fwd": lambda: L.call("pmu_conv3x3_fwd", fin, w.data_ptr(), L.ptr(wpf), b.data_ptr(), Cout,
-                                  out.data_ptr(), part.data_ptr(), s),
+                                  out.data_ptr(), part.data_ptr(), None, s),
             "dgrad": lambda: L.call("pmu_conv3x3_dgrad", fdz, w.data_ptr(), L.ptr(wpd), Cin, Cin, dx.data_ptr(),
-                                    None, s),
+                                    None, None, s),
+            "fwd_tee": lambda: L.call("pmu_conv3x3_fwd", fin, w.data_ptr(), L.ptr(wpf), b.data_ptr(), Cout,
+                                      out.data_ptr(), part.data_ptr(), xt32.data_ptr(), s),
+            "dgrad_tee": lambda: L.call("pmu_conv3x3_dgrad", fdz, w.data_ptr(), L.ptr(wpd), Cin, Cin, dx.data_ptr(),
+                                        None, dzt32.data_ptr(), s),
+            "wgrad_t32": lambda: L.call("pmu_conv3x3_wgrad", frame_of([Src(dzt32)], N, H, W),
+                                        frame_of([Src(xt32)], N, H, W), Cout, dw.data_ptr(), ws.data_ptr(), wsb, s),
             "pack": lambda: pack_weights(w, False),
             "wgrad": lambda: L.call("pmu_conv3x3_wgrad", fdz, fin, Cout, dw.data_ptr(), ws.data_ptr(), wsb, s),
         }
