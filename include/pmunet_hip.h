@@ -97,6 +97,20 @@ size_t pmu_conv3x3_wgrad_ws(int N, int H, int W, int Cin, int Cout);
 int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int Cout, float* dw,
                       float* ws, size_t ws_bytes, void* stream);
 
+/* ---- fp32 Winograd F(2x2,3x3) variant (the c2 fp32 path) ------------------------------
+ * The same operators as pmu_conv3x3_fwd / _dgrad in fp32, computed as 16 per-component GEMMs of
+ * transformed operands (B^T d B) and weights (G g G^T), output A^T M A: fp32 rounding differs from
+ * the direct sum by ~1e-6 relative.  Weights pre-transformed by pmu_conv3x3_pack_wino ([32 output
+ * rows][16 channels] blocks); part rows = pmu_conv3x3_tiles_wino() (16 x 16 pixel tiles); tee as
+ * pmu_conv3x3_fwd / _dgrad. */
+size_t pmu_conv3x3_packed_size_wino(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_wino(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream);
+int pmu_conv3x3_tiles_wino(int N, int H, int W);
+int pmu_conv3x3_fwd_wino(const pmu_frame* in, const float* wp, const float* bias, int Cout, float* z,
+                         float* part, float* tee, void* stream);
+int pmu_conv3x3_dgrad_wino(const pmu_frame* dz, const float* wp, int Cin, int Csplit, float* dx0, float* dx1,
+                           float* tee, void* stream);
+
 /* ---- bf16-MFMA variants (config c5, BASELINE.json configs[4]: "... bf16") --------------
  * torch.autocast(bfloat16) arithmetic for the same operators: the operand (after the fused fp32
  * BN/ReLU/pool/concat transform) and the weights are rounded to bf16 (RNE), products are summed in

@@ -1,0 +1,477 @@
+// 3x3 / pad 1 convolution in fp32 by Winograd F(2x2, 3x3) on f32 MFMA (the forward of nn.Conv2d at
+// PMU/model/unet/unet_parts.py:15,18 and its input gradient), the c2 headline path.
+//
+// Every 2x2 block of output pixels ("Winograd tile") is computed from the 4x4 operand patch d around
+// it as  Y = A^T [ (G g G^T) .* (B^T d B) ] A : 16 element-wise products per input/output channel
+// pair instead of 36, i.e. the reduction over input channels becomes 16 independent GEMMs
+// ("components") of  M[comp][tile][co] = sum_ci V[comp][tile][ci] * U[comp][ci][co].
+// All arithmetic is fp32 (transforms with coefficients 0, +-1, +-1/2); the result differs from the
+// direct sum only by fp32 rounding (~1e-6 relative), far inside the 1e-3 parity bound.
+//
+// Block: 512 threads, 64 tiles (8 x 8 -> a 16 x 16 output patch) x 32 output channels.  Wave w owns
+// 16 tiles (tile group w & 3) x 16 output channels (half w >> 2) for all 16 components: acc[16] of
+// v_mfma_f32_16x16x4_f32 (64 accumulator registers), so the output transform of each (tile, channel)
+// is local to its lane, and two waves share each SIMD.  Per chunk of 16 input channels:
+//   * the 18 x 18 x 16 operand halo is staged into LDS through the shared frame staging (BN+ReLU,
+//     max-pool, F.pad + concat, or BN+ReLU backward applied on the fly, pmu_stage.h);
+//   * U (pre-transformed weights, 16 comps x 16 ch x 32 co) is copied into LDS;
+//   * per 4-channel MFMA step each lane reads its tile's 4 x 4 patch for one channel (ds_read_b64 of
+//     two channels serve two steps; conflict-free through the padded row pitch), forms the 16
+//     components of B^T d B in registers and issues 16 MFMAs with U fragments read as ds_read_b128
+//     (4 components per read).
+// Epilogue: A^T M A per lane (+bias), BN partial sums per block (fwd), or the split dx store (dgrad).
+#include <string.h>
+#include <stdlib.h>
+#include "pmu_stage.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TX = 8, TY = 8;             // Winograd tiles per block
+constexpr int OW = 2 * TX, OH = 2 * TY;   // 16 x 16 output pixels
+constexpr int HW = OW + 2, HH = OH + 2;   // 18 x 18 halo
+constexpr int BK = 16;                    // input channels per chunk
+constexpr int LS = BK + 4;                // LDS floats per halo pixel
+constexpr int ROWP = HW * LS + 2;         // halo row pitch: tile-row step 2*ROWP = 20 (mod 64) -> b64 patch reads conflict-free
+constexpr int A_FLOATS = HH * ROWP;
+constexpr int CO = 32;                    // output channels per block
+constexpr int U_FLOATS = BK * 16 * CO;    // one chunk of transformed weights
+constexpr int NT = 512;                   // 8 waves: 4 tile groups x 2 channel halves
+constexpr int NI = 3;                     // halo items per thread: ceil(324 * 4 / 512)
+
+struct WinoArgs {
+  DevFrame in;
+  const float* wp;    // packed U [co block][chunk][ch 16][comp group 4][co 32][comp 4]
+  const float* bias;
+  float* out0;
+  float* out1;
+  float* part;        // [spatial tiles][2][NOUT] BN partial sums (fwd) or null
+  float* tee;         // [N][H][W][KC] copy of the staged operand or null
+  int NOUT, KC, split, tiles_w, tiles_h, nco;
+};
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// U = G g G^T for F(2x2, 3x3), G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]; one thread per
+// (co block, chunk, channel, co) writes its 16 components as 4 float4 (component groups)
+__global__ void pack_wino_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, float* __restrict__ wp) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  const int nch = (KC + BK - 1) / BK, ncob = (NOUT + CO - 1) / CO;
+  const long long total = (long long)ncob * nch * BK * CO;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int col = (int)(e % CO);
+    long long r = e / CO;
+    const int kl = (int)(r % BK); r /= BK;
+    const int ch = (int)(r % nch);
+    const int jb = (int)(r / nch);
+    const int j = jb * CO + col, k = ch * BK + kl;
+    float g[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        float v = 0.f;
+        if (j < NOUT && k < KC)  // dgrad: the input gradient convolves dz with w[co][ci] rotated by 180 degrees
+          v = dgrad ? w[((long long)k * Cin + j) * 9 + (2 - a) * 3 + (2 - b)] : w[((long long)j * Cin + k) * 9 + a * 3 + b];
+        g[a][b] = v;
+      }
+    float t[4][3];  // G g
+    for (int b = 0; b < 3; ++b) {
+      t[0][b] = g[0][b];
+      t[1][b] = 0.5f * (g[0][b] + g[1][b] + g[2][b]);
+      t[2][b] = 0.5f * (g[0][b] - g[1][b] + g[2][b]);
+      t[3][b] = g[2][b];
+    }
+    float u[16];  // (G g) G^T
+    for (int a = 0; a < 4; ++a) {
+      u[4 * a + 0] = t[a][0];
+      u[4 * a + 1] = 0.5f * (t[a][0] + t[a][1] + t[a][2]);
+      u[4 * a + 2] = 0.5f * (t[a][0] - t[a][1] + t[a][2]);
+      u[4 * a + 3] = t[a][2];
+    }
+    float* dst = wp + ((long long)jb * nch + ch) * U_FLOATS;
+    for (int gq = 0; gq < 4; ++gq)
+      *reinterpret_cast<float4*>(dst + ((kl * 4 + gq) * CO + col) * 4) =
+          make_float4(u[4 * gq], u[4 * gq + 1], u[4 * gq + 2], u[4 * gq + 3]);
+  }
+}
+
+// V = B^T d B, B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]; v[4i + k]
+__device__ __forceinline__ void input_transform(const float (&d)[4][4], float (&v)[16]) {
+  float t[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t[0][j] = d[0][j] - d[2][j];
+    t[1][j] = d[1][j] + d[2][j];
+    t[2][j] = d[2][j] - d[1][j];
+    t[3][j] = d[1][j] - d[3][j];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[4 * i + 0] = t[i][0] - t[i][2];
+    v[4 * i + 1] = t[i][1] + t[i][2];
+    v[4 * i + 2] = t[i][2] - t[i][1];
+    v[4 * i + 3] = t[i][1] - t[i][3];
+  }
+}
+
+// One chunk (16 channels) of MFMAs: per 4-channel step each lane reads its tile's 4x4 patch for one
+// channel, transforms it, and issues 16 components x 2 channel halves of 16x16x4 MFMAs.  The next
+// step's patch and U fragments are loaded before this step's MFMAs (sched_barrier keeps the order).
+// MFMA k-slot -> channel: in step ks a lane of k-group kk (= lane >> 4) multiplies channel
+// 8*(ks>>1) + 2*kk + (ks&1), so one ds_read_b64 per patch element serves two steps.
+__device__ __forceinline__ int wino_chan(int ks, int kk) { return 8 * (ks >> 1) + 2 * kk + (ks & 1); }
+
+// the 4x4 patch of this lane's tile for a pair of steps (two adjacent channels per element)
+__device__ __forceinline__ void wino_load_patch(const float* As, int pbase, int kp, float2 (&d)[16]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[4 * i + j] = *reinterpret_cast<const float2*>(As + pbase + i * ROWP + j * LS + 8 * kp);
+}
+// U fragments of one step: 16 components (4 x b128) for this lane's channel and output channel
+__device__ __forceinline__ void wino_load_u(const float* Us, int ubase, int ks, int kk, float4 (&u)[4]) {
+  const float* up = Us + ubase + wino_chan(ks, kk) * 4 * CO * 4;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) u[g] = *reinterpret_cast<const float4*>(up + g * CO * 4);
+}
+
+__device__ __forceinline__ void wino_mfmas(const float2 (&dp)[16], bool hi, const float4 (&u)[4], f32x4 (&acc)[16]) {
+  float dd[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dd[i][j] = hi ? dp[4 * i + j].y : dp[4 * i + j].x;
+  float v[16];
+  input_transform(dd, v);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    acc[4 * g + 0] = mfma16(v[4 * g + 0], u[g].x, acc[4 * g + 0]);
+    acc[4 * g + 1] = mfma16(v[4 * g + 1], u[g].y, acc[4 * g + 1]);
+    acc[4 * g + 2] = mfma16(v[4 * g + 2], u[g].z, acc[4 * g + 2]);
+    acc[4 * g + 3] = mfma16(v[4 * g + 3], u[g].w, acc[4 * g + 3]);
+  }
+}
+
+// One chunk (16 channels, 4 steps of 16 MFMAs per wave); the next step's operands are read before
+// this step's MFMAs (sched_barrier keeps the order).
+__device__ __forceinline__ void wino_chunk(const float* As, const float* Us, int pbase, int ubase, int kk,
+                                           f32x4 (&acc)[16]) {
+  float2 dp[2][16];
+  float4 u[2][4];
+  wino_load_patch(As, pbase, 0, dp[0]);
+  wino_load_u(Us, ubase, 0, kk, u[0]);
+#pragma unroll
+  for (int ks = 0; ks < BK / 4; ++ks) {
+    if (ks + 1 < BK / 4) {
+      if (((ks + 1) & 1) == 0) wino_load_patch(As, pbase, (ks + 1) >> 1, dp[((ks + 1) >> 1) & 1]);
+      wino_load_u(Us, ubase, ks + 1, kk, u[(ks + 1) & 1]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    wino_mfmas(dp[(ks >> 1) & 1], ks & 1, u[ks & 1], acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// the operand for the weight gradient: the chunk's interior 16 x 16 pixels x 16 channels
+__device__ __forceinline__ void wino_tee(const WinoArgs& a, const float* As, int k0, int n, int h0, int w0, int tid) {
+  const DevFrame& F = a.in;
+#pragma unroll
+  for (int i = 0; i < 1024 / NT; ++i) {
+    const int u = tid + NT * i;
+    const int q = u >> 2, qq = u & 3;
+    const int r = q >> 4, c = q & 15;
+    const int h = h0 + r, w = w0 + c, kc = k0 + 4 * qq;
+    if (h < F.H && w < F.W && kc < a.KC)
+      *reinterpret_cast<float4*>(a.tee + (((long long)n * F.H + h) * F.W + w) * a.KC + kc) =
+          *reinterpret_cast<const float4*>(As + (r + 1) * ROWP + (c + 1) * LS + 4 * qq);
+  }
+}
+
+// block geometry shared by both kernels
+struct WinoGeo {
+  int cob_blk, spatial, n, h0, w0, j0, tg, hh, kk, pbase, ubase;
+};
+__device__ __forceinline__ WinoGeo wino_geo(const WinoArgs& a) {
+  WinoGeo g;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  g.cob_blk = blockIdx.x % a.nco;
+  int sp = blockIdx.x / a.nco;
+  g.spatial = sp;
+  const int tw = sp % a.tiles_w; sp /= a.tiles_w;
+  const int th = sp % a.tiles_h; sp /= a.tiles_h;
+  g.n = sp;
+  g.h0 = th * OH; g.w0 = tw * OW;
+  g.j0 = g.cob_blk * CO;
+  g.tg = wave & 3;   // tiles 16*tg .. 16*tg+15 (tile rows 2tg, 2tg+1)
+  g.hh = wave >> 2;  // output channels j0 + 16*hh .. +15
+  g.kk = lane >> 4;
+  const int lt = 16 * g.tg + (lane & 15);
+  g.pbase = (2 * (lt >> 3)) * ROWP + (2 * (lt & 7)) * LS + 2 * g.kk;
+  g.ubase = (g.hh * 16 + (lane & 15)) * 4;
+  return g;
+}
+
+__device__ __forceinline__ void wino_items(const WinoGeo& g, int (&ih)[NI], int (&iw)[NI], int (&dst)[NI]) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int it = threadIdx.x + NT * i;
+    const int hp = it >> 2;
+    const int hr = hp / HW, hc = hp - hr * HW;
+    ih[i] = (it < HH * HW * 4) ? g.h0 - 1 + hr : PMU_NO_ITEM;
+    iw[i] = g.w0 - 1 + hc;
+    dst[i] = hr * ROWP + hc * LS + 4 * (it & 3);
+  }
+}
+
+// epilogue: lane holds M[comp][tile 16*tg + 4*(lane>>4) + r][output channel j0 + 16*hh + (lane&15)]
+template <bool DGRAD>
+__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, const WinoGeo& g, f32x4 (&acc)[16], float* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const DevFrame& F = a.in;
+  const int j = g.j0 + 16 * g.hh + (lane & 15);
+  const bool jok = j < a.NOUT;
+  const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int t = 16 * g.tg + 4 * (lane >> 4) + r;
+    const int oh = g.h0 + 2 * (t >> 3), ow = g.w0 + 2 * (t & 7);
+    float m[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) m[c] = acc[c][r];
+    // Y = A^T M A, A^T = [1 1 1 0; 0 1 -1 -1]
+    float sr[2][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sr[0][k] = m[k] + m[4 + k] + m[8 + k];
+      sr[1][k] = m[4 + k] - m[8 + k] - m[12 + k];
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float y0 = sr[p][0] + sr[p][1] + sr[p][2] + b;
+      const float y1 = sr[p][1] - sr[p][2] - sr[p][3] + b;
+      const int hh = oh + p;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ww = ow + q;
+        const float y = q ? y1 : y0;
+        if (!jok || hh >= F.H || ww >= F.W) continue;
+        const long long pix = ((long long)g.n * F.H + hh) * F.W + ww;
+        if (!DGRAD) {
+          a.out0[pix * a.NOUT + j] = y;
+          s1 += y;
+          s2 = fmaf(y, y, s2);
+        } else if (j < a.split) {
+          a.out0[pix * a.split + j] = y;
+        } else {
+          a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = y;
+        }
+      }
+    }
+  }
+  if (!DGRAD && a.part) {
+    float* red = smem;  // [8 waves][16][2]; the last chunk's barrier freed the stage
+    s1 += __shfl_xor(s1, 16, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (lane < 16) {
+      red[(wave * 16 + lane) * 2 + 0] = s1;
+      red[(wave * 16 + lane) * 2 + 1] = s2;
+    }
+    __syncthreads();
+    if (tid < CO) {  // channel tid: half tid >> 4, summed over the 4 tile groups (waves 4*half + tg)
+      const int jj = g.j0 + tid, hf = tid >> 4, l = tid & 15;
+      if (jj < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int tg = 0; tg < 4; ++tg) {
+          t1 += red[((4 * hf + tg) * 16 + l) * 2 + 0];
+          t2 += red[((4 * hf + tg) * 16 + l) * 2 + 1];
+        }
+        a.part[((long long)g.spatial * 2 + 0) * a.NOUT + jj] = t1;
+        a.part[((long long)g.spatial * 2 + 1) * a.NOUT + jj] = t2;
+      }
+    }
+  }
+}
+
+// synchronous staging (any frame): stage, barrier, MFMAs, barrier
+template <bool DGRAD>
+__global__ __launch_bounds__(NT, 1) void conv3x3_wino_kernel(WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[A_FLOATS + U_FLOATS];
+  float* As = smem;
+  float* Us = smem + A_FLOATS;
+  const int tid = threadIdx.x;
+  const WinoGeo g = wino_geo(a);
+  const DevFrame& F = a.in;
+  const int nchunks = (a.KC + BK - 1) / BK;
+  int ih[NI], iw[NI], dst[NI];
+  wino_items(g, ih, iw, dst);
+  f32x4 acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float4* wsrc = reinterpret_cast<const float4*>(a.wp + (long long)g.cob_blk * nchunks * U_FLOATS);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int k0 = ch * BK;
+#pragma unroll 1
+    for (int i = 0; i < NI; ++i)  // generic staging: this kernel takes the frames the pipelined one does not
+      if (ih[i] != PMU_NO_ITEM) *reinterpret_cast<float4*>(As + dst[i]) = frame_value4(F, g.n, ih[i], iw[i], k0 + 4 * (tid & 3));
+    {
+      const float4* s = wsrc + (long long)ch * (U_FLOATS / 4);
+#pragma unroll
+      for (int r = 0; r < U_FLOATS / 4 / NT; ++r) reinterpret_cast<float4*>(Us)[tid + NT * r] = s[tid + NT * r];
+    }
+    __syncthreads();
+    if (a.tee && g.cob_blk == 0) wino_tee(a, As, k0, g.n, g.h0, g.w0, tid);
+    wino_chunk(As, Us, g.pbase, g.ubase, g.kk, acc);
+    __syncthreads();
+  }
+  wino_epilogue<DGRAD>(a, g, acc, smem);
+}
+
+// Software-pipelined variant (the default for fast-path frames): the next chunk's operand items and
+// U tile are loaded into registers before this chunk's MFMAs and written to the other LDS stage after
+// them — one barrier per chunk; 1 block (8 waves, 2 per SIMD) per CU, 118 KB LDS.
+constexpr int STAGE = A_FLOATS + U_FLOATS;
+static_assert(U_FLOATS / 4 / NT == 4, "4 U float4 per thread per chunk");
+
+template <bool DGRAD, int POOL>
+__global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x;
+  const WinoGeo g = wino_geo(a);
+  const DevFrame& F = a.in;
+  const int nchunks = (a.KC + BK - 1) / BK;
+  const int cq4 = 4 * (tid & 3);
+  int ih[NI], iw[NI], dst[NI];
+  wino_items(g, ih, iw, dst);
+  f32x4 acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  PmuPref<POOL, DGRAD, NI> pf;
+  float4 pb0, pb1, pb2, pb3;  // plain locals: an array here is kept in scratch
+  const float4* wsrc = reinterpret_cast<const float4*>(a.wp + (long long)g.cob_blk * nchunks * U_FLOATS) + tid;
+#define PMU_WPREFETCH(CH)                                                                                   \
+  {                                                                                                        \
+    const int k0_ = (CH) * BK;                                                                             \
+    const bool second_ = F.nsrc > 1 && k0_ >= F.C0;                                                        \
+    pmu_prefetch<POOL, DGRAD, NI>(pmu_pick_src(F, second_), k0_ - (second_ ? F.C0 : 0) + cq4, g.n, ih, iw, pf); \
+    const float4* s_ = wsrc + (long long)(CH) * (U_FLOATS / 4);                                            \
+    pb0 = s_[0]; pb1 = s_[NT]; pb2 = s_[2 * NT]; pb3 = s_[3 * NT];                                         \
+  }
+#define PMU_WCOMMIT(BUF)                                                                                    \
+  {                                                                                                        \
+    pmu_commit<POOL, DGRAD, NI>(pf, ih, dst, (BUF));                                                       \
+    float4* u_ = reinterpret_cast<float4*>((BUF) + A_FLOATS) + tid;                                        \
+    u_[0] = pb0; u_[NT] = pb1; u_[2 * NT] = pb2; u_[3 * NT] = pb3;                                         \
+  }
+  PMU_WPREFETCH(0)
+  PMU_WCOMMIT(smem)
+  __syncthreads();
+  for (int ch = 0; ch < nchunks; ++ch) {
+    float* cur = smem + (ch & 1) * STAGE;
+    if (ch + 1 < nchunks) PMU_WPREFETCH(ch + 1)
+    if (a.tee && g.cob_blk == 0) wino_tee(a, cur, ch * BK, g.n, g.h0, g.w0, tid);
+    wino_chunk(cur, cur + A_FLOATS, g.pbase, g.ubase, g.kk, acc);
+    if (ch + 1 < nchunks) PMU_WCOMMIT(smem + ((ch + 1) & 1) * STAGE)
+    __syncthreads();
+  }
+#undef PMU_WPREFETCH
+#undef PMU_WCOMMIT
+  wino_epilogue<DGRAD>(a, g, acc, smem);
+}
+
+// a source the pipelined staging takes: float4 channels, chunks never straddle sources
+static bool wino_pipe_src_ok(const pmu_src& s) {
+  if (s.C % BK != 0) return false;
+  if (s.pool == PMU_POOL_NONE) return true;
+  return s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU;
+}
+
+static bool wino_sync_forced() {
+  static const bool v = [] {
+    const char* e = getenv("PMU_WINO_IMPL");
+    return e && strcmp(e, "sync") == 0;
+  }();
+  return v;
+}
+
+int launch_wino(const pmu_frame* in, const float* wp, const float* bias, int NOUT, int KC, float* out0, float* out1,
+                int split, float* part, float* tee, bool dgrad, void* stream) {
+  WinoArgs a;
+  a.in = make_dev_frame(in);
+  a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part; a.tee = tee;
+  a.NOUT = NOUT; a.KC = KC; a.split = split;
+  a.tiles_w = pmu_cdiv(in->W, OW);
+  a.tiles_h = pmu_cdiv(in->H, OH);
+  a.nco = pmu_cdiv(NOUT, CO);
+  const long long blocks = (long long)a.nco * a.tiles_w * a.tiles_h * in->N;
+  PMU_REQUIRE(blocks < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)blocks);
+  if (!wino_sync_forced()) {
+    const pmu_src& s0 = in->src[0];
+    const bool two = in->nsrc > 1;
+    const bool ok = wino_pipe_src_ok(s0) && (!two || wino_pipe_src_ok(in->src[1]));
+    const int pool = s0.pool;
+    const bool same_pool = !two || in->src[1].pool == pool;
+    const bool modes_ok = dgrad ? (!two && s0.mode == PMU_SRC_BNBWD)
+                                : (s0.mode != PMU_SRC_BNBWD && (!two || in->src[1].mode != PMU_SRC_BNBWD));
+    if (ok && same_pool && modes_ok) {
+      if (dgrad && pool == PMU_POOL_NONE)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<true, PMU_POOL_NONE>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_NONE)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_MAX2)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_MAX2>), grid, dim3(NT), 0, st, a);
+      else
+        goto sync;
+      PMU_CHECK_LAUNCH();
+      return PMU_OK;
+    }
+  }
+sync:
+  if (dgrad) hipLaunchKernelGGL((conv3x3_wino_kernel<true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino_kernel<false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+}  // namespace
+
+extern "C" int pmu_conv3x3_tiles_wino(int N, int H, int W) { return N * pmu_cdiv(H, OH) * pmu_cdiv(W, OW); }
+
+extern "C" size_t pmu_conv3x3_packed_size_wino(int Cout, int Cin, int dgrad) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  return (size_t)pmu_cdiv(NOUT, CO) * pmu_cdiv(KC, BK) * U_FLOATS * sizeof(float);
+}
+
+extern "C" int pmu_conv3x3_pack_wino(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream) {
+  PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
+  const long long total = (long long)pmu_conv3x3_packed_size_wino(Cout, Cin, dgrad) / sizeof(float) / 16;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(pack_wino_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_conv3x3_fwd_wino(const pmu_frame* in, const float* wp, const float* bias, int Cout, float* z,
+                                    float* part, float* tee, void* stream) {
+  PMU_REQUIRE(valid_frame(in) && wp && z && Cout > 0);
+  const int Cin = in->src[0].C + (in->nsrc > 1 ? in->src[1].C : 0);
+  PMU_REQUIRE(!tee || Cin % 4 == 0);
+  return launch_wino(in, wp, bias, Cout, Cin, z, nullptr, Cout, part, tee, false, stream);
+}
+
+extern "C" int pmu_conv3x3_dgrad_wino(const pmu_frame* dz, const float* wp, int Cin, int Csplit, float* dx0, float* dx1,
+                                      float* tee, void* stream) {
+  PMU_REQUIRE(valid_frame(dz) && dz->nsrc == 1 && wp && dx0 && Cin > 0);
+  PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
+  const int Cout = dz->src[0].C;
+  PMU_REQUIRE(!tee || Cout % 4 == 0);
+  return launch_wino(dz, wp, nullptr, Cin, Cout, dx0, dx1, Csplit, nullptr, tee, true, stream);
+}

@@ -13,6 +13,7 @@ Reference call graph mirrored here (PMU/ = Probabilistic-Multiplanar-Unet/):
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -212,14 +213,21 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             L.call("pmu_conv3x3_fwd_bf16", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout,
                    z.data_ptr(), L.ptr(part), L.ptr(xt), s)
     else:
-        R = lb.pmu_conv3x3_tiles(N, H, W)
-        part = _empty(R, 2 * Cout, device=dev) if need_stats else None
-        wp = pack_weights(conv.weight, dgrad=False)
         Cin = sum(sr.C for sr in srcs)
         # the weight gradient reads the operand the kernel staged (RAW) instead of re-deriving it
         xt32 = _empty(N, H, W, Cin, device=dev) if keep and tee32_ok(Cin, Cout) else None
-        L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), wp.data_ptr(), L.ptr(conv.bias),
-               Cout, z.data_ptr(), L.ptr(part), L.ptr(xt32), s)
+        if use_wino():
+            R = lb.pmu_conv3x3_tiles_wino(N, H, W)
+            part = _empty(R, 2 * Cout, device=dev) if need_stats else None
+            wp = pack_weights_wino(conv.weight, dgrad=False)
+            L.call("pmu_conv3x3_fwd_wino", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout,
+                   z.data_ptr(), L.ptr(part), L.ptr(xt32), s)
+        else:
+            R = lb.pmu_conv3x3_tiles(N, H, W)
+            part = _empty(R, 2 * Cout, device=dev) if need_stats else None
+            wp = pack_weights(conv.weight, dgrad=False)
+            L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), wp.data_ptr(),
+                   L.ptr(conv.bias), Cout, z.data_ptr(), L.ptr(part), L.ptr(xt32), s)
     st = bn_forward(part, R, Cout, N * H * W, bn, training, dev)
     bfl = bf16 and planes is None
     return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes, bf16=bfl, xt=xt if bfl else None,
@@ -262,18 +270,25 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
         L.call("pmu_conv3x3_wgrad", dzf, frame_of(out.srcs, N, H, W), Cout, dw.data_ptr(), ws.data_ptr(), wsb, s)
     if not need_dx or out.planes is not None:
         return None
+    return _dgrad32(dzf, conv, N, H, W, split, None)
+
+
+def _dgrad32(dzf, conv, N, H, W, split, tee):
+    """fp32 input gradient of a 3x3 conv (Winograd or direct); dx, or (dx0, dx1) split at ``split``."""
+    s = L.stream()
+    dev = conv.weight.device
     Cin = conv.in_channels
-    wp = pack_weights(conv.weight, dgrad=True)
-    if split is None:
-        dx = _empty(N, H, W, Cin, device=dev)
-        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, Cin, dx.data_ptr(), None,
-               None, s)
-        return dx
-    dx0 = _empty(N, H, W, split, device=dev)
-    dx1 = _empty(N, H, W, Cin - split, device=dev)
-    L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, split, dx0.data_ptr(),
-           dx1.data_ptr(), None, s)
-    return dx0, dx1
+    sp = Cin if split is None else split
+    dx0 = _empty(N, H, W, sp, device=dev)
+    dx1 = _empty(N, H, W, Cin - sp, device=dev) if split is not None else None
+    if use_wino():
+        wp = pack_weights_wino(conv.weight, dgrad=True)
+        L.call("pmu_conv3x3_dgrad_wino", dzf, wp.data_ptr(), Cin, sp, dx0.data_ptr(), L.ptr(dx1), L.ptr(tee), s)
+    else:
+        wp = pack_weights(conv.weight, dgrad=True)
+        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, sp, dx0.data_ptr(),
+               L.ptr(dx1), L.ptr(tee), s)
+    return dx0 if split is None else (dx0, dx1)
 
 
 def _conv_backward_tee32(out: ConvBNOut, dzf, conv, dw, split):
@@ -285,19 +300,8 @@ def _conv_backward_tee32(out: ConvBNOut, dzf, conv, dw, split):
     N, H, W, Cout = out.z.shape
     dev = out.z.device
     Cin = conv.in_channels
-    wp = pack_weights(conv.weight, dgrad=True)
     dzt = _empty(N, H, W, Cout, device=dev)
-    if split is None:
-        dx = _empty(N, H, W, Cin, device=dev)
-        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, Cin, dx.data_ptr(), None,
-               dzt.data_ptr(), s)
-        res = dx
-    else:
-        dx0 = _empty(N, H, W, split, device=dev)
-        dx1 = _empty(N, H, W, Cin - split, device=dev)
-        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, split, dx0.data_ptr(),
-               dx1.data_ptr(), dzt.data_ptr(), s)
-        res = (dx0, dx1)
+    res = _dgrad32(dzf, conv, N, H, W, split, dzt)
     wsb = lb.pmu_conv3x3_wgrad_ws(N, H, W, Cin, Cout)
     ws = _empty(max(1, (wsb + 3) // 4), device=dev)
     L.call("pmu_conv3x3_wgrad", frame_of([Src(dzt)], N, H, W), frame_of([Src(out.xt32)], N, H, W), Cout,
@@ -372,6 +376,20 @@ def pack_weights_bf16(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     wp = torch.empty(n, dtype=torch.int16, device=w.device)
     L.call("pmu_conv3x3_pack_bf16", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
     return wp
+
+
+def pack_weights_wino(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """Winograd-transformed weights U = G g G^T in the fp32 Winograd kernel's blocks (pmu_conv3x3_pack_wino)."""
+    Cout, Cin = w.shape[0], w.shape[1]
+    n = L.lib().pmu_conv3x3_packed_size_wino(Cout, Cin, int(dgrad)) // 4
+    wp = _empty(n, device=w.device)
+    L.call("pmu_conv3x3_pack_wino", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
+def use_wino() -> bool:
+    """fp32 3x3 convs (fwd and input gradient) by Winograd F(2x2,3x3) (PMU_FP32_CONV=direct: direct sum)."""
+    return os.environ.get("PMU_FP32_CONV", "wino") != "direct"
 
 
 def pack_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:

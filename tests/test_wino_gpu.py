@@ -1,0 +1,108 @@
+"""GPU parity of the fp32 Winograd F(2x2,3x3) conv kernels (pmu_conv3x3_fwd_wino / _dgrad_wino).
+
+Reference: the same operand (pmu_frame_to_f32 of the frame: BN+ReLU, max-pool, F.pad+cat, or the
+BN+ReLU backward of dz) convolved in fp64 on the CPU.  Winograd's fp32 transforms round differently
+from a direct sum: tolerance max|d| / max|ref| <= 2e-5 (the model-level bound is 1e-3).
+"""
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _to_f32(srcs, N, H, W):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import frame_of
+    C = sum(sr.C for sr in srcs)
+    out = torch.empty(N, H, W, C, device=srcs[0].x.device)
+    L.call("pmu_frame_to_f32", frame_of(srcs, N, H, W), out.data_ptr(), L.stream())
+    return out
+
+
+def _coef(C, g, dev):
+    return torch.cat([torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.2]).to(dev)
+
+
+def _frame(kind, N, H, W, C, g, dev):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    if kind == "raw":
+        return [Src(torch.randn(N, H, W, C, generator=g).to(dev))]
+    if kind == "bnrelu":
+        return [Src(torch.randn(N, H, W, C, generator=g).to(dev), L.SRC_BNRELU, _coef(C, g, dev))]
+    if kind == "maxpool":
+        return [Src(torch.randn(N, 2 * H + 1, 2 * W, C, generator=g).to(dev), L.SRC_BNRELU, _coef(C, g, dev),
+                    pool=L.POOL_MAX2)]
+    if kind == "concat":
+        c0 = C // 2
+        z = torch.randn(N, H, W, c0, generator=g).to(dev)
+        u = torch.randn(N, H - 1, W - 2, C - c0, generator=g).to(dev)
+        return [Src(z, L.SRC_BNRELU, _coef(c0, g, dev)), Src(u, off=(0, 1))]
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind,N,H,W,Cin,Cout", [("bnrelu", 2, 32, 32, 64, 64), ("raw", 1, 37, 45, 20, 40),
+                                                 ("maxpool", 2, 24, 20, 64, 128), ("concat", 2, 33, 17, 128, 64),
+                                                 ("bnrelu", 3, 16, 16, 512, 96), ("raw", 1, 7, 9, 6, 10)])
+def test_conv3x3_fwd_wino(dev, kind, N, H, W, Cin, Cout):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import frame_of, pack_weights_wino
+    g = torch.Generator().manual_seed(31 + H + Cin)
+    srcs = _frame(kind, N, H, W, Cin, g, dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    z = torch.empty(N, H, W, Cout, device=dev)
+    R = L.lib().pmu_conv3x3_tiles_wino(N, H, W)
+    part = torch.empty(R, 2 * Cout, device=dev)
+    tee = torch.full((N, H, W, Cin), float("nan"), device=dev) if Cin % 4 == 0 else None
+    wp = pack_weights_wino(w, False)
+    L.call("pmu_conv3x3_fwd_wino", frame_of(srcs, N, H, W), wp.data_ptr(), b.data_ptr(), Cout, z.data_ptr(),
+           part.data_ptr(), L.ptr(tee), L.stream())
+    torch.cuda.synchronize()
+    op = _to_f32(srcs, N, H, W)
+    if tee is not None:
+        assert torch.equal(tee, op)
+    ref = TF.conv2d(op.permute(0, 3, 1, 2).double().cpu(), w.double().cpu(), b.double().cpu(), padding=1)
+    ref = ref.permute(0, 2, 3, 1)
+    assert _rel(z, ref) <= TOL
+    # BN partials: per-tile sums over the pixels sum to the channel totals
+    tot = part.double().sum(0).cpu()
+    scale = ref.abs().sum((0, 1, 2))
+    assert float(((tot[:Cout] - ref.sum((0, 1, 2))).abs() / scale).max()) <= 1e-5
+    assert float(((tot[Cout:] - (ref * ref).sum((0, 1, 2))).abs() / (ref * ref).sum((0, 1, 2))).max()) <= 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 40, 36, 64, 64, 64), (2, 17, 33, 128, 64, 64),
+                                                  (1, 16, 16, 96, 128, 32), (2, 9, 7, 12, 20, 12)])
+def test_conv3x3_dgrad_wino(dev, N, H, W, Cin, Cout, split):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_of, pack_weights_wino
+    g = torch.Generator().manual_seed(7 + H + Cout)
+    da = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    z = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    bco = torch.cat([torch.rand(Cout, generator=g) + 0.5, torch.randn(Cout, generator=g) * 0.1,
+                     torch.randn(Cout, generator=g) * 0.1, torch.randn(Cout, generator=g) * 0.01,
+                     torch.randn(Cout, generator=g) * 0.01]).to(dev)
+    dsrc = [Src(da, L.SRC_BNBWD, bco, z=z)]
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    wp = pack_weights_wino(w, True)
+    dx0 = torch.empty(N, H, W, split, device=dev)
+    dx1 = torch.empty(N, H, W, Cin - split, device=dev) if split < Cin else None
+    dzt = torch.full((N, H, W, Cout), float("nan"), device=dev)
+    L.call("pmu_conv3x3_dgrad_wino", frame_of(dsrc, N, H, W), wp.data_ptr(), Cin, split, dx0.data_ptr(),
+           L.ptr(dx1), dzt.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    dz = _to_f32(dsrc, N, H, W)
+    assert torch.equal(dzt, dz)
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double().cpu(), dz.permute(0, 3, 1, 2).double().cpu(),
+                                     padding=1).permute(0, 2, 3, 1)
+    got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
+    assert _rel(got, ref) <= TOL

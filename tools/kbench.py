@@ -96,6 +96,9 @@ def main():
         wrd = packr(w, True)
         xt32 = torch.empty(N, H, W, Cin, device=dev)
         dzt32 = torch.empty(N, H, W, Cout, device=dev)
+        from pmu_hip.engine import pack_weights_wino
+        wwf, wwd = pack_weights_wino(w, False), pack_weights_wino(w, True)
+        partw = torch.empty(L.lib().pmu_conv3x3_tiles_wino(N, H, W), 2 * Cout, device=dev)
         ops = {
             "fwd_raw": lambda: L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), cpi, N, H, W, wrf.data_ptr(), b.data_ptr(),
                                       Cout, out.data_ptr(), partr.data_ptr(), s),
@@ -119,6 +122,10 @@ def main():
                                         None, dzt32.data_ptr(), s),
             "wgrad_t32": lambda: L.call("pmu_conv3x3_wgrad", frame_of([Src(dzt32)], N, H, W),
                                         frame_of([Src(xt32)], N, H, W), Cout, dw.data_ptr(), ws.data_ptr(), wsb, s),
+            "fwd_wino": lambda: L.call("pmu_conv3x3_fwd_wino", fin, wwf.data_ptr(), b.data_ptr(), Cout,
+                                       out.data_ptr(), partw.data_ptr(), None, s),
+            "dgrad_wino": lambda: L.call("pmu_conv3x3_dgrad_wino", fdz, wwd.data_ptr(), Cin, Cin, dx.data_ptr(),
+                                         None, None, s),
             "pack": lambda: pack_weights(w, False),
             "wgrad": lambda: L.call("pmu_conv3x3_wgrad", fdz, fin, Cout, dw.data_ptr(), ws.data_ptr(), wsb, s),
         }
