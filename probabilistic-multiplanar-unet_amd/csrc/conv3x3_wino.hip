@@ -123,18 +123,41 @@ __device__ __forceinline__ void input_transform(const float (&d)[4][4], float (&
 // 8*(ks>>1) + 2*kk + (ks&1), so one ds_read_b64 per patch element serves two steps.
 __device__ __forceinline__ int wino_chan(int ks, int kk) { return 8 * (ks >> 1) + 2 * kk + (ks & 1); }
 
-// the 4x4 patch of this lane's tile for a pair of steps (two adjacent channels per element)
-__device__ __forceinline__ void wino_load_patch(const float* As, int pbase, int kp, float2 (&d)[16]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d[4 * i + j] = *reinterpret_cast<const float2*>(As + pbase + i * ROWP + j * LS + 8 * kp);
+// LDS reads of the MFMA loop as explicit instructions: the patch reads must stay single ds_read_b64
+// (256 B/clk, conflict-free here; the compiler merges pairs into ds_read2_b64, which banks on 16-lane
+// groups mod 32 where the tiles' even pixel steps collide 2-way).  Being asm, the compiler inserts
+// no waits for them: wino_chunk waits (lgkmcnt(0)) at the top of each step, before issuing the next
+// step's reads, when the reads for this step — issued a whole step of MFMAs earlier — have landed.
+template <int OFF>
+__device__ __forceinline__ float2 lds_b64(unsigned addr) {
+  float2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
 }
-// U fragments of one step: 16 components (4 x b128) for this lane's channel and output channel
-__device__ __forceinline__ void wino_load_u(const float* Us, int ubase, int ks, int kk, float4 (&u)[4]) {
-  const float* up = Us + ubase + wino_chan(ks, kk) * 4 * CO * 4;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) u[g] = *reinterpret_cast<const float4*>(up + g * CO * 4);
+template <int OFF>
+__device__ __forceinline__ float4 lds_b128(unsigned addr) {
+  float4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(p);
+}
+
+// the 4x4 patch of this lane's tile for a pair of steps (two adjacent channels per element);
+// addr = byte address of the patch origin for the pair
+__device__ __forceinline__ void wino_load_patch(unsigned addr, float2 (&d)[16]) {
+#define PMU_P(I, J) d[4 * I + J] = lds_b64<((I) * ROWP + (J) * LS) * 4>(addr);
+  PMU_P(0, 0) PMU_P(0, 1) PMU_P(0, 2) PMU_P(0, 3) PMU_P(1, 0) PMU_P(1, 1) PMU_P(1, 2) PMU_P(1, 3)
+  PMU_P(2, 0) PMU_P(2, 1) PMU_P(2, 2) PMU_P(2, 3) PMU_P(3, 0) PMU_P(3, 1) PMU_P(3, 2) PMU_P(3, 3)
+#undef PMU_P
+}
+// U fragments of one step: 16 components (4 x b128); addr = byte address for this lane's channel
+__device__ __forceinline__ void wino_load_u(unsigned addr, float4 (&u)[4]) {
+  u[0] = lds_b128<0>(addr);
+  u[1] = lds_b128<CO * 16>(addr);
+  u[2] = lds_b128<2 * CO * 16>(addr);
+  u[3] = lds_b128<3 * CO * 16>(addr);
 }
 
 __device__ __forceinline__ void wino_mfmas(const float2 (&dp)[16], bool hi, const float4 (&u)[4], f32x4 (&acc)[16]) {
@@ -158,20 +181,26 @@ __device__ __forceinline__ void wino_mfmas(const float2 (&dp)[16], bool hi, cons
 // this step's MFMAs (sched_barrier keeps the order).
 __device__ __forceinline__ void wino_chunk(const float* As, const float* Us, int pbase, int ubase, int kk,
                                            f32x4 (&acc)[16]) {
+  const unsigned pa = lds_addr(As + pbase), ua = lds_addr(Us + ubase) + (unsigned)(2 * kk * 4 * CO * 4 * 4);
   float2 dp[2][16];
   float4 u[2][4];
-  wino_load_patch(As, pbase, 0, dp[0]);
-  wino_load_u(Us, ubase, 0, kk, u[0]);
+  wino_load_patch(pa, dp[0]);
+  wino_load_u(ua, u[0]);
 #pragma unroll
   for (int ks = 0; ks < BK / 4; ++ks) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     if (ks + 1 < BK / 4) {
-      if (((ks + 1) & 1) == 0) wino_load_patch(As, pbase, (ks + 1) >> 1, dp[((ks + 1) >> 1) & 1]);
-      wino_load_u(Us, ubase, ks + 1, kk, u[(ks + 1) & 1]);
+      const int n1 = ks + 1;
+      if ((n1 & 1) == 0) wino_load_patch(pa + 32 * (n1 >> 1), dp[(n1 >> 1) & 1]);
+      // channel 8*(n1>>1) + 2*kk + (n1&1): the kk part is in ua
+      wino_load_u(ua + (unsigned)((8 * (n1 >> 1) + (n1 & 1)) * 4 * CO * 4 * 4), u[n1 & 1]);
     }
     __builtin_amdgcn_sched_barrier(0);
     wino_mfmas(dp[(ks >> 1) & 1], ks & 1, u[ks & 1], acc);
     __builtin_amdgcn_sched_barrier(0);
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // the operand for the weight gradient: the chunk's interior 16 x 16 pixels x 16 channels
