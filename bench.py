@@ -67,13 +67,21 @@ class KernelTimer:
     MFMA = ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad", "pmu_convT2x2_fwd",
             "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd",
             "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16", "pmu_convT2x2_fwd_bf16",
-            "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16")
+            "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16",
+            "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino")
 
     def __init__(self):
         self.rec = []
 
     @staticmethod
     def _flops(name, args):
+        if name in ("pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino"):
+            # Winograd F(2x2,3x3): 16 products per 2x2 output tile per channel pair (the MFMA work of
+            # the algorithm; the direct sum it replaces is 36)
+            f = args[0]._obj
+            cframe = sum(f.src[i].C for i in range(f.nsrc))
+            nout = args[3] if name.endswith("fwd_wino") else args[2]
+            return 2.0 * 16 * f.N * ((f.H + 1) // 2) * ((f.W + 1) // 2) * cframe * nout
         if name == "pmu_conv3x3_fwd_bf16":
             f = args[0]._obj
             return 2.0 * f.N * f.H * f.W * sum(f.src[i].C for i in range(f.nsrc)) * args[3] * 9
@@ -190,7 +198,8 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
 # C-ABI entry -> regex over the device kernels it launches (rocprof kernel names), for the PMC traffic lookup
 KERNEL_FAMILY = {
     "pmu_conv3x3_fwd": r"conv3x3_(pipe_)?kernel<false", "pmu_conv3x3_dgrad": r"conv3x3_(pipe_)?kernel<true",
-    "pmu_conv3x3_wgrad": r"wgrad3x3_kernel<", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
+    "pmu_conv3x3_wgrad": r"wgrad3x3_kernel<",
+    "pmu_conv3x3_fwd_wino": r"conv3x3_wino_(pipe_)?kernel<false", "pmu_conv3x3_dgrad_wino": r"conv3x3_wino_(pipe_)?kernel<true", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
     "pmu_convT2x2_dgrad": r"convT_pipe_kernel<true>|DuGatherA",
     "pmu_convT2x2_wgrad": r"convT_wgrad_(pipe_)?kernel", "pmu_fcomb_fwd": r"fcomb_fwd_kernel",
     "pmu_fcomb_bwd": r"fcomb_bwd_kernel",

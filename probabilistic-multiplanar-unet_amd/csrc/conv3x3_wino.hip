@@ -160,6 +160,7 @@ __device__ __forceinline__ void wino_load_u(unsigned addr, float4 (&u)[4]) {
   u[3] = lds_b128<3 * CO * 16>(addr);
 }
 
+template <bool NOXF = false>
 __device__ __forceinline__ void wino_mfmas(const float2 (&dp)[16], bool hi, const float4 (&u)[4], f32x4 (&acc)[16]) {
   float dd[4][4];
 #pragma unroll
@@ -167,7 +168,13 @@ __device__ __forceinline__ void wino_mfmas(const float2 (&dp)[16], bool hi, cons
 #pragma unroll
     for (int j = 0; j < 4; ++j) dd[i][j] = hi ? dp[4 * i + j].y : dp[4 * i + j].x;
   float v[16];
-  input_transform(dd, v);
+  if (NOXF) {  // timing experiment only (PMU_WINO_EXP=3): no input transform
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = dd[c >> 2][c & 3];
+  } else {
+    input_transform(dd, v);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // all 16 components first: the MFMAs then issue back to back
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     acc[4 * g + 0] = mfma16(v[4 * g + 0], u[g].x, acc[4 * g + 0]);
@@ -179,6 +186,7 @@ __device__ __forceinline__ void wino_mfmas(const float2 (&dp)[16], bool hi, cons
 
 // One chunk (16 channels, 4 steps of 16 MFMAs per wave); the next step's operands are read before
 // this step's MFMAs (sched_barrier keeps the order).
+template <bool NOXF = false>
 __device__ __forceinline__ void wino_chunk(const float* As, const float* Us, int pbase, int ubase, int kk,
                                            f32x4 (&acc)[16]) {
   const unsigned pa = lds_addr(As + pbase), ua = lds_addr(Us + ubase) + (unsigned)(2 * kk * 4 * CO * 4 * 4);
@@ -197,7 +205,7 @@ __device__ __forceinline__ void wino_chunk(const float* As, const float* Us, int
       wino_load_u(ua + (unsigned)((8 * (n1 >> 1) + (n1 & 1)) * 4 * CO * 4 * 4), u[n1 & 1]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    wino_mfmas(dp[(ks >> 1) & 1], ks & 1, u[ks & 1], acc);
+    wino_mfmas<NOXF>(dp[(ks >> 1) & 1], ks & 1, u[ks & 1], acc);
     __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -225,8 +233,13 @@ struct WinoGeo {
 __device__ __forceinline__ WinoGeo wino_geo(const WinoArgs& a) {
   WinoGeo g;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  g.cob_blk = blockIdx.x % a.nco;
-  int sp = blockIdx.x / a.nco;
+  // XCD-aware order: the hardware deals consecutive workgroups round-robin over the 8 XCDs; remap
+  // so each XCD runs a contiguous range of logical blocks, i.e. the output-channel blocks of one
+  // spatial tile share their operand halo through that XCD's L2
+  const int nb = gridDim.x, x = blockIdx.x & 7, q = nb >> 3, r = nb & 7;
+  const int lb = x * q + (x < r ? x : r) + (blockIdx.x >> 3);
+  g.cob_blk = lb % a.nco;
+  int sp = lb / a.nco;
   g.spatial = sp;
   const int tw = sp % a.tiles_w; sp /= a.tiles_w;
   const int th = sp % a.tiles_h; sp /= a.tiles_h;
@@ -365,9 +378,12 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_kernel(WinoArgs a) {
 // U tile are loaded into registers before this chunk's MFMAs and written to the other LDS stage after
 // them — one barrier per chunk; 1 block (8 waves, 2 per SIMD) per CU, 118 KB LDS.
 constexpr int STAGE = A_FLOATS + U_FLOATS;
-static_assert(U_FLOATS / 4 / NT == 4, "4 U float4 per thread per chunk");
+static_assert(U_FLOATS / 4 / NT == 4, "4 U float4 (LDS-DMA) per thread per chunk");
 
-template <bool DGRAD, int POOL>
+// EXP (timing experiments, PMU_WINO_EXP): 1 = no restaging (every chunk reuses the first), 2 = that
+// and no barrier, 3 = no input transform (results wrong for 1-3); 4 / 5 = commit in step 1 / 3
+// instead of 2 (correct).
+template <bool DGRAD, int POOL, int EXP = 0>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
   const int tid = threadIdx.x;
@@ -382,35 +398,66 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
   for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   PmuPref<POOL, DGRAD, NI> pf;
-  float4 pb0, pb1, pb2, pb3;  // plain locals: an array here is kept in scratch
-  const float4* wsrc = reinterpret_cast<const float4*>(a.wp + (long long)g.cob_blk * nchunks * U_FLOATS) + tid;
-#define PMU_WPREFETCH(CH)                                                                                   \
+  // U is a plain copy: global_load_lds (LDS-DMA, no registers) straight into the stage, in the
+  // global layout (wave-instruction = 1 KB contiguous)
+  const float* wsrc = a.wp + (long long)g.cob_blk * nchunks * U_FLOATS + 4 * tid;
+  const int wave_off = (tid >> 6) * 256;  // floats: this wave's 1 KB within each 8 KB row of 512 float4
+#define PMU_WPREFETCH(CH, BUF)                                                                              \
   {                                                                                                        \
     const int k0_ = (CH) * BK;                                                                             \
     const bool second_ = F.nsrc > 1 && k0_ >= F.C0;                                                        \
     pmu_prefetch<POOL, DGRAD, NI>(pmu_pick_src(F, second_), k0_ - (second_ ? F.C0 : 0) + cq4, g.n, ih, iw, pf); \
-    const float4* s_ = wsrc + (long long)(CH) * (U_FLOATS / 4);                                            \
-    pb0 = s_[0]; pb1 = s_[NT]; pb2 = s_[2 * NT]; pb3 = s_[3 * NT];                                         \
+    const float* s_ = wsrc + (long long)(CH) * U_FLOATS;                                                   \
+    float* d_ = (BUF) + A_FLOATS + wave_off;                                                               \
+    PMU_GLDS(s_, d_) PMU_GLDS(s_ + 4 * NT, d_ + 4 * NT) PMU_GLDS(s_ + 8 * NT, d_ + 8 * NT)                 \
+    PMU_GLDS(s_ + 12 * NT, d_ + 12 * NT)                                                                   \
   }
-#define PMU_WCOMMIT(BUF)                                                                                    \
-  {                                                                                                        \
-    pmu_commit<POOL, DGRAD, NI>(pf, ih, dst, (BUF));                                                       \
-    float4* u_ = reinterpret_cast<float4*>((BUF) + A_FLOATS) + tid;                                        \
-    u_[0] = pb0; u_[NT] = pb1; u_[2 * NT] = pb2; u_[3 * NT] = pb3;                                         \
-  }
-  PMU_WPREFETCH(0)
+#define PMU_GLDS(S, D)                                                                                      \
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
+                                   (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
+#define PMU_WCOMMIT(BUF) pmu_commit<POOL, DGRAD, NI>(pf, ih, dst, (BUF));
+  PMU_WPREFETCH(0, smem)
   PMU_WCOMMIT(smem)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
     float* cur = smem + (ch & 1) * STAGE;
-    if (ch + 1 < nchunks) PMU_WPREFETCH(ch + 1)
+    if (EXP == 1 || EXP == 2) cur = smem;
+    if (ch + 1 < nchunks && EXP != 1 && EXP != 2) PMU_WPREFETCH(ch + 1, smem + ((ch + 1) & 1) * STAGE)
     if (a.tee && g.cob_blk == 0) wino_tee(a, cur, ch * BK, g.n, g.h0, g.w0, tid);
-    wino_chunk(cur, cur + A_FLOATS, g.pbase, g.ubase, g.kk, acc);
-    if (ch + 1 < nchunks) PMU_WCOMMIT(smem + ((ch + 1) & 1) * STAGE)
-    __syncthreads();
+    {
+      // wino_chunk with the next chunk's LDS stores issued inside step CS: they drain under this
+      // chunk's MFMAs instead of in a store phase all waves of the block would enter together
+      constexpr int CS = EXP == 4 ? 1 : EXP == 5 ? 3 : 2;
+      const bool commit = ch + 1 < nchunks && EXP != 1 && EXP != 2;
+      const unsigned pa = lds_addr(cur + g.pbase);
+      const unsigned ua = lds_addr(cur + A_FLOATS + g.ubase) + (unsigned)(2 * g.kk * 4 * CO * 4 * 4);
+      float2 dp[2][16];
+      float4 u[2][4];
+      wino_load_patch(pa, dp[0]);
+      wino_load_u(ua, u[0]);
+#pragma unroll
+      for (int ks = 0; ks < BK / 4; ++ks) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + 1 < BK / 4) {
+          const int n1 = ks + 1;
+          if ((n1 & 1) == 0) wino_load_patch(pa + 32 * (n1 >> 1), dp[(n1 >> 1) & 1]);
+          wino_load_u(ua + (unsigned)((8 * (n1 >> 1) + (n1 & 1)) * 4 * CO * 4 * 4), u[n1 & 1]);
+        }
+        if (ks == CS && commit) PMU_WCOMMIT(smem + ((ch + 1) & 1) * STAGE)
+        __builtin_amdgcn_sched_barrier(0);
+        wino_mfmas<EXP == 3>(dp[(ks >> 1) & 1], ks & 1, u[ks & 1], acc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA of the next U has landed
+    if (EXP != 2) __syncthreads();
   }
 #undef PMU_WPREFETCH
 #undef PMU_WCOMMIT
+#undef PMU_GLDS
   wino_epilogue<DGRAD>(a, g, acc, smem);
 }
 
@@ -419,6 +466,14 @@ static bool wino_pipe_src_ok(const pmu_src& s) {
   if (s.C % BK != 0) return false;
   if (s.pool == PMU_POOL_NONE) return true;
   return s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU;
+}
+
+static int wino_exp() {
+  static const int v = [] {
+    const char* e = getenv("PMU_WINO_EXP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 static bool wino_sync_forced() {
@@ -453,6 +508,16 @@ int launch_wino(const pmu_frame* in, const float* wp, const float* bias, int NOU
     if (ok && same_pool && modes_ok) {
       if (dgrad && pool == PMU_POOL_NONE)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<true, PMU_POOL_NONE>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 1)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 1>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 2)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 2>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 3)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 3>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 4)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 4>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 5)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 5>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_NONE)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_MAX2)
