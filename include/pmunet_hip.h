@@ -110,6 +110,12 @@ int pmu_conv3x3_fwd_wino(const pmu_frame* in, const float* wp, const float* bias
                          float* part, float* tee, void* stream);
 int pmu_conv3x3_dgrad_wino(const pmu_frame* dz, const float* wp, int Cin, int Csplit, float* dx0, float* dx1,
                            float* tee, void* stream);
+/* dw[Cout][Cin][3][3] from the teed operands dzt [N][H][W][Cout] and xt [N][H][W][Cin] (fp32), by
+ * Winograd F(2x2,3x3): dw = G^T [sum over 2x2 tiles of (A dY A^T) .* (B^T X B)] G.  Cout % 32 == 0,
+ * Cin % 64 == 0 (pmu_conv3x3_wgrad_ws_wino returns 0 otherwise); ws must hold that many bytes. */
+size_t pmu_conv3x3_wgrad_ws_wino(int N, int H, int W, int Cin, int Cout);
+int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, int H, int W, int Cout, int Cin,
+                           float* dw, float* ws, size_t ws_bytes, void* stream);
 
 /* ---- bf16-MFMA variants (config c5, BASELINE.json configs[4]: "... bf16") --------------
  * torch.autocast(bfloat16) arithmetic for the same operators: the operand (after the fused fp32

@@ -1,0 +1,255 @@
+// Weight gradient of the 3x3 / pad 1 convolution in fp32 by Winograd F(2x2, 3x3) (the autograd of
+// nn.Conv2d w.r.t. its weight, PMU/model/unet/unet_parts.py:15,18), on the materialised operands the
+// forward and input-gradient kernels tee (xt = the conv's input operand, dzt = dL/dz; both NHWC fp32).
+//
+// For a 2x2 output tile with gradient block dY (per output channel) and 4x4 input patch X (per input
+// channel), the forward is Y = A^T [(G g G^T) .* (B^T X B)] A, so
+//     dL/dg = G^T [ (A dY A^T) .* (B^T X B) ] G     (summed over tiles)
+// i.e. 16 per-component GEMMs over the tiles, M[c][co][ci] = sum_t Z[c][t][co] V[c][t][ci] with
+// Z = A dY A^T, V = B^T X B, followed by the 3x4x4x3 output transform G^T M G — 16 products per tile
+// and channel pair where the direct sum takes 36.  fp32 throughout; the result differs from the
+// direct sum by fp32 rounding only.
+//
+// Block: 512 threads, 32 output x 64 input channels, all 16 components; wave w owns the 16 x 16
+// (co, ci) fragment (w & 1, w >> 1) for every component (acc[16] of v_mfma_f32_16x16x4_f32, 64
+// registers).  K = tiles, in K-tiles of 64 output pixels (4 x 16 = 16 Winograd tiles, 4 MFMA steps);
+// the next K-tile's dzt / xt values are loaded into registers during the current one's MFMAs
+// (double-buffered LDS).  Split-K over blocks: each writes M for its tile range to a slab, and the
+// reduce kernel sums the slabs in a fixed order (deterministic) and applies G^T M G.
+#include "pmu_common.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NT = 512;
+constexpr int WCO = 32, WCI = 64;        // channels per block
+constexpr int TH = 4, TW = 16;           // output pixels per K-tile
+constexpr int HH = TH + 2, HWD = TW + 2; // 6 x 18 operand halo
+constexpr int DLS = WCO + 8;             // LDS floats per dz pixel (tile step 2 px = 80 = 16 mod 32: conflict-free)
+constexpr int XLS = WCI + 8;             // LDS floats per x pixel (72: 144 = 16 mod 32)
+constexpr int D_FLOATS = TH * TW * DLS;
+constexpr int X_FLOATS = HH * HWD * XLS;
+constexpr int SLOT = D_FLOATS + X_FLOATS;
+constexpr int NXI = 4;                   // x float4 items per thread: ceil(108 * 16 / 512)
+
+struct WgwArgs {
+  const float* dz;  // [N][H][W][Cout]
+  const float* x;   // [N][H][W][Cin]
+  float* ws;        // [nsplit][16][Cout][Cin]
+  int N, H, W, Cout, Cin, tiles_w, tiles_h, ntiles, nsplit, nco;
+};
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// in-flight global loads of one K-tile for this thread
+struct WgwRegs {
+  float4 d;
+  float4 x[NXI];
+};
+
+__device__ __forceinline__ void wgw_origin(const WgwArgs& a, int tile, int& n, int& h0, int& w0) {
+  int t = tile;
+  const int tw = t % a.tiles_w; t /= a.tiles_w;
+  const int th = t % a.tiles_h; t /= a.tiles_h;
+  n = t; h0 = th * TH; w0 = tw * TW;
+}
+
+__device__ __forceinline__ void wgw_load(const WgwArgs& a, int tile, int co0, int ci0, int tid, WgwRegs& r) {
+  int n, h0, w0;
+  wgw_origin(a, tile, n, h0, w0);
+  {
+    const int px = tid >> 3, q = tid & 7;
+    const int h = h0 + (px >> 4), w = w0 + (px & 15);
+    const bool ok = h < a.H && w < a.W;
+    const long long idx = ok ? (((long long)n * a.H + h) * a.W + w) * a.Cout + co0 + 4 * q : 0;
+    r.d = *reinterpret_cast<const float4*>(a.dz + idx);
+    if (!ok) r.d = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int i = 0; i < NXI; ++i) {
+    const int it = tid + NT * i;
+    const int px = it >> 4, q = it & 15;
+    const int hr = px / HWD, hc = px - hr * HWD;
+    const int h = h0 - 1 + hr, w = w0 - 1 + hc;
+    const bool ok = it < HH * HWD * 16 && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    const long long idx = ok ? (((long long)n * a.H + h) * a.W + w) * a.Cin + ci0 + 4 * q : 0;
+    r.x[i] = *reinterpret_cast<const float4*>(a.x + idx);
+    if (!ok) r.x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void wgw_store(const WgwRegs& r, int tid, float* slot) {
+  {
+    const int px = tid >> 3, q = tid & 7;
+    *reinterpret_cast<float4*>(slot + px * DLS + 4 * q) = r.d;
+  }
+  float* xs = slot + D_FLOATS;
+#pragma unroll
+  for (int i = 0; i < NXI; ++i) {
+    const int it = tid + NT * i;
+    if (it < HH * HWD * 16) *reinterpret_cast<float4*>(xs + (it >> 4) * XLS + 4 * (it & 15)) = r.x[i];
+  }
+}
+
+// one MFMA step: tiles 4s..4s+3 (k = lane >> 4)
+__device__ __forceinline__ void wgw_step(const float* slot, int s, int lane, int cf, int pf, f32x4 (&acc)[16]) {
+  const int t = 4 * s + (lane >> 4);
+  const int ty = t >> 3, tx = t & 7;
+  const float* dp = slot + ((2 * ty) * TW + 2 * tx) * DLS + cf * 16 + (lane & 15);
+  const float* xp = slot + D_FLOATS + ((2 * ty) * HWD + 2 * tx) * XLS + pf * 16 + (lane & 15);
+  // Z = A dY A^T, A = [1 0; 1 1; 1 -1; 0 -1]
+  const float d00 = dp[0], d01 = dp[DLS], d10 = dp[TW * DLS], d11 = dp[(TW + 1) * DLS];
+  float r[4][2];  // A dY
+  r[0][0] = d00; r[0][1] = d01;
+  r[1][0] = d00 + d10; r[1][1] = d01 + d11;
+  r[2][0] = d00 - d10; r[2][1] = d01 - d11;
+  r[3][0] = -d10; r[3][1] = -d11;
+  float z[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    z[4 * i + 0] = r[i][0];
+    z[4 * i + 1] = r[i][0] + r[i][1];
+    z[4 * i + 2] = r[i][0] - r[i][1];
+    z[4 * i + 3] = -r[i][1];
+  }
+  // V = B^T X B, B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]
+  float xv[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[i][j] = xp[(i * HWD + j) * XLS];
+  float tt[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    tt[0][j] = xv[0][j] - xv[2][j];
+    tt[1][j] = xv[1][j] + xv[2][j];
+    tt[2][j] = xv[2][j] - xv[1][j];
+    tt[3][j] = xv[1][j] - xv[3][j];
+  }
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[4 * i + 0] = tt[i][0] - tt[i][2];
+    v[4 * i + 1] = tt[i][1] + tt[i][2];
+    v[4 * i + 2] = tt[i][2] - tt[i][1];
+    v[4 * i + 3] = tt[i][1] - tt[i][3];
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = mfma16(z[c], v[c], acc[c]);
+}
+
+__global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cf = wave & 1, pf = wave >> 1;
+  const int co0 = (blockIdx.x % a.nco) * WCO, ci0 = (blockIdx.x / a.nco) * WCI;
+  const int split = blockIdx.y;
+  const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
+  const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);
+
+  f32x4 acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  WgwRegs regs;
+  if (t_beg < t_end) {
+    wgw_load(a, t_beg, co0, ci0, tid, regs);
+    wgw_store(regs, tid, smem);
+  }
+  __syncthreads();
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    const int cur = (tile - t_beg) & 1;
+    const bool more = tile + 1 < t_end;
+    if (more) wgw_load(a, tile + 1, co0, ci0, tid, regs);  // in flight during the MFMAs
+    const float* slot = smem + cur * SLOT;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) wgw_step(slot, s, lane, cf, pf, acc);
+    if (more) wgw_store(regs, tid, smem + (cur ^ 1) * SLOT);
+    __syncthreads();
+  }
+
+  // slab: ws[split][c][co][ci], D row = co (4*(lane>>4) + r), col = ci (lane & 15)
+  const int ci = ci0 + pf * 16 + (lane & 15);
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + cf * 16 + 4 * (lane >> 4) + r;
+      a.ws[(((long long)split * 16 + c) * a.Cout + co) * a.Cin + ci] = acc[c][r];
+    }
+}
+
+// dw[co][ci][3][3] = G^T (sum over splits of M) G, G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]
+__global__ void wgrad_wino_reduce_kernel(const float* __restrict__ ws, int nsplit, int Cout, int Cin,
+                                         float* __restrict__ dw) {
+  const long long CC = (long long)Cout * Cin;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < CC; e += (long long)gridDim.x * blockDim.x) {
+    float m[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) m[c] = 0.f;
+    for (int s = 0; s < nsplit; ++s)
+#pragma unroll
+      for (int c = 0; c < 16; ++c) m[c] += ws[((long long)s * 16 + c) * CC + e];
+    float t[3][4];  // G^T M
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float h = 0.5f * (m[4 + k] + m[8 + k]);
+      t[0][k] = m[k] + h;
+      t[1][k] = 0.5f * (m[4 + k] - m[8 + k]);
+      t[2][k] = h + m[12 + k];
+    }
+    float* o = dw + e * 9;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float h = 0.5f * (t[i][1] + t[i][2]);
+      o[3 * i + 0] = t[i][0] + h;
+      o[3 * i + 1] = 0.5f * (t[i][1] - t[i][2]);
+      o[3 * i + 2] = h + t[i][3];
+    }
+  }
+}
+
+void wgw_geometry(int N, int H, int W, int Cout, int Cin, WgwArgs& a) {
+  a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.Cin = Cin;
+  a.tiles_w = pmu_cdiv(W, TW);
+  a.tiles_h = pmu_cdiv(H, TH);
+  a.ntiles = N * a.tiles_w * a.tiles_h;
+  a.nco = Cout / WCO;
+  const int blocks_mn = a.nco * (Cin / WCI);
+  int s = 512 / blocks_mn;  // ~2 blocks per CU over the launch
+  if (s < 1) s = 1;
+  if (s > a.ntiles) s = a.ntiles;
+  a.nsplit = s;
+}
+
+}  // namespace
+
+extern "C" size_t pmu_conv3x3_wgrad_ws_wino(int N, int H, int W, int Cin, int Cout) {
+  if (Cout % WCO != 0 || Cin % WCI != 0) return 0;
+  WgwArgs a;
+  wgw_geometry(N, H, W, Cout, Cin, a);
+  return (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float);
+}
+
+extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, int H, int W, int Cout, int Cin,
+                                      float* dw, float* ws, size_t ws_bytes, void* stream) {
+  PMU_REQUIRE(dzt && xt && dw && ws && N > 0 && H > 0 && W > 0);
+  PMU_REQUIRE(Cout % WCO == 0 && Cin % WCI == 0);
+  WgwArgs a;
+  a.dz = dzt; a.x = xt; a.ws = ws;
+  wgw_geometry(N, H, W, Cout, Cin, a);
+  PMU_REQUIRE(ws_bytes >= (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(wgrad3x3_wino_kernel, dim3((unsigned)(a.nco * (Cin / WCI)), (unsigned)a.nsplit), dim3(NT), 0,
+                     st, a);
+  PMU_CHECK_LAUNCH();
+  const long long CC = (long long)Cout * Cin;
+  const int blocks = (int)((CC + 255) / 256);
+  hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, a.nsplit, Cout, Cin,
+                     dw);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}

@@ -51,6 +51,9 @@ SIGNATURES = {
     "pmu_conv3x3_tiles_wino": (c_int, [c_int, c_int, c_int]),
     "pmu_conv3x3_fwd_wino": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_wino": (c_int, [_FP, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_wgrad_ws_wino": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_conv3x3_wgrad_wino": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                       c_size_t, c_void_p]),
     "pmu_conv3x3_packed_size_bf16": (c_size_t, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_fwd_bf16": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),

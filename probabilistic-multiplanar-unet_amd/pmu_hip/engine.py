@@ -302,10 +302,16 @@ def _conv_backward_tee32(out: ConvBNOut, dzf, conv, dw, split):
     Cin = conv.in_channels
     dzt = _empty(N, H, W, Cout, device=dev)
     res = _dgrad32(dzf, conv, N, H, W, split, dzt)
-    wsb = lb.pmu_conv3x3_wgrad_ws(N, H, W, Cin, Cout)
-    ws = _empty(max(1, (wsb + 3) // 4), device=dev)
-    L.call("pmu_conv3x3_wgrad", frame_of([Src(dzt)], N, H, W), frame_of([Src(out.xt32)], N, H, W), Cout,
-           dw.data_ptr(), ws.data_ptr(), wsb, s)
+    wsb = lb.pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout) if use_wino() else 0
+    if wsb:
+        ws = _empty((wsb + 3) // 4, device=dev)
+        L.call("pmu_conv3x3_wgrad_wino", dzt.data_ptr(), out.xt32.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(),
+               ws.data_ptr(), wsb, s)
+    else:
+        wsb = lb.pmu_conv3x3_wgrad_ws(N, H, W, Cin, Cout)
+        ws = _empty(max(1, (wsb + 3) // 4), device=dev)
+        L.call("pmu_conv3x3_wgrad", frame_of([Src(dzt)], N, H, W), frame_of([Src(out.xt32)], N, H, W), Cout,
+               dw.data_ptr(), ws.data_ptr(), wsb, s)
     out.xt32 = None
     return res
 

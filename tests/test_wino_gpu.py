@@ -106,3 +106,23 @@ def test_conv3x3_dgrad_wino(dev, N, H, W, Cin, Cout, split):
                                      padding=1).permute(0, 2, 3, 1)
     got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
     assert _rel(got, ref) <= TOL
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 32, 32, 64, 64), (2, 17, 33, 128, 32), (3, 9, 13, 64, 96),
+                                            (1, 40, 36, 192, 64)])
+def test_conv3x3_wgrad_wino(dev, N, H, W, Cin, Cout):
+    from pmu_hip import _lib as L
+    g = torch.Generator().manual_seed(3 + H + Cin + Cout)
+    x = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    dz = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    wsb = L.lib().pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout)
+    assert wsb > 0
+    ws = torch.empty(wsb // 4, device=dev)
+    dw = torch.empty(Cout, Cin, 3, 3, device=dev)
+    L.call("pmu_conv3x3_wgrad_wino", dz.data_ptr(), x.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(), ws.data_ptr(),
+           wsb, L.stream())
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_weight(x.permute(0, 3, 1, 2).double().cpu(), (Cout, Cin, 3, 3),
+                                      dz.permute(0, 3, 1, 2).double().cpu(), padding=1)
+    assert _rel(dw, ref) <= TOL
+    assert L.lib().pmu_conv3x3_wgrad_ws_wino(N, H, W, 32, Cout) == 0  # Cin % 64 != 0: not taken

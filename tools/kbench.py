@@ -94,8 +94,10 @@ def main():
         wrf = packr(w, False)
         partr = torch.empty(L.lib().pmu_conv3x3_tiles_raw(N, H, W, Cout), 2 * Cout, device=dev)
         wrd = packr(w, True)
-        xt32 = torch.empty(N, H, W, Cin, device=dev)
-        dzt32 = torch.empty(N, H, W, Cout, device=dev)
+        xt32 = torch.randn(N, H, W, Cin, device=dev)
+        dzt32 = torch.randn(N, H, W, Cout, device=dev)
+        wsbw = L.lib().pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout)
+        wsw = torch.empty(max(wsbw, 4) // 4, device=dev)
         from pmu_hip.engine import pack_weights_wino
         wwf, wwd = pack_weights_wino(w, False), pack_weights_wino(w, True)
         partw = torch.empty(L.lib().pmu_conv3x3_tiles_wino(N, H, W), 2 * Cout, device=dev)
@@ -126,6 +128,8 @@ def main():
                                        out.data_ptr(), partw.data_ptr(), None, s),
             "dgrad_wino": lambda: L.call("pmu_conv3x3_dgrad_wino", fdz, wwd.data_ptr(), Cin, Cin, dx.data_ptr(),
                                          None, None, s),
+            "wgrad_wino": lambda: L.call("pmu_conv3x3_wgrad_wino", dzt32.data_ptr(), xt32.data_ptr(), N, H, W, Cout,
+                                         Cin, dw.data_ptr(), wsw.data_ptr(), wsbw, s),
             "pack": lambda: pack_weights(w, False),
             "wgrad": lambda: L.call("pmu_conv3x3_wgrad", fdz, fin, Cout, dw.data_ptr(), ws.data_ptr(), wsb, s),
         }
