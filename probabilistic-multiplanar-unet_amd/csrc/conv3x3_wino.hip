@@ -428,7 +428,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
     {
       // wino_chunk with the next chunk's LDS stores issued inside step CS: they drain under this
       // chunk's MFMAs instead of in a store phase all waves of the block would enter together
-      constexpr int CS = EXP == 4 ? 1 : EXP == 5 ? 3 : 2;
+      // (BN-backward and max-pool operands hold more prefetch registers: they commit after the steps)
+      constexpr int CS = EXP == 4 ? 1 : EXP == 5 ? 3 : (DGRAD || POOL != PMU_POOL_NONE) ? 4 : 2;
       const bool commit = ch + 1 < nchunks && EXP != 1 && EXP != 2;
       const unsigned pa = lds_addr(cur + g.pbase);
       const unsigned ua = lds_addr(cur + A_FLOATS + g.ubase) + (unsigned)(2 * g.kk * 4 * CO * 4 * 4);
@@ -451,6 +452,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (CS == 4 && commit) PMU_WCOMMIT(smem + ((ch + 1) & 1) * STAGE)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA of the next U has landed
     if (EXP != 2) __syncthreads();

@@ -94,14 +94,26 @@ __device__ __forceinline__ void wgw_store(const WgwRegs& r, int tid, float* slot
   }
 }
 
-// one MFMA step: tiles 4s..4s+3 (k = lane >> 4)
-__device__ __forceinline__ void wgw_step(const float* slot, int s, int lane, int cf, int pf, f32x4 (&acc)[16]) {
+// operand values of one MFMA step: tiles 4s..4s+3 (k = lane >> 4), this lane's co (dz 2x2) and ci (x 4x4)
+struct WgwOps {
+  float d[4];
+  float x[16];
+};
+__device__ __forceinline__ void wgw_read(const float* slot, int s, int lane, int cf, int pf, WgwOps& o) {
   const int t = 4 * s + (lane >> 4);
   const int ty = t >> 3, tx = t & 7;
   const float* dp = slot + ((2 * ty) * TW + 2 * tx) * DLS + cf * 16 + (lane & 15);
   const float* xp = slot + D_FLOATS + ((2 * ty) * HWD + 2 * tx) * XLS + pf * 16 + (lane & 15);
+  o.d[0] = dp[0]; o.d[1] = dp[DLS]; o.d[2] = dp[TW * DLS]; o.d[3] = dp[(TW + 1) * DLS];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o.x[4 * i + j] = xp[(i * HWD + j) * XLS];
+}
+
+__device__ __forceinline__ void wgw_mfmas(const WgwOps& o, f32x4 (&acc)[16]) {
   // Z = A dY A^T, A = [1 0; 1 1; 1 -1; 0 -1]
-  const float d00 = dp[0], d01 = dp[DLS], d10 = dp[TW * DLS], d11 = dp[(TW + 1) * DLS];
+  const float d00 = o.d[0], d01 = o.d[1], d10 = o.d[2], d11 = o.d[3];
   float r[4][2];  // A dY
   r[0][0] = d00; r[0][1] = d01;
   r[1][0] = d00 + d10; r[1][1] = d01 + d11;
@@ -116,18 +128,13 @@ __device__ __forceinline__ void wgw_step(const float* slot, int s, int lane, int
     z[4 * i + 3] = -r[i][1];
   }
   // V = B^T X B, B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]
-  float xv[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) xv[i][j] = xp[(i * HWD + j) * XLS];
   float tt[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    tt[0][j] = xv[0][j] - xv[2][j];
-    tt[1][j] = xv[1][j] + xv[2][j];
-    tt[2][j] = xv[2][j] - xv[1][j];
-    tt[3][j] = xv[1][j] - xv[3][j];
+    tt[0][j] = o.x[j] - o.x[8 + j];
+    tt[1][j] = o.x[4 + j] + o.x[8 + j];
+    tt[2][j] = o.x[8 + j] - o.x[4 + j];
+    tt[3][j] = o.x[4 + j] - o.x[12 + j];
   }
   float v[16];
 #pragma unroll
@@ -137,6 +144,7 @@ __device__ __forceinline__ void wgw_step(const float* slot, int s, int lane, int
     v[4 * i + 2] = tt[i][2] - tt[i][1];
     v[4 * i + 3] = tt[i][1] - tt[i][3];
   }
+  __builtin_amdgcn_sched_barrier(0);  // all components first: the MFMAs then issue back to back
 #pragma unroll
   for (int c = 0; c < 16; ++c) acc[c] = mfma16(z[c], v[c], acc[c]);
 }
@@ -165,9 +173,18 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
     const bool more = tile + 1 < t_end;
     if (more) wgw_load(a, tile + 1, co0, ci0, tid, regs);  // in flight during the MFMAs
     const float* slot = smem + cur * SLOT;
+    // each step's LDS reads are issued before the previous step's MFMAs; the next K-tile's stores
+    // go out inside step 2, under the MFMAs
+    WgwOps ops[2];
+    wgw_read(slot, 0, lane, cf, pf, ops[0]);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) wgw_step(slot, s, lane, cf, pf, acc);
-    if (more) wgw_store(regs, tid, smem + (cur ^ 1) * SLOT);
+    for (int s = 0; s < 4; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < 4) wgw_read(slot, s + 1, lane, cf, pf, ops[(s + 1) & 1]);
+      if (s == 2 && more) wgw_store(regs, tid, smem + (cur ^ 1) * SLOT);
+      __builtin_amdgcn_sched_barrier(0);
+      wgw_mfmas(ops[s & 1], acc);
+    }
     __syncthreads();
   }
 
