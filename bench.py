@@ -68,13 +68,16 @@ class KernelTimer:
             "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd",
             "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16", "pmu_convT2x2_fwd_bf16",
             "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16",
-            "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino")
+            "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino", "pmu_conv3x3_wgrad_wino")
 
     def __init__(self):
         self.rec = []
 
     @staticmethod
     def _flops(name, args):
+        if name == "pmu_conv3x3_wgrad_wino":
+            N, H, W, cout, cin = args[2], args[3], args[4], args[5], args[6]
+            return 2.0 * 16 * N * ((H + 1) // 2) * ((W + 1) // 2) * cin * cout
         if name in ("pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino"):
             # Winograd F(2x2,3x3): 16 products per 2x2 output tile per channel pair (the MFMA work of
             # the algorithm; the direct sum it replaces is 36)
@@ -199,7 +202,8 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
 KERNEL_FAMILY = {
     "pmu_conv3x3_fwd": r"conv3x3_(pipe_)?kernel<false", "pmu_conv3x3_dgrad": r"conv3x3_(pipe_)?kernel<true",
     "pmu_conv3x3_wgrad": r"wgrad3x3_kernel<",
-    "pmu_conv3x3_fwd_wino": r"conv3x3_wino_(pipe_)?kernel<false", "pmu_conv3x3_dgrad_wino": r"conv3x3_wino_(pipe_)?kernel<true", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
+    "pmu_conv3x3_fwd_wino": r"conv3x3_wino_(pipe_)?kernel<false", "pmu_conv3x3_dgrad_wino": r"conv3x3_wino_(pipe_)?kernel<true",
+    "pmu_conv3x3_wgrad_wino": r"wgrad3x3_wino_kernel", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
     "pmu_convT2x2_dgrad": r"convT_pipe_kernel<true>|DuGatherA",
     "pmu_convT2x2_wgrad": r"convT_wgrad_(pipe_)?kernel", "pmu_fcomb_fwd": r"fcomb_fwd_kernel",
     "pmu_fcomb_bwd": r"fcomb_bwd_kernel",

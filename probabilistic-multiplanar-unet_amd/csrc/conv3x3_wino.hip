@@ -467,7 +467,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
 static bool wino_pipe_src_ok(const pmu_src& s) {
   if (s.C % BK != 0) return false;
   if (s.pool == PMU_POOL_NONE) return true;
-  return s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU;
+  return (s.pool == PMU_POOL_MAX2 || s.pool == PMU_POOL_AVG2CEIL) && s.mode == PMU_SRC_BNRELU;
 }
 
 static int wino_exp() {
@@ -524,6 +524,8 @@ int launch_wino(const pmu_frame* in, const float* wp, const float* bias, int NOU
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_MAX2)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_MAX2>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_AVG2CEIL)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_AVG2CEIL>), grid, dim3(NT), 0, st, a);
       else
         goto sync;
       PMU_CHECK_LAUNCH();

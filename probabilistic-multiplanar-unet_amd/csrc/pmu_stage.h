@@ -169,11 +169,12 @@ __device__ __forceinline__ DevSrc pmu_pick_src(const DevFrame& F, bool second) {
 
 template <int POOL, bool BWD, int NI>
 struct PmuPref {
-  static constexpr int NL = (POOL == PMU_POOL_MAX2) ? 4 : 1;
+  static constexpr int NL = (POOL == PMU_POOL_MAX2 || POOL == PMU_POOL_AVG2CEIL) ? 4 : 1;
   float4 x[NI][NL];
   float4 z[BWD ? NI : 1];
   float4 sc, sh, mu, kx, kc;
   unsigned okmask;
+  unsigned em;  // AvgPool2d(ceil): 3 bits per item, which of the window's (0,1), (1,0), (1,1) exist
   int raw;
 };
 
@@ -191,11 +192,11 @@ __device__ __forceinline__ void pmu_prefetch(const DevSrc& s, int c, int n, cons
     p.kc = *reinterpret_cast<const float4*>(s.coef + 4 * s.C + c);
   }
   const long long rs = (long long)s.W * s.C;
-  unsigned m = 0u;
+  unsigned m = 0u, em = 0u;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     int hs = ih[i] - s.off_h, ws = iw[i] - s.off_w;
-    if (POOL == PMU_POOL_MAX2) { hs *= 2; ws *= 2; }
+    if (POOL != PMU_POOL_NONE) { hs *= 2; ws *= 2; }
     const int lim_h = (POOL == PMU_POOL_MAX2) ? s.H - 1 : s.H;
     const int lim_w = (POOL == PMU_POOL_MAX2) ? s.W - 1 : s.W;
     const bool ok = (ih[i] != PMU_NO_ITEM) && hs >= 0 && ws >= 0 && hs < lim_h && ws < lim_w;
@@ -207,9 +208,17 @@ __device__ __forceinline__ void pmu_prefetch(const DevSrc& s, int c, int n, cons
       p.x[i][2] = *reinterpret_cast<const float4*>(s.x + idx + rs);
       p.x[i][3] = *reinterpret_cast<const float4*>(s.x + idx + rs + s.C);
     }
+    if (POOL == PMU_POOL_AVG2CEIL) {  // ceil-mode windows: only the elements inside the input
+      const bool e01 = ok && ws + 1 < s.W, e10 = ok && hs + 1 < s.H;
+      em |= ((e01 ? 1u : 0u) | (e10 ? 2u : 0u) | ((e01 && e10) ? 4u : 0u)) << (3 * i);
+      p.x[i][1] = *reinterpret_cast<const float4*>(s.x + idx + (e01 ? s.C : 0));
+      p.x[i][2] = *reinterpret_cast<const float4*>(s.x + idx + (e10 ? rs : 0));
+      p.x[i][3] = *reinterpret_cast<const float4*>(s.x + idx + ((e01 && e10) ? rs + s.C : 0));
+    }
     if (BWD) p.z[i] = *reinterpret_cast<const float4*>(s.z + idx);
   }
   p.okmask = m;
+  p.em = em;
 }
 
 struct PmuNoTee {
@@ -239,6 +248,7 @@ __device__ __forceinline__ void pmu_commit(const PmuPref<POOL, BWD, NI>& p, cons
         v = pmu_max4(v, pmu_bnrelu4(p.x[i][2], p.sc, p.sh));
         v = pmu_max4(v, pmu_bnrelu4(p.x[i][3], p.sc, p.sh));
       }
+      if constexpr (POOL == PMU_POOL_AVG2CEIL) v = pmu_avg4(v, p.x[i], (p.em >> (3 * i)) & 7u, p.sc, p.sh);
     }
     if (!((p.okmask >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
     pmu_lds_store4<BF>(lds, dst[i], v);

@@ -134,7 +134,7 @@ def _planes(x, segm):
 class GaussianFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, g, x, segm, *params):
-        mls, st = prob_engine.gaussian_forward(g, _planes(x, segm), g.training)
+        mls, st = prob_engine.gaussian_forward(g, _planes(x, segm), g.training, keep=True)
         ctx.g, ctx.st = g, st
         return mls
 

@@ -54,9 +54,10 @@ class GaussState:
     hw: tuple
 
 
-def gaussian_forward(g, planes, training: bool):
+def gaussian_forward(g, planes, training: bool, keep: bool = False):
     """AxisAlignedConvGaussian.forward up to mu_log_sigma (N, 2L) (probabilistic_unet.py:82-105).
-    ``planes``: the input channels (cat(input, segm) for the posterior) as contiguous (N,H,W) maps."""
+    ``planes``: the input channels (cat(input, segm) for the posterior) as contiguous (N,H,W) maps.
+    keep: a backward follows (the convs keep their operand copies for the weight gradients)."""
     dev = planes[0].device
     N, H, W = planes[0].shape
     layers = encoder_layers(g.encoder)
@@ -72,7 +73,7 @@ def gaussian_forward(g, planes, training: bool):
             if pooled:
                 h, w = (h + 1) // 2, (w + 1) // 2
             o = conv_bn_forward([prev.act(L.POOL_AVG2CEIL if pooled else L.POOL_NONE)], conv, bn, N, h, w,
-                                training, dev)
+                                training, dev, keep=keep)
         outs.append(o)
         prev = o
     C = prev.z.shape[3]

@@ -41,6 +41,9 @@ def _frame(kind, N, H, W, C, g, dev):
     if kind == "maxpool":
         return [Src(torch.randn(N, 2 * H + 1, 2 * W, C, generator=g).to(dev), L.SRC_BNRELU, _coef(C, g, dev),
                     pool=L.POOL_MAX2)]
+    if kind == "avgpool":  # AvgPool2d(2, 2, ceil_mode=True) of an odd-height map (the encoders' pooling)
+        return [Src(torch.randn(N, 2 * H - 1, 2 * W, C, generator=g).to(dev), L.SRC_BNRELU, _coef(C, g, dev),
+                    pool=L.POOL_AVG2CEIL)]
     if kind == "concat":
         c0 = C // 2
         z = torch.randn(N, H, W, c0, generator=g).to(dev)
@@ -51,7 +54,8 @@ def _frame(kind, N, H, W, C, g, dev):
 
 @pytest.mark.parametrize("kind,N,H,W,Cin,Cout", [("bnrelu", 2, 32, 32, 64, 64), ("raw", 1, 37, 45, 20, 40),
                                                  ("maxpool", 2, 24, 20, 64, 128), ("concat", 2, 33, 17, 128, 64),
-                                                 ("bnrelu", 3, 16, 16, 512, 96), ("raw", 1, 7, 9, 6, 10)])
+                                                 ("bnrelu", 3, 16, 16, 512, 96), ("raw", 1, 7, 9, 6, 10),
+                                                 ("avgpool", 2, 20, 24, 64, 64), ("avgpool", 1, 9, 5, 128, 32)])
 def test_conv3x3_fwd_wino(dev, kind, N, H, W, Cin, Cout):
     from pmu_hip import _lib as L
     from pmu_hip.engine import frame_of, pack_weights_wino
