@@ -529,6 +529,9 @@ def main():
                 "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "bytes/launch (HBM)",
                 "traffic_source": tsrc, "launches": n, "avg_launch_ms": round(t / n * 1e3, 4),
                 "flops_per_launch": fl / n}
+        if dom.endswith("_wino"):  # Winograd executes 16 of the direct sum's 36 products per 2x2 tile
+            roof["flops_basis"] = "Winograd F(2x2,3x3) MFMA products (16 per 2x2 output tile per channel pair)"
+            roof["direct_conv_equiv_tflops"] = round(ach * 36 / 16, 2)
         kernels = {k: {"launches": v[0], "ms": round(v[2] * 1e3, 3),
                        "tflops": (round(v[1] / v[2] / 1e12, 2) if v[1] else None)} for k, v in sorted(per.items())}
         if flops_step is None:   # algorithmic FLOPs of the step = those of the MFMA kernels it launches
