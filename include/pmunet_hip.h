@@ -110,6 +110,12 @@ int pmu_conv3x3_fwd_wino(const pmu_frame* in, const float* wp, const float* bias
                          float* part, float* tee, void* stream);
 int pmu_conv3x3_dgrad_wino(const pmu_frame* dz, const float* wp, int Cin, int Csplit, float* dx0, float* dx1,
                            float* tee, void* stream);
+/* The same on a materialised operand (pmu_frame_to_f32 of the frame; the default fp32 path): xt /
+ * dzt [N][H][W][C] fp32 with C % 16 == 0, staged by LDS-DMA.  part rows = pmu_conv3x3_tiles_wino(). */
+int pmu_conv3x3_fwd_wino_raw(const float* xt, int Cin, int N, int H, int W, const float* wp, const float* bias,
+                             int Cout, float* z, float* part, void* stream);
+int pmu_conv3x3_dgrad_wino_raw(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                               int Csplit, float* dx0, float* dx1, void* stream);
 /* dw[Cout][Cin][3][3] from the teed operands dzt [N][H][W][Cout] and xt [N][H][W][Cin] (fp32), by
  * Winograd F(2x2,3x3): dw = G^T [sum over 2x2 tiles of (A dY A^T) .* (B^T X B)] G.  Cout % 32 == 0,
  * Cin % 64 == 0 (pmu_conv3x3_wgrad_ws_wino returns 0 otherwise); ws must hold that many bytes. */

@@ -381,8 +381,8 @@ constexpr int STAGE = A_FLOATS + U_FLOATS;
 static_assert(U_FLOATS / 4 / NT == 4, "4 U float4 (LDS-DMA) per thread per chunk");
 
 // EXP (timing experiments, PMU_WINO_EXP): 1 = no restaging (every chunk reuses the first), 2 = that
-// and no barrier, 3 = no input transform (results wrong for 1-3); 4 / 5 = commit in step 1 / 3
-// instead of 2 (correct).
+// and no barrier, 3 = no input transform, 6 = no U restaging, 7 = no operand restaging (results wrong
+// for 1-3, 6, 7); 4 / 5 = commit in step 1 / 3 instead of 2 (correct).
 template <bool DGRAD, int POOL, int EXP = 0>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
@@ -406,16 +406,19 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
   {                                                                                                        \
     const int k0_ = (CH) * BK;                                                                             \
     const bool second_ = F.nsrc > 1 && k0_ >= F.C0;                                                        \
-    pmu_prefetch<POOL, DGRAD, NI>(pmu_pick_src(F, second_), k0_ - (second_ ? F.C0 : 0) + cq4, g.n, ih, iw, pf); \
+    if (EXP != 7)                                                                                          \
+      pmu_prefetch<POOL, DGRAD, NI>(pmu_pick_src(F, second_), k0_ - (second_ ? F.C0 : 0) + cq4, g.n, ih, iw, pf); \
     const float* s_ = wsrc + (long long)(CH) * U_FLOATS;                                                   \
     float* d_ = (BUF) + A_FLOATS + wave_off;                                                               \
-    PMU_GLDS(s_, d_) PMU_GLDS(s_ + 4 * NT, d_ + 4 * NT) PMU_GLDS(s_ + 8 * NT, d_ + 8 * NT)                 \
-    PMU_GLDS(s_ + 12 * NT, d_ + 12 * NT)                                                                   \
+    if (EXP != 6) {                                                                                        \
+      PMU_GLDS(s_, d_) PMU_GLDS(s_ + 4 * NT, d_ + 4 * NT) PMU_GLDS(s_ + 8 * NT, d_ + 8 * NT)               \
+      PMU_GLDS(s_ + 12 * NT, d_ + 12 * NT)                                                                 \
+    }                                                                                                      \
   }
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
                                    (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
-#define PMU_WCOMMIT(BUF) pmu_commit<POOL, DGRAD, NI>(pf, ih, dst, (BUF));
+#define PMU_WCOMMIT(BUF) if (EXP != 7) pmu_commit<POOL, DGRAD, NI>(pf, ih, dst, (BUF));
   PMU_WPREFETCH(0, smem)
   PMU_WCOMMIT(smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -461,6 +464,142 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
 #undef PMU_WCOMMIT
 #undef PMU_GLDS
   wino_epilogue<DGRAD>(a, g, acc, smem);
+}
+
+// ---------------------------------------------------------------------------------------------
+// RAW-operand variant (the default fp32 path): the operand was materialised once (BN+ReLU / pool /
+// F.pad+cat applied, or the BN backward of dz) — the tensor the weight gradient reads anyway — so
+// the staging is a copy done by LDS-DMA (global_load_lds, no registers, no VALU), and each lane reads
+// its 4x4 patch once per chunk as 16 ds_read_b128 (4 channels: channel 4*kk + ks feeds step ks).
+// Halo rows are RROWP = 384 floats (2*RROWP = 0 mod 64), pixels 20 floats: with the tile/lane map
+// the b128 patch reads are conflict-free.  Units of the image outside the input are zeroed once
+// (their DMA lanes are masked), pad units are never written.
+// ---------------------------------------------------------------------------------------------
+constexpr int RROWP = 384;
+constexpr int R_A_FLOATS = HH * RROWP;
+constexpr int R_STAGE = R_A_FLOATS + U_FLOATS;
+constexpr int R_UNITS = R_A_FLOATS / 4;           // 16-B units of the operand image (data + pads)
+constexpr int R_NGL = (R_UNITS + NT - 1) / NT;    // operand DMA instructions per thread per chunk
+static_assert(R_NGL == 4, "operand image of 4 DMA rounds");
+
+template <bool DGRAD>
+__global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * R_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const WinoGeo g = wino_geo(a);
+  const DevFrame& F = a.in;
+  const float* x = F.s0.x;
+  const int KC = a.KC;
+  const int nchunks = KC / BK;
+
+  // this thread's operand units: global float offset (chunk 0) or -1 (outside the input / pad)
+  long long goff[R_NGL];
+#pragma unroll
+  for (int r = 0; r < R_NGL; ++r) {
+    const int u = r * NT + tid;
+    const int hr = u / (RROWP / 4), wu = u - hr * (RROWP / 4);
+    const int hc = wu / 5, q = wu - hc * 5;
+    const bool data = u < R_UNITS && q < 4 && hc < HW;
+    const int h = g.h0 - 1 + hr, w = g.w0 - 1 + hc;
+    const bool in = data && h >= 0 && w >= 0 && h < F.H && w < F.W;
+    goff[r] = in ? (((long long)g.n * F.H + h) * F.W + w) * KC + 4 * q : -1;
+    if (data && !in) {  // zero padding, in both stages, once
+      *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(smem + R_STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const float* wsrc = a.wp + (long long)g.cob_blk * nchunks * U_FLOATS + 4 * tid;
+  const int wave_off = (tid >> 6) * 256;
+#define PMU_GLDS(S, D)                                                                                      \
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
+                                   (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
+#define PMU_RFETCH(CH, BUF)                                                                                 \
+  {                                                                                                        \
+    const int k0_ = (CH) * BK;                                                                             \
+    float* b_ = (BUF);                                                                                     \
+    for (int r = 0; r < R_NGL; ++r)                                                                        \
+      if (goff[r] >= 0) PMU_GLDS(x + goff[r] + k0_, b_ + 4 * (r * NT) + wave_off)                          \
+    const float* s_ = wsrc + (long long)(CH) * U_FLOATS;                                                   \
+    float* d_ = b_ + R_A_FLOATS + wave_off;                                                                \
+    PMU_GLDS(s_, d_) PMU_GLDS(s_ + 4 * NT, d_ + 4 * NT) PMU_GLDS(s_ + 8 * NT, d_ + 8 * NT)                 \
+    PMU_GLDS(s_ + 12 * NT, d_ + 12 * NT)                                                                   \
+  }
+  f32x4 acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int lt = 16 * g.tg + (lane & 15);
+  const int pbase = (2 * (lt >> 3)) * RROWP + (2 * (lt & 7)) * LS + 4 * g.kk;
+  PMU_RFETCH(0, smem)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ch = 0; ch < nchunks; ++ch) {
+    float* cur = smem + (ch & 1) * R_STAGE;
+    if (ch + 1 < nchunks) PMU_RFETCH(ch + 1, smem + ((ch + 1) & 1) * R_STAGE)
+    const unsigned pa = lds_addr(cur + pbase);
+    // U of step ks for this lane: channel 4*kk + ks
+    const unsigned ua = lds_addr(cur + R_A_FLOATS + g.ubase) + (unsigned)(4 * g.kk * 4 * CO * 4 * 4);
+    float4 pt[16];
+#define PMU_P(I, J) pt[4 * I + J] = lds_b128<((I) * RROWP + (J) * LS) * 4>(pa);
+    PMU_P(0, 0) PMU_P(0, 1) PMU_P(0, 2) PMU_P(0, 3) PMU_P(1, 0) PMU_P(1, 1) PMU_P(1, 2) PMU_P(1, 3)
+    PMU_P(2, 0) PMU_P(2, 1) PMU_P(2, 2) PMU_P(2, 3) PMU_P(3, 0) PMU_P(3, 1) PMU_P(3, 2) PMU_P(3, 3)
+#undef PMU_P
+    float4 u[2][4];
+    wino_load_u(ua, u[0]);
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < BK / 4) wino_load_u(ua + (unsigned)((ks + 1) * 4 * CO * 4 * 4), u[(ks + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      float dd[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 t = pt[4 * i + j];
+          dd[i][j] = ks == 0 ? t.x : ks == 1 ? t.y : ks == 2 ? t.z : t.w;
+        }
+      float v[16];
+      input_transform(dd, v);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const float4 uu = u[ks & 1][gq];
+        acc[4 * gq + 0] = mfma16(v[4 * gq + 0], uu.x, acc[4 * gq + 0]);
+        acc[4 * gq + 1] = mfma16(v[4 * gq + 1], uu.y, acc[4 * gq + 1]);
+        acc[4 * gq + 2] = mfma16(v[4 * gq + 2], uu.z, acc[4 * gq + 2]);
+        acc[4 * gq + 3] = mfma16(v[4 * gq + 3], uu.w, acc[4 * gq + 3]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
+    __syncthreads();
+  }
+#undef PMU_RFETCH
+#undef PMU_GLDS
+  wino_epilogue<DGRAD>(a, g, acc, smem);
+}
+
+int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
+                    float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
+  PMU_REQUIRE(x && wp && out0 && KC > 0 && KC % BK == 0 && NOUT > 0 && N > 0 && H > 0 && W > 0);
+  WinoArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in.s0.x = x; a.in.s0.C = KC; a.in.s0.H = H; a.in.s0.W = W;
+  a.in.nsrc = 1; a.in.N = N; a.in.H = H; a.in.W = W; a.in.C0 = KC; a.in.C = KC; a.in.vec = 1;
+  a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part; a.tee = nullptr;
+  a.NOUT = NOUT; a.KC = KC; a.split = split;
+  a.tiles_w = pmu_cdiv(W, OW);
+  a.tiles_h = pmu_cdiv(H, OH);
+  a.nco = pmu_cdiv(NOUT, CO);
+  const long long blocks = (long long)a.nco * a.tiles_w * a.tiles_h * N;
+  PMU_REQUIRE(blocks < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  if (dgrad) hipLaunchKernelGGL((conv3x3_wino_raw_kernel<true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino_raw_kernel<false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
 }
 
 // a source the pipelined staging takes: float4 channels, chunks never straddle sources
@@ -520,6 +659,10 @@ int launch_wino(const pmu_frame* in, const float* wp, const float* bias, int NOU
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 4>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 5)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 5>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 6)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 6>), grid, dim3(NT), 0, st, a);
+      else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 7)
+        hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 7>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_NONE)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_MAX2)
@@ -572,4 +715,15 @@ extern "C" int pmu_conv3x3_dgrad_wino(const pmu_frame* dz, const float* wp, int 
   const int Cout = dz->src[0].C;
   PMU_REQUIRE(!tee || Cout % 4 == 0);
   return launch_wino(dz, wp, nullptr, Cin, Cout, dx0, dx1, Csplit, nullptr, tee, true, stream);
+}
+
+extern "C" int pmu_conv3x3_fwd_wino_raw(const float* xt, int Cin, int N, int H, int W, const float* wp,
+                                        const float* bias, int Cout, float* z, float* part, void* stream) {
+  return launch_wino_raw(xt, Cin, N, H, W, wp, bias, Cout, z, nullptr, Cout, part, false, stream);
+}
+
+extern "C" int pmu_conv3x3_dgrad_wino_raw(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                                          int Csplit, float* dx0, float* dx1, void* stream) {
+  PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
+  return launch_wino_raw(dzt, Cout, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
 }

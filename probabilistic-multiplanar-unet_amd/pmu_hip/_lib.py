@@ -51,6 +51,10 @@ SIGNATURES = {
     "pmu_conv3x3_tiles_wino": (c_int, [c_int, c_int, c_int]),
     "pmu_conv3x3_fwd_wino": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_wino": (c_int, [_FP, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_fwd_wino_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                         c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_wino_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                           c_void_p, c_void_p]),
     "pmu_conv3x3_wgrad_ws_wino": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_conv3x3_wgrad_wino": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                        c_size_t, c_void_p]),

@@ -220,8 +220,16 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             R = lb.pmu_conv3x3_tiles_wino(N, H, W)
             part = _empty(R, 2 * Cout, device=dev) if need_stats else None
             wp = pack_weights_wino(conv.weight, dgrad=False)
-            L.call("pmu_conv3x3_fwd_wino", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout,
-                   z.data_ptr(), L.ptr(part), L.ptr(xt32), s)
+            if wino_raw_ok(Cin):
+                # the operand materialised once (the weight gradient's operand anyway), then a
+                # DMA-staged Winograd GEMM on it
+                xm = frame_to_f32(srcs, N, H, W)
+                L.call("pmu_conv3x3_fwd_wino_raw", xm.data_ptr(), Cin, N, H, W, wp.data_ptr(), L.ptr(conv.bias),
+                       Cout, z.data_ptr(), L.ptr(part), s)
+                xt32 = xm if xt32 is not None else None
+            else:
+                L.call("pmu_conv3x3_fwd_wino", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout,
+                       z.data_ptr(), L.ptr(part), L.ptr(xt32), s)
         else:
             R = lb.pmu_conv3x3_tiles(N, H, W)
             part = _empty(R, 2 * Cout, device=dev) if need_stats else None
@@ -256,7 +264,7 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     if out.bf16:
         return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split)
     if out.xt32 is not None and need_dx:
-        return _conv_backward_tee32(out, dzf, conv, dw, split)
+        return _conv_backward_tee32(out, dz_src, conv, dw, split)
     if out.planes is not None:
         Cin = len(out.planes)
         wsb = lb.pmu_conv_first_wgrad_ws(N, H, W, Cin, Cout)
@@ -270,18 +278,26 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
         L.call("pmu_conv3x3_wgrad", dzf, frame_of(out.srcs, N, H, W), Cout, dw.data_ptr(), ws.data_ptr(), wsb, s)
     if not need_dx or out.planes is not None:
         return None
-    return _dgrad32(dzf, conv, N, H, W, split, None)
+    return _dgrad32(dz_src, conv, N, H, W, split, None)
 
 
-def _dgrad32(dzf, conv, N, H, W, split, tee):
-    """fp32 input gradient of a 3x3 conv (Winograd or direct); dx, or (dx0, dx1) split at ``split``."""
+def _dgrad32(dz_src, conv, N, H, W, split, tee):
+    """fp32 input gradient of a 3x3 conv (Winograd or direct); dx, or (dx0, dx1) split at ``split``.
+    tee: receives dz (the BN+ReLU backward applied) for the weight gradient."""
     s = L.stream()
     dev = conv.weight.device
-    Cin = conv.in_channels
+    Cin, Cout = conv.in_channels, conv.out_channels
     sp = Cin if split is None else split
     dx0 = _empty(N, H, W, sp, device=dev)
     dx1 = _empty(N, H, W, Cin - sp, device=dev) if split is not None else None
-    if use_wino():
+    dzf = frame_of([dz_src], N, H, W)
+    if use_wino() and wino_raw_ok(Cout):
+        dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
+        L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
+        wp = pack_weights_wino(conv.weight, dgrad=True)
+        L.call("pmu_conv3x3_dgrad_wino_raw", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
+               L.ptr(dx1), s)
+    elif use_wino():
         wp = pack_weights_wino(conv.weight, dgrad=True)
         L.call("pmu_conv3x3_dgrad_wino", dzf, wp.data_ptr(), Cin, sp, dx0.data_ptr(), L.ptr(dx1), L.ptr(tee), s)
     else:
@@ -291,7 +307,7 @@ def _dgrad32(dzf, conv, N, H, W, split, tee):
     return dx0 if split is None else (dx0, dx1)
 
 
-def _conv_backward_tee32(out: ConvBNOut, dzf, conv, dw, split):
+def _conv_backward_tee32(out: ConvBNOut, dz_src, conv, dw, split):
     """fp32 backward with materialised operands: the input-gradient kernel tees dz (BN+ReLU backward
     applied) as it stages it, and the weight gradient multiplies that with the operand the forward
     teed — both RAW frames, so its staging is a plain copy."""
@@ -301,7 +317,7 @@ def _conv_backward_tee32(out: ConvBNOut, dzf, conv, dw, split):
     dev = out.z.device
     Cin = conv.in_channels
     dzt = _empty(N, H, W, Cout, device=dev)
-    res = _dgrad32(dzf, conv, N, H, W, split, dzt)
+    res = _dgrad32(dz_src, conv, N, H, W, split, dzt)
     wsb = lb.pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout) if use_wino() else 0
     if wsb:
         ws = _empty((wsb + 3) // 4, device=dev)
@@ -396,6 +412,20 @@ def pack_weights_wino(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
 def use_wino() -> bool:
     """fp32 3x3 convs (fwd and input gradient) by Winograd F(2x2,3x3) (PMU_FP32_CONV=direct: direct sum)."""
     return os.environ.get("PMU_FP32_CONV", "wino") != "direct"
+
+
+def wino_raw_ok(C: int) -> bool:
+    """Winograd on a materialised operand (pmu_conv3x3_*_wino_raw): C % 16 == 0 (PMU_FP32_CONV=wino_fused
+    keeps the fused-staging Winograd kernels)."""
+    return C % 16 == 0 and os.environ.get("PMU_FP32_CONV", "wino") == "wino"
+
+
+def frame_to_f32(srcs, N, H, W) -> torch.Tensor:
+    """The fp32 operand of a frame, materialised NHWC (pmu_frame_to_f32)."""
+    C = sum(sr.C for sr in srcs)
+    out = _empty(N, H, W, C, device=srcs[0].x.device)
+    L.call("pmu_frame_to_f32", frame_of(srcs, N, H, W), out.data_ptr(), L.stream())
+    return out
 
 
 def pack_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:

@@ -130,3 +130,45 @@ def test_conv3x3_wgrad_wino(dev, N, H, W, Cin, Cout):
                                       dz.permute(0, 3, 1, 2).double().cpu(), padding=1)
     assert _rel(dw, ref) <= TOL
     assert L.lib().pmu_conv3x3_wgrad_ws_wino(N, H, W, 32, Cout) == 0  # Cin % 64 != 0: not taken
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 32, 32, 64, 64), (1, 37, 45, 16, 40), (3, 16, 16, 512, 96),
+                                            (2, 9, 7, 32, 10), (1, 70, 20, 48, 32)])
+def test_conv3x3_fwd_wino_raw(dev, N, H, W, Cin, Cout):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import pack_weights_wino
+    g = torch.Generator().manual_seed(41 + H + Cin)
+    x = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    z = torch.empty(N, H, W, Cout, device=dev)
+    part = torch.empty(L.lib().pmu_conv3x3_tiles_wino(N, H, W), 2 * Cout, device=dev)
+    wp = pack_weights_wino(w, False)
+    L.call("pmu_conv3x3_fwd_wino_raw", x.data_ptr(), Cin, N, H, W, wp.data_ptr(), b.data_ptr(), Cout, z.data_ptr(),
+           part.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = TF.conv2d(x.permute(0, 3, 1, 2).double().cpu(), w.double().cpu(), b.double().cpu(), padding=1)
+    ref = ref.permute(0, 2, 3, 1)
+    assert _rel(z, ref) <= TOL
+    tot = part.double().sum(0).cpu()
+    assert float(((tot[:Cout] - ref.sum((0, 1, 2))).abs() / ref.abs().sum((0, 1, 2))).max()) <= 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 40, 36, 64, 64, 64), (2, 17, 33, 128, 64, 64),
+                                                  (1, 16, 16, 96, 128, 32), (2, 9, 7, 12, 16, 12)])
+def test_conv3x3_dgrad_wino_raw(dev, N, H, W, Cin, Cout, split):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import pack_weights_wino
+    g = torch.Generator().manual_seed(5 + H + Cout)
+    dz = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    wp = pack_weights_wino(w, True)
+    dx0 = torch.empty(N, H, W, split, device=dev)
+    dx1 = torch.empty(N, H, W, Cin - split, device=dev) if split < Cin else None
+    L.call("pmu_conv3x3_dgrad_wino_raw", dz.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, split, dx0.data_ptr(),
+           L.ptr(dx1), L.stream())
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double().cpu(), dz.permute(0, 3, 1, 2).double().cpu(),
+                                     padding=1).permute(0, 2, 3, 1)
+    got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
+    assert _rel(got, ref) <= TOL

@@ -124,6 +124,11 @@ def main():
                                         None, dzt32.data_ptr(), s),
             "wgrad_t32": lambda: L.call("pmu_conv3x3_wgrad", frame_of([Src(dzt32)], N, H, W),
                                         frame_of([Src(xt32)], N, H, W), Cout, dw.data_ptr(), ws.data_ptr(), wsb, s),
+            "fwd_wr": lambda: L.call("pmu_conv3x3_fwd_wino_raw", xt32.data_ptr(), Cin, N, H, W, wwf.data_ptr(),
+                                       b.data_ptr(), Cout, out.data_ptr(), partw.data_ptr(), s),
+            "dgrad_wr": lambda: L.call("pmu_conv3x3_dgrad_wino_raw", dzt32.data_ptr(), Cout, N, H, W, wwd.data_ptr(),
+                                         Cin, Cin, dx.data_ptr(), None, s),
+            "mat32": lambda: L.call("pmu_frame_to_f32", fin, xt32.data_ptr(), s),
             "fwd_wino": lambda: L.call("pmu_conv3x3_fwd_wino", fin, wwf.data_ptr(), b.data_ptr(), Cout,
                                        out.data_ptr(), partw.data_ptr(), None, s),
             "dgrad_wino": lambda: L.call("pmu_conv3x3_dgrad_wino", fdz, wwd.data_ptr(), Cin, Cin, dx.data_ptr(),
