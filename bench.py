@@ -68,13 +68,18 @@ class KernelTimer:
             "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd",
             "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16", "pmu_convT2x2_fwd_bf16",
             "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16",
-            "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino", "pmu_conv3x3_wgrad_wino")
+            "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino", "pmu_conv3x3_wgrad_wino",
+            "pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw")
 
     def __init__(self):
         self.rec = []
 
     @staticmethod
     def _flops(name, args):
+        if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw"):
+            cin, N, H, W = args[1], args[2], args[3], args[4]
+            nout = args[7] if name.startswith("pmu_conv3x3_fwd") else args[6]
+            return 2.0 * 16 * N * ((H + 1) // 2) * ((W + 1) // 2) * cin * nout
         if name == "pmu_conv3x3_wgrad_wino":
             N, H, W, cout, cin = args[2], args[3], args[4], args[5], args[6]
             return 2.0 * 16 * N * ((H + 1) // 2) * ((W + 1) // 2) * cin * cout
@@ -203,7 +208,8 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_fwd": r"conv3x3_(pipe_)?kernel<false", "pmu_conv3x3_dgrad": r"conv3x3_(pipe_)?kernel<true",
     "pmu_conv3x3_wgrad": r"wgrad3x3_kernel<",
     "pmu_conv3x3_fwd_wino": r"conv3x3_wino_(pipe_)?kernel<false", "pmu_conv3x3_dgrad_wino": r"conv3x3_wino_(pipe_)?kernel<true",
-    "pmu_conv3x3_wgrad_wino": r"wgrad3x3_wino_kernel", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
+    "pmu_conv3x3_wgrad_wino": r"wgrad3x3_wino_kernel",
+    "pmu_conv3x3_fwd_wino_raw": r"conv3x3_wino_raw_kernel<false", "pmu_conv3x3_dgrad_wino_raw": r"conv3x3_wino_raw_kernel<true", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
     "pmu_convT2x2_dgrad": r"convT_pipe_kernel<true>|DuGatherA",
     "pmu_convT2x2_wgrad": r"convT_wgrad_(pipe_)?kernel", "pmu_fcomb_fwd": r"fcomb_fwd_kernel",
     "pmu_fcomb_bwd": r"fcomb_bwd_kernel",

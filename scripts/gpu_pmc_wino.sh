@@ -1,7 +1,7 @@
 set -u
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/pmcw; mkdir -p $O; cd $R
 export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -d $O/p1 -o p1 --output-format csv -- python tools/kbench.py --ops fwd_wino,fwd --only ${SHAPE:-32,512,512} --iters 2 > $O/p1.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES -d $O/p1 -o p1 --output-format csv -- python tools/kbench.py --ops ${OPS:-fwd_wino,fwd} --only ${SHAPE:-32,512,512} --iters 2 > $O/p1.log 2>&1 || exit $?
 find $O/p1 -name "*counter_collection.csv" | head -1 > $O/files.txt
 python - <<'PY'
 import csv, collections, os
