@@ -94,6 +94,43 @@ __device__ __forceinline__ void wgw_store(const WgwRegs& r, int tid, float* slot
   }
 }
 
+// LDS-DMA staging of one K-tile: the slot is the dz image (64 px x 10 units, 8 data) followed by the
+// x halo image (108 px x 18 units, 16 data); each global_load_lds wave-instruction fills 64 consecutive
+// units, its lanes' global sources chosen per unit.  Units outside the input are zeroed with a
+// ds_write instead (their DMA lanes masked); pad units are not written.
+constexpr int D_UPX = DLS / 4, X_UPX = XLS / 4;
+constexpr int D_UNITS = TH * TW * D_UPX;
+constexpr int W_UNITS = D_UNITS + HH * HWD * X_UPX;
+constexpr int W_NGL = (W_UNITS + NT - 1) / NT;
+static_assert(D_UNITS * 4 == D_FLOATS && W_UNITS * 4 == SLOT, "slot = dz image + x image");
+
+__device__ __forceinline__ void wgw_dma(const WgwArgs& a, int tile, int co0, int ci0, int tid, float* slot) {
+  int n, h0, w0;
+  wgw_origin(a, tile, n, h0, w0);
+  const int wbase = (tid >> 6) * 256;
+#pragma unroll
+  for (int r = 0; r < W_NGL; ++r) {
+    const int u = r * NT + tid;
+    // dz image unit (u < D_UNITS) or x halo unit, branch-free
+    const bool isd = u < D_UNITS;
+    const int pd = u / D_UPX, qd = u - pd * D_UPX;
+    const int v = u - D_UNITS;
+    const int px = v / X_UPX, qx = v - px * X_UPX;
+    const int hr = px / HWD, hc = px - hr * HWD;
+    const int h = isd ? h0 + (pd >> 4) : h0 - 1 + hr;
+    const int w = isd ? w0 + (pd & 15) : w0 - 1 + hc;
+    const bool data = isd ? qd < 8 : (u < W_UNITS && qx < 16);
+    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    const long long pix = ((long long)n * a.H + h) * a.W + w;
+    const float* src = isd ? a.dz + pix * a.Cout + co0 + 4 * qd : a.x + pix * a.Cin + ci0 + 4 * qx;
+    if (in)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(slot + 4 * r * NT + wbase), 16, 0, 0);
+    else if (data)
+      *reinterpret_cast<float4*>(slot + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 // operand values of one MFMA step: tiles 4s..4s+3 (k = lane >> 4), this lane's co (dz 2x2) and ci (x 4x4)
 struct WgwOps {
   float d[4];
@@ -162,29 +199,25 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
 #pragma unroll
   for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  WgwRegs regs;
-  if (t_beg < t_end) {
-    wgw_load(a, t_beg, co0, ci0, tid, regs);
-    wgw_store(regs, tid, smem);
-  }
+  if (t_beg < t_end) wgw_dma(a, t_beg, co0, ci0, tid, smem);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   for (int tile = t_beg; tile < t_end; ++tile) {
     const int cur = (tile - t_beg) & 1;
     const bool more = tile + 1 < t_end;
-    if (more) wgw_load(a, tile + 1, co0, ci0, tid, regs);  // in flight during the MFMAs
+    if (more) wgw_dma(a, tile + 1, co0, ci0, tid, smem + (cur ^ 1) * SLOT);  // lands during the MFMAs
     const float* slot = smem + cur * SLOT;
-    // each step's LDS reads are issued before the previous step's MFMAs; the next K-tile's stores
-    // go out inside step 2, under the MFMAs
+    // each step's LDS reads are issued before the previous step's MFMAs
     WgwOps ops[2];
     wgw_read(slot, 0, lane, cf, pf, ops[0]);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < 4) wgw_read(slot, s + 1, lane, cf, pf, ops[(s + 1) & 1]);
-      if (s == 2 && more) wgw_store(regs, tid, smem + (cur ^ 1) * SLOT);
       __builtin_amdgcn_sched_barrier(0);
       wgw_mfmas(ops[s & 1], acc);
     }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
