@@ -12,10 +12,11 @@
 //
 // Block: 512 threads, 32 output x 64 input channels, all 16 components; wave w owns the 16 x 16
 // (co, ci) fragment (w & 1, w >> 1) for every component (acc[16] of v_mfma_f32_16x16x4_f32, 64
-// registers).  K = tiles, in K-tiles of 64 output pixels (4 x 16 = 16 Winograd tiles, 4 MFMA steps);
-// the next K-tile's dzt / xt values are loaded into registers during the current one's MFMAs
-// (double-buffered LDS).  Split-K over blocks: each writes M for its tile range to a slab, and the
+// registers).  K = tiles, in K-tiles of 128 output pixels (8 x 16 = 32 Winograd tiles, 8 MFMA steps);
+// the next K-tile's dzt / xt images are fetched by LDS-DMA (global_load_lds) during the current
+// one's MFMAs (double-buffered LDS, 145 KB).  Split-K over blocks: each writes M for its tile range to a slab, and the
 // reduce kernel sums the slabs in a fixed order (deterministic) and applies G^T M G.
+#include <stdlib.h>
 #include "pmu_common.h"
 
 namespace {
@@ -24,14 +25,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 512;
 constexpr int WCO = 32, WCI = 64;        // channels per block
-constexpr int TH = 4, TW = 16;           // output pixels per K-tile
-constexpr int HH = TH + 2, HWD = TW + 2; // 6 x 18 operand halo
+constexpr int TH = 8, TW = 16;           // output pixels per K-tile
+constexpr int NSTEP = (TH / 2) * (TW / 2) / 4;  // MFMA steps (4 Winograd tiles each) per K-tile
+constexpr int HH = TH + 2, HWD = TW + 2; // 10 x 18 operand halo
 constexpr int DLS = WCO + 8;             // LDS floats per dz pixel (tile step 2 px = 80 = 16 mod 32: conflict-free)
 constexpr int XLS = WCI + 8;             // LDS floats per x pixel (72: 144 = 16 mod 32)
 constexpr int D_FLOATS = TH * TW * DLS;
 constexpr int X_FLOATS = HH * HWD * XLS;
 constexpr int SLOT = D_FLOATS + X_FLOATS;
-constexpr int NXI = 4;                   // x float4 items per thread: ceil(108 * 16 / 512)
 
 struct WgwArgs {
   const float* dz;  // [N][H][W][Cout]
@@ -44,12 +45,6 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// in-flight global loads of one K-tile for this thread
-struct WgwRegs {
-  float4 d;
-  float4 x[NXI];
-};
-
 __device__ __forceinline__ void wgw_origin(const WgwArgs& a, int tile, int& n, int& h0, int& w0) {
   int t = tile;
   const int tw = t % a.tiles_w; t /= a.tiles_w;
@@ -57,45 +52,8 @@ __device__ __forceinline__ void wgw_origin(const WgwArgs& a, int tile, int& n, i
   n = t; h0 = th * TH; w0 = tw * TW;
 }
 
-__device__ __forceinline__ void wgw_load(const WgwArgs& a, int tile, int co0, int ci0, int tid, WgwRegs& r) {
-  int n, h0, w0;
-  wgw_origin(a, tile, n, h0, w0);
-  {
-    const int px = tid >> 3, q = tid & 7;
-    const int h = h0 + (px >> 4), w = w0 + (px & 15);
-    const bool ok = h < a.H && w < a.W;
-    const long long idx = ok ? (((long long)n * a.H + h) * a.W + w) * a.Cout + co0 + 4 * q : 0;
-    r.d = *reinterpret_cast<const float4*>(a.dz + idx);
-    if (!ok) r.d = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-#pragma unroll
-  for (int i = 0; i < NXI; ++i) {
-    const int it = tid + NT * i;
-    const int px = it >> 4, q = it & 15;
-    const int hr = px / HWD, hc = px - hr * HWD;
-    const int h = h0 - 1 + hr, w = w0 - 1 + hc;
-    const bool ok = it < HH * HWD * 16 && h >= 0 && w >= 0 && h < a.H && w < a.W;
-    const long long idx = ok ? (((long long)n * a.H + h) * a.W + w) * a.Cin + ci0 + 4 * q : 0;
-    r.x[i] = *reinterpret_cast<const float4*>(a.x + idx);
-    if (!ok) r.x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
-__device__ __forceinline__ void wgw_store(const WgwRegs& r, int tid, float* slot) {
-  {
-    const int px = tid >> 3, q = tid & 7;
-    *reinterpret_cast<float4*>(slot + px * DLS + 4 * q) = r.d;
-  }
-  float* xs = slot + D_FLOATS;
-#pragma unroll
-  for (int i = 0; i < NXI; ++i) {
-    const int it = tid + NT * i;
-    if (it < HH * HWD * 16) *reinterpret_cast<float4*>(xs + (it >> 4) * XLS + 4 * (it & 15)) = r.x[i];
-  }
-}
-
-// LDS-DMA staging of one K-tile: the slot is the dz image (64 px x 10 units, 8 data) followed by the
-// x halo image (108 px x 18 units, 16 data); each global_load_lds wave-instruction fills 64 consecutive
+// LDS-DMA staging of one K-tile: the slot is the dz image (128 px x 10 units, 8 data) followed by the
+// x halo image (180 px x 18 units, 16 data); each global_load_lds wave-instruction fills 64 consecutive
 // units, its lanes' global sources chosen per unit.  Units outside the input are zeroed with a
 // ds_write instead (their DMA lanes masked); pad units are not written.
 constexpr int D_UPX = DLS / 4, X_UPX = XLS / 4;
@@ -148,6 +106,7 @@ __device__ __forceinline__ void wgw_read(const float* slot, int s, int lane, int
     for (int j = 0; j < 4; ++j) o.x[4 * i + j] = xp[(i * HWD + j) * XLS];
 }
 
+template <bool NOXF = false>
 __device__ __forceinline__ void wgw_mfmas(const WgwOps& o, f32x4 (&acc)[16]) {
   // Z = A dY A^T, A = [1 0; 1 1; 1 -1; 0 -1]
   const float d00 = o.d[0], d01 = o.d[1], d10 = o.d[2], d11 = o.d[3];
@@ -181,17 +140,29 @@ __device__ __forceinline__ void wgw_mfmas(const WgwOps& o, f32x4 (&acc)[16]) {
     v[4 * i + 2] = tt[i][2] - tt[i][1];
     v[4 * i + 3] = tt[i][1] - tt[i][3];
   }
+  if (NOXF) {  // timing experiment only: operands untransformed
+#pragma unroll
+    for (int c = 0; c < 16; ++c) { z[c] = o.x[c]; v[c] = o.x[c]; }
+  }
   __builtin_amdgcn_sched_barrier(0);  // all components first: the MFMAs then issue back to back
 #pragma unroll
   for (int c = 0; c < 16; ++c) acc[c] = mfma16(z[c], v[c], acc[c]);
 }
 
+// EXP (timing experiments, PMU_WINO_EXP): 1 = no restaging (every K-tile reuses the first),
+// 3 = no operand transforms; results are wrong for EXP != 0
+template <int EXP = 0>
 __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cf = wave & 1, pf = wave >> 1;
-  const int co0 = (blockIdx.x % a.nco) * WCO, ci0 = (blockIdx.x / a.nco) * WCI;
-  const int split = blockIdx.y;
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; remap so each XCD runs a
+  // contiguous range of logical blocks — the (co, ci) blocks of one split share its K-tiles in L2
+  const int nmn = gridDim.x, nb = nmn * gridDim.y, id = blockIdx.y * nmn + blockIdx.x;
+  const int xc = id & 7, q8 = nb >> 3, r8 = nb & 7;
+  const int lb = xc * q8 + (xc < r8 ? xc : r8) + (id >> 3);
+  const int mn = lb % nmn, split = lb / nmn;
+  const int co0 = (mn % a.nco) * WCO, ci0 = (mn / a.nco) * WCI;
   const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
   const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);
 
@@ -205,17 +176,17 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
   for (int tile = t_beg; tile < t_end; ++tile) {
     const int cur = (tile - t_beg) & 1;
     const bool more = tile + 1 < t_end;
-    if (more) wgw_dma(a, tile + 1, co0, ci0, tid, smem + (cur ^ 1) * SLOT);  // lands during the MFMAs
-    const float* slot = smem + cur * SLOT;
+    if (more && EXP != 1) wgw_dma(a, tile + 1, co0, ci0, tid, smem + (cur ^ 1) * SLOT);  // lands during the MFMAs
+    const float* slot = smem + (EXP == 1 ? 0 : cur * SLOT);
     // each step's LDS reads are issued before the previous step's MFMAs
     WgwOps ops[2];
     wgw_read(slot, 0, lane, cf, pf, ops[0]);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < NSTEP; ++s) {
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < 4) wgw_read(slot, s + 1, lane, cf, pf, ops[(s + 1) & 1]);
+      if (s + 1 < NSTEP) wgw_read(slot, s + 1, lane, cf, pf, ops[(s + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      wgw_mfmas(ops[s & 1], acc);
+      wgw_mfmas<EXP == 3>(ops[s & 1], acc);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
@@ -293,8 +264,14 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
   wgw_geometry(N, H, W, Cout, Cin, a);
   PMU_REQUIRE(ws_bytes >= (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float));
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(wgrad3x3_wino_kernel, dim3((unsigned)(a.nco * (Cin / WCI)), (unsigned)a.nsplit), dim3(NT), 0,
-                     st, a);
+  const dim3 grid((unsigned)(a.nco * (Cin / WCI)), (unsigned)a.nsplit);
+  static const int exp_ = [] {
+    const char* e = getenv("PMU_WINO_EXP");
+    return e ? atoi(e) : 0;
+  }();
+  if (exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino_kernel<1>), grid, dim3(NT), 0, st, a);
+  else if (exp_ == 3) hipLaunchKernelGGL((wgrad3x3_wino_kernel<3>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((wgrad3x3_wino_kernel<0>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   const long long CC = (long long)Cout * Cin;
   const int blocks = (int)((CC + 255) / 256);
