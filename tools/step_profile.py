@@ -20,6 +20,10 @@ MODE = {0: "raw", 1: "bnrelu", 2: "bnbwd"}
 
 def describe(name, args):
     try:
+        if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw"):
+            return f"{args[3]}x{args[4]} C{args[1]} -> {args[7] if 'fwd' in name else args[6]}"
+        if name == "pmu_conv3x3_wgrad_wino":
+            return f"{args[3]}x{args[4]} {args[5]}x{args[6]}"
         if name in ("pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw"):
             return f"{args[3]}x{args[4]} Cp{args[1]} -> {args[7] if name.endswith('fwd_raw') else args[6]}"
         if name == "pmu_conv3x3_wgrad_bf16":
@@ -51,7 +55,7 @@ def main():
     ns = argparse.Namespace(batch=16 if c5 else args.batch, size=512 if c5 else args.size, classes=3 if c5 else 1,
                             workload=args.workload, data="synthetic", channels=3 if c5 else 1,
                             precision=args.precision or ("bf16" if c5 else "fp32"))
-    build = bench.build_unet if args.workload == "unet" else bench.build_probunet
+    build = bench.build_probunet if args.workload == "probunet" else bench.build_unet
     step, _, _, _ = build(ns, torch.device("cuda", 0), 1, 0)
     for _ in range(2):
         step()
