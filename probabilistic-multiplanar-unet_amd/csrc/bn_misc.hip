@@ -93,11 +93,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
     const float4 is = *reinterpret_cast<const float4*>(invstd + c);
     float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
     if (pg < npg) {
-      for (int i = pg; i < ppb; i += npg) {
-        const long long p = p0 + i;
-        if (p >= P) break;
-        const float4 d = *reinterpret_cast<const float4*>(da + p * C + c);
-        const float4 zz = *reinterpret_cast<const float4*>(z + p * C + c);
+      // the block's pixels of this thread, in order; unrolled so 8 loads are in flight per thread
+      const long long pend = min(P, p0 + ppb);
+      const int nit = pend > p0 + pg ? (int)((pend - p0 - pg + npg - 1) / npg) : 0;
+      const float* dp = da + (p0 + pg) * C + c;
+      const float* zp = z + (p0 + pg) * C + c;
+      const long long step = (long long)npg * C;
+#pragma unroll 4
+      for (int it = 0; it < nit; ++it) {
+        const float4 d = *reinterpret_cast<const float4*>(dp + it * step);
+        const float4 zz = *reinterpret_cast<const float4*>(zp + it * step);
         const float dv[4] = {d.x, d.y, d.z, d.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
         const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
         const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
