@@ -520,43 +520,46 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  float4 ra0, ra1, rb0, rb1;
-  auto load = [&](int k0) {
-    long long off = k0 + kq;
-    if constexpr (DGRAD) {
-      const int ab = k0 / p.Cout;
-      off = ((long long)(ab >> 1) * p.Wd + (ab & 1)) * p.Cout + (k0 - ab * p.Cout) + kq;
-    }
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    ra0 = rok0 ? *reinterpret_cast<const float4*>(p.a + ab0 + off) : z4;
-    ra1 = rok1 ? *reinterpret_cast<const float4*>(p.a + ab1 + off) : z4;
-    rb0 = *reinterpret_cast<const float4*>(br0 + k0);
-    rb1 = *reinterpret_cast<const float4*>(br1 + k0);
-  };
-  auto store = [&](int buf, int k0) {
-    if constexpr (!DGRAD) {  // BN + ReLU of the producer, in registers (rows past M stay zero)
-      const float4 sc = *reinterpret_cast<const float4*>(p.coef + k0 + kq);
-      const float4 sh = *reinterpret_cast<const float4*>(p.coef + p.Cin + k0 + kq);
-      auto f = [&](float4 v) {
-        return make_float4(fmaxf(0.f, fmaf(v.x, sc.x, sh.x)), fmaxf(0.f, fmaf(v.y, sc.y, sh.y)),
-                           fmaxf(0.f, fmaf(v.z, sc.z, sh.z)), fmaxf(0.f, fmaf(v.w, sc.w, sh.w)));
-      };
-      if (rok0) ra0 = f(ra0);
-      if (rok1) ra1 = f(ra1);
-    }
-    *reinterpret_cast<float4*>(&As[buf][rl0 * PLS + kq]) = ra0;
-    *reinterpret_cast<float4*>(&As[buf][rl1 * PLS + kq]) = ra1;
-    *reinterpret_cast<float4*>(&Bs[buf][rl0 * PLS + kq]) = rb0;
-    *reinterpret_cast<float4*>(&Bs[buf][rl1 * PLS + kq]) = rb1;
-  };
+  // staging as macros over plain locals (captured by a lambda, the DGRAD registers went to scratch)
+  float4 ra0, ra1, rb0, rb1, rsc, rsh;
+#define PMU_TLOAD(K0)                                                                                       \
+  {                                                                                                        \
+    const int k0_ = (K0);                                                                                  \
+    long long off_ = k0_ + kq;                                                                             \
+    if constexpr (DGRAD) {                                                                                 \
+      const int ab_ = k0_ / p.Cout;                                                                        \
+      off_ = ((long long)(ab_ >> 1) * p.Wd + (ab_ & 1)) * p.Cout + (k0_ - ab_ * p.Cout) + kq;              \
+    } else { /* the chunk's BN coefficients travel with its operand (loaded under the MFMAs too) */       \
+      rsc = *reinterpret_cast<const float4*>(p.coef + k0_ + kq);                                           \
+      rsh = *reinterpret_cast<const float4*>(p.coef + p.Cin + k0_ + kq);                                   \
+    }                                                                                                      \
+    const float4 z4_ = make_float4(0.f, 0.f, 0.f, 0.f);                                                    \
+    ra0 = rok0 ? *reinterpret_cast<const float4*>(p.a + ab0 + off_) : z4_;                                 \
+    ra1 = rok1 ? *reinterpret_cast<const float4*>(p.a + ab1 + off_) : z4_;                                 \
+    rb0 = *reinterpret_cast<const float4*>(br0 + k0_);                                                     \
+    rb1 = *reinterpret_cast<const float4*>(br1 + k0_);                                                     \
+  }
+#define PMU_TBN(V) make_float4(fmaxf(0.f, fmaf((V).x, rsc.x, rsh.x)), fmaxf(0.f, fmaf((V).y, rsc.y, rsh.y)), \
+                               fmaxf(0.f, fmaf((V).z, rsc.z, rsh.z)), fmaxf(0.f, fmaf((V).w, rsc.w, rsh.w)))
+#define PMU_TSTORE(BUF)                                                                                     \
+  {                                                                                                        \
+    if constexpr (!DGRAD) { /* BN + ReLU of the producer, in registers (rows past M stay zero) */          \
+      if (rok0) ra0 = PMU_TBN(ra0);                                                                        \
+      if (rok1) ra1 = PMU_TBN(ra1);                                                                        \
+    }                                                                                                      \
+    *reinterpret_cast<float4*>(&As[BUF][rl0 * PLS + kq]) = ra0;                                            \
+    *reinterpret_cast<float4*>(&As[BUF][rl1 * PLS + kq]) = ra1;                                            \
+    *reinterpret_cast<float4*>(&Bs[BUF][rl0 * PLS + kq]) = rb0;                                            \
+    *reinterpret_cast<float4*>(&Bs[BUF][rl1 * PLS + kq]) = rb1;                                            \
+  }
 
   const int nch = p.K / PK;
-  load(0);
-  store(0, 0);
+  PMU_TLOAD(0)
+  PMU_TSTORE(0)
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
     const int cur = c & 1;
-    if (c + 1 < nch) load((c + 1) * PK);
+    if (c + 1 < nch) PMU_TLOAD((c + 1) * PK)
     float av[2][8], bv[2][8];
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
@@ -575,9 +578,12 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
       for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
         for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma_f32_32x32x2(av[fm][s], bv[fn][s], acc[fm][fn]);
-    if (c + 1 < nch) store(cur ^ 1, (c + 1) * PK);
+    if (c + 1 < nch) PMU_TSTORE(cur ^ 1)
     __syncthreads();
   }
+#undef PMU_TLOAD
+#undef PMU_TBN
+#undef PMU_TSTORE
   // epilogue
 #pragma unroll
   for (int fn = 0; fn < 2; ++fn) {
