@@ -17,6 +17,7 @@
 // one's MFMAs (double-buffered LDS, 145 KB).  Split-K over blocks: each writes M for its tile range to a slab, and the
 // reduce kernel sums the slabs in a fixed order (deterministic) and applies G^T M G.
 #include <stdlib.h>
+#include <string.h>
 #include "pmu_common.h"
 
 namespace {
@@ -203,6 +204,108 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row-split variant on v_mfma_f32_32x32x2_f32 (the default): wave w owns component row i = w & 3
+// (components 4i..4i+3) for 32 output x 32 input channels (half w >> 2 of the block's 64), acc[4] of
+// 32x32 (64 registers).  A step covers 2 Winograd tiles (k = lane >> 5).  Row i of B^T X B needs
+// only 2 of the 4 patch rows (tt = x[ra] + s x[rb]) and row i of A dY A^T one combination of the
+// dz rows, so a step costs 12 LDS reads and ~15 VALU for 4 MFMAs of 64 cycles — half the transform
+// work per MFMA cycle of the 16x16x4 layout above.
+// ---------------------------------------------------------------------------------------------
+constexpr int NSTEP2 = (TH / 2) * (TW / 2) / 2;  // 2 tiles per step
+
+struct WgwOps2 {
+  float d[4];   // dz 2x2 of (tile, co)
+  float xa[4];  // patch row ra of (tile, ci)
+  float xb[4];  // patch row rb
+};
+
+template <int EXP = 0>
+__global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = wave & 3, half = wave >> 2;
+  // B^T row `row` = x[ra] + sx * x[rb]; A row `row` of dY: alpha * d0 + beta * d1
+  const int ra = row == 0 ? 0 : row == 2 ? 2 : 1;
+  const int rb = row == 0 ? 2 : row == 1 ? 2 : row == 2 ? 1 : 3;
+  const float sx = row == 1 ? 1.f : -1.f;
+  const float alpha = row == 3 ? 0.f : 1.f;
+  const float beta = row == 0 ? 0.f : row == 1 ? 1.f : -1.f;
+  const int nmn = gridDim.x, nb = nmn * gridDim.y, id = blockIdx.y * nmn + blockIdx.x;
+  const int xc = id & 7, q8 = nb >> 3, r8 = nb & 7;
+  const int lb = xc * q8 + (xc < r8 ? xc : r8) + (id >> 3);
+  const int mn = lb % nmn, split = lb / nmn;
+  const int co0 = (mn % a.nco) * WCO, ci0 = (mn / a.nco) * WCI;
+  const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
+  const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+
+  auto read = [&](const float* slot, int s, WgwOps2& o) {
+    const int t = 2 * s + (lane >> 5);
+    const int ty = t >> 3, tx = t & 7;
+    const float* dp = slot + ((2 * ty) * TW + 2 * tx) * DLS + (lane & 31);
+    const float* xp = slot + D_FLOATS + ((2 * ty + ra) * HWD + 2 * tx) * XLS + 32 * half + (lane & 31);
+    const int db = (rb - ra) * HWD * XLS;
+    o.d[0] = dp[0]; o.d[1] = dp[DLS]; o.d[2] = dp[TW * DLS]; o.d[3] = dp[(TW + 1) * DLS];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o.xa[j] = xp[j * XLS];
+      o.xb[j] = xp[db + j * XLS];
+    }
+  };
+  if (t_beg < t_end) wgw_dma(a, t_beg, co0, ci0, tid, smem);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    const int cur = (tile - t_beg) & 1;
+    const bool more = tile + 1 < t_end;
+    if (more && EXP != 1) wgw_dma(a, tile + 1, co0, ci0, tid, smem + (cur ^ 1) * SLOT);
+    const float* slot = smem + (EXP == 1 ? 0 : cur * SLOT);
+    WgwOps2 ops[2];
+    read(slot, 0, ops[0]);
+#pragma unroll
+    for (int s = 0; s < NSTEP2; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < NSTEP2) read(slot, s + 1, ops[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const WgwOps2& o = ops[s & 1];
+      // Z row: r = alpha * dY[0] + beta * dY[1] (2 columns), then [r0, r0 + r1, r0 - r1, -r1]
+      const float r0 = fmaf(beta, o.d[2], alpha * o.d[0]);
+      const float r1 = fmaf(beta, o.d[3], alpha * o.d[1]);
+      float z[4] = {r0, r0 + r1, r0 - r1, -r1};
+      // V row: tt = x[ra] + sx * x[rb], then [t0 - t2, t1 + t2, t2 - t1, t1 - t3]
+      float tt[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tt[j] = fmaf(sx, o.xb[j], o.xa[j]);
+      float v[4] = {tt[0] - tt[2], tt[1] + tt[2], tt[2] - tt[1], tt[1] - tt[3]};
+      if (EXP == 3) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { z[k] = o.d[k]; v[k] = o.xa[k]; }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = mfma_f32_32x32x2(z[k], v[k], acc[k]);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // slab: ws[split][4*row + k][co][ci], D row = co (acc_row), col = ci (lane & 31)
+  const int ci = ci0 + 32 * half + (lane & 31);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + acc_row(r, lane);
+      a.ws[(((long long)split * 16 + 4 * row + k) * a.Cout + co) * a.Cin + ci] = acc[k][r];
+    }
+}
+
 // dw[co][ci][3][3] = G^T (sum over splits of M) G, G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]
 __global__ void wgrad_wino_reduce_kernel(const float* __restrict__ ws, int nsplit, int Cout, int Cin,
                                          float* __restrict__ dw) {
@@ -269,9 +372,19 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
     const char* e = getenv("PMU_WINO_EXP");
     return e ? atoi(e) : 0;
   }();
-  if (exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino_kernel<1>), grid, dim3(NT), 0, st, a);
-  else if (exp_ == 3) hipLaunchKernelGGL((wgrad3x3_wino_kernel<3>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((wgrad3x3_wino_kernel<0>), grid, dim3(NT), 0, st, a);
+  static const bool v16 = [] {
+    const char* e = getenv("PMU_WGRAD_WINO");
+    return e && strcmp(e, "16x16") == 0;
+  }();
+  if (v16) {  // the 16x16x4 layout (all components per wave)
+    if (exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino_kernel<1>), grid, dim3(NT), 0, st, a);
+    else if (exp_ == 3) hipLaunchKernelGGL((wgrad3x3_wino_kernel<3>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((wgrad3x3_wino_kernel<0>), grid, dim3(NT), 0, st, a);
+  } else {
+    if (exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino32_kernel<1>), grid, dim3(NT), 0, st, a);
+    else if (exp_ == 3) hipLaunchKernelGGL((wgrad3x3_wino32_kernel<3>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0>), grid, dim3(NT), 0, st, a);
+  }
   PMU_CHECK_LAUNCH();
   const long long CC = (long long)Cout * Cin;
   const int blocks = (int)((CC + 255) / 256);
