@@ -29,8 +29,11 @@ constexpr int WCO = 32, WCI = 64;        // channels per block
 constexpr int TH = 8, TW = 16;           // output pixels per K-tile
 constexpr int NSTEP = (TH / 2) * (TW / 2) / 4;  // MFMA steps (4 Winograd tiles each) per K-tile
 constexpr int HH = TH + 2, HWD = TW + 2; // 10 x 18 operand halo
-constexpr int DLS = WCO + 8;             // LDS floats per dz pixel (tile step 2 px = 80 = 16 mod 32: conflict-free)
-constexpr int XLS = WCI + 8;             // LDS floats per x pixel (72: 144 = 16 mod 32)
+// LDS floats per dz / x pixel: unpadded — the row-split kernel's 32-lane read groups all read one
+// pixel's consecutive channels (conflict-free at any pitch), and the DMA then moves no pad units.
+// (The 16x16x4 kernel's groups span two tiles and bank 2-way at this pitch; it is the fallback.)
+constexpr int DLS = WCO;
+constexpr int XLS = WCI;
 constexpr int D_FLOATS = TH * TW * DLS;
 constexpr int X_FLOATS = HH * HWD * XLS;
 constexpr int SLOT = D_FLOATS + X_FLOATS;
@@ -53,8 +56,8 @@ __device__ __forceinline__ void wgw_origin(const WgwArgs& a, int tile, int& n, i
   n = t; h0 = th * TH; w0 = tw * TW;
 }
 
-// LDS-DMA staging of one K-tile: the slot is the dz image (128 px x 10 units, 8 data) followed by the
-// x halo image (180 px x 18 units, 16 data); each global_load_lds wave-instruction fills 64 consecutive
+// LDS-DMA staging of one K-tile: the slot is the dz image (128 px x 8 units) followed by the
+// x halo image (180 px x 16 units); each global_load_lds wave-instruction fills 64 consecutive
 // units, its lanes' global sources chosen per unit.  Units outside the input are zeroed with a
 // ds_write instead (their DMA lanes masked); pad units are not written.
 constexpr int D_UPX = DLS / 4, X_UPX = XLS / 4;
@@ -78,7 +81,7 @@ __device__ __forceinline__ void wgw_dma(const WgwArgs& a, int tile, int co0, int
     const int hr = px / HWD, hc = px - hr * HWD;
     const int h = isd ? h0 + (pd >> 4) : h0 - 1 + hr;
     const int w = isd ? w0 + (pd & 15) : w0 - 1 + hc;
-    const bool data = isd ? qd < 8 : (u < W_UNITS && qx < 16);
+    const bool data = isd ? qd < WCO / 4 : (u < W_UNITS && qx < WCI / 4);
     const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
     const long long pix = ((long long)n * a.H + h) * a.W + w;
     const float* src = isd ? a.dz + pix * a.Cout + co0 + 4 * qd : a.x + pix * a.Cin + ci0 + 4 * qx;
