@@ -172,3 +172,47 @@ def test_conv3x3_dgrad_wino_raw(dev, N, H, W, Cin, Cout, split):
                                      padding=1).permute(0, 2, 3, 1)
     got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
     assert _rel(got, ref) <= TOL
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_unet_wino_matches_direct(dev, monkeypatch, fused):
+    """The whole c2 architecture, one training step, with the Winograd kernels (default: materialised
+    operands; or the fused-staging variant) and with the direct-sum kernels, both against the fp64
+    CPU oracle: the Winograd gradients are as close to fp64 as the direct ones (within 2x of the
+    direct path's own error, which is BN-amplified fp32 rounding at batch 2), outputs within 1e-4."""
+    from helpers import grad_err
+    from model import UNet
+    from oracle.unet_ref import unet_forward, unet_loss, unet_param_keys
+    torch.manual_seed(0)
+    net = UNet(1, 1, [64, 128, 256, 512, 1024])
+    sd0 = {k: v.clone() for k, v in net.state_dict().items()}
+    g = torch.Generator().manual_seed(4)
+    x = torch.rand(2, 1, 48, 64, generator=g)
+    target = (torch.rand(2, 1, 48, 64, generator=g) > 0.5).float()
+    keys = unet_param_keys(sd0)
+    sd = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in sd0.items()}
+    params = {k: sd[k].clone().requires_grad_(True) for k in keys}
+    work = dict(sd)
+    work.update(params)
+    unet_loss(unet_forward(work, x.double(), 5, 1), target.double(), 1).backward()
+    g64 = {k: params[k].grad for k in keys}
+
+    net = net.to(dev).train()
+    xd, td = x.to(dev), target.to(dev)
+
+    def step(mode):
+        monkeypatch.setenv("PMU_FP32_CONV", mode)
+        net.load_state_dict(sd0)
+        for p in net.parameters():
+            p.grad = None
+        out = net(xd)
+        torch.nn.functional.binary_cross_entropy(out, td).backward()
+        torch.cuda.synchronize()
+        return out.detach().clone(), {n: p.grad.detach().cpu().double() for n, p in net.named_parameters()}
+
+    o_d, g_d = step("direct")
+    o_w, g_w = step("wino_fused" if fused else "wino")
+    assert _rel(o_w, o_d) <= 1e-4
+    e_d, _ = grad_err(g_d, g64)
+    e_w, k_w = grad_err(g_w, g64)
+    assert e_w <= max(2 * e_d, 1e-4), (e_w, e_d, k_w)
