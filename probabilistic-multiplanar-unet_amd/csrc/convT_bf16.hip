@@ -359,15 +359,17 @@ __global__ __launch_bounds__(256) void convT_dbias_part_kernel(const float* __re
   __shared__ float4 red[256];
   const int nq = Cout / 4, PL = 256 / nq;
   const int t = threadIdx.x, qd = t % nq, pl = t / nq;
-  const long long npx = (long long)N * H2 * W2;
+  const unsigned npx = (unsigned)N * H2 * W2;  // < 2^32 (host-checked)
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (pl < PL) {
-    for (long long r = (long long)blockIdx.x * PL + pl; r < npx; r += (long long)gridDim.x * PL) {
-      const long long row = r / W2;
-      const int x = (int)(r - row * W2);
-      const long long n = row / H2;
-      const int y = (int)(row - n * H2);
-      const float4 v = *reinterpret_cast<const float4*>(du + ((n * Hd + oh + y) * Wd + ow + x) * Cout + 4 * qd);
+    const unsigned stride = gridDim.x * PL;
+    // pixels r, r + stride, ... in order; 4 loads in flight per thread
+#pragma unroll 4
+    for (unsigned r = blockIdx.x * PL + pl; r < npx; r += stride) {
+      const unsigned row = r / (unsigned)W2, x = r - row * W2;
+      const unsigned n = row / (unsigned)H2, y = row - n * H2;
+      const float4 v = *reinterpret_cast<const float4*>(
+          du + (((long long)n * Hd + oh + y) * Wd + ow + x) * Cout + 4 * qd);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
   }
@@ -398,12 +400,20 @@ __global__ __launch_bounds__(256) void convT_dbias_part1_kernel(const float* __r
     part[(long long)blockIdx.x * Cout + c] = s;
   }
 }
-__global__ void convT_dbias_sum_kernel(const float* __restrict__ part, int G, int Cout, float* __restrict__ db) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= Cout) return;
+// db[c] = sum of the G partial rows: 64 channels per block, 4 row groups summed in a fixed order
+__global__ __launch_bounds__(256) void convT_dbias_sum_kernel(const float* __restrict__ part, int G, int Cout,
+                                                              float* __restrict__ db) {
+  __shared__ float red[256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
   float s = 0.f;
-  for (int gidx = 0; gidx < G; ++gidx) s += part[(long long)gidx * Cout + c];
-  db[c] = s;
+  if (c < Cout) {
+    const int g0 = (G * grp) / 4, g1 = (G * (grp + 1)) / 4;
+#pragma unroll 4
+    for (int gidx = g0; gidx < g1; ++gidx) s += part[(long long)gidx * Cout + c];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (grp == 0 && c < Cout) db[c] = ((red[threadIdx.x] + red[64 + threadIdx.x]) + red[128 + threadIdx.x]) + red[192 + threadIdx.x];
 }
 
 static void twb_geometry(int N, int H, int W, int Cin, int Cout, int* ntiles, int* nsplit) {
@@ -414,7 +424,7 @@ static void twb_geometry(int N, int H, int W, int Cin, int Cout, int* ntiles, in
   if (sp > *ntiles) sp = *ntiles;
   *nsplit = sp;
 }
-constexpr int DB_G = 256;  // dbias partial rows
+constexpr int DB_G = 2048;  // dbias partial rows (blocks of the partial-sum pass: 8 per CU)
 
 }  // namespace
 
@@ -474,6 +484,7 @@ extern "C" int pmu_convT2x2_wgrad_bf16(const unsigned short* xt, const unsigned 
   PMU_REQUIRE(xt && dut && dw && ws && N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0);
   PMU_REQUIRE(off_h >= 0 && off_w >= 0 && off_h + 2 * H <= Hd && off_w + 2 * W <= Wd && (!dbias || du));
   PMU_REQUIRE(ws_bytes >= pmu_convT2x2_wgrad_ws_bf16(N, H, W, Cin, Cout));
+  PMU_REQUIRE((long long)N * 4 * H * W < (1LL << 32));  // the bias-sum pass decodes pixels in 32 bits
   TwbArgs a;
   a.xt = xt; a.dut = dut; a.ws = ws;
   a.N = N; a.H = H; a.W = W; a.Hd = Hd; a.Wd = Wd; a.oh = off_h; a.ow = off_w; a.Cin = Cin; a.Cout = Cout;
@@ -496,7 +507,7 @@ extern "C" int pmu_convT2x2_wgrad_bf16(const unsigned short* xt, const unsigned 
       hipLaunchKernelGGL(convT_dbias_part1_kernel, dim3(DB_G), dim3(256), 0, st, du, N, 2 * H, 2 * W, Hd, Wd, off_h,
                          off_w, Cout, part);
     PMU_CHECK_LAUNCH();
-    hipLaunchKernelGGL(convT_dbias_sum_kernel, dim3((unsigned)pmu_cdiv(Cout, 256)), dim3(256), 0, st, (const float*)part,
+    hipLaunchKernelGGL(convT_dbias_sum_kernel, dim3((unsigned)pmu_cdiv(Cout, 64)), dim3(256), 0, st, (const float*)part,
                        DB_G, Cout, dbias);
     PMU_CHECK_LAUNCH();
   }
