@@ -34,18 +34,21 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(FirstArgs a) {
     wl[k * a.Cout + co] = a.w[co * K9 + k];  // w[co][ci][kh][kw] -> k = ci*9+tap
   }
   __syncthreads();
-  const long long P = (long long)a.N * a.H * a.W;
-  const long long p0 = (long long)blockIdx.x * FPIX;
+  // 32-bit pixel decode (N*H*W < 2^31, host-checked): 64-bit divisions per pixel dominated this kernel
+  const unsigned P = (unsigned)a.N * a.H * a.W, Wu = (unsigned)a.W, Hu = (unsigned)a.H;
+  const unsigned p0 = blockIdx.x * FPIX;
   float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.bias) bias = *reinterpret_cast<const float4*>(a.bias + 4 * cq);
   float s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   if (pl < npl) {
     for (int i = pl; i < FPIX; i += npl) {
-      const long long p = p0 + i;
+      const unsigned p = p0 + i;
       if (p >= P) break;
-      const int w = (int)(p % a.W);
-      const int h = (int)((p / a.W) % a.H);
-      const int n = (int)(p / ((long long)a.W * a.H));
+      const unsigned t = p / Wu;
+      const int w = (int)(p - t * Wu);
+      const unsigned nn = t / Hu;
+      const int h = (int)(t - nn * Hu);
+      const int n = (int)nn;
       float o[4] = {bias.x, bias.y, bias.z, bias.w};
       for (int ci = 0; ci < a.Cin; ++ci) {
         const float* pl_ = a.planes[ci] + (long long)n * a.H * a.W;
@@ -58,7 +61,7 @@ __global__ __launch_bounds__(256) void conv_first_fwd_kernel(FirstArgs a) {
           o[2] = fmaf(x, wv.z, o[2]); o[3] = fmaf(x, wv.w, o[3]);
         }
       }
-      *reinterpret_cast<float4*>(a.z + p * a.Cout + 4 * cq) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(a.z + (long long)p * a.Cout + 4 * cq) = make_float4(o[0], o[1], o[2], o[3]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) { s1[e] += o[e]; s2[e] = fmaf(o[e], o[e], s2[e]); }
     }
@@ -256,6 +259,7 @@ extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, in
                                   void* stream) {
   PMU_REQUIRE(planes && Cin >= 1 && Cin <= 4 && N > 0 && H > 0 && W > 0 && w && z);
   PMU_REQUIRE(Cout >= 4 && Cout <= 256 && Cout % 4 == 0 && 256 % (Cout / 4) == 0);
+  PMU_REQUIRE((long long)N * H * W < (1LL << 31));
   FirstArgs a;
   for (int i = 0; i < 4; ++i) a.planes[i] = i < Cin ? planes[i] : nullptr;
   for (int i = 0; i < Cin; ++i) PMU_REQUIRE(planes[i]);
