@@ -254,6 +254,15 @@ def fcomb_flops(name, args):
     return 0.0
 
 
+def dp_sync(net, world):
+    """N > 1: bucketed gradient all-reduce overlapped with the backward (pmu_hip.dp); the
+    one-shot all-reduce after the backward with PMU_DP_OVERLAP=0."""
+    if world == 1 or os.environ.get("PMU_DP_OVERLAP", "1") == "0":
+        return None
+    from pmu_hip.dp import BucketAllReduce
+    return BucketAllReduce(net)
+
+
 def build_unet(args, dev, world, rank):
     """c2: UNet fwd + loss + bwd + (all-reduce) + fused clip/SGD on one batch of slices."""
     from model import UNet
@@ -266,6 +275,7 @@ def build_unet(args, dev, world, rank):
         for t in list(net.parameters()) + list(net.buffers()):
             dist.broadcast(t.data, 0)
     opt = FusedSGD(net.parameters(), lr=1e-3, momentum=0.9, clip=0.1)
+    sync = dp_sync(net, world)
     g = torch.Generator(device="cpu").manual_seed(1 + rank)
     B, S = args.batch, args.size
     crit = nn.BCELoss() if args.classes == 1 else nn.CrossEntropyLoss()
@@ -293,8 +303,12 @@ def build_unet(args, dev, world, rank):
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.precision == "bf16"):
             out = net(x)
         loss = crit(out, tgt)
+        if sync is not None:
+            sync.begin()
         loss.backward()
-        if world > 1:
+        if sync is not None:
+            sync.finish()
+        elif world > 1:
             dist.all_reduce(flat_grad_buffer(net, plist))
         opt.step(grad_scale=1.0 / world)
         return loss
@@ -409,6 +423,7 @@ def build_probunet(args, dev, world, rank):
         for t in list(net.parameters()) + list(net.buffers()):
             dist.broadcast(t.data, 0)
     opt = FusedSGD(net.parameters(), lr=1e-3, momentum=0.9, clip=0.1)
+    sync = dp_sync(net, world)
     g = torch.Generator(device="cpu").manual_seed(1 + rank)
     B, S = args.batch, args.size
     x = torch.rand(B, 1, S, S, generator=g).to(dev)
@@ -422,8 +437,12 @@ def build_probunet(args, dev, world, rank):
         net.forward(x, segm, training=True)
         net.sample(testing=False)
         loss = -net.elbo(segm)
+        if sync is not None:
+            sync.begin()
         loss.backward()
-        if world > 1:
+        if sync is not None:
+            sync.finish()
+        elif world > 1:
             dist.all_reduce(flat_grad_buffer(net, plist))
         opt.step(grad_scale=1.0 / world)
         with torch.no_grad():

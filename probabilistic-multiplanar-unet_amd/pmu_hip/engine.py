@@ -77,18 +77,32 @@ def _empty(*shape, dtype=F32, device=None):
 class GradSink(dict):
     """param -> gradient tensor.  ``new(p)`` hands out the destination a kernel writes: a view
     of the network's persistent flat gradient buffer when one is attached (stable pointers for
-    the fused optimizer / one-shot all-reduce), else a fresh tensor."""
+    the fused optimizer / one-shot all-reduce), else a fresh tensor.
 
-    def __init__(self, views=None):
+    ``on_ready`` (flat-buffer sinks only): called by ``flush()`` with the parameters whose
+    gradient kernels have been enqueued on the stream since the previous flush, so a
+    data-parallel reducer (pmu_hip.dp) can start a bucket's all-reduce while the rest of the
+    backward still runs."""
+
+    def __init__(self, views=None, on_ready=None):
         super().__init__()
         self.views = views
+        self.on_ready = on_ready if views is not None else None
+        self._pending = []
 
     def new(self, p):
         t = self.views.get(p) if self.views is not None else None
         if t is None:
             t = torch.empty_like(p)
         self[p] = t
+        if self.on_ready is not None:
+            self._pending.append(p)
         return t
+
+    def flush(self):
+        if self.on_ready is not None and self._pending:
+            ready, self._pending = self._pending, []
+            self.on_ready(ready)
 
 
 # ----------------------------------------------------------------------------------------
@@ -593,6 +607,7 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         ws = _empty(max(1, (wsb + 3) // 4), device=dev)
         L.call("pmu_wgrad1x1", dl.data_ptr(), frame_of([last.act()], N, H, W), K, dwo.data_ptr(), dbo.data_ptr(),
                ws.data_ptr(), wsb, s)
+        grads.flush()
     else:
         da = dy.permute(0, 2, 3, 1).contiguous()   # NCHW-shaped channels-last view -> NHWC
 
@@ -604,8 +619,10 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         us: UpState = st.ups[j]
         c1w, b1, c2w, b2 = _dc_layers(up.conv)
         da1 = conv_bn_backward(us.c2, da, c2w, b2, grads)
+        grads.flush()
         Cskip = us.c1.srcs[0].C
         dsk, dup = conv_bn_backward(us.c1, da1, c1w, b1, grads, split=Cskip)
+        grads.flush()
         dskip[nlev - 2 - j] = dsk
         convT = up.up
         prev = us.prev
@@ -637,6 +654,7 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             ws = _empty(max(1, (wsb + 3) // 4), device=dev)
             L.call("pmu_convT2x2_wgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1],
                    frame_of([prev.act()], N, hi, wi), Cup, dwt.data_ptr(), L.ptr(dbt), ws.data_ptr(), wsb, s)
+        grads.flush()
         da = dx
     # ---- encoder, deepest first; da = gradient w.r.t. the deepest encoder output
     for lev in reversed(range(nlev)):
@@ -648,7 +666,9 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         if lev != nlev - 1:
             da = dskip[lev]   # skip grad with the pooled path accumulated below
         da1 = conv_bn_backward(o2, da, c2w, b2, grads)
+        grads.flush()
         dpool = conv_bn_backward(o1, da1, c1w, b1, grads, need_dx=(lev > 0))
+        grads.flush()
         if lev > 0:
             prev = st.enc[lev - 1][1]
             hp, wp = prev.z.shape[1], prev.z.shape[2]

@@ -76,7 +76,7 @@ def grad_sink_for(module, params) -> GradSink:
         o = offs.get(id(p))
         if o is not None:
             views[p] = buf[o:o + p.numel()].view_as(p)
-    return GradSink(views)
+    return GradSink(views, on_ready=root.__dict__.get("_pmu_grad_ready"))
 
 
 # ----------------------------------------------------------------------------------------
@@ -103,6 +103,7 @@ class UNetFunction(torch.autograd.Function):
         net = ctx.net
         plist = list(net.parameters())
         grads = engine.unet_backward(net, ctx.st, dy, grad_sink_for(net, plist))
+        grads.flush()
         ctx.st = None
         return (None, None, None) + tuple(grads.get(p) for p in plist)
 
@@ -143,6 +144,7 @@ class GaussianFunction(torch.autograd.Function):
         g = ctx.g
         plist = list(g.parameters())
         grads = prob_engine.gaussian_backward(g, ctx.st, dmls, grad_sink_for(g, plist))
+        grads.flush()
         ctx.st = None
         return (None, None, None) + tuple(grads.get(p) for p in plist)
 
@@ -178,6 +180,7 @@ class FcombFunction(torch.autograd.Function):
         plist = list(fc.parameters())
         grads = grad_sink_for(fc, plist)
         dfeat, dz = prob_engine.fcomb_backward(fc, fh, zc, zb, dy, grads)
+        grads.flush()
         ctx.save = None
         # dfeat is NHWC storage; hand it back with the (N,F,H,W) shape of the features input
         return (None, dfeat.permute(0, 3, 1, 2), dz) + tuple(grads.get(p) for p in plist)

@@ -17,7 +17,9 @@ is data-parallel when launched with torch.distributed (one process per GPU, RCCL
   max(1, acc_steps // world)), every rank scales its loss by 1 / (micro-batches per step), and one
   SUM all-reduce of the flat gradient buffer yields exactly the reference's accumulated gradient
   (``dp_micro_batches`` / ``allreduce_grads``; checked against the reference's own accumulation in
-  tests/test_dp_gloo.py).  BatchNorm statistics stay per micro-batch, as in the reference.
+  tests/test_dp_gloo.py).  BatchNorm statistics stay per micro-batch, as in the reference.  The
+  all-reduce is bucketed and issued during the last micro-batch's backward (pmu_hip.dp;
+  PMU_DP_OVERLAP=0 selects the one-shot all-reduce after the backward).
 """
 from __future__ import annotations
 
@@ -149,6 +151,10 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, "min" if net.n_classes > 1 else "max",
                                                            factor=lrf, patience=lrp)
     plist = list(net.parameters())
+    sync = None
+    if world > 1 and os.environ.get("PMU_DP_OVERLAP", "1") != "0":
+        from pmu_hip.dp import BucketAllReduce
+        sync = BucketAllReduce(net)
     for epoch in range(epochs):
         net.train()
         # ---- train phase
@@ -157,14 +163,19 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
         scale = 1.0 / (per_rank * world)
         optimizer.zero_grad()
         for step_mbs in steps:
-            for mb in step_mbs:
+            for i, mb in enumerate(step_mbs):
                 b = dataset.get_batch(mb)
                 imgs = b["image"]
                 true_masks = b["mask"].to(dtype=trainer.mask_type)
                 masks_pred = trainer.predict(imgs, true_masks)
                 loss = trainer.loss(imgs, true_masks, masks_pred) * scale
+                if sync is not None and i == len(step_mbs) - 1:
+                    sync.begin()      # the last micro-batch's backward issues the bucket all-reduces
                 loss.backward()
-            allreduce_grads(net, plist)
+            if sync is not None:
+                sync.finish()
+            else:
+                allreduce_grads(net, plist)
             optimizer.step()
             optimizer.zero_grad()
             writer.add_scalar("Loss/train", loss.item(), global_step)

@@ -97,3 +97,87 @@ def test_dp_allreduce_matches_reference_accumulation(flat):
         assert err <= 1e-5, (rank, err, key)
     assert res[0][2] == res[1][2]                          # shared shuffle seed
     assert sorted(res[0][3] + res[1][3]) == list(range(32)) and not set(res[0][3]) & set(res[1][3])
+
+
+def _bucket_worker(rank, world, port, mode, q):
+    """Rank body of the bucketed, backward-overlapped all-reduce (pmu_hip.dp.BucketAllReduce)."""
+    import sys
+    for p in (os.path.join(ROOT, "probabilistic-multiplanar-unet_amd"), ROOT, os.path.dirname(__file__)):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(2)
+        from model import UNet
+        from oracle.unet_ref import unet_forward, unet_loss
+        from pmu_hip.dp import BucketAllReduce
+        from pmu_hip.functions import grad_sink_for
+        from train import dp_micro_batches
+        z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
+        net = UNet(1, 1, [16, 32])
+        sd = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("init/")}
+        net.load_state_dict(sd)
+        x, t = torch.from_numpy(z["x"]), torch.from_numpy(z["t"])
+        steps, per_rank = dp_micro_batches(list(range(32)), 4, 8, world, rank)
+        named = dict(net.named_parameters())
+        plist = list(net.parameters())
+        params = {k: named[k].detach().clone().requires_grad_(True) for k in named}
+        work = dict(sd)
+        work.update(params)
+        for mb in steps[0]:
+            idx = torch.tensor(mb)
+            (unet_loss(unet_forward(work, x[idx], 2, 1), t[idx], 1) / (per_rank * world)).backward()
+        sync = BucketAllReduce(net, bucket_bytes=16 << 10)   # several buckets on this small net
+        nb = len(sync.buckets)
+        # 2 rounds: the buffer and the bucket state are reused from step to step
+        for _ in range(2):
+            for p in plist:
+                p.grad = None
+            sync.begin()
+            order = list(named.items())
+            if mode != "forward_order":
+                order = order[::-1]                     # the order the HIP backward reports layers
+            if mode == "foreign":
+                for k, p in order:
+                    p.grad = params[k].grad.clone()      # accumulated outside the flat buffer
+            else:
+                sink = grad_sink_for(net, plist)
+                for k, p in order:
+                    g = sink.new(p)
+                    g.copy_(params[k].grad)
+                    p.grad = g
+                    sink.flush()                          # one layer's gradient kernels enqueued
+            issued = sync.issued_in_backward
+            sync.finish()
+        out = {k: p.grad.detach().numpy().copy() for k, p in named.items()}
+        q.put((rank, out, nb, issued))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["backward_order", "forward_order", "foreign"])
+def test_dp_bucketed_overlap_matches_reference_accumulation(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
+    ref = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("grad/")}
+    from helpers import grad_err
+    for rank, out, nb, issued in res:
+        err, key = grad_err({k: torch.from_numpy(out[k]) for k in ref}, ref)
+        assert err <= 1e-5, (mode, rank, err, key)
+        assert nb > 2
+        if mode == "backward_order":
+            assert issued == nb          # every bucket was issued from inside the "backward"
+        elif mode == "forward_order":
+            assert issued == nb          # the last report completes bucket 0, then all issue in order
+        else:
+            assert issued == 0           # no flat-buffer sink: nothing issued before finish()
