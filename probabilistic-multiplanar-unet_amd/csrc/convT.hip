@@ -8,6 +8,7 @@
 // du is the gradient of the concat's "up" half in the skip's frame; the convT output sits at
 // (off_h, off_w) inside it (F.pad, unet_parts.py:58-62).
 // Tile 128x128x16, 4 waves (2x2), wave tile 64x64 = 2x2 32x32 accumulators, LDS rows k-contiguous.
+#include <cstdlib>
 #include "pmu_stage.h"
 
 namespace {
@@ -481,9 +482,10 @@ struct PipeArgs {
   int Ncols, K;        // GEMM N and K
   int H, W, Cin, Cout;
   int Hd, Wd, off_h, off_w;
+  int lw, lh;          // fwd: log2 W, log2 H when powers of two, else -1
 };
 
-template <bool DGRAD>
+template <bool DGRAD, int EXP = 0>
 __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
   __shared__ __attribute__((aligned(16))) float As[2][PM * PLS];
   __shared__ __attribute__((aligned(16))) float Bs[2][PN * PLS];
@@ -533,9 +535,10 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
       rsc = *reinterpret_cast<const float4*>(p.coef + k0_ + kq);                                           \
       rsh = *reinterpret_cast<const float4*>(p.coef + p.Cin + k0_ + kq);                                   \
     }                                                                                                      \
-    const float4 z4_ = make_float4(0.f, 0.f, 0.f, 0.f);                                                    \
-    ra0 = rok0 ? *reinterpret_cast<const float4*>(p.a + ab0 + off_) : z4_;                                 \
-    ra1 = rok1 ? *reinterpret_cast<const float4*>(p.a + ab1 + off_) : z4_;                                 \
+    /* unconditional: rows past M read row 0 (row_base) and are zeroed at the store; a guarded */        \
+    /* load became 4 branchy dword loads per row */                                                        \
+    ra0 = *reinterpret_cast<const float4*>(p.a + ab0 + off_);                                              \
+    ra1 = *reinterpret_cast<const float4*>(p.a + ab1 + off_);                                              \
     rb0 = *reinterpret_cast<const float4*>(br0 + k0_);                                                     \
     rb1 = *reinterpret_cast<const float4*>(br1 + k0_);                                                     \
   }
@@ -543,10 +546,12 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
                                fmaxf(0.f, fmaf((V).z, rsc.z, rsh.z)), fmaxf(0.f, fmaf((V).w, rsc.w, rsh.w)))
 #define PMU_TSTORE(BUF)                                                                                     \
   {                                                                                                        \
-    if constexpr (!DGRAD) { /* BN + ReLU of the producer, in registers (rows past M stay zero) */          \
-      if (rok0) ra0 = PMU_TBN(ra0);                                                                        \
-      if (rok1) ra1 = PMU_TBN(ra1);                                                                        \
+    if constexpr (!DGRAD && EXP != 2) { /* BN + ReLU of the producer, in registers */                     \
+      ra0 = PMU_TBN(ra0);                                                                                  \
+      ra1 = PMU_TBN(ra1);                                                                                  \
     }                                                                                                      \
+    if (!rok0) ra0 = make_float4(0.f, 0.f, 0.f, 0.f); /* rows past M stay zero */                          \
+    if (!rok1) ra1 = make_float4(0.f, 0.f, 0.f, 0.f);                                                      \
     *reinterpret_cast<float4*>(&As[BUF][rl0 * PLS + kq]) = ra0;                                            \
     *reinterpret_cast<float4*>(&As[BUF][rl1 * PLS + kq]) = ra1;                                            \
     *reinterpret_cast<float4*>(&Bs[BUF][rl0 * PLS + kq]) = rb0;                                            \
@@ -601,17 +606,33 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
       const float b = p.bias ? p.bias[co] : 0.f;
       const unsigned Wu = (unsigned)p.W, Hu = (unsigned)p.H;  // 32-bit decode (M < 2^31, host-checked)
       float* outc = p.out + (long long)(ab >> 1) * 2 * p.W * p.Cout + (ab & 1) * p.Cout + co;
+      const bool full = m0 + PM <= p.M;
+      if (p.lw >= 0 && p.lh >= 0) {  // power-of-two H, W: shift/mask decode
 #pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
+        for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
-          if (m < (unsigned)p.M) {
-            const unsigned t = m / Wu, j = m - t * Wu;
-            const unsigned n = t / Hu, i = t - n * Hu;
-            outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * p.Cout] = acc[fm][fn][r] + b;
+          for (int r = 0; r < 16; ++r) {
+            const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
+            if (EXP == 1 && acc[fm][fn][r] != -1.2345f) continue;
+            if (full || m < (unsigned)p.M) {
+              const unsigned j = m & (Wu - 1), t = m >> p.lw;
+              const unsigned i = t & (Hu - 1), n = t >> p.lh;
+              outc[(size_t)(((n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j)) * (unsigned)p.Cout] = acc[fm][fn][r] + b;
+            }
           }
-        }
+      } else {
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
+            if (m < (unsigned)p.M) {
+              const unsigned t = m / Wu, j = m - t * Wu;
+              const unsigned n = t / Hu, i = t - n * Hu;
+              outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * p.Cout] = acc[fm][fn][r] + b;
+            }
+          }
+      }
     }
   }
 }
@@ -674,8 +695,18 @@ extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float
     p.a = in->src[0].x; p.coef = in->src[0].coef; p.bp = wp; p.bias = bias; p.out = u;
     p.M = M; p.Ncols = 4 * Cout; p.K = in->src[0].C;
     p.H = in->H; p.W = in->W; p.Cin = in->src[0].C; p.Cout = Cout;
+    auto log2_or = [](int v) { return (v & (v - 1)) == 0 ? __builtin_ctz((unsigned)v) : -1; };
+    p.lw = log2_or(in->W); p.lh = log2_or(in->H);
+    // the output index (((n*2H + 2i)*2W + 2j)*Cout + co) stays 32-bit in the shift path
+    if (4LL * M * Cout >= (1LL << 32)) p.lw = -1;
     dim3 grid((unsigned)pmu_cdiv(M, PM), (unsigned)(p.Ncols / PN));
-    hipLaunchKernelGGL(convT_pipe_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
+    static const int exp = [] {
+      const char* e = getenv("PMU_CONVT_EXP");
+      return e ? atoi(e) : 0;
+    }();
+    if (exp == 1) hipLaunchKernelGGL((convT_pipe_kernel<false, 1>), grid, dim3(256), 0, (hipStream_t)stream, p);
+    else if (exp == 2) hipLaunchKernelGGL((convT_pipe_kernel<false, 2>), grid, dim3(256), 0, (hipStream_t)stream, p);
+    else hipLaunchKernelGGL(convT_pipe_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }

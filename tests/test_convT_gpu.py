@@ -1,0 +1,50 @@
+"""ConvTranspose2d(k2, s2) of Up (PMU/model/unet/unet_parts.py:41-67) on the pipelined fp32 kernels,
+against a float64 CPU reference: the forward with the producer's BN+ReLU applied while staging
+(pmu_convT2x2_fwd), and the input gradient (pmu_convT2x2_dgrad).  Power-of-two maps take the
+shift/mask epilogue, the odd ones the division epilogue; M = N*H*W is not a multiple of the
+128-row tile in the odd cases."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "probabilistic-multiplanar-unet_amd"))
+
+TOL = 2e-5   # fp32 MFMA sums vs float64, relative to the output's max magnitude
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 16, 16, 128, 64), (3, 13, 10, 128, 64), (1, 8, 32, 256, 128),
+                                            (2, 7, 9, 64, 32)])
+def test_convT_fwd_dgrad_match_float64(N, H, W, Cin, Cout):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_of, pack_convT_weights
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(N * 1000 + H * 10 + W)
+    z = torch.randn(N, H, W, Cin, generator=g)
+    sc, sh = torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.2
+    w = torch.randn(Cin, Cout, 2, 2, generator=g) * 0.05
+    b = torch.randn(Cout, generator=g) * 0.1
+    du = torch.randn(N, 2 * H, 2 * W, Cout, generator=g)
+    # float64 reference
+    act = torch.relu(z.double() * sc.double() + sh.double()).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv_transpose2d(act, w.double(), b.double(), stride=2).permute(0, 2, 3, 1)
+    a = act.clone().requires_grad_(True)
+    torch.nn.functional.conv_transpose2d(a, w.double(), None, stride=2).backward(du.double().permute(0, 3, 1, 2))
+    ref_dx = a.grad.permute(0, 2, 3, 1)
+    # HIP
+    zd, wd, bd, dud = z.to(dev), w.to(dev), b.to(dev), du.to(dev)
+    coef = torch.cat([sc, sh]).to(dev)
+    u = torch.empty(N, 2 * H, 2 * W, Cout, device=dev)
+    dx = torch.empty(N, H, W, Cin, device=dev)
+    s = L.stream()
+    L.call("pmu_convT2x2_fwd", frame_of([Src(zd, L.SRC_BNRELU, coef)], N, H, W), wd.data_ptr(),
+           pack_convT_weights(wd, False).data_ptr(), bd.data_ptr(), Cout, u.data_ptr(), s)
+    L.call("pmu_convT2x2_dgrad", dud.data_ptr(), 2 * H, 2 * W, 0, 0, wd.data_ptr(),
+           pack_convT_weights(wd, True).data_ptr(), N, H, W, Cin, Cout, dx.data_ptr(), s)
+    torch.cuda.synchronize()
+    e_u = ((u.cpu().double() - ref).abs().max() / ref.abs().max()).item()
+    e_dx = ((dx.cpu().double() - ref_dx).abs().max() / ref_dx.abs().max()).item()
+    assert e_u <= TOL and e_dx <= TOL, (e_u, e_dx)
