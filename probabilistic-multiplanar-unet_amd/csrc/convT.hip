@@ -374,9 +374,15 @@ __global__ __launch_bounds__(256, 2) void convT_wgrad_pipe_kernel(TwArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * (TPIX * TB + 4 * TPIX * TB)];
   constexpr int SL = TPIX * TB + 4 * TPIX * TB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nci = a.Cin / TB;
-  const int ci0 = (blockIdx.x % nci) * TB, co0 = (blockIdx.x / nci) * TB;
-  const int split = blockIdx.y;
+  const int nci = a.Cin / TB, nblk = nci * (a.Cout / TB);
+  // 1-D grid, XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; remap so each XCD
+  // runs a contiguous range of logical blocks, i.e. all channel blocks of one K split (the same
+  // pixels) run together on one XCD and share their du / act tiles through its L2
+  const int nb = gridDim.x, x = blockIdx.x & 7, q = nb >> 3, rr = nb & 7;
+  const int lb = x * q + (x < rr ? x : rr) + (blockIdx.x >> 3);
+  const int bx = lb % nblk;
+  const int ci0 = (bx % nci) * TB, co0 = (bx / nci) * TB;
+  const int split = lb / nblk;
   const int cif = wave >> 1, cof = wave & 1;
   const bool do_bias = (a.bws != nullptr) && ci0 == 0;
   const DevSrc& xs = a.act.s0;
@@ -773,7 +779,7 @@ extern "C" int pmu_convT2x2_wgrad(const float* du, int Hd, int Wd, int off_h, in
   const bool pipe = act->nsrc == 1 && xs.mode == PMU_SRC_BNRELU && xs.pool == PMU_POOL_NONE && xs.off_h == 0 &&
                     xs.off_w == 0 && xs.H == act->H && xs.W == act->W && a.Cin % TB == 0 && Cout % TB == 0;
   if (pipe)
-    hipLaunchKernelGGL(convT_wgrad_pipe_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(convT_wgrad_pipe_kernel, dim3(grid.x * grid.y), dim3(256), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(convT_wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   PMU_CHECK_LAUNCH();

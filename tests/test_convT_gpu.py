@@ -1,6 +1,6 @@
 """ConvTranspose2d(k2, s2) of Up (PMU/model/unet/unet_parts.py:41-67) on the pipelined fp32 kernels,
 against a float64 CPU reference: the forward with the producer's BN+ReLU applied while staging
-(pmu_convT2x2_fwd), and the input gradient (pmu_convT2x2_dgrad).  Power-of-two maps take the
+(pmu_convT2x2_fwd), and the input gradient (pmu_convT2x2_dgrad) and the weight/bias gradient (pmu_convT2x2_wgrad).  Power-of-two maps take the
 shift/mask epilogue, the odd ones the division epilogue; M = N*H*W is not a multiple of the
 128-row tile in the odd cases."""
 import os
@@ -32,7 +32,9 @@ def test_convT_fwd_dgrad_match_float64(N, H, W, Cin, Cout):
     act = torch.relu(z.double() * sc.double() + sh.double()).permute(0, 3, 1, 2)
     ref = torch.nn.functional.conv_transpose2d(act, w.double(), b.double(), stride=2).permute(0, 2, 3, 1)
     a = act.clone().requires_grad_(True)
-    torch.nn.functional.conv_transpose2d(a, w.double(), None, stride=2).backward(du.double().permute(0, 3, 1, 2))
+    wr = w.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    torch.nn.functional.conv_transpose2d(a, wr, br, stride=2).backward(du.double().permute(0, 3, 1, 2))
     ref_dx = a.grad.permute(0, 2, 3, 1)
     # HIP
     zd, wd, bd, dud = z.to(dev), w.to(dev), b.to(dev), du.to(dev)
@@ -44,7 +46,16 @@ def test_convT_fwd_dgrad_match_float64(N, H, W, Cin, Cout):
            pack_convT_weights(wd, False).data_ptr(), bd.data_ptr(), Cout, u.data_ptr(), s)
     L.call("pmu_convT2x2_dgrad", dud.data_ptr(), 2 * H, 2 * W, 0, 0, wd.data_ptr(),
            pack_convT_weights(wd, True).data_ptr(), N, H, W, Cin, Cout, dx.data_ptr(), s)
+    dw = torch.empty_like(wd)
+    db = torch.empty(Cout, device=dev)
+    wsb = L.lib().pmu_convT2x2_wgrad_ws(N, H, W, Cin, Cout)
+    ws = torch.empty(max(1, (wsb + 3) // 4), device=dev)
+    L.call("pmu_convT2x2_wgrad", dud.data_ptr(), 2 * H, 2 * W, 0, 0, frame_of([Src(zd, L.SRC_BNRELU, coef)], N, H, W),
+           Cout, dw.data_ptr(), db.data_ptr(), ws.data_ptr(), wsb, s)
     torch.cuda.synchronize()
+    e_w = ((dw.cpu().double() - wr.grad).abs().max() / wr.grad.abs().max()).item()
+    e_b = ((db.cpu().double() - br.grad).abs().max() / br.grad.abs().max()).item()
+    assert e_w <= TOL and e_b <= TOL, (e_w, e_b)
     e_u = ((u.cpu().double() - ref).abs().max() / ref.abs().max()).item()
     e_dx = ((dx.cpu().double() - ref_dx).abs().max() / ref_dx.abs().max()).item()
     assert e_u <= TOL and e_dx <= TOL, (e_u, e_dx)
