@@ -9,8 +9,6 @@ namespace {
 // ---------------------------------------------------------------------------------
 // First layer: Cin <= 4 input planes (NCHW-style, one pointer per channel), VALU.
 // ---------------------------------------------------------------------------------
-constexpr int FPIX = 256;  // pixels per block
-
 struct FirstArgs {
   const float* planes[4];
   int Cin, N, H, W, Cout;
@@ -20,55 +18,73 @@ struct FirstArgs {
   float* part;
 };
 
-// thread = (channel quad cq, pixel lane pl); 256 / (Cout/4) pixel lanes per block step
-__global__ __launch_bounds__(256) void conv_first_fwd_kernel(FirstArgs a) {
-  __shared__ float wl[4 * 9 * 256];  // [ci*9+tap][co], Cout <= 256
+// Tiled forward: block = 8 x 32 output pixels of one image x all Cout.  The (8+2) x (32+2) x CIN
+// input patch is staged in LDS once (zero halo), each thread keeps its channel quad's 9*CIN
+// weight float4 in registers, and per pixel reads the 9*CIN inputs from LDS (one address per pixel:
+// broadcast over the quad lanes) into packed 2-wide FMAs.  The per-pixel global loads of the
+// untiled kernel (27 per pixel at CIN = 3) and its LDS weight reads made it ~5x slower than the
+// z write it must do.
+constexpr int FT_H = 8, FT_W = 32, FT_PH = FT_H + 2, FT_PW = FT_W + 2;
+
+typedef float pmu_f2 __attribute__((ext_vector_type(2)));
+
+template <int CIN>
+__global__ __launch_bounds__(256) void conv_first_fwd_tile_kernel(FirstArgs a, int tiles_w, int tiles_h) {
+  __shared__ float patch[CIN * FT_PH * FT_PW];
   __shared__ float red[256 * 8];
   const int tid = threadIdx.x;
-  const int CQ = a.Cout >> 2;
-  const int npl = 256 / CQ;
+  const int CQ = a.Cout >> 2, npl = 256 / CQ;
   const int cq = tid % CQ, pl = tid / CQ;
-  const int K9 = a.Cin * 9;
-  for (int i = tid; i < K9 * a.Cout; i += 256) {
-    const int co = i % a.Cout, k = i / a.Cout;
-    wl[k * a.Cout + co] = a.w[co * K9 + k];  // w[co][ci][kh][kw] -> k = ci*9+tap
+  int t = blockIdx.x;
+  const int tw = t % tiles_w; t /= tiles_w;
+  const int th = t % tiles_h;
+  const int n = t / tiles_h;
+  const int h0 = th * FT_H, w0 = tw * FT_W;
+  const unsigned HW = (unsigned)a.H * (unsigned)a.W;
+  for (int e = tid; e < CIN * FT_PH * FT_PW; e += 256) {
+    const int ci = e / (FT_PH * FT_PW), r = e - ci * (FT_PH * FT_PW);
+    const int ph = r / FT_PW, pw = r - ph * FT_PW;
+    const int h = h0 - 1 + ph, w = w0 - 1 + pw;
+    float v = 0.f;
+    if (h >= 0 && h < a.H && w >= 0 && w < a.W) v = a.planes[ci][(unsigned)n * HW + (unsigned)(h * a.W + w)];
+    patch[e] = v;
+  }
+  pmu_f2 wlo[CIN * 9], whi[CIN * 9];  // w[co = 4cq + {0,1}], w[4cq + {2,3}] per (ci, tap)
+#pragma unroll
+  for (int k = 0; k < CIN * 9; ++k) {
+    wlo[k] = pmu_f2{a.w[(4 * cq + 0) * CIN * 9 + k], a.w[(4 * cq + 1) * CIN * 9 + k]};
+    whi[k] = pmu_f2{a.w[(4 * cq + 2) * CIN * 9 + k], a.w[(4 * cq + 3) * CIN * 9 + k]};
+  }
+  pmu_f2 blo = {0.f, 0.f}, bhi = {0.f, 0.f};
+  if (a.bias) {
+    blo = pmu_f2{a.bias[4 * cq], a.bias[4 * cq + 1]};
+    bhi = pmu_f2{a.bias[4 * cq + 2], a.bias[4 * cq + 3]};
   }
   __syncthreads();
-  // 32-bit pixel decode (N*H*W < 2^31, host-checked): 64-bit divisions per pixel dominated this kernel
-  const unsigned P = (unsigned)a.N * a.H * a.W, Wu = (unsigned)a.W, Hu = (unsigned)a.H;
-  const unsigned p0 = blockIdx.x * FPIX;
-  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.bias) bias = *reinterpret_cast<const float4*>(a.bias + 4 * cq);
-  float s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
-  if (pl < npl) {
-    for (int i = pl; i < FPIX; i += npl) {
-      const unsigned p = p0 + i;
-      if (p >= P) break;
-      const unsigned t = p / Wu;
-      const int w = (int)(p - t * Wu);
-      const unsigned nn = t / Hu;
-      const int h = (int)(t - nn * Hu);
-      const int n = (int)nn;
-      float o[4] = {bias.x, bias.y, bias.z, bias.w};
-      for (int ci = 0; ci < a.Cin; ++ci) {
-        const float* pl_ = a.planes[ci] + (long long)n * a.H * a.W;
+  pmu_f2 s1lo = {0.f, 0.f}, s1hi = {0.f, 0.f}, s2lo = {0.f, 0.f}, s2hi = {0.f, 0.f};
+  for (int i = pl; i < FT_H * FT_W; i += npl) {
+    const int r = i / FT_W, c = i - r * FT_W;
+    const int h = h0 + r, w = w0 + c;
+    if (h >= a.H || w >= a.W) continue;
+    pmu_f2 olo = blo, ohi = bhi;
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
-          const float x = (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) ? pl_[hh * a.W + ww] : 0.f;
-          const float4 wv = *reinterpret_cast<const float4*>(wl + (ci * 9 + tap) * a.Cout + 4 * cq);
-          o[0] = fmaf(x, wv.x, o[0]); o[1] = fmaf(x, wv.y, o[1]);
-          o[2] = fmaf(x, wv.z, o[2]); o[3] = fmaf(x, wv.w, o[3]);
-        }
+    for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const float x = patch[(ci * FT_PH + r + tap / 3) * FT_PW + c + tap % 3];
+        const pmu_f2 x2 = {x, x};
+        olo = __builtin_elementwise_fma(x2, wlo[ci * 9 + tap], olo);
+        ohi = __builtin_elementwise_fma(x2, whi[ci * 9 + tap], ohi);
       }
-      *reinterpret_cast<float4*>(a.z + (long long)p * a.Cout + 4 * cq) = make_float4(o[0], o[1], o[2], o[3]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { s1[e] += o[e]; s2[e] = fmaf(o[e], o[e], s2[e]); }
-    }
+    const unsigned p = (unsigned)n * HW + (unsigned)(h * a.W + w);
+    *reinterpret_cast<float4*>(a.z + (size_t)p * a.Cout + 4 * cq) = make_float4(olo.x, olo.y, ohi.x, ohi.y);
+    s1lo += olo; s1hi += ohi;
+    s2lo = __builtin_elementwise_fma(olo, olo, s2lo);
+    s2hi = __builtin_elementwise_fma(ohi, ohi, s2hi);
   }
   if (!a.part) return;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) { red[tid * 8 + e] = s1[e]; red[tid * 8 + 4 + e] = s2[e]; }
+  red[tid * 8 + 0] = s1lo.x; red[tid * 8 + 1] = s1lo.y; red[tid * 8 + 2] = s1hi.x; red[tid * 8 + 3] = s1hi.y;
+  red[tid * 8 + 4] = s2lo.x; red[tid * 8 + 5] = s2lo.y; red[tid * 8 + 6] = s2hi.x; red[tid * 8 + 7] = s2hi.y;
   __syncthreads();
   if (tid < CQ) {
     float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
@@ -251,7 +267,7 @@ __global__ void rows_sum_kernel(const float* __restrict__ ws, int R, int Wd, flo
 }  // namespace
 
 extern "C" int pmu_conv_first_tiles(int N, int H, int W) {
-  return pmu_cdiv((long long)N * H * W, FPIX);
+  return N * pmu_cdiv(H, FT_H) * pmu_cdiv(W, FT_W);
 }
 
 extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,
@@ -264,8 +280,15 @@ extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, in
   for (int i = 0; i < 4; ++i) a.planes[i] = i < Cin ? planes[i] : nullptr;
   for (int i = 0; i < Cin; ++i) PMU_REQUIRE(planes[i]);
   a.Cin = Cin; a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.w = w; a.bias = bias; a.z = z; a.part = part;
-  hipLaunchKernelGGL(conv_first_fwd_kernel, dim3((unsigned)pmu_conv_first_tiles(N, H, W)), dim3(256), 0,
-                     (hipStream_t)stream, a);
+  const int tw = pmu_cdiv(W, FT_W), th = pmu_cdiv(H, FT_H);
+  const dim3 grid((unsigned)pmu_conv_first_tiles(N, H, W));
+  hipStream_t st = (hipStream_t)stream;
+  switch (Cin) {
+    case 1: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<1>, grid, dim3(256), 0, st, a, tw, th); break;
+    case 2: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<2>, grid, dim3(256), 0, st, a, tw, th); break;
+    case 3: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<3>, grid, dim3(256), 0, st, a, tw, th); break;
+    default: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<4>, grid, dim3(256), 0, st, a, tw, th); break;
+  }
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
