@@ -154,84 +154,110 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(FirstWgArgs a) {
   }
 }
 
-// Fast path (dz = one unpooled BN-backward source, Cout % 4 == 0): thread = (channel quad, pixel
-// group); float4 loads of da and z with the quad's BN-backward coefficients in registers; the
-// 3x3 x CIN input neighbourhood read once per pixel; partial dW reduced over the pixel groups of
-// a wave by shuffles, over the 4 waves through LDS, and over blocks by rows_sum4_kernel.
-constexpr int FWP2 = 4096;  // pixels per block (fast path)
+// Fast path (dz = one unpooled BN-backward source, Cout % 4 == 0, tiled): a block walks FW_TPB consecutive 8 x 32 pixel tiles (the tile order of the
+// forward).  Each tile's (8+2) x (32+2) x CIN input patch goes through LDS (the next tile's patch
+// values are loaded into registers under the current tile's FMAs), so the 9*CIN input reads per
+// pixel are LDS broadcasts instead of the global loads of the untiled kernel; dz is formed from
+// float4 loads of da and z (BN-backward coefficients of the thread's channel quad in registers).
+constexpr int FW_TPB = 16;  // tiles per block
 
 template <int CIN>
-__global__ __launch_bounds__(256) void conv_first_wgrad_fast_kernel(FirstWgArgs a) {
-  constexpr int K9 = CIN * 9;
+__global__ __launch_bounds__(256) void conv_first_wgrad_tile_kernel(FirstWgArgs a, int tiles_w, int tiles_h,
+                                                                    int ntiles) {
+  constexpr int K9 = CIN * 9, PE = CIN * FT_PH * FT_PW, NPE = (PE + 255) / 256;
+  __shared__ float patch[PE];
   __shared__ float red[512 * K9];  // [slot][Cout][K9]: 4 slots x Cout <= 128, or 1 slot x Cout = 256
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const DevSrc& s = a.dz.s0;
   const int Cout = a.Cout, CQ = Cout >> 2, PG = 256 / CQ;
   const int cq = tid % CQ, pg = tid / CQ;
   const int H = a.dz.H, W = a.dz.W;
-  const long long P = (long long)a.dz.N * H * W;
+  const unsigned HW = (unsigned)H * (unsigned)W;
   const int c = 4 * cq;
   const float4 sc = *reinterpret_cast<const float4*>(s.coef + c);
   const float4 sh = *reinterpret_cast<const float4*>(s.coef + Cout + c);
   const float4 mu = *reinterpret_cast<const float4*>(s.coef + 2 * Cout + c);
   const float4 kx = *reinterpret_cast<const float4*>(s.coef + 3 * Cout + c);
   const float4 kc = *reinterpret_cast<const float4*>(s.coef + 4 * Cout + c);
-  float acc[4][K9];
+  pmu_f2 acc[2][K9];  // channels {4cq, 4cq+1} and {4cq+2, 4cq+3}
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
+  for (int k = 0; k < K9; ++k) { acc[0][k] = pmu_f2{0.f, 0.f}; acc[1][k] = pmu_f2{0.f, 0.f}; }
+  const int t_beg = blockIdx.x * FW_TPB, t_end = min(ntiles, t_beg + FW_TPB);
+  float pv[NPE];
+  auto load_patch = [&](int tile) {
+    int t = tile;
+    const int tw = t % tiles_w; t /= tiles_w;
+    const int th = t % tiles_h;
+    const int n = t / tiles_h;
+    const int h0 = th * FT_H, w0 = tw * FT_W;
 #pragma unroll
-    for (int k = 0; k < K9; ++k) acc[e][k] = 0.f;
-  long long p = (long long)blockIdx.x * FWP2 + pg;
-  const long long pend = min(P, (long long)(blockIdx.x + 1) * FWP2);
-  // incremental (n, h, w) of p
-  int w = (int)(p % W);
-  long long t = p / W;
-  int h = (int)(t % H);
-  long long n = t / H;
-  for (; p < pend; p += PG) {
-    const float4 d = *reinterpret_cast<const float4*>(s.x + p * Cout + c);
-    const float4 z = *reinterpret_cast<const float4*>(s.z + p * Cout + c);
-    float g[4];
-    g[0] = pmu_bnbwd1(d.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x);
-    g[1] = pmu_bnbwd1(d.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y);
-    g[2] = pmu_bnbwd1(d.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z);
-    g[3] = pmu_bnbwd1(d.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w);
-#pragma unroll
-    for (int ci = 0; ci < CIN; ++ci) {
-      const float* pl = a.planes[ci] + n * H * W;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
-        const bool in = hh >= 0 && hh < H && ww >= 0 && ww < W;
-        const float x = in ? pl[hh * W + ww] : 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e][ci * 9 + tap] = fmaf(g[e], x, acc[e][ci * 9 + tap]);
-      }
+    for (int q = 0; q < NPE; ++q) {
+      const int e = tid + 256 * q;
+      const int ci = e / (FT_PH * FT_PW), r = e - ci * (FT_PH * FT_PW);
+      const int ph = r / FT_PW, pw = r - ph * FT_PW;
+      const int h = h0 - 1 + ph, w = w0 - 1 + pw;
+      float v = 0.f;
+      if (e < PE && h >= 0 && h < H && w >= 0 && w < W) v = a.planes[ci][(unsigned)n * HW + (unsigned)(h * W + w)];
+      pv[q] = v;
     }
-    w += PG;
-    while (w >= W) {
-      w -= W;
-      if (++h == H) { h = 0; ++n; }
+  };
+  if (t_beg < t_end) load_patch(t_beg);
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    __syncthreads();  // the previous tile's patch reads are done
+#pragma unroll
+    for (int q = 0; q < NPE; ++q)
+      if (tid + 256 * q < PE) patch[tid + 256 * q] = pv[q];
+    __syncthreads();
+    if (tile + 1 < t_end) load_patch(tile + 1);  // in flight under this tile's FMAs
+    int t = tile;
+    const int tw = t % tiles_w; t /= tiles_w;
+    const int th = t % tiles_h;
+    const int n = t / tiles_h;
+    const int h0 = th * FT_H, w0 = tw * FT_W;
+    for (int i = pg; i < FT_H * FT_W; i += PG) {
+      const int r = i / FT_W, cc = i - r * FT_W;
+      const int h = h0 + r, w = w0 + cc;
+      if (h >= H || w >= W) continue;
+      const size_t p = (size_t)((unsigned)n * HW + (unsigned)(h * W + w));
+      const float4 d = *reinterpret_cast<const float4*>(s.x + p * Cout + c);
+      const float4 z = *reinterpret_cast<const float4*>(s.z + p * Cout + c);
+      const pmu_f2 glo = {pmu_bnbwd1(d.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x), pmu_bnbwd1(d.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y)};
+      const pmu_f2 ghi = {pmu_bnbwd1(d.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z), pmu_bnbwd1(d.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w)};
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const float x = patch[(ci * FT_PH + r + tap / 3) * FT_PW + cc + tap % 3];
+          const pmu_f2 x2 = {x, x};
+          acc[0][ci * 9 + tap] = __builtin_elementwise_fma(glo, x2, acc[0][ci * 9 + tap]);
+          acc[1][ci * 9 + tap] = __builtin_elementwise_fma(ghi, x2, acc[1][ci * 9 + tap]);
+        }
     }
   }
-  // reduce over the pixel groups inside the wave (lanes with equal cq are CQ apart)
+  // reduce over the pixel groups inside the wave (lanes with equal cq are CQ apart), then waves
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
+  for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
     for (int k = 0; k < K9; ++k) {
-      float v = acc[e][k];
-      for (int off = CQ; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
-      acc[e][k] = v;
+      float v0 = acc[hf][k].x, v1 = acc[hf][k].y;
+      for (int off = CQ; off < 64; off <<= 1) {
+        v0 += __shfl_xor(v0, off, 64);
+        v1 += __shfl_xor(v1, off, 64);
+      }
+      acc[hf][k] = pmu_f2{v0, v1};
     }
   const int cq_per_wave = CQ < 64 ? CQ : 64;
-  const int nwr = CQ < 64 ? 4 : 1;  // waves holding distinct partials of the same channels
+  const int nwr = CQ < 64 ? 4 : 1;
+  __syncthreads();
   if (lane < cq_per_wave) {
     const int slot = CQ < 64 ? wave : 0;
-    const int ch0 = 4 * cq;
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int k = 0; k < K9; ++k) red[(slot * Cout + ch0 + e) * K9 + k] = acc[e][k];
+    for (int k = 0; k < K9; ++k) {
+      red[(slot * Cout + c + 0) * K9 + k] = acc[0][k].x;
+      red[(slot * Cout + c + 1) * K9 + k] = acc[0][k].y;
+      red[(slot * Cout + c + 2) * K9 + k] = acc[1][k].x;
+      red[(slot * Cout + c + 3) * K9 + k] = acc[1][k].y;
+    }
   }
   __syncthreads();
   for (int o = tid; o < Cout * K9; o += 256) {
@@ -302,7 +328,8 @@ static bool first_wgrad_fast(const pmu_frame* dz, int Cout) {
 extern "C" size_t pmu_conv_first_wgrad_ws(int N, int H, int W, int Cin, int Cout) {
   const long long P = (long long)N * H * W;
   const size_t slow = (size_t)pmu_cdiv(P, FWPIX) * Cout * Cin * 9 * sizeof(float);
-  const size_t fast = (size_t)pmu_cdiv(P, FWP2) * Cout * Cin * 9 * sizeof(float);
+  const size_t fast = (size_t)pmu_cdiv(N * pmu_cdiv(H, FT_H) * pmu_cdiv(W, FT_W), FW_TPB) * Cout * Cin * 9 *
+                      sizeof(float);
   return slow > fast ? slow : fast;
 }
 
@@ -320,12 +347,14 @@ extern "C" int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* pla
   const long long P = (long long)dz->N * dz->H * dz->W;
   int nb;
   if (first_wgrad_fast(dz, Cout)) {
-    nb = pmu_cdiv(P, FWP2);
+    const int tw = pmu_cdiv(dz->W, FT_W), th = pmu_cdiv(dz->H, FT_H), nt = dz->N * tw * th;
+    PMU_REQUIRE(P < (1LL << 31));
+    nb = pmu_cdiv(nt, FW_TPB);
     switch (Cin) {
-      case 1: hipLaunchKernelGGL(conv_first_wgrad_fast_kernel<1>, dim3((unsigned)nb), dim3(256), 0, st, a); break;
-      case 2: hipLaunchKernelGGL(conv_first_wgrad_fast_kernel<2>, dim3((unsigned)nb), dim3(256), 0, st, a); break;
-      case 3: hipLaunchKernelGGL(conv_first_wgrad_fast_kernel<3>, dim3((unsigned)nb), dim3(256), 0, st, a); break;
-      default: hipLaunchKernelGGL(conv_first_wgrad_fast_kernel<4>, dim3((unsigned)nb), dim3(256), 0, st, a); break;
+      case 1: hipLaunchKernelGGL(conv_first_wgrad_tile_kernel<1>, dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break;
+      case 2: hipLaunchKernelGGL(conv_first_wgrad_tile_kernel<2>, dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break;
+      case 3: hipLaunchKernelGGL(conv_first_wgrad_tile_kernel<3>, dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break;
+      default: hipLaunchKernelGGL(conv_first_wgrad_tile_kernel<4>, dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break;
     }
   } else {
     nb = pmu_cdiv(P, FWPIX);
