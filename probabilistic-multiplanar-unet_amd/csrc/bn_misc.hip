@@ -421,6 +421,45 @@ __device__ __forceinline__ bool head_fast_frame(const DevFrame& f) {
 
 constexpr int HPPB = 2048;  // pixels per block in the fast head kernels
 
+// 1x1 head forward on one unpooled BN+ReLU source: thread = (channel quad cq, pixel group), the 16 B
+// loads of a pixel's quads coalesce into its whole C-channel row; per class the quad dot products
+// are summed over the pixel's CQ lanes by xor shuffles and lane cq == 0 writes y[n][k][pix].
+// (One thread per pixel read a 16-B piece of 64 different rows per load instruction.)
+__global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const float* __restrict__ w,
+                                                            const float* __restrict__ b, int K, int do_sigmoid,
+                                                            float* __restrict__ y) {
+  const int tid = threadIdx.x;
+  const int C = f.C, CQ = C >> 2, PG = 256 / CQ;
+  const int cq = tid & (CQ - 1), pg = tid / CQ;
+  const unsigned HWu = (unsigned)f.H * (unsigned)f.W;
+  const long long P = (long long)f.N * HWu;
+  const float4 sc = *reinterpret_cast<const float4*>(f.s0.coef + 4 * cq);
+  const float4 sh = *reinterpret_cast<const float4*>(f.s0.coef + C + 4 * cq);
+  float4 wq[HEAD_KMAX];
+  float bk[HEAD_KMAX];
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k) {
+    wq[k] = k < K ? *reinterpret_cast<const float4*>(w + k * C + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bk[k] = (k < K && b) ? b[k] : 0.f;
+  }
+  const unsigned pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
+  for (unsigned p = blockIdx.x * HPPB + pg; p < pend; p += PG) {  // 32-bit decode (P < 2^31)
+    const float4 a = pmu_bnrelu4(*reinterpret_cast<const float4*>(f.s0.x + (size_t)p * C + 4 * cq), sc, sh);
+    const unsigned n = p / HWu, pix = p - n * HWu;
+#pragma unroll
+    for (int k = 0; k < HEAD_KMAX; ++k) {
+      if (k >= K) break;
+      float v = fmaf(a.x, wq[k].x, fmaf(a.y, wq[k].y, fmaf(a.z, wq[k].z, a.w * wq[k].w)));
+      for (int o = 1; o < CQ; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (cq == 0) {
+        v += bk[k];
+        if (do_sigmoid) v = 1.f / (1.f + expf(-v));
+        y[(size_t)(n * K + k) * HWu + pix] = v;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                                                             int do_sigmoid, const float* __restrict__ w, int K, int C,
                                                             long long HW, long long P, float* __restrict__ dl,
@@ -432,21 +471,22 @@ __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restr
 #pragma unroll
   for (int k = 0; k < HEAD_KMAX; ++k)
     wq[k] = k < K ? *reinterpret_cast<const float4*>(w + k * C + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
-  const long long pend = min(P, (long long)(blockIdx.x + 1) * HPPB);
-  for (long long p = (long long)blockIdx.x * HPPB + pg; p < pend; p += PG) {
-    const long long n = p / HW, pix = p - n * HW;
+  // 32-bit pixel decode (P < 2^31, host-checked): 64-bit divisions per pixel dominated
+  const unsigned HWu = (unsigned)HW, pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
+  for (unsigned p = blockIdx.x * HPPB + pg; p < pend; p += PG) {
+    const unsigned n = p / HWu, pix = p - n * HWu;
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < HEAD_KMAX; ++k) {
       if (k >= K) break;
-      const long long i = (n * K + k) * HW + pix;
+      const size_t i = (size_t)(n * K + k) * HWu + pix;
       float g = dy[i];
       if (do_sigmoid) { const float sg = y[i]; g = g * (sg * (1.f - sg)); }
       if (cq == 0) dl[i] = g;
       o.x = fmaf(g, wq[k].x, o.x); o.y = fmaf(g, wq[k].y, o.y);
       o.z = fmaf(g, wq[k].z, o.z); o.w = fmaf(g, wq[k].w, o.w);
     }
-    *reinterpret_cast<float4*>(da + p * C + 4 * cq) = o;
+    *reinterpret_cast<float4*>(da + (size_t)p * C + 4 * cq) = o;
   }
 }
 
@@ -465,14 +505,14 @@ __global__ __launch_bounds__(256) void wgrad1x1_fast_kernel(const float* __restr
   float accb[HEAD_KMAX];
 #pragma unroll
   for (int k = 0; k < HEAD_KMAX; ++k) { acc[k] = make_float4(0.f, 0.f, 0.f, 0.f); accb[k] = 0.f; }
-  const long long pend = min(P, (long long)(blockIdx.x + 1) * HPPB);
-  for (long long p = (long long)blockIdx.x * HPPB + pg; p < pend; p += PG) {
-    const long long n = p / HW, pix = p - n * HW;
-    const float4 a = pmu_bnrelu4(*reinterpret_cast<const float4*>(f.s0.x + p * C + 4 * cq), sc, sh);
+  const unsigned HWu = (unsigned)HW, pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
+  for (unsigned p = blockIdx.x * HPPB + pg; p < pend; p += PG) {  // 32-bit decode (P < 2^31)
+    const unsigned n = p / HWu, pix = p - n * HWu;
+    const float4 a = pmu_bnrelu4(*reinterpret_cast<const float4*>(f.s0.x + (size_t)p * C + 4 * cq), sc, sh);
 #pragma unroll
     for (int k = 0; k < HEAD_KMAX; ++k) {
       if (k >= K) break;
-      const float g = dl[(n * K + k) * HW + pix];
+      const float g = dl[(size_t)(n * K + k) * HWu + pix];
       acc[k].x = fmaf(g, a.x, acc[k].x); acc[k].y = fmaf(g, a.y, acc[k].y);
       acc[k].z = fmaf(g, a.z, acc[k].z); acc[k].w = fmaf(g, a.w, acc[k].w);
       accb[k] += g;
@@ -715,6 +755,12 @@ extern "C" int pmu_head1x1_fwd(const pmu_frame* in, const float* w, const float*
   PMU_REQUIRE(valid_frame(in) && w && y && K >= 1 && K <= HEAD_KMAX);
   const DevFrame f = make_dev_frame(in);
   const long long P = (long long)in->N * in->H * in->W;
+  if (host_head_fast(in) && P < (1LL << 31)) {
+    hipLaunchKernelGGL(head_fwd_fast_kernel, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
+                       f, w, b, K, do_sigmoid, y);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   hipLaunchKernelGGL(head_fwd_kernel, dim3((unsigned)pmu_cdiv(P, 256)), dim3(256), 0, (hipStream_t)stream,
                      f, w, b, K, do_sigmoid, y);
   PMU_CHECK_LAUNCH();
@@ -726,7 +772,7 @@ extern "C" int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, 
   PMU_REQUIRE(dy && w && dl && da && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y));
   const long long P = (long long)N * H * W;
   const int CQ = C >> 2;
-  if ((C & 3) == 0 && CQ <= 64 && (CQ & (CQ - 1)) == 0) {
+  if ((C & 3) == 0 && CQ <= 64 && (CQ & (CQ - 1)) == 0 && P < (1LL << 31)) {
     hipLaunchKernelGGL(head_bwd_fast_kernel, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
                        dy, y, do_sigmoid, w, K, C, (long long)H * W, P, dl, da);
     PMU_CHECK_LAUNCH();
@@ -749,7 +795,7 @@ extern "C" int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float*
   const DevFrame f = make_dev_frame(act);
   PMU_REQUIRE(f.C <= 256);
   const long long P = (long long)act->N * act->H * act->W;
-  const bool fast = host_head_fast(act);
+  const bool fast = host_head_fast(act) && P < (1LL << 31);
   const int R = fast ? pmu_cdiv(P, HPPB) : pmu_cdiv(P, W1_PPB);
   PMU_REQUIRE(ws_bytes >= (size_t)R * K * (f.C + 1) * sizeof(float));
   if (fast)
