@@ -235,26 +235,29 @@ __global__ __launch_bounds__(256, 2) void convT_wgrad_bf16_kernel(TwbArgs a) {
     const bool ok_ = p_ < P && c_ < a.Cip;                                                         \
     R = keep_if(ok_, *reinterpret_cast<const uint4*>(a.xt + (ok_ ? p_ * a.Cip + c_ : 0)));        \
   }
+// D units of a thread cover two du pixel slots (I even / odd: tile pixel (tid >> 3) and +32) and 4
+// taps; the slots are decoded once per tile in 32 bits (N*H*W < 2^30, host-checked).  Decoding each
+// unit with 64-bit divisions made this kernel VALU-bound.
 #define PMU_DL(I, R)                                                                                \
   {                                                                                                \
-    const int u_ = tid + 256 * (I);                                                                \
-    const int tap_ = u_ >> 9;                                                                      \
-    const long long p_ = (long long)tile_ * WPX + ((u_ >> 3) & 63);                                \
-    const int c_ = co0 + 8 * (u_ & 7);                                                             \
-    const bool ok_ = p_ < P && c_ < a.Cop;                                                         \
-    long long q_ = 0;                                                                              \
-    if (ok_) {                                                                                     \
-      const int j_ = (int)(p_ % a.W);                                                              \
-      const long long t2_ = p_ / a.W;                                                              \
-      const int i_ = (int)(t2_ % a.H);                                                             \
-      const long long n_ = t2_ / a.H;                                                              \
-      q_ = ((n_ * a.Hd + a.oh + 2 * i_ + (tap_ >> 1)) * a.Wd + a.ow + 2 * j_ + (tap_ & 1)) * a.Cop + c_; \
-    }                                                                                              \
+    const int tap_ = (I) >> 1;                                                                     \
+    const int c_ = co0 + 8 * (tid & 7);                                                            \
+    const bool ok_ = okd_[(I) & 1] && c_ < a.Cop;                                                  \
+    const unsigned q_ = ok_ ? qd_[(I) & 1] + (unsigned)(((tap_ >> 1) * a.Wd + (tap_ & 1)) * a.Cop + c_) : 0u; \
     R = keep_if(ok_, *reinterpret_cast<const uint4*>(a.dut + q_));                                 \
   }
 #define PMU_LOAD(T)                                                                                 \
   {                                                                                                \
     const int tile_ = (T);                                                                         \
+    unsigned qd_[2];  /* 32-bit element offsets (du < 2^32 elements, host-checked) */            \
+    bool okd_[2];                                                                                  \
+    _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                             \
+      const unsigned p_ = (unsigned)tile_ * WPX + (unsigned)(tid >> 3) + 32u * s_;                 \
+      okd_[s_] = p_ < (unsigned)P;                                                                 \
+      const unsigned t2_ = p_ / (unsigned)a.W, j_ = p_ - t2_ * (unsigned)a.W;                      \
+      const unsigned n_ = t2_ / (unsigned)a.H, i_ = t2_ - n_ * (unsigned)a.H;                      \
+      qd_[s_] = ((n_ * a.Hd + a.oh + 2 * i_) * a.Wd + a.ow + 2 * j_) * a.Cop;                       \
+    }                                                                                              \
     PMU_XL(0, rx0) PMU_XL(1, rx1) PMU_XL(2, rx2) PMU_XL(3, rx3)                                    \
     PMU_DL(0, rd0) PMU_DL(1, rd1) PMU_DL(2, rd2) PMU_DL(3, rd3)                                    \
     PMU_DL(4, rd4) PMU_DL(5, rd5) PMU_DL(6, rd6) PMU_DL(7, rd7)                                    \
@@ -485,6 +488,7 @@ extern "C" int pmu_convT2x2_wgrad_bf16(const unsigned short* xt, const unsigned 
   PMU_REQUIRE(off_h >= 0 && off_w >= 0 && off_h + 2 * H <= Hd && off_w + 2 * W <= Wd && (!dbias || du));
   PMU_REQUIRE(ws_bytes >= pmu_convT2x2_wgrad_ws_bf16(N, H, W, Cin, Cout));
   PMU_REQUIRE((long long)N * 4 * H * W < (1LL << 32));  // the bias-sum pass decodes pixels in 32 bits
+  PMU_REQUIRE((long long)N * Hd * Wd * pmu_cdiv(Cout, 8) * 8 < (1LL << 32));  // 32-bit du offsets
   TwbArgs a;
   a.xt = xt; a.dut = dut; a.ws = ws;
   a.N = N; a.H = H; a.W = W; a.Hd = Hd; a.Wd = Wd; a.oh = off_h; a.ow = off_w; a.Cin = Cin; a.Cout = Cout;
