@@ -24,6 +24,7 @@ struct TArgs {
   float* out;                 // fwd: u [N][2H][2W][Cout];  dgrad: dx [M][Cin]
   long long M;
   int Ncols, K, H, W, Cin, Cout, Hd, Wd, off_h, off_w;
+  int lw, lh;                 // fwd: log2 W, log2 H when powers of two (shift/mask epilogue), else -1
 };
 
 __global__ void convT_pack_bf16_kernel(const float* __restrict__ w, int Cin, int Cout, int dgrad,
@@ -57,12 +58,10 @@ __global__ __launch_bounds__(256, 2) void convT_bf16_kernel(TArgs p) {
     const long long m = m0 + (tid >> 3) + 32 * i;
     aok[i] = m < p.M;
     const long long mm = aok[i] ? m : 0;
-    if constexpr (DGRAD) {
-      const int j = (int)(mm % p.W);
-      const long long t = mm / p.W;
-      const int ii = (int)(t % p.H);
-      const long long n = t / p.H;
-      abase[i] = ((n * p.Hd + p.off_h + 2 * ii) * p.Wd + p.off_w + 2 * j) * p.Cout;
+    if constexpr (DGRAD) {  // 32-bit decode (M < 2^31, host-checked)
+      const unsigned t = (unsigned)mm / (unsigned)p.W, j = (unsigned)mm - t * (unsigned)p.W;
+      const unsigned n = t / (unsigned)p.H, ii = t - n * (unsigned)p.H;
+      abase[i] = ((long long)(n * p.Hd + p.off_h + 2 * ii) * p.Wd + p.off_w + 2 * j) * p.Cout;
     } else {
       abase[i] = mm * p.Cin;
     }
@@ -158,17 +157,32 @@ __global__ __launch_bounds__(256, 2) void convT_bf16_kernel(TArgs p) {
       const float b = p.bias ? p.bias[co] : 0.f;
       const unsigned Wu = (unsigned)p.W, Hu = (unsigned)p.H;  // 32-bit decode (M < 2^31, host-checked)
       float* outc = p.out + (long long)(ab >> 1) * 2 * p.W * p.Cout + (ab & 1) * p.Cout + co;
+      if (p.lw >= 0 && p.lh >= 0) {  // shift/mask decode: the divisions cost as much as a short K loop
+        const bool full = m0 + TM <= p.M;
 #pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
+        for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
-          if (m < (unsigned)p.M) {
-            const unsigned t = m / Wu, j = m - t * Wu;
-            const unsigned n = t / Hu, i = t - n * Hu;
-            outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * p.Cout] = acc[fm][fn][r] + b;
+          for (int r = 0; r < 16; ++r) {
+            const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
+            if (full || m < (unsigned)p.M) {
+              const unsigned j = m & (Wu - 1), t = m >> p.lw;
+              const unsigned i = t & (Hu - 1), n = t >> p.lh;
+              outc[(size_t)((n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * (unsigned)p.Cout] = acc[fm][fn][r] + b;
+            }
           }
-        }
+      } else {
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
+            if (m < (unsigned)p.M) {
+              const unsigned t = m / Wu, j = m - t * Wu;
+              const unsigned n = t / Hu, i = t - n * Hu;
+              outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * p.Cout] = acc[fm][fn][r] + b;
+            }
+          }
+      }
     }
   }
 }
@@ -455,6 +469,9 @@ extern "C" int pmu_convT2x2_fwd_bf16(const pmu_frame* in, const unsigned short* 
   p.a = in->src[0].x; p.coef = in->src[0].coef; p.bp = wp; p.bias = bias; p.out = u;
   p.M = (long long)in->N * in->H * in->W; p.Ncols = 4 * Cout; p.K = in->src[0].C;
   p.H = in->H; p.W = in->W; p.Cin = in->src[0].C; p.Cout = Cout;
+  auto log2_or = [](int v) { return (v & (v - 1)) == 0 ? __builtin_ctz((unsigned)v) : -1; };
+  p.lw = log2_or(in->W); p.lh = log2_or(in->H);
+  if (4LL * p.M * Cout >= (1LL << 32)) p.lw = -1;  // the shift path's output index is 32-bit
   dim3 grid((unsigned)pmu_cdiv(p.M, TM), (unsigned)(p.Ncols / TN));
   hipLaunchKernelGGL(convT_bf16_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
   PMU_CHECK_LAUNCH();
@@ -465,6 +482,7 @@ extern "C" int pmu_convT2x2_dgrad_bf16(const float* du, int Hd, int Wd, int off_
                                        int N, int H, int W, int Cin, int Cout, float* dx, void* stream) {
   PMU_REQUIRE(du && wp && dx && N > 0 && H > 0 && W > 0 && Cin % TN == 0 && Cout % TK == 0);
   PMU_REQUIRE(off_h >= 0 && off_w >= 0 && off_h + 2 * H <= Hd && off_w + 2 * W <= Wd);
+  PMU_REQUIRE((long long)N * H * W < (1LL << 31));  // 32-bit pixel decode
   TArgs p{};
   p.a = du; p.bp = wp; p.out = dx;
   p.M = (long long)N * H * W; p.Ncols = Cin; p.K = 4 * Cout;
