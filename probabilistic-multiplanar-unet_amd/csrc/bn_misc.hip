@@ -589,31 +589,38 @@ __global__ __launch_bounds__(256) void sgd_clip_kernel(const pmu_sgd_chunk* __re
 }
 
 // ---------------- dice counts ----------------
-__global__ __launch_bounds__(256) void dice_counts_kernel(const float* __restrict__ y, const float* __restrict__ mask,
-                                                          int N, int K, int H, int W, double* __restrict__ out) {
-  __shared__ double red[256];
-  const long long HW = (long long)H * W;
-  const long long P = (long long)N * HW;
+// Per-class Dice counts of one prediction: integer counters per thread (32-bit pixel decode),
+// reduced by shuffles within each wave, through LDS over the block's 16 waves, and by one fp64
+// atomicAdd per counter per block (integer-valued: order-independent).  The 64-bit pixel division
+// and fp64 adds per pixel, and the per-counter LDS tree with 9 barriers each, made the previous
+// version ~140 us per call for a 32 x 256^2 batch.
+constexpr int DICE_T = 256, DICE_MAXB = 2048;
+__global__ __launch_bounds__(DICE_T) void dice_counts_kernel(const float* __restrict__ y, const float* __restrict__ mask,
+                                                             int N, int K, int H, int W, double* __restrict__ out) {
+  __shared__ unsigned red[DICE_T / 64][3 * HEAD_KMAX];
+  const unsigned HW = (unsigned)H * (unsigned)W;
+  const unsigned P = (unsigned)N * HW;  // < 2^31, host-checked
   const int KK = K == 1 ? 1 : K;
-  double loc[3 * HEAD_KMAX];
+  unsigned loc[3 * HEAD_KMAX];
 #pragma unroll
-  for (int i = 0; i < 3 * HEAD_KMAX; ++i) loc[i] = 0.0;
-  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (long long)gridDim.x * blockDim.x) {
-    const int n = (int)(p / HW);
-    const long long pix = p - (long long)n * HW;
+  for (int i = 0; i < 3 * HEAD_KMAX; ++i) loc[i] = 0u;
+  double b0 = 0.0, b1 = 0.0, b2 = 0.0;  // K == 1
+  for (unsigned p = blockIdx.x * DICE_T + threadIdx.x; p < P; p += gridDim.x * DICE_T) {
+    const unsigned n = p / HW, pix = p - n * HW;
     const float t = mask[p];
-    if (K == 1) {
+    if (K == 1) {  // the mask is summed as the float it is (dice_coeff on (pred > 0.5) vs mask)
       const float pr = y[p] > 0.5f ? 1.f : 0.f;
-      loc[0] += (double)(pr * t); loc[1] += (double)pr; loc[2] += (double)t;
+      b0 += (double)(pr * t); b1 += (double)pr; b2 += (double)t;
     } else {
+      const float* yp = y + (size_t)n * K * HW + pix;
       float m = -INFINITY;
-      for (int k = 0; k < K; ++k) m = fmaxf(m, y[((long long)n * K + k) * HW + pix]);
+      for (int k = 0; k < K; ++k) m = fmaxf(m, yp[(size_t)k * HW]);
       float e[HEAD_KMAX];
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < HEAD_KMAX; ++k) {
         e[k] = 0.f;
-        if (k < K) { e[k] = expf(y[((long long)n * K + k) * HW + pix] - m); s += e[k]; }
+        if (k < K) { e[k] = expf(yp[(size_t)k * HW] - m); s += e[k]; }
       }
       int am = 0;
       float best = e[0] / s;
@@ -624,22 +631,41 @@ __global__ __launch_bounds__(256) void dice_counts_kernel(const float* __restric
 #pragma unroll
       for (int k = 0; k < HEAD_KMAX; ++k) {
         if (k < K) {
-          const double pr = (am == k) ? 1.0 : 0.0;
-          const double tk = (t == (float)k) ? 1.0 : 0.0;
-          loc[3 * k + 0] += pr * tk; loc[3 * k + 1] += pr; loc[3 * k + 2] += tk;
+          const unsigned pr = (am == k) ? 1u : 0u, tk = (t == (float)k) ? 1u : 0u;
+          loc[3 * k + 0] += pr & tk; loc[3 * k + 1] += pr; loc[3 * k + 2] += tk;
         }
       }
     }
   }
-  for (int i = 0; i < 3 * KK; ++i) {
-    red[threadIdx.x] = loc[i];
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-      __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (K == 1) {
+    __shared__ double redd[DICE_T / 64][3];
+    double v[3] = {b0, b1, b2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      for (int o = 32; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o, 64);
+      if (lane == 0) redd[wave][i] = v[i];
     }
-    if (threadIdx.x == 0) atomicAdd(out + i, red[0]);  // integer-valued doubles: order-independent
     __syncthreads();
+    if (threadIdx.x < 3) {
+      double tsum = 0.0;
+      for (int wv = 0; wv < DICE_T / 64; ++wv) tsum += redd[wv][threadIdx.x];
+      atomicAdd(out + threadIdx.x, tsum);
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 3 * HEAD_KMAX; ++i) {
+    if (i >= 3 * KK) break;
+    unsigned v = loc[i];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wave][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 * KK) {
+    unsigned long long tsum = 0;
+    for (int wv = 0; wv < DICE_T / 64; ++wv) tsum += red[wv][threadIdx.x];
+    atomicAdd(out + threadIdx.x, (double)tsum);
   }
 }
 
@@ -823,9 +849,10 @@ extern "C" int pmu_dice_counts(const float* y, const float* mask, int N, int K, 
   PMU_REQUIRE(y && mask && counts && N > 0 && K >= 1 && K <= HEAD_KMAX && H > 0 && W > 0);
   if (hipMemsetAsync(counts, 0, sizeof(double) * 3 * K, (hipStream_t)stream) != hipSuccess) return PMU_ERR_ARG;
   const long long P = (long long)N * H * W;
-  unsigned g = (unsigned)pmu_cdiv(P, 256);
-  if (g > 1024) g = 1024;
-  hipLaunchKernelGGL(dice_counts_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, y, mask, N, K, H, W, counts);
+  PMU_REQUIRE(P < (1LL << 31));
+  unsigned g = (unsigned)pmu_cdiv(P, DICE_T);
+  if (g > DICE_MAXB) g = DICE_MAXB;
+  hipLaunchKernelGGL(dice_counts_kernel, dim3(g), dim3(DICE_T), 0, (hipStream_t)stream, y, mask, N, K, H, W, counts);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

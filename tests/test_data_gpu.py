@@ -174,3 +174,26 @@ def test_train_net_and_predict_volume_end_to_end(dev, tmp_path):
         for k in (1, 2):
             ref = class_dice(vols[v].cpu(), truth.cpu(), k)
             assert abs(float(res["dice"][v, k]) - ref) <= 5e-3   # softmax in-kernel: a few fp32 near-ties may flip
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 3])
+def test_dice_counts_multiblock_exact(K):
+    """pmu_dice_counts over a grid-strided multi-block launch: the per-class counts equal a float64
+    CPU count (softmax -> argmax for K > 1, pred > 0.5 for K == 1) exactly."""
+    from pmu_hip.metrics import dice_counts
+    g = torch.Generator().manual_seed(5 + K)
+    N, H, W = 8, 128, 160
+    y = torch.randn(N, K, H, W, generator=g) if K > 1 else torch.rand(N, 1, H, W, generator=g)
+    mask = torch.randint(0, max(K, 2), (N, 1, H, W), generator=g).float()
+    got = dice_counts(y.cuda(), mask.cuda(), K).cpu()
+    if K == 1:
+        pr = (y[:, 0] > 0.5).double()
+        t = mask[:, 0].double()
+        want = torch.tensor([[(pr * t).sum(), pr.sum(), t.sum()]], dtype=torch.float64)
+    else:
+        am = torch.softmax(y, 1).argmax(1)
+        t = mask[:, 0].long()
+        want = torch.tensor([[((am == k) & (t == k)).sum(), (am == k).sum(), (t == k).sum()] for k in range(K)],
+                            dtype=torch.float64)
+    assert torch.equal(got, want), (got, want)
