@@ -283,6 +283,23 @@ __global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const float* __restri
   }
 }
 
+// Vector path (C % 4 == 0, < 2^31 float4 units): one float4 per thread, 32-bit decode.  The scalar
+// kernel above paid four 64-bit divisions per element.
+__global__ __launch_bounds__(256) void avgpool2_bwd_vec_kernel(const float* __restrict__ dpool, int N, int H, int W,
+                                                               int C, unsigned units, float* __restrict__ dx) {
+  const int Hp = (H + 1) / 2, Wp = (W + 1) / 2;
+  const unsigned CQ = (unsigned)C >> 2, Wu = (unsigned)W, Hu = (unsigned)H;
+  for (unsigned u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const unsigned p = u / CQ, cq = u - p * CQ;
+    const unsigned t = p / Wu, w = p - t * Wu;
+    const unsigned n = t / Hu, h = t - n * Hu;
+    const int hp = (int)h >> 1, wp = (int)w >> 1;
+    const float cnt = (float)((min(2 * hp + 2, H) - 2 * hp) * (min(2 * wp + 2, W) - 2 * wp));
+    const float4 g = *reinterpret_cast<const float4*>(dpool + ((size_t)(n * Hp + hp) * Wp + wp) * C + 4 * cq);
+    *reinterpret_cast<float4*>(dx + (size_t)u * 4) = make_float4(g.x / cnt, g.y / cnt, g.z / cnt, g.w / cnt);
+  }
+}
+
 // ---------------- 1x1 head ----------------
 constexpr int HEAD_KMAX = 8;
 __global__ __launch_bounds__(256) void head_fwd_kernel(DevFrame f, const float* __restrict__ w, const float* __restrict__ b,
@@ -763,6 +780,15 @@ extern "C" int pmu_maxpool2_bwd(const float* dpool, const float* z, const float*
 
 extern "C" int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream) {
   PMU_REQUIRE(dpool && dx && N > 0 && H > 0 && W > 0 && C > 0);
+  const long long units = (long long)N * H * W * (C / 4);
+  if (C % 4 == 0 && units < (1LL << 31)) {
+    long long g = (units + 255) / 256;
+    if (g > 16384) g = 16384;
+    hipLaunchKernelGGL(avgpool2_bwd_vec_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, dpool, N, H, W,
+                       C, (unsigned)units, dx);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   hipLaunchKernelGGL(avgpool2_bwd_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0,
                      (hipStream_t)stream, dpool, N, H, W, C, dx);
   PMU_CHECK_LAUNCH();
