@@ -287,9 +287,9 @@ __global__ __launch_bounds__(256) void fcomb_bwd_kernel(const float* __restrict_
       const int r = e / KP, k = e % KP;
       const long long px = p0 + r;
       float v = 0.f;
-      if (px < P && k < p.K) {
-        const long long n = px / HW, pix = px - n * HW;
-        v = dl[(n * p.K + k) * HW + pix];
+      if (px < P && k < p.K) {  // 32-bit decode (P < 2^31, host-checked)
+        const unsigned n = (unsigned)px / (unsigned)HW, pix = (unsigned)px - n * (unsigned)HW;
+        v = dl[((size_t)n * p.K + k) * (unsigned)HW + pix];
       }
       Db[r * 33 + k] = v;
     }
@@ -310,8 +310,8 @@ __global__ __launch_bounds__(256) void fcomb_bwd_kernel(const float* __restrict_
         float b;
         if (l == 0) {
           const long long px = p0 + rr;
-          const int n = (int)((px < P ? px : P - 1) / HW);
-          b = o < p.F ? zb[(long long)n * p.F + o] : 0.f;
+          const unsigned n = (unsigned)(px < P ? px : P - 1) / (unsigned)HW;
+          b = o < p.F ? zb[(size_t)n * p.F + o] : 0.f;
         } else {
           b = o < p.F ? p.b[l][o] : 0.f;
         }
@@ -650,6 +650,7 @@ extern "C" int pmu_fcomb_bwd(const float* feat, const float* z, const float* zb,
   PMU_REQUIRE(feat && z && zb && dl && dfeat && dw && db && dwl && dbl && ws);
   PMU_REQUIRE(N > 0 && H > 0 && W > 0 && make_w(p, w, b, wl, bl, F, L, K, NH));
   PMU_REQUIRE(ws_bytes >= pmu_fcomb_bwd_ws(N, H, W));
+  PMU_REQUIRE((long long)N * H * W < (1LL << 31) && (long long)N * H * W * K < (1LL << 32));  // 32-bit decode
   FcombOut o;
   for (int l = 0; l < MAXNH; ++l) {
     o.dw[l] = l < NH ? dw[l] : nullptr;
