@@ -548,13 +548,16 @@ def main():
         n, fl, t = mf[dom]
         ach = fl / t / 1e12
         traffic, tsrc = pmc_traffic(args.workload, dom)
-        peak = BF16_MFMA_PEAK_TF if dom.endswith("_bf16") else FP32_MFMA_PEAK_TF
+        # bf16-MFMA kernels: the *_bf16 family and the bf16 raw GEMMs (pmu_conv3x3_{fwd,dgrad}_raw);
+        # the fp32 Winograd raw kernels are named *_wino_raw
+        bf16_dom = dom.endswith("_bf16") or (dom.endswith("_raw") and "_wino" not in dom)
+        peak = BF16_MFMA_PEAK_TF if bf16_dom else FP32_MFMA_PEAK_TF
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "bytes/launch (HBM)",
                 "traffic_source": tsrc, "launches": n, "avg_launch_ms": round(t / n * 1e3, 4),
                 "flops_per_launch": fl / n}
-        if dom.endswith("_wino"):  # Winograd executes 16 of the direct sum's 36 products per 2x2 tile
+        if "_wino" in dom:  # Winograd executes 16 of the direct sum's 36 products per 2x2 tile
             roof["flops_basis"] = "Winograd F(2x2,3x3) MFMA products (16 per 2x2 output tile per channel pair)"
             roof["direct_conv_equiv_tflops"] = round(ach * 36 / 16, 2)
         kernels = {k: {"launches": v[0], "ms": round(v[2] * 1e3, 3),
