@@ -359,6 +359,13 @@ def phantom_batches(S, B, rank, world, dev):
 
 
 @torch.no_grad()
+def roofline_peak(kernel):
+    """Dense MFMA peak (TFLOP/s) for a C-ABI kernel family: bf16 for the *_bf16 family and the bf16
+    raw GEMMs (pmu_conv3x3_{fwd,dgrad}_raw), fp32 otherwise (the Winograd raw kernels are *_wino_raw)."""
+    bf16 = kernel.endswith("_bf16") or (kernel.endswith("_raw") and "_wino" not in kernel)
+    return BF16_MFMA_PEAK_TF if bf16 else FP32_MFMA_PEAK_TF
+
+
 def c5_eval(net, dev, D, batch, precision):
     """Config c5's evaluation (PMU/eval.py:131-203 via predict.predict_volume's batching): predict all
     3 x D slices (D x D x 3 channels) of a seeded D^3 phantom along the axial/coronal/sagittal views
@@ -548,10 +555,7 @@ def main():
         n, fl, t = mf[dom]
         ach = fl / t / 1e12
         traffic, tsrc = pmc_traffic(args.workload, dom)
-        # bf16-MFMA kernels: the *_bf16 family and the bf16 raw GEMMs (pmu_conv3x3_{fwd,dgrad}_raw);
-        # the fp32 Winograd raw kernels are named *_wino_raw
-        bf16_dom = dom.endswith("_bf16") or (dom.endswith("_raw") and "_wino" not in dom)
-        peak = BF16_MFMA_PEAK_TF if bf16_dom else FP32_MFMA_PEAK_TF
+        peak = roofline_peak(dom)
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "bytes/launch (HBM)",

@@ -174,3 +174,13 @@ def test_library_rejects_bad_arguments_without_gpu():
     assert cdll.pmu_sgd_clip(None, 0, None, ctypes.c_float(1), ctypes.c_float(1), ctypes.c_float(0.9),
                              ctypes.c_float(0.1), None) == PMU_ERR_ARG
     assert cdll.pmu_conv3x3_tiles(32, 256, 256) == 32 * 32 * 8
+
+
+def test_bench_roofline_peak_by_kernel_family():
+    """bench.py prices the dominant kernel against the MFMA peak of the dtype it computes in."""
+    import bench
+    for k in ("pmu_conv3x3_wgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_fwd_bf16"):
+        assert bench.roofline_peak(k) == bench.BF16_MFMA_PEAK_TF, k
+    for k in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw", "pmu_conv3x3_wgrad_wino",
+              "pmu_convT2x2_wgrad", "pmu_fcomb_bwd"):
+        assert bench.roofline_peak(k) == bench.FP32_MFMA_PEAK_TF, k
