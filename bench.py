@@ -32,6 +32,8 @@ import torch.nn as nn  # noqa: E402
 
 METRIC = "2D slices/sec fwd+bwd, 256×256×1 batch32 U-Net; Dice vs ref"
 METRIC_C5 = "2D slices/sec fwd+bwd, 512×512×3 batch16 U-Net bf16 (BASELINE.json configs[4])"
+METRIC_C4 = ("2D slices/sec ProbabilisticUnet train step (prior+posterior, latent 6, KL+CE) + 16 fcomb samples, "
+             "256×256×1 batch32 (BASELINE.json configs[3])")
 FP32_MFMA_PEAK_TF = 157.3
 BF16_MFMA_PEAK_TF = 2516.0   # dense bf16 MFMA (MI355X_MICROARCH.md; 2.5 PF, no sparsity)
 FILTERS = [64, 128, 256, 512, 1024]
@@ -135,28 +137,73 @@ class KernelTimer:
             return 2.0 * a.N * a.H * a.W * cin * args[6] * 4
         return fcomb_flops(name, args)
 
+    @staticmethod
+    def _direct(name, args, fl):
+        """The direct-sum FLOPs of a launch: a Winograd F(2x2,3x3) launch executes 16
+        products per 2x2 output tile and channel pair where the direct sum takes 9 per pixel."""
+        if "_wino" not in name or not fl:
+            return fl
+        if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw"):
+            H, W = args[3], args[4]
+        elif name == "pmu_conv3x3_wgrad_wino":
+            H, W = args[3], args[4]
+        else:
+            f = args[0]._obj
+            H, W = f.H, f.W
+        return fl * (9.0 * H * W) / (16.0 * ((H + 1) // 2) * ((W + 1) // 2))
+
     def __call__(self, name, args, e0, e1):
-        self.rec.append((name, self._flops(name, args), e0, e1))
+        fl = self._flops(name, args)
+        self.rec.append((name, fl, self._direct(name, args, fl), e0, e1))
 
     def summary(self):
+        """{name: [launches, executed MFMA FLOPs, seconds, direct-sum FLOPs]}"""
         torch.cuda.synchronize()
         per = {}
-        for name, fl, e0, e1 in self.rec:
+        for name, fl, dfl, e0, e1 in self.rec:
             t = e0.elapsed_time(e1) * 1e-3
-            d = per.setdefault(name, [0, 0.0, 0.0])
+            d = per.setdefault(name, [0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += fl
             d[2] += t
+            d[3] += dfl
         return per
+
+
+def host_cpu():
+    """(threads to use, description) of the host cores this process may run on: the affinity set,
+    capped by a cgroup CPU quota when one is set (a GPU box grants a share of a bigger machine)."""
+    total = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = total
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    threads = min(avail, quota) if quota else avail
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, {"cpu_model": model, "os_cpu_count": total, "affinity_cpus": avail, "cgroup_cpu_quota": quota}
 
 
 def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classes=1):
     """CPU oracle (torch-CPU restatement of the reference) on a bounded sample: batch 2 of the
-    bench geometry, 1 warm-up + timed steps until ~max_seconds (at most 5).  The reference's CPU
-    path is fp32 only, so the c5 (bf16) sample is timed in fp32."""
+    bench geometry, 1 warm-up + timed steps until ~max_seconds (at most 5), on every host core this
+    process may use.  The reference's CPU path is fp32 only, so the c5 (bf16) sample is fp32."""
     from oracle.unet_ref import unet_param_keys, unet_train_step
     from oracle.probunet_ref import probunet_train_step
-    threads = min(16, os.cpu_count() or 1)
+    threads, host = host_cpu()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(1)
@@ -173,17 +220,17 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
 
         def one():
             unet_train_step(sd, x, t, 5, classes, lr=1e-3, bufs=bufs)
-        what = "fwd+bwd+clip+SGD steps"
+        what = "UNet fwd+loss+bwd+clip+SGD steps"
     else:
         from model import ProbabilisticUnet
-        net = ProbabilisticUnet(1, 3, FILTERS, latent_dim=6, no_convs_fcomb=4, beta=10.0)
+        net = ProbabilisticUnet(channels, classes, FILTERS, latent_dim=6, no_convs_fcomb=4, beta=10.0)
         sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
         del net
-        segm = torch.randint(0, 3, (B, 1, 256, 256), generator=g).float()
+        segm = torch.randint(0, classes, (B, 1, size, size), generator=g).float()
         eps = torch.randn(B, 6, generator=g)
 
         def one():
-            probunet_train_step(sd, x, segm, eps, 5, 6, 3, 4, 10.0)
+            probunet_train_step(sd, x, segm, eps, 5, 6, classes, 4, 10.0)
         what = "ProbabilisticUnet fwd+elbo+bwd steps (no optimizer, no eval samples)"
     one()  # warm-up
     times = []
@@ -196,11 +243,47 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
             break
     times.sort()
     med = times[len(times) // 2]
-    return {"value": round(B / med, 4), "unit": "slices/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/{'unet' if workload == 'unet' else 'probunet'}_ref.py torch-CPU fp32, "
-                      f"{size}x{size}x{channels}, {classes} class(es), "
-                      f"filters {FILTERS}, batch {B}, median of {len(times)} {what} after 1 warm-up, "
-                      f"{threads} threads"}
+    res = {"value": round(B / med, 4), "unit": "slices/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/{'unet' if workload == 'unet' else 'probunet'}_ref.py torch-CPU fp32, "
+                     f"{size}x{size}x{channels}, {classes} class(es), filters {FILTERS}, batch {B}, median of "
+                     f"{len(times)} {what} after 1 warm-up, {threads} threads"}
+    res.update(host)
+    return res
+
+
+def dice_vs_ref(net, x, t, classes, precision):
+    """The "Dice vs ref" half of the headline metric (BASELINE.json): the HIP network's prediction on
+    the bench batch vs the fp32 CPU oracle's (oracle/unet_ref.py) for the same weights and input,
+    both in train mode (BatchNorm batch statistics) as in the timed step.  Label maps: (p > 0.5) for
+    one class (the trainer's eval, unet_trainer.py:39-58), softmax argmax otherwise.  Reported: per
+    class the Dice of the HIP labels against the oracle's labels, the label agreement, each side's
+    Dice against the target (trainer eval) and their difference."""
+    from oracle.unet_ref import dice_coeff, unet_forward
+    threads, _ = host_cpu()
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    with torch.no_grad():
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=precision == "bf16"):
+            y = net(x).float().cpu()
+        yr = unet_forward(sd, x.cpu(), len(FILTERS), classes)
+    tc = t.cpu()
+    if classes == 1:
+        lab, labr, tgt, ks = (y > 0.5).long()[:, 0], (yr > 0.5).long()[:, 0], tc[:, 0].long(), [1]
+    else:
+        lab, labr = y.argmax(1), yr.argmax(1)
+        tgt, ks = tc.reshape(lab.shape).long(), list(range(1, classes))
+    def d(a, b):
+        return float(dice_coeff(a.float(), b.float()))
+    per = [d(lab == k, labr == k) for k in ks]
+    to_t = [d(lab == k, tgt == k) for k in ks]
+    to_tr = [d(labr == k, tgt == k) for k in ks]
+    return {"classes": ks, "dice_hip_vs_oracle_labels": [round(v, 6) for v in per],
+            "label_agreement": round(float((lab == labr).float().mean()), 7),
+            "dice_to_target_hip": [round(v, 6) for v in to_t], "dice_to_target_oracle": [round(v, 6) for v in to_tr],
+            "max_abs_dice_delta": float(max(abs(a - b) for a, b in zip(to_t, to_tr))),
+            "max_abs_output_delta": float((y - yr).abs().max()),
+            "precision": precision, "oracle": "oracle/unet_ref.py torch-CPU fp32",
+            "sample": f"the bench batch ({x.shape[0]} slices) after the timed steps, train mode"}
 
 
 # C-ABI entry -> regex over the device kernels it launches (rocprof kernel names), for the PMC traffic lookup
@@ -208,7 +291,7 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_fwd": r"conv3x3_(pipe_)?kernel<false", "pmu_conv3x3_dgrad": r"conv3x3_(pipe_)?kernel<true",
     "pmu_conv3x3_wgrad": r"wgrad3x3_kernel<",
     "pmu_conv3x3_fwd_wino": r"conv3x3_wino_(pipe_)?kernel<false", "pmu_conv3x3_dgrad_wino": r"conv3x3_wino_(pipe_)?kernel<true",
-    "pmu_conv3x3_wgrad_wino": r"wgrad3x3_wino_kernel",
+    "pmu_conv3x3_wgrad_wino": (r"wgrad3x3_wino(32)?_kernel", r"wgrad_wino_reduce_kernel"),
     "pmu_conv3x3_fwd_wino_raw": r"conv3x3_wino_raw_kernel<false", "pmu_conv3x3_dgrad_wino_raw": r"conv3x3_wino_raw_kernel<true", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
     "pmu_convT2x2_dgrad": r"convT_pipe_kernel<true>|DuGatherA",
     "pmu_convT2x2_wgrad": r"convT_wgrad_(pipe_)?kernel", "pmu_fcomb_fwd": r"fcomb_fwd_kernel",
@@ -222,22 +305,28 @@ KERNEL_FAMILY = {
 
 
 def pmc_traffic(workload, api):
-    """HBM bytes per launch of ``api``'s kernel family from the newest committed PMC summary
+    """HBM bytes per C-ABI call of ``api`` from the newest committed PMC summary
     (profiles/r*/pmc_traffic_<workload>.json, written by tools/pmc_traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE passes of this bench command).  None when absent."""
+    FETCH_SIZE / WRITE_SIZE passes of this bench command): the bytes of its main kernel family (a
+    regex) plus those of an auxiliary kernel the call also launches (e.g. the weight gradient's
+    slab reduce), divided by the main kernel's dispatch count.  None when absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{workload}.json")))
     import re
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{workload}.json")),
+                   key=lambda f: int(re.search(r"r(\d+)", os.path.relpath(f, ROOT)).group(1)))
     fam = KERNEL_FAMILY.get(api)
     if not files or fam is None:
         return None, None
+    main, aux = fam if isinstance(fam, tuple) else (fam, None)
     data = json.load(open(files[-1]))["kernels"]
     tot, n = 0.0, 0
     for k, v in data.items():
-        if re.search(fam, k):
-            d = v["dispatches_fetch_pass"]
+        d = v["dispatches_fetch_pass"]
+        if re.search(main, k):
             tot += v["hbm_bytes_per_dispatch"] * d
             n += d
+        elif aux and re.search(aux, k):
+            tot += v["hbm_bytes_per_dispatch"] * d
     if n == 0:
         return None, None
     return tot / n, os.path.relpath(files[-1], ROOT)
@@ -314,6 +403,7 @@ def build_unet(args, dev, world, rank):
         return loss
 
     step.net = net
+    step.batch = lambda: (x, tgt)
     flops = conv_flops_per_slice(S, S, FILTERS, args.channels, args.classes) * B
     lossn = "BCE" if args.classes == 1 else "CE"
     tag = "c5" if args.workload == "c5" else "c2"
@@ -542,8 +632,7 @@ def main():
     ms = dt / args.steps * 1e3
     value = world * B * args.steps / dt
 
-    roof = None
-    kernels = None
+    roof = kernels = mfma_busy = None
     if not args.no_kernel_timing:
         timer = KernelTimer()
         L.set_call_observer(timer)
@@ -552,7 +641,7 @@ def main():
         per = timer.summary()
         mf = {k: v for k, v in per.items() if k in KernelTimer.MFMA}
         dom = max(mf, key=lambda k: mf[k][2])
-        n, fl, t = mf[dom]
+        n, fl, t, dfl = mf[dom]
         ach = fl / t / 1e12
         traffic, tsrc = pmc_traffic(args.workload, dom)
         peak = roofline_peak(dom)
@@ -560,32 +649,46 @@ def main():
                 "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "bytes/launch (HBM)",
                 "traffic_source": tsrc, "launches": n, "avg_launch_ms": round(t / n * 1e3, 4),
-                "flops_per_launch": fl / n}
+                "flops_per_launch": fl / n, "flops_basis": "MFMA products the kernel executes"}
         if "_wino" in dom:  # Winograd executes 16 of the direct sum's 36 products per 2x2 tile
-            roof["flops_basis"] = "Winograd F(2x2,3x3) MFMA products (16 per 2x2 output tile per channel pair)"
-            roof["direct_conv_equiv_tflops"] = round(ach * 36 / 16, 2)
+            roof["flops_basis"] = ("executed Winograd F(2x2,3x3) MFMA products (16 per 2x2 output tile per "
+                                   "channel pair); frac is MFMA utilisation")
+            roof["direct_sum_flops_per_launch"] = dfl / n
+            roof["direct_sum_equiv_tflops"] = round(dfl / t / 1e12, 2)
+            roof["direct_sum_equiv_frac"] = round(dfl / t / 1e12 / peak, 4)
+            roof["direct_sum_note"] = ("SURVEY.md §8(d) basis (9 MACs per pixel per channel pair): >1 is possible "
+                                       "because Winograd executes 16/36 of those products; not a utilisation")
         kernels = {k: {"launches": v[0], "ms": round(v[2] * 1e3, 3),
                        "tflops": (round(v[1] / v[2] / 1e12, 2) if v[1] else None)} for k, v in sorted(per.items())}
-        if flops_step is None:   # algorithmic FLOPs of the step = those of the MFMA kernels it launches
-            flops_step = sum(v[1] for v in per.values())
+        # executed MFMA work of the step at each kernel's own peak, over the step time: the MFMA-busy
+        # equivalent of the whole step (BN, pooling, optimizer and launch gaps count as idle)
+        mfma_busy = sum(v[1] / (roofline_peak(k) * 1e12) for k, v in mf.items()) / (ms * 1e-3)
+        if flops_step is None:   # direct-sum FLOPs of the step = those of the MFMA kernels it launches
+            flops_step = sum(v[3] for v in per.values())
     evalres = None
     if args.workload == "c5" and not args.no_eval and rank == 0:
         evalres = c5_eval(step.net, dev, args.eval_size, B, args.precision)
-    cpu = None
+    cpu = dvr = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if args.workload != "probunet":
+            xb, tb = step.batch()
+            dvr = dice_vs_ref(step.net, xb, tb, args.classes, args.precision)
         cpu = cpu_baseline(workload="probunet" if args.workload == "probunet" else "unet", size=args.size,
-                           channels=args.channels, classes=args.classes)
+                           channels=args.channels, classes=3 if args.workload == "probunet" else args.classes)
     if rank == 0:
         res = {
-            "metric": METRIC_C5 if args.workload == "c5" else METRIC, "value": round(value, 3), "unit": "slices/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC_C5 if args.workload == "c5" else METRIC_C4 if args.workload == "probunet" else METRIC,
+            "value": round(value, 3), "unit": "slices/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.precision if args.workload != "probunet" else "fp32",
             "data": data, "config": config,
             "step_tflops": round(flops_step / (ms * 1e-3) / 1e12, 2) if flops_step else None,
-            "step_mfma_frac": round(flops_step / (ms * 1e-3) / 1e12 /
-                                    (BF16_MFMA_PEAK_TF if args.precision == "bf16" else FP32_MFMA_PEAK_TF), 4)
-            if flops_step else None,
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "loss": float(loss.detach()),
+            "step_tflops_basis": "direct-sum algorithmic FLOPs per step (SURVEY.md §8d) / step time",
+            "step_mfma_busy_frac": round(mfma_busy, 4) if mfma_busy is not None else None,
+            "step_mfma_busy_basis": ("sum over MFMA kernels of executed FLOPs / that kernel's dtype peak, over the "
+                                     "step time (HIP events of one instrumented step)"),
+            "roofline": roof, "cpu_baseline": cpu, "dice_vs_ref": dvr, "kernels": kernels,
+            "loss": float(loss.detach()),
         }
         if evalres is not None:
             res["c5_volume_fusion_eval"] = evalres

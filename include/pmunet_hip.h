@@ -259,7 +259,7 @@ int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float* dw, float*
  * ptrs: device array of 3*ntensors pointers (p, g, buf); chunks: device array, one block each. */
 typedef struct pmu_sgd_chunk {
   int tensor; /* index into ptrs/3 */
-  int len;    /* elements in this chunk (<= 65536) */
+  int len;    /* elements in this chunk (any; 16-B aligned chunks of 16384 stream float4) */
   long long start;
 } pmu_sgd_chunk;
 int pmu_sgd_clip(const pmu_sgd_chunk* chunks, int nchunks, void* const* ptrs, float gscale, float lr,

@@ -5,8 +5,9 @@ this module; only tests/, __graft_entry__.smoke() and bench.py's ``cpu_baseline`
 It is written from scratch on torch CPU functional ops and operates on a state_dict (the
 reference's key names), so it needs neither the reference code nor the HIP library.
 
-Parity is pinned: tests/test_oracle_golden.py checks this module against golden vectors that
-tests/golden/make_golden.py produced by importing the reference itself
+Parity is pinned: tests/test_cpu_host.py (G1, G2, G4) and tests/test_train_cpu.py (G8, through
+oracle/train_ref.py) check this module against golden vectors that tests/golden/make_golden.py
+produced by importing the reference itself
 (PMU/ = /root/reference/Probabilistic-Multiplanar-Unet/).
 """
 from __future__ import annotations

@@ -589,19 +589,59 @@ __global__ void rows_sum_split_kernel(const float* __restrict__ ws, int R, int K
 }
 
 // ---------------- SGD + clip ----------------
+// clamp as torch.clamp / clip_grad_value_ does it: a NaN gradient stays NaN (a diverging run shows)
+__device__ __forceinline__ float sgd_one(float& p, float g, float b, float gscale, float lr, float momentum,
+                                         float clip) {
+  float gv = g * gscale;
+  if (clip > 0.f && gv == gv) gv = fminf(fmaxf(gv, -clip), clip);
+  const float bv = fmaf(momentum, b, gv);
+  p = fmaf(-lr, bv, p);
+  return bv;
+}
+
+// One block per chunk (<= PMU_SGD_CHUNK elements of one tensor).  16-B aligned chunks (the flat
+// gradient buffer pads every parameter to 64 floats) stream float4 loads/stores, 4 per thread in
+// flight; others (and the < 4-element tail) go scalar.
 __global__ __launch_bounds__(256) void sgd_clip_kernel(const pmu_sgd_chunk* __restrict__ chunks, void* const* __restrict__ ptrs,
                                                        float gscale, float lr, float momentum, float clip) {
   const pmu_sgd_chunk ck = chunks[blockIdx.x];
-  float* p = (float*)ptrs[3 * ck.tensor + 0];
-  float* g = (float*)ptrs[3 * ck.tensor + 1];
-  float* b = (float*)ptrs[3 * ck.tensor + 2];
-  for (int i = threadIdx.x; i < ck.len; i += blockDim.x) {
-    const long long j = ck.start + i;
-    float gv = g[j] * gscale;
-    if (clip > 0.f) gv = fminf(fmaxf(gv, -clip), clip);
-    const float bv = fmaf(momentum, b[j], gv);
-    b[j] = bv;
-    p[j] = fmaf(-lr, bv, p[j]);
+  float* p = (float*)ptrs[3 * ck.tensor + 0] + ck.start;
+  float* g = (float*)ptrs[3 * ck.tensor + 1] + ck.start;
+  float* b = (float*)ptrs[3 * ck.tensor + 2] + ck.start;
+  const int tid = threadIdx.x;
+  int done = 0;
+  if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)b) & 15) == 0) {
+    const int n4 = ck.len >> 2;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    float4* b4 = reinterpret_cast<float4*>(b);
+    for (int i0 = 0; i0 < n4; i0 += 4 * 256) {
+      float4 pv[4], gv[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256 + tid;
+        if (i < n4) { pv[u] = p4[i]; gv[u] = g4[i]; bv[u] = b4[i]; }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256 + tid;
+        if (i < n4) {
+          float4 o;
+          o.x = sgd_one(pv[u].x, gv[u].x, bv[u].x, gscale, lr, momentum, clip);
+          o.y = sgd_one(pv[u].y, gv[u].y, bv[u].y, gscale, lr, momentum, clip);
+          o.z = sgd_one(pv[u].z, gv[u].z, bv[u].z, gscale, lr, momentum, clip);
+          o.w = sgd_one(pv[u].w, gv[u].w, bv[u].w, gscale, lr, momentum, clip);
+          b4[i] = o;
+          p4[i] = pv[u];
+        }
+      }
+    }
+    done = n4 << 2;
+  }
+  for (int j = done + tid; j < ck.len; j += 256) {
+    float pv = p[j];
+    b[j] = sgd_one(pv, g[j], b[j], gscale, lr, momentum, clip);
+    p[j] = pv;
   }
 }
 

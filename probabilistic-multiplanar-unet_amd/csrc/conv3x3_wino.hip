@@ -609,6 +609,8 @@ static bool wino_pipe_src_ok(const pmu_src& s) {
   return (s.pool == PMU_POOL_MAX2 || s.pool == PMU_POOL_AVG2CEIL) && s.mode == PMU_SRC_BNRELU;
 }
 
+#ifdef PMU_EXPERIMENTS
+// timing experiments (EXP 1-3, 6, 7 compute wrong results): only in `make EXPERIMENTS=1` builds
 static int wino_exp() {
   static const int v = [] {
     const char* e = getenv("PMU_WINO_EXP");
@@ -616,6 +618,7 @@ static int wino_exp() {
   }();
   return v;
 }
+#endif
 
 static bool wino_sync_forced() {
   static const bool v = [] {
@@ -649,6 +652,7 @@ int launch_wino(const pmu_frame* in, const float* wp, const float* bias, int NOU
     if (ok && same_pool && modes_ok) {
       if (dgrad && pool == PMU_POOL_NONE)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<true, PMU_POOL_NONE>), grid, dim3(NT), 0, st, a);
+#ifdef PMU_EXPERIMENTS
       else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 1)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 1>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 2)
@@ -663,6 +667,7 @@ int launch_wino(const pmu_frame* in, const float* wp, const float* bias, int NOU
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 6>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_NONE && wino_exp() == 7)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE, 7>), grid, dim3(NT), 0, st, a);
+#endif
       else if (!dgrad && pool == PMU_POOL_NONE)
         hipLaunchKernelGGL((conv3x3_wino_pipe_kernel<false, PMU_POOL_NONE>), grid, dim3(NT), 0, st, a);
       else if (!dgrad && pool == PMU_POOL_MAX2)

@@ -706,13 +706,17 @@ extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float
     // the output index (((n*2H + 2i)*2W + 2j)*Cout + co) stays 32-bit in the shift path
     if (4LL * M * Cout >= (1LL << 32)) p.lw = -1;
     dim3 grid((unsigned)pmu_cdiv(M, PM), (unsigned)(p.Ncols / PN));
+#ifdef PMU_EXPERIMENTS
+    // timing experiments (wrong results): only in `make EXPERIMENTS=1` builds
     static const int exp = [] {
       const char* e = getenv("PMU_CONVT_EXP");
       return e ? atoi(e) : 0;
     }();
     if (exp == 1) hipLaunchKernelGGL((convT_pipe_kernel<false, 1>), grid, dim3(256), 0, (hipStream_t)stream, p);
     else if (exp == 2) hipLaunchKernelGGL((convT_pipe_kernel<false, 2>), grid, dim3(256), 0, (hipStream_t)stream, p);
-    else hipLaunchKernelGGL(convT_pipe_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
+    else
+#endif
+    hipLaunchKernelGGL(convT_pipe_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }

@@ -371,23 +371,27 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
   PMU_REQUIRE(ws_bytes >= (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(a.nco * (Cin / WCI)), (unsigned)a.nsplit);
-  static const int exp_ = [] {
-    const char* e = getenv("PMU_WINO_EXP");
-    return e ? atoi(e) : 0;
-  }();
   static const bool v16 = [] {
     const char* e = getenv("PMU_WGRAD_WINO");
     return e && strcmp(e, "16x16") == 0;
   }();
-  if (v16) {  // the 16x16x4 layout (all components per wave)
-    if (exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino_kernel<1>), grid, dim3(NT), 0, st, a);
-    else if (exp_ == 3) hipLaunchKernelGGL((wgrad3x3_wino_kernel<3>), grid, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((wgrad3x3_wino_kernel<0>), grid, dim3(NT), 0, st, a);
-  } else {
-    if (exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino32_kernel<1>), grid, dim3(NT), 0, st, a);
-    else if (exp_ == 3) hipLaunchKernelGGL((wgrad3x3_wino32_kernel<3>), grid, dim3(NT), 0, st, a);
-    else hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0>), grid, dim3(NT), 0, st, a);
-  }
+#ifdef PMU_EXPERIMENTS
+  // timing experiments (wrong results for EXP != 0): only in `make EXPERIMENTS=1` builds
+  static const int exp_ = [] {
+    const char* e = getenv("PMU_WINO_EXP");
+    return e ? atoi(e) : 0;
+  }();
+  if (exp_ == 1 || exp_ == 3) {
+    if (v16 && exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino_kernel<1>), grid, dim3(NT), 0, st, a);
+    else if (v16) hipLaunchKernelGGL((wgrad3x3_wino_kernel<3>), grid, dim3(NT), 0, st, a);
+    else if (exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino32_kernel<1>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((wgrad3x3_wino32_kernel<3>), grid, dim3(NT), 0, st, a);
+  } else
+#endif
+  if (v16)  // the 16x16x4 layout (all components per wave)
+    hipLaunchKernelGGL((wgrad3x3_wino_kernel<0>), grid, dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   const long long CC = (long long)Cout * Cin;
   const int blocks = (int)((CC + 255) / 256);

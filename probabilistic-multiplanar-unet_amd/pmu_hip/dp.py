@@ -4,16 +4,22 @@ The reference trains on one device (PMU/train.py:77-117: loss / acc_steps, backw
 the multi-GPU layout here is one process per GPU with a SUM all-reduce of the gradients, which
 reproduces the reference's accumulated gradient exactly (train.py, tests/test_dp_gloo.py).
 
-``BucketAllReduce`` splits the root module's flat gradient buffer (pmu_hip.functions.
-flat_grad_buffer: parameters in registration order) into contiguous buckets taken from its END,
-i.e. in the order the backward produces them (head, decoder from the top level down, deepest
-encoder level, ..., first encoder block).  The HIP backward reports every layer whose gradient
-kernels it has enqueued (GradSink.flush); when a bucket is complete its all-reduce is issued at
-once (RCCL's stream waits on an event of the compute stream at that point), so the exchange of
-the decoder's and the deep levels' gradients runs while the shallow levels' backward still
-computes.  Buckets are issued strictly in index order on every rank (the collective order must
-match across ranks); ``finish`` issues whatever is left (parameters that got no gradient keep
-stale slots, which the optimizer ignores since their .grad is None) and waits.
+``BucketAllReduce`` cuts the root module's flat gradient buffer (pmu_hip.functions.
+flat_grad_buffer) into contiguous buckets **in the order the backward produces the gradients**.
+That order is learned, as DDP does, from the first step: the HIP backward reports every layer
+whose gradient kernels it has enqueued (GradSink.flush); the first step records those reports,
+all-reduces the whole buffer once after the backward, and then re-lays the buffer out in report
+order (``functions.set_grad_order``).  From the second step on, bucket b holds the b-th stretch
+of gradients the backward emits, so when a bucket is complete its all-reduce is issued at once
+(RCCL's stream waits on an event of the compute stream at that point) and crosses xGMI while the
+rest of the backward still computes.  Buckets go out strictly in index order on every rank (the
+collective order must match across ranks).  Parameters the backward never reported (e.g. the
+Probabilistic U-Net's ``unet.outc``, which gets no gradient) sit after the last bucket in a small
+tail that ``finish`` always exchanges, so every rank issues the same collectives.  The learned
+order is rank 0's, broadcast once, so a rank that ran no backward in the first step (an idle rank
+of train.py's exact accumulation) agrees on it.  Gradients autograd kept outside the buffer (a
+module applied twice in one graph, ``zero_grad(set_to_none=False)``) are copied into their slots
+before the remaining buckets go out and copied back after.
 
 Bucket size: xGMI is point-to-point (7 links per GPU), so a ring all-reduce is per-link bound and
 gains nothing from one huge message; ~32 MB buckets keep each RCCL call well past its latency
@@ -26,7 +32,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from .functions import _offsets, flat_grad_buffer
+from .functions import _offsets, _slot, flat_grad_buffer, set_grad_order
 
 DEFAULT_BUCKET_BYTES = 32 << 20
 
@@ -35,9 +41,11 @@ class BucketAllReduce:
     """Overlapped SUM all-reduce of ``net``'s gradients.  Usage per optimizer step::
 
         sync.begin()          # before the LAST backward of the step (accumulation: the others
-        loss.backward()       #   just add into the flat buffer)
+        loss.backward()       #   just add into the .grad tensors)
         sync.finish()         # all buckets issued and waited on; grads hold the sums
-    """
+
+    ``issued_at[b]`` is the index of the GradSink flush (counted from ``begin``) during which
+    bucket b was issued, or None when ``finish`` issued it; ``flushes`` the number of flushes."""
 
     def __init__(self, net, bucket_bytes: int | None = None, group=None):
         if bucket_bytes is None:
@@ -45,30 +53,44 @@ class BucketAllReduce:
         self.net = net
         self.group = group
         self.plist = list(net.parameters())
-        self.buf = flat_grad_buffer(net, self.plist)
-        offs = _offsets(net, self.plist)
-        cap = max(1, bucket_bytes // self.buf.element_size())
-        self.buckets = []      # (lo, hi) element ranges of buf, backward order
+        self.cap = max(1, bucket_bytes // 4)
+        self.buckets = None      # (lo, hi) element ranges of the buffer, backward order
         self.bucket_of = {}
-        members = []
-        hi = self.buf.numel()
-        for p in reversed(self.plist):
+        self.tail = None         # (lo, hi, members): parameters the backward never reported
+        self.recording = None
+        self.active = False
+        self.works = []
+        self.issued_at = []
+        self.flushes = 0
+        net.__dict__["_pmu_grad_ready"] = self._ready
+        order = net.__dict__.get("_pmu_dp_order")
+        if order is not None:    # a layout learned by an earlier reducer of this module
+            self._build(order)
+
+    # ---------------------------------------------------------------- layout
+    def _build(self, reported):
+        """Buckets over ``reported`` (parameters in backward report order); the rest form the tail."""
+        ids = {id(p) for p in reported}
+        rest = [p for p in self.plist if id(p) not in ids]
+        set_grad_order(self.net, list(reported) + rest)
+        self.net.__dict__["_pmu_dp_order"] = list(reported)
+        self.buf = flat_grad_buffer(self.net, self.plist)
+        offs = _offsets(self.net, self.plist)
+        self.buckets, self.bucket_of = [], {}
+        lo, members = 0, []
+        for p in reported:
             members.append(p)
-            lo = offs[id(p)]
-            if hi - lo >= cap:
+            hi = offs[id(p)] + _slot(p.numel())
+            if hi - lo >= self.cap:
                 self._add(lo, hi, members)
-                members, hi = [], lo
+                lo, members = hi, []
         if members:
-            self._add(0, hi, members)
+            self._add(lo, offs[id(members[-1])] + _slot(members[-1].numel()), members)
+        end = self.buckets[-1][1] if self.buckets else 0
+        self.tail = (end, self.buf.numel(), rest) if rest else None
         self.sizes = [0] * len(self.buckets)
         for b in self.bucket_of.values():
             self.sizes[b] += 1
-        self.active = False
-        self.left = []
-        self.next = 0
-        self.works = []
-        self.issued_in_backward = 0
-        net.__dict__["_pmu_grad_ready"] = self._ready
 
     def _add(self, lo, hi, members):
         b = len(self.buckets)
@@ -76,56 +98,105 @@ class BucketAllReduce:
         for p in members:
             self.bucket_of[id(p)] = b
 
+    # ---------------------------------------------------------------- step
     def begin(self):
+        self.works = []
+        self.flushes = 0
+        self.active = True
+        if self.buckets is None:
+            self.recording = []
+            return
         self.left = list(self.sizes)
         self.next = 0
-        self.works = []
-        self.issued_in_backward = 0
-        self.active = True
+        self.issued_at = [None] * len(self.buckets)
 
-    def _issue(self, b):
-        lo, hi = self.buckets[b]
+    def _issue_range(self, lo, hi):
         self.works.append(dist.all_reduce(self.buf[lo:hi], group=self.group, async_op=True))
 
     def _ready(self, params):
         """GradSink.flush callback: ``params``' gradient kernels are enqueued."""
         if not self.active:
             return
+        if self.recording is not None:
+            seen = {id(p) for p in self.recording}
+            self.recording += [p for p in params if id(p) not in seen]
+            return
+        self.flushes += 1
         for p in params:
             b = self.bucket_of.get(id(p))
             if b is not None:
                 self.left[b] -= 1
         while self.next < len(self.buckets) and self.left[self.next] <= 0:
-            self._issue(self.next)
+            self.issued_at[self.next] = self.flushes - 1
+            self._issue_range(*self.buckets[self.next])
             self.next += 1
-            self.issued_in_backward += 1
 
-    def finish(self):
+    @property
+    def issued_in_backward(self) -> int:
+        return sum(1 for i in self.issued_at if i is not None)
+
+    def _agree(self, reported):
+        """Rank 0's report order, broadcast (every rank must cut the same buckets; an idle rank
+        recorded nothing)."""
+        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return reported
+        dev = self.buf.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        pos = {id(p): i for i, p in enumerate(self.plist)}
+        t = torch.full((len(self.plist),), -1, dtype=torch.int64)
+        t[:len(reported)] = torch.tensor([pos[id(p)] for p in reported], dtype=torch.int64)
+        t = t.to(dev)
+        dist.broadcast(t, 0, group=self.group)
+        return [self.plist[i] for i in t.cpu().tolist() if i >= 0]
+
+    def finish(self, idle: bool = False):
+        """Issue what is left, wait, and leave the sums in the gradients.  ``idle``: this rank ran
+        no backward this step (fewer micro-batches than ranks); it contributes zeros and adopts
+        the summed gradients of every parameter the backward reports."""
         if not self.active:
             raise RuntimeError("BucketAllReduce.finish() without begin()")
         self.active = False
-        lo, hi = self.buf.data_ptr(), self.buf.data_ptr() + self.buf.numel() * self.buf.element_size()
+        self.buf = buf = flat_grad_buffer(self.net, self.plist)
+        offs = _offsets(self.net, self.plist)
+        lo, hi = buf.data_ptr(), buf.data_ptr() + buf.numel() * buf.element_size()
         foreign = [p for p in self.plist if p.grad is not None and not lo <= p.grad.data_ptr() < hi]
-        if foreign and self.next > 0:
-            # a bucket already in flight would race with autograd copying it into a fresh .grad
-            raise RuntimeError("gradients were not adopted from the flat buffer while buckets were in flight")
-        while self.next < len(self.buckets):
-            self._issue(self.next)
-            self.next += 1
+        if idle:
+            if any(p.grad is not None for p in self.plist):
+                raise RuntimeError("BucketAllReduce.finish(idle=True) with gradients present")
+            buf.zero_()
+        slot = lambda p: buf[offs[id(p)]:offs[id(p)] + p.numel()].view_as(p)  # noqa: E731
+        if self.recording is not None:
+            # first step: the whole buffer in one all-reduce, then the learned layout
+            for p in foreign:
+                slot(p).copy_(p.grad)
+            self._issue_range(0, buf.numel())
+            reported = self._agree(self.recording)
+            self.recording = None
+            self._wait(foreign, slot, reported if idle else ())
+            if reported:
+                self._build(reported)
+            return
         if foreign:
-            # grads that autograd accumulated outside the buffer (zero_grad(set_to_none=False)):
-            # one flattened bucket, issued after the buffer's buckets on every rank
-            flat = torch.cat([p.grad.reshape(-1) for p in foreign])
-            self.works.append(dist.all_reduce(flat, group=self.group, async_op=True))
+            issued = {id(p) for b in range(self.next) for p in self.plist if self.bucket_of.get(id(p)) == b}
+            if any(id(p) in issued for p in foreign):
+                # a bucket already in flight would race with autograd copying it into a fresh .grad
+                raise RuntimeError("gradients were not adopted from the flat buffer while buckets were in flight")
+            for p in foreign:
+                slot(p).copy_(p.grad)
+        while self.next < len(self.buckets):
+            self._issue_range(*self.buckets[self.next])
+            self.next += 1
+        if self.tail is not None:   # always, so every rank issues the same collectives
+            self._issue_range(self.tail[0], self.tail[1])
+        self._wait(foreign, slot, self.net.__dict__["_pmu_dp_order"] if idle else ())
+
+    def _wait(self, foreign, slot, adopt):
         for w in self.works:
             w.wait()
         self.works = []
-        if foreign:
-            off = 0
-            for p in foreign:
-                n = p.grad.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
+        for p in foreign:   # grads autograd kept outside the buffer get their sums back
+            p.grad.copy_(slot(p))
+        for p in adopt:     # idle rank: the summed gradients of the busy ranks
+            p.grad = slot(p)
 
     def detach(self):
         self.net.__dict__.pop("_pmu_grad_ready", None)

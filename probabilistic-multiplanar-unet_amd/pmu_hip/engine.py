@@ -676,3 +676,26 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             L.call("pmu_maxpool2_bwd", dpool.data_ptr(), prev.z.data_ptr(), prev.bn.coef.data_ptr(), N, hp, wp, Cp,
                    dskip[lev - 1].data_ptr(), 1, s)
     return grads
+
+
+def unet_report_order(net) -> list:
+    """The parameter groups in the order unet_backward reports them (one GradSink.flush each): the
+    head, then per up block (last first) conv2, conv1 and the ConvTranspose2d, then per encoder level
+    (deepest first) conv2 and conv1 — within a conv layer BN weight, BN bias, conv bias, conv weight.
+    This is the layout pmu_hip.dp learns from the first data-parallel step (and what the CPU tests
+    of the bucket logic replay)."""
+    def conv_group(conv, bn):
+        return [p for p in (bn.weight, bn.bias, conv.bias, conv.weight) if p is not None]
+    groups = []
+    if net.apply_last_layer:
+        groups.append([p for p in (net.outc.conv.weight, net.outc.conv.bias) if p is not None])
+    for j in reversed(range(len(net.up_blocks))):
+        up = net.up_blocks[j]
+        c1w, b1, c2w, b2 = _dc_layers(up.conv)
+        groups += [conv_group(c2w, b2), conv_group(c1w, b1),
+                   [p for p in (up.up.weight, up.up.bias) if p is not None]]
+    blocks = [net.inc] + [d.maxpool_conv[1] for d in net.down_blocks]
+    for dc in reversed(blocks):
+        c1w, b1, c2w, b2 = _dc_layers(dc)
+        groups += [conv_group(c2w, b2), conv_group(c1w, b1)]
+    return groups

@@ -36,10 +36,35 @@ def grad_root(module):
     return root if root is not None else module
 
 
+ALIGN = 64   # every slot starts on a 256-B boundary: the fused optimizer streams float4
+
+
+def _slot(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+def grad_layout(net, plist):
+    """Parameters in flat-buffer order: the order the backward produced them when one was recorded
+    (``set_grad_order``, pmu_hip.dp learns it from the first step), else registration order."""
+    order = net.__dict__.get("_pmu_grad_order")
+    if order is None:
+        return list(plist)
+    pos = {pid: i for i, pid in enumerate(order)}
+    return sorted(plist, key=lambda p: pos.get(id(p), len(pos)))
+
+
+def set_grad_order(net, params_in_order):
+    """Lay the flat gradient buffer out in this parameter order from the next backward on (the
+    current .grad views keep the old layout until they are released)."""
+    net.__dict__["_pmu_grad_order"] = [id(p) for p in params_in_order]
+    net.__dict__["_pmu_grad_offsets"] = None
+
+
 def flat_grad_buffer(net, plist=None):
-    """The persistent flat fp32 gradient buffer of ``net`` (registration order), created on demand."""
+    """The persistent flat fp32 gradient buffer of ``net``, created on demand: one 64-float aligned
+    slot per parameter (pads stay zero), in ``grad_layout`` order."""
     plist = plist if plist is not None else list(net.parameters())
-    total = sum(p.numel() for p in plist)
+    total = sum(_slot(p.numel()) for p in plist)
     buf = net.__dict__.get("_pmu_grad_flat")
     dev = plist[0].device
     if buf is None or buf.numel() != total or buf.device != dev:
@@ -50,22 +75,46 @@ def flat_grad_buffer(net, plist=None):
 
 
 def _offsets(root, plist):
+    """{id(param): element offset of its slot in the flat buffer}."""
     cached = root.__dict__.get("_pmu_grad_offsets")
     key = tuple(id(p) for p in plist)
     if cached is None or cached[0] != key:
         offs, o = {}, 0
-        for p in plist:
+        for p in grad_layout(root, plist):
             offs[id(p)] = o
-            o += p.numel()
+            o += _slot(p.numel())
         cached = (key, offs)
         root.__dict__["_pmu_grad_offsets"] = cached
     return cached[1]
 
 
+class LiveNode:
+    """Marks one pending autograd node of ``module`` (created in forward, released when its backward
+    has run or its graph was freed).  While two nodes of one module are pending — the module applied
+    twice in one graph, e.g. loss(net(x1)) + loss(net(x2)) — their gradients must not both be views
+    of the same flat-buffer slots: autograd sums the two node outputs before AccumulateGrad, and
+    aliased views would give 2*g2 instead of g1 + g2."""
+    __slots__ = ("d",)
+
+    def __init__(self, module):
+        self.d = module.__dict__
+        self.d["_pmu_live"] = self.d.get("_pmu_live", 0) + 1
+
+    def release(self):
+        if self.d is not None:
+            self.d["_pmu_live"] -= 1
+            self.d = None
+
+    def __del__(self):
+        self.release()
+
+
 def grad_sink_for(module, params) -> GradSink:
     """Destination of this node's parameter gradients (fresh flat-buffer views, see module doc).
-    The views are created per backward and not retained, so autograd can adopt them as .grad."""
-    if not all(p.grad is None for p in params):
+    The views are created per backward and not retained, so autograd can adopt them as .grad.
+    Plain tensors instead when a .grad already exists (autograd accumulates into it) or another
+    node of the same module is still pending (see LiveNode)."""
+    if not all(p.grad is None for p in params) or module.__dict__.get("_pmu_live", 0) > 1:
         return GradSink()
     root = grad_root(module)
     plist = list(root.parameters())
@@ -96,13 +145,16 @@ class UNetFunction(torch.autograd.Function):
         out, st = engine.unet_forward(net, x, net.training, bf16=bf16, keep=True)
         ctx.net = net
         ctx.st = st
+        ctx.live = LiveNode(net)
         return out
 
     @staticmethod
     def backward(ctx, dy):
         net = ctx.net
         plist = list(net.parameters())
-        grads = engine.unet_backward(net, ctx.st, dy, grad_sink_for(net, plist))
+        sink = grad_sink_for(net, plist)
+        ctx.live.release()
+        grads = engine.unet_backward(net, ctx.st, dy, sink)
         grads.flush()
         ctx.st = None
         return (None, None, None) + tuple(grads.get(p) for p in plist)
@@ -137,13 +189,16 @@ class GaussianFunction(torch.autograd.Function):
     def forward(ctx, g, x, segm, *params):
         mls, st = prob_engine.gaussian_forward(g, _planes(x, segm), g.training, keep=True)
         ctx.g, ctx.st = g, st
+        ctx.live = LiveNode(g)
         return mls
 
     @staticmethod
     def backward(ctx, dmls):
         g = ctx.g
         plist = list(g.parameters())
-        grads = prob_engine.gaussian_backward(g, ctx.st, dmls, grad_sink_for(g, plist))
+        sink = grad_sink_for(g, plist)
+        ctx.live.release()
+        grads = prob_engine.gaussian_backward(g, ctx.st, dmls, sink)
         grads.flush()
         ctx.st = None
         return (None, None, None) + tuple(grads.get(p) for p in plist)
@@ -171,6 +226,7 @@ class FcombFunction(torch.autograd.Function):
         y, fh, zc, zb = prob_engine.fcomb_forward(fc, feat, z.unsqueeze(0))
         ctx.fc = fc
         ctx.save = (fh, zc[0], zb)
+        ctx.live = LiveNode(fc)
         return y[0]
 
     @staticmethod
@@ -179,6 +235,7 @@ class FcombFunction(torch.autograd.Function):
         fh, zc, zb = ctx.save
         plist = list(fc.parameters())
         grads = grad_sink_for(fc, plist)
+        ctx.live.release()
         dfeat, dz = prob_engine.fcomb_backward(fc, fh, zc, zb, dy, grads)
         grads.flush()
         ctx.save = None

@@ -17,7 +17,7 @@ import torch
 
 from . import _lib as L
 
-CHUNK = 65536
+CHUNK = 16384   # elements per block: 16 per thread, 4 float4 loads of p, g and buf in flight
 
 
 class FusedSGD(torch.optim.Optimizer):
@@ -27,10 +27,16 @@ class FusedSGD(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, momentum=momentum, clip=clip))
         self._tables = {}
 
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict; the loaded momentum buffers replace the ones the
+        kernel's cached pointer tables name."""
+        super().load_state_dict(state_dict)
+        self._tables.clear()
+
     def _table(self, plist, dev):
-        key = tuple((p.data_ptr(), p.grad.data_ptr()) for p in plist)
+        key = tuple((p.data_ptr(), p.grad.data_ptr(), id(self.state[p].get("momentum_buffer"))) for p in plist)
         tab = self._tables.get(key)
-        if tab is not None:
+        if tab is not None and all(t is self.state[p].get("momentum_buffer") for t, p in zip(tab[3], plist)):
             return tab
         ptrs, chunks = [], []
         for i, p in enumerate(plist):
@@ -48,6 +54,7 @@ class FusedSGD(torch.optim.Optimizer):
         tab = (ptr_t, ck_t, len(chunks), [self.state[p]["momentum_buffer"] for p in plist])
         if len(self._tables) > 8:
             self._tables.clear()
+        key = tuple((p.data_ptr(), p.grad.data_ptr(), id(self.state[p]["momentum_buffer"])) for p in plist)
         self._tables[key] = tab
         return tab
 

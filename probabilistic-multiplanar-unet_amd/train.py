@@ -13,13 +13,20 @@ MI355X-first differences: batches are assembled on the GPU from resident scans
 (MRI_Dataset.get_batch) instead of a 6-worker DataLoader re-reading volumes from disk, and the loop
 is data-parallel when launched with torch.distributed (one process per GPU, RCCL):
 
-  the acc micro-batches of an optimizer step are dealt round-robin over the ranks (each rank takes
-  max(1, acc_steps // world)), every rank scales its loss by 1 / (micro-batches per step), and one
-  SUM all-reduce of the flat gradient buffer yields exactly the reference's accumulated gradient
-  (``dp_micro_batches`` / ``allreduce_grads``; checked against the reference's own accumulation in
-  tests/test_dp_gloo.py).  BatchNorm statistics stay per micro-batch, as in the reference.  The
-  all-reduce is bucketed and issued during the last micro-batch's backward (pmu_hip.dp;
-  PMU_DP_OVERLAP=0 selects the one-shot all-reduce after the backward).
+  every optimizer step consumes the reference's acc_steps consecutive micro-batches; micro-batch k
+  of a step goes to rank k % world, every rank scales its loss by 1 / acc_steps, and one SUM
+  all-reduce of the flat gradient buffer yields exactly the reference's accumulated gradient, for
+  any world size (ranks beyond acc_steps are idle for the step; the global batch never changes).
+  ``dp_micro_batches`` / ``allreduce_grads``; checked against the reference's own accumulation in
+  tests/test_dp_gloo.py.  BatchNorm statistics stay per micro-batch, as in the reference; before
+  validation and checkpoints the replicas' running statistics are averaged (``BNSync``) so every
+  rank validates, schedules the learning rate and saves the same model.  The all-reduce is
+  bucketed and issued during the last micro-batch's backward (pmu_hip.dp; PMU_DP_OVERLAP=0 selects
+  the one-shot all-reduce after the backward).
+
+The default RNG stream is consumed as the reference's (random_split, then per loader iterator a
+base-seed draw and the RandomSampler's seed), so a seeded single-GPU run visits the slices in the
+reference's order (tests/test_train_gpu.py checks a whole run against golden vectors G8).
 """
 from __future__ import annotations
 
@@ -75,39 +82,65 @@ def shared_generator():
     return torch.Generator().manual_seed(int(seed))
 
 
-def epoch_order(n, world):
-    """Shuffled sample order of one epoch: the reference DataLoader's RandomSampler (:47) on one
-    rank, a broadcast-seeded permutation shared by all ranks otherwise."""
+def loader_order(n, shuffle, world):
+    """Sample order of one pass of the reference's DataLoader (:47-48), with its RNG draws: creating
+    the loader iterator draws a base seed from the default generator (workers' seeds), then a
+    RandomSampler (shuffle) draws its own seed and permutes.  Reproducing both draws keeps the
+    default RNG stream — and so the split and every epoch's order — identical to the reference's.
+    world > 1: rank 0's draws, broadcast, so all ranks agree."""
+    seed = torch.empty((), dtype=torch.int64).random_().item()   # _BaseDataLoaderIter._base_seed
+    del seed
+    if not shuffle:
+        return list(range(n))
     if world == 1:
         return list(RandomSampler(range(n)))
     return torch.randperm(n, generator=shared_generator()).tolist()
 
 
+def epoch_order(n, world):
+    """Shuffled sample order of one training epoch (see loader_order)."""
+    return loader_order(n, True, world)
+
+
 def dp_micro_batches(order, micro, acc_steps, world, rank):
-    """Deal the drop_last micro-batches of one epoch's sample ``order`` to ranks.
+    """Deal one epoch's drop_last micro-batches (sample ``order``, ``micro`` slices each) to ranks,
+    exactly as the reference accumulates them (:45-49, :77-110).
 
-    Returns (steps, per_rank_acc): ``steps`` is a list of optimizer steps, each a list of this
-    rank's micro-batches (lists of dataset indices).  Every optimizer step consumes
-    per_rank_acc * world micro-batches, dealt round-robin (micro-batch k of a step -> rank k % world)."""
-    per_rank = max(1, acc_steps // world)
-    per_step = per_rank * world
+    Every optimizer step consumes the reference's ``acc_steps`` consecutive micro-batches; micro-
+    batch k of a step goes to rank k % world.  Each rank scales its loss by 1 / acc_steps (the
+    reference's loss / acc_steps) and a SUM all-reduce then gives exactly the reference's
+    accumulated gradient — for any world size: with world > acc_steps the extra ranks are idle for
+    the step (they contribute zeros), so the global batch never changes.
+
+    Returns (steps, leftover): ``steps[s]`` = this rank's micro-batches of optimizer step s (lists
+    of dataset indices; empty = idle), ``leftover`` = this rank's share of the trailing micro-
+    batches that fill no step (the reference runs them and never steps: only their BatchNorm
+    running-statistics updates survive)."""
     mbs = [list(order[i:i + micro]) for i in range(0, len(order) - micro + 1, micro)]
-    nsteps = len(mbs) // per_step
-    steps = []
-    for s in range(nsteps):
-        group = mbs[s * per_step:(s + 1) * per_step]
-        steps.append([group[k] for k in range(rank, per_step, world)])
-    return steps, per_rank
+    nsteps = len(mbs) // acc_steps
+    steps = [[mbs[s * acc_steps + k] for k in range(rank, acc_steps, world)] for s in range(nsteps)]
+    rest = mbs[nsteps * acc_steps:]
+    return steps, [rest[k] for k in range(rank, len(rest), world)]
 
 
-def allreduce_grads(net, plist=None):
+def allreduce_grads(net, plist=None, idle=False):
     """SUM all-reduce of every gradient: one collective over the flat gradient buffer when all
-    grads are its views (the HIP autograd nodes arrange that), else one flattened bucket."""
+    grads are its views (the HIP autograd nodes arrange that), else one flattened bucket.
+    ``idle``: this rank ran no micro-batch this step; it contributes zeros and adopts the sums
+    (every parameter gets a gradient; ones no rank computed stay zero)."""
     world, _ = world_info()
     if world == 1:
         return
-    from pmu_hip.functions import flat_grad_buffer
+    from pmu_hip.functions import _offsets, flat_grad_buffer
     plist = plist if plist is not None else [p for p in net.parameters()]
+    if idle:
+        buf = flat_grad_buffer(net, plist)
+        buf.zero_()
+        dist.all_reduce(buf)
+        offs = _offsets(net, plist)
+        for p in plist:
+            p.grad = buf[offs[id(p)]:offs[id(p)] + p.numel()].view_as(p)
+        return
     with_grad = [p for p in plist if p.grad is not None]
     buf = net.__dict__.get("_pmu_grad_flat")
     if buf is not None:
@@ -126,8 +159,51 @@ def allreduce_grads(net, plist=None):
             off += n
 
 
+class BNSync:
+    """Keeps the replicas' BatchNorm buffers identical for validation and checkpoints (world > 1):
+    running_mean / running_var are averaged over the ranks (each rank's EMA saw only its own
+    micro-batches) and num_batches_tracked becomes the count over all ranks, which equals the
+    reference's single-process count."""
+
+    def __init__(self, net):
+        self.bns = [m for m in net.modules() if isinstance(m, torch.nn.BatchNorm2d) and m.track_running_stats]
+        self.base = [int(m.num_batches_tracked) for m in self.bns]
+
+    def __call__(self):
+        world, _ = world_info()
+        if world == 1 or not self.bns:
+            return
+        dev = self.bns[0].running_mean.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        stats = torch.cat([torch.cat([m.running_mean, m.running_var]) for m in self.bns]).to(dev)
+        dist.all_reduce(stats)
+        stats = (stats / world).to(self.bns[0].running_mean.device)
+        cnt = torch.tensor([int(m.num_batches_tracked) - b for m, b in zip(self.bns, self.base)],
+                           dtype=torch.int64, device=dev)
+        dist.all_reduce(cnt)
+        o = 0
+        for i, m in enumerate(self.bns):
+            c = m.running_mean.numel()
+            m.running_mean.copy_(stats[o:o + c])
+            m.running_var.copy_(stats[o + c:o + 2 * c])
+            o += 2 * c
+            m.num_batches_tracked.fill_(self.base[i] + int(cnt[i]))
+            self.base[i] = int(m.num_batches_tracked)
+
+
+def _from_rank(value, src, dev):
+    """A float held by rank ``src`` on every rank (the reference logs the last micro-batch's loss)."""
+    world, rank = world_info()
+    if world == 1:
+        return value
+    t = torch.tensor([value if rank == src else 0.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    return float(t)
+
+
 def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2, om=0.9, val_percent=0.1,
-              save_cp=False, dataset=None):
+              save_cp=False, dataset=None, writer=None):
+    """train.py:27-196.  ``dataset`` (an MRI_Dataset; default: built from dir_img/dir_mask) and
+    ``writer`` (a SummaryWriter-like sink; default: TensorBoard when installed) are injectable."""
     from pmu_hip.optim import FusedSGD
     from utils.mri_dataset import MRI_Dataset
 
@@ -142,10 +218,16 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
         train, val = random_split(dataset, [n_train, n_val], generator=shared_generator())
     acc_steps = 4 if batch_size > 4 else 1
     micro = batch_size // acc_steps
-    writer = _writer(f"LRF_{lrf}_LRP_{lrp}_EP_{epochs}_LR_{lr}_BS_{batch_size}") if rank == 0 else _NullWriter()
+    if writer is None:
+        writer = _writer(f"LRF_{lrf}_LRP_{lrp}_EP_{epochs}_LR_{lr}_BS_{batch_size}") if rank == 0 else _NullWriter()
+    elif rank != 0:
+        writer = _NullWriter()
     global_step = 0
     logging.info(f"Starting training: epochs {epochs}, batch size {batch_size}, lr {lr}, training size {n_train}, "
                  f"validation size {n_val}, checkpoints {save_cp}, device {device}, ranks {world}")
+    if world > acc_steps:
+        logging.warning(f"{world} ranks > {acc_steps} accumulation micro-batches per step: {world - acc_steps} "
+                        f"rank(s) idle each step (the global batch stays {batch_size}, as in the reference)")
     net = trainer.net
     optimizer = FusedSGD(net.parameters(), lr=lr, momentum=om, clip=0.1)
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, "min" if net.n_classes > 1 else "max",
@@ -155,14 +237,17 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
     if world > 1 and os.environ.get("PMU_DP_OVERLAP", "1") != "0":
         from pmu_hip.dp import BucketAllReduce
         sync = BucketAllReduce(net)
+    bn_sync = BNSync(net)
+    n_train_mb = n_train // micro if micro else 0
     for epoch in range(epochs):
         net.train()
         # ---- train phase
         order = [train.indices[i] for i in epoch_order(n_train, world)]
-        steps, per_rank = dp_micro_batches(order, micro, acc_steps, world, rank)
-        scale = 1.0 / (per_rank * world)
+        steps, leftover = dp_micro_batches(order, micro, acc_steps, world, rank)
+        scale = 1.0 / acc_steps
         optimizer.zero_grad()
-        for step_mbs in steps:
+        for s, step_mbs in enumerate(steps):
+            last = None
             for i, mb in enumerate(step_mbs):
                 b = dataset.get_batch(mb)
                 imgs = b["image"]
@@ -172,17 +257,32 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
                 if sync is not None and i == len(step_mbs) - 1:
                     sync.begin()      # the last micro-batch's backward issues the bucket all-reduces
                 loss.backward()
+                last = loss
+            idle = not step_mbs
             if sync is not None:
-                sync.finish()
+                if idle:
+                    sync.begin()
+                sync.finish(idle=idle)
             else:
-                allreduce_grads(net, plist)
+                allreduce_grads(net, plist, idle=idle and world > 1)
+            # the reference logs the step's last micro-batch (k = acc_steps - 1) at its global step
+            owner = (acc_steps - 1) % world
+            out_loss = _from_rank(float(last.item()) if (last is not None and rank == owner) else 0.0, owner, device)
+            writer.add_scalar("Loss/train", out_loss, global_step + s * acc_steps + acc_steps - 1)
             optimizer.step()
             optimizer.zero_grad()
-            writer.add_scalar("Loss/train", loss.item(), global_step)
-            global_step += 1
-        # ---- validation phase (every rank evaluates the full validation split)
+        if leftover:   # trailing micro-batches: forward for their BatchNorm statistics, no step
+            with torch.no_grad():
+                for mb in leftover:
+                    b = dataset.get_batch(mb)
+                    trainer.predict(b["image"], b["mask"].to(dtype=trainer.mask_type))
+        global_step += n_train_mb
+        # ---- validation phase (replicas agree on BN statistics; every rank evaluates the split)
+        bn_sync()
         net.eval()
+        loader_order(n_val, False, world)     # the validation loader's iterator draw (:49)
         val_batches = [list(val.indices[i:i + micro]) for i in range(0, n_val - micro + 1, micro)] if micro else []
+        val_count = len(val_batches)
         dices, dice_sums, loss_sum = 0, np.zeros(max(0, net.n_classes - 1)), 0.0
         for mb in val_batches:
             b = dataset.get_batch(mb)
@@ -195,12 +295,24 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
                 dice_sums += dice
             else:
                 dices += dice
-        val_count = max(1, len(val_batches))
+            if global_step % val_count == 0:   # one example per validation round (:155-160)
+                writer.add_images("images", imgs, global_step)
+                writer.add_images("masks/true", trainer.mask_to_image(true_masks), global_step)
+                writer.add_images("masks/pred", trainer.mask_to_image(masks_pred, prediction=True), global_step)
+            global_step += 1
+        val_count = max(1, val_count)
         avg_loss = loss_sum / val_count
         writer.add_scalar("Loss/validation", avg_loss, global_step)
+        writer.add_scalar("learning_rate", optimizer.param_groups[0]["lr"], global_step)
         for c in range(net.n_classes - 1):
             writer.add_scalar(f"dice/class_{c + 1}", dice_sums[c] / val_count, global_step)
-        val_score = (dices / val_count)[0] if net.n_classes == 1 and val_batches else avg_loss
+        if net.n_classes == 1:
+            val_score = float((dices / val_count)[0]) if val_batches else 0.0
+            logging.info(f"Validation Dice Coeff: {val_score}")
+            writer.add_scalar("metrics/dice", val_score, global_step)
+        else:
+            val_score = avg_loss
+        val_score = _from_rank(val_score, 0, device)   # one learning-rate schedule for all replicas
         scheduler.step(val_score)
         if rank == 0:
             os.makedirs(dir_checkpoint, exist_ok=True)
@@ -208,6 +320,7 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
             logging.info(f"Saved model {trainer.name}_checkpoint{epoch}.pt")
         gc.collect()
     if rank == 0:
+        os.makedirs(dir_checkpoint, exist_ok=True)
         torch.save(net.state_dict(), os.path.join(dir_checkpoint, trainer.name + "_model.pt"))
         logging.info(f"Saved model {trainer.name}_model.pt")
     writer.close()

@@ -306,11 +306,87 @@ def g7_dp_accumulation():
     np.savez_compressed(os.path.join(OUT, "g7_dp.npz"), **out)
 
 
+def g8_train_net(nib):
+    """The reference's own train_net (train.py:27-196) end to end on a tiny in-memory multi-planar
+    dataset: two 24x24x20 scans (cube-padded to 24^3, 3 views, background slices filtered) with
+    binary ellipsoid labels, a UNet(1,1,[16,32]) in place of the trainer's default-width net,
+    batch 8 (4 accumulated micro-batches of 2), 2 epochs, validation 10%, ReduceLROnPlateau.
+
+    Recorded: the initial weights, the seed set right before train_net, the volumes, every
+    SummaryWriter scalar (tag, value, global_step) and image (tag, step, tensor), the dataset item
+    order, and the final state_dict.  Shims beyond the import ones: the DataLoader runs with
+    num_workers=0 (the worker processes change neither the RNG draws nor the batches), the
+    SummaryWriter records instead of writing, checkpoints go to a temporary directory."""
+    import tempfile
+    import utils.mri_dataset as md
+    md.mri_collate = None   # imported by train.py:19, never defined (SURVEY.md §8c shim 4)
+    import train as ref_train
+    from model import UNet
+    from torch.utils.data import DataLoader
+    from trainer import UNetTrainer
+    g = np.random.default_rng(8)
+    out = {}
+    names = ["s0.nii", "s1.nii"]
+    ax = np.arange(24) - 11.5
+    for i, name in enumerate(names):
+        ii, jj, kk = np.meshgrid(ax, ax, ax[:20] + 2, indexing="ij")
+        r2 = (ii / (7.0 + i)) ** 2 + (jj / 6.0) ** 2 + (kk / 5.0) ** 2
+        lab = (r2 < 1.0).astype(np.float64)
+        img = g.random((24, 24, 20)) * 80.0 + lab * 120.0
+        nib.store["img_" + name], nib.store["lab_" + name] = img, lab
+        out[f"vol/{name}/img"], out[f"vol/{name}/lab"] = img, lab
+    md.listdir = lambda d: list(names)
+    orig_load = nib.load
+    nib.load = lambda p: orig_load(("img_" if "imgs" in p else "lab_") + os.path.basename(p))
+    order = []
+
+    class LoggedDataset(md.MRI_Dataset):
+        def __getitem__(self, i):
+            order.append(int(i))
+            return super().__getitem__(i)
+    ref_train.MRI_Dataset = LoggedDataset
+    ref_train.DataLoader = lambda *a, **k: DataLoader(*a, **{**k, "num_workers": 0, "pin_memory": False})
+    scalars, images = [], []
+
+    class RecordingWriter:
+        def __init__(self, *a, **k):
+            pass
+
+        def add_scalar(self, tag, v, step):
+            scalars.append((tag, float(v), int(step)))
+
+        def add_images(self, tag, t, step):
+            images.append((tag, int(step), t.detach().cpu().float().numpy().copy()))
+
+        def close(self):
+            pass
+    ref_train.SummaryWriter = RecordingWriter
+    tmp = tempfile.mkdtemp()
+    ref_train.dir_img, ref_train.dir_mask, ref_train.dir_checkpoint = "/imgs/", "/labs/", tmp + "/"
+    tr = UNetTrainer(torch.device("cpu"), 1, 1)
+    torch.manual_seed(0)
+    tr.net = UNet(1, 1, [16, 32])
+    out.update(sd_np("init", tr.net.state_dict()))
+    torch.manual_seed(123)
+    ref_train.train_net(tr, torch.device("cpu"), epochs=2, batch_size=8, lr=0.01, lrf=0.5, lrp=0, om=0.9,
+                        val_percent=0.1)
+    out.update(sd_np("final", tr.net.state_dict()))
+    out["seed"] = np.array(123)
+    out["order"] = np.array(order, dtype=np.int64)
+    out["scalar_tags"] = np.array([t for t, _, _ in scalars])
+    out["scalar_values"] = np.array([v for _, v, _ in scalars], dtype=np.float64)
+    out["scalar_steps"] = np.array([s for _, _, s in scalars], dtype=np.int64)
+    for i, (tag, step, t) in enumerate(images):
+        out[f"image{i}/tag"], out[f"image{i}/step"], out[f"image{i}/data"] = np.array(tag), np.array(step), t
+    nib.load = orig_load
+    np.savez_compressed(os.path.join(OUT, "g8_train_net.npz"), **out)
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit(f"reference not found at {REF}: fixtures are generated in the build container only")
     nib = install_shims()
-    which = set(sys.argv[1:]) or {"g1", "g2", "g3", "g4", "g5", "g6", "g7"}
+    which = set(sys.argv[1:]) or {"g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8"}
     if "g1" in which:
         g1_unet_c1()
     if "g2" in which:
@@ -325,6 +401,8 @@ def main():
         g6_fusion()
     if "g7" in which:
         g7_dp_accumulation()
+    if "g8" in which:
+        g8_train_net(nib)
     print("golden fixtures written to", OUT)
 
 

@@ -67,23 +67,20 @@ def test_oracle_accumulation_matches_reference_g7():
 
 
 @pytest.mark.parametrize("n,micro,acc,world", [(103, 2, 4, 2), (64, 4, 4, 4), (50, 1, 1, 2), (77, 8, 4, 8),
-                                               (40, 2, 4, 1)])
+                                               (40, 2, 4, 1), (90, 2, 4, 3)])
 def test_dp_micro_batches_partition(n, micro, acc, world):
-    """Every optimizer step deals per_rank*world drop_last micro-batches round-robin: ranks are
-    disjoint, cover the same micro-batches a single process would use, and take equal step counts."""
+    """The ranks' micro-batches are disjoint and together are exactly the single process's drop_last
+    micro-batches (steps of acc, then the trailing ones); every rank has the same step count."""
     from train import dp_micro_batches
     order = list(np.random.default_rng(0).permutation(n))
     per = [dp_micro_batches(order, micro, acc, world, r) for r in range(world)]
     steps = {len(s) for s, _ in per}
     assert len(steps) == 1
-    per_rank = per[0][1]
-    assert per_rank == max(1, acc // world)
-    seen = [i for s, _ in per for st in s for mb in st for i in mb]
+    seen = [i for s, left in per for mb in [m for st in s for m in st] + left for i in mb]
     assert len(seen) == len(set(seen))
-    for s, _ in per:
-        for st in s:
-            assert len(st) == per_rank and all(len(mb) == micro for mb in st)
-    used = steps.pop() * per_rank * world * micro
+    for s, left in per:
+        assert all(len(mb) == micro for st in s for mb in st) and all(len(mb) == micro for mb in left)
+    used = (n // micro) * micro
     assert sorted(seen) == sorted(order[:used])
 
 

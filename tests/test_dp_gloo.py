@@ -1,11 +1,14 @@
-"""Data-parallel host logic on CPU with the gloo backend, world size 2 (row e).
+"""Data-parallel host logic on CPU with the gloo backend, world sizes 2, 4 and 8 (row e).
 
-Each rank computes its round-robin share of the 8 micro-batches of G7 (c1, 4 slices each) with
-loss / (micro-batches per step), as train.py's loop does, and train.allreduce_grads sums them.
-The result must equal the reference's single-process accumulation (tests/golden/g7_dp.npz).
-Both all-reduce paths are exercised: the flat gradient buffer (grads are views of it, as the HIP
-autograd nodes produce them) and the flattened-bucket fallback.  The per-rank gradients here come
-from the CPU oracle: the HIP forward/backward needs a GPU, the all-reduce logic under test does not.
+Each rank computes its share of the micro-batches of one optimizer step as train.py deals them
+(micro-batch k -> rank k % world, loss / acc_steps), and the all-reduce sums them.  The result must
+equal the reference's single-process accumulation: G7 (tests/golden/g7_dp.npz: 8 micro-batches of
+4 slices, loss / 8, produced by the reference itself), and for world > acc_steps (idle ranks) the
+oracle's accumulation of 2 micro-batches (the oracle is pinned to G1/G7).  Paths exercised: the
+one-shot flat-buffer all-reduce, the flattened fallback, and the bucketed all-reduce overlapped
+with the backward (pmu_hip.dp.BucketAllReduce) replaying the HIP backward's report order
+(engine.unet_report_order).  The per-rank gradients come from the CPU oracle: the HIP backward
+needs a GPU, the exchange logic under test does not.
 """
 import os
 import socket
@@ -28,156 +31,176 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, flat, q):
+def _setup(rank, world, port):
     import sys
     for p in (os.path.join(ROOT, "probabilistic-multiplanar-unet_amd"), ROOT, os.path.dirname(__file__)):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+
+
+def _local_grads(net, sd, x, t, mbs, acc):
+    """This rank's summed gradients of its micro-batches, loss / acc each (oracle fwd/bwd)."""
+    from oracle.unet_ref import unet_forward, unet_loss
+    named = dict(net.named_parameters())
+    params = {k: named[k].detach().clone().requires_grad_(True) for k in named}
+    work = dict(sd)
+    work.update(params)
+    for mb in mbs:
+        idx = torch.tensor(mb)
+        (unet_loss(unet_forward(work, x[idx], 2, 1), t[idx], 1) / acc).backward()
+    return {k: (params[k].grad if params[k].grad is not None else None) for k in named}
+
+
+def _g7_net():
+    from model import UNet
+    z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
+    net = UNet(1, 1, [16, 32])
+    sd = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("init/")}
+    net.load_state_dict(sd)
+    return net, sd, torch.from_numpy(z["x"]), torch.from_numpy(z["t"])
+
+
+def _run(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda r: r[0])
+
+
+def _reference(acc):
+    """G7's gradients (acc = 8), or the oracle's accumulation of G7's first `acc` micro-batches."""
+    z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
+    if acc == 8:
+        return {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("grad/")}
+    net, sd, x, t = _g7_net()
+    g = _local_grads(net, sd, x, t, [list(range(4 * i, 4 * i + 4)) for i in range(acc)], acc)
+    return g
+
+
+# ------------------------------------------------------------------------ one-shot all-reduce
+def _flat_worker(rank, world, port, q, flat, acc):
+    _setup(rank, world, port)
     try:
-        torch.set_num_threads(2)
-        from model import UNet
-        from oracle.unet_ref import unet_forward, unet_loss
         from pmu_hip.functions import grad_sink_for
         from train import allreduce_grads, dp_micro_batches, shared_generator
-        z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
-        net = UNet(1, 1, [16, 32])
-        sd = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("init/")}
-        net.load_state_dict(sd)
-        x, t = torch.from_numpy(z["x"]), torch.from_numpy(z["t"])
-        # the 32 samples in order; train.py deals micro-batches of 4 round-robin, 4 per rank per step
-        steps, per_rank = dp_micro_batches(list(range(32)), 4, 8, world, rank)
-        assert len(steps) == 1 and per_rank == 4
+        net, sd, x, t = _g7_net()
+        steps, leftover = dp_micro_batches(list(range(4 * acc)), 4, acc, world, rank)
+        assert len(steps) == 1 and not leftover
+        mbs = steps[0]
+        assert len(mbs) == len(range(rank, acc, world))
         named = dict(net.named_parameters())
         plist = list(net.parameters())
-        keys = list(named)
-        params = {k: named[k].detach().clone().requires_grad_(True) for k in keys}
-        work = dict(sd)
-        work.update(params)
-        for mb in steps[0]:
-            idx = torch.tensor(mb)
-            (unet_loss(unet_forward(work, x[idx], 2, 1), t[idx], 1) / (per_rank * world)).backward()
-        if flat:
-            sink = grad_sink_for(net, plist)      # views of the flat buffer, as the HIP nodes write them
-            for k, p in named.items():
-                g = sink.new(p)
-                g.copy_(params[k].grad)
-                p.grad = g
-        else:
-            for k, p in named.items():
-                p.grad = params[k].grad.clone()
-        allreduce_grads(net, plist)
-        # every rank must agree on the generator the loop shuffles with
-        seed = shared_generator().initial_seed()
+        idle = not mbs
+        if not idle:
+            g = _local_grads(net, sd, x, t, mbs, acc)
+            if flat:
+                sink = grad_sink_for(net, plist)      # views of the flat buffer, as the HIP nodes write them
+                for k, p in named.items():
+                    v = sink.new(p)
+                    v.copy_(g[k])
+                    p.grad = v
+            else:
+                for k, p in named.items():
+                    p.grad = g[k].clone()
+        allreduce_grads(net, plist, idle=idle)
+        seed = shared_generator().initial_seed()   # every rank must agree on the shuffle generator
         out = {k: p.grad.detach().numpy().copy() for k, p in named.items()}
-        q.put((rank, out, seed, [i for st in steps for mb in st for i in mb]))
+        q.put((rank, out, seed, [i for mb in mbs for i in mb]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("flat", [True, False])
-def test_dp_allreduce_matches_reference_accumulation(flat):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    world = 2
-    procs = [ctx.Process(target=_worker, args=(r, world, port, flat, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    res.sort(key=lambda r: r[0])
-    z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
-    ref = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("grad/")}
+@pytest.mark.parametrize("world,acc,flat", [(2, 8, True), (2, 8, False), (4, 8, True), (8, 8, True),
+                                            (3, 8, True), (4, 2, True)])
+def test_dp_allreduce_matches_reference_accumulation(world, acc, flat):
+    res = _run(_flat_worker, world, flat, acc)
+    ref = _reference(acc)
     from helpers import grad_err
     for rank, out, _, _ in res:
         err, key = grad_err({k: torch.from_numpy(out[k]) for k in ref}, ref)
         assert err <= 1e-5, (rank, err, key)
-    assert res[0][2] == res[1][2]                          # shared shuffle seed
-    assert sorted(res[0][3] + res[1][3]) == list(range(32)) and not set(res[0][3]) & set(res[1][3])
+    assert len({r[2] for r in res}) == 1                       # shared shuffle seed
+    seen = [i for r in res for i in r[3]]
+    assert sorted(seen) == list(range(4 * acc)) and len(set(seen)) == len(seen)
 
 
-def _bucket_worker(rank, world, port, mode, q):
-    """Rank body of the bucketed, backward-overlapped all-reduce (pmu_hip.dp.BucketAllReduce)."""
-    import sys
-    for p in (os.path.join(ROOT, "probabilistic-multiplanar-unet_amd"), ROOT, os.path.dirname(__file__)):
-        sys.path.insert(0, p)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+# ------------------------------------------------------------------------ bucketed, overlapped
+def _bucket_worker(rank, world, port, q, mode, acc):
+    _setup(rank, world, port)
     try:
-        torch.set_num_threads(2)
-        from model import UNet
-        from oracle.unet_ref import unet_forward, unet_loss
         from pmu_hip.dp import BucketAllReduce
+        from pmu_hip.engine import unet_report_order
         from pmu_hip.functions import grad_sink_for
         from train import dp_micro_batches
-        z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
-        net = UNet(1, 1, [16, 32])
-        sd = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("init/")}
-        net.load_state_dict(sd)
-        x, t = torch.from_numpy(z["x"]), torch.from_numpy(z["t"])
-        steps, per_rank = dp_micro_batches(list(range(32)), 4, 8, world, rank)
+        net, sd, x, t = _g7_net()
+        steps, _ = dp_micro_batches(list(range(4 * acc)), 4, acc, world, rank)
+        mbs = steps[0]
         named = dict(net.named_parameters())
         plist = list(net.parameters())
-        params = {k: named[k].detach().clone().requires_grad_(True) for k in named}
-        work = dict(sd)
-        work.update(params)
-        for mb in steps[0]:
-            idx = torch.tensor(mb)
-            (unet_loss(unet_forward(work, x[idx], 2, 1), t[idx], 1) / (per_rank * world)).backward()
+        g = _local_grads(net, sd, x, t, mbs, acc) if mbs else None
+        name_of = {id(p): k for k, p in named.items()}
+        groups = unet_report_order(net)
+        if mode == "forward_order":
+            groups = groups[::-1]
         sync = BucketAllReduce(net, bucket_bytes=16 << 10)   # several buckets on this small net
-        nb = len(sync.buckets)
-        # 2 rounds: the buffer and the bucket state are reused from step to step
-        for _ in range(2):
+        log = []
+        # 3 rounds: round 0 learns the layout, later rounds reuse buffer and bucket state
+        for rnd in range(3):
             for p in plist:
                 p.grad = None
             sync.begin()
-            order = list(named.items())
-            if mode != "forward_order":
-                order = order[::-1]                     # the order the HIP backward reports layers
-            if mode == "foreign":
-                for k, p in order:
-                    p.grad = params[k].grad.clone()      # accumulated outside the flat buffer
-            else:
-                sink = grad_sink_for(net, plist)
-                for k, p in order:
-                    g = sink.new(p)
-                    g.copy_(params[k].grad)
-                    p.grad = g
-                    sink.flush()                          # one layer's gradient kernels enqueued
-            issued = sync.issued_in_backward
-            sync.finish()
-        out = {k: p.grad.detach().numpy().copy() for k, p in named.items()}
-        q.put((rank, out, nb, issued))
+            if g is not None:
+                if mode == "foreign":
+                    for p in plist:
+                        p.grad = g[name_of[id(p)]].clone()   # accumulated outside the flat buffer
+                else:
+                    sink = grad_sink_for(net, plist)
+                    for grp in groups:
+                        for p in grp:
+                            v = sink.new(p)
+                            v.copy_(g[name_of[id(p)]])
+                            p.grad = v
+                        sink.flush()                         # one layer's gradient kernels enqueued
+            log.append((sync.issued_in_backward, sync.issued_at[0] if sync.issued_at else None, sync.flushes,
+                        len(sync.buckets or [])))
+            sync.finish(idle=g is None)
+            out = {k: p.grad.detach().numpy().copy() for k, p in named.items()}
+        q.put((rank, out, log))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["backward_order", "forward_order", "foreign"])
-def test_dp_bucketed_overlap_matches_reference_accumulation(mode):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    world = 2
-    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, mode, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
-    ref = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("grad/")}
+@pytest.mark.parametrize("mode,world,acc", [("backward_order", 2, 8), ("forward_order", 2, 8), ("foreign", 2, 8),
+                                            ("backward_order", 4, 8), ("backward_order", 8, 8),
+                                            ("backward_order", 4, 2)])
+def test_dp_bucketed_overlap_matches_reference_accumulation(mode, world, acc):
+    res = _run(_bucket_worker, world, mode, acc)
+    ref = _reference(acc)
     from helpers import grad_err
-    for rank, out, nb, issued in res:
+    for rank, out, log in res:
         err, key = grad_err({k: torch.from_numpy(out[k]) for k in ref}, ref)
         assert err <= 1e-5, (mode, rank, err, key)
-        assert nb > 2
-        if mode == "backward_order":
-            assert issued == nb          # every bucket was issued from inside the "backward"
-        elif mode == "forward_order":
-            assert issued == nb          # the last report completes bucket 0, then all issue in order
-        else:
-            assert issued == 0           # no flat-buffer sink: nothing issued before finish()
+        issued0, _, _, nb0 = log[0]
+        assert issued0 == 0 and nb0 == 0            # round 0 records the report order
+        for issued, first, flushes, nb in log[1:]:
+            if mode == "foreign":                     # no flat-buffer reports: nothing to learn
+                assert issued == 0 and nb == 0
+                continue
+            assert nb > 2
+            busy = rank < acc
+            if mode == "backward_order" and busy:
+                assert issued == nb                   # every bucket issued from inside the "backward"
+                assert first is not None and first < flushes // 2   # bucket 0 long before the end
+            elif mode == "forward_order" and busy:
+                assert issued == nb                   # the layout follows the learned (reversed) order too
+            else:
+                assert issued == 0                    # foreign grads / idle rank: all at finish()

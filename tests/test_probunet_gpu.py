@@ -209,3 +209,24 @@ def test_probunet_odd_filters_vs_oracle(dev):
     keys = [k for k in gref if not k.startswith("unet.outc")]
     err, key = grad_err({k: named[k].grad for k in keys}, {k: gref[k] for k in keys})
     assert err <= GRAD_TOL, (err, key)
+
+
+def test_fcomb_applied_twice_in_one_graph(dev):
+    """Fcomb on two latent samples in one loss (sample() + reconstruct() both with grad): the
+    parameter gradients add, as in the reference (probabilistic_unet.py:167-181)."""
+    from oracle.probunet_ref import fcomb_forward
+    net = _net(dev).train()
+    fc = net.fcomb
+    g = torch.Generator().manual_seed(4)
+    feat = torch.randn(2, 4, 12, 10, generator=g)
+    z1, z2 = torch.randn(2, 6, generator=g), torch.randn(2, 6, generator=g)
+    w = torch.randn(2, 3, 12, 10, generator=g)
+    sd = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in fc.state_dict().items()}
+    ref_sd = {"fcomb." + k: v for k, v in sd.items()}
+    (((fcomb_forward(ref_sd, feat, z1, 4) * w).sum()) + 2.0 * (fcomb_forward(ref_sd, feat, z2, 4) * w).sum()).backward()
+    fd = feat.to(dev)
+    wd = w.to(dev)
+    ((fc(fd, z1.to(dev)) * wd).sum() + 2.0 * (fc(fd, z2.to(dev)) * wd).sum()).backward()
+    named = dict(fc.named_parameters())
+    err, key = grad_err({k: named[k].grad for k in sd}, {k: sd[k].grad for k in sd})
+    assert err <= GRAD_TOL, (err, key)

@@ -10,6 +10,9 @@ from helpers import ACT_TOL, GRAD_TOL, LOSS_RTOL, grad_err, max_abs
 
 pytestmark = pytest.mark.gpu
 
+# the one ill-conditioned geometry: full depth at 37x45 with N=2, BatchNorm over 8 values at the
+# deepest level; accepted at 2x the fp32 reference's own error vs fp64
+ILL_CONDITIONED = ([64, 128, 256, 512, 1024], 3, 2, 37, 45)
 CASES = [
     # (num_filters, n_classes, N, H, W)
     ([16, 32], 1, 4, 64, 64),            # c1 geometry
@@ -77,13 +80,14 @@ def test_unet_train_step_parity(num_filters, n_classes, N, H, W, dev):
     missing = [k for k, v in ggot.items() if v is None]
     assert not missing, f"no grad for {missing[:4]}"
     err, key = grad_err(ggot, gref)
-    if err > GRAD_TOL:
-        # ill-conditioned geometry (BN over a handful of values at depth): accept if we are as
-        # close to the fp64 truth as the fp32 reference itself is (within 2x)
+    if err > GRAD_TOL and (num_filters, n_classes, N, H, W) == ILL_CONDITIONED:
+        # accept if we are as close to the fp64 truth as the fp32 reference itself is (within 2x)
         g64, ref_noise = _NOISE
         err64, key64 = grad_err(ggot, g64)
         assert err64 <= max(GRAD_TOL, 2.0 * ref_noise), \
             f"grad error {err:.3e} at {key}; vs fp64 {err64:.3e} at {key64} (reference fp32 noise {ref_noise:.3e})"
+    else:
+        assert err <= GRAD_TOL, f"grad error {err:.3e} at {key}"
     for k, v in sd_after.items():
         if k.endswith("running_mean") or k.endswith("running_var"):
             assert max_abs(v, work[k]) <= ACT_TOL, k
@@ -139,3 +143,34 @@ def test_unet_features_mode(dev):
     err, key = grad_err(ggot, gref)
     assert err <= GRAD_TOL, f"{err} {key}"
     assert named["outc.conv.weight"].grad is None
+
+
+def test_unet_applied_twice_in_one_graph(dev):
+    """loss(net(x1)) + loss(net(x2)): both HIP nodes' gradients must add (g1 + g2), as the reference's
+    per-op autograd graph does — the flat-buffer views must not alias across the two nodes."""
+    from model import UNet
+    from oracle.unet_ref import unet_forward, unet_loss, unet_param_keys
+    torch.manual_seed(0)
+    net = UNet(1, 3, [8, 16, 32])
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    g = torch.Generator().manual_seed(9)
+    x1, x2 = torch.rand(2, 1, 32, 32, generator=g), torch.rand(3, 1, 32, 32, generator=g)
+    t1, t2 = torch.randint(0, 3, (2, 1, 32, 32), generator=g), torch.randint(0, 3, (3, 1, 32, 32), generator=g)
+    keys = unet_param_keys(sd)
+    params = {k: sd[k].clone().requires_grad_(True) for k in keys}
+    work = dict(sd)
+    work.update(params)
+    (unet_loss(unet_forward(work, x1, 3, 3), t1, 3) + 0.5 * unet_loss(unet_forward(work, x2, 3, 3), t2, 3)).backward()
+    net = net.to(dev).train()
+    loss = unet_loss(net(x1.to(dev)), t1.to(dev), 3) + 0.5 * unet_loss(net(x2.to(dev)), t2.to(dev), 3)
+    loss.backward()
+    named = dict(net.named_parameters())
+    err, key = grad_err({k: named[k].grad for k in keys}, {k: params[k].grad for k in keys})
+    assert err <= GRAD_TOL, (err, key)
+    # a following single application goes back to the flat gradient buffer
+    for p in net.parameters():
+        p.grad = None
+    unet_loss(net(x1.to(dev)), t1.to(dev), 3).backward()
+    buf = net.__dict__["_pmu_grad_flat"]
+    lo, hi = buf.data_ptr(), buf.data_ptr() + 4 * buf.numel()
+    assert all(lo <= p.grad.data_ptr() < hi for p in net.parameters())

@@ -47,23 +47,33 @@ def main():
     want = allg[0].clone()
     for a in allg[1:]:
         want += a
+    from pmu_hip.engine import unet_report_order
     sync = BucketAllReduce(net, bucket_bytes=64 << 10)
+    # the backward's real report order, seen through the reducer's flush callback
+    reports = []
+    orig = net.__dict__["_pmu_grad_ready"]
+    net.__dict__["_pmu_grad_ready"] = lambda ps: (reports.append([id(p) for p in ps]), orig(ps))
     ok = True
-    for it in range(2):
+    for it in range(3):
         for p in plist:
             p.grad = None
+        reports.clear()
         sync.begin()
         crit(net(x), t).backward()
-        issued = sync.issued_in_backward
+        issued, first, flushes = sync.issued_in_backward, (sync.issued_at or [None])[0], sync.flushes
         sync.finish()
         torch.cuda.synchronize()
         got = torch.cat([p.grad.reshape(-1) for p in plist]).cpu()
         err = (got - want).abs().max().item()
         buf = net.__dict__["_pmu_grad_flat"]
         adopted = all(buf.data_ptr() <= p.grad.data_ptr() < buf.data_ptr() + 4 * buf.numel() for p in plist)
-        print(f"rank {rank} iter {it}: buckets {len(sync.buckets)} issued in backward {issued} "
-              f"max|sync - sum(local)| {err:.3e} adopted {adopted}", flush=True)
-        ok = ok and err == 0.0 and adopted and issued == len(sync.buckets) and len(sync.buckets) > 2
+        order_ok = reports == [[id(p) for p in grp] for grp in unet_report_order(net)]
+        nb = len(sync.buckets)
+        print(f"rank {rank} iter {it}: buckets {nb} issued in backward {issued} (bucket 0 at flush {first} of "
+              f"{flushes}) max|sync - sum(local)| {err:.3e} adopted {adopted} report order {order_ok}", flush=True)
+        ok = ok and err == 0.0 and adopted and order_ok
+        if it > 0:   # the learned layout: every bucket from inside the backward, bucket 0 early
+            ok = ok and issued == nb and nb > 2 and first is not None and first < flushes // 2
     flag = torch.tensor([1 if ok else 0])
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if rank == 0:
