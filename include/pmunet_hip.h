@@ -216,7 +216,8 @@ int pmu_bnrelu_apply(const float* z, const float* coef, long long P, int C, floa
 
 /* ---- pooling backward ------------------------------------------------------------ */
 /* dx[N][H][W][C] += dpool routed to the first max (row-major) of each 2x2 window of
- * relu(z*scale+shift).  accumulate=0 overwrites dx (zeros outside windows). */
+ * relu(z*scale+shift), or of z itself when coef is NULL (a standalone Down block's raw input).
+ * accumulate=0 overwrites dx (zeros outside windows). */
 int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int N, int H, int W,
                      int C, float* dx, int accumulate, void* stream);
 /* AvgPool2d(2,2,ceil_mode=True) backward: dx = dpool/count(window), overwrite. */

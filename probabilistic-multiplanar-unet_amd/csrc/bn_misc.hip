@@ -184,6 +184,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce1_kernel(const float* __rest
   }
 }
 
+// RAW: the pooled tensor is z itself (a standalone Down block on an arbitrary input), not relu(z*sc+sh)
+template <bool RAW>
 __global__ __launch_bounds__(256) void maxpool2_bwd1_kernel(const float* __restrict__ dpool, const float* __restrict__ z,
                                                             const float* __restrict__ coef, int N, int H, int W, int C,
                                                             float* __restrict__ dx, int accumulate) {
@@ -199,14 +201,14 @@ __global__ __launch_bounds__(256) void maxpool2_bwd1_kernel(const float* __restr
     const int hp = h >> 1, wp = w >> 1;
     if (hp < Hp && wp < Wp) {
       const int me = ((h & 1) << 1) | (w & 1);
-      const float sc = coef[c], sh = coef[C + c];
+      const float sc = RAW ? 1.f : coef[c], sh = RAW ? 0.f : coef[C + c];
       const long long b = ((n * H + 2 * hp) * W + 2 * wp) * C + c;
       const long long off[4] = {0, C, (long long)W * C, (long long)W * C + C};
-      float best = fmaxf(0.f, fmaf(z[b], sc, sh));
+      float best = RAW ? z[b] : fmaxf(0.f, fmaf(z[b], sc, sh));
       int arg = 0;
 #pragma unroll
       for (int k = 1; k < 4; ++k) {
-        const float v = fmaxf(0.f, fmaf(z[b + off[k]], sc, sh));
+        const float v = RAW ? z[b + off[k]] : fmaxf(0.f, fmaf(z[b + off[k]], sc, sh));
         if (v > best) { best = v; arg = k; }
       }
       if (arg == me) o += dpool[((n * Hp + hp) * Wp + wp) * C + c];
@@ -217,6 +219,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd1_kernel(const float* __restr
 
 // ---------------- pooling backward ----------------
 // grid-stride over dx elements in channel quads
+template <bool RAW>
 __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restrict__ dpool, const float* __restrict__ z,
                                                            const float* __restrict__ coef, int N, int H, int W, int C,
                                                            float* __restrict__ dx, int accumulate) {
@@ -235,22 +238,26 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restri
     const int hp = h >> 1, wp = w >> 1;
     if (hp < Hp && wp < Wp) {
       const int me = ((h & 1) << 1) | (w & 1);
-      const float4 sc = *reinterpret_cast<const float4*>(coef + c);
-      const float4 sh = *reinterpret_cast<const float4*>(coef + C + c);
+      const float4 sc = RAW ? make_float4(1.f, 1.f, 1.f, 1.f) : *reinterpret_cast<const float4*>(coef + c);
+      const float4 sh = RAW ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(coef + C + c);
       const long long b = (((long long)n * H + 2 * hp) * W + 2 * wp) * C + c;
       const long long off[4] = {0, C, (long long)W * C, (long long)W * C + C};
       float best[4];
       int arg[4] = {0, 0, 0, 0};
       {
         const float4 v = *reinterpret_cast<const float4*>(z + b);
-        best[0] = fmaxf(0.f, fmaf(v.x, sc.x, sh.x)); best[1] = fmaxf(0.f, fmaf(v.y, sc.y, sh.y));
-        best[2] = fmaxf(0.f, fmaf(v.z, sc.z, sh.z)); best[3] = fmaxf(0.f, fmaf(v.w, sc.w, sh.w));
+        if (RAW) {
+          best[0] = v.x; best[1] = v.y; best[2] = v.z; best[3] = v.w;
+        } else {
+          best[0] = fmaxf(0.f, fmaf(v.x, sc.x, sh.x)); best[1] = fmaxf(0.f, fmaf(v.y, sc.y, sh.y));
+          best[2] = fmaxf(0.f, fmaf(v.z, sc.z, sh.z)); best[3] = fmaxf(0.f, fmaf(v.w, sc.w, sh.w));
+        }
       }
 #pragma unroll
       for (int k = 1; k < 4; ++k) {
         const float4 v = *reinterpret_cast<const float4*>(z + b + off[k]);
-        const float a0 = fmaxf(0.f, fmaf(v.x, sc.x, sh.x)), a1 = fmaxf(0.f, fmaf(v.y, sc.y, sh.y));
-        const float a2 = fmaxf(0.f, fmaf(v.z, sc.z, sh.z)), a3 = fmaxf(0.f, fmaf(v.w, sc.w, sh.w));
+        const float a0 = RAW ? v.x : fmaxf(0.f, fmaf(v.x, sc.x, sh.x)), a1 = RAW ? v.y : fmaxf(0.f, fmaf(v.y, sc.y, sh.y));
+        const float a2 = RAW ? v.z : fmaxf(0.f, fmaf(v.z, sc.z, sh.z)), a3 = RAW ? v.w : fmaxf(0.f, fmaf(v.w, sc.w, sh.w));
         if (a0 > best[0]) { best[0] = a0; arg[0] = k; }
         if (a1 > best[1]) { best[1] = a1; arg[1] = k; }
         if (a2 > best[2]) { best[2] = a2; arg[2] = k; }
@@ -805,15 +812,23 @@ static unsigned grid_for(long long n) {
 
 extern "C" int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int N, int H, int W,
                                 int C, float* dx, int accumulate, void* stream) {
-  PMU_REQUIRE(dpool && z && coef && dx && N > 0 && H > 1 && W > 1 && C > 0);
+  PMU_REQUIRE(dpool && z && dx && N > 0 && H > 1 && W > 1 && C > 0);
   if (C % 4 != 0) {
-    hipLaunchKernelGGL(maxpool2_bwd1_kernel, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0,
-                       (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+    if (coef)
+      hipLaunchKernelGGL(maxpool2_bwd1_kernel<false>, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0,
+                         (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+    else
+      hipLaunchKernelGGL(maxpool2_bwd1_kernel<true>, dim3(grid_for((long long)N * H * W * C)), dim3(256), 0,
+                         (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }
-  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0,
-                     (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+  if (coef)
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<false>, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0,
+                       (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+  else
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<true>, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0,
+                       (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -50,7 +50,9 @@ class Encoder(nn.Module):
         self.layers.apply(init_weights)
 
     def forward(self, input):
-        raise NotImplementedError("Encoder runs fused inside AxisAlignedConvGaussian.forward on the HIP path")
+        """The encoding (N, num_filters[-1], h, w).  AxisAlignedConvGaussian.forward does not call this:
+        it runs encoder + mean + latent head as one fused node; a direct call is its own node."""
+        return _fns().encoder_apply(self, input)
 
 
 class AxisAlignedConvGaussian(nn.Module):
@@ -70,11 +72,26 @@ class AxisAlignedConvGaussian(nn.Module):
         self.conv_layer = nn.Conv2d(num_filters[-1], 2 * self.latent_dim, (1, 1), stride=1)
         self.show_img = 0
         self.show_seg = 0
-        self.show_concat = 0
-        self.show_enc = 0
-        self.sum_input = 0
         nn.init.kaiming_normal_(self.conv_layer.weight, mode="fan_in", nonlinearity="relu")
         nn.init.normal_(self.conv_layer.bias)
+
+    # the reference's debug attributes (:85-93), computed when read instead of on every forward
+    @property
+    def show_concat(self):
+        """cat(input, segm) of the last forward that had a mask (0 before any)."""
+        if not isinstance(self.show_seg, torch.Tensor):
+            return 0
+        return torch.cat((self.show_img, self.show_seg), dim=1)
+
+    @property
+    def sum_input(self):
+        c = self.show_concat
+        return torch.sum(c) if isinstance(c, torch.Tensor) else 0
+
+    @property
+    def show_enc(self):
+        """The encoder output of the last forward (relu(bn) of its last conv, NCHW-shaped)."""
+        return _fns().gaussian_encoding(self)
 
     def forward(self, input, segm=None):
         if segm is not None:
@@ -181,8 +198,27 @@ class ProbabilisticUnet(nn.Module):
         return self.fcomb.forward_samples(self.unet_features, zs)
 
     def sample_at(self, z):
-        """Logits at latent location ``z`` (L,) — batch-1 features, as in the reference (:242-247)."""
-        return self.fcomb.forward(self.unet_features, z.to(device).unsqueeze(0))
+        """Logits at latent location ``z``.  z (L,): batch-1 features, as in the reference (:242-247),
+        -> (1, K, H, W).  Extension: z (S, L), S locations (e.g. latent_grid's) decoded in one fused
+        pass over the features (read once) -> (S, N, K, H, W), for features of any batch N."""
+        z = z.to(device=self.unet_features.device, dtype=torch.float32)
+        if z.dim() == 1:
+            return self.fcomb.forward(self.unet_features, z.unsqueeze(0))
+        N = self.unet_features.shape[0]
+        return self.fcomb.forward_samples(self.unet_features, z[:, None, :].expand(z.shape[0], N, z.shape[1]))
+
+    @staticmethod
+    def latent_grid(n_preds, mu, sigma, dims=(0, 1)):
+        """The latent sweep of visualize_sampling.visualize_sample (visualize_sampling.py:22-26):
+        z[dims[0]] = mu + a*sigma, z[dims[1]] = mu + b*sigma for a, b in range(-(n//2), n//2 + 1), the
+        other components at mu.  Returns (rows*cols, L), row-major (a outer)."""
+        mu, sigma = mu.reshape(-1).float(), sigma.reshape(-1).float()
+        ks = torch.arange(-(n_preds // 2), n_preds // 2 + 1, dtype=torch.float32, device=mu.device)
+        a, b = torch.meshgrid(ks, ks, indexing="ij")
+        z = mu.repeat(a.numel(), 1)
+        z[:, dims[0]] = a.reshape(-1) * sigma[dims[0]] + mu[dims[0]]
+        z[:, dims[1]] = b.reshape(-1) * sigma[dims[1]] + mu[dims[1]]
+        return z
 
     def reconstruct(self, use_posterior_mean=False, calculate_posterior=False, z_posterior=None):
         """Decode a posterior sample (or its mean) with the UNet features (:251-262)."""

@@ -6,7 +6,8 @@ Conv2d, BatchNorm2d, ReLU]`` (unet_parts.py:14-21), ``maxpool_conv = [MaxPool2d,
 default-initialisation RNG order are identical to the reference.  Their arithmetic never
 runs in PyTorch: ``UNet.forward`` hands the whole stack to the HIP engine
 (``pmu_hip.engine``), which fuses BN+ReLU, pooling, padding and concatenation into the conv
-kernels.  Calling a block on its own runs that block on the same engine.
+kernels.  Calling a block on its own runs that block on the same engine, as one autograd node
+with a materialised output (``pmu_hip.blocks``).
 """
 import torch.nn as nn
 
@@ -26,7 +27,7 @@ class DoubleConv(nn.Module):
 
     def forward(self, x):
         from pmu_hip.blocks import double_conv_apply
-        return double_conv_apply(self, x, pool=None)
+        return double_conv_apply(self, x)
 
 
 class Down(nn.Module):
@@ -37,8 +38,8 @@ class Down(nn.Module):
         self.maxpool_conv = nn.Sequential(nn.MaxPool2d(2), DoubleConv(in_channels, out_channels))
 
     def forward(self, x):
-        from pmu_hip.blocks import double_conv_apply
-        return double_conv_apply(self.maxpool_conv[1], x, pool="max")
+        from pmu_hip.blocks import down_apply
+        return down_apply(self, x)
 
 
 class Up(nn.Module):

@@ -188,6 +188,7 @@ class GaussianFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, g, x, segm, *params):
         mls, st = prob_engine.gaussian_forward(g, _planes(x, segm), g.training, keep=True)
+        g.__dict__["_pmu_enc_out"] = (st.layers[-1].z, st.layers[-1].bn.coef)
         ctx.g, ctx.st = g, st
         ctx.live = LiveNode(g)
         return mls
@@ -213,8 +214,28 @@ def gaussian_apply(g, x, segm=None):
     if torch.is_grad_enabled() and any(p.requires_grad for p in params):
         return GaussianFunction.apply(g, x, segm, *params)
     with torch.no_grad():
-        mls, _ = prob_engine.gaussian_forward(g, _planes(x, segm), g.training)
+        mls, st = prob_engine.gaussian_forward(g, _planes(x, segm), g.training)
+    g.__dict__["_pmu_enc_out"] = (st.layers[-1].z, st.layers[-1].bn.coef)
     return mls
+
+
+def gaussian_encoding(g):
+    """The last forward's encoder output relu(bn(z)) as an NCHW-shaped (channels-last) tensor, or 0."""
+    zc = g.__dict__.get("_pmu_enc_out")
+    if zc is None:
+        return 0
+    from . import _lib as L
+    z, coef = zc
+    N, H, W, C = z.shape
+    out = torch.empty_like(z)
+    L.call("pmu_bnrelu_apply", z.data_ptr(), coef.data_ptr(), N * H * W, C, out.data_ptr(), L.stream())
+    return out.permute(0, 3, 1, 2)
+
+
+def encoder_apply(enc, x):
+    """Encoder.forward called on its own (probabilistic_unet.py:51-53)."""
+    from .blocks import encoder_apply as _enc
+    return _enc(enc, x)
 
 
 # ----------------------------------------------------------------------------------------

@@ -369,3 +369,85 @@ def test_convT_wgrad_bf16(dev, N, H, W, Cin, Cout, oh, ow):
     ref = torch.einsum("nijc,niajbk->ckab", x, dr)
     assert _rel(dw, ref) <= TOL
     assert _rel(db, dui.sum((0, 1, 2))) <= 1e-5
+
+
+def _phantom_slices(D, N, seed=21):
+    """N axial 3-channel slices (D x D) through a seeded D^3 phantom: two nested ellipsoid shells
+    (classes 1, 2, as the knee labels of PMU/Utils/nii.py:83-90) under three noisy contrasts."""
+    g = torch.Generator().manual_seed(seed)
+    ax = torch.arange(D, dtype=torch.float32) - D / 2
+    r2 = ((ax[:, None, None] / (0.40 * D)) ** 2 + (ax[None, :, None] / (0.33 * D)) ** 2 +
+          (ax[None, None, :] / (0.36 * D)) ** 2)
+    lab = (r2 < 1.0).long() + (r2 < 0.4).long()
+    idx = torch.linspace(D * 0.25, D * 0.75, N).long()
+    y = lab[:, :, idx].permute(2, 0, 1)                         # (N, D, D)
+    x = torch.stack([0.5 * torch.rand(N, D, D, generator=g) + (0.15 + 0.1 * c) * y.float() for c in range(3)], 1)
+    return x, y
+
+
+def test_c5_bf16_dice_gap_vs_fp32_oracle(dev):
+    """Config c5's architecture — UNet(3, 3, [64..1024]), all 5 levels — trained for 12 identical
+    steps (CE + clip + SGD, lr 0.05) on seeded 3-channel phantom slices, three ways: the fp32 CPU
+    oracle (the reference's arithmetic), the HIP fp32 path, and the HIP bf16 path (torch.autocast
+    bf16).  Then the eval-mode argmax maps of all three on the batch: the fp32 HIP path must match
+    the oracle within the parity contract (Dice 1e-3, argmax agreement >= 0.999); the bf16 path's
+    gap is reported and bounded (argmax agreement >= 0.98, per-class Dice gap <= 0.02)."""
+    import json
+    import os
+    from model import UNet
+    from oracle.unet_ref import trainer_dice, unet_forward, unet_param_keys, unet_train_step
+    from pmu_hip.optim import FusedSGD
+    D, N, steps, lr = 128, 8, 12, 0.05
+    x, y = _phantom_slices(D, N)
+    t = y[:, None]
+    torch.manual_seed(0)
+    net0 = UNet(3, 3, [64, 128, 256, 512, 1024])
+    sd0 = {k: v.clone() for k, v in net0.state_dict().items()}
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    sd = {k: v.clone() for k, v in sd0.items()}
+    bufs = {k: torch.zeros_like(sd[k]) for k in unet_param_keys(sd)}
+    losses_ref = [float(unet_train_step(sd, x, t, 5, 3, lr=lr, bufs=bufs)[1]) for _ in range(steps)]
+    modes = ("eval", "train")   # BN running statistics (inference) / batch statistics (the train step)
+    ref_out = {}
+    with torch.no_grad():
+        for m in modes:
+            ref_out[m] = unet_forward({k: v.clone() for k, v in sd.items()}, x, 5, 3, training=m == "train")
+    res = {"oracle": {"losses": losses_ref}}
+    for m in modes:
+        res["oracle"][f"dice_to_target_{m}"] = trainer_dice(ref_out[m], t, 3)
+    for prec in ("fp32", "bf16"):
+        net = UNet(3, 3, [64, 128, 256, 512, 1024])
+        net.load_state_dict(sd0)
+        net = net.to(dev).train()
+        opt = FusedSGD(net.parameters(), lr=lr, momentum=0.9, clip=0.1)
+        xd, td = x.to(dev), y.to(dev)
+        losses = []
+        for _ in range(steps):
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec == "bf16"):
+                out = net(xd)
+            loss = torch.nn.functional.cross_entropy(out, td)
+            loss.backward()
+            opt.step()
+            losses.append(float(loss))
+        r = {"losses": losses}
+        for m in modes:
+            net.train(m == "train")
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=prec == "bf16"):
+                out = net(xd).float().cpu()
+            lab, ref_lab = out.argmax(1), ref_out[m].argmax(1)
+            d_hip = trainer_dice(out, t, 3)
+            onehot = torch.nn.functional.one_hot(lab, 3).permute(0, 3, 1, 2).float()
+            r[f"dice_to_target_{m}"] = d_hip
+            r[f"argmax_agreement_vs_oracle_{m}"] = float((lab == ref_lab).float().mean())
+            r[f"dice_vs_oracle_labels_{m}"] = trainer_dice(onehot, ref_lab[:, None], 3)
+            r[f"dice_gap_{m}"] = [abs(a - b) for a, b in zip(d_hip, res["oracle"][f"dice_to_target_{m}"])]
+        res[prec] = r
+    print("C5_DICE_GAP " + json.dumps(res))
+    for m in modes:
+        assert res["fp32"][f"argmax_agreement_vs_oracle_{m}"] >= 0.999, m
+        assert max(res["fp32"][f"dice_gap_{m}"]) <= 1e-3, m
+        assert res["bf16"][f"argmax_agreement_vs_oracle_{m}"] >= 0.98, m
+        assert max(res["bf16"][f"dice_gap_{m}"]) <= 0.02, m
+    # the phantom is learnable: the reference itself segments it after 12 steps
+    assert min(res["oracle"]["dice_to_target_train"]) > 0.5, res["oracle"]
