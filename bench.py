@@ -28,7 +28,6 @@ for p in (PKG, ROOT):
         sys.path.insert(0, p)
 
 import torch  # noqa: E402
-import torch.nn as nn  # noqa: E402
 
 METRIC = "2D slices/sec fwd+bwd, 256×256×1 batch32 U-Net; Dice vs ref"
 METRIC_C5 = "2D slices/sec fwd+bwd, 512×512×3 batch16 U-Net bf16 (BASELINE.json configs[4])"
@@ -367,7 +366,8 @@ def build_unet(args, dev, world, rank):
     sync = dp_sync(net, world)
     g = torch.Generator(device="cpu").manual_seed(1 + rank)
     B, S = args.batch, args.size
-    crit = nn.BCELoss() if args.classes == 1 else nn.CrossEntropyLoss()
+    from pmu_hip.loss import BCELoss, CrossEntropyLoss   # the trainer's criteria (row a6) on HIP kernels
+    crit = BCELoss() if args.classes == 1 else CrossEntropyLoss()
     batches = None
     if args.data == "phantom":
         batches = phantom_batches(S, B, rank, world, dev)

@@ -18,6 +18,7 @@
  *   pmu_maxpool2_bwd / pmu_avgpool2_bwd                              unet_parts.py:33, probabilistic_unet.py:36
  *   pmu_head1x1_fwd/_bwd, pmu_wgrad1x1   OutConv + sigmoid           unet_parts.py:70-76, unet_model.py:48-49
  *   pmu_sgd_clip         clip_grad_value_(0.1) + SGD(momentum)        PMU/train.py:65,108-110
+ *   pmu_bce_* / pmu_ce_* BCELoss / CrossEntropyLoss (+ grad)          trainer/unet_trainer.py:23,30-37
  *   pmu_dice_counts      dice_coeff + argmax/one-hot                  PMU/dice_loss.py:5-12, trainer/unet_trainer.py:39-58
  *   pmu_dice_sums        dice_coeff's three sums for arbitrary tensors PMU/dice_loss.py:5-12
  *   pmu_fcomb_*          Fcomb 1x1 chain with tiled z                 probabilistic_unet.py:116-181
@@ -265,6 +266,26 @@ typedef struct pmu_sgd_chunk {
 } pmu_sgd_chunk;
 int pmu_sgd_clip(const pmu_sgd_chunk* chunks, int nchunks, void* const* ptrs, float gscale, float lr,
                  float momentum, float clip, void* stream);
+
+/* ---- losses (row a6) -------------------------------------------------------------------
+ * nn.BCELoss on the sigmoid head / nn.CrossEntropyLoss on the logits (PMU/trainer/unet_trainer.py:
+ * 23,30-37) and the summed CE of ProbabilisticUnet.elbo (probabilistic_unet.py:286-304).
+ * reduction: 0 none (loss[i] per element / pixel), 1 mean, 2 sum (loss[0]).  Forward partial sums
+ * are fp64 in a fixed order (deterministic); ws: pmu_loss_ws(n) bytes (n = elements / pixels).
+ * count_out (optional, device float): the mean's denominator (n for BCE, non-ignored pixels for
+ * CE), read by pmu_ce_bwd for reduction 1.  Backward: gout is the upstream gradient on the device
+ * (a scalar for mean/sum, per element for none); BCE dy = g (y - t) / max(y (1 - y), 1e-12) (torch's
+ * formula; mean divides g by n); CE dx = g (softmax - onehot(t)), ignore_index pixels 0.
+ * Logits x NCHW [N][K][HW], targets int64 [N][HW]. */
+size_t pmu_loss_ws(long long n);
+int pmu_bce_fwd(const float* y, const float* t, long long n, int reduction, float* loss, double* ws,
+                float* count_out, void* stream);
+int pmu_bce_bwd(const float* y, const float* t, long long n, int reduction, const float* gout, float* dy,
+                void* stream);
+int pmu_ce_fwd(const float* x, const long long* tgt, int N, int K, long long HW, int reduction,
+               long long ignore_index, float* loss, double* ws, float* count_out, void* stream);
+int pmu_ce_bwd(const float* x, const long long* tgt, int N, int K, long long HW, int reduction,
+               long long ignore_index, const float* gout, const float* count, float* dx, void* stream);
 
 /* ---- metrics ------------------------------------------------------------------------- */
 /* counts[k][3] = (sum pred_k*t_k, sum pred_k, sum t_k) for k < K, exact (integer-valued fp64).

@@ -9,8 +9,8 @@ HIP path:
   * Fcomb                  -> one node (FcombFunction): fused per-pixel MLP on MFMA, z folded in
     as a per-sample bias instead of tiling it over H x W.
   * UNet features          -> model.UNet(apply_last_layer=False) on the HIP path.
-The distributions (Independent(Normal)), the analytic KL on (N, latent_dim) tensors and the
-reconstruction loss are the same torch.distributions / nn losses the reference uses.
+The distributions (Independent(Normal)) and the analytic KL on (N, latent_dim) tensors are the same
+torch.distributions the reference uses; the summed cross entropy runs on pmu_hip.loss.
 """
 import torch
 import torch.nn as nn
@@ -241,7 +241,8 @@ class ProbabilisticUnet(nn.Module):
         if self.n_classes == 1:
             criterion = nn.BCEWithLogitsLoss(reduction="none")
         else:
-            criterion = nn.CrossEntropyLoss(reduction="none")
+            from pmu_hip.loss import CrossEntropyLoss   # HIP kernels; the sum of :304 fused in
+            criterion = CrossEntropyLoss(reduction="sum")
         z_posterior = self.posterior_latent_space.rsample()
         self.kl = torch.mean(self.kl_divergence(analytic=analytic_kl, calculate_posterior=False,
                                                 z_posterior=z_posterior))

@@ -119,6 +119,13 @@ SIGNATURES = {
     "pmu_wgrad1x1_ws": (c_size_t, [c_int, c_int, c_int]),
     "pmu_wgrad1x1": (c_int, [c_void_p, _FP, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_sgd_clip": (c_int, [c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_void_p]),
+    "pmu_loss_ws": (c_size_t, [c_longlong]),
+    "pmu_bce_fwd": (c_int, [c_void_p, c_void_p, c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_bce_bwd": (c_int, [c_void_p, c_void_p, c_longlong, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmu_ce_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_longlong, c_int, c_longlong, c_void_p, c_void_p,
+                           c_void_p, c_void_p]),
+    "pmu_ce_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_longlong, c_int, c_longlong, c_void_p, c_void_p,
+                           c_void_p, c_void_p]),
     "pmu_dice_counts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_dice_sums": (c_int, [c_void_p, c_void_p, c_longlong, c_void_p, c_void_p]),
     "pmu_slice_view_layout": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,

@@ -1,9 +1,9 @@
 """ProbUNetTrainer — drop-in for PMU/trainer/probunet_trainer.py:10-92."""
 import torch
-import torch.nn as nn
 
 from model import ProbabilisticUnet
 from model.probabilistic_unet.utils import l2_regularisation  # noqa: F401  (same import surface)
+from pmu_hip.loss import BCELoss, CrossEntropyLoss
 from pmu_hip.metrics import trainer_dice
 
 from .trainer import Trainer, load_checkpoint, masks_to_rgb
@@ -21,7 +21,7 @@ class ProbUNetTrainer(Trainer):
         if load_model is not None:
             load_checkpoint(self.net, load_model, device)
         self.net = self.net.to(device)
-        self.criterion = nn.BCELoss() if self.net.n_classes == 1 else nn.CrossEntropyLoss()
+        self.criterion = BCELoss() if self.net.n_classes == 1 else CrossEntropyLoss()
 
     def predict(self, imgs, true_masks, z=None):
         """forward (posterior too when grad is enabled) then a prior sample, or logits at ``z`` (:27-32)."""

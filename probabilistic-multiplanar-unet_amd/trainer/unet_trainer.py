@@ -1,13 +1,14 @@
 """UNetTrainer — drop-in for PMU/trainer/unet_trainer.py:10-129.
 
 Same constructor, attributes (device, name, mask_type, net, criterion) and methods.  The net runs
-on the HIP path (model.UNet); the loss is the reference's own nn.BCELoss / nn.CrossEntropyLoss
-(row a6); eval's per-class Dice comes from one fused argmax+count kernel (pmu_hip.metrics).
+on the HIP path (model.UNet); the loss is BCELoss / CrossEntropyLoss on HIP kernels (pmu_hip.loss,
+row a6; same constructors and reductions as torch's); eval's per-class Dice comes from one fused
+argmax+count kernel (pmu_hip.metrics).
 """
 import torch
-import torch.nn as nn
 
 from model import UNet
+from pmu_hip.loss import BCELoss, CrossEntropyLoss
 from pmu_hip.metrics import trainer_dice
 
 from .trainer import Trainer, load_checkpoint, masks_to_rgb
@@ -23,7 +24,7 @@ class UNetTrainer(Trainer):
         if load_model is not None:
             load_checkpoint(self.net, load_model, device)
         self.net = self.net.to(device)
-        self.criterion = nn.BCELoss() if self.net.n_classes == 1 else nn.CrossEntropyLoss()
+        self.criterion = BCELoss() if self.net.n_classes == 1 else CrossEntropyLoss()
 
     def predict(self, imgs, true_masks):
         return self.net(imgs)
