@@ -45,6 +45,7 @@ struct RawArgs {
   float* out1;
   float* part;
   int N, H, W, Cp, NOUT, split, tiles_w, tiles_h, nch;
+  int ncb, xcd;              // output-channel blocks; 1: 1-D XCD-ordered grid, channel blocks fastest
 };
 
 __device__ __forceinline__ unsigned short bf16_bits(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
@@ -81,12 +82,23 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
   unsigned short* As = smem;
   unsigned short* Bs = smem + G::A_EL;
   const int tid = threadIdx.x, lane = tid & 63, wm = tid >> 6;
-  int t = blockIdx.x;
+  // (spatial tile, output-channel block): with a.xcd the channel blocks of one spatial tile run
+  // back to back on one XCD, so its halo operand is fetched from HBM once and re-read from L2
+  int t, cb;
+  if (a.xcd) {
+    const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+    cb = lb % a.ncb;
+    t = lb / a.ncb;
+  } else {
+    t = blockIdx.x;
+    cb = blockIdx.y;
+  }
+  const int tsp = t;
   const int tw = t % a.tiles_w; t /= a.tiles_w;
   const int th = t % a.tiles_h; t /= a.tiles_h;
   const int n = t;
   const int h0 = th * TH, w0 = tw * TW;
-  const int j0 = blockIdx.y * BNT;
+  const int j0 = cb * BNT;
 
   // A units: halo pixel hp = it >> 2, 8-channel unit q = it & 3; tile-constant 32-bit offsets
   int eo[NA], dsta[NA];
@@ -263,8 +275,8 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
           t1 += red[(v * BNT + tid) * 2 + 0];
           t2 += red[(v * BNT + tid) * 2 + 1];
         }
-        a.part[((long long)blockIdx.x * 2 + 0) * a.NOUT + j] = t1;
-        a.part[((long long)blockIdx.x * 2 + 1) * a.NOUT + j] = t2;
+        a.part[((long long)tsp * 2 + 0) * a.NOUT + j] = t1;
+        a.part[((long long)tsp * 2 + 1) * a.NOUT + j] = t2;
       }
     }
   }
@@ -306,7 +318,13 @@ static int launch_raw(const unsigned short* x, int Cp, int N, int H, int W, cons
   const int TH = bmt / TW;
   a.tiles_w = pmu_cdiv(W, TW);
   a.tiles_h = pmu_cdiv(H, TH);
-  dim3 grid((unsigned)(a.tiles_w * a.tiles_h * N), (unsigned)ncb);
+  static const int xcd = [] {
+    const char* e = getenv("PMU_RAW_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  a.ncb = ncb;
+  a.xcd = xcd;
+  const dim3 grid = xcd ? dim3((unsigned)(a.tiles_w * a.tiles_h * N * ncb)) : dim3((unsigned)(a.tiles_w * a.tiles_h * N), (unsigned)ncb);
   hipStream_t st = (hipStream_t)stream;
 #define PMU_RK(D, T, B)                                                                 \
   if (dgrad == D && twl == T && bmt == B) {                                             \

@@ -489,6 +489,7 @@ struct PipeArgs {
   int H, W, Cin, Cout;
   int Hd, Wd, off_h, off_w;
   int lw, lh;          // fwd: log2 W, log2 H when powers of two, else -1
+  int nnb, xcd;        // column blocks; 1: 1-D XCD-ordered grid, column blocks fastest
 };
 
 template <bool DGRAD, int EXP = 0>
@@ -497,8 +498,20 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
   __shared__ __attribute__((aligned(16))) float Bs[2][PN * PLS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const long long m0 = (long long)blockIdx.x * PM;
-  const int n0 = blockIdx.y * PN;
+  // with p.xcd the column blocks of one row block run back to back on one XCD, so the A rows (the
+  // big operand) come from HBM once and are re-read from that XCD's L2
+  long long mb;
+  int nb_;
+  if (p.xcd) {
+    const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+    nb_ = lb % p.nnb;
+    mb = lb / p.nnb;
+  } else {
+    mb = blockIdx.x;
+    nb_ = blockIdx.y;
+  }
+  const long long m0 = mb * PM;
+  const int n0 = nb_ * PN;
   const int hsel = (lane >> 5) * 8;
   // this thread's two A rows and two B rows (fixed over the K loop), 4 consecutive k each
   const int kq = (tid & 3) * 4;
@@ -679,6 +692,15 @@ static void convT_wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* tw
 
 }  // namespace
 
+static void pipe_grid(PipeArgs& p, int nnb) {
+  static const int xcd = [] {
+    const char* e = getenv("PMU_CONVT_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  p.nnb = nnb;
+  p.xcd = xcd && (long long)pmu_cdiv(p.M, PM) * nnb < (1LL << 31);
+}
+
 extern "C" size_t pmu_convT2x2_packed_size(int Cin, int Cout) {
   return (Cin > 0 && Cout > 0) ? (size_t)4 * Cin * Cout * sizeof(float) : 0;
 }
@@ -705,7 +727,8 @@ extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float
     p.lw = log2_or(in->W); p.lh = log2_or(in->H);
     // the output index (((n*2H + 2i)*2W + 2j)*Cout + co) stays 32-bit in the shift path
     if (4LL * M * Cout >= (1LL << 32)) p.lw = -1;
-    dim3 grid((unsigned)pmu_cdiv(M, PM), (unsigned)(p.Ncols / PN));
+    pipe_grid(p, p.Ncols / PN);
+    const dim3 grid = p.xcd ? dim3((unsigned)(pmu_cdiv(M, PM) * p.nnb)) : dim3((unsigned)pmu_cdiv(M, PM), (unsigned)p.nnb);
 #ifdef PMU_EXPERIMENTS
     // timing experiments (wrong results): only in `make EXPERIMENTS=1` builds
     static const int exp = [] {
@@ -744,7 +767,8 @@ extern "C" int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, in
     p.M = M; p.Ncols = Cin; p.K = 4 * Cout;
     p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout;
     p.Hd = Hd; p.Wd = Wd; p.off_h = off_h; p.off_w = off_w;
-    dim3 grid((unsigned)pmu_cdiv(M, PM), (unsigned)(Cin / PN));
+    pipe_grid(p, Cin / PN);
+    const dim3 grid = p.xcd ? dim3((unsigned)(pmu_cdiv(M, PM) * p.nnb)) : dim3((unsigned)pmu_cdiv(M, PM), (unsigned)p.nnb);
     hipLaunchKernelGGL(convT_pipe_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, p);
     PMU_CHECK_LAUNCH();
     return PMU_OK;

@@ -8,6 +8,7 @@
 // Tile 128 x 128 x 32 (two 32x32x16 k-steps per chunk), 4 waves of 64 x 64 (2 x 2 accumulators),
 // double-buffered bf16 LDS (80-B rows: ds_read_b128 conflict-free), the next chunk's global loads
 // in registers under the current chunk's MFMAs, 2 blocks per CU.
+#include <cstdlib>
 #include "pmu_stage.h"
 
 namespace {
@@ -25,6 +26,7 @@ struct TArgs {
   long long M;
   int Ncols, K, H, W, Cin, Cout, Hd, Wd, off_h, off_w;
   int lw, lh;                 // fwd: log2 W, log2 H when powers of two (shift/mask epilogue), else -1
+  int nnb, xcd;               // column blocks; 1: 1-D XCD-ordered grid, column blocks fastest
 };
 
 __global__ void convT_pack_bf16_kernel(const float* __restrict__ w, int Cin, int Cout, int dgrad,
@@ -46,8 +48,20 @@ __global__ __launch_bounds__(256, 2) void convT_bf16_kernel(TArgs p) {
   __shared__ __attribute__((aligned(16))) unsigned short Bs[2][TN * TLS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const long long m0 = (long long)blockIdx.x * TM;
-  const int n0 = blockIdx.y * TN;
+  // with p.xcd the column blocks of one row block run back to back on one XCD: the A rows (the
+  // big operand) come from HBM once and are re-read from that XCD's L2
+  long long mb;
+  int nb_;
+  if (p.xcd) {
+    const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+    nb_ = lb % p.nnb;
+    mb = lb / p.nnb;
+  } else {
+    mb = blockIdx.x;
+    nb_ = blockIdx.y;
+  }
+  const long long m0 = mb * TM;
+  const int n0 = nb_ * TN;
   const int hsel = (lane >> 5) * 8;
   // A: rows (tid>>3) + 32i, 4 consecutive k at 4*(tid&7); B: rows (tid>>2) + 64i, 8 k at 8*(tid&3)
   const int kq = 4 * (tid & 7), bq = 8 * (tid & 3);
@@ -445,6 +459,15 @@ constexpr int DB_G = 2048;  // dbias partial rows (blocks of the partial-sum pas
 
 }  // namespace
 
+static void set_grid(TArgs& p, int nnb) {
+  static const int xcd = [] {
+    const char* e = getenv("PMU_CONVT_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  p.nnb = nnb;
+  p.xcd = xcd && (long long)pmu_cdiv(p.M, TM) * nnb < (1LL << 31);
+}
+
 extern "C" int pmu_convT2x2_pack_bf16(const float* w, int Cin, int Cout, int dgrad, unsigned short* wp, void* stream) {
   PMU_REQUIRE(w && wp && Cin > 0 && Cout > 0);
   const long long E = 4LL * Cin * Cout;
@@ -472,7 +495,8 @@ extern "C" int pmu_convT2x2_fwd_bf16(const pmu_frame* in, const unsigned short* 
   auto log2_or = [](int v) { return (v & (v - 1)) == 0 ? __builtin_ctz((unsigned)v) : -1; };
   p.lw = log2_or(in->W); p.lh = log2_or(in->H);
   if (4LL * p.M * Cout >= (1LL << 32)) p.lw = -1;  // the shift path's output index is 32-bit
-  dim3 grid((unsigned)pmu_cdiv(p.M, TM), (unsigned)(p.Ncols / TN));
+  set_grid(p, p.Ncols / TN);
+  const dim3 grid = p.xcd ? dim3((unsigned)(pmu_cdiv(p.M, TM) * p.nnb)) : dim3((unsigned)pmu_cdiv(p.M, TM), (unsigned)p.nnb);
   hipLaunchKernelGGL(convT_bf16_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
@@ -487,7 +511,8 @@ extern "C" int pmu_convT2x2_dgrad_bf16(const float* du, int Hd, int Wd, int off_
   p.a = du; p.bp = wp; p.out = dx;
   p.M = (long long)N * H * W; p.Ncols = Cin; p.K = 4 * Cout;
   p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout; p.Hd = Hd; p.Wd = Wd; p.off_h = off_h; p.off_w = off_w;
-  dim3 grid((unsigned)pmu_cdiv(p.M, TM), (unsigned)(Cin / TN));
+  set_grid(p, Cin / TN);
+  const dim3 grid = p.xcd ? dim3((unsigned)(pmu_cdiv(p.M, TM) * p.nnb)) : dim3((unsigned)pmu_cdiv(p.M, TM), (unsigned)p.nnb);
   hipLaunchKernelGGL(convT_bf16_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, p);
   PMU_CHECK_LAUNCH();
   return PMU_OK;

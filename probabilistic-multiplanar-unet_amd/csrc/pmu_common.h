@@ -17,6 +17,14 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
   } while (0)
 
 static inline int pmu_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// XCD-aware logical block order: the hardware deals consecutive workgroups round-robin over the 8
+// XCDs (each with its own L2); the logical id gives every XCD a contiguous range of the nb blocks,
+// so a kernel that walks its column blocks fastest re-reads a row block's operand from its own L2.
+__device__ __forceinline__ int pmu_xcd_block(int bid, int nb) {
+  const int x = bid & 7, q = nb >> 3, r = nb & 7;
+  return x * q + (x < r ? x : r) + (bid >> 3);
+}
 __device__ __forceinline__ int pmu_cdiv_dev(int a, int b) { return (a + b - 1) / b; }
 
 // f32-in / f32-accumulate MFMA: D[32x32] += A[32x2] * B[2x32].
