@@ -445,17 +445,32 @@ __global__ __launch_bounds__(256, 2) void convT_wgrad_pipe_kernel(TwArgs a) {
   }
 }
 
-// dW[ci][co][a][b] = sum_s ws[s][ab][ci][co]
-__global__ void convT_wreduce_kernel(const float* __restrict__ ws, int nsplit, int Cin, int Cout, float* __restrict__ dw) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (ab*Cin + ci)*Cout + co
+// dW[ci][co][a][b] = sum_s ws[s][ab][ci][co]: a block owns 64 consecutive elements, its 4 waves sum
+// the splits s = g, g+4, ... and wave 0 adds the 4 partials in order (deterministic)
+__global__ __launch_bounds__(256) void convT_wreduce_kernel(const float* __restrict__ ws, int nsplit, int Cin, int Cout,
+                                                            float* __restrict__ dw) {
+  __shared__ float red[4][64];
   const long long CC = (long long)Cin * Cout;
   const long long E = 4 * CC;
-  if (e >= E) return;
-  float s = 0.f;
-  for (int sp = 0; sp < nsplit; ++sp) s += ws[(long long)sp * E + e];
-  const int ab = (int)(e / CC);
-  const long long cc = e - ab * CC;  // ci*Cout + co
-  dw[cc * 4 + ab] = s;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + lane;  // (ab*Cin + ci)*Cout + co
+  float s0 = 0.f, s1 = 0.f;
+  if (e < E) {
+    int sp = g;
+    for (; sp + 4 < nsplit; sp += 8) {
+      s0 += ws[(long long)sp * E + e];
+      s1 += ws[(long long)(sp + 4) * E + e];
+    }
+    for (; sp < nsplit; sp += 4) s0 += ws[(long long)sp * E + e];
+  }
+  red[g][lane] = s0 + s1;
+  __syncthreads();
+  if (g == 0 && e < E) {
+    const float s = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    const int ab = (int)(e / CC);
+    const long long cc = e - ab * CC;  // ci*Cout + co
+    dw[cc * 4 + ab] = s;
+  }
 }
 
 __global__ void rows_sum_f32_kernel(const float* __restrict__ ws, int R, int Wd, float* __restrict__ out) {
@@ -812,7 +827,7 @@ extern "C" int pmu_convT2x2_wgrad(const float* du, int Hd, int Wd, int off_h, in
     hipLaunchKernelGGL(convT_wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   PMU_CHECK_LAUNCH();
   const long long E = 4LL * a.Cin * Cout;
-  hipLaunchKernelGGL(convT_wreduce_kernel, dim3((unsigned)pmu_cdiv(E, 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(convT_wreduce_kernel, dim3((unsigned)pmu_cdiv(E, 64)), dim3(256), 0, (hipStream_t)stream,
                      (const float*)ws, a.nsplit, a.Cin, Cout, dw);
   PMU_CHECK_LAUNCH();
   if (dbias) {

@@ -309,33 +309,52 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
     }
 }
 
-// dw[co][ci][3][3] = G^T (sum over splits of M) G, G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]
-__global__ void wgrad_wino_reduce_kernel(const float* __restrict__ ws, int nsplit, int Cout, int Cin,
-                                         float* __restrict__ dw) {
+// dw[co][ci][3][3] = G^T (sum over splits of M) G, G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1].
+// Block = 16 consecutive (co, ci) elements x 16 components: thread (comp = t >> 4, e = t & 15) sums
+// its slab column over the splits (4 independent partial sums, combined in a fixed order:
+// deterministic), the 16 sums meet in LDS and 16 threads apply the output transform.  (One thread
+// per element walking 16 x nsplit loads left the small-channel layers latency-bound: 16 blocks for
+// a 64 x 64 layer.)
+__global__ __launch_bounds__(256) void wgrad_wino_reduce_kernel(const float* __restrict__ ws, int nsplit, int Cout,
+                                                                int Cin, float* __restrict__ dw) {
+  __shared__ float mm[16][17];
   const long long CC = (long long)Cout * Cin;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < CC; e += (long long)gridDim.x * blockDim.x) {
-    float m[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) m[c] = 0.f;
-    for (int s = 0; s < nsplit; ++s)
-#pragma unroll
-      for (int c = 0; c < 16; ++c) m[c] += ws[((long long)s * 16 + c) * CC + e];
-    float t[3][4];  // G^T M
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float h = 0.5f * (m[4 + k] + m[8 + k]);
-      t[0][k] = m[k] + h;
-      t[1][k] = 0.5f * (m[4 + k] - m[8 + k]);
-      t[2][k] = h + m[12 + k];
+  const int c = threadIdx.x >> 4, el = threadIdx.x & 15;
+  const long long e = (long long)blockIdx.x * 16 + el;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (e < CC) {
+    const float* p = ws + (long long)c * CC + e;
+    const long long st = 16 * CC;
+    int sp = 0;
+    for (; sp + 3 < nsplit; sp += 4) {
+      s0 += p[(long long)sp * st];
+      s1 += p[(long long)(sp + 1) * st];
+      s2 += p[(long long)(sp + 2) * st];
+      s3 += p[(long long)(sp + 3) * st];
     }
-    float* o = dw + e * 9;
+    for (; sp < nsplit; ++sp) s0 += p[(long long)sp * st];
+  }
+  mm[c][el] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (threadIdx.x >= 16 || e >= CC) return;
+  float m[16];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float h = 0.5f * (t[i][1] + t[i][2]);
-      o[3 * i + 0] = t[i][0] + h;
-      o[3 * i + 1] = 0.5f * (t[i][1] - t[i][2]);
-      o[3 * i + 2] = h + t[i][3];
-    }
+  for (int k = 0; k < 16; ++k) m[k] = mm[k][el];
+  float t[3][4];  // G^T M
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float h = 0.5f * (m[4 + k] + m[8 + k]);
+    t[0][k] = m[k] + h;
+    t[1][k] = 0.5f * (m[4 + k] - m[8 + k]);
+    t[2][k] = h + m[12 + k];
+  }
+  float* o = dw + e * 9;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float h = 0.5f * (t[i][1] + t[i][2]);
+    o[3 * i + 0] = t[i][0] + h;
+    o[3 * i + 1] = 0.5f * (t[i][1] - t[i][2]);
+    o[3 * i + 2] = h + t[i][3];
   }
 }
 
@@ -394,9 +413,8 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
     hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   const long long CC = (long long)Cout * Cin;
-  const int blocks = (int)((CC + 255) / 256);
-  hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, a.nsplit, Cout, Cin,
-                     dw);
+  hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3((unsigned)((CC + 15) / 16)), dim3(256), 0, st, (const float*)ws,
+                     a.nsplit, Cout, Cin, dw);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
