@@ -448,7 +448,6 @@ def phantom_batches(S, B, rank, world, dev):
     return gen()
 
 
-@torch.no_grad()
 def roofline_peak(kernel):
     """Dense MFMA peak (TFLOP/s) for a C-ABI kernel family: bf16 for the *_bf16 family and the bf16
     raw GEMMs (pmu_conv3x3_{fwd,dgrad}_raw), fp32 otherwise (the Winograd raw kernels are *_wino_raw)."""
@@ -456,6 +455,7 @@ def roofline_peak(kernel):
     return BF16_MFMA_PEAK_TF if bf16 else FP32_MFMA_PEAK_TF
 
 
+@torch.no_grad()   # inference: no autograd graph, no saved activations per batch
 def c5_eval(net, dev, D, batch, precision):
     """Config c5's evaluation (PMU/eval.py:131-203 via predict.predict_volume's batching): predict all
     3 x D slices (D x D x 3 channels) of a seeded D^3 phantom along the axial/coronal/sagittal views
