@@ -439,6 +439,362 @@ __global__ __launch_bounds__(256) void fcomb_bwd_kernel(const float* __restrict_
   if (tid < KP) myws[MAXNH * FW * FW + KP * FW + MAXNH * FW + tid] = dbl;
 }
 
+// ------------------------------------------------------------------------------------------
+// backward, register-resident (the default): a wave owns 32 pixels at a time, exactly like the
+// forward, and keeps the recomputed chain f, H_1..H_NH transposed in registers.  Every layer of
+// the backward is one MFMA chain:
+//   dIn^T[c][px] = sum_o W[o][c] dU^T[o][px]   A = W column (b32 LDS reads), B = dU registers
+//   dW[o][c]    += sum_px dU[px][o] Hin[px][c] A, B from a 32-px LDS scratch per wave,
+//                                              accumulators register-resident across groups
+// The scratch (dU and the layer input, [px][65]) is written once per layer from registers; the
+// bias sums are its column sums.  Each wave walks a contiguous range of 32-px groups, so its
+// per-image dzb partials touch at most IPW images; the four waves' weight-gradient fragments are
+// summed in LDS in wave order and each block writes one slab (fixed-order reduction, no atomics).
+// ------------------------------------------------------------------------------------------
+constexpr int SRS = 65;               // scratch row stride
+constexpr int SCR = 2 * 32 * SRS;     // per-wave scratch floats (A: dU / dy, B: layer input)
+constexpr int WLDS = (MAXNH * FW + KP) * RRS + MAXNH * FW + KP;  // staged weights + biases
+
+struct BwdGeom {
+  long long G;  // 32-px groups
+  int nb;       // blocks (4 waves each)
+  int gpw;      // groups per wave
+  int ipw;      // images a wave's range can touch
+};
+
+__host__ __device__ inline BwdGeom bwd_geom(int N, long long HW) {
+  BwdGeom g;
+  g.G = ((long long)N * HW + 31) / 32;
+  long long nb = (g.G + 3) / 4;
+  if (nb > 256) nb = 256;  // one block (a wave per SIMD) per CU
+  if (nb < 1) nb = 1;
+  g.nb = (int)nb;
+  g.gpw = (int)((g.G + 4 * nb - 1) / (4 * nb));
+  g.ipw = (int)(((long long)g.gpw * 32 - 1) / HW) + 2;
+  return g;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void zero2(f32x16 (&a)[2]) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a[b][r] = 0.f;
+}
+
+// out^T = W . in^T over 64 input channels (forward layer, weights via b128 as in the forward kernel)
+__device__ __forceinline__ void bwd_layer_fwd(const float* wl, const f32x16 (&in)[2], f32x16 (&out)[2]) {
+  zero2(out);
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 w4[2];
+#pragma unroll
+      for (int ob = 0; ob < 2; ++ob) w4[ob] = *reinterpret_cast<const float4*>(wl + (ob * 32) * RRS + kb * 32 + 8 * q);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob) {
+          const float wa = s4 == 0 ? w4[ob].x : s4 == 1 ? w4[ob].y : s4 == 2 ? w4[ob].z : w4[ob].w;
+          out[ob] = mfma_f32_32x32x2(wa, in[kb][4 * q + s4], out[ob]);
+        }
+    }
+}
+
+// dx^T[c][px] = sum_o W[o][c] du^T[o][px] over NKB 32-row blocks of o (rows o >= omax skipped)
+template <int NKB>
+__device__ __forceinline__ void bwd_layer_dx(const float* W, const f32x16 (&du)[NKB], int omax, int lane,
+                                             f32x16 (&dx)[2]) {
+  zero2(dx);
+  const int h = lane >> 5;
+  const float* wc = W + 4 * h * RRS + (lane & 31);
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int o0 = kb * 32 + (s & 3) + 8 * (s >> 2);  // row of the h = 0 half
+      if (o0 >= omax) continue;                         // wave-uniform
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) dx[cb] = mfma_f32_32x32x2(wc[o0 * RRS + cb * 32], du[kb][s], dx[cb]);
+    }
+}
+
+// scratch[px][ch] <- transposed activation block(s) held in registers
+template <int NB>
+__device__ __forceinline__ void put_act(float* S, const f32x16 (&a)[NB], int lane) {
+  float* row = S + (lane & 31) * SRS;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) row[b * 32 + acc_row(r, lane)] = a[b][r];
+}
+
+// dW[ob][cb] += sum_px SA[px][ob*32+o] SB[px][cb*32+c]
+template <int NOB>
+__device__ __forceinline__ void bwd_layer_dw(const float* SA, const float* SB, int lane, f32x16 (&dw)[NOB][2]) {
+  const float* pa = SA + (lane >> 5) * SRS + (lane & 31);
+  const float* pb = SB + (lane >> 5) * SRS + (lane & 31);
+#pragma unroll 4
+  for (int t = 0; t < 16; ++t) {
+    float a[NOB], b[2];
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob) a[ob] = pa[2 * t * SRS + ob * 32];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) b[cb] = pb[2 * t * SRS + cb * 32];
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) dw[ob][cb] = mfma_f32_32x32x2(a[ob], b[cb], dw[ob][cb]);
+  }
+}
+
+__device__ __forceinline__ void relu_mask(f32x16 (&d)[2], const f32x16 (&hval)[2]) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) d[b][r] = hval[b][r] > 0.f ? d[b][r] : 0.f;
+}
+
+template <int NH>
+__global__ __launch_bounds__(256, 1) void fcomb_bwd_reg_kernel(const float* feat,
+                                                               const float* __restrict__ zb,
+                                                               const float* __restrict__ dl, FcombW p, int N,
+                                                               long long HW, float* __restrict__ dfeat,
+                                                               float* __restrict__ ws, float* __restrict__ dzb_slab,
+                                                               BwdGeom geo) {
+  __shared__ __attribute__((aligned(16))) float sm[WLDS + 4 * SCR];
+  float* Bsh = sm + (MAXNH * FW + KP) * RRS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  for (int e = tid; e < MAXNH * FW * FW; e += 256) {
+    const int l = e / (FW * FW), r = e % (FW * FW), o = r / FW, c = r % FW;
+    float v = 0.f;
+    if (l < p.NH && o < p.F && c < p.F) v = p.w[l][(long long)o * (l == 0 ? p.F + p.L : p.F) + c];
+    sm[(l * FW + o) * RRS + c] = v;
+  }
+  for (int e = tid; e < KP * FW; e += 256) {
+    const int o = e / FW, c = e % FW;
+    sm[(MAXNH * FW + o) * RRS + c] = (o < p.K && c < p.F) ? p.wl[o * p.F + c] : 0.f;
+  }
+  for (int e = tid; e < MAXNH * FW + KP; e += 256) {
+    float v = 0.f;
+    if (e < MAXNH * FW) {
+      const int l = e / FW, o = e % FW;
+      if (l >= 1 && l < p.NH && o < p.F) v = p.b[l][o];
+    } else if (e - MAXNH * FW < p.K) {
+      v = p.bl[e - MAXNH * FW];
+    }
+    Bsh[e] = v;
+  }
+  __syncthreads();
+
+  float* SA = sm + WLDS + wave * SCR;
+  float* SB = SA + 32 * SRS;
+  const float* wrow = sm + (lane & 31) * RRS + 4 * h;
+  const bool f4 = (p.F & 3) == 0;
+  const unsigned uHW = (unsigned)HW;
+  const long long P = (long long)N * HW;
+  const int gw = blockIdx.x * 4 + wave;
+  const long long g0 = (long long)gw * geo.gpw;
+  const long long g1 = g0 + geo.gpw < geo.G ? g0 + geo.gpw : geo.G;
+  const int nlo = (int)((unsigned long long)(g0 * 32) / uHW);
+  float* mydzb = dzb_slab + (long long)gw * geo.ipw * FW;
+  for (int j = 0; j < geo.ipw; ++j) mydzb[j * FW + lane] = 0.f;
+
+  f32x16 dW[NH][2][2], dWl[1][2];
+#pragma unroll
+  for (int l = 0; l < NH; ++l)
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob) zero2(dW[l][ob]);
+  zero2(dWl[0]);
+  float dbl = 0.f, dbh[NH > 1 ? NH : 1];  // lane = channel
+#pragma unroll
+  for (int l = 0; l < (NH > 1 ? NH : 1); ++l) dbh[l] = 0.f;
+
+  for (long long g = g0; g < g1; ++g) {
+    const long long px = g * 32 + (lane & 31);
+    const bool valid = px < P;
+    const unsigned pxc = (unsigned)(valid ? px : P - 1);
+    const unsigned n = pxc / uHW, pix = pxc - n * uHW;
+    // ---- recompute the chain: A[0] = f, A[l] = H_l
+    // A[0] = f is re-read from HBM for dW_1 rather than held (its 32 registers would spill)
+    auto load_f = [&](f32x16 (&fa)[2]) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float4 fv = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (valid) fv = ld4_row(feat + (size_t)pxc * p.F, kb * 32 + 8 * q + 4 * h, p.F, f4);
+          fa[kb][4 * q + 0] = fv.x;
+          fa[kb][4 * q + 1] = fv.y;
+          fa[kb][4 * q + 2] = fv.z;
+          fa[kb][4 * q + 3] = fv.w;
+        }
+    };
+    f32x16 A[NH + 1][2];
+    load_f(A[0]);
+#pragma unroll
+    for (int l = 0; l < NH; ++l) {
+      f32x16 u[2];
+      bwd_layer_fwd(wrow + (l * FW) * RRS, A[l], u);
+#pragma unroll
+      for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c0 = ob * 32 + 8 * q + 4 * h;
+          const float4 bv = l == 0 ? ld4_row(zb + (size_t)n * p.F, c0, p.F, f4)
+                                   : *reinterpret_cast<const float4*>(Bsh + l * FW + c0);
+          A[l + 1][ob][4 * q + 0] = fmaxf(0.f, u[ob][4 * q + 0] + bv.x);
+          A[l + 1][ob][4 * q + 1] = fmaxf(0.f, u[ob][4 * q + 1] + bv.y);
+          A[l + 1][ob][4 * q + 2] = fmaxf(0.f, u[ob][4 * q + 2] + bv.z);
+          A[l + 1][ob][4 * q + 3] = fmaxf(0.f, u[ob][4 * q + 3] + bv.w);
+        }
+    }
+    // ---- dy^T (classes in the acc layout of one 32-row block)
+    f32x16 dy[1];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = acc_row(r, lane);
+      dy[0][r] = (valid && k < p.K) ? dl[((size_t)n * p.K + k) * uHW + pix] : 0.f;
+    }
+    // ---- last layer: dWl += dy^T H_NH, dbl += sum dy, dH = Wl^T dy
+    put_act(SA, dy, lane);
+    put_act(SB, A[NH], lane);
+    wave_sync();
+    bwd_layer_dw<1>(SA, SB, lane, dWl);
+    if (lane < KP) {
+      float s = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < 32; ++r) s += SA[r * SRS + lane];
+      dbl += s;
+    }
+    f32x16 d[2];
+    bwd_layer_dx<1>(sm + (MAXNH * FW) * RRS, dy, p.K, lane, d);
+    relu_mask(d, A[NH]);
+    // ---- hidden layers NH-1 .. 0: d = dU_{l+1}
+#pragma unroll
+    for (int l = NH - 1; l >= 0; --l) {
+      wave_sync();  // previous scratch reads done (in-order LDS; fences keep the compiler honest)
+      put_act(SA, d, lane);
+      if (l == 0) {
+        f32x16 fa[2];
+        load_f(fa);
+        put_act(SB, fa, lane);
+      } else {
+        put_act(SB, A[l], lane);
+      }
+      wave_sync();
+      bwd_layer_dw<2>(SA, SB, lane, dW[l]);
+      if (l > 0) {
+        float s = 0.f;
+#pragma unroll 8
+        for (int r = 0; r < 32; ++r) s += SA[r * SRS + lane];
+        dbh[l] += s;
+      } else {
+        // per-image sums of dU_1 over this group's valid pixels
+        int r = 0;
+        while (r < 32 && g * 32 + r < P) {
+          const unsigned nn = (unsigned)(g * 32 + r) / uHW;
+          long long end = (long long)(nn + 1) * HW - g * 32;
+          if (end > 32) end = 32;
+          if (end > P - g * 32) end = P - g * 32;
+          float s = 0.f;
+          for (int q = r; q < (int)end; ++q) s += SA[q * SRS + lane];
+          mydzb[(nn - nlo) * FW + lane] += s;
+          r = (int)end;
+        }
+      }
+      f32x16 dx[2];
+      bwd_layer_dx<2>(sm + (l * FW) * RRS, d, FW, lane, dx);
+      if (l > 0) {
+        relu_mask(dx, A[l]);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) d[b] = dx[b];
+      } else if (valid) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c0 = cb * 32 + 8 * q + 4 * h;
+            float* out = dfeat + (size_t)pxc * p.F;
+            if (f4) {
+              if (c0 < p.F)
+                *reinterpret_cast<float4*>(out + c0) =
+                    make_float4(dx[cb][4 * q], dx[cb][4 * q + 1], dx[cb][4 * q + 2], dx[cb][4 * q + 3]);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                if (c0 + i < p.F) out[c0 + i] = dx[cb][4 * q + i];
+            }
+          }
+      }
+    }
+  }
+
+  // ---- block reduction of the four waves' partials (wave order), one slab per block
+  __syncthreads();
+  float* red = sm;  // WS_BLOCK floats, layout of the slab
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int l = 0; l < NH; ++l)
+#pragma unroll
+        for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              float* e = red + (l * FW + ob * 32 + acc_row(r, lane)) * FW + cb * 32 + (lane & 31);
+              *e = w == 0 ? dW[l][ob][cb][r] : *e + dW[l][ob][cb][r];
+            }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float* e = red + MAXNH * FW * FW + acc_row(r, lane) * FW + cb * 32 + (lane & 31);
+          *e = w == 0 ? dWl[0][cb][r] : *e + dWl[0][cb][r];
+        }
+      float* rb = red + MAXNH * FW * FW + KP * FW;
+#pragma unroll
+      for (int l = 0; l < MAXNH; ++l) {
+        const float v = (l >= 1 && l < NH) ? dbh[l < NH ? l : 0] : 0.f;
+        rb[l * FW + lane] = w == 0 ? v : rb[l * FW + lane] + v;
+      }
+      if (lane < KP) rb[MAXNH * FW + lane] = w == 0 ? dbl : rb[MAXNH * FW + lane] + dbl;
+    }
+    __syncthreads();
+  }
+  float* myws = ws + (long long)blockIdx.x * WS_BLOCK;
+  for (int e = tid; e < WS_BLOCK; e += 256) {
+    const bool unused = e < MAXNH * FW * FW && e / (FW * FW) >= NH;
+    myws[e] = unused ? 0.f : red[e];
+  }
+}
+
+// dzb_out[n][c] = sum over the waves whose group range touches image n (wave order)
+__global__ void fcomb_dzb_reduce_kernel(const float* __restrict__ slab, int N, long long HW, BwdGeom geo,
+                                        float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * FW) return;
+  const int n = e / FW, c = e % FW;
+  const long long gfirst = (long long)n * HW / 32, glast = ((long long)(n + 1) * HW - 1) / 32;
+  const int nw = geo.nb * 4;
+  const long long wlo = gfirst / geo.gpw;
+  long long whi = glast / geo.gpw;
+  if (whi > nw - 1) whi = nw - 1;
+  float s = 0.f;
+  for (long long w = wlo; w <= whi; ++w) {
+    const long long nlo = w * geo.gpw * 32 / HW;
+    s += slab[(w * geo.ipw + (n - nlo)) * FW + c];
+  }
+  out[e] = s;
+}
+
 struct FcombOut {
   float* dw[MAXNH];  // dw[0] = dW_1 [F][F+L]
   float* db[MAXNH];
@@ -639,7 +995,19 @@ extern "C" size_t pmu_fcomb_bwd_ws(int N, int H, int W) {
   if (N <= 0 || H <= 0 || W <= 0) return 0;
   const long long ntiles = ((long long)N * H * W + BT - 1) / BT;
   const int nb = fcomb_bwd_blocks(ntiles);
-  return ((size_t)nb * WS_BLOCK + (size_t)nb * N * FW + (size_t)N * FW) * sizeof(float);
+  const size_t lds = (size_t)nb * WS_BLOCK + (size_t)nb * N * FW;  // LDS-tile kernel
+  const BwdGeom g = bwd_geom(N, (long long)H * W);
+  const size_t reg = (size_t)g.nb * WS_BLOCK + (size_t)g.nb * 4 * g.ipw * FW;  // register-resident
+  return ((lds > reg ? lds : reg) + (size_t)N * FW) * sizeof(float);
+}
+
+static int fcomb_bwd_impl() {  // PMU_FCOMB_BWD=tile selects the LDS-tile kernel (A/B)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PMU_FCOMB_BWD");
+    v = (e && e[0] == 't') ? 0 : 1;
+  }
+  return v;
 }
 
 extern "C" int pmu_fcomb_bwd(const float* feat, const float* z, const float* zb, const float* dl,
@@ -659,6 +1027,32 @@ extern "C" int pmu_fcomb_bwd(const float* feat, const float* z, const float* zb,
   }
   o.dwl = dwl; o.dbl = dbl; o.dz = dz;
   const long long HW = (long long)H * W;
+  hipStream_t st0 = (hipStream_t)stream;
+  if (fcomb_bwd_impl() == 1) {
+    const BwdGeom geo = bwd_geom(N, HW);
+    float* slab = ws + (size_t)geo.nb * WS_BLOCK;
+    float* dzb = slab + (size_t)geo.nb * 4 * geo.ipw * FW;
+    if (NH == 1)
+      hipLaunchKernelGGL(fcomb_bwd_reg_kernel<1>, dim3(geo.nb), dim3(256), 0, st0, feat, zb, dl, p, N, HW, dfeat, ws,
+                         slab, geo);
+    else if (NH == 2)
+      hipLaunchKernelGGL(fcomb_bwd_reg_kernel<2>, dim3(geo.nb), dim3(256), 0, st0, feat, zb, dl, p, N, HW, dfeat, ws,
+                         slab, geo);
+    else
+      hipLaunchKernelGGL(fcomb_bwd_reg_kernel<3>, dim3(geo.nb), dim3(256), 0, st0, feat, zb, dl, p, N, HW, dfeat, ws,
+                         slab, geo);
+    PMU_CHECK_LAUNCH();
+    hipLaunchKernelGGL(fcomb_reduce_kernel, dim3((unsigned)pmu_cdiv(WS_BLOCK, 256)), dim3(256), 0, st0, ws, slab,
+                       geo.nb, 0, p, o, dzb);
+    PMU_CHECK_LAUNCH();
+    hipLaunchKernelGGL(fcomb_dzb_reduce_kernel, dim3((unsigned)pmu_cdiv((long long)N * FW, 256)), dim3(256), 0, st0,
+                       slab, N, HW, geo, dzb);
+    PMU_CHECK_LAUNCH();
+    hipLaunchKernelGGL(fcomb_zgrad_kernel, dim3((unsigned)pmu_cdiv(F + F * L + (long long)N * L, 256)), dim3(256), 0,
+                       st0, dzb, z, N, p, o);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   const long long ntiles = ((long long)N * HW + BT - 1) / BT;
   const int nb = fcomb_bwd_blocks(ntiles);
   FcombG gg;
