@@ -250,6 +250,19 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
     return res
 
 
+def cpu_leg(args, step):
+    """The bench's CPU-oracle leg (rank 0, N=1, after the timed region): the oracle as the checker
+    of the bench batch (``dice_vs_ref``, not for the probabilistic workload) and the timed CPU
+    baseline.  The only place bench.py touches oracle/."""
+    dvr = None
+    if args.workload != "probunet":
+        xb, tb = step.batch()
+        dvr = dice_vs_ref(step.net, xb, tb, args.classes, args.precision)
+    cpu = cpu_baseline(workload="probunet" if args.workload == "probunet" else "unet", size=args.size,
+                       channels=args.channels, classes=3 if args.workload == "probunet" else args.classes)
+    return cpu, dvr
+
+
 def dice_vs_ref(net, x, t, classes, precision):
     """The "Dice vs ref" half of the headline metric (BASELINE.json): the HIP network's prediction on
     the bench batch vs the fp32 CPU oracle's (oracle/unet_ref.py) for the same weights and input,
@@ -670,11 +683,7 @@ def main():
         evalres = c5_eval(step.net, dev, args.eval_size, B, args.precision)
     cpu = dvr = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if args.workload != "probunet":
-            xb, tb = step.batch()
-            dvr = dice_vs_ref(step.net, xb, tb, args.classes, args.precision)
-        cpu = cpu_baseline(workload="probunet" if args.workload == "probunet" else "unet", size=args.size,
-                           channels=args.channels, classes=3 if args.workload == "probunet" else args.classes)
+        cpu, dvr = cpu_leg(args, step)
     if rank == 0:
         res = {
             "metric": METRIC_C5 if args.workload == "c5" else METRIC_C4 if args.workload == "probunet" else METRIC,
