@@ -49,6 +49,7 @@ struct WinoArgs {
   float* part;        // [spatial tiles][2][NOUT] BN partial sums (fwd) or null
   float* tee;         // [N][H][W][KC] copy of the staged operand or null
   int NOUT, KC, split, tiles_w, tiles_h, nco;
+  int prio;           // 1: waves 4-7 run at s_setprio 1 (PMU_WINO_PRIO, raw kernel)
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -529,6 +530,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int lt = 16 * g.tg + (lane & 15);
   const int pbase = (2 * (lt >> 3)) * RROWP + (2 * (lt & 7)) * LS + 4 * g.kk;
+  if (a.prio && (tid >> 6) >= 4) __builtin_amdgcn_s_setprio(1);  // the younger half wins VALU arbitration
   PMU_RFETCH(0, smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -593,6 +595,11 @@ int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp
   a.tiles_w = pmu_cdiv(W, OW);
   a.tiles_h = pmu_cdiv(H, OH);
   a.nco = pmu_cdiv(NOUT, CO);
+  static const int prio = [] {  // PMU_WINO_PRIO=0|1 (A/B of static wave priority)
+    const char* e = getenv("PMU_WINO_PRIO");
+    return e ? atoi(e) : 0;
+  }();
+  a.prio = prio;
   const long long blocks = (long long)a.nco * a.tiles_w * a.tiles_h * N;
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
@@ -631,6 +638,7 @@ static bool wino_sync_forced() {
 int launch_wino(const pmu_frame* in, const float* wp, const float* bias, int NOUT, int KC, float* out0, float* out1,
                 int split, float* part, float* tee, bool dgrad, void* stream) {
   WinoArgs a;
+  a.prio = 0;
   a.in = make_dev_frame(in);
   a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part; a.tee = tee;
   a.NOUT = NOUT; a.KC = KC; a.split = split;

@@ -43,6 +43,7 @@ struct WgwArgs {
   const float* x;   // [N][H][W][Cin]
   float* ws;        // [nsplit][16][Cout][Cin]
   int N, H, W, Cout, Cin, tiles_w, tiles_h, ntiles, nsplit, nco;
+  int prio;         // 1: waves 4-7 run at s_setprio 1 (PMU_WINO_PRIO)
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -247,6 +248,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+  if (a.prio && half) __builtin_amdgcn_s_setprio(1);  // the younger half wins VALU arbitration
 
   auto read = [&](const float* slot, int s, WgwOps2& o) {
     const int t = 2 * s + (lane >> 5);
@@ -380,6 +382,14 @@ extern "C" size_t pmu_conv3x3_wgrad_ws_wino(int N, int H, int W, int Cin, int Co
   return (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float);
 }
 
+static int wino_prio() {  // PMU_WINO_PRIO=0|1 (A/B of static wave priority)
+  static const int v = [] {
+    const char* e = getenv("PMU_WINO_PRIO");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, int H, int W, int Cout, int Cin,
                                       float* dw, float* ws, size_t ws_bytes, void* stream) {
   PMU_REQUIRE(dzt && xt && dw && ws && N > 0 && H > 0 && W > 0);
@@ -387,6 +397,7 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
   WgwArgs a;
   a.dz = dzt; a.x = xt; a.ws = ws;
   wgw_geometry(N, H, W, Cout, Cin, a);
+  a.prio = wino_prio();
   PMU_REQUIRE(ws_bytes >= (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(a.nco * (Cin / WCI)), (unsigned)a.nsplit);

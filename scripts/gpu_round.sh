@@ -1,6 +1,6 @@
 # Round evidence in one call: all GPU tests, smoke, c2 / c4 / c5 bench lines (with CPU baselines and
 # dice_vs_ref), rocprofv3 kernel-trace stats of the c2, c4 and c5 bench commands, and the separate
-# FETCH_SIZE / WRITE_SIZE PMC passes of c2 and c5 (tools/pmc_traffic.py).
+# FETCH_SIZE / WRITE_SIZE PMC passes of c2, c5 and c4 (tools/pmc_traffic.py).
 set -u
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/round; mkdir -p $O
 cd $R
@@ -20,5 +20,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 cd $R
 WL=unet bash scripts/gpu_pmc_bench.sh > $O/pmc.log 2>&1 || exit $?
 WL=c5 EXTRA=--no-eval bash scripts/gpu_pmc_bench.sh > $O/pmc_c5.log 2>&1 || exit $?
+WL=probunet EXTRA=--no-eval bash scripts/gpu_pmc_bench.sh > $O/pmc_c4.log 2>&1 || exit $?
 cut -c 1-300 $O/bench.json; cut -c 1-300 $O/bench_c4.json; cut -c 1-300 $O/bench_c5.json
 echo round-done
