@@ -185,6 +185,33 @@ def test_probunet_full_width_vs_oracle(dev):
     assert err <= 2 * GRAD_TOL, (err, key)
 
 
+def test_probunet_c4_geometry_vs_oracle(dev):
+    """The c4 bench geometry (ProbUNetTrainer architecture at 256x256, 3 classes) at batch 8: loss,
+    reconstruction and every gradient vs the fp32 CPU oracle — the grid sizes, split-K slab counts
+    and Fcomb backward group ranges of the benchmarked shapes, not only the small test shapes."""
+    from oracle.probunet_ref import probunet_param_keys, probunet_train_step
+    torch.manual_seed(0)
+    net = _net(dev, num_filters=(64, 128, 256, 512, 1024)).train()
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    g = torch.Generator().manual_seed(11)
+    N, H, W = 8, 256, 256
+    x = torch.rand(N, 1, H, W, generator=g)
+    segm = torch.randint(0, 3, (N, 1, H, W), generator=g).float()
+    eps = torch.randn(N, 6, generator=g)
+    res, gref = probunet_train_step(sd, x, segm, eps, 5, 6, 3, 4, 10.0)
+    net.forward(x.to(dev), segm.to(dev), training=True)
+    _inject(net.posterior_latent_space, eps.to(dev), "rsample")
+    elbo = net.elbo(segm.to(dev))
+    (-elbo).backward()
+    torch.cuda.synchronize()
+    assert abs(float(-elbo) - float(res["loss"])) <= LOSS_RTOL * abs(float(res["loss"]))
+    assert max_abs(net.reconstruction, res["rec"]) <= 5 * ACT_TOL
+    named = dict(net.named_parameters())
+    keys = [k for k in probunet_param_keys(sd) if not k.startswith("unet.outc")]
+    err, key = grad_err({k: named[k].grad for k in keys}, {k: gref[k] for k in keys})
+    assert err <= 2 * GRAD_TOL, (err, key)
+
+
 def test_probunet_flat_grad_buffer(dev):
     """All gradients of one backward land in the model's single flat buffer (one all-reduce)."""
     from pmu_hip.functions import flat_grad_buffer
