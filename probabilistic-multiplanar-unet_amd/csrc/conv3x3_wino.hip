@@ -50,6 +50,7 @@ struct WinoArgs {
   float* tee;         // [N][H][W][KC] copy of the staged operand or null
   int NOUT, KC, split, tiles_w, tiles_h, nco;
   int prio;           // 1: waves 4-7 run at s_setprio 1 (PMU_WINO_PRIO, raw kernel)
+  int cpb;            // output-channel blocks per workgroup, walked in passes (raw kernel; else 1)
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -239,8 +240,9 @@ __device__ __forceinline__ WinoGeo wino_geo(const WinoArgs& a) {
   // spatial tile share their operand halo through that XCD's L2
   const int nb = gridDim.x, x = blockIdx.x & 7, q = nb >> 3, r = nb & 7;
   const int lb = x * q + (x < r ? x : r) + (blockIdx.x >> 3);
-  g.cob_blk = lb % a.nco;
-  int sp = lb / a.nco;
+  const int ncog = (a.nco + a.cpb - 1) / a.cpb;  // co-block groups (cpb co-blocks each)
+  g.cob_blk = (lb % ncog) * a.cpb;
+  int sp = lb / ncog;
   g.spatial = sp;
   const int tw = sp % a.tiles_w; sp /= a.tiles_w;
   const int th = sp % a.tiles_h; sp /= a.tiles_h;
@@ -483,9 +485,13 @@ constexpr int R_UNITS = R_A_FLOATS / 4;           // 16-B units of the operand i
 constexpr int R_NGL = (R_UNITS + NT - 1) / NT;    // operand DMA instructions per thread per chunk
 static_assert(R_NGL == 4, "operand image of 4 DMA rounds");
 
-template <bool DGRAD>
+// MULTI: the workgroup walks a.cpb output-channel blocks in passes (the input gradient, where it
+// pays: its K-short 64-channel layers lose most to the per-workgroup prologue); the forward keeps
+// one pass and the epilogue out of the loop (its inner loop measured 5-13% slower otherwise).
+template <bool DGRAD, bool MULTI>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * R_STAGE];
+  __shared__ __attribute__((aligned(16))) float smem[2 * R_STAGE + 8 * 16 * 2];
+  float* red = smem + 2 * R_STAGE;  // the epilogue's BN partials (kept apart: a DMA may be in flight)
   const int tid = threadIdx.x, lane = tid & 63;
   const WinoGeo g = wino_geo(a);
   const DevFrame& F = a.in;
@@ -509,18 +515,23 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
       *reinterpret_cast<float4*>(smem + R_STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  // passes over this block's output-channel blocks: the flat chunk sequence (pass, chunk) is one
+  // pipeline, so the next pass's first operand image and U tile arrive under this pass's last MFMAs
+  const int npass = !MULTI ? 1 : a.cpb < a.nco - g.cob_blk ? a.cpb : a.nco - g.cob_blk;
+  const int total = npass * nchunks;
   const float* wsrc = a.wp + (long long)g.cob_blk * nchunks * U_FLOATS + 4 * tid;
   const int wave_off = (tid >> 6) * 256;
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
                                    (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
-#define PMU_RFETCH(CH, BUF)                                                                                 \
+#define PMU_RFETCH(GI, BUF)                                                                                 \
   {                                                                                                        \
-    const int k0_ = (CH) * BK;                                                                             \
+    const int p_ = (GI) / nchunks;                                                                         \
+    const int k0_ = ((GI) - p_ * nchunks) * BK;                                                            \
     float* b_ = (BUF);                                                                                     \
     for (int r = 0; r < R_NGL; ++r)                                                                        \
       if (goff[r] >= 0) PMU_GLDS(x + goff[r] + k0_, b_ + 4 * (r * NT) + wave_off)                          \
-    const float* s_ = wsrc + (long long)(CH) * U_FLOATS;                                                   \
+    const float* s_ = wsrc + (long long)(GI) * U_FLOATS; /* pass p_ = co-block cob_blk + p_ */              \
     float* d_ = b_ + R_A_FLOATS + wave_off;                                                                \
     PMU_GLDS(s_, d_) PMU_GLDS(s_ + 4 * NT, d_ + 4 * NT) PMU_GLDS(s_ + 8 * NT, d_ + 8 * NT)                 \
     PMU_GLDS(s_ + 12 * NT, d_ + 12 * NT)                                                                   \
@@ -534,9 +545,9 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   PMU_RFETCH(0, smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int ch = 0; ch < nchunks; ++ch) {
-    float* cur = smem + (ch & 1) * R_STAGE;
-    if (ch + 1 < nchunks) PMU_RFETCH(ch + 1, smem + ((ch + 1) & 1) * R_STAGE)
+  for (int gi = 0; gi < total; ++gi) {
+    float* cur = smem + (gi & 1) * R_STAGE;
+    if (gi + 1 < total) PMU_RFETCH(gi + 1, smem + ((gi + 1) & 1) * R_STAGE)
     const unsigned pa = lds_addr(cur + pbase);
     // U of step ks for this lane: channel 4*kk + ks
     const unsigned ua = lds_addr(cur + R_A_FLOATS + g.ubase) + (unsigned)(4 * g.kk * 4 * CO * 4 * 4);
@@ -577,10 +588,18 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
     __syncthreads();
+    if (MULTI && gi % nchunks == nchunks - 1) {  // end of a pass: this co-block's output
+      WinoGeo gp = g;
+      gp.cob_blk = g.cob_blk + gi / nchunks;
+      gp.j0 = gp.cob_blk * CO;
+      wino_epilogue<DGRAD>(a, gp, acc, red);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
 #undef PMU_RFETCH
 #undef PMU_GLDS
-  wino_epilogue<DGRAD>(a, g, acc, smem);
+  if (!MULTI) wino_epilogue<DGRAD>(a, g, acc, red);
 }
 
 int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
@@ -600,11 +619,27 @@ int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp
     return e ? atoi(e) : 0;
   }();
   a.prio = prio;
-  const long long blocks = (long long)a.nco * a.tiles_w * a.tiles_h * N;
+  // co-block passes per workgroup: fewer, longer workgroups (the prologue of all but the first pass
+  // hides under MFMAs) while keeping >= 8 workgroups per CU; PMU_WINO_CPB forces a value (A/B)
+  static const int cpb_env = [] {
+    const char* e = getenv("PMU_WINO_CPB");
+    return e ? atoi(e) : 0;
+  }();
+  const long long spatial = (long long)a.tiles_w * a.tiles_h * N;
+  int cpb = 1;
+  if (!dgrad) {
+    // one pass (see MULTI)
+  } else if (cpb_env > 0) {
+    cpb = cpb_env < a.nco ? cpb_env : a.nco;
+  } else {
+    while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= 2048) cpb *= 2;
+  }
+  a.cpb = cpb;
+  const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
-  if (dgrad) hipLaunchKernelGGL((conv3x3_wino_raw_kernel<true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((conv3x3_wino_raw_kernel<false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  if (dgrad) hipLaunchKernelGGL((conv3x3_wino_raw_kernel<true, true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino_raw_kernel<false, false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -639,6 +674,7 @@ int launch_wino(const pmu_frame* in, const float* wp, const float* bias, int NOU
                 int split, float* part, float* tee, bool dgrad, void* stream) {
   WinoArgs a;
   a.prio = 0;
+  a.cpb = 1;
   a.in = make_dev_frame(in);
   a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part; a.tee = tee;
   a.NOUT = NOUT; a.KC = KC; a.split = split;
