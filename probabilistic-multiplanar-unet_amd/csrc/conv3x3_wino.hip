@@ -487,7 +487,7 @@ static_assert(R_NGL == 4, "operand image of 4 DMA rounds");
 
 // MULTI: the workgroup walks a.cpb output-channel blocks in passes (the input gradient, where it
 // pays: its K-short 64-channel layers lose most to the per-workgroup prologue); the forward keeps
-// one pass and the epilogue out of the loop (its inner loop measured 5-13% slower otherwise).
+// one pass (as a multi-pass kernel its inner loop measured 5-14% slower: 237 instead of 201 VGPRs).
 template <bool DGRAD, bool MULTI>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * R_STAGE + 8 * 16 * 2];
@@ -545,7 +545,9 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   PMU_RFETCH(0, smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int gi = 0; gi < total; ++gi) {
+  for (int p = 0; p < npass; ++p) {
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int gi = p * nchunks + ch;
     float* cur = smem + (gi & 1) * R_STAGE;
     if (gi + 1 < total) PMU_RFETCH(gi + 1, smem + ((gi + 1) & 1) * R_STAGE)
     const unsigned pa = lds_addr(cur + pbase);
@@ -588,18 +590,19 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
     __syncthreads();
-    if (MULTI && gi % nchunks == nchunks - 1) {  // end of a pass: this co-block's output
-      WinoGeo gp = g;
-      gp.cob_blk = g.cob_blk + gi / nchunks;
-      gp.j0 = gp.cob_blk * CO;
-      wino_epilogue<DGRAD>(a, gp, acc, red);
+  }
+    // end of a pass: this co-block's output
+    WinoGeo gp = g;
+    gp.cob_blk = g.cob_blk + p;
+    gp.j0 = gp.cob_blk * CO;
+    wino_epilogue<DGRAD>(a, gp, acc, red);
+    if (MULTI) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
 #undef PMU_RFETCH
 #undef PMU_GLDS
-  if (!MULTI) wino_epilogue<DGRAD>(a, g, acc, red);
 }
 
 int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
