@@ -29,17 +29,38 @@ __global__ __launch_bounds__(256) void colsum_f64_kernel(const float* __restrict
     out[(long long)g * Wd + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-__global__ void bn_fwd_finalize_kernel(const double* __restrict__ acc, int G, int C, double count,
-                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                       float eps, float momentum, float* running_mean, float* running_var,
-                                       float* mean_out, float* invstd_out, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int g = 0; g < G; ++g) {
-    s1 += acc[((long long)g * 2 + 0) * C + c];
-    s2 += acc[((long long)g * 2 + 1) * C + c];
-  }
+// sums of acc[g][0..1][c] over the G groups: 4 threads per channel each take every 4th group
+// (their loads in flight together instead of one dependent walk of G), combined in fixed order.
+// Block = 256 threads = 4 x 64 channels; returns the sums in the q == 0 threads.
+__device__ __forceinline__ bool group_sums(const double* __restrict__ acc, int G, int C, double& s1, double& s2) {
+  __shared__ double red[2][4][64];
+  const int q = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + cl;
+  s1 = 0.0;
+  s2 = 0.0;
+  if (c < C)
+    for (int g = q; g < G; g += 4) {
+      s1 += acc[((long long)g * 2 + 0) * C + c];
+      s2 += acc[((long long)g * 2 + 1) * C + c];
+    }
+  red[0][q][cl] = s1;
+  red[1][q][cl] = s2;
+  __syncthreads();
+  if (q != 0 || c >= C) return false;
+  s1 = ((red[0][0][cl] + red[0][1][cl]) + red[0][2][cl]) + red[0][3][cl];
+  s2 = ((red[1][0][cl] + red[1][1][cl]) + red[1][2][cl]) + red[1][3][cl];
+  return true;
+}
+
+__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __restrict__ acc, int G, int C,
+                                                              double count, const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float eps,
+                                                              float momentum, float* running_mean,
+                                                              float* running_var, float* mean_out,
+                                                              float* invstd_out, float* coef) {
+  double s1, s2;
+  if (!group_sums(acc, G, C, s1, s2)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const double mean = s1 / count;
   double var = s2 / count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -134,17 +155,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ acc, int G, int C, double count,
-                                       const float* __restrict__ gamma, const float* __restrict__ coef,
-                                       const float* __restrict__ mean, const float* __restrict__ invstd,
-                                       float* dgamma, float* dbeta, float* dbias, float* bcoef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sg = 0.0, sgx = 0.0;
-  for (int g = 0; g < G; ++g) {
-    sg += acc[((long long)g * 2 + 0) * C + c];
-    sgx += acc[((long long)g * 2 + 1) * C + c];
-  }
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ acc, int G, int C,
+                                                              double count, const float* __restrict__ gamma,
+                                                              const float* __restrict__ coef,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd, float* dgamma,
+                                                              float* dbeta, float* dbias, float* bcoef) {
+  double sg, sgx;
+  if (!group_sums(acc, G, C, sg, sgx)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const double is = invstd[c];
   const double gm = gamma ? (double)gamma[c] : 1.0;
   const double scale = gm * is;
@@ -755,7 +774,7 @@ extern "C" int pmu_bn_fwd_finalize(const double* acc, int G, int C, double count
                                    float* running_var, float* mean, float* invstd, float* coef, void* stream) {
   PMU_REQUIRE(acc && G > 0 && C > 0 && count > 0 && mean && invstd && coef);
   PMU_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)pmu_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)pmu_cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream,
                      acc, G, C, count, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, coef);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
@@ -797,7 +816,7 @@ extern "C" int pmu_bn_bwd_finalize(const double* acc, int G, int C, double count
                                    const float* coef, const float* mean, const float* invstd, float* dgamma,
                                    float* dbeta, float* dbias, float* bcoef, void* stream) {
   PMU_REQUIRE(acc && G > 0 && C > 0 && count > 0 && coef && mean && invstd && bcoef);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)pmu_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((unsigned)pmu_cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream,
                      acc, G, C, count, gamma, coef, mean, invstd, dgamma, dbeta, dbias, bcoef);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
