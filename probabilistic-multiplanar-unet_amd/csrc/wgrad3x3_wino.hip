@@ -218,13 +218,14 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
 // ---------------------------------------------------------------------------------------------
 constexpr int NSTEP2 = (TH / 2) * (TW / 2) / 2;  // 2 tiles per step
 
+
 struct WgwOps2 {
   float d[4];   // dz 2x2 of (tile, co)
   float xa[4];  // patch row ra of (tile, ci)
   float xb[4];  // patch row rb
 };
 
-template <int EXP = 0>
+template <int EXP = 0, int AHEAD = 2>
 __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -271,14 +272,16 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
     const bool more = tile + 1 < t_end;
     if (more && EXP != 1) wgw_dma(a, tile + 1, co0, ci0, tid, smem + (cur ^ 1) * SLOT);
     const float* slot = smem + (EXP == 1 ? 0 : cur * SLOT);
-    WgwOps2 ops[2];
-    read(slot, 0, ops[0]);
+    // operand reads run AHEAD steps in front of the MFMAs (ring of AHEAD + 1 operand sets)
+    WgwOps2 ops[AHEAD + 1];
+#pragma unroll
+    for (int s = 0; s < AHEAD; ++s) read(slot, s, ops[s]);
 #pragma unroll
     for (int s = 0; s < NSTEP2; ++s) {
       __builtin_amdgcn_sched_barrier(0);
-      if (s + 1 < NSTEP2) read(slot, s + 1, ops[(s + 1) & 1]);
+      if (s + AHEAD < NSTEP2) read(slot, s + AHEAD, ops[(s + AHEAD) % (AHEAD + 1)]);
       __builtin_amdgcn_sched_barrier(0);
-      const WgwOps2& o = ops[s & 1];
+      const WgwOps2& o = ops[s % (AHEAD + 1)];
       // Z row: r = alpha * dY[0] + beta * dY[1] (2 columns), then [r0, r0 + r1, r0 - r1, -r1]
       const float r0 = fmaf(beta, o.d[2], alpha * o.d[0]);
       const float r1 = fmaf(beta, o.d[3], alpha * o.d[1]);
@@ -401,6 +404,10 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
   PMU_REQUIRE(ws_bytes >= (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(a.nco * (Cin / WCI)), (unsigned)a.nsplit);
+  static const int ahead = [] {
+    const char* e = getenv("PMU_WGW_AHEAD");
+    return e ? atoi(e) : 2;
+  }();
   static const bool v16 = [] {
     const char* e = getenv("PMU_WGRAD_WINO");
     return e && strcmp(e, "16x16") == 0;
@@ -420,8 +427,12 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
 #endif
   if (v16)  // the 16x16x4 layout (all components per wave)
     hipLaunchKernelGGL((wgrad3x3_wino_kernel<0>), grid, dim3(NT), 0, st, a);
+  else if (ahead == 1)  // PMU_WGW_AHEAD=1|2|3: operand read-ahead depth in steps (A/B)
+    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0, 1>), grid, dim3(NT), 0, st, a);
+  else if (ahead == 3)
+    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0, 3>), grid, dim3(NT), 0, st, a);
   else
-    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0, 2>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   const long long CC = (long long)Cout * Cin;
   hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3((unsigned)((CC + 15) / 16)), dim3(256), 0, st, (const float*)ws,
