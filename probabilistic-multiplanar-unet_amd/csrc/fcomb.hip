@@ -78,6 +78,7 @@ __device__ __forceinline__ float4 ld4_row(const float* row, int c0, int F, bool 
                      c0 + 3 < F ? row[c0 + 3] : 0.f);
 }
 
+template <bool FEWK>  // FEWK: K <= 4 classes, last layer on VALU
 __global__ __launch_bounds__(256, 2) void fcomb_fwd_kernel(const float* __restrict__ feat, const float* __restrict__ zb,
                                                            FcombW p, int S, int N, long long HW, float* __restrict__ y,
                                                            long long ngroups) {
@@ -188,6 +189,36 @@ __global__ __launch_bounds__(256, 2) void fcomb_fwd_kernel(const float* __restri
             hc[ob][4 * q + 2] = fmaxf(0.f, na[ob][4 * q + 2] + bv.z);
             hc[ob][4 * q + 3] = fmaxf(0.f, na[ob][4 * q + 3] + bv.w);
           }
+      }
+      if (FEWK) {
+        // ---- last layer for a few classes (the trainer's 3): VALU dot products instead of a
+        // 32-row MFMA tile that would be 7/8 padding. Lane (px, h) holds half the channels of its
+        // pixel: register 4q+s4 of block kb = channel kb*32 + 8q + 4h + s4.
+        float yk[4] = {0.f, 0.f, 0.f, 0.f};
+        const float* wlast = Wsh + (MAXNH * FW) * RRS + 4 * h;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (k >= p.K) break;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 w4 = *reinterpret_cast<const float4*>(wlast + k * RRS + kb * 32 + 8 * q);
+              yk[k] = fmaf(w4.x, hc[kb][4 * q + 0], yk[k]);
+              yk[k] = fmaf(w4.y, hc[kb][4 * q + 1], yk[k]);
+              yk[k] = fmaf(w4.z, hc[kb][4 * q + 2], yk[k]);
+              yk[k] = fmaf(w4.w, hc[kb][4 * q + 3], yk[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) yk[k] += __shfl_xor(yk[k], 32, 64);
+        if (valid) {
+          float* yo = y + ((long long)s * N + n) * p.K * HW + pix;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)  // the two halves store alternate classes
+            if (k < p.K && (k & 1) == h) yo[(long long)k * HW] = yk[k] + Bsh[MAXNH * FW + k];
+        }
+        continue;
       }
       // ---- last layer (K <= 32 rows); two accumulators (one per input block) to break the chain
       f32x16 la[2];
@@ -985,8 +1016,12 @@ extern "C" int pmu_fcomb_fwd(const float* feat, const float* zb, const float* co
   const long long ngroups = ((long long)N * HW + 31) / 32;
   long long g = (ngroups + 3) / 4;
   if (g > 512) g = 512;  // persistent: 2 blocks per CU
-  hipLaunchKernelGGL(fcomb_fwd_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, feat, zb, p, S, N, HW, y,
-                     ngroups);
+  if (K <= 4)
+    hipLaunchKernelGGL(fcomb_fwd_kernel<true>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, feat, zb, p, S, N,
+                       HW, y, ngroups);
+  else
+    hipLaunchKernelGGL(fcomb_fwd_kernel<false>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, feat, zb, p, S, N,
+                       HW, y, ngroups);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
