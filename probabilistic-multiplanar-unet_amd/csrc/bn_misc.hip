@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void sgd_clip_kernel(const pmu_sgd_chunk* __re
 // atomicAdd per counter per block (integer-valued: order-independent).  The 64-bit pixel division
 // and fp64 adds per pixel, and the per-counter LDS tree with 9 barriers each, made the previous
 // version ~140 us per call for a 32 x 256^2 batch.
-constexpr int DICE_T = 256, DICE_MAXB = 2048;
+constexpr int DICE_T = 256, DICE_MAXB = 512;
 __global__ __launch_bounds__(DICE_T) void dice_counts_kernel(const float* __restrict__ y, const float* __restrict__ mask,
                                                              int N, int K, int H, int W, double* __restrict__ out) {
   __shared__ unsigned red[DICE_T / 64][3 * HEAD_KMAX];
@@ -688,28 +688,49 @@ __global__ __launch_bounds__(DICE_T) void dice_counts_kernel(const float* __rest
 #pragma unroll
   for (int i = 0; i < 3 * HEAD_KMAX; ++i) loc[i] = 0u;
   double b0 = 0.0, b1 = 0.0, b2 = 0.0;  // K == 1
-  for (unsigned p = blockIdx.x * DICE_T + threadIdx.x; p < P; p += gridDim.x * DICE_T) {
-    const unsigned n = p / HW, pix = p - n * HW;
-    const float t = mask[p];
-    if (K == 1) {  // the mask is summed as the float it is (dice_coeff on (pred > 0.5) vs mask)
-      const float pr = y[p] > 0.5f ? 1.f : 0.f;
-      b0 += (double)(pr * t); b1 += (double)pr; b2 += (double)t;
-    } else {
+  // DB pixels per thread per round, all their loads issued before any is used (the per-pixel loop
+  // was HBM-latency bound); fewer blocks, so the per-block counter atomics do not pile up on the
+  // K*3 addresses (2048 blocks x 9 same-address fp64 atomics cost ~40 us per call)
+  constexpr int DB = 8;
+  const unsigned stride = gridDim.x * DICE_T;
+  for (unsigned p0 = blockIdx.x * DICE_T + threadIdx.x; p0 < P; p0 += DB * stride) {
+    float tv[DB], yv[DB][HEAD_KMAX];
+#pragma unroll
+    for (int b = 0; b < DB; ++b) {
+      const unsigned p = p0 + b * stride;
+      const bool ok = p < P;
+      const unsigned pc = ok ? p : P - 1;
+      const unsigned n = pc / HW, pix = pc - n * HW;
+      tv[b] = ok ? mask[pc] : -1.f;
       const float* yp = y + (size_t)n * K * HW + pix;
+#pragma unroll
+      for (int k = 0; k < HEAD_KMAX; ++k) yv[b][k] = (k < KK) ? yp[(size_t)k * HW] : 0.f;
+    }
+#pragma unroll
+    for (int b = 0; b < DB; ++b) {
+      if (p0 + b * stride >= P) break;
+      const float t = tv[b];
+      if (K == 1) {  // the mask is summed as the float it is (dice_coeff on (pred > 0.5) vs mask)
+        const float pr = yv[b][0] > 0.5f ? 1.f : 0.f;
+        b0 += (double)(pr * t); b1 += (double)pr; b2 += (double)t;
+        continue;
+      }
       float m = -INFINITY;
-      for (int k = 0; k < K; ++k) m = fmaxf(m, yp[(size_t)k * HW]);
+#pragma unroll
+      for (int k = 0; k < HEAD_KMAX; ++k)
+        if (k < K) m = fmaxf(m, yv[b][k]);
       float e[HEAD_KMAX];
-      float s = 0.f;
+      float sm = 0.f;
 #pragma unroll
       for (int k = 0; k < HEAD_KMAX; ++k) {
         e[k] = 0.f;
-        if (k < K) { e[k] = expf(yp[(size_t)k * HW] - m); s += e[k]; }
+        if (k < K) { e[k] = expf(yv[b][k] - m); sm += e[k]; }
       }
       int am = 0;
-      float best = e[0] / s;
+      float best = e[0] / sm;
 #pragma unroll
       for (int k = 1; k < HEAD_KMAX; ++k) {
-        if (k < K) { const float pk = e[k] / s; if (pk > best) { best = pk; am = k; } }
+        if (k < K) { const float pk = e[k] / sm; if (pk > best) { best = pk; am = k; } }
       }
 #pragma unroll
       for (int k = 0; k < HEAD_KMAX; ++k) {
@@ -950,7 +971,7 @@ extern "C" int pmu_dice_counts(const float* y, const float* mask, int N, int K, 
   if (hipMemsetAsync(counts, 0, sizeof(double) * 3 * K, (hipStream_t)stream) != hipSuccess) return PMU_ERR_ARG;
   const long long P = (long long)N * H * W;
   PMU_REQUIRE(P < (1LL << 31));
-  unsigned g = (unsigned)pmu_cdiv(P, DICE_T);
+  unsigned g = (unsigned)pmu_cdiv(P, DICE_T * 8);
   if (g > DICE_MAXB) g = DICE_MAXB;
   hipLaunchKernelGGL(dice_counts_kernel, dim3(g), dim3(DICE_T), 0, (hipStream_t)stream, y, mask, N, K, H, W, counts);
   PMU_CHECK_LAUNCH();
