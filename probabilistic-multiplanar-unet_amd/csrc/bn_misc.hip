@@ -708,7 +708,7 @@ __global__ __launch_bounds__(DICE_T) void dice_counts_kernel(const float* __rest
     }
 #pragma unroll
     for (int b = 0; b < DB; ++b) {
-      if (p0 + b * stride >= P) break;
+      if (p0 + b * stride >= P) continue;
       const float t = tv[b];
       if (K == 1) {  // the mask is summed as the float it is (dice_coeff on (pred > 0.5) vs mask)
         const float pr = yv[b][0] > 0.5f ? 1.f : 0.f;
@@ -760,10 +760,11 @@ __global__ __launch_bounds__(DICE_T) void dice_counts_kernel(const float* __rest
   }
 #pragma unroll
   for (int i = 0; i < 3 * HEAD_KMAX; ++i) {
-    if (i >= 3 * KK) break;
-    unsigned v = loc[i];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) red[wave][i] = v;
+    if (i < 3 * KK) {
+      unsigned v = loc[i];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == 0) red[wave][i] = v;
+    }
   }
   __syncthreads();
   if (threadIdx.x < 3 * KK) {
