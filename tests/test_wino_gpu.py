@@ -216,3 +216,41 @@ def test_unet_wino_matches_direct(dev, monkeypatch, fused):
     e_d, _ = grad_err(g_d, g64)
     e_w, k_w = grad_err(g_w, g64)
     assert e_w <= max(2 * e_d, 1e-4), (e_w, e_d, k_w)
+
+
+_MULTIPASS = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from pmu_hip import _lib as L
+from pmu_hip.engine import pack_weights_wino
+N, H, W, Cin, Cout, split = 2, 40, 36, 160, 64, 96
+g = torch.Generator().manual_seed(17)
+dz = torch.randn(N, H, W, Cout, generator=g).cuda()
+w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).cuda()
+wp = pack_weights_wino(w, True)
+dx0 = torch.empty(N, H, W, split, device="cuda")
+dx1 = torch.empty(N, H, W, Cin - split, device="cuda")
+L.call("pmu_conv3x3_dgrad_wino_raw", dz.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, split, dx0.data_ptr(),
+       dx1.data_ptr(), L.stream())
+torch.cuda.synchronize()
+ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double().cpu(), dz.permute(0, 3, 1, 2).double().cpu(),
+                                 padding=1).permute(0, 2, 3, 1)
+got = torch.cat([dx0, dx1], dim=3).double().cpu()
+print(float((got - ref).abs().max() / ref.abs().max()))
+"""
+
+
+@pytest.mark.parametrize("cpb", [2, 3, 5])
+def test_dgrad_wino_raw_multipass(cpb):
+    """The input gradient's output-channel passes (a workgroup walking cpb co-blocks of one tile,
+    the next pass's operands fetched under the current pass's MFMAs), forced through PMU_WINO_CPB
+    — the test shapes alone stay below the automatic threshold.  Cin = 160 = 5 co-blocks, so cpb 2
+    and 3 leave a short last group and cpb 5 walks them all; a concat split inside a pass."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "probabilistic-multiplanar-unet_amd")
+    env = dict(os.environ, PMU_WINO_CPB=str(cpb))
+    out = subprocess.run([sys.executable, "-c", _MULTIPASS, pkg], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert float(out.stdout.strip().splitlines()[-1]) <= TOL
