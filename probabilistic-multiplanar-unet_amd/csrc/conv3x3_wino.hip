@@ -271,13 +271,20 @@ __device__ __forceinline__ void wino_items(const WinoGeo& g, int (&ih)[NI], int 
 }
 
 // epilogue: lane holds M[comp][tile 16*tg + 4*(lane>>4) + r][output channel j0 + 16*hh + (lane&15)]
+// this lane's output-channel bias (forward); loaded before a pass's MFMAs by the multi-pass kernel
 template <bool DGRAD>
-__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, const WinoGeo& g, f32x4 (&acc)[16], float* smem) {
+__device__ __forceinline__ float wino_bias(const WinoArgs& a, const WinoGeo& g) {
+  const int j = g.j0 + 16 * g.hh + (threadIdx.x & 15);
+  return (!DGRAD && j < a.NOUT && a.bias) ? a.bias[j] : 0.f;
+}
+
+template <bool DGRAD>
+__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, const WinoGeo& g, f32x4 (&acc)[16], float* smem,
+                                              float b) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const DevFrame& F = a.in;
   const int j = g.j0 + 16 * g.hh + (lane & 15);
   const bool jok = j < a.NOUT;
-  const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -374,7 +381,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_kernel(WinoArgs a) {
     wino_chunk(As, Us, g.pbase, g.ubase, g.kk, acc);
     __syncthreads();
   }
-  wino_epilogue<DGRAD>(a, g, acc, smem);
+  wino_epilogue<DGRAD>(a, g, acc, smem, wino_bias<DGRAD>(a, g));
 }
 
 // Software-pipelined variant (the default for fast-path frames): the next chunk's operand items and
@@ -466,7 +473,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
 #undef PMU_WPREFETCH
 #undef PMU_WCOMMIT
 #undef PMU_GLDS
-  wino_epilogue<DGRAD>(a, g, acc, smem);
+  wino_epilogue<DGRAD>(a, g, acc, smem, wino_bias<DGRAD>(a, g));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -485,9 +492,10 @@ constexpr int R_UNITS = R_A_FLOATS / 4;           // 16-B units of the operand i
 constexpr int R_NGL = (R_UNITS + NT - 1) / NT;    // operand DMA instructions per thread per chunk
 static_assert(R_NGL == 4, "operand image of 4 DMA rounds");
 
-// MULTI: the workgroup walks a.cpb output-channel blocks in passes (the input gradient, where it
-// pays: its K-short 64-channel layers lose most to the per-workgroup prologue); the forward keeps
-// one pass (as a multi-pass kernel its inner loop measured 5-14% slower: 237 instead of 201 VGPRs).
+// MULTI: the workgroup walks a.cpb output-channel blocks in passes (the K-short 64-channel layers
+// lose most to the per-workgroup prologue).  The forward's bias is loaded before each pass's MFMAs:
+// loaded in the epilogue, the compiler waited vmcnt(0) on the next pass's in-flight DMAs at the
+// next register reuse, and the forward measured 14% slower as a multi-pass kernel.
 template <bool DGRAD, bool MULTI>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * R_STAGE + 8 * 16 * 2];
@@ -499,8 +507,11 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   const int KC = a.KC;
   const int nchunks = KC / BK;
 
-  // this thread's operand units: global float offset (chunk 0) or -1 (outside the input / pad)
-  long long goff[R_NGL];
+  // this thread's operand units: global BYTE offset (chunk 0; < 2^32, host-checked) and whether
+  // the unit is inside the input.  The DMA addresses are a uniform base (SGPRs) plus these 32-bit
+  // offsets, so the loop issues them in global_load_lds's saddr form and writes no address VGPRs.
+  unsigned goff[R_NGL];
+  unsigned gin = 0u;
 #pragma unroll
   for (int r = 0; r < R_NGL; ++r) {
     const int u = r * NT + tid;
@@ -509,7 +520,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
     const bool data = u < R_UNITS && q < 4 && hc < HW;
     const int h = g.h0 - 1 + hr, w = g.w0 - 1 + hc;
     const bool in = data && h >= 0 && w >= 0 && h < F.H && w < F.W;
-    goff[r] = in ? (((long long)g.n * F.H + h) * F.W + w) * KC + 4 * q : -1;
+    goff[r] = in ? (unsigned)(((((long long)g.n * F.H + h) * F.W + w) * KC + 4 * q) * 4) : 0u;
+    gin |= in ? (1u << r) : 0u;
     if (data && !in) {  // zero padding, in both stages, once
       *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
       *reinterpret_cast<float4*>(smem + R_STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -519,7 +531,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   // pipeline, so the next pass's first operand image and U tile arrive under this pass's last MFMAs
   const int npass = !MULTI ? 1 : a.cpb < a.nco - g.cob_blk ? a.cpb : a.nco - g.cob_blk;
   const int total = npass * nchunks;
-  const float* wsrc = a.wp + (long long)g.cob_blk * nchunks * U_FLOATS + 4 * tid;
+  const float* wsrc = a.wp + (long long)g.cob_blk * nchunks * U_FLOATS;  // uniform
+  const unsigned uoff = 16u * tid;
   const int wave_off = (tid >> 6) * 256;
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
@@ -529,12 +542,14 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
     const int p_ = (GI) / nchunks;                                                                         \
     const int k0_ = ((GI) - p_ * nchunks) * BK;                                                            \
     float* b_ = (BUF);                                                                                     \
+    const char* xb_ = reinterpret_cast<const char*>(x + k0_);                                              \
     for (int r = 0; r < R_NGL; ++r)                                                                        \
-      if (goff[r] >= 0) PMU_GLDS(x + goff[r] + k0_, b_ + 4 * (r * NT) + wave_off)                          \
-    const float* s_ = wsrc + (long long)(GI) * U_FLOATS; /* pass p_ = co-block cob_blk + p_ */              \
+      if ((gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                           \
+    /* pass p_ = co-block cob_blk + p_ */                                                                  \
+    const char* s_ = reinterpret_cast<const char*>(wsrc + (long long)(GI) * U_FLOATS) + uoff;              \
     float* d_ = b_ + R_A_FLOATS + wave_off;                                                                \
-    PMU_GLDS(s_, d_) PMU_GLDS(s_ + 4 * NT, d_ + 4 * NT) PMU_GLDS(s_ + 8 * NT, d_ + 8 * NT)                 \
-    PMU_GLDS(s_ + 12 * NT, d_ + 12 * NT)                                                                   \
+    PMU_GLDS(s_, d_) PMU_GLDS(s_ + 16 * NT, d_ + 4 * NT) PMU_GLDS(s_ + 32 * NT, d_ + 8 * NT)               \
+    PMU_GLDS(s_ + 48 * NT, d_ + 12 * NT)                                                                   \
   }
   f32x4 acc[16];
 #pragma unroll
@@ -546,6 +561,12 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int p = 0; p < npass; ++p) {
+  // the pass's bias, loaded before its MFMAs (a load issued in the epilogue made the compiler
+  // wait vmcnt(0) — on the next pass's in-flight DMAs — at the next register reuse)
+  WinoGeo gp = g;
+  gp.cob_blk = g.cob_blk + p;
+  gp.j0 = gp.cob_blk * CO;
+  const float bias_p = wino_bias<DGRAD>(a, gp);
   for (int ch = 0; ch < nchunks; ++ch) {
     const int gi = p * nchunks + ch;
     float* cur = smem + (gi & 1) * R_STAGE;
@@ -592,10 +613,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
     __syncthreads();
   }
     // end of a pass: this co-block's output
-    WinoGeo gp = g;
-    gp.cob_blk = g.cob_blk + p;
-    gp.j0 = gp.cob_blk * CO;
-    wino_epilogue<DGRAD>(a, gp, acc, red);
+    wino_epilogue<DGRAD>(a, gp, acc, red, bias_p);
     if (MULTI) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -608,6 +626,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
 int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
                     float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
   PMU_REQUIRE(x && wp && out0 && KC > 0 && KC % BK == 0 && NOUT > 0 && N > 0 && H > 0 && W > 0);
+  PMU_REQUIRE((long long)N * H * W * KC * 4 < (1LL << 32));  // 32-bit DMA byte offsets
   WinoArgs a;
   memset(&a, 0, sizeof(a));
   a.in.s0.x = x; a.in.s0.C = KC; a.in.s0.H = H; a.in.s0.W = W;
@@ -629,19 +648,28 @@ int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp
     return e ? atoi(e) : 0;
   }();
   const long long spatial = (long long)a.tiles_w * a.tiles_h * N;
+  static const bool fwd_multi = [] {  // PMU_WINO_FWD_MULTI=0: one pass per forward workgroup (A/B)
+    const char* e = getenv("PMU_WINO_FWD_MULTI");
+    return !(e && atoi(e) == 0);
+  }();
   int cpb = 1;
-  if (!dgrad) {
+  if (!dgrad && !fwd_multi) {
     // one pass (see MULTI)
   } else if (cpb_env > 0) {
     cpb = cpb_env < a.nco ? cpb_env : a.nco;
   } else {
-    while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= 2048) cpb *= 2;
+    static const long long min_wg = [] {  // PMU_WINO_MINWG: fewest workgroups the passes may leave
+      const char* e = getenv("PMU_WINO_MINWG");
+      return e ? atoll(e) : 2048LL;
+    }();
+    while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= min_wg) cpb *= 2;
   }
   a.cpb = cpb;
   const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   if (dgrad) hipLaunchKernelGGL((conv3x3_wino_raw_kernel<true, true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  else if (fwd_multi) hipLaunchKernelGGL((conv3x3_wino_raw_kernel<false, true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
   else hipLaunchKernelGGL((conv3x3_wino_raw_kernel<false, false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;

@@ -236,16 +236,34 @@ torch.cuda.synchronize()
 ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double().cpu(), dz.permute(0, 3, 1, 2).double().cpu(),
                                  padding=1).permute(0, 2, 3, 1)
 got = torch.cat([dx0, dx1], dim=3).double().cpu()
-print(float((got - ref).abs().max() / ref.abs().max()))
+err = float((got - ref).abs().max() / ref.abs().max())
+# forward with 5 output-channel blocks: z, bias and the BN partial sums of every pass
+Cin, Cout = 64, 160
+x = torch.randn(N, H, W, Cin, generator=g).cuda()
+w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).cuda()
+b = torch.randn(Cout, generator=g).cuda()
+z = torch.empty(N, H, W, Cout, device="cuda")
+part = torch.empty(L.lib().pmu_conv3x3_tiles_wino(N, H, W), 2 * Cout, device="cuda")
+wp = pack_weights_wino(w, False)
+L.call("pmu_conv3x3_fwd_wino_raw", x.data_ptr(), Cin, N, H, W, wp.data_ptr(), b.data_ptr(), Cout, z.data_ptr(),
+       part.data_ptr(), L.stream())
+torch.cuda.synchronize()
+ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).double().cpu(), w.double().cpu(), b.double().cpu(),
+                                 padding=1).permute(0, 2, 3, 1)
+err = max(err, float((z.double().cpu() - ref).abs().max() / ref.abs().max()))
+tot = part.double().sum(0).cpu()
+err = max(err, float(((tot[:Cout] - ref.sum((0, 1, 2))).abs() / ref.abs().sum((0, 1, 2))).max()))
+print(err)
 """
 
 
 @pytest.mark.parametrize("cpb", [2, 3, 5])
-def test_dgrad_wino_raw_multipass(cpb):
-    """The input gradient's output-channel passes (a workgroup walking cpb co-blocks of one tile,
-    the next pass's operands fetched under the current pass's MFMAs), forced through PMU_WINO_CPB
-    — the test shapes alone stay below the automatic threshold.  Cin = 160 = 5 co-blocks, so cpb 2
-    and 3 leave a short last group and cpb 5 walks them all; a concat split inside a pass."""
+def test_wino_raw_multipass(cpb):
+    """The output-channel passes of the raw Winograd kernels (a workgroup walking cpb co-blocks of
+    one tile, the next pass's operands fetched under the current pass's MFMAs), forced through
+    PMU_WINO_CPB — the test shapes alone stay below the automatic threshold.  Input gradient with
+    Cin = 160 and forward with Cout = 160 (5 co-blocks): cpb 2 and 3 leave a short last group, cpb
+    5 walks them all; a concat split inside a pass; bias and BN partial sums per pass."""
     import os
     import subprocess
     import sys
