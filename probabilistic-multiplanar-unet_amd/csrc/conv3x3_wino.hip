@@ -660,7 +660,7 @@ int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp
   } else {
     static const long long min_wg = [] {  // PMU_WINO_MINWG: fewest workgroups the passes may leave
       const char* e = getenv("PMU_WINO_MINWG");
-      return e ? atoll(e) : 2048LL;
+      return e ? atoll(e) : 1024LL;
     }();
     while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= min_wg) cpb *= 2;
   }
