@@ -219,13 +219,23 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
 constexpr int NSTEP2 = (TH / 2) * (TW / 2) / 2;  // 2 tiles per step
 
 
+template <int OFF>
+__device__ __forceinline__ float lds_b32(unsigned addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(p);
+}
+
 struct WgwOps2 {
   float d[4];   // dz 2x2 of (tile, co)
   float xa[4];  // patch row ra of (tile, ci)
   float xb[4];  // patch row rb
 };
 
-template <int EXP = 0, int AHEAD = 2>
+template <int EXP = 0>
 __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -251,18 +261,36 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
     for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
   if (a.prio && half) __builtin_amdgcn_s_setprio(1);  // the younger half wins VALU arbitration
 
-  auto read = [&](const float* slot, int s, WgwOps2& o) {
-    const int t = 2 * s + (lane >> 5);
-    const int ty = t >> 3, tx = t & 7;
-    const float* dp = slot + ((2 * ty) * TW + 2 * tx) * DLS + (lane & 31);
-    const float* xp = slot + D_FLOATS + ((2 * ty + ra) * HWD + 2 * tx) * XLS + 32 * half + (lane & 31);
-    const int db = (rb - ra) * HWD * XLS;
-    o.d[0] = dp[0]; o.d[1] = dp[DLS]; o.d[2] = dp[TW * DLS]; o.d[3] = dp[(TW + 1) * DLS];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o.xa[j] = xp[j * XLS];
-      o.xb[j] = xp[db + j * XLS];
-    }
+  // Operand reads as explicit ds_read_b32 (asm): the compiler's own waits put an lgkmcnt(0)
+  // right after each step's read-ahead (its counter bookkeeping gave up), exposing the LDS latency
+  // every step.  Here a step waits for its operands — read one step earlier — before issuing the
+  // next step's reads, as the forward kernel does.  Per lane: three base addresses per K-tile, a
+  // compile-time offset per step and value.  Step s covers tiles t = 2s + h (h = lane >> 5):
+  // ty = s >> 2, tx = 2 (s & 3) + h.
+  const int hl = lane >> 5;
+  const int db = (rb - ra) * HWD * XLS;
+  unsigned dbase = 0, xabase = 0, xbbase = 0;
+  auto set_bases = [&](const float* slot) {
+    dbase = lds_addr(slot + (2 * hl) * DLS + (lane & 31));
+    xabase = lds_addr(slot + D_FLOATS + ra * HWD * XLS + (2 * hl) * XLS + 32 * half + (lane & 31));
+    xbbase = xabase + 4u * (unsigned)db;
+  };
+  auto read = [&](int s, WgwOps2& o) {
+    const unsigned dstep = 4u * (unsigned)((2 * (s >> 2) * TW + 4 * (s & 3)) * DLS);
+    const unsigned xstep = 4u * (unsigned)((2 * (s >> 2) * HWD + 4 * (s & 3)) * XLS);
+    const unsigned da = dbase + dstep, xa = xabase + xstep, xb = xbbase + xstep;
+    o.d[0] = lds_b32<0>(da);
+    o.d[1] = lds_b32<4 * DLS>(da);
+    o.d[2] = lds_b32<4 * TW * DLS>(da);
+    o.d[3] = lds_b32<4 * (TW + 1) * DLS>(da);
+    o.xa[0] = lds_b32<0>(xa);
+    o.xa[1] = lds_b32<4 * XLS>(xa);
+    o.xa[2] = lds_b32<8 * XLS>(xa);
+    o.xa[3] = lds_b32<12 * XLS>(xa);
+    o.xb[0] = lds_b32<0>(xb);
+    o.xb[1] = lds_b32<4 * XLS>(xb);
+    o.xb[2] = lds_b32<8 * XLS>(xb);
+    o.xb[3] = lds_b32<12 * XLS>(xb);
   };
   if (t_beg < t_end) wgw_dma(a, t_beg, co0, ci0, tid, smem);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -271,17 +299,16 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
     const int cur = (tile - t_beg) & 1;
     const bool more = tile + 1 < t_end;
     if (more && EXP != 1) wgw_dma(a, tile + 1, co0, ci0, tid, smem + (cur ^ 1) * SLOT);
-    const float* slot = smem + (EXP == 1 ? 0 : cur * SLOT);
-    // operand reads run AHEAD steps in front of the MFMAs (ring of AHEAD + 1 operand sets)
-    WgwOps2 ops[AHEAD + 1];
-#pragma unroll
-    for (int s = 0; s < AHEAD; ++s) read(slot, s, ops[s]);
+    set_bases(smem + (EXP == 1 ? 0 : cur * SLOT));
+    WgwOps2 ops[2];
+    read(0, ops[0]);
 #pragma unroll
     for (int s = 0; s < NSTEP2; ++s) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // step s's operands (read one step ago)
       __builtin_amdgcn_sched_barrier(0);
-      if (s + AHEAD < NSTEP2) read(slot, s + AHEAD, ops[(s + AHEAD) % (AHEAD + 1)]);
+      if (s + 1 < NSTEP2) read(s + 1, ops[(s + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      const WgwOps2& o = ops[s % (AHEAD + 1)];
+      const WgwOps2& o = ops[s & 1];
       // Z row: r = alpha * dY[0] + beta * dY[1] (2 columns), then [r0, r0 + r1, r0 - r1, -r1]
       const float r0 = fmaf(beta, o.d[2], alpha * o.d[0]);
       const float r1 = fmaf(beta, o.d[3], alpha * o.d[1]);
@@ -298,6 +325,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc[k] = mfma_f32_32x32x2(z[k], v[k], acc[k]);
+      __builtin_amdgcn_sched_barrier(0);  // the next step's wait stays behind these MFMAs
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
@@ -404,10 +432,6 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
   PMU_REQUIRE(ws_bytes >= (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(a.nco * (Cin / WCI)), (unsigned)a.nsplit);
-  static const int ahead = [] {
-    const char* e = getenv("PMU_WGW_AHEAD");
-    return e ? atoi(e) : 2;
-  }();
   static const bool v16 = [] {
     const char* e = getenv("PMU_WGRAD_WINO");
     return e && strcmp(e, "16x16") == 0;
@@ -427,12 +451,8 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
 #endif
   if (v16)  // the 16x16x4 layout (all components per wave)
     hipLaunchKernelGGL((wgrad3x3_wino_kernel<0>), grid, dim3(NT), 0, st, a);
-  else if (ahead == 1)  // PMU_WGW_AHEAD=1|2|3: operand read-ahead depth in steps (A/B)
-    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0, 1>), grid, dim3(NT), 0, st, a);
-  else if (ahead == 3)
-    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0, 3>), grid, dim3(NT), 0, st, a);
   else
-    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0, 2>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   const long long CC = (long long)Cout * Cin;
   hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3((unsigned)((CC + 15) / 16)), dim3(256), 0, st, (const float*)ws,
