@@ -507,6 +507,16 @@ struct PipeArgs {
   int nnb, xcd;        // column blocks; 1: 1-D XCD-ordered grid, column blocks fastest
 };
 
+template <int OFF>
+__device__ __forceinline__ float4 ct_lds_b128(unsigned addr) {
+  float4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+__device__ __forceinline__ unsigned ct_lds_addr(const float* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(p);
+}
+
 template <bool DGRAD, int EXP = 0>
 __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
   __shared__ __attribute__((aligned(16))) float As[2][PM * PLS];
@@ -599,24 +609,40 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
   for (int c = 0; c < nch; ++c) {
     const int cur = c & 1;
     if (c + 1 < nch) PMU_TLOAD((c + 1) * PK)
-    float av[2][8], bv[2][8];
+    // the chunk's operands in two halves (k-steps 0-3, then 4-7), the second half's reads in flight
+    // under the first half's 16 MFMAs (one wait for all eight reads exposed the LDS latency)
+    // (explicit ds_read_b128 + waits: the compiler's own wait was one lgkmcnt(0) for all eight)
+    float4 av[2][2], bv[2][2];  // [half][fragment]
+    const unsigned aa = ct_lds_addr(&As[cur][(wm * 64 + (lane & 31)) * PLS + hsel]);
+    const unsigned ba = ct_lds_addr(&Bs[cur][(wn * 64 + (lane & 31)) * PLS + hsel]);
+    __builtin_amdgcn_sched_barrier(0);
+    av[0][0] = ct_lds_b128<0>(aa);
+    bv[0][0] = ct_lds_b128<0>(ba);
+    av[0][1] = ct_lds_b128<32 * PLS * 4>(aa);
+    bv[0][1] = ct_lds_b128<32 * PLS * 4>(ba);
+    av[1][0] = ct_lds_b128<16>(aa);
+    bv[1][0] = ct_lds_b128<16>(ba);
+    av[1][1] = ct_lds_b128<32 * PLS * 4 + 16>(aa);
+    bv[1][1] = ct_lds_b128<32 * PLS * 4 + 16>(ba);
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const float* pa = &As[cur][(wm * 64 + f * 32 + (lane & 31)) * PLS + hsel];
-      const float4 x0 = *reinterpret_cast<const float4*>(pa), x1 = *reinterpret_cast<const float4*>(pa + 4);
-      av[f][0] = x0.x; av[f][1] = x0.y; av[f][2] = x0.z; av[f][3] = x0.w;
-      av[f][4] = x1.x; av[f][5] = x1.y; av[f][6] = x1.z; av[f][7] = x1.w;
-      const float* pb = &Bs[cur][(wn * 64 + f * 32 + (lane & 31)) * PLS + hsel];
-      const float4 y0 = *reinterpret_cast<const float4*>(pb), y1 = *reinterpret_cast<const float4*>(pb + 4);
-      bv[f][0] = y0.x; bv[f][1] = y0.y; bv[f][2] = y0.z; bv[f][3] = y0.w;
-      bv[f][4] = y1.x; bv[f][5] = y1.y; bv[f][6] = y1.z; bv[f][7] = y1.w;
+    for (int hf = 0; hf < 2; ++hf) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (hf == 0) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < 2; ++fn) {
+            const float4 x = av[hf][fm], y = bv[hf][fn];
+            const float xa = s == 0 ? x.x : s == 1 ? x.y : s == 2 ? x.z : x.w;
+            const float yb = s == 0 ? y.x : s == 1 ? y.y : s == 2 ? y.z : y.w;
+            acc[fm][fn] = mfma_f32_32x32x2(xa, yb, acc[fm][fn]);
+          }
     }
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < 2; ++fn) acc[fm][fn] = mfma_f32_32x32x2(av[fm][s], bv[fn][s], acc[fm][fn]);
+    __builtin_amdgcn_sched_barrier(0);
     if (c + 1 < nch) PMU_TSTORE(cur ^ 1)
     __syncthreads();
   }
