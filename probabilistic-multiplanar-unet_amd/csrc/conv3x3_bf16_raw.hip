@@ -140,14 +140,15 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
   const uint4* wt = reinterpret_cast<const uint4*>(a.wp) + (long long)(j0 / BNT) * a.nch * B_UNITS +
                     ((tid >> 5) * 8 + (tid & 7)) * 4 + bq;
   uint4 ra0, ra1, ra2, ra3, ra4, ra5;                     // plain locals (no scratch)
+  unsigned kmask = 0u;                                    // A units in range (zeroed at commit)
   uint4 rb0, rb1, rb2, rb3, rb4, rb5, rb6, rb7, rb8;
   static_assert(NA <= 6 && NB <= 9, "staging register layout");
   // channel units past Cp (a partial last chunk) read as zero
 #define PMU_RA(I, R)                                                                               \
   if ((I) < NA) {                                                                                 \
     const bool k_ = ((okm >> (I)) & 1u) && k0_ + 8 * ((tid >> 3) & 3) < a.Cp;              \
-    const uint4 v_ = *reinterpret_cast<const uint4*>(a.x + (k_ ? (unsigned)(eo[I] + k0_) : 0u));  \
-    R = make_uint4(k_ ? v_.x : 0u, k_ ? v_.y : 0u, k_ ? v_.z : 0u, k_ ? v_.w : 0u);               \
+    R = *reinterpret_cast<const uint4*>(a.x + (k_ ? (unsigned)(eo[I] + k0_) : 0u));               \
+    kmask = k_ ? (kmask | (1u << (I))) : (kmask & ~(1u << (I)));                                  \
   }
 #define PMU_RB(I, R) \
   if ((I) < NB) R = s_[(B_UNITS % BMT == 0 || (I) + 1 < NB || tid + BMT * (I) < B_UNITS) ? BMT * (I) : 0];
@@ -160,8 +161,12 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
     PMU_RB(0, rb0) PMU_RB(1, rb1) PMU_RB(2, rb2) PMU_RB(3, rb3) PMU_RB(4, rb4)                    \
     PMU_RB(5, rb5) PMU_RB(6, rb6) PMU_RB(7, rb7) PMU_RB(8, rb8)                                   \
   }
-#define PMU_WA(I, R) \
-  if ((I) < NA && ((vm >> (I)) & 1u)) *reinterpret_cast<uint4*>(As + dsta[I]) = R;
+#define PMU_WA(I, R)                                                                               \
+  if ((I) < NA && ((vm >> (I)) & 1u)) {                                                           \
+    const bool k_ = (kmask >> (I)) & 1u; /* zeroed here, not at the load: no wait before the MFMAs */ \
+    *reinterpret_cast<uint4*>(As + dsta[I]) =                                                     \
+        make_uint4(k_ ? R.x : 0u, k_ ? R.y : 0u, k_ ? R.z : 0u, k_ ? R.w : 0u);                  \
+  }
 #define PMU_WB(I, R)                                                                               \
   if ((I) < NB && (B_UNITS % BMT == 0 || (I) + 1 < NB || tid + BMT * (I) < B_UNITS))               \
     *reinterpret_cast<uint4*>(Bs + (((tid + BMT * (I)) >> 5) * 8 + (tid & 7)) * LS + 8 * bq) = R;

@@ -59,9 +59,13 @@ __device__ __forceinline__ bf16x8 frag_of(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+// The next K tile rides in registers under the MFMAs.  Out-of-range units are zeroed when they are
+// STORED (okd / okx bit masks): zeroing them at load time made the compiler wait for the loads
+// right there (vmcnt before the MFMAs), exposing the whole global-load latency every tile.
 template <int WCO, int TWL>
 struct TileIO {
   uint4 d[Geo<WCO>::ND], x[Geo<WCO>::NX];
+  unsigned okd, okx;
 };
 
 template <int WCO, int TWL>
@@ -72,6 +76,8 @@ __device__ __forceinline__ void tile_load(const WgbArgs& a, int tile, int co0, i
   const int tw = t % a.tiles_w; t /= a.tiles_w;
   const int th = t % a.tiles_h; t /= a.tiles_h;
   const int n = t, h0 = th * TH, w0 = tw * TW;
+  r.okd = 0u;
+  r.okx = 0u;
 #pragma unroll
   for (int i = 0; i < G::ND; ++i) {
     const int u = tid + NT * i;
@@ -80,8 +86,8 @@ __device__ __forceinline__ void tile_load(const WgbArgs& a, int tile, int co0, i
     const int c = co0 + 8 * cu;
     const bool ok = (G::DU % NT == 0 || u < G::DU) && h < a.H && w < a.W && c < a.Cop;
     const long long idx = ok ? (((long long)n * a.H + h) * a.W + w) * a.Cop + c : 0;
-    const uint4 v = *reinterpret_cast<const uint4*>(a.dzt + idx);
-    r.d[i] = keep_if(ok, v);
+    r.d[i] = *reinterpret_cast<const uint4*>(a.dzt + idx);
+    r.okd |= ok ? (1u << i) : 0u;
   }
 #pragma unroll
   for (int i = 0; i < G::NX; ++i) {
@@ -92,8 +98,8 @@ __device__ __forceinline__ void tile_load(const WgbArgs& a, int tile, int co0, i
     const int c = ci0 + 8 * cu;
     const bool ok = u < HP * (WCI / 8) && h >= 0 && w >= 0 && h < a.H && w < a.W && c < a.Cip;
     const long long idx = ok ? (((long long)n * a.H + h) * a.W + w) * a.Cip + c : 0;
-    const uint4 v = *reinterpret_cast<const uint4*>(a.xt + idx);
-    r.x[i] = keep_if(ok, v);
+    r.x[i] = *reinterpret_cast<const uint4*>(a.xt + idx);
+    r.okx |= ok ? (1u << i) : 0u;
   }
 }
 
@@ -108,14 +114,14 @@ __device__ __forceinline__ void tile_store(const TileIO<WCO, TWL>& r, int tid, u
     const int u = tid + NT * i;
     if (G::DU % NT != 0 && u >= G::DU) continue;
     const int px = u / (WCO / 8), cu = u % (WCO / 8);
-    *reinterpret_cast<uint4*>(Ds + px * G::DS + 8 * cu) = r.d[i];
+    *reinterpret_cast<uint4*>(Ds + px * G::DS + 8 * cu) = keep_if((r.okd >> i) & 1u, r.d[i]);
   }
 #pragma unroll
   for (int i = 0; i < G::NX; ++i) {
     const int u = tid + NT * i;
     if (u >= HP * (WCI / 8)) continue;
     const int hp = u / (WCI / 8), cu = u % (WCI / 8);
-    *reinterpret_cast<uint4*>(Xs + hp * XS + 8 * cu) = r.x[i];
+    *reinterpret_cast<uint4*>(Xs + hp * XS + 8 * cu) = keep_if((r.okx >> i) & 1u, r.x[i]);
   }
 }
 
