@@ -117,6 +117,20 @@ int pmu_conv3x3_fwd_wino_raw(const float* xt, int Cin, int N, int H, int W, cons
                              int Cout, float* z, float* part, void* stream);
 int pmu_conv3x3_dgrad_wino_raw(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
                                int Csplit, float* dx0, float* dx1, void* stream);
+/* ---- fp32 Winograd F(4x4,3x3) on a materialised operand (images >= 32 x 32: the c2 fp32 default) --
+ * Replaces the same nn.Conv2d forward / input gradient (PMU/model/unet/unet_parts.py:15,18; autograd of
+ * PMU/model/unet/unet_model.py:31-54) as pmu_conv3x3_*_wino_raw: 36 per-component GEMMs of
+ * B^T d B (6x6 patches) and G g G^T, output A^T M A per 4x4 tile; fp32 rounding differs from the direct
+ * sum by a few 1e-6 relative.  xt / dzt [N][H][W][C] fp32 with C % 8 == 0; weights pre-transformed by
+ * pmu_conv3x3_pack_wino4 ([32 output rows][8 channels][36 components] blocks); part rows =
+ * pmu_conv3x3_tiles_wino4() (32 x 32 pixel blocks). */
+size_t pmu_conv3x3_packed_size_wino4(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_wino4(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream);
+int pmu_conv3x3_tiles_wino4(int N, int H, int W);
+int pmu_conv3x3_fwd_wino4(const float* xt, int Cin, int N, int H, int W, const float* wp, const float* bias,
+                          int Cout, float* z, float* part, void* stream);
+int pmu_conv3x3_dgrad_wino4(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                            int Csplit, float* dx0, float* dx1, void* stream);
 /* dw[Cout][Cin][3][3] from the teed operands dzt [N][H][W][Cout] and xt [N][H][W][Cin] (fp32), by
  * Winograd F(2x2,3x3): dw = G^T [sum over 2x2 tiles of (A dY A^T) .* (B^T X B)] G.  Cout % 32 == 0,
  * Cin % 64 == 0 (pmu_conv3x3_wgrad_ws_wino returns 0 otherwise); ws must hold that many bytes. */

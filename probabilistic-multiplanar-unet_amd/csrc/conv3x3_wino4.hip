@@ -1,0 +1,459 @@
+// 3x3 / pad 1 convolution in fp32 by Winograd F(4x4, 3x3) on f32 MFMA: the forward of nn.Conv2d at
+// PMU/model/unet/unet_parts.py:15,18 and its input gradient, on a materialised NHWC operand (the
+// tensor the weight gradient reads anyway), for images of at least 32 x 32 pixels.
+//
+// Every 4x4 block of output pixels ("tile") comes from the 6x6 operand patch d around it as
+//   Y = A^T [ (G g G^T) .* (B^T d B) ] A
+// i.e. 36 element-wise products per input/output channel pair for 16 outputs (2.25 per output, against
+// 4 for F(2x2,3x3) in conv3x3_wino.hip and 9 for the direct sum).  The reduction over input channels
+// becomes 36 independent GEMMs ("components")  M[c][tile][co] = sum_ci V[c][tile][ci] * U[c][ci][co].
+// All arithmetic is fp32 (points 0, +-1, +-2, inf; U computed in double and rounded once): the result
+// differs from the direct sum by rounding only (a few 1e-6 relative), far inside the 1e-3 parity bound.
+//
+// Block: 256 threads = 4 waves, one per SIMD (the 512-register file lets a wave hold 2 x 36 f32x4
+// accumulators), 64 tiles (8 x 8 -> a 32 x 32 output patch) x 32 output channels.  Wave w owns the
+// tiles of tile rows 2w, 2w+1 (lane & 15 -> tile) for both 16-channel halves of the 32 outputs: its
+// V (the transformed patch, the MFMA A operand) feeds two MFMAs, so the input transform costs two
+// VALU instructions per MFMA.  Per chunk of 8 input channels, double-buffered LDS stages receive the
+// 34 x 34 x 8 operand image and the chunk's U (8 ch x 32 co x 36 comps) by global_load_lds (LDS-DMA:
+// no registers, no VALU); each lane reads its tile's 6 x 6 patch for two channels as 36 ds_read_b64
+// (conflict-free: halo pixels in groups of 4 with a pad unit, rows of 312 floats) and runs two MFMA
+// steps (channel 2*kk + ks in k-slot kk = lane >> 4).
+// Epilogue: A^T M A per lane (+bias), BN partial sums per block (forward) or the split dx store.
+#include <string.h>
+#include <stdlib.h>
+#include <utility>
+#include "pmu_common.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TX = 8, TY = 8;                 // tiles per block
+constexpr int OW = 4 * TX, OH = 4 * TY;       // 32 x 32 output pixels
+constexpr int HW = OW + 2, HH = OH + 2;       // 34 x 34 halo
+constexpr int BK = 8;                         // input channels per chunk
+constexpr int GP = 36;                        // floats per group of 4 halo pixels (4 x 8 ch + 1 pad unit)
+constexpr int ROWF = 312;                     // floats per halo row: 8 groups + 2 px = 304, and 2*ROWF = 16 (mod 32) b64 units
+constexpr int ROWU = ROWF / 4;                // 16-B units per halo row
+constexpr int A_FLOATS = HH * ROWF;
+constexpr int CO = 32;                        // output channels per block
+constexpr int NC = 36;                        // Winograd components
+constexpr int U_FLOATS = BK * CO * NC;        // one chunk of transformed weights [ch 8][co 32][comp 36]
+constexpr int STAGE = A_FLOATS + U_FLOATS;
+constexpr int NT = 512;
+constexpr int A_UNITS = A_FLOATS / 4;
+constexpr int NGL = (A_UNITS + NT - 1) / NT;  // operand DMA instructions per thread per chunk
+constexpr int UGL = (U_FLOATS / 4 + NT - 1) / NT;  // U DMA rounds per chunk (the last one by waves 0-3)
+constexpr int RED_FLOATS = 8 * 16 * 2;
+static_assert(U_FLOATS % (4 * 256) == 0, "U of whole wave DMA instructions");
+static_assert((2 * STAGE + RED_FLOATS) * 4 <= 160 * 1024, "LDS");
+
+struct W4Args {
+  const float* x;     // [N][H][W][KC]
+  const float* wp;    // packed U [co block][chunk][ch 8][co 32][comp 36]
+  const float* bias;
+  float* out0;
+  float* out1;
+  float* part;        // [spatial blocks][2][NOUT] BN partial sums (fwd) or null
+  int H, W, KC, NOUT, split, bw, bh, nco, cpb;
+};
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// U = G g G^T, G = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1]
+__device__ __forceinline__ void g6(const double (&g)[3], double (&t)[6]) {
+  t[0] = g[0] / 4.0;
+  t[1] = -(g[0] + g[1] + g[2]) / 6.0;
+  t[2] = -(g[0] - g[1] + g[2]) / 6.0;
+  t[3] = g[0] / 24.0 + g[1] / 12.0 + g[2] / 6.0;
+  t[4] = g[0] / 24.0 - g[1] / 12.0 + g[2] / 6.0;
+  t[5] = g[2];
+}
+
+// one thread per (co block, chunk, channel, co) writes its 36 components as 9 float4
+__global__ void pack_wino4_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, float* __restrict__ wp) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  const int nch = (KC + BK - 1) / BK, ncob = (NOUT + CO - 1) / CO;
+  const long long total = (long long)ncob * nch * BK * CO;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int col = (int)(e % CO);
+    long long r = e / CO;
+    const int kl = (int)(r % BK); r /= BK;
+    const int ch = (int)(r % nch);
+    const int jb = (int)(r / nch);
+    const int j = jb * CO + col, k = ch * BK + kl;
+    double g[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        double v = 0.0;
+        if (j < NOUT && k < KC)  // dgrad: the input gradient convolves dz with w[co][ci] rotated by 180 degrees
+          v = dgrad ? w[((long long)k * Cin + j) * 9 + (2 - a) * 3 + (2 - b)] : w[((long long)j * Cin + k) * 9 + a * 3 + b];
+        g[a][b] = v;
+      }
+    double t[6][3];  // G g (columns)
+    for (int b = 0; b < 3; ++b) {
+      const double col3[3] = {g[0][b], g[1][b], g[2][b]};
+      double o[6];
+      g6(col3, o);
+      for (int a = 0; a < 6; ++a) t[a][b] = o[a];
+    }
+    float u[36];     // (G g) G^T
+    for (int a = 0; a < 6; ++a) {
+      const double row3[3] = {t[a][0], t[a][1], t[a][2]};
+      double o[6];
+      g6(row3, o);
+      for (int b = 0; b < 6; ++b) u[6 * a + b] = (float)o[b];
+    }
+    float* dst = wp + (((long long)jb * nch + ch) * BK + kl) * (CO * NC) + col * NC;
+    for (int q = 0; q < 9; ++q)
+      *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
+  }
+}
+
+// B^T row on d0..d5, B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+__device__ __forceinline__ void bt6(float d0, float d1, float d2, float d3, float d4, float d5, float& r0, float& r1,
+                                    float& r2, float& r3, float& r4, float& r5) {
+  r0 = fmaf(-5.f, d2, fmaf(4.f, d0, d4));
+  const float a = fmaf(-4.f, d2, d4), b = fmaf(-4.f, d1, d3);
+  r1 = a + b;
+  r2 = a - b;
+  const float c = d4 - d2, e = d3 - d1;
+  r3 = fmaf(2.f, e, c);
+  r4 = fmaf(-2.f, e, c);
+  r5 = fmaf(-5.f, d3, fmaf(4.f, d1, d5));
+}
+
+// V = B^T d B; v[6a + b]
+__device__ __forceinline__ void input_transform4(const float (&d)[36], float (&v)[36]) {
+  float t[36];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    bt6(d[j], d[6 + j], d[12 + j], d[18 + j], d[24 + j], d[30 + j], t[j], t[6 + j], t[12 + j], t[18 + j], t[24 + j],
+        t[30 + j]);
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+    bt6(t[6 * a], t[6 * a + 1], t[6 * a + 2], t[6 * a + 3], t[6 * a + 4], t[6 * a + 5], v[6 * a], v[6 * a + 1],
+        v[6 * a + 2], v[6 * a + 3], v[6 * a + 4], v[6 * a + 5]);
+}
+
+// A^T row on m0..m5, A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
+__device__ __forceinline__ void at4(float m0, float m1, float m2, float m3, float m4, float m5, float& y0, float& y1,
+                                    float& y2, float& y3) {
+  const float s12 = m1 + m2, d12 = m1 - m2, s34 = m3 + m4, d34 = m3 - m4;
+  y0 = m0 + s12 + s34;
+  y1 = fmaf(2.f, d34, d12);
+  y2 = fmaf(4.f, s34, s12);
+  y3 = fmaf(8.f, d34, d12) + m5;
+}
+
+template <int OFF>
+__device__ __forceinline__ float4 lds_b128(unsigned addr) {
+  float4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(p);
+}
+
+template <int OFF>
+__device__ __forceinline__ float lds_b32(unsigned addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+// patch element e (row e / 6, column e % 6) of this lane's tile: byte offset from the patch origin
+template <int E>
+struct PatchOff {
+  static constexpr int value = ((E / 6) * ROWF + ((E % 6) >> 2) * GP + ((E % 6) & 3) * 8) * 4;
+};
+// elements E0 .. E0+N-1 of the 6x6 patch of this lane's tile for one channel (ds_read_b32 each)
+template <int E0, int N>
+__device__ __forceinline__ void load_patch_part(unsigned pa, float (&d)[36]) {
+  if constexpr (N > 0) {
+    d[E0] = lds_b32<PatchOff<E0>::value>(pa);
+    load_patch_part<E0 + 1, N - 1>(pa, d);
+  }
+}
+// s_waitcnt lgkmcnt(N) (vmcnt / expcnt left at their maxima; gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt");
+  __builtin_amdgcn_s_waitcnt(0xC07F | (N << 8));
+}
+
+// epilogue: lane holds M[comp][tile 4*kk + r of the wave's group][co j0 + 16*hh + (lane & 15)] in acc[comp][r]
+template <bool DGRAD>
+__device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, int w0, int j0, int spatial,
+                                               f32x4 (&acc)[NC], float* red, float bias) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kk = lane >> 4;
+  const int tg = wave & 3, hh = wave >> 2;
+  const int j = j0 + 16 * hh + (lane & 15);
+  const bool jok = j < a.NOUT;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int t = 4 * kk + r;                    // tile within the group
+    const int oh = h0 + 4 * (2 * tg + (t >> 3)), ow = w0 + 4 * (t & 7);
+    float T[4][6];
+#pragma unroll
+    for (int b = 0; b < 6; ++b)
+      at4(acc[b][r], acc[6 + b][r], acc[12 + b][r], acc[18 + b][r], acc[24 + b][r], acc[30 + b][r], T[0][b], T[1][b],
+          T[2][b], T[3][b]);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float y[4];
+      at4(T[p][0], T[p][1], T[p][2], T[p][3], T[p][4], T[p][5], y[0], y[1], y[2], y[3]);
+      const int hh2 = oh + p;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ww = ow + q;
+        if (!jok || hh2 >= a.H || ww >= a.W) continue;
+        const float v = y[q] + bias;
+        const long long pix = ((long long)n * a.H + hh2) * a.W + ww;
+        if (!DGRAD) {
+          a.out0[pix * a.NOUT + j] = v;
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        } else if (j < a.split) {
+          a.out0[pix * a.split + j] = v;
+        } else {
+          a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+        }
+      }
+    }
+  }
+  if (!DGRAD && a.part) {
+    s1 += __shfl_xor(s1, 16, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (lane < 16) {
+      red[(wave * 16 + lane) * 2 + 0] = s1;
+      red[(wave * 16 + lane) * 2 + 1] = s2;
+    }
+    __syncthreads();
+    if (tid < CO) {  // channel tid: half tid >> 4, summed over the 4 tile groups (waves 4*half + tg) in order
+      const int jj = j0 + tid, hf = tid >> 4, l = tid & 15;
+      if (jj < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          t1 += red[((4 * hf + g) * 16 + l) * 2 + 0];
+          t2 += red[((4 * hf + g) * 16 + l) * 2 + 1];
+        }
+        a.part[((long long)spatial * 2 + 0) * a.NOUT + jj] = t1;
+        a.part[((long long)spatial * 2 + 1) * a.NOUT + jj] = t2;
+      }
+    }
+  }
+}
+
+// ---- one MFMA step (4 channels: channel 2*kk + KS in k-slot kk) of a wave -----------------------
+// LDS reads in issue order: the step's patch (36 x b32), U groups 0..2 (one b128 = 4 components each),
+// then U group g + 3 after group g's MFMAs.  Being asm, the reads get no compiler waits: group g waits
+// (lgkmcnt) for all but the reads issued after it (DS reads complete in order).
+template <int G>
+__device__ __forceinline__ void w4_uread(unsigned ua, float4 (&ur)[3]) {
+  ur[G % 3] = lds_b128<4 * G * 4>(ua);
+}
+
+template <int G>
+__device__ __forceinline__ void w4_group(unsigned ua, const float (&v)[36], float4 (&ur)[3], f32x4 (&acc)[NC]) {
+  if constexpr (G > 0) wait_lgkm<(G + 2 < 9 ? 2 : 8 - G)>();
+  __builtin_amdgcn_sched_barrier(0);
+  const float4 q = ur[G % 3];
+  acc[4 * G + 0] = mfma16(v[4 * G + 0], q.x, acc[4 * G + 0]);
+  acc[4 * G + 1] = mfma16(v[4 * G + 1], q.y, acc[4 * G + 1]);
+  acc[4 * G + 2] = mfma16(v[4 * G + 2], q.z, acc[4 * G + 2]);
+  acc[4 * G + 3] = mfma16(v[4 * G + 3], q.w, acc[4 * G + 3]);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (G + 3 < 9) w4_uread<G + 3>(ua, ur);
+}
+
+template <int... Gs>
+__device__ __forceinline__ void w4_groups(std::integer_sequence<int, Gs...>, unsigned ua, const float (&v)[36],
+                                          float4 (&ur)[3], f32x4 (&acc)[NC]) {
+  (w4_group<Gs>(ua, v, ur, acc), ...);
+}
+
+// pa = byte address of this lane's patch origin for the step's channel, ua = of its U row
+__device__ __forceinline__ void w4_step(unsigned pa, unsigned ua, f32x4 (&acc)[NC]) {
+  float d[36], v[36];
+  float4 ur[3];
+  load_patch_part<0, 36>(pa, d);
+  w4_uread<0>(ua, ur);
+  w4_uread<1>(ua, ur);
+  w4_uread<2>(ua, ur);
+  wait_lgkm<2>();  // the patch and U group 0
+  __builtin_amdgcn_sched_barrier(0);
+  input_transform4(d, v);
+  __builtin_amdgcn_sched_barrier(0);
+  w4_groups(std::make_integer_sequence<int, 9>{}, ua, v, ur, acc);
+}
+
+// A workgroup walks a.cpb output-channel blocks of one spatial block in passes; the flat
+// (pass, chunk) sequence is one DMA pipeline, so the next pass's first chunk lands under this
+// pass's last MFMAs.
+template <bool DGRAD>
+__global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
+  float* red = smem + 2 * STAGE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+  const int ncog = (a.nco + a.cpb - 1) / a.cpb;
+  const int cob0 = (lb % ncog) * a.cpb;
+  int sp = lb / ncog;
+  const int spatial = sp;
+  const int bx = sp % a.bw; sp /= a.bw;
+  const int by = sp % a.bh;
+  const int n = sp / a.bh;
+  const int h0 = by * OH, w0 = bx * OW;
+  const int KC = a.KC, nchunks = KC / BK;
+
+  // this thread's operand units: byte offset of chunk 0 (< 2^32, host-checked) and whether the unit
+  // is inside the input; units of the image outside it are zeroed in both stages once
+  unsigned goff[NGL];
+  unsigned gin = 0u;
+#pragma unroll
+  for (int r = 0; r < NGL; ++r) {
+    const int u = r * NT + tid;
+    const int hr = u / ROWU, wu = u - hr * ROWU;
+    const int g = wu / 9, w9 = wu - 9 * g;
+    const int px = 4 * g + (w9 >> 1);
+    const bool data = u < A_UNITS && w9 < 8 && px < HW;
+    const int h = h0 - 1 + hr, w = w0 - 1 + px;
+    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    goff[r] = in ? (unsigned)(((((long long)n * a.H + h) * a.W + w) * KC + 4 * (w9 & 1)) * 4) : 0u;
+    gin |= in ? (1u << r) : 0u;
+    if (data && !in) {
+      *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(smem + STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const int npass = a.cpb < a.nco - cob0 ? a.cpb : a.nco - cob0;
+  const int total = npass * nchunks;
+  const float* wsrc = a.wp + (long long)cob0 * nchunks * U_FLOATS;
+  const unsigned uoff = 16u * tid;
+  const int wave_off = wave * 256;
+#define PMU_GLDS(S, D)                                                                                      \
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
+                                   (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
+#define PMU_FETCH4(GI, BUF)                                                                                 \
+  {                                                                                                        \
+    const int p_ = (GI) / nchunks;                                                                         \
+    const int k0_ = ((GI) - p_ * nchunks) * BK;                                                            \
+    float* b_ = (BUF);                                                                                     \
+    const char* xb_ = reinterpret_cast<const char*>(a.x + k0_);                                            \
+    _Pragma("unroll") for (int r = 0; r < NGL; ++r)                                                        \
+      if ((gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                           \
+    const char* s_ = reinterpret_cast<const char*>(wsrc + (long long)(GI) * U_FLOATS) + uoff;              \
+    float* d_ = b_ + A_FLOATS + wave_off;                                                                  \
+    _Pragma("unroll") for (int r = 0; r < UGL; ++r)                                                        \
+      if (r * NT * 4 + (wave + 1) * 256 <= U_FLOATS) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)          \
+  }
+  const int t = lane & 15, kk = lane >> 4, tg = wave & 3, hh = wave >> 2;
+  const int pbase = 4 * (2 * tg + (t >> 3)) * ROWF + GP * (t & 7) + 2 * kk;
+  const int ubase = A_FLOATS + (2 * kk * CO + 16 * hh + t) * NC;
+  f32x4 acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  PMU_FETCH4(0, smem)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int p = 0; p < npass; ++p) {
+    const int j0 = (cob0 + p) * CO;
+    const int jb = j0 + 16 * hh + t;
+    const float bias = (!DGRAD && a.bias && jb < a.NOUT) ? a.bias[jb] : 0.f;
+    for (int ch = 0; ch < nchunks; ++ch) {
+      const int gi = p * nchunks + ch;
+      float* cur = smem + (gi & 1) * STAGE;
+      if (gi + 1 < total) PMU_FETCH4(gi + 1, smem + ((gi + 1) & 1) * STAGE)
+      const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
+      w4_step(pa, ua, acc);                          // channel 2*kk
+      w4_step(pa + 4, ua + CO * NC * 4, acc);        // channel 2*kk + 1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
+      __syncthreads();
+    }
+    // launder the block origin so the epilogue's address arithmetic is not hoisted out of the pass
+    // loop (it would be held, and spilled, across the MFMA loop)
+    int ne = n, h0e = h0, w0e = w0;
+    asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
+    wino4_epilogue<DGRAD>(a, ne, h0e, w0e, j0, spatial, acc, red, bias);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#undef PMU_FETCH4
+#undef PMU_GLDS
+}
+
+int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
+                 float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
+  PMU_REQUIRE(x && wp && out0 && KC > 0 && KC % BK == 0 && NOUT > 0 && N > 0 && H > 0 && W > 0);
+  PMU_REQUIRE((long long)N * H * W * KC * 4 < (1LL << 32));  // 32-bit DMA byte offsets
+  W4Args a;
+  memset(&a, 0, sizeof(a));
+  a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
+  a.H = H; a.W = W; a.KC = KC; a.NOUT = NOUT; a.split = split;
+  a.bw = pmu_cdiv(W, OW);
+  a.bh = pmu_cdiv(H, OH);
+  a.nco = pmu_cdiv(NOUT, CO);
+  const long long spatial = (long long)a.bw * a.bh * N;
+  // co-block passes per workgroup (the per-workgroup prologue is paid once per pass group) while
+  // keeping >= PMU_WINO4_MINWG workgroups; PMU_WINO4_CPB forces a value (A/B)
+  static const int cpb_env = [] {
+    const char* e = getenv("PMU_WINO4_CPB");
+    return e ? atoi(e) : 0;
+  }();
+  static const long long min_wg = [] {
+    const char* e = getenv("PMU_WINO4_MINWG");
+    return e ? atoll(e) : 512LL;
+  }();
+  int cpb = 1;
+  if (cpb_env > 0) {
+    cpb = cpb_env < a.nco ? cpb_env : a.nco;
+  } else {
+    while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= min_wg) cpb *= 2;
+  }
+  a.cpb = cpb;
+  const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
+  PMU_REQUIRE(blocks < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino4_kernel<false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+}  // namespace
+
+extern "C" int pmu_conv3x3_tiles_wino4(int N, int H, int W) { return N * pmu_cdiv(H, OH) * pmu_cdiv(W, OW); }
+
+extern "C" size_t pmu_conv3x3_packed_size_wino4(int Cout, int Cin, int dgrad) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  return (size_t)pmu_cdiv(NOUT, CO) * pmu_cdiv(KC, BK) * U_FLOATS * sizeof(float);
+}
+
+extern "C" int pmu_conv3x3_pack_wino4(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream) {
+  PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
+  const long long total = (long long)pmu_conv3x3_packed_size_wino4(Cout, Cin, dgrad) / sizeof(float) / NC;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(pack_wino4_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_conv3x3_fwd_wino4(const float* xt, int Cin, int N, int H, int W, const float* wp, const float* bias,
+                                     int Cout, float* z, float* part, void* stream) {
+  return launch_wino4(xt, Cin, N, H, W, wp, bias, Cout, z, nullptr, Cout, part, false, stream);
+}
+
+extern "C" int pmu_conv3x3_dgrad_wino4(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                                       int Csplit, float* dx0, float* dx1, void* stream) {
+  PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
+  return launch_wino4(dzt, Cout, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
+}

@@ -230,7 +230,16 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         Cin = sum(sr.C for sr in srcs)
         # the weight gradient reads the operand the kernel staged (RAW) instead of re-deriving it
         xt32 = _empty(N, H, W, Cin, device=dev) if keep and tee32_ok(Cin, Cout) else None
-        if use_wino():
+        if use_wino() and wino4_ok(Cin, H, W):
+            # F(4x4,3x3) on the materialised operand (images of >= 32 x 32)
+            R = lb.pmu_conv3x3_tiles_wino4(N, H, W)
+            part = _empty(R, 2 * Cout, device=dev) if need_stats else None
+            wp = pack_weights_wino4(conv.weight, dgrad=False)
+            xm = frame_to_f32(srcs, N, H, W)
+            L.call("pmu_conv3x3_fwd_wino4", xm.data_ptr(), Cin, N, H, W, wp.data_ptr(), L.ptr(conv.bias),
+                   Cout, z.data_ptr(), L.ptr(part), s)
+            xt32 = xm if xt32 is not None else None
+        elif use_wino():
             R = lb.pmu_conv3x3_tiles_wino(N, H, W)
             part = _empty(R, 2 * Cout, device=dev) if need_stats else None
             wp = pack_weights_wino(conv.weight, dgrad=False)
@@ -305,7 +314,13 @@ def _dgrad32(dz_src, conv, N, H, W, split, tee):
     dx0 = _empty(N, H, W, sp, device=dev)
     dx1 = _empty(N, H, W, Cin - sp, device=dev) if split is not None else None
     dzf = frame_of([dz_src], N, H, W)
-    if use_wino() and wino_raw_ok(Cout):
+    if use_wino() and wino4_ok(Cout, H, W):
+        dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
+        L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
+        wp = pack_weights_wino4(conv.weight, dgrad=True)
+        L.call("pmu_conv3x3_dgrad_wino4", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
+               L.ptr(dx1), s)
+    elif use_wino() and wino_raw_ok(Cout):
         dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
         L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
         wp = pack_weights_wino(conv.weight, dgrad=True)
@@ -421,6 +436,23 @@ def pack_weights_wino(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     wp = _empty(n, device=w.device)
     L.call("pmu_conv3x3_pack_wino", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
     return wp
+
+
+def pack_weights_wino4(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """F(4x4,3x3) weights U = G g G^T in the F(4x4) kernel's blocks (pmu_conv3x3_pack_wino4)."""
+    Cout, Cin = w.shape[0], w.shape[1]
+    n = L.lib().pmu_conv3x3_packed_size_wino4(Cout, Cin, int(dgrad)) // 4
+    wp = _empty(n, device=w.device)
+    L.call("pmu_conv3x3_pack_wino4", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
+def wino4_ok(C: int, H: int, W: int) -> bool:
+    """Winograd F(4x4,3x3) on a materialised operand (pmu_conv3x3_*_wino4): reduction channels C % 8 == 0
+    and images of at least 32 x 32 (its blocks are 32 x 32 output pixels; smaller maps keep F(2x2)).
+    PMU_WINO4=0 keeps F(2x2,3x3) everywhere (A/B)."""
+    return (C % 8 == 0 and H >= 32 and W >= 32 and os.environ.get("PMU_WINO4", "1") != "0"
+            and os.environ.get("PMU_FP32_CONV", "wino") == "wino")
 
 
 def use_wino() -> bool:
