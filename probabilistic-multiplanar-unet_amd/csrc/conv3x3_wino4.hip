@@ -63,6 +63,9 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// position of component c = 6a + b (half a / 3, local index cl = c - 18 (a / 3)) in a packed U row of 36
+constexpr int upos(int ch, int cl) { return cl < 16 ? 16 * ch + cl : 32 + 2 * ch + (cl - 16); }
+
 // U = G g G^T, G = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1]
 __device__ __forceinline__ void g6(const double (&g)[3], double (&t)[6]) {
   t[0] = g[0] / 4.0;
@@ -107,9 +110,11 @@ __global__ void pack_wino4_kernel(const float* __restrict__ w, int Cout, int Cin
       g6(row3, o);
       for (int b = 0; b < 6; ++b) u[6 * a + b] = (float)o[b];
     }
+    float row[36];   // the row in component-half order (upos)
+    for (int c = 0; c < 36; ++c) row[upos(c / 18, c % 18)] = u[c];
     float* dst = wp + (((long long)jb * nch + ch) * BK + kl) * (CO * NC) + col * NC;
     for (int q = 0; q < 9; ++q)
-      *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
+      *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
   }
 }
 
@@ -155,6 +160,12 @@ __device__ __forceinline__ float4 lds_b128(unsigned addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
   return v;
 }
+template <int OFF>
+__device__ __forceinline__ float2 lds_b64(unsigned addr) {
+  float2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
 __device__ __forceinline__ unsigned lds_addr(const float* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(p);
 }
@@ -185,43 +196,175 @@ __device__ __forceinline__ void wait_lgkm() {
   __builtin_amdgcn_s_waitcnt(0xC07F | (N << 8));
 }
 
-// epilogue: lane holds M[comp][tile 4*kk + r of the wave's group][co j0 + 16*hh + (lane & 15)] in acc[comp][r]
-template <bool DGRAD>
+// component c = 6a + b of the 6x6 grid belongs to half CH = a / 3 (local index cl = c - 18 CH); a packed
+// U row of 36 holds [half 0: cl 0..15 | half 1: cl 0..15 | half 0: cl 16,17 | half 1: cl 16,17], so a
+// half is 4 b128 + 1 b64 reads
+
+// the half CH of V = B^T d B: rows a = 3 CH .. 3 CH + 2 of the column pass, then their row pass;
+// v[6 a' + b], a' = a - 3 CH
+template <int CH>
+__device__ __forceinline__ void input_transform_half(const float (&d)[36], float (&v)[18]) {
+  float t[18];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const float d0 = d[j], d1 = d[6 + j], d2 = d[12 + j], d3 = d[18 + j], d4 = d[24 + j], d5 = d[30 + j];
+    if (CH == 0) {
+      t[j] = fmaf(-5.f, d2, fmaf(4.f, d0, d4));
+      const float a = fmaf(-4.f, d2, d4), b = fmaf(-4.f, d1, d3);
+      t[6 + j] = a + b;
+      t[12 + j] = a - b;
+    } else {
+      const float c = d4 - d2, e = d3 - d1;
+      t[j] = fmaf(2.f, e, c);
+      t[6 + j] = fmaf(-2.f, e, c);
+      t[12 + j] = fmaf(-5.f, d3, fmaf(4.f, d1, d5));
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    bt6(t[6 * a], t[6 * a + 1], t[6 * a + 2], t[6 * a + 3], t[6 * a + 4], t[6 * a + 5], v[6 * a], v[6 * a + 1],
+        v[6 * a + 2], v[6 * a + 3], v[6 * a + 4], v[6 * a + 5]);
+}
+
+// ---- one MFMA step (4 channels: channel 2*kk + ks in k-slot kk) of a wave -------------------------
+// The wave's 18 components x 2 co halves = 36 MFMAs in 5 groups (4 components each, the last 2).  LDS
+// reads in issue order: the step's patch (36 x b32), U groups 0..2 (one read per co half each), then
+// group g + 3 after group g's MFMAs.  Being asm, the reads get no compiler waits: group g waits
+// (lgkmcnt) for all but the reads issued after it (DS reads complete in order).
+template <int CH, int G>
+__device__ __forceinline__ void w4_uread(unsigned ua, float4 (&ur)[3][2], float2 (&ut)[2]) {
+  if constexpr (G < 4) {
+    ur[G % 3][0] = lds_b128<upos(CH, 4 * G) * 4>(ua);
+    ur[G % 3][1] = lds_b128<(16 * NC + upos(CH, 4 * G)) * 4>(ua);
+  } else {
+    ut[0] = lds_b64<upos(CH, 16) * 4>(ua);
+    ut[1] = lds_b64<(16 * NC + upos(CH, 16)) * 4>(ua);
+  }
+}
+
+template <int CH, int G>
+__device__ __forceinline__ void w4_group(unsigned ua, const float (&v)[18], float4 (&ur)[3][2], float2 (&ut)[2],
+                                         f32x4 (&acc)[2][18]) {
+  if constexpr (G > 0) wait_lgkm<2 * ((G + 2 < 4 ? G + 2 : 4) - G)>();
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (G < 4) {
+    constexpr int c0 = 4 * G;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 q = ur[G % 3][h];
+      acc[h][c0 + 0] = mfma16(v[c0 + 0], q.x, acc[h][c0 + 0]);
+      acc[h][c0 + 1] = mfma16(v[c0 + 1], q.y, acc[h][c0 + 1]);
+      acc[h][c0 + 2] = mfma16(v[c0 + 2], q.z, acc[h][c0 + 2]);
+      acc[h][c0 + 3] = mfma16(v[c0 + 3], q.w, acc[h][c0 + 3]);
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      acc[h][16] = mfma16(v[16], ut[h].x, acc[h][16]);
+      acc[h][17] = mfma16(v[17], ut[h].y, acc[h][17]);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (G + 3 <= 4) w4_uread<CH, G + 3>(ua, ur, ut);
+}
+
+// pa = byte address of this lane's patch origin for the step's channel, ua = of its U row (co half 0)
+template <int CH>
+__device__ __forceinline__ void w4_step(unsigned pa, unsigned ua, f32x4 (&acc)[2][18]) {
+  float d[36], v[18];
+  float4 ur[3][2];
+  float2 ut[2];
+  load_patch_part<0, 36>(pa, d);
+  w4_uread<CH, 0>(ua, ur, ut);
+  w4_uread<CH, 1>(ua, ur, ut);
+  w4_uread<CH, 2>(ua, ur, ut);
+  wait_lgkm<4>();  // the patch and U group 0
+  __builtin_amdgcn_sched_barrier(0);
+  input_transform_half<CH>(d, v);
+  __builtin_amdgcn_sched_barrier(0);
+  w4_group<CH, 0>(ua, v, ur, ut, acc);
+  w4_group<CH, 1>(ua, v, ur, ut, acc);
+  w4_group<CH, 2>(ua, v, ur, ut, acc);
+  w4_group<CH, 3>(ua, v, ur, ut, acc);
+  w4_group<CH, 4>(ua, v, ur, ut, acc);
+}
+
+// this half's share of Y = A^T M A for tile r of co half h: P[4p + q] = sum over the half's rows a of
+// A^T[p][a] (M[a][:] A)[q]
+template <int CH>
+__device__ __forceinline__ void w4_partial(const f32x4 (&acc)[2][18], int h, int r, float (&P)[16]) {
+  float R[3][4];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    at4(acc[h][6 * a][r], acc[h][6 * a + 1][r], acc[h][6 * a + 2][r], acc[h][6 * a + 3][r], acc[h][6 * a + 4][r],
+        acc[h][6 * a + 5][r], R[a][0], R[a][1], R[a][2], R[a][3]);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (CH == 0) {  // A^T columns 0..2: (1,0,0,0), (1,1,1,1), (1,-1,1,-1)
+      const float s = R[1][q] + R[2][q], df = R[1][q] - R[2][q];
+      P[q] = R[0][q] + s;
+      P[4 + q] = df;
+      P[8 + q] = s;
+      P[12 + q] = df;
+    } else {        // A^T columns 3..5: (1,2,4,8), (1,-2,4,-8), (0,0,0,1)
+      const float s = R[0][q] + R[1][q], df = R[0][q] - R[1][q];
+      P[q] = s;
+      P[4 + q] = 2.f * df;
+      P[8 + q] = 4.f * s;
+      P[12 + q] = fmaf(8.f, df, R[2][q]);
+    }
+  }
+}
+
+// epilogue: lane holds M[comp (half CH)][tile 4*kk + r of the wave's group][co j0 + 16 h + (lane & 15)]
+// in acc[h][cl][r].  The two waves of a tile group (halves 0 and 1) swap the partial outputs of the
+// co half the other one finishes through xb (a free LDS stage), in two rounds of two tiles per lane;
+// wave (tg, CH) then finishes co half CH: bias, store, BN partial sums.
+template <bool DGRAD, int CH>
 __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, int w0, int j0, int spatial,
-                                               f32x4 (&acc)[NC], float* red, float bias) {
+                                               const f32x4 (&acc)[2][18], float* xb, float* red, float bias) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kk = lane >> 4;
-  const int tg = wave & 3, hh = wave >> 2;
-  const int j = j0 + 16 * hh + (lane & 15);
+  const int tg = wave & 3, partner = tg + 4 * (1 - CH);
+  const int j = j0 + 16 * CH + (lane & 15);
   const bool jok = j < a.NOUT;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int t = 4 * kk + r;                    // tile within the group
-    const int oh = h0 + 4 * (2 * tg + (t >> 3)), ow = w0 + 4 * (t & 7);
-    float T[4][6];
+  for (int rho = 0; rho < 2; ++rho) {
+    if (rho) __syncthreads();  // round 0's reads are done before xb is rewritten
 #pragma unroll
-    for (int b = 0; b < 6; ++b)
-      at4(acc[b][r], acc[6 + b][r], acc[12 + b][r], acc[18 + b][r], acc[24 + b][r], acc[30 + b][r], T[0][b], T[1][b],
-          T[2][b], T[3][b]);
+    for (int rr = 0; rr < 2; ++rr) {
+      float P[16];
+      w4_partial<CH>(acc, 1 - CH, 2 * rho + rr, P);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      float y[4];
-      at4(T[p][0], T[p][1], T[p][2], T[p][3], T[p][4], T[p][5], y[0], y[1], y[2], y[3]);
-      const int hh2 = oh + p;
+      for (int e = 0; e < 16; ++e) xb[((wave * 2 + rr) * 16 + e) * 64 + lane] = P[e];
+    }
+    __syncthreads();
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ww = ow + q;
-        if (!jok || hh2 >= a.H || ww >= a.W) continue;
-        const float v = y[q] + bias;
-        const long long pix = ((long long)n * a.H + hh2) * a.W + ww;
-        if (!DGRAD) {
-          a.out0[pix * a.NOUT + j] = v;
-          s1 += v;
-          s2 = fmaf(v, v, s2);
-        } else if (j < a.split) {
-          a.out0[pix * a.split + j] = v;
-        } else {
-          a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+    for (int rr = 0; rr < 2; ++rr) {
+      const int r = 2 * rho + rr;
+      float P[16];
+      w4_partial<CH>(acc, CH, r, P);
+      const int t = 4 * kk + r;  // tile within the group
+      const int oh = h0 + 4 * (2 * tg + (t >> 3)), ow = w0 + 4 * (t & 7);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int hh2 = oh + p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ww = ow + q;
+          const float y = P[4 * p + q] + xb[((partner * 2 + rr) * 16 + 4 * p + q) * 64 + lane];
+          if (!jok || hh2 >= a.H || ww >= a.W) continue;
+          const float v = y + bias;
+          const long long pix = ((long long)n * a.H + hh2) * a.W + ww;
+          if (!DGRAD) {
+            a.out0[pix * a.NOUT + j] = v;
+            s1 += v;
+            s2 = fmaf(v, v, s2);
+          } else if (j < a.split) {
+            a.out0[pix * a.split + j] = v;
+          } else {
+            a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+          }
         }
       }
     }
@@ -250,95 +393,26 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
       }
     }
   }
+  __syncthreads();  // the exchange reads are done before the next pass's DMA refills xb's stage
 }
 
-// ---- one MFMA step (4 channels: channel 2*kk + KS in k-slot kk) of a wave -----------------------
-// LDS reads in issue order: the step's patch (36 x b32), U groups 0..2 (one b128 = 4 components each),
-// then U group g + 3 after group g's MFMAs.  Being asm, the reads get no compiler waits: group g waits
-// (lgkmcnt) for all but the reads issued after it (DS reads complete in order).
-template <int G>
-__device__ __forceinline__ void w4_uread(unsigned ua, float4 (&ur)[3]) {
-  ur[G % 3] = lds_b128<4 * G * 4>(ua);
-}
+struct W4Block {
+  int n, h0, w0, cob0, spatial, nchunks, npass;
+  unsigned gin;    // operand units inside the input (DMA'd)
+  unsigned gzero;  // image units outside it (zero, written once; restored after an exchange in their stage)
+};
 
-template <int G>
-__device__ __forceinline__ void w4_group(unsigned ua, const float (&v)[36], float4 (&ur)[3], f32x4 (&acc)[NC]) {
-  if constexpr (G > 0) wait_lgkm<(G + 2 < 9 ? 2 : 8 - G)>();
-  __builtin_amdgcn_sched_barrier(0);
-  const float4 q = ur[G % 3];
-  acc[4 * G + 0] = mfma16(v[4 * G + 0], q.x, acc[4 * G + 0]);
-  acc[4 * G + 1] = mfma16(v[4 * G + 1], q.y, acc[4 * G + 1]);
-  acc[4 * G + 2] = mfma16(v[4 * G + 2], q.z, acc[4 * G + 2]);
-  acc[4 * G + 3] = mfma16(v[4 * G + 3], q.w, acc[4 * G + 3]);
-  __builtin_amdgcn_sched_barrier(0);
-  if constexpr (G + 3 < 9) w4_uread<G + 3>(ua, ur);
-}
-
-template <int... Gs>
-__device__ __forceinline__ void w4_groups(std::integer_sequence<int, Gs...>, unsigned ua, const float (&v)[36],
-                                          float4 (&ur)[3], f32x4 (&acc)[NC]) {
-  (w4_group<Gs>(ua, v, ur, acc), ...);
-}
-
-// pa = byte address of this lane's patch origin for the step's channel, ua = of its U row
-__device__ __forceinline__ void w4_step(unsigned pa, unsigned ua, f32x4 (&acc)[NC]) {
-  float d[36], v[36];
-  float4 ur[3];
-  load_patch_part<0, 36>(pa, d);
-  w4_uread<0>(ua, ur);
-  w4_uread<1>(ua, ur);
-  w4_uread<2>(ua, ur);
-  wait_lgkm<2>();  // the patch and U group 0
-  __builtin_amdgcn_sched_barrier(0);
-  input_transform4(d, v);
-  __builtin_amdgcn_sched_barrier(0);
-  w4_groups(std::make_integer_sequence<int, 9>{}, ua, v, ur, acc);
-}
-
-// A workgroup walks a.cpb output-channel blocks of one spatial block in passes; the flat
-// (pass, chunk) sequence is one DMA pipeline, so the next pass's first chunk lands under this
-// pass's last MFMAs.
-template <bool DGRAD>
-__global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
+// the pass / chunk pipeline of a wave of component half CH (waves 4 CH .. 4 CH + 3)
+template <bool DGRAD, int CH>
+__device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, const unsigned (&goff)[NGL],
+                                           float* smem) {
   float* red = smem + 2 * STAGE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
-  const int ncog = (a.nco + a.cpb - 1) / a.cpb;
-  const int cob0 = (lb % ncog) * a.cpb;
-  int sp = lb / ncog;
-  const int spatial = sp;
-  const int bx = sp % a.bw; sp /= a.bw;
-  const int by = sp % a.bh;
-  const int n = sp / a.bh;
-  const int h0 = by * OH, w0 = bx * OW;
-  const int KC = a.KC, nchunks = KC / BK;
-
-  // this thread's operand units: byte offset of chunk 0 (< 2^32, host-checked) and whether the unit
-  // is inside the input; units of the image outside it are zeroed in both stages once
-  unsigned goff[NGL];
-  unsigned gin = 0u;
-#pragma unroll
-  for (int r = 0; r < NGL; ++r) {
-    const int u = r * NT + tid;
-    const int hr = u / ROWU, wu = u - hr * ROWU;
-    const int g = wu / 9, w9 = wu - 9 * g;
-    const int px = 4 * g + (w9 >> 1);
-    const bool data = u < A_UNITS && w9 < 8 && px < HW;
-    const int h = h0 - 1 + hr, w = w0 - 1 + px;
-    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
-    goff[r] = in ? (unsigned)(((((long long)n * a.H + h) * a.W + w) * KC + 4 * (w9 & 1)) * 4) : 0u;
-    gin |= in ? (1u << r) : 0u;
-    if (data && !in) {
-      *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(smem + STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-  const int npass = a.cpb < a.nco - cob0 ? a.cpb : a.nco - cob0;
-  const int total = npass * nchunks;
-  const float* wsrc = a.wp + (long long)cob0 * nchunks * U_FLOATS;
+  const int nchunks = B.nchunks, total = B.npass * nchunks;
+  const float* wsrc = a.wp + (long long)B.cob0 * nchunks * U_FLOATS;
   const unsigned uoff = 16u * tid;
   const int wave_off = wave * 256;
+  const unsigned gin = B.gin;
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
                                    (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
@@ -355,40 +429,102 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
     _Pragma("unroll") for (int r = 0; r < UGL; ++r)                                                        \
       if (r * NT * 4 + (wave + 1) * 256 <= U_FLOATS) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)          \
   }
-  const int t = lane & 15, kk = lane >> 4, tg = wave & 3, hh = wave >> 2;
+  const int t = lane & 15, kk = lane >> 4, tg = wave & 3;
   const int pbase = 4 * (2 * tg + (t >> 3)) * ROWF + GP * (t & 7) + 2 * kk;
-  const int ubase = A_FLOATS + (2 * kk * CO + 16 * hh + t) * NC;
-  f32x4 acc[NC];
+  const int ubase = A_FLOATS + (2 * kk * CO + t) * NC;
+  f32x4 acc[2][18];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int c = 0; c < 18; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   PMU_FETCH4(0, smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int p = 0; p < npass; ++p) {
-    const int j0 = (cob0 + p) * CO;
-    const int jb = j0 + 16 * hh + t;
+  for (int p = 0; p < B.npass; ++p) {
+    const int j0 = (B.cob0 + p) * CO;
+    const int jb = j0 + 16 * CH + t;
     const float bias = (!DGRAD && a.bias && jb < a.NOUT) ? a.bias[jb] : 0.f;
-    for (int ch = 0; ch < nchunks; ++ch) {
-      const int gi = p * nchunks + ch;
+    int gi = p * nchunks;
+    for (int ch = 0; ch < nchunks; ++ch, ++gi) {
       float* cur = smem + (gi & 1) * STAGE;
       if (gi + 1 < total) PMU_FETCH4(gi + 1, smem + ((gi + 1) & 1) * STAGE)
       const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
-      w4_step(pa, ua, acc);                          // channel 2*kk
-      w4_step(pa + 4, ua + CO * NC * 4, acc);        // channel 2*kk + 1
+      w4_step<CH>(pa, ua, acc);                          // channel 2*kk
+      w4_step<CH>(pa + 4, ua + CO * NC * 4, acc);        // channel 2*kk + 1
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
       __syncthreads();
     }
     // launder the block origin so the epilogue's address arithmetic is not hoisted out of the pass
     // loop (it would be held, and spilled, across the MFMA loop)
-    int ne = n, h0e = h0, w0e = w0;
+    int ne = B.n, h0e = B.h0, w0e = B.w0;
     asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
-    wino4_epilogue<DGRAD>(a, ne, h0e, w0e, j0, spatial, acc, red, bias);
+    float* xb = smem + ((gi - 1) & 1) * STAGE;
+    wino4_epilogue<DGRAD, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    if (p + 1 < B.npass && B.gzero) {
+      // the exchange overwrote xb's stage: restore its zero units before the next pass DMAs into it
 #pragma unroll
-    for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < NGL; ++r)
+        if ((B.gzero >> r) & 1u) *reinterpret_cast<float4*>(xb + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int c = 0; c < 18; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #undef PMU_FETCH4
 #undef PMU_GLDS
+}
+
+// A workgroup walks a.cpb output-channel blocks of one spatial block in passes; the flat
+// (pass, chunk) sequence is one DMA pipeline, so the next pass's first chunk lands under this
+// pass's epilogue.  Waves 0-3 compute components 0..17 (rows 0-2 of the 6x6 grid), waves 4-7 the
+// rest, each for its tile group's 16 tiles x all 32 output channels.
+template <bool DGRAD>
+__global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
+  const int tid = threadIdx.x;
+  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+  const int ncog = (a.nco + a.cpb - 1) / a.cpb;
+  W4Block B;
+  B.cob0 = (lb % ncog) * a.cpb;
+  int sp = lb / ncog;
+  B.spatial = sp;
+  const int bx = sp % a.bw; sp /= a.bw;
+  const int by = sp % a.bh;
+  B.n = sp / a.bh;
+  B.h0 = by * OH;
+  B.w0 = bx * OW;
+  const int KC = a.KC;
+  B.nchunks = KC / BK;
+  B.npass = a.cpb < a.nco - B.cob0 ? a.cpb : a.nco - B.cob0;
+
+  // this thread's operand units: byte offset of chunk 0 (< 2^32, host-checked) and whether the unit
+  // is inside the input; units of the image outside it are zeroed in both stages once
+  unsigned goff[NGL];
+  unsigned gin = 0u, gzero = 0u;
+#pragma unroll
+  for (int r = 0; r < NGL; ++r) {
+    const int u = r * NT + tid;
+    const int hr = u / ROWU, wu = u - hr * ROWU;
+    const int g = wu / 9, w9 = wu - 9 * g;
+    const int px = 4 * g + (w9 >> 1);
+    const bool data = u < A_UNITS && w9 < 8 && px < HW;
+    const int h = B.h0 - 1 + hr, w = B.w0 - 1 + px;
+    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    goff[r] = in ? (unsigned)(((((long long)B.n * a.H + h) * a.W + w) * KC + 4 * (w9 & 1)) * 4) : 0u;
+    gin |= in ? (1u << r) : 0u;
+    gzero |= (data && !in) ? (1u << r) : 0u;
+    if (data && !in) {
+      *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(smem + STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  B.gin = gin;
+  B.gzero = gzero;
+  if (tid >> 8) wino4_main<DGRAD, 1>(a, B, goff, smem);
+  else wino4_main<DGRAD, 0>(a, B, goff, smem);
 }
 
 int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
