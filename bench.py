@@ -70,13 +70,19 @@ class KernelTimer:
             "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16", "pmu_convT2x2_fwd_bf16",
             "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16",
             "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino", "pmu_conv3x3_wgrad_wino",
-            "pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw")
+            "pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw", "pmu_conv3x3_fwd_wino4",
+            "pmu_conv3x3_dgrad_wino4")
 
     def __init__(self):
         self.rec = []
 
     @staticmethod
     def _flops(name, args):
+        if name in ("pmu_conv3x3_fwd_wino4", "pmu_conv3x3_dgrad_wino4"):
+            # Winograd F(4x4,3x3): 36 products per 4x4 output tile per channel pair
+            cin, N, H, W = args[1], args[2], args[3], args[4]
+            nout = args[7] if name.startswith("pmu_conv3x3_fwd") else args[6]
+            return 2.0 * 36 * N * ((H + 3) // 4) * ((W + 3) // 4) * cin * nout
         if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw"):
             cin, N, H, W = args[1], args[2], args[3], args[4]
             nout = args[7] if name.startswith("pmu_conv3x3_fwd") else args[6]
@@ -142,6 +148,9 @@ class KernelTimer:
         products per 2x2 output tile and channel pair where the direct sum takes 9 per pixel."""
         if "_wino" not in name or not fl:
             return fl
+        if name.endswith("_wino4"):
+            H, W = args[3], args[4]
+            return fl * (9.0 * H * W) / (36.0 * ((H + 3) // 4) * ((W + 3) // 4))
         if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw"):
             H, W = args[3], args[4]
         elif name == "pmu_conv3x3_wgrad_wino":
@@ -304,6 +313,7 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_wgrad": r"wgrad3x3_kernel<",
     "pmu_conv3x3_fwd_wino": r"conv3x3_wino_(pipe_)?kernel<false", "pmu_conv3x3_dgrad_wino": r"conv3x3_wino_(pipe_)?kernel<true",
     "pmu_conv3x3_wgrad_wino": (r"wgrad3x3_wino(32)?_kernel", r"wgrad_wino_reduce_kernel"),
+    "pmu_conv3x3_fwd_wino4": r"conv3x3_wino4_kernel<false", "pmu_conv3x3_dgrad_wino4": r"conv3x3_wino4_kernel<true",
     "pmu_conv3x3_fwd_wino_raw": r"conv3x3_wino_raw_kernel<false", "pmu_conv3x3_dgrad_wino_raw": r"conv3x3_wino_raw_kernel<true", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
     "pmu_convT2x2_dgrad": r"convT_pipe_kernel<true>|DuGatherA",
     "pmu_convT2x2_wgrad": r"convT_wgrad_(pipe_)?kernel", "pmu_fcomb_fwd": r"fcomb_fwd_kernel",
@@ -666,11 +676,15 @@ def main():
         if "_wino" in dom:  # Winograd executes 16 of the direct sum's 36 products per 2x2 tile
             roof["flops_basis"] = ("executed Winograd F(2x2,3x3) MFMA products (16 per 2x2 output tile per "
                                    "channel pair); frac is MFMA utilisation")
+            if dom.endswith("_wino4"):
+                roof["flops_basis"] = ("executed Winograd F(4x4,3x3) MFMA products (36 per 4x4 output tile per "
+                                       "channel pair); frac is MFMA utilisation")
             roof["direct_sum_flops_per_launch"] = dfl / n
             roof["direct_sum_equiv_tflops"] = round(dfl / t / 1e12, 2)
             roof["direct_sum_equiv_frac"] = round(dfl / t / 1e12 / peak, 4)
             roof["direct_sum_note"] = ("SURVEY.md §8(d) basis (9 MACs per pixel per channel pair): >1 is possible "
-                                       "because Winograd executes 16/36 of those products; not a utilisation")
+                                       "because Winograd executes 16/36 (F(2x2)) or 36/144 (F(4x4)) of those "
+                                       "products; not a utilisation")
         kernels = {k: {"launches": v[0], "ms": round(v[2] * 1e3, 3),
                        "tflops": (round(v[1] / v[2] / 1e12, 2) if v[1] else None)} for k, v in sorted(per.items())}
         # executed MFMA work of the step at each kernel's own peak, over the step time: the MFMA-busy

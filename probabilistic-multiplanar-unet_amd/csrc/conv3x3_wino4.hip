@@ -461,8 +461,9 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
     asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
     float* xb = smem + ((gi - 1) & 1) * STAGE;
     wino4_epilogue<DGRAD, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
-    if (p + 1 < B.npass && B.gzero) {
-      // the exchange overwrote xb's stage: restore its zero units before the next pass DMAs into it
+    if (p + 1 < B.npass) {  // block-uniform: every wave takes the barrier
+      // the exchange overwrote xb's stage: restore its zero units (each thread its own) before the
+      // next pass reads it
 #pragma unroll
       for (int r = 0; r < NGL; ++r)
         if ((B.gzero >> r) & 1u) *reinterpret_cast<float4*>(xb + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f);
