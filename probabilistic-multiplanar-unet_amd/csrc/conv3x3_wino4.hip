@@ -57,6 +57,7 @@ struct W4Args {
   float* out1;
   float* part;        // [spatial blocks][2][NOUT] BN partial sums (fwd) or null
   int H, W, KC, NOUT, split, bw, bh, nco, cpb;
+  int prio;           // 1: waves of component half 1 run at s_setprio 1 (PMU_WINO4_PRIO)
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -242,10 +243,12 @@ __device__ __forceinline__ void w4_uread(unsigned ua, float4 (&ur)[3][2], float2
   }
 }
 
-template <int CH, int G>
+// PF: the next step's patch (channel +1) is read during this step's last two groups (12 + 24 reads,
+// after the U reads: the counted waits stay <= 15), so the next step starts on landed data.
+template <int CH, int G, bool PF>
 __device__ __forceinline__ void w4_group(unsigned ua, const float (&v)[18], float4 (&ur)[3][2], float2 (&ut)[2],
-                                         f32x4 (&acc)[2][18]) {
-  if constexpr (G > 0) wait_lgkm<2 * ((G + 2 < 4 ? G + 2 : 4) - G)>();
+                                         f32x4 (&acc)[2][18], unsigned pn, float (&dn)[36]) {
+  if constexpr (G > 0) wait_lgkm<(PF && G == 4) ? 12 : 2 * ((G + 2 < 4 ? G + 2 : 4) - G)>();
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (G < 4) {
     constexpr int c0 = 4 * G;
@@ -266,11 +269,15 @@ __device__ __forceinline__ void w4_group(unsigned ua, const float (&v)[18], floa
   }
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (G + 3 <= 4) w4_uread<CH, G + 3>(ua, ur, ut);
+  if constexpr (PF && G == 3) load_patch_part<0, 12>(pn, dn);
+  if constexpr (PF && G == 4) load_patch_part<12, 24>(pn, dn);
 }
 
-// pa = byte address of this lane's patch origin for the step's channel, ua = of its U row (co half 0)
-template <int CH>
-__device__ __forceinline__ void w4_step(unsigned pa, unsigned ua, f32x4 (&acc)[2][18]) {
+// One chunk (two MFMA steps: channels 2*kk and 2*kk + 1).  pa = byte address of this lane's patch
+// origin (channel 2*kk), ua = of its U row (channel 2*kk, co half 0).  PF: step 1's patch is read
+// during step 0's MFMAs instead of after them.
+template <int CH, bool PF>
+__device__ __forceinline__ void w4_chunk(unsigned pa, unsigned ua, f32x4 (&acc)[2][18]) {
   float d[36], v[18];
   float4 ur[3][2];
   float2 ut[2];
@@ -282,11 +289,25 @@ __device__ __forceinline__ void w4_step(unsigned pa, unsigned ua, f32x4 (&acc)[2
   __builtin_amdgcn_sched_barrier(0);
   input_transform_half<CH>(d, v);
   __builtin_amdgcn_sched_barrier(0);
-  w4_group<CH, 0>(ua, v, ur, ut, acc);
-  w4_group<CH, 1>(ua, v, ur, ut, acc);
-  w4_group<CH, 2>(ua, v, ur, ut, acc);
-  w4_group<CH, 3>(ua, v, ur, ut, acc);
-  w4_group<CH, 4>(ua, v, ur, ut, acc);
+  const unsigned pa1 = pa + 4, ua1 = ua + CO * NC * 4;
+  w4_group<CH, 0, PF>(ua, v, ur, ut, acc, pa1, d);
+  w4_group<CH, 1, PF>(ua, v, ur, ut, acc, pa1, d);
+  w4_group<CH, 2, PF>(ua, v, ur, ut, acc, pa1, d);
+  w4_group<CH, 3, PF>(ua, v, ur, ut, acc, pa1, d);
+  w4_group<CH, 4, PF>(ua, v, ur, ut, acc, pa1, d);
+  if constexpr (!PF) load_patch_part<0, 36>(pa1, d);
+  w4_uread<CH, 0>(ua1, ur, ut);
+  w4_uread<CH, 1>(ua1, ur, ut);
+  w4_uread<CH, 2>(ua1, ur, ut);
+  wait_lgkm<4>();  // step 1's patch and U group 0
+  __builtin_amdgcn_sched_barrier(0);
+  input_transform_half<CH>(d, v);
+  __builtin_amdgcn_sched_barrier(0);
+  w4_group<CH, 0, false>(ua1, v, ur, ut, acc, pa1, d);
+  w4_group<CH, 1, false>(ua1, v, ur, ut, acc, pa1, d);
+  w4_group<CH, 2, false>(ua1, v, ur, ut, acc, pa1, d);
+  w4_group<CH, 3, false>(ua1, v, ur, ut, acc, pa1, d);
+  w4_group<CH, 4, false>(ua1, v, ur, ut, acc, pa1, d);
 }
 
 // this half's share of Y = A^T M A for tile r of co half h: P[4p + q] = sum over the half's rows a of
@@ -403,7 +424,7 @@ struct W4Block {
 };
 
 // the pass / chunk pipeline of a wave of component half CH (waves 4 CH .. 4 CH + 3)
-template <bool DGRAD, int CH>
+template <bool DGRAD, int CH, bool PF>
 __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, const unsigned (&goff)[NGL],
                                            float* smem) {
   float* red = smem + 2 * STAGE;
@@ -450,8 +471,7 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
       float* cur = smem + (gi & 1) * STAGE;
       if (gi + 1 < total) PMU_FETCH4(gi + 1, smem + ((gi + 1) & 1) * STAGE)
       const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
-      w4_step<CH>(pa, ua, acc);                          // channel 2*kk
-      w4_step<CH>(pa + 4, ua + CO * NC * 4, acc);        // channel 2*kk + 1
+      w4_chunk<CH, PF>(pa, ua, acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
       __syncthreads();
     }
@@ -482,7 +502,7 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
 // (pass, chunk) sequence is one DMA pipeline, so the next pass's first chunk lands under this
 // pass's epilogue.  Waves 0-3 compute components 0..17 (rows 0-2 of the 6x6 grid), waves 4-7 the
 // rest, each for its tile group's 16 tiles x all 32 output channels.
-template <bool DGRAD>
+template <bool DGRAD, bool PF>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
   const int tid = threadIdx.x;
@@ -524,8 +544,9 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   }
   B.gin = gin;
   B.gzero = gzero;
-  if (tid >> 8) wino4_main<DGRAD, 1>(a, B, goff, smem);
-  else wino4_main<DGRAD, 0>(a, B, goff, smem);
+  if (a.prio && (tid >> 8)) __builtin_amdgcn_s_setprio(1);
+  if (tid >> 8) wino4_main<DGRAD, 1, PF>(a, B, goff, smem);
+  else wino4_main<DGRAD, 0, PF>(a, B, goff, smem);
 }
 
 int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
@@ -548,7 +569,7 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
   }();
   static const long long min_wg = [] {
     const char* e = getenv("PMU_WINO4_MINWG");
-    return e ? atoll(e) : 512LL;
+    return e ? atoll(e) : 1024LL;
   }();
   int cpb = 1;
   if (cpb_env > 0) {
@@ -557,11 +578,23 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
     while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= min_wg) cpb *= 2;
   }
   a.cpb = cpb;
+  static const int pf = [] {
+    const char* e = getenv("PMU_WINO4_PF");
+    return e ? atoi(e) : 0;
+  }();
+  static const int prio = [] {  // PMU_WINO4_PRIO=1: waves of component half 1 at s_setprio 1 (A/B)
+    const char* e = getenv("PMU_WINO4_PRIO");
+    return e ? atoi(e) : 0;
+  }();
+  a.prio = prio;
   const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
-  if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((conv3x3_wino4_kernel<false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  const dim3 grid((unsigned)blocks);
+  if (dgrad && pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true>), grid, dim3(NT), 0, st, a);
+  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false>), grid, dim3(NT), 0, st, a);
+  else if (pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<false, true>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
