@@ -67,28 +67,43 @@ constexpr int W_UNITS = D_UNITS + HH * HWD * X_UPX;
 constexpr int W_NGL = (W_UNITS + NT - 1) / NT;
 static_assert(D_UNITS * 4 == D_FLOATS && W_UNITS * 4 == SLOT, "slot = dz image + x image");
 
+// block geometry by output-channel width: 32 (512 threads) or 64 (1024 threads: 4 waves per SIMD,
+// the x halo image shared by twice the output channels; PMU_WGW64)
+template <int WCO_>
+struct WgwCfg {
+  static constexpr int WCO = WCO_, NT = 16 * WCO_, DLS = WCO_;
+  static constexpr int D_FLOATS = TH * TW * DLS;
+  static constexpr int SLOT = D_FLOATS + X_FLOATS;
+  static constexpr int D_UPX = DLS / 4;
+  static constexpr int D_UNITS = TH * TW * D_UPX;
+  static constexpr int W_UNITS = D_UNITS + HH * HWD * X_UPX;
+  static constexpr int W_NGL = (W_UNITS + NT - 1) / NT;
+};
+
+template <int WCO_ = 32>
 __device__ __forceinline__ void wgw_dma(const WgwArgs& a, int tile, int co0, int ci0, int tid, float* slot) {
+  using C = WgwCfg<WCO_>;
   int n, h0, w0;
   wgw_origin(a, tile, n, h0, w0);
   const int wbase = (tid >> 6) * 256;
 #pragma unroll
-  for (int r = 0; r < W_NGL; ++r) {
-    const int u = r * NT + tid;
+  for (int r = 0; r < C::W_NGL; ++r) {
+    const int u = r * C::NT + tid;
     // dz image unit (u < D_UNITS) or x halo unit, branch-free
-    const bool isd = u < D_UNITS;
-    const int pd = u / D_UPX, qd = u - pd * D_UPX;
-    const int v = u - D_UNITS;
+    const bool isd = u < C::D_UNITS;
+    const int pd = u / C::D_UPX, qd = u - pd * C::D_UPX;
+    const int v = u - C::D_UNITS;
     const int px = v / X_UPX, qx = v - px * X_UPX;
     const int hr = px / HWD, hc = px - hr * HWD;
     const int h = isd ? h0 + (pd >> 4) : h0 - 1 + hr;
     const int w = isd ? w0 + (pd & 15) : w0 - 1 + hc;
-    const bool data = isd ? qd < WCO / 4 : (u < W_UNITS && qx < WCI / 4);
+    const bool data = isd ? qd < C::WCO / 4 : (u < C::W_UNITS && qx < WCI / 4);
     const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
     const long long pix = ((long long)n * a.H + h) * a.W + w;
     const float* src = isd ? a.dz + pix * a.Cout + co0 + 4 * qd : a.x + pix * a.Cin + ci0 + 4 * qx;
     if (in)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(slot + 4 * r * NT + wbase), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(slot + 4 * r * C::NT + wbase), 16, 0, 0);
     else if (data)
       *reinterpret_cast<float4*>(slot + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
@@ -235,11 +250,12 @@ struct WgwOps2 {
   float xb[4];  // patch row rb
 };
 
-template <int EXP = 0>
-__global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * SLOT];
+template <int EXP = 0, int WCO_ = 32>
+__global__ __launch_bounds__(16 * WCO_, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
+  using C = WgwCfg<WCO_>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int row = wave & 3, half = wave >> 2;
+  const int row = wave & 3, half = (wave >> 2) & 1, cg = wave >> 3;  // cg: 32-channel group of WCO_ = 64
   // B^T row `row` = x[ra] + sx * x[rb]; A row `row` of dY: alpha * d0 + beta * d1
   const int ra = row == 0 ? 0 : row == 2 ? 2 : 1;
   const int rb = row == 0 ? 2 : row == 1 ? 2 : row == 2 ? 1 : 3;
@@ -250,7 +266,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
   const int xc = id & 7, q8 = nb >> 3, r8 = nb & 7;
   const int lb = xc * q8 + (xc < r8 ? xc : r8) + (id >> 3);
   const int mn = lb % nmn, split = lb / nmn;
-  const int co0 = (mn % a.nco) * WCO, ci0 = (mn / a.nco) * WCI;
+  const int co0 = (mn % a.nco) * C::WCO, ci0 = (mn / a.nco) * WCI;
   const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
   const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);
 
@@ -271,18 +287,18 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
   const int db = (rb - ra) * HWD * XLS;
   unsigned dbase = 0, xabase = 0, xbbase = 0;
   auto set_bases = [&](const float* slot) {
-    dbase = lds_addr(slot + (2 * hl) * DLS + (lane & 31));
-    xabase = lds_addr(slot + D_FLOATS + ra * HWD * XLS + (2 * hl) * XLS + 32 * half + (lane & 31));
+    dbase = lds_addr(slot + (2 * hl) * C::DLS + 32 * cg + (lane & 31));
+    xabase = lds_addr(slot + C::D_FLOATS + ra * HWD * XLS + (2 * hl) * XLS + 32 * half + (lane & 31));
     xbbase = xabase + 4u * (unsigned)db;
   };
   auto read = [&](int s, WgwOps2& o) {
-    const unsigned dstep = 4u * (unsigned)((2 * (s >> 2) * TW + 4 * (s & 3)) * DLS);
+    const unsigned dstep = 4u * (unsigned)((2 * (s >> 2) * TW + 4 * (s & 3)) * C::DLS);
     const unsigned xstep = 4u * (unsigned)((2 * (s >> 2) * HWD + 4 * (s & 3)) * XLS);
     const unsigned da = dbase + dstep, xa = xabase + xstep, xb = xbbase + xstep;
     o.d[0] = lds_b32<0>(da);
-    o.d[1] = lds_b32<4 * DLS>(da);
-    o.d[2] = lds_b32<4 * TW * DLS>(da);
-    o.d[3] = lds_b32<4 * (TW + 1) * DLS>(da);
+    o.d[1] = lds_b32<4 * C::DLS>(da);
+    o.d[2] = lds_b32<4 * TW * C::DLS>(da);
+    o.d[3] = lds_b32<4 * (TW + 1) * C::DLS>(da);
     o.xa[0] = lds_b32<0>(xa);
     o.xa[1] = lds_b32<4 * XLS>(xa);
     o.xa[2] = lds_b32<8 * XLS>(xa);
@@ -292,14 +308,14 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
     o.xb[2] = lds_b32<8 * XLS>(xb);
     o.xb[3] = lds_b32<12 * XLS>(xb);
   };
-  if (t_beg < t_end) wgw_dma(a, t_beg, co0, ci0, tid, smem);
+  if (t_beg < t_end) wgw_dma<WCO_>(a, t_beg, co0, ci0, tid, smem);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   for (int tile = t_beg; tile < t_end; ++tile) {
     const int cur = (tile - t_beg) & 1;
     const bool more = tile + 1 < t_end;
-    if (more && EXP != 1) wgw_dma(a, tile + 1, co0, ci0, tid, smem + (cur ^ 1) * SLOT);
-    set_bases(smem + (EXP == 1 ? 0 : cur * SLOT));
+    if (more && EXP != 1) wgw_dma<WCO_>(a, tile + 1, co0, ci0, tid, smem + (cur ^ 1) * C::SLOT);
+    set_bases(smem + (EXP == 1 ? 0 : cur * C::SLOT));
     WgwOps2 ops[2];
     read(0, ops[0]);
 #pragma unroll
@@ -337,7 +353,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino32_kernel(WgwArgs a) {
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int co = co0 + acc_row(r, lane);
+      const int co = co0 + 32 * cg + acc_row(r, lane);
       a.ws[(((long long)split * 16 + 4 * row + k) * a.Cout + co) * a.Cin + ci] = acc[k][r];
     }
 }
@@ -391,12 +407,31 @@ __global__ __launch_bounds__(256) void wgrad_wino_reduce_kernel(const float* __r
   }
 }
 
+// 64-channel blocks when Cout allows (PMU_WGW64=0: the 32-channel, 512-thread blocks everywhere)
+static bool wgw_v16() {  // PMU_WGRAD_WINO=16x16: the 16x16x4 layout (all components per wave)
+  static const bool v = [] {
+    const char* e = getenv("PMU_WGRAD_WINO");
+    return e && strcmp(e, "16x16") == 0;
+  }();
+  return v;
+}
+static int wgw_wco(int Cout) {
+  static const bool w64 = [] {
+    const char* e = getenv("PMU_WGW64");
+#ifdef PMU_EXPERIMENTS
+    if (getenv("PMU_WINO_EXP")) return false;  // the timing experiments are 32-channel kernels
+#endif
+    return !(e && atoi(e) == 0);
+  }();
+  return (w64 && !wgw_v16() && Cout % 64 == 0) ? 64 : 32;
+}
+
 void wgw_geometry(int N, int H, int W, int Cout, int Cin, WgwArgs& a) {
   a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.Cin = Cin;
   a.tiles_w = pmu_cdiv(W, TW);
   a.tiles_h = pmu_cdiv(H, TH);
   a.ntiles = N * a.tiles_w * a.tiles_h;
-  a.nco = Cout / WCO;
+  a.nco = Cout / wgw_wco(Cout);
   const int blocks_mn = a.nco * (Cin / WCI);
   int s = 512 / blocks_mn;  // ~2 blocks per CU over the launch
   if (s < 1) s = 1;
@@ -432,10 +467,7 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
   PMU_REQUIRE(ws_bytes >= (size_t)a.nsplit * 16 * Cout * Cin * sizeof(float));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(a.nco * (Cin / WCI)), (unsigned)a.nsplit);
-  static const bool v16 = [] {
-    const char* e = getenv("PMU_WGRAD_WINO");
-    return e && strcmp(e, "16x16") == 0;
-  }();
+  const bool v16 = wgw_v16();
 #ifdef PMU_EXPERIMENTS
   // timing experiments (wrong results for EXP != 0): only in `make EXPERIMENTS=1` builds
   static const int exp_ = [] {
@@ -451,6 +483,8 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
 #endif
   if (v16)  // the 16x16x4 layout (all components per wave)
     hipLaunchKernelGGL((wgrad3x3_wino_kernel<0>), grid, dim3(NT), 0, st, a);
+  else if (wgw_wco(Cout) == 64)
+    hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0, 64>), grid, dim3(1024), 0, st, a);
   else
     hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
