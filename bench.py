@@ -71,7 +71,7 @@ class KernelTimer:
             "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16",
             "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino", "pmu_conv3x3_wgrad_wino",
             "pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw", "pmu_conv3x3_fwd_wino4",
-            "pmu_conv3x3_dgrad_wino4")
+            "pmu_conv3x3_dgrad_wino4", "pmu_conv3x3_fwd_wino2h", "pmu_conv3x3_dgrad_wino2h")
 
     def __init__(self):
         self.rec = []
@@ -83,7 +83,8 @@ class KernelTimer:
             cin, N, H, W = args[1], args[2], args[3], args[4]
             nout = args[7] if name.startswith("pmu_conv3x3_fwd") else args[6]
             return 2.0 * 36 * N * ((H + 3) // 4) * ((W + 3) // 4) * cin * nout
-        if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw"):
+        if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw", "pmu_conv3x3_fwd_wino2h",
+                    "pmu_conv3x3_dgrad_wino2h"):
             cin, N, H, W = args[1], args[2], args[3], args[4]
             nout = args[7] if name.startswith("pmu_conv3x3_fwd") else args[6]
             return 2.0 * 16 * N * ((H + 1) // 2) * ((W + 1) // 2) * cin * nout
@@ -151,7 +152,8 @@ class KernelTimer:
         if name.endswith("_wino4"):
             H, W = args[3], args[4]
             return fl * (9.0 * H * W) / (36.0 * ((H + 3) // 4) * ((W + 3) // 4))
-        if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw"):
+        if name in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw", "pmu_conv3x3_fwd_wino2h",
+                    "pmu_conv3x3_dgrad_wino2h"):
             H, W = args[3], args[4]
         elif name == "pmu_conv3x3_wgrad_wino":
             H, W = args[3], args[4]
@@ -314,6 +316,7 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_fwd_wino": r"conv3x3_wino_(pipe_)?kernel<false", "pmu_conv3x3_dgrad_wino": r"conv3x3_wino_(pipe_)?kernel<true",
     "pmu_conv3x3_wgrad_wino": (r"wgrad3x3_wino(32)?_kernel", r"wgrad_wino_reduce_kernel"),
     "pmu_conv3x3_fwd_wino4": r"conv3x3_wino4_kernel<false", "pmu_conv3x3_dgrad_wino4": r"conv3x3_wino4_kernel<true",
+    "pmu_conv3x3_fwd_wino2h": r"conv3x3_wino2h_kernel<false", "pmu_conv3x3_dgrad_wino2h": r"conv3x3_wino2h_kernel<true",
     "pmu_conv3x3_fwd_wino_raw": r"conv3x3_wino_raw_kernel<false", "pmu_conv3x3_dgrad_wino_raw": r"conv3x3_wino_raw_kernel<true", "pmu_convT2x2_fwd": r"convT_pipe_kernel<false>|ActRowA",
     "pmu_convT2x2_dgrad": r"convT_pipe_kernel<true>|DuGatherA",
     "pmu_convT2x2_wgrad": r"convT_wgrad_(pipe_)?kernel", "pmu_fcomb_fwd": r"fcomb_fwd_kernel",

@@ -117,6 +117,17 @@ int pmu_conv3x3_fwd_wino_raw(const float* xt, int Cin, int N, int H, int W, cons
                              int Cout, float* z, float* part, void* stream);
 int pmu_conv3x3_dgrad_wino_raw(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
                                int Csplit, float* dx0, float* dx1, void* stream);
+/* The same F(2x2,3x3) operators on a materialised operand in 1024-thread workgroups (16 waves, four per
+ * SIMD; 64 output channels x 16 x 16 pixels per block; waves split the 16 components in halves).
+ * C % 8 == 0; weights by pmu_conv3x3_pack_wino2h ([64 output rows][8 channels][16 components]);
+ * part rows = pmu_conv3x3_tiles_wino2h() (16 x 16 pixel blocks). */
+size_t pmu_conv3x3_packed_size_wino2h(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_wino2h(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream);
+int pmu_conv3x3_tiles_wino2h(int N, int H, int W);
+int pmu_conv3x3_fwd_wino2h(const float* xt, int Cin, int N, int H, int W, const float* wp, const float* bias,
+                           int Cout, float* z, float* part, void* stream);
+int pmu_conv3x3_dgrad_wino2h(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                             int Csplit, float* dx0, float* dx1, void* stream);
 /* ---- fp32 Winograd F(4x4,3x3) on a materialised operand (images >= 32 x 32: the c2 fp32 default) --
  * Replaces the same nn.Conv2d forward / input gradient (PMU/model/unet/unet_parts.py:15,18; autograd of
  * PMU/model/unet/unet_model.py:31-54) as pmu_conv3x3_*_wino_raw: 36 per-component GEMMs of

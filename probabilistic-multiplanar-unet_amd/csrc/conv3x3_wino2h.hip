@@ -1,0 +1,464 @@
+// 3x3 / pad 1 convolution in fp32 by Winograd F(2x2, 3x3), high-occupancy variant: the forward of
+// nn.Conv2d at PMU/model/unet/unet_parts.py:15,18 (and its input gradient) on a materialised NHWC
+// operand, the same arithmetic as conv3x3_wino.hip's raw kernel (16 products per 2x2 tile per channel
+// pair; transforms with coefficients 0, +-1, +-1/2; results equal the direct sum to fp32 rounding).
+//
+// Block: 1024 threads = 16 waves, four per SIMD (the weight gradient measured 12% faster going from
+// two to four waves per SIMD): 64 tiles (8 x 8 -> a 16 x 16 output patch) x 64 output channels.
+// Wave w = (tile group tg = w & 3: tile rows 2tg, 2tg+1; component half ch = (w >> 2) & 1: rows
+// 2ch, 2ch+1 of the 4x4 component grid; channel group cg = w >> 3: 32 outputs).  A wave keeps 8
+// components x 2 co halves = 16 f32x4 accumulators (64 registers, < 128 in all), forms only its half
+// of V = B^T d B (16 VALU for 16 MFMAs) and the two component halves of a tile group swap partial
+// outputs through a free LDS stage in the epilogue.  Per chunk of 8 input channels (two MFMA steps),
+// double-buffered stages receive the 18 x 18 x 8 operand image (2-pixel groups + a pad unit) and U
+// (8 ch x 64 co x 16 comps) by LDS-DMA; the patch is read per step as 16 ds_read_b32.
+#include <string.h>
+#include <stdlib.h>
+#include "pmu_common.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TX = 8, TY = 8;                 // tiles per block
+constexpr int OW = 2 * TX, OH = 2 * TY;       // 16 x 16 output pixels
+constexpr int HW = OW + 2, HH = OH + 2;       // 18 x 18 halo
+constexpr int BK = 8;                         // input channels per chunk
+constexpr int GP = 20;                        // floats per group of 2 halo pixels (2 x 8 ch + 1 pad unit)
+constexpr int ROWF = 184;                     // floats per halo row (9 groups = 180, padded)
+constexpr int ROWU = ROWF / 4;
+constexpr int A_FLOATS = HH * ROWF;
+constexpr int CO = 64;                        // output channels per block
+constexpr int NC = 16;                        // Winograd components
+constexpr int U_FLOATS = BK * CO * NC;        // [ch 8][co 64][comp 16]
+constexpr int STAGE = A_FLOATS + U_FLOATS;
+constexpr int NT = 1024;
+constexpr int A_UNITS = A_FLOATS / 4;
+constexpr int NGL = (A_UNITS + NT - 1) / NT;
+constexpr int UGL = U_FLOATS / 4 / NT;
+constexpr int RED_FLOATS = 16 * 16 * 2;
+constexpr int XB_FLOATS = 16 * 2 * 4 * 64;    // one exchange round: 16 waves x 2 tiles x 4 outputs x 64 lanes
+static_assert(U_FLOATS % (4 * NT) == 0, "U of whole DMA rounds");
+static_assert(XB_FLOATS <= STAGE, "exchange round fits a stage");
+static_assert((2 * STAGE + RED_FLOATS) * 4 <= 160 * 1024, "LDS");
+
+struct W2Args {
+  const float* x;     // [N][H][W][KC]
+  const float* wp;    // packed U [co block][chunk][ch 8][co 64][comp 16]
+  const float* bias;
+  float* out0;
+  float* out1;
+  float* part;        // [spatial blocks][2][NOUT] BN partial sums (fwd) or null
+  int H, W, KC, NOUT, split, bw, bh, nco, cpb;
+};
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// U = G g G^T, G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]; one thread per (co block, chunk,
+// channel, co) writes its 16 components (c = 4a + b) as 4 float4
+__global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, float* __restrict__ wp) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  const int nch = (KC + BK - 1) / BK, ncob = (NOUT + CO - 1) / CO;
+  const long long total = (long long)ncob * nch * BK * CO;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int col = (int)(e % CO);
+    long long r = e / CO;
+    const int kl = (int)(r % BK); r /= BK;
+    const int ch = (int)(r % nch);
+    const int jb = (int)(r / nch);
+    const int j = jb * CO + col, k = ch * BK + kl;
+    float g[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        float v = 0.f;
+        if (j < NOUT && k < KC)  // dgrad: the input gradient convolves dz with w[co][ci] rotated by 180 degrees
+          v = dgrad ? w[((long long)k * Cin + j) * 9 + (2 - a) * 3 + (2 - b)] : w[((long long)j * Cin + k) * 9 + a * 3 + b];
+        g[a][b] = v;
+      }
+    float t[4][3];
+    for (int b = 0; b < 3; ++b) {
+      t[0][b] = g[0][b];
+      t[1][b] = 0.5f * (g[0][b] + g[1][b] + g[2][b]);
+      t[2][b] = 0.5f * (g[0][b] - g[1][b] + g[2][b]);
+      t[3][b] = g[2][b];
+    }
+    float u[16];
+    for (int a = 0; a < 4; ++a) {
+      u[4 * a + 0] = t[a][0];
+      u[4 * a + 1] = 0.5f * (t[a][0] + t[a][1] + t[a][2]);
+      u[4 * a + 2] = 0.5f * (t[a][0] - t[a][1] + t[a][2]);
+      u[4 * a + 3] = t[a][2];
+    }
+    float* dst = wp + (((long long)jb * nch + ch) * BK + kl) * (CO * NC) + col * NC;
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
+  }
+}
+
+template <int OFF>
+__device__ __forceinline__ float lds_b32(unsigned addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ float4 lds_b128(unsigned addr) {
+  float4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(p);
+}
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt");
+  __builtin_amdgcn_s_waitcnt(0xC07F | (N << 8));
+}
+
+// patch element (i, j) of this lane's tile: byte offset from the patch origin
+#define PMU_W2P(I, J) ((((I) * ROWF) + ((J) >> 1) * GP + ((J) & 1) * 8) * 4)
+
+// one MFMA step (channel 2*kk + ks in k-slot kk): patch (16 x b32), U (2 groups x 2 co halves x b128),
+// half CH of B^T d B (rows 2CH, 2CH+1; B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]), 16 MFMAs
+template <int CH>
+__device__ __forceinline__ void w2_step(unsigned pa, unsigned ua, f32x4 (&acc)[2][8]) {
+  float d[16];
+#define PMU_RD(I, J) d[4 * (I) + (J)] = lds_b32<PMU_W2P(I, J)>(pa);
+  PMU_RD(0, 0) PMU_RD(0, 1) PMU_RD(0, 2) PMU_RD(0, 3) PMU_RD(1, 0) PMU_RD(1, 1) PMU_RD(1, 2) PMU_RD(1, 3)
+  PMU_RD(2, 0) PMU_RD(2, 1) PMU_RD(2, 2) PMU_RD(2, 3) PMU_RD(3, 0) PMU_RD(3, 1) PMU_RD(3, 2) PMU_RD(3, 3)
+#undef PMU_RD
+  // U of this half: components 8CH .. 8CH+7 of co half h at row offset 16*NC*h
+  const float4 u00 = lds_b128<(8 * CH) * 4>(ua);
+  const float4 u10 = lds_b128<(16 * NC + 8 * CH) * 4>(ua);
+  const float4 u01 = lds_b128<(8 * CH + 4) * 4>(ua);
+  const float4 u11 = lds_b128<(16 * NC + 8 * CH + 4) * 4>(ua);
+  wait_lgkm<2>();  // the patch and U group 0
+  __builtin_amdgcn_sched_barrier(0);
+  float t[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (CH == 0) {
+      t[0][j] = d[j] - d[8 + j];
+      t[1][j] = d[4 + j] + d[8 + j];
+    } else {
+      t[0][j] = d[8 + j] - d[4 + j];
+      t[1][j] = d[4 + j] - d[12 + j];
+    }
+  }
+  float v[8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    v[4 * a + 0] = t[a][0] - t[a][2];
+    v[4 * a + 1] = t[a][1] + t[a][2];
+    v[4 * a + 2] = t[a][2] - t[a][1];
+    v[4 * a + 3] = t[a][1] - t[a][3];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  acc[0][0] = mfma16(v[0], u00.x, acc[0][0]);
+  acc[1][0] = mfma16(v[0], u10.x, acc[1][0]);
+  acc[0][1] = mfma16(v[1], u00.y, acc[0][1]);
+  acc[1][1] = mfma16(v[1], u10.y, acc[1][1]);
+  acc[0][2] = mfma16(v[2], u00.z, acc[0][2]);
+  acc[1][2] = mfma16(v[2], u10.z, acc[1][2]);
+  acc[0][3] = mfma16(v[3], u00.w, acc[0][3]);
+  acc[1][3] = mfma16(v[3], u10.w, acc[1][3]);
+  __builtin_amdgcn_sched_barrier(0);
+  wait_lgkm<0>();
+  __builtin_amdgcn_sched_barrier(0);
+  acc[0][4] = mfma16(v[4], u01.x, acc[0][4]);
+  acc[1][4] = mfma16(v[4], u11.x, acc[1][4]);
+  acc[0][5] = mfma16(v[5], u01.y, acc[0][5]);
+  acc[1][5] = mfma16(v[5], u11.y, acc[1][5]);
+  acc[0][6] = mfma16(v[6], u01.z, acc[0][6]);
+  acc[1][6] = mfma16(v[6], u11.z, acc[1][6]);
+  acc[0][7] = mfma16(v[7], u01.w, acc[0][7]);
+  acc[1][7] = mfma16(v[7], u11.w, acc[1][7]);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// this half's share of Y = A^T M A (A^T = [1 1 1 0; 0 1 -1 -1]) for tile r of co half h:
+// P[2p + q] = sum over the half's rows a of A^T[p][a] (M[a][:] A)[q]
+template <int CH>
+__device__ __forceinline__ void w2_partial(const f32x4 (&acc)[2][8], int h, int r, float (&P)[4]) {
+  float R[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const float m0 = acc[h][4 * a][r], m1 = acc[h][4 * a + 1][r], m2 = acc[h][4 * a + 2][r], m3 = acc[h][4 * a + 3][r];
+    R[a][0] = m0 + m1 + m2;
+    R[a][1] = m1 - m2 - m3;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (CH == 0) {  // rows 0, 1: A^T columns (1, 0), (1, 1)
+      P[q] = R[0][q] + R[1][q];
+      P[2 + q] = R[1][q];
+    } else {        // rows 2, 3: A^T columns (1, -1), (0, -1)
+      P[q] = R[0][q];
+      P[2 + q] = -R[0][q] - R[1][q];
+    }
+  }
+}
+
+// epilogue: lane holds M[comp (half CH)][tile 4*kk + r of the group][co j0 + 32 cg + 16 h + (lane & 15)];
+// the two component halves of (tg, cg) swap the partial outputs of the co half the other finishes
+// through xb (a free LDS stage), in two rounds of two tiles per lane
+template <bool DGRAD, int CH>
+__device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, int w0, int j0, int spatial,
+                                                const f32x4 (&acc)[2][8], float* xb, float* red, float bias) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kk = lane >> 4;
+  const int tg = wave & 3, cg = wave >> 3, partner = tg + 4 * (1 - CH) + 8 * cg;
+  const int j = j0 + 32 * cg + 16 * CH + (lane & 15);
+  const bool jok = j < a.NOUT;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int rho = 0; rho < 2; ++rho) {
+    if (rho) __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      float P[4];
+      w2_partial<CH>(acc, 1 - CH, 2 * rho + rr, P);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xb[((wave * 2 + rr) * 4 + e) * 64 + lane] = P[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int r = 2 * rho + rr;
+      float P[4];
+      w2_partial<CH>(acc, CH, r, P);
+      const int t = 4 * kk + r;
+      const int oh = h0 + 2 * (2 * tg + (t >> 3)), ow = w0 + 2 * (t & 7);
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int hh = oh + p, ww = ow + q;
+          const float y = P[2 * p + q] + xb[((partner * 2 + rr) * 4 + 2 * p + q) * 64 + lane];
+          if (!jok || hh >= a.H || ww >= a.W) continue;
+          const float v = y + bias;
+          const long long pix = ((long long)n * a.H + hh) * a.W + ww;
+          if (!DGRAD) {
+            a.out0[pix * a.NOUT + j] = v;
+            s1 += v;
+            s2 = fmaf(v, v, s2);
+          } else if (j < a.split) {
+            a.out0[pix * a.split + j] = v;
+          } else {
+            a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+          }
+        }
+    }
+  }
+  if (!DGRAD && a.part) {
+    s1 += __shfl_xor(s1, 16, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (lane < 16) {
+      red[(wave * 16 + lane) * 2 + 0] = s1;
+      red[(wave * 16 + lane) * 2 + 1] = s2;
+    }
+    __syncthreads();
+    if (tid < CO) {  // channel tid = 32 cg + 16 h + l, summed over the 4 tile groups in order
+      const int jj = j0 + tid, cgg = tid >> 5, hf = (tid >> 4) & 1, l = tid & 15;
+      if (jj < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int wv = g + 4 * hf + 8 * cgg;
+          t1 += red[(wv * 16 + l) * 2 + 0];
+          t2 += red[(wv * 16 + l) * 2 + 1];
+        }
+        a.part[((long long)spatial * 2 + 0) * a.NOUT + jj] = t1;
+        a.part[((long long)spatial * 2 + 1) * a.NOUT + jj] = t2;
+      }
+    }
+  }
+  __syncthreads();  // the exchange reads are done before the next pass reuses xb's stage
+}
+
+struct W2Block {
+  int n, h0, w0, cob0, spatial, nchunks, npass;
+  unsigned gin, gzero;
+};
+
+template <bool DGRAD, int CH>
+__device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, const unsigned (&goff)[NGL],
+                                            float* smem) {
+  float* red = smem + 2 * STAGE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nchunks = B.nchunks, total = B.npass * nchunks;
+  const float* wsrc = a.wp + (long long)B.cob0 * nchunks * U_FLOATS;
+  const unsigned uoff = 16u * tid;
+  const int wave_off = wave * 256;
+  const unsigned gin = B.gin;
+#define PMU_GLDS(S, D)                                                                                      \
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
+                                   (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
+#define PMU_FETCH2(GI, BUF)                                                                                 \
+  {                                                                                                        \
+    const int p_ = (GI) / nchunks;                                                                         \
+    const int k0_ = ((GI) - p_ * nchunks) * BK;                                                            \
+    float* b_ = (BUF);                                                                                     \
+    const char* xb_ = reinterpret_cast<const char*>(a.x + k0_);                                            \
+    _Pragma("unroll") for (int r = 0; r < NGL; ++r)                                                        \
+      if ((gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                           \
+    const char* s_ = reinterpret_cast<const char*>(wsrc + (long long)(GI) * U_FLOATS) + uoff;              \
+    float* d_ = b_ + A_FLOATS + wave_off;                                                                  \
+    _Pragma("unroll") for (int r = 0; r < UGL; ++r) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)           \
+  }
+  const int t = lane & 15, kk = lane >> 4, tg = wave & 3, cg = wave >> 3;
+  const int pbase = 2 * (2 * tg + (t >> 3)) * ROWF + GP * (t & 7) + 2 * kk;
+  const int ubase = A_FLOATS + (2 * kk * CO + 32 * cg + t) * NC;
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  PMU_FETCH2(0, smem)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int p = 0; p < B.npass; ++p) {
+    const int j0 = (B.cob0 + p) * CO;
+    const int jb = j0 + 32 * cg + 16 * CH + t;
+    const float bias = (!DGRAD && a.bias && jb < a.NOUT) ? a.bias[jb] : 0.f;
+    int gi = p * nchunks;
+    for (int ch = 0; ch < nchunks; ++ch, ++gi) {
+      float* cur = smem + (gi & 1) * STAGE;
+      if (gi + 1 < total) PMU_FETCH2(gi + 1, smem + ((gi + 1) & 1) * STAGE)
+      const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
+      w2_step<CH>(pa, ua, acc);                          // channel 2*kk
+      w2_step<CH>(pa + 4, ua + CO * NC * 4, acc);        // channel 2*kk + 1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
+      __syncthreads();
+    }
+    int ne = B.n, h0e = B.h0, w0e = B.w0;
+    asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
+    float* xb = smem + ((gi - 1) & 1) * STAGE;
+    wino2h_epilogue<DGRAD, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    if (p + 1 < B.npass) {  // block-uniform: restore the zero units the exchange overwrote
+#pragma unroll
+      for (int r = 0; r < NGL; ++r)
+        if ((B.gzero >> r) & 1u) *reinterpret_cast<float4*>(xb + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#undef PMU_FETCH2
+#undef PMU_GLDS
+}
+
+template <bool DGRAD>
+__global__ __launch_bounds__(NT, 1) void conv3x3_wino2h_kernel(W2Args a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
+  const int tid = threadIdx.x;
+  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+  const int ncog = (a.nco + a.cpb - 1) / a.cpb;
+  W2Block B;
+  B.cob0 = (lb % ncog) * a.cpb;
+  int sp = lb / ncog;
+  B.spatial = sp;
+  const int bx = sp % a.bw; sp /= a.bw;
+  const int by = sp % a.bh;
+  B.n = sp / a.bh;
+  B.h0 = by * OH;
+  B.w0 = bx * OW;
+  const int KC = a.KC;
+  B.nchunks = KC / BK;
+  B.npass = a.cpb < a.nco - B.cob0 ? a.cpb : a.nco - B.cob0;
+  unsigned goff[NGL];
+  unsigned gin = 0u, gzero = 0u;
+#pragma unroll
+  for (int r = 0; r < NGL; ++r) {
+    const int u = r * NT + tid;
+    const int hr = u / ROWU, wu = u - hr * ROWU;
+    const int g = wu / 5, w5 = wu - 5 * g;
+    const int px = 2 * g + (w5 >> 1);
+    const bool data = u < A_UNITS && w5 < 4 && px < HW;
+    const int h = B.h0 - 1 + hr, w = B.w0 - 1 + px;
+    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    goff[r] = in ? (unsigned)(((((long long)B.n * a.H + h) * a.W + w) * KC + 4 * (w5 & 1)) * 4) : 0u;
+    gin |= in ? (1u << r) : 0u;
+    gzero |= (data && !in) ? (1u << r) : 0u;
+    if (data && !in) {
+      *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(smem + STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  B.gin = gin;
+  B.gzero = gzero;
+  if ((tid >> 8) & 1) wino2h_main<DGRAD, 1>(a, B, goff, smem);
+  else wino2h_main<DGRAD, 0>(a, B, goff, smem);
+}
+
+int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
+                  float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
+  PMU_REQUIRE(x && wp && out0 && KC > 0 && KC % BK == 0 && NOUT > 0 && N > 0 && H > 0 && W > 0);
+  PMU_REQUIRE((long long)N * H * W * KC * 4 < (1LL << 32));  // 32-bit DMA byte offsets
+  W2Args a;
+  memset(&a, 0, sizeof(a));
+  a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
+  a.H = H; a.W = W; a.KC = KC; a.NOUT = NOUT; a.split = split;
+  a.bw = pmu_cdiv(W, OW);
+  a.bh = pmu_cdiv(H, OH);
+  a.nco = pmu_cdiv(NOUT, CO);
+  const long long spatial = (long long)a.bw * a.bh * N;
+  static const int cpb_env = [] {
+    const char* e = getenv("PMU_WINO2H_CPB");
+    return e ? atoi(e) : 0;
+  }();
+  static const long long min_wg = [] {
+    const char* e = getenv("PMU_WINO2H_MINWG");
+    return e ? atoll(e) : 1024LL;
+  }();
+  int cpb = 1;
+  if (cpb_env > 0) {
+    cpb = cpb_env < a.nco ? cpb_env : a.nco;
+  } else {
+    while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= min_wg) cpb *= 2;
+  }
+  a.cpb = cpb;
+  const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
+  PMU_REQUIRE(blocks < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  if (dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+}  // namespace
+
+extern "C" int pmu_conv3x3_tiles_wino2h(int N, int H, int W) { return N * pmu_cdiv(H, OH) * pmu_cdiv(W, OW); }
+
+extern "C" size_t pmu_conv3x3_packed_size_wino2h(int Cout, int Cin, int dgrad) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  return (size_t)pmu_cdiv(NOUT, CO) * pmu_cdiv(KC, BK) * U_FLOATS * sizeof(float);
+}
+
+extern "C" int pmu_conv3x3_pack_wino2h(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream) {
+  PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
+  const long long total = (long long)pmu_conv3x3_packed_size_wino2h(Cout, Cin, dgrad) / sizeof(float) / NC;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(pack_wino2h_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_conv3x3_fwd_wino2h(const float* xt, int Cin, int N, int H, int W, const float* wp, const float* bias,
+                                      int Cout, float* z, float* part, void* stream) {
+  return launch_wino2h(xt, Cin, N, H, W, wp, bias, Cout, z, nullptr, Cout, part, false, stream);
+}
+
+extern "C" int pmu_conv3x3_dgrad_wino2h(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                                        int Csplit, float* dx0, float* dx1, void* stream) {
+  PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
+  return launch_wino2h(dzt, Cout, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
+}

@@ -55,6 +55,13 @@ SIGNATURES = {
                                          c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_wino_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                            c_void_p, c_void_p]),
+    "pmu_conv3x3_packed_size_wino2h": (c_size_t, [c_int, c_int, c_int]),
+    "pmu_conv3x3_pack_wino2h": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_conv3x3_tiles_wino2h": (c_int, [c_int, c_int, c_int]),
+    "pmu_conv3x3_fwd_wino2h": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                       c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_wino2h": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                         c_void_p, c_void_p]),
     "pmu_conv3x3_packed_size_wino4": (c_size_t, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_wino4": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_tiles_wino4": (c_int, [c_int, c_int, c_int]),

@@ -243,7 +243,14 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             R = lb.pmu_conv3x3_tiles_wino(N, H, W)
             part = _empty(R, 2 * Cout, device=dev) if need_stats else None
             wp = pack_weights_wino(conv.weight, dgrad=False)
-            if wino_raw_ok(Cin):
+            if wino_raw_ok(Cin) and wino2h_ok(Cin):
+                # 1024-thread F(2x2) workgroups (four waves per SIMD) on the materialised operand
+                xm = frame_to_f32(srcs, N, H, W)
+                wp2 = pack_weights_wino2h(conv.weight, dgrad=False)
+                L.call("pmu_conv3x3_fwd_wino2h", xm.data_ptr(), Cin, N, H, W, wp2.data_ptr(), L.ptr(conv.bias),
+                       Cout, z.data_ptr(), L.ptr(part), s)
+                xt32 = xm if xt32 is not None else None
+            elif wino_raw_ok(Cin):
                 # the operand materialised once (the weight gradient's operand anyway), then a
                 # DMA-staged Winograd GEMM on it
                 xm = frame_to_f32(srcs, N, H, W)
@@ -319,6 +326,12 @@ def _dgrad32(dz_src, conv, N, H, W, split, tee):
         L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
         wp = pack_weights_wino4(conv.weight, dgrad=True)
         L.call("pmu_conv3x3_dgrad_wino4", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
+               L.ptr(dx1), s)
+    elif use_wino() and wino_raw_ok(Cout) and wino2h_ok(Cout):
+        dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
+        L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
+        wp = pack_weights_wino2h(conv.weight, dgrad=True)
+        L.call("pmu_conv3x3_dgrad_wino2h", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
                L.ptr(dx1), s)
     elif use_wino() and wino_raw_ok(Cout):
         dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
@@ -461,6 +474,22 @@ def wino4_ok(C: int, H: int, W: int, kind: str) -> bool:
     mode = os.environ.get("PMU_WINO4", "dgrad")
     return (C % 8 == 0 and H >= 32 and W >= 32 and (mode == "1" or mode == kind)
             and os.environ.get("PMU_FP32_CONV", "wino") == "wino")
+
+
+def pack_weights_wino2h(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """F(2x2,3x3) weights in the 1024-thread kernel's 64-channel blocks (pmu_conv3x3_pack_wino2h)."""
+    Cout, Cin = w.shape[0], w.shape[1]
+    n = L.lib().pmu_conv3x3_packed_size_wino2h(Cout, Cin, int(dgrad)) // 4
+    wp = _empty(n, device=w.device)
+    L.call("pmu_conv3x3_pack_wino2h", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
+def wino2h_ok(C: int) -> bool:
+    """The 1024-thread F(2x2) kernels (pmu_conv3x3_{fwd,dgrad}_wino2h; four waves per SIMD where the
+    512-thread raw kernel runs two): C % 8 == 0.  kbench on the c2 shapes: forward 11.57 -> 10.98 ms
+    (256x256 layers 1.04 -> 0.90 ms).  PMU_WINO2H=0: the 512-thread raw kernels (A/B)."""
+    return C % 8 == 0 and os.environ.get("PMU_WINO2H", "1") != "0"
 
 
 def use_wino() -> bool:

@@ -104,6 +104,8 @@ def main():
         from pmu_hip.engine import pack_weights_wino4
         w4f, w4d = pack_weights_wino4(w, False), pack_weights_wino4(w, True)
         part4 = torch.empty(L.lib().pmu_conv3x3_tiles_wino4(N, H, W), 2 * Cout, device=dev)
+        from pmu_hip.engine import pack_weights_wino2h
+        w2f, w2d = pack_weights_wino2h(w, False), pack_weights_wino2h(w, True)
         ops = {
             "fwd_raw": lambda: L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), cpi, N, H, W, wrf.data_ptr(), b.data_ptr(),
                                       Cout, out.data_ptr(), partr.data_ptr(), s),
@@ -135,6 +137,10 @@ def main():
                                      b.data_ptr(), Cout, out.data_ptr(), part4.data_ptr(), s),
             "dgrad_w4": lambda: L.call("pmu_conv3x3_dgrad_wino4", dzt32.data_ptr(), Cout, N, H, W, w4d.data_ptr(),
                                        Cin, Cin, dx.data_ptr(), None, s),
+            "fwd_w2h": lambda: L.call("pmu_conv3x3_fwd_wino2h", xt32.data_ptr(), Cin, N, H, W, w2f.data_ptr(),
+                                      b.data_ptr(), Cout, out.data_ptr(), partw.data_ptr(), s),
+            "dgrad_w2h": lambda: L.call("pmu_conv3x3_dgrad_wino2h", dzt32.data_ptr(), Cout, N, H, W, w2d.data_ptr(),
+                                        Cin, Cin, dx.data_ptr(), None, s),
             "mat32": lambda: L.call("pmu_frame_to_f32", fin, xt32.data_ptr(), s),
             "fwd_wino": lambda: L.call("pmu_conv3x3_fwd_wino", fin, wwf.data_ptr(), b.data_ptr(), Cout,
                                        out.data_ptr(), partw.data_ptr(), None, s),
