@@ -263,15 +263,55 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
 
 def cpu_leg(args, step):
     """The bench's CPU-oracle leg (rank 0, N=1, after the timed region): the oracle as the checker
-    of the bench batch (``dice_vs_ref``, not for the probabilistic workload) and the timed CPU
-    baseline.  The only place bench.py touches oracle/."""
+    of the bench batch (``dice_vs_ref``) and the timed CPU baseline.  The only place bench.py
+    touches oracle/."""
     dvr = None
     if args.workload != "probunet":
         xb, tb = step.batch()
         dvr = dice_vs_ref(step.net, xb, tb, args.classes, args.precision)
+    else:
+        dvr = dice_vs_ref_probunet(step.net, *step.batch())
     cpu = cpu_baseline(workload="probunet" if args.workload == "probunet" else "unet", size=args.size,
                        channels=args.channels, classes=3 if args.workload == "probunet" else args.classes)
     return cpu, dvr
+
+
+def dice_vs_ref_probunet(net, x, segm, n=8):
+    """c4's "Dice vs ref": the HIP ProbabilisticUnet's reconstruction (forward(training=True) + elbo
+    with the posterior sample mu + sigma * eps, eps seeded and injected on both sides, as
+    tests/test_probunet_gpu.py does) on the first ``n`` slices of the bench batch vs the fp32 CPU
+    oracle's (oracle/probunet_ref.py) for the same weights: argmax label maps per class, label
+    agreement, Dice of each side against segm, loss and reconstruction deltas."""
+    from oracle.probunet_ref import probunet_forward_loss
+    from oracle.unet_ref import dice_coeff
+    threads, _ = host_cpu()
+    torch.set_num_threads(threads)
+    x, segm = x[:n], segm[:n]
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    eps = torch.randn(x.shape[0], 6, generator=torch.Generator().manual_seed(7))
+    with torch.no_grad():
+        net.forward(x, segm, training=True)
+        d = net.posterior_latent_space
+        d.rsample = lambda sample_shape=torch.Size(): d.base_dist.loc + d.base_dist.scale * eps.to(x.device)
+        loss = float(-net.elbo(segm))
+        y = net.reconstruction.float().cpu()
+        res = probunet_forward_loss(sd, x.cpu(), segm.cpu(), eps, len(FILTERS), 6, 3, 4, 10.0)
+    yr = res["rec"].float()
+    lab, labr, tgt = y.argmax(1), yr.argmax(1), segm.cpu()[:, 0].long()
+    ks = [1, 2]
+    def dc(a, b):
+        return float(dice_coeff(a.float(), b.float()))
+    to_t = [dc(lab == k, tgt == k) for k in ks]
+    to_tr = [dc(labr == k, tgt == k) for k in ks]
+    return {"classes": ks, "dice_hip_vs_oracle_labels": [round(dc(lab == k, labr == k), 6) for k in ks],
+            "label_agreement": round(float((lab == labr).float().mean()), 7),
+            "dice_to_target_hip": [round(v, 6) for v in to_t], "dice_to_target_oracle": [round(v, 6) for v in to_tr],
+            "max_abs_dice_delta": float(max(abs(a - b) for a, b in zip(to_t, to_tr))),
+            "max_abs_output_delta": float((y - yr).abs().max()),
+            "loss_rel_delta": abs(loss - float(res["loss"])) / abs(float(res["loss"])),
+            "precision": "fp32", "oracle": "oracle/probunet_ref.py torch-CPU fp32",
+            "sample": f"the first {x.shape[0]} slices of the bench batch after the timed steps, train mode, "
+                      "posterior noise injected (seeded)"}
 
 
 def dice_vs_ref(net, x, t, classes, precision):
@@ -579,6 +619,8 @@ def build_probunet(args, dev, world, rank):
                           % (FILTERS, S, S),
               "global_batch": B * world, "per_gpu_batch": B, "image": [S, S], "parallelism": f"dp{world}"}
     data = "synthetic (x~U[0,1), random 3-class masks, seeded)"
+    step.net = net
+    step.batch = lambda: (x, segm)
     return step, None, config, data
 
 
