@@ -11,7 +11,8 @@
 // of V = B^T d B (16 VALU for 16 MFMAs) and the two component halves of a tile group swap partial
 // outputs through a free LDS stage in the epilogue.  Per chunk of 8 input channels (two MFMA steps),
 // double-buffered stages receive the 18 x 18 x 8 operand image (2-pixel groups + a pad unit) and U
-// (8 ch x 64 co x 16 comps) by LDS-DMA; the patch is read per step as 16 ds_read_b32.
+// (8 ch x 64 co x 16 comps, rows padded to 20 floats) by LDS-DMA; the patch is read per step as 16
+// ds_read_b32.
 #include <string.h>
 #include <stdlib.h>
 #include "pmu_common.h"
@@ -30,21 +31,23 @@ constexpr int ROWU = ROWF / 4;
 constexpr int A_FLOATS = HH * ROWF;
 constexpr int CO = 64;                        // output channels per block
 constexpr int NC = 16;                        // Winograd components
-constexpr int U_FLOATS = BK * CO * NC;        // [ch 8][co 64][comp 16]
+constexpr int NCP = 20;                       // floats per U row: 16 components + a pad unit (odd unit stride:
+                                              // the lanes' b128 U reads are conflict-free; 16 banked 4-way)
+constexpr int U_FLOATS = BK * CO * NCP;       // [ch 8][co 64][comp 16 + 4 pad]
 constexpr int STAGE = A_FLOATS + U_FLOATS;
 constexpr int NT = 1024;
 constexpr int A_UNITS = A_FLOATS / 4;
 constexpr int NGL = (A_UNITS + NT - 1) / NT;
-constexpr int UGL = U_FLOATS / 4 / NT;
+constexpr int UGL = (U_FLOATS / 4 + NT - 1) / NT;  // U DMA rounds (the last one by the first waves)
 constexpr int RED_FLOATS = 16 * 16 * 2;
 constexpr int XB_FLOATS = 16 * 2 * 4 * 64;    // one exchange round: 16 waves x 2 tiles x 4 outputs x 64 lanes
-static_assert(U_FLOATS % (4 * NT) == 0, "U of whole DMA rounds");
+static_assert(U_FLOATS % (4 * 64) == 0, "U of whole wave DMA instructions");
 static_assert(XB_FLOATS <= STAGE, "exchange round fits a stage");
 static_assert((2 * STAGE + RED_FLOATS) * 4 <= 160 * 1024, "LDS");
 
 struct W2Args {
   const float* x;     // [N][H][W][KC]
-  const float* wp;    // packed U [co block][chunk][ch 8][co 64][comp 16]
+  const float* wp;    // packed U [co block][chunk][ch 8][co 64][comp 16 + 4 pad]
   const float* bias;
   float* out0;
   float* out1;
@@ -91,9 +94,10 @@ __global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Ci
       u[4 * a + 2] = 0.5f * (t[a][0] - t[a][1] + t[a][2]);
       u[4 * a + 3] = t[a][2];
     }
-    float* dst = wp + (((long long)jb * nch + ch) * BK + kl) * (CO * NC) + col * NC;
+    float* dst = wp + (((long long)jb * nch + ch) * BK + kl) * (CO * NCP) + col * NCP;
     for (int q = 0; q < 4; ++q)
       *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
+    *reinterpret_cast<float4*>(dst + 16) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -130,11 +134,11 @@ __device__ __forceinline__ void w2_step(unsigned pa, unsigned ua, f32x4 (&acc)[2
   PMU_RD(0, 0) PMU_RD(0, 1) PMU_RD(0, 2) PMU_RD(0, 3) PMU_RD(1, 0) PMU_RD(1, 1) PMU_RD(1, 2) PMU_RD(1, 3)
   PMU_RD(2, 0) PMU_RD(2, 1) PMU_RD(2, 2) PMU_RD(2, 3) PMU_RD(3, 0) PMU_RD(3, 1) PMU_RD(3, 2) PMU_RD(3, 3)
 #undef PMU_RD
-  // U of this half: components 8CH .. 8CH+7 of co half h at row offset 16*NC*h
+  // U of this half: components 8CH .. 8CH+7 of co half h at row offset 16*NCP*h
   const float4 u00 = lds_b128<(8 * CH) * 4>(ua);
-  const float4 u10 = lds_b128<(16 * NC + 8 * CH) * 4>(ua);
+  const float4 u10 = lds_b128<(16 * NCP + 8 * CH) * 4>(ua);
   const float4 u01 = lds_b128<(8 * CH + 4) * 4>(ua);
-  const float4 u11 = lds_b128<(16 * NC + 8 * CH + 4) * 4>(ua);
+  const float4 u11 = lds_b128<(16 * NCP + 8 * CH + 4) * 4>(ua);
   wait_lgkm<2>();  // the patch and U group 0
   __builtin_amdgcn_sched_barrier(0);
   float t[2][4];
@@ -308,11 +312,12 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
       if ((gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                           \
     const char* s_ = reinterpret_cast<const char*>(wsrc + (long long)(GI) * U_FLOATS) + uoff;              \
     float* d_ = b_ + A_FLOATS + wave_off;                                                                  \
-    _Pragma("unroll") for (int r = 0; r < UGL; ++r) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)           \
+    _Pragma("unroll") for (int r = 0; r < UGL; ++r)                                                        \
+      if (r * NT * 4 + (wave + 1) * 256 <= U_FLOATS) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)          \
   }
   const int t = lane & 15, kk = lane >> 4, tg = wave & 3, cg = wave >> 3;
   const int pbase = 2 * (2 * tg + (t >> 3)) * ROWF + GP * (t & 7) + 2 * kk;
-  const int ubase = A_FLOATS + (2 * kk * CO + 32 * cg + t) * NC;
+  const int ubase = A_FLOATS + (2 * kk * CO + 32 * cg + t) * NCP;
   f32x4 acc[2][8];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -332,7 +337,7 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
       if (gi + 1 < total) PMU_FETCH2(gi + 1, smem + ((gi + 1) & 1) * STAGE)
       const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
       w2_step<CH>(pa, ua, acc);                          // channel 2*kk
-      w2_step<CH>(pa + 4, ua + CO * NC * 4, acc);        // channel 2*kk + 1
+      w2_step<CH>(pa + 4, ua + CO * NCP * 4, acc);       // channel 2*kk + 1
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
       __syncthreads();
     }
@@ -445,7 +450,7 @@ extern "C" size_t pmu_conv3x3_packed_size_wino2h(int Cout, int Cin, int dgrad) {
 
 extern "C" int pmu_conv3x3_pack_wino2h(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream) {
   PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
-  const long long total = (long long)pmu_conv3x3_packed_size_wino2h(Cout, Cin, dgrad) / sizeof(float) / NC;
+  const long long total = (long long)pmu_conv3x3_packed_size_wino2h(Cout, Cin, dgrad) / sizeof(float) / NCP;
   const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
   hipLaunchKernelGGL(pack_wino2h_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
   PMU_CHECK_LAUNCH();
