@@ -29,21 +29,28 @@ constexpr int GP = 20;                        // floats per group of 2 halo pixe
 constexpr int ROWF = 184;                     // floats per halo row (9 groups = 180, padded)
 constexpr int ROWU = ROWF / 4;
 constexpr int A_FLOATS = HH * ROWF;
-constexpr int CO = 64;                        // output channels per block
 constexpr int NC = 16;                        // Winograd components
 constexpr int NCP = 20;                       // floats per U row: 16 components + a pad unit (odd unit stride:
                                               // the lanes' b128 U reads are conflict-free; 16 banked 4-way)
-constexpr int U_FLOATS = BK * CO * NCP;       // [ch 8][co 64][comp 16 + 4 pad]
-constexpr int STAGE = A_FLOATS + U_FLOATS;
-constexpr int NT = 1024;
 constexpr int A_UNITS = A_FLOATS / 4;
-constexpr int NGL = (A_UNITS + NT - 1) / NT;
-constexpr int UGL = (U_FLOATS / 4 + NT - 1) / NT;  // U DMA rounds (the last one by the first waves)
-constexpr int RED_FLOATS = 16 * 16 * 2;
-constexpr int XB_FLOATS = 16 * 2 * 4 * 64;    // one exchange round: 16 waves x 2 tiles x 4 outputs x 64 lanes
-static_assert(U_FLOATS % (4 * 64) == 0, "U of whole wave DMA instructions");
-static_assert(XB_FLOATS <= STAGE, "exchange round fits a stage");
-static_assert((2 * STAGE + RED_FLOATS) * 4 <= 160 * 1024, "LDS");
+
+// block geometry by output channels per block: 64 (1024 threads, 16 waves, one block per CU) or 32
+// (512 threads, 8 waves, 67 KB of LDS: two blocks per CU, PMU_WINO2H_CO=32)
+template <int CO_>
+struct W2Cfg {
+  static constexpr int CO = CO_;
+  static constexpr int NT = 16 * CO_;
+  static constexpr int NW = NT / 64;
+  static constexpr int U_FLOATS = BK * CO_ * NCP;          // [ch 8][co][comp 16 + 4 pad]
+  static constexpr int STAGE = A_FLOATS + U_FLOATS;
+  static constexpr int NGL = (A_UNITS + NT - 1) / NT;
+  static constexpr int UGL = (U_FLOATS / 4 + NT - 1) / NT;  // U DMA rounds (the last one by the first waves)
+  static constexpr int RED_FLOATS = NW * 16 * 2;
+  static constexpr int XB_FLOATS = NW * 2 * 4 * 64;         // one exchange round: waves x 2 tiles x 4 outputs x lanes
+  static_assert(U_FLOATS % (4 * 64) == 0, "U of whole wave DMA instructions");
+  static_assert(XB_FLOATS <= STAGE, "exchange round fits a stage");
+  static_assert((2 * STAGE + RED_FLOATS) * 4 <= 160 * 1024, "LDS");
+};
 
 struct W2Args {
   const float* x;     // [N][H][W][KC]
@@ -61,6 +68,7 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 
 // U = G g G^T, G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]; one thread per (co block, chunk,
 // channel, co) writes its 16 components (c = 4a + b) as 4 float4
+template <int CO>
 __global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, float* __restrict__ wp) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
   const int nch = (KC + BK - 1) / BK, ncob = (NOUT + CO - 1) / CO;
@@ -209,7 +217,7 @@ __device__ __forceinline__ void w2_partial(const f32x4 (&acc)[2][8], int h, int 
 // epilogue: lane holds M[comp (half CH)][tile 4*kk + r of the group][co j0 + 32 cg + 16 h + (lane & 15)];
 // the two component halves of (tg, cg) swap the partial outputs of the co half the other finishes
 // through xb (a free LDS stage), in two rounds of two tiles per lane
-template <bool DGRAD, int CH>
+template <bool DGRAD, int CH, int CO>
 __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, int w0, int j0, int spatial,
                                                 const f32x4 (&acc)[2][8], float* xb, float* red, float bias) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kk = lane >> 4;
@@ -289,9 +297,11 @@ struct W2Block {
   unsigned gin, gzero;
 };
 
-template <bool DGRAD, int CH>
-__device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, const unsigned (&goff)[NGL],
+template <bool DGRAD, int CH, int CO_>
+__device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, const unsigned (&goff)[W2Cfg<CO_>::NGL],
                                             float* smem) {
+  using C = W2Cfg<CO_>;
+  constexpr int CO = C::CO, NT = C::NT, NGL = C::NGL, UGL = C::UGL, U_FLOATS = C::U_FLOATS, STAGE = C::STAGE;
   float* red = smem + 2 * STAGE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nchunks = B.nchunks, total = B.npass * nchunks;
@@ -344,7 +354,7 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
     int ne = B.n, h0e = B.h0, w0e = B.w0;
     asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
     float* xb = smem + ((gi - 1) & 1) * STAGE;
-    wino2h_epilogue<DGRAD, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    wino2h_epilogue<DGRAD, CH, CO>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
     if (p + 1 < B.npass) {  // block-uniform: restore the zero units the exchange overwrote
 #pragma unroll
       for (int r = 0; r < NGL; ++r)
@@ -360,9 +370,11 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
 #undef PMU_GLDS
 }
 
-template <bool DGRAD>
-__global__ __launch_bounds__(NT, 1) void conv3x3_wino2h_kernel(W2Args a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
+template <bool DGRAD, int CO_>
+__global__ __launch_bounds__(16 * CO_, 1) void conv3x3_wino2h_kernel(W2Args a) {
+  using C = W2Cfg<CO_>;
+  constexpr int NT = C::NT, NGL = C::NGL, STAGE = C::STAGE;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + C::RED_FLOATS];
   const int tid = threadIdx.x;
   const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
   const int ncog = (a.nco + a.cpb - 1) / a.cpb;
@@ -399,8 +411,17 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino2h_kernel(W2Args a) {
   }
   B.gin = gin;
   B.gzero = gzero;
-  if ((tid >> 8) & 1) wino2h_main<DGRAD, 1>(a, B, goff, smem);
-  else wino2h_main<DGRAD, 0>(a, B, goff, smem);
+  if ((tid >> 8) & 1) wino2h_main<DGRAD, 1, CO_>(a, B, goff, smem);
+  else wino2h_main<DGRAD, 0, CO_>(a, B, goff, smem);
+}
+
+// output channels per block (PMU_WINO2H_CO=32: 512-thread blocks, two per CU; A/B)
+static int w2h_co() {
+  static const int v = [] {
+    const char* e = getenv("PMU_WINO2H_CO");
+    return (e && atoi(e) == 32) ? 32 : 64;
+  }();
+  return v;
 }
 
 int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
@@ -413,6 +434,7 @@ int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, 
   a.H = H; a.W = W; a.KC = KC; a.NOUT = NOUT; a.split = split;
   a.bw = pmu_cdiv(W, OW);
   a.bh = pmu_cdiv(H, OH);
+  const int CO = w2h_co();
   a.nco = pmu_cdiv(NOUT, CO);
   const long long spatial = (long long)a.bw * a.bh * N;
   static const int cpb_env = [] {
@@ -433,8 +455,11 @@ int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, 
   const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
-  if (dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false>), dim3((unsigned)blocks), dim3(NT), 0, st, a);
+  const dim3 grid((unsigned)blocks);
+  if (CO == 32 && dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, 32>), grid, dim3(512), 0, st, a);
+  else if (CO == 32) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, 32>), grid, dim3(512), 0, st, a);
+  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, 64>), grid, dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, 64>), grid, dim3(1024), 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -445,14 +470,18 @@ extern "C" int pmu_conv3x3_tiles_wino2h(int N, int H, int W) { return N * pmu_cd
 
 extern "C" size_t pmu_conv3x3_packed_size_wino2h(int Cout, int Cin, int dgrad) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
-  return (size_t)pmu_cdiv(NOUT, CO) * pmu_cdiv(KC, BK) * U_FLOATS * sizeof(float);
+  const int CO = w2h_co();
+  return (size_t)pmu_cdiv(NOUT, CO) * pmu_cdiv(KC, BK) * (BK * CO * NCP) * sizeof(float);
 }
 
 extern "C" int pmu_conv3x3_pack_wino2h(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream) {
   PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
   const long long total = (long long)pmu_conv3x3_packed_size_wino2h(Cout, Cin, dgrad) / sizeof(float) / NCP;
   const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(pack_wino2h_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
+  if (w2h_co() == 32)
+    hipLaunchKernelGGL(pack_wino2h_kernel<32>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
+  else
+    hipLaunchKernelGGL(pack_wino2h_kernel<64>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
