@@ -433,7 +433,14 @@ void wgw_geometry(int N, int H, int W, int Cout, int Cin, WgwArgs& a) {
   a.ntiles = N * a.tiles_w * a.tiles_h;
   a.nco = Cout / wgw_wco(Cout);
   const int blocks_mn = a.nco * (Cin / WCI);
-  int s = 512 / blocks_mn;  // ~2 blocks per CU over the launch
+  static const int target_env = [] {  // PMU_WGW_BLOCKS: workgroups the split-K aims for (A/B)
+    const char* e = getenv("PMU_WGW_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  // one wave of workgroups: 256 of the 1024-thread 64-channel blocks (one per CU; 320 / 512 / 768
+  // measured 19.2 / 13.4 / 14.2 ms vs 12.9-13.0 ms per c2 step), 512 of the 512-thread ones (two per CU)
+  const int target = target_env > 0 ? target_env : (wgw_wco(Cout) == 64 ? 256 : 512);
+  int s = target / blocks_mn;
   if (s < 1) s = 1;
   if (s > a.ntiles) s = a.ntiles;
   a.nsplit = s;
