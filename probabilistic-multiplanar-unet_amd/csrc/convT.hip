@@ -725,7 +725,11 @@ static void convT_wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* tw
   *tiles_h = pmu_cdiv(H, TH);
   *ntiles = N * *tiles_w * *tiles_h;
   const int bmn = pmu_cdiv(Cin, TB) * pmu_cdiv(Cout, TB);
-  int sp = 1024 / bmn;
+  static const int target = [] {  // PMU_CONVT_WBLOCKS: workgroups the split-K aims for (A/B)
+    const char* e = getenv("PMU_CONVT_WBLOCKS");
+    return e ? atoi(e) : 512;  // one wave of the 2-per-CU workgroups: 1.68 -> 1.54 ms per c2 step (1024 before)
+  }();
+  int sp = target / bmn;
   if (sp < 1) sp = 1;
   if (sp > *ntiles) sp = *ntiles;
   *nsplit = sp;

@@ -450,7 +450,11 @@ __global__ __launch_bounds__(256) void convT_dbias_sum_kernel(const float* __res
 static void twb_geometry(int N, int H, int W, int Cin, int Cout, int* ntiles, int* nsplit) {
   *ntiles = (int)(((long long)N * H * W + WPX - 1) / WPX);
   const int bmn = pmu_cdiv(Cin, WCI) * pmu_cdiv(Cout, WCO);
-  int sp = 512 / bmn;
+  static const int target = [] {  // PMU_CONVT_BWBLOCKS: workgroups the split-K aims for (A/B)
+    const char* e = getenv("PMU_CONVT_BWBLOCKS");
+    return e ? atoi(e) : 512;
+  }();
+  int sp = target / bmn;
   if (sp < 1) sp = 1;
   if (sp > *ntiles) sp = *ntiles;
   *nsplit = sp;

@@ -308,7 +308,12 @@ static void geometry(int N, int H, int W, int Cin, int Cout, int* wco, int* twl,
   *tiles_h = pmu_cdiv(H, TH);
   *ntiles = N * *tiles_w * *tiles_h;
   const int blocks_mn = pmu_cdiv(Cout, *wco) * pmu_cdiv(Cin, WCI);
-  int s = 512 / blocks_mn;  // ~2 rounds of one block per CU (fewer splits: smaller slabs to reduce)
+  static const int target = [] {  // PMU_WGB_BLOCKS: workgroups the split-K aims for (A/B)
+    const char* e = getenv("PMU_WGB_BLOCKS");
+    return e ? atoi(e) : 256;
+  }();
+  // one round of one block per CU: c5 6.41 -> 5.9 ms per step (512: two rounds; 128 / 192: 9.8 / 7.2 ms)
+  int s = target / blocks_mn;
   if (s < 1) s = 1;
   if (s > *ntiles) s = *ntiles;
   *nsplit = s;
