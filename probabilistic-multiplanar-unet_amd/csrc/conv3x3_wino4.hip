@@ -58,6 +58,7 @@ struct W4Args {
   float* part;        // [spatial blocks][2][NOUT] BN partial sums (fwd) or null
   int H, W, KC, NOUT, split, bw, bh, nco, cpb;
   int prio;           // 1: waves of component half 1 run at s_setprio 1 (PMU_WINO4_PRIO)
+  int ts, tc;         // 2-D workgroup grouping (spatial x co-groups per group; tc = 0: co-groups fastest)
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -509,8 +510,20 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
   const int ncog = (a.nco + a.cpb - 1) / a.cpb;
   W4Block B;
-  B.cob0 = (lb % ncog) * a.cpb;
-  int sp = lb / ncog;
+  int cg, sp;
+  if (a.tc > 0) {
+    // 2-D grouping (the host checked ncog % tc == 0 and spatial % ts == 0): an XCD's consecutive
+    // workgroups cover ts spatial blocks x tc co-groups, so its L2 holds ts operand images and tc U
+    // slices at a time instead of 1 image and all U slices
+    const int gsz = a.ts * a.tc, g = lb / gsz, i = lb - g * gsz;
+    const int gpr = ncog / a.tc;
+    cg = (g % gpr) * a.tc + i % a.tc;
+    sp = (g / gpr) * a.ts + i / a.tc;
+  } else {
+    cg = lb % ncog;
+    sp = lb / ncog;
+  }
+  B.cob0 = cg * a.cpb;
   B.spatial = sp;
   const int bx = sp % a.bw; sp /= a.bw;
   const int by = sp % a.bh;
@@ -587,6 +600,18 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
     return e ? atoi(e) : 0;
   }();
   a.prio = prio;
+  static const int grp = [] {  // PMU_WINO4_GROUP=0: co-groups fastest (A/B)
+    const char* e = getenv("PMU_WINO4_GROUP");
+    return e ? atoi(e) : 1;
+  }();
+  {
+    const int ncog = pmu_cdiv(a.nco, cpb);
+    a.tc = 0; a.ts = 0;
+    if (grp) {
+      const int tc = ncog < 8 ? ncog : 8, ts = 32 / tc;
+      if (ncog % tc == 0 && spatial % ts == 0 && tc > 1 && ts > 1) { a.tc = tc; a.ts = ts; }
+    }
+  }
   const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
