@@ -74,11 +74,22 @@ __global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Ci
   const int nch = (KC + BK - 1) / BK, ncob = (NOUT + CO - 1) / CO;
   const long long total = (long long)ncob * nch * BK * CO;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const int col = (int)(e % CO);
-    long long r = e / CO;
-    const int kl = (int)(r % BK); r /= BK;
-    const int ch = (int)(r % nch);
-    const int jb = (int)(r / nch);
+    // consecutive threads read consecutive 3x3 filters: along the reduction channel (forward:
+    // w[co][ci]) or the output channel (dgrad: w[co][ci] with ci the output)
+    int col, kl, ch, jb;
+    if (dgrad) {
+      col = (int)(e % CO);
+      long long r = e / CO;
+      kl = (int)(r % BK); r /= BK;
+      ch = (int)(r % nch);
+      jb = (int)(r / nch);
+    } else {
+      kl = (int)(e % BK);
+      long long r = e / BK;
+      ch = (int)(r % nch); r /= nch;
+      col = (int)(r % CO);
+      jb = (int)(r / CO);
+    }
     const int j = jb * CO + col, k = ch * BK + kl;
     float g[3][3];
     for (int a = 0; a < 3; ++a)

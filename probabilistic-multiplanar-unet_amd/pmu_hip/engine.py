@@ -242,7 +242,6 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         elif use_wino():
             R = lb.pmu_conv3x3_tiles_wino(N, H, W)
             part = _empty(R, 2 * Cout, device=dev) if need_stats else None
-            wp = pack_weights_wino(conv.weight, dgrad=False)
             if wino_raw_ok(Cin) and wino2h_ok(Cin):
                 # 1024-thread F(2x2) workgroups (four waves per SIMD) on the materialised operand
                 xm = frame_to_f32(srcs, N, H, W)
@@ -253,11 +252,13 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             elif wino_raw_ok(Cin):
                 # the operand materialised once (the weight gradient's operand anyway), then a
                 # DMA-staged Winograd GEMM on it
+                wp = pack_weights_wino(conv.weight, dgrad=False)
                 xm = frame_to_f32(srcs, N, H, W)
                 L.call("pmu_conv3x3_fwd_wino_raw", xm.data_ptr(), Cin, N, H, W, wp.data_ptr(), L.ptr(conv.bias),
                        Cout, z.data_ptr(), L.ptr(part), s)
                 xt32 = xm if xt32 is not None else None
             else:
+                wp = pack_weights_wino(conv.weight, dgrad=False)
                 L.call("pmu_conv3x3_fwd_wino", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout,
                        z.data_ptr(), L.ptr(part), L.ptr(xt32), s)
         else:
