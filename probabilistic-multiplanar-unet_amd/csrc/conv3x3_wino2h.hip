@@ -66,30 +66,36 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+__device__ __forceinline__ void wino2_u(const float (&g)[3][3], float (&u)[16]) {
+  float t[4][3];
+  for (int b = 0; b < 3; ++b) {
+    t[0][b] = g[0][b];
+    t[1][b] = 0.5f * (g[0][b] + g[1][b] + g[2][b]);
+    t[2][b] = 0.5f * (g[0][b] - g[1][b] + g[2][b]);
+    t[3][b] = g[2][b];
+  }
+  for (int a = 0; a < 4; ++a) {
+    u[4 * a + 0] = t[a][0];
+    u[4 * a + 1] = 0.5f * (t[a][0] + t[a][1] + t[a][2]);
+    u[4 * a + 2] = 0.5f * (t[a][0] - t[a][1] + t[a][2]);
+    u[4 * a + 3] = t[a][2];
+  }
+}
+
 // U = G g G^T, G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1]; one thread per (co block, chunk,
-// channel, co) writes its 16 components (c = 4a + b) as 4 float4
+// channel, co) writes its 16 components (c = 4a + b) as 4 float4 (input-gradient packing: consecutive
+// threads read consecutive filters w[co][ci..])
 template <int CO>
 __global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, float* __restrict__ wp) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
   const int nch = (KC + BK - 1) / BK, ncob = (NOUT + CO - 1) / CO;
   const long long total = (long long)ncob * nch * BK * CO;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    // consecutive threads read consecutive 3x3 filters: along the reduction channel (forward:
-    // w[co][ci]) or the output channel (dgrad: w[co][ci] with ci the output)
-    int col, kl, ch, jb;
-    if (dgrad) {
-      col = (int)(e % CO);
-      long long r = e / CO;
-      kl = (int)(r % BK); r /= BK;
-      ch = (int)(r % nch);
-      jb = (int)(r / nch);
-    } else {
-      kl = (int)(e % BK);
-      long long r = e / BK;
-      ch = (int)(r % nch); r /= nch;
-      col = (int)(r % CO);
-      jb = (int)(r / CO);
-    }
+    const int col = (int)(e % CO);
+    long long r = e / CO;
+    const int kl = (int)(r % BK); r /= BK;
+    const int ch = (int)(r % nch);
+    const int jb = (int)(r / nch);
     const int j = jb * CO + col, k = ch * BK + kl;
     float g[3][3];
     for (int a = 0; a < 3; ++a)
@@ -99,25 +105,40 @@ __global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Ci
           v = dgrad ? w[((long long)k * Cin + j) * 9 + (2 - a) * 3 + (2 - b)] : w[((long long)j * Cin + k) * 9 + a * 3 + b];
         g[a][b] = v;
       }
-    float t[4][3];
-    for (int b = 0; b < 3; ++b) {
-      t[0][b] = g[0][b];
-      t[1][b] = 0.5f * (g[0][b] + g[1][b] + g[2][b]);
-      t[2][b] = 0.5f * (g[0][b] - g[1][b] + g[2][b]);
-      t[3][b] = g[2][b];
-    }
     float u[16];
-    for (int a = 0; a < 4; ++a) {
-      u[4 * a + 0] = t[a][0];
-      u[4 * a + 1] = 0.5f * (t[a][0] + t[a][1] + t[a][2]);
-      u[4 * a + 2] = 0.5f * (t[a][0] - t[a][1] + t[a][2]);
-      u[4 * a + 3] = t[a][2];
-    }
+    wino2_u(g, u);
     float* dst = wp + (((long long)jb * nch + ch) * BK + kl) * (CO * NCP) + col * NCP;
     for (int q = 0; q < 4; ++q)
       *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
     *reinterpret_cast<float4*>(dst + 16) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+}
+
+// Forward packing, one workgroup per (co block, chunk): the 8 x CO filters w[co][ci0..ci0+7] are read
+// along ci (8 lanes cover 288 contiguous bytes), transformed into LDS in the packed order, and the
+// workgroup's contiguous BK x CO x NCP segment is stored with consecutive float4s.
+template <int CO>
+__global__ __launch_bounds__(256) void pack_wino2h_fwd_kernel(const float* __restrict__ w, int Cout, int Cin,
+                                                              float* __restrict__ wp) {
+  constexpr int SEG = BK * CO * NCP;
+  __shared__ float4 seg4[SEG / 4];
+  const int nch = (Cin + BK - 1) / BK;
+  const int ch = blockIdx.x % nch, jb = blockIdx.x / nch;
+  for (int f = threadIdx.x; f < BK * CO; f += blockDim.x) {
+    const int kl = f % BK, col = f / BK;
+    const int j = jb * CO + col, k = ch * BK + kl;
+    float g[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) g[a][b] = (j < Cout && k < Cin) ? w[((long long)j * Cin + k) * 9 + a * 3 + b] : 0.f;
+    float u[16];
+    wino2_u(g, u);
+    float4* d = seg4 + (kl * CO + col) * (NCP / 4);
+    for (int q = 0; q < 4; ++q) d[q] = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
+    d[4] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  float4* dst = reinterpret_cast<float4*>(wp + (long long)blockIdx.x * SEG);
+  for (int i = threadIdx.x; i < SEG / 4; i += blockDim.x) dst[i] = seg4[i];
 }
 
 template <int OFF>
@@ -489,7 +510,13 @@ extern "C" int pmu_conv3x3_pack_wino2h(const float* w, int Cout, int Cin, int dg
   PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
   const long long total = (long long)pmu_conv3x3_packed_size_wino2h(Cout, Cin, dgrad) / sizeof(float) / NCP;
   const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  if (w2h_co() == 32)
+  if (!dgrad) {  // one workgroup per (co block, chunk) segment
+    const unsigned segs = (unsigned)(pmu_cdiv(Cout, w2h_co()) * pmu_cdiv(Cin, BK));
+    if (w2h_co() == 32)
+      hipLaunchKernelGGL(pack_wino2h_fwd_kernel<32>, dim3(segs), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, wp);
+    else
+      hipLaunchKernelGGL(pack_wino2h_fwd_kernel<64>, dim3(segs), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, wp);
+  } else if (w2h_co() == 32)
     hipLaunchKernelGGL(pack_wino2h_kernel<32>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
   else
     hipLaunchKernelGGL(pack_wino2h_kernel<64>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
