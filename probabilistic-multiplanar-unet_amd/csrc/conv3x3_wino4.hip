@@ -78,17 +78,19 @@ __device__ __forceinline__ void g6(const double (&g)[3], double (&t)[6]) {
   t[5] = g[2];
 }
 
-// one thread per (co block, chunk, channel, co) writes its 36 components as 9 float4
-__global__ void pack_wino4_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, float* __restrict__ wp) {
+// One workgroup per (co block, chunk): the BK x CO filters are transformed into LDS in the packed
+// order and the contiguous BK x CO x 36 segment is stored with consecutive float4s. Consecutive
+// threads read consecutive filters: along the output channel for the input gradient (w[k][j..]),
+// along the reduction channel for the forward (w[j][k..]).
+__global__ __launch_bounds__(256) void pack_wino4_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
+                                                         float* __restrict__ wp) {
+  constexpr int SEG = BK * CO * NC;
+  __shared__ float4 seg4[SEG / 4];
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
-  const int nch = (KC + BK - 1) / BK, ncob = (NOUT + CO - 1) / CO;
-  const long long total = (long long)ncob * nch * BK * CO;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const int col = (int)(e % CO);
-    long long r = e / CO;
-    const int kl = (int)(r % BK); r /= BK;
-    const int ch = (int)(r % nch);
-    const int jb = (int)(r / nch);
+  const int nch = (KC + BK - 1) / BK;
+  const int ch = blockIdx.x % nch, jb = blockIdx.x / nch;
+  for (int f = threadIdx.x; f < BK * CO; f += blockDim.x) {
+    const int col = dgrad ? f % CO : f / BK, kl = dgrad ? f / CO : f % BK;
     const int j = jb * CO + col, k = ch * BK + kl;
     double g[3][3];
     for (int a = 0; a < 3; ++a)
@@ -114,10 +116,12 @@ __global__ void pack_wino4_kernel(const float* __restrict__ w, int Cout, int Cin
     }
     float row[36];   // the row in component-half order (upos)
     for (int c = 0; c < 36; ++c) row[upos(c / 18, c % 18)] = u[c];
-    float* dst = wp + (((long long)jb * nch + ch) * BK + kl) * (CO * NC) + col * NC;
-    for (int q = 0; q < 9; ++q)
-      *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+    float4* d = seg4 + (kl * CO + col) * (NC / 4);
+    for (int q = 0; q < 9; ++q) d[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
   }
+  __syncthreads();
+  float4* dst = reinterpret_cast<float4*>(wp + (long long)blockIdx.x * SEG);
+  for (int i = threadIdx.x; i < SEG / 4; i += blockDim.x) dst[i] = seg4[i];
 }
 
 // B^T row on d0..d5, B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
@@ -635,9 +639,9 @@ extern "C" size_t pmu_conv3x3_packed_size_wino4(int Cout, int Cin, int dgrad) {
 
 extern "C" int pmu_conv3x3_pack_wino4(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream) {
   PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
-  const long long total = (long long)pmu_conv3x3_packed_size_wino4(Cout, Cin, dgrad) / sizeof(float) / NC;
-  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(pack_wino4_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  const unsigned segs = (unsigned)(pmu_cdiv(NOUT, CO) * pmu_cdiv(KC, BK));  // one workgroup per segment
+  hipLaunchKernelGGL(pack_wino4_kernel, dim3(segs), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad, wp);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
