@@ -1,0 +1,74 @@
+"""GPU check of the Winograd weight packs (pmu_conv3x3_pack_wino2h / _pack_wino4) against an fp64
+restatement of the packed layout, on ragged channel counts (partial co blocks and chunks are zero).
+
+Layouts (csrc/conv3x3_wino2h.hip, csrc/conv3x3_wino4.hip): [co block][chunk of 8][ci in chunk][co in
+block][components]; F(2x2): 64 co per block, components 4a+b of G g G^T plus 4 zero pad; F(4x4): 32 co
+per block, the 36 components 6a+b of G g G^T in component-half order (upos).  The input-gradient
+packs transform w[co][ci] rotated by 180 degrees, with ci as the output channel.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+G2 = torch.tensor([[1, 0, 0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0, 0, 1]], dtype=torch.float64)
+G4 = torch.tensor([[1 / 4, 0, 0], [-1 / 6, -1 / 6, -1 / 6], [-1 / 6, 1 / 6, -1 / 6], [1 / 24, 1 / 12, 1 / 6],
+                   [1 / 24, -1 / 12, 1 / 6], [0, 0, 1]], dtype=torch.float64)
+
+
+def _upos(half, cl):
+    return 16 * half + cl if cl < 16 else 32 + 2 * half + (cl - 16)
+
+
+def _expected(w, dgrad, G, CO, ncp, order=None):
+    w = w.double().cpu()
+    if dgrad:  # filters indexed [out = ci][reduction = co], rotated
+        w = w.flip(2, 3).transpose(0, 1)
+    nout, kc = w.shape[:2]
+    u = torch.einsum("ia,jkab,lb->jkil", G, w, G).reshape(nout, kc, -1)  # [out][k][comp]
+    nco, nch = -(-nout // CO), -(-kc // 8)
+    ncomp = u.shape[2]
+    full = torch.zeros(nco * CO, nch * 8, ncomp, dtype=torch.float64)
+    full[:nout, :kc] = u
+    if order is not None:
+        full = full[:, :, order]
+    if ncp > ncomp:
+        full = torch.cat([full, torch.zeros(full.shape[0], full.shape[1], ncp - ncomp, dtype=torch.float64)], 2)
+    # [co block][col][chunk][kl][comp] -> [co block][chunk][kl][col][comp]
+    return full.reshape(nco, CO, nch, 8, ncp).permute(0, 2, 3, 1, 4).contiguous().reshape(-1)
+
+
+_ORDER4 = [0] * 36
+for _c in range(36):
+    _ORDER4[_upos(_c // 18, _c % 18)] = _c
+
+
+@pytest.mark.parametrize("Cout,Cin", [(64, 64), (40, 24), (128, 72), (96, 8)])
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_pack_wino2h(dev, Cout, Cin, dgrad):
+    from pmu_hip import _lib as L
+    g = torch.Generator().manual_seed(Cout * 7 + Cin)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g).to(dev)
+    n = L.lib().pmu_conv3x3_packed_size_wino2h(Cout, Cin, int(dgrad)) // 4
+    wp = torch.full((n,), float("nan"), device=dev)
+    L.call("pmu_conv3x3_pack_wino2h", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = _expected(w, dgrad, G2, 64, 20)
+    assert ref.numel() == n
+    assert float((wp.double().cpu() - ref).abs().max()) <= 1e-6 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("Cout,Cin", [(64, 64), (40, 24), (96, 72), (32, 8)])
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_pack_wino4(dev, Cout, Cin, dgrad):
+    from pmu_hip import _lib as L
+    g = torch.Generator().manual_seed(Cout * 5 + Cin)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g).to(dev)
+    n = L.lib().pmu_conv3x3_packed_size_wino4(Cout, Cin, int(dgrad)) // 4
+    wp = torch.full((n,), float("nan"), device=dev)
+    L.call("pmu_conv3x3_pack_wino4", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = _expected(w, dgrad, G4, 32, 36, order=_ORDER4)
+    assert ref.numel() == n
+    # U is computed in double and rounded once: equal to the fp64 restatement rounded to fp32
+    assert float((wp.double().cpu() - ref.float().double()).abs().max()) <= 1e-7 * float(ref.abs().max())
