@@ -190,6 +190,11 @@ class BNSync:
             self.base[i] = int(m.num_batches_tracked)
 
 
+def _sync(device):
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+
+
 def _from_rank(value, src, dev):
     """A float held by rank ``src`` on every rank (the reference logs the last micro-batch's loss)."""
     world, rank = world_info()
@@ -200,11 +205,30 @@ def _from_rank(value, src, dev):
     return float(t)
 
 
+def reference_acc_steps(batch_size):
+    """The reference's gradient-accumulation rule (:44-45)."""
+    return 4 if batch_size > 4 else 1
+
+
 def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2, om=0.9, val_percent=0.1,
-              save_cp=False, dataset=None, writer=None):
+              save_cp=False, dataset=None, writer=None, acc_steps=None, dtype="fp32", stats=None,
+              optimizer_factory=None):
     """train.py:27-196.  ``dataset`` (an MRI_Dataset; default: built from dir_img/dir_mask) and
-    ``writer`` (a SummaryWriter-like sink; default: TensorBoard when installed) are injectable."""
-    from pmu_hip.optim import FusedSGD
+    ``writer`` (a SummaryWriter-like sink; default: TensorBoard when installed) are injectable.
+
+    Build-side options (all default to the reference's behaviour):
+      acc_steps: micro-batches per optimizer step (None: the reference's 4 if batch_size > 4 else 1).
+        The global batch stays ``batch_size`` = acc_steps micro-batches of batch_size // acc_steps,
+        with loss / acc_steps.  Config c3 — 8 ranks x 32 slices — is ``batch_size=256, acc_steps=8``
+        on 8 ranks: one micro-batch of 32 per rank per step, the reference's accumulation of 8
+        micro-batches (:95-110).
+      dtype: "bf16" runs the predictions under torch.autocast("cuda", bfloat16) (config c5's
+        arithmetic on the bf16-MFMA kernels); "fp32" is the reference's.
+      stats: a list that receives one dict per epoch with the train phase's throughput.
+      optimizer_factory: params -> optimizer (default: FusedSGD(lr, momentum=om, clip=0.1), the
+        reference's clip_grad_value_(0.1) + SGD(lr, momentum=om) in one kernel)."""
+    import time
+    from contextlib import nullcontext
     from utils.mri_dataset import MRI_Dataset
 
     world, rank = world_info()
@@ -216,8 +240,16 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
         train, val = random_split(dataset, [n_train, n_val])
     else:
         train, val = random_split(dataset, [n_train, n_val], generator=shared_generator())
-    acc_steps = 4 if batch_size > 4 else 1
+    if acc_steps is None:
+        acc_steps = reference_acc_steps(batch_size)
+    if acc_steps < 1 or batch_size // acc_steps < 1:
+        raise ValueError(f"batch size {batch_size} cannot be split into {acc_steps} micro-batches")
     micro = batch_size // acc_steps
+    if dtype not in ("fp32", "bf16"):
+        raise ValueError(f"dtype must be fp32 or bf16, not {dtype!r}")
+
+    def precision():
+        return torch.autocast("cuda", dtype=torch.bfloat16) if dtype == "bf16" else nullcontext()
     if writer is None:
         writer = _writer(f"LRF_{lrf}_LRP_{lrp}_EP_{epochs}_LR_{lr}_BS_{batch_size}") if rank == 0 else _NullWriter()
     elif rank != 0:
@@ -229,7 +261,11 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
         logging.warning(f"{world} ranks > {acc_steps} accumulation micro-batches per step: {world - acc_steps} "
                         f"rank(s) idle each step (the global batch stays {batch_size}, as in the reference)")
     net = trainer.net
-    optimizer = FusedSGD(net.parameters(), lr=lr, momentum=om, clip=0.1)
+    if optimizer_factory is None:
+        from pmu_hip.optim import FusedSGD
+        optimizer = FusedSGD(net.parameters(), lr=lr, momentum=om, clip=0.1)
+    else:
+        optimizer = optimizer_factory(net.parameters())
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, "min" if net.n_classes > 1 else "max",
                                                            factor=lrf, patience=lrp)
     plist = list(net.parameters())
@@ -246,13 +282,17 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
         steps, leftover = dp_micro_batches(order, micro, acc_steps, world, rank)
         scale = 1.0 / acc_steps
         optimizer.zero_grad()
+        if stats is not None:
+            _sync(device)
+            t0 = time.perf_counter()
         for s, step_mbs in enumerate(steps):
             last = None
             for i, mb in enumerate(step_mbs):
                 b = dataset.get_batch(mb)
                 imgs = b["image"]
                 true_masks = b["mask"].to(dtype=trainer.mask_type)
-                masks_pred = trainer.predict(imgs, true_masks)
+                with precision():
+                    masks_pred = trainer.predict(imgs, true_masks)
                 loss = trainer.loss(imgs, true_masks, masks_pred) * scale
                 if sync is not None and i == len(step_mbs) - 1:
                     sync.begin()      # the last micro-batch's backward issues the bucket all-reduces
@@ -271,11 +311,25 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
             writer.add_scalar("Loss/train", out_loss, global_step + s * acc_steps + acc_steps - 1)
             optimizer.step()
             optimizer.zero_grad()
-        if leftover:   # trailing micro-batches: forward for their BatchNorm statistics, no step
-            with torch.no_grad():
-                for mb in leftover:
-                    b = dataset.get_batch(mb)
-                    trainer.predict(b["image"], b["mask"].to(dtype=trainer.mask_type))
+        if stats is not None:
+            _sync(device)
+            if world > 1:
+                dist.barrier()
+            dt = time.perf_counter() - t0
+            stats.append({"epoch": epoch, "optimizer_steps": len(steps), "slices": len(steps) * micro * acc_steps,
+                          "seconds": dt, "slices_per_s": len(steps) * micro * acc_steps / dt if dt > 0 else 0.0,
+                          "ranks": world, "acc_steps": acc_steps, "micro_batch": micro, "dtype": dtype})
+        # Trailing micro-batches that fill no step: the reference runs predict, loss and backward on
+        # them (:77-98) and its validation zero_grad drops the gradient (:122).  Predict and loss run
+        # here exactly as in a step (grad enabled: the posterior encoder runs and updates its BatchNorm
+        # statistics, the posterior sample is drawn); the backward, whose result is discarded, is not.
+        for mb in leftover:
+            b = dataset.get_batch(mb)
+            imgs, true_masks = b["image"], b["mask"].to(dtype=trainer.mask_type)
+            with precision():
+                masks_pred = trainer.predict(imgs, true_masks)
+            trainer.loss(imgs, true_masks, masks_pred)
+            del masks_pred
         global_step += n_train_mb
         # ---- validation phase (replicas agree on BN statistics; every rank evaluates the split)
         bn_sync()
@@ -288,7 +342,8 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
             b = dataset.get_batch(mb)
             imgs, true_masks = b["image"], b["mask"].to(dtype=trainer.mask_type)
             with torch.no_grad():
-                masks_pred = trainer.predict(imgs, true_masks)
+                with precision():
+                    masks_pred = trainer.predict(imgs, true_masks)
                 dice = trainer.eval(imgs, true_masks, masks_pred)
                 loss_sum += trainer.loss(imgs, true_masks, masks_pred).item()
             if net.n_classes > 1:
@@ -326,7 +381,7 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
     writer.close()
 
 
-def get_args():
+def get_args(argv=None):
     parser = argparse.ArgumentParser(description="Train the UNet on images and target masks",
                                      formatter_class=argparse.ArgumentDefaultsHelpFormatter)
     parser.add_argument("-e", "--epochs", metavar="E", type=int, default=5, help="Number of epochs", dest="epochs")
@@ -346,24 +401,98 @@ def get_args():
                         help="Percent of the data that is used as validation (0-100)")
     parser.add_argument("-m", "--model", dest="net", type=str, default="unet", help="what model to use: unet or probunet")
     parser.add_argument("-d", "--dir", dest="dir", type=str, default=None, help="image and label superdirs.")
-    return parser.parse_args()
+    # build-side flags; every default is the reference's behaviour
+    parser.add_argument("--acc-steps", dest="acc_steps", type=int, default=None,
+                        help="micro-batches per optimizer step (default: the reference's 4 if batch size > 4 else 1); "
+                             "c3 = 8 ranks x 32: -b 256 --acc-steps 8 on 8 ranks")
+    parser.add_argument("--dtype", dest="dtype", choices=["fp32", "bf16"], default="fp32",
+                        help="bf16: predictions under torch.autocast(bfloat16) on the bf16-MFMA kernels (config c5)")
+    parser.add_argument("--filters", dest="filters", type=str, default=None,
+                        help="comma-separated num_filters of the U-Net (default 64,128,256,512,1024)")
+    parser.add_argument("--classes", dest="classes", type=int, default=None,
+                        help="number of classes (default: 1 for unet, 3 for probunet, as the reference's __main__)")
+    parser.add_argument("--channels", dest="channels", type=int, default=1, help="input channels per slice")
+    parser.add_argument("--nproc", dest="nproc", type=int, default=1,
+                        help="launch this many ranks on this node, one per GPU (torch.distributed.run, RCCL); "
+                             "ignored when already launched by torchrun")
+    parser.add_argument("--bench", dest="bench", action="store_true",
+                        help="train on a seeded synthetic ellipsoid phantom resident on the GPU (no data "
+                             "directory) and print the train phase's throughput per epoch as JSON")
+    parser.add_argument("--bench-size", dest="bench_size", type=int, default=256, help="--bench phantom edge D (D^3)")
+    parser.add_argument("--bench-scans", dest="bench_scans", type=int, default=2, help="--bench phantom count")
+    return parser.parse_args(argv)
 
 
-def main():
+def _relaunch(nproc, argv):
+    """--nproc N outside torchrun: run this script under torch.distributed.run with N ranks as a child
+    process (nothing here has touched the GPU yet) and return its exit code."""
+    import socket
+    import subprocess
+    import sys
+    args, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a == "--nproc":
+            skip = True
+            continue
+        if a.startswith("--nproc="):
+            continue
+        args.append(a)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + args
+    return subprocess.call(cmd)
+
+
+def bench_dataset(n_classes, size, scans, device, seed=11):
+    """--bench data: ``scans`` seeded size^3 volumes — two nested ellipsoid shells (labels 1, 2 as the
+    knee labels of PMU/Utils/nii.py:83-90; 1 class: the union) under a noisy contrast — resident on
+    the GPU as an MRI_Dataset (filtered 3-view index map, as the reference's)."""
+    from utils.mri_dataset import MRI_Dataset
+    rng = np.random.default_rng(seed)
+    vols = {}
+    ax = np.arange(size) - size / 2
+    ii, jj, kk = np.meshgrid(ax, ax, ax, indexing="ij", sparse=True)
+    for s in range(scans):
+        a, b, c = 0.30 + 0.1 * rng.random(3)
+        r2 = (ii / (a * size)) ** 2 + (jj / (b * size)) ** 2 + (kk / (c * size)) ** 2
+        lab = np.where(r2 < 1.0, 1.0, 0.0)
+        if n_classes > 2:
+            lab = lab + np.where(r2 < 0.35, 1.0, 0.0)
+        img = rng.random((size, size, size)) * 200.0 + lab * 300.0
+        vols[f"scan{s}"] = (img, lab)
+    return MRI_Dataset("/bench/images", "/bench/labels", n_classes, filter=True, files=sorted(vols),
+                       loader=lambda p: vols[os.path.basename(p)][0 if "images" in p else 1], device=device)
+
+
+def main(argv=None):
     global dir_img, dir_mask
+    import json
+    import sys
     logging.basicConfig(level=logging.INFO, format="%(levelname)s: %(message)s")
-    args = get_args()
+    argv = sys.argv[1:] if argv is None else argv
+    args = get_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.nproc > 1 and "WORLD_SIZE" not in os.environ:
+        return _relaunch(args.nproc, argv)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     logging.info(f"Using device {device} with properties= {torch.cuda.get_device_properties(device)}")
+    filters = [int(f) for f in args.filters.split(",")] if args.filters else None
     if args.net == "unet":
-        trainer = UNetTrainer(device, n_channels=1, n_classes=1, load_model=args.load)
+        trainer = UNetTrainer(device, n_channels=args.channels, n_classes=args.classes or 1, load_model=args.load,
+                              num_filters=filters)
     elif args.net == "probunet":
-        trainer = ProbUNetTrainer(device, n_channels=1, n_classes=3, load_model=args.load, latent_dim=6, beta=10)
+        trainer = ProbUNetTrainer(device, n_channels=args.channels, n_classes=args.classes or 3, load_model=args.load,
+                                  latent_dim=6, beta=10, num_filters=filters)
     else:
         raise SystemExit(f"Error! {args.net} is not a valid model")
     if world > 1:  # identical replicas
@@ -372,15 +501,22 @@ def main():
     if args.dir is not None:
         dir_img = os.path.join(args.dir, "images")
         dir_mask = os.path.join(args.dir, "labels")
+    dataset = bench_dataset(trainer.net.n_classes, args.bench_size, args.bench_scans, device) if args.bench else None
+    stats = [] if args.bench else None
     try:
         train_net(trainer=trainer, epochs=args.epochs, batch_size=args.batchsize, lr=args.lr, lrf=args.lrf,
-                  lrp=args.lrp, om=args.om, device=device, val_percent=args.val / 100)
+                  lrp=args.lrp, om=args.om, device=device, val_percent=args.val / 100, dataset=dataset,
+                  acc_steps=args.acc_steps, dtype=args.dtype, stats=stats)
     except KeyboardInterrupt:
         torch.save(trainer.net.state_dict(), "INTERRUPTED.pth")
         logging.info("Saved interrupt")
+    if stats is not None and int(os.environ.get("RANK", "0")) == 0:
+        for st in stats:
+            print("TRAIN_BENCH " + json.dumps({"model": args.net, "batch_size": args.batchsize, **st}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())

@@ -11,12 +11,14 @@ from .trainer import Trainer, load_checkpoint, masks_to_rgb
 
 class ProbUNetTrainer(Trainer):
 
-    def __init__(self, device, n_channels=1, n_classes=1, load_model=None, latent_dim=6, beta=10):
+    def __init__(self, device, n_channels=1, n_classes=1, load_model=None, latent_dim=6, beta=10, num_filters=None):
+        """num_filters (extension, train.py --filters): None = the reference's [64..1024] (:16)."""
         self.device = device
         self.mask_type = torch.float32
         self.name = "probunet"
+        filters = [64, 128, 256, 512, 1024] if num_filters is None else list(num_filters)
         self.net = ProbabilisticUnet(input_channels=n_channels, num_classes=n_classes,
-                                     num_filters=[64, 128, 256, 512, 1024], latent_dim=latent_dim, no_convs_fcomb=4,
+                                     num_filters=filters, latent_dim=latent_dim, no_convs_fcomb=4,
                                      beta=beta)
         if load_model is not None:
             load_checkpoint(self.net, load_model, device)

@@ -16,11 +16,15 @@ from .trainer import Trainer, load_checkpoint, masks_to_rgb
 
 class UNetTrainer(Trainer):
 
-    def __init__(self, device, n_channels=1, n_classes=1, load_model=None):
+    def __init__(self, device, n_channels=1, n_classes=1, load_model=None, num_filters=None):
+        """num_filters (extension, train.py --filters): the U-Net widths; None = the reference's default."""
         self.device = device
         self.name = "unet"
         self.mask_type = torch.float32 if n_classes == 1 else torch.long
-        self.net = UNet(n_channels=n_channels, n_classes=n_classes)
+        if num_filters is None:
+            self.net = UNet(n_channels=n_channels, n_classes=n_classes)
+        else:
+            self.net = UNet(n_channels=n_channels, n_classes=n_classes, num_filters=list(num_filters))
         if load_model is not None:
             load_checkpoint(self.net, load_model, device)
         self.net = self.net.to(device)

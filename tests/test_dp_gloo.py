@@ -204,3 +204,86 @@ def test_dp_bucketed_overlap_matches_reference_accumulation(mode, world, acc):
                 assert issued == nb                   # the layout follows the learned (reversed) order too
             else:
                 assert issued == 0                    # foreign grads / idle rank: all at finish()
+
+
+# ------------------------------------------------------------------------ train_net itself (config c3)
+def _train_net_worker(rank, world, port, q, acc, overlap, ckpt_dir):
+    os.environ["PMU_DP_OVERLAP"] = overlap
+    _setup(rank, world, port)
+    try:
+        import train as T
+        from torch.utils.data import Subset
+        from oracle.unet_ref import trainer_dice, unet_forward, unet_loss
+        net, sd, x, t = _g7_net()
+        seen = []
+
+        class G7Slices:
+            """G7's 32 slices behind MRI_Dataset's batch interface (get_batch)."""
+            def __len__(self):
+                return x.shape[0]
+
+            def get_batch(self, idx):
+                seen.append([int(i) for i in idx])
+                i = torch.tensor([int(v) for v in idx])
+                return {"image": x[i], "mask": t[i]}
+
+        class OracleTrainer:
+            """UNetTrainer's interface on the CPU oracle over the module's own parameters and buffers
+            (the HIP forward needs a GPU; the data-parallel logic under test does not)."""
+            name, mask_type, device = "unet", torch.float32, torch.device("cpu")
+
+            def __init__(self):
+                self.net = net
+
+            def predict(self, imgs, masks):
+                return unet_forward(dict(net.state_dict(keep_vars=True)), imgs, 2, 1, training=net.training)
+
+            def loss(self, imgs, masks, pred):
+                return unet_loss(pred, masks, 1)
+
+            def eval(self, imgs, masks, pred):
+                return np.array(trainer_dice(pred, masks, 1))
+
+        class ClipSGD(torch.optim.SGD):
+            """clip_grad_value_(0.1) + SGD(momentum) (PMU/train.py:65,108-110) on CPU tensors."""
+            def step(self, closure=None):
+                torch.nn.utils.clip_grad_value_([p for g in self.param_groups for p in g["params"]], 0.1)
+                return super().step(closure)
+
+        # G7's micro-batch grouping: the split and the epoch order are identities here (the seeded
+        # shuffles are tested elsewhere), so micro-batch k is slices 4k..4k+3, as G7 accumulates them
+        T.random_split = lambda ds, lengths, generator=None: [Subset(ds, list(range(lengths[0]))),
+                                                              Subset(ds, list(range(lengths[0], sum(lengths))))]
+        T.epoch_order = lambda n, world: list(range(n))
+        T.dir_checkpoint = ckpt_dir + "/"
+        stats = []
+        T.train_net(OracleTrainer(), torch.device("cpu"), epochs=1, batch_size=4 * acc, lr=0.1, val_percent=0.0,
+                    dataset=G7Slices(), acc_steps=acc, stats=stats,
+                    optimizer_factory=lambda ps: ClipSGD(ps, lr=0.1, momentum=0.9))
+        out = {k: p.detach().numpy().copy() for k, p in net.named_parameters()}
+        q.put((rank, out, seen, stats))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,overlap", [(8, "1"), (8, "0"), (4, "1")])
+def test_train_net_dp_matches_reference_step(world, overlap, tmp_path):
+    """train.py's train_net on `world` gloo ranks with acc_steps=8, batch 32 (config c3's shape, 8
+    micro-batches of 4): every rank trains (at world 8 exactly one micro-batch per rank, no idle
+    rank) and the replicas end the step on the parameters of the reference's single-process step —
+    G7's accumulated gradient (8 micro-batches, loss / 8), clip_grad_value_(0.1), SGD(0.1, 0.9)."""
+    acc = 8
+    res = _run(_train_net_worker, world, acc, overlap, str(tmp_path))
+    z = np.load(os.path.join(GOLD, "g7_dp.npz"), allow_pickle=False)
+    init = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("init/")}
+    grads = {k[5:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("grad/")}
+    from oracle.unet_ref import sgd_clip_step
+    params = {k: init[k].clone() for k in grads}
+    sgd_clip_step(params, grads, {k: torch.zeros_like(v) for k, v in params.items()}, 0.1)
+    for rank, out, seen, stats in res:
+        assert len(seen) == acc // world, (rank, seen)          # no idle rank, an equal share each
+        assert [sorted(mb) for mb in seen] == [list(range(4 * k, 4 * k + 4)) for k in range(rank, acc, world)]
+        for k, want in params.items():
+            d = float((torch.from_numpy(out[k]) - want).abs().max())
+            assert d <= 1e-6, (rank, k, d)
+        assert stats and stats[0]["slices"] == 32 and stats[0]["optimizer_steps"] == 1

@@ -84,3 +84,71 @@ def test_train_loader_order_consumes_rng_like_the_reference():
     torch.manual_seed(5)
     assert train.loader_order(5, False, 1) == list(range(5))
     assert torch.equal(torch.rand(1), after_ref)
+
+
+def test_leftover_micro_batches_run_predict_and_loss_with_grad(tmp_path):
+    """Trailing micro-batches that fill no optimizer step run exactly as the reference runs them
+    (PMU/train.py:77-98): predict with grad enabled (for ProbUNetTrainer: the posterior encoder and
+    its BatchNorm statistics) and the loss (the posterior sample); no optimizer step follows."""
+    import train as T
+    events = []
+
+    class Net(torch.nn.Module):
+        n_classes = 1
+
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.ones(1))
+
+    net = Net()
+
+    class DS:
+        def __len__(self):
+            return 32
+
+        def get_batch(self, idx):
+            return {"image": torch.rand(len(idx), 1, 4, 4), "mask": torch.zeros(len(idx), 1, 4, 4)}
+
+    class Tr:
+        name, mask_type, device = "probe", torch.float32, torch.device("cpu")
+
+        def __init__(self):
+            self.net = net
+
+        def predict(self, imgs, masks):
+            events.append(("predict", torch.is_grad_enabled(), net.training))
+            return imgs.mean() * net.w
+
+        def loss(self, imgs, masks, pred):
+            events.append(("loss", torch.is_grad_enabled(), net.training))
+            return pred * 1.0
+
+        def eval(self, imgs, masks, pred):
+            return np.array([1.0])
+
+    steps = []
+
+    class SGDProbe(torch.optim.SGD):
+        def step(self, closure=None):
+            steps.append(1)
+            return super().step(closure)
+
+    T.dir_checkpoint = str(tmp_path) + "/"
+    # batch 12 -> acc_steps 4 (reference rule), micro-batch 3: 10 micro-batches = 2 steps + 2 leftover
+    T.train_net(Tr(), torch.device("cpu"), epochs=1, batch_size=12, lr=0.1, val_percent=0.0, dataset=DS(),
+                optimizer_factory=lambda ps: SGDProbe(ps, lr=0.1))
+    train_events = [e for e in events if e[2]]
+    assert len(steps) == 2
+    assert train_events == [("predict", True, True), ("loss", True, True)] * 10
+
+
+def test_acc_steps_flag_splits_the_global_batch():
+    """--acc-steps / train_net(acc_steps=): the global batch stays batch_size, dealt as acc_steps
+    micro-batches; absent, the reference's rule (4 if batch_size > 4 else 1, PMU/train.py:45)."""
+    import train as T
+    assert T.reference_acc_steps(32) == 4 and T.reference_acc_steps(4) == 1
+    a = T.get_args(["-b", "256", "--acc-steps", "8", "--dtype", "bf16", "--filters", "16,32", "--bench"])
+    assert (a.batchsize, a.acc_steps, a.dtype, a.filters, a.bench) == (256, 8, "bf16", "16,32", True)
+    assert T.get_args([]).acc_steps is None and T.get_args([]).dtype == "fp32"
+    steps, left = T.dp_micro_batches(list(range(256)), 32, 8, 8, 3)
+    assert steps == [[list(range(96, 128))]] and left == []
