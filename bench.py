@@ -11,7 +11,8 @@ N GPUs : one process per GPU (torch.distributed.run), 32 slices per GPU (weak sc
 Prints ONE JSON line on rank 0.  `roofline` is the dominant MFMA kernel family timed with HIP
 events on the launch stream during one instrumented step after the timed region;
 `cpu_baseline` times the CPU oracle (oracle/unet_ref.py, a torch-CPU restatement of the
-reference) on a bounded sample, rank 0 at N=1 only.
+reference) per BASELINE.md's protocol (c2: batch 32, 1 warm-up, median of 3 steps, all permitted
+host cores; with and without the SGD update), rank 0 at N=1 only.
 """
 from __future__ import annotations
 
@@ -207,17 +208,19 @@ def host_cpu():
     return threads, {"cpu_model": model, "os_cpu_count": total, "affinity_cpus": avail, "cgroup_cpu_quota": quota}
 
 
-def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classes=1):
-    """CPU oracle (torch-CPU restatement of the reference) on a bounded sample: batch 2 of the
-    bench geometry, 1 warm-up + timed steps until ~max_seconds (at most 5), on every host core this
-    process may use.  The reference's CPU path is fp32 only, so the c5 (bf16) sample is fp32."""
-    from oracle.unet_ref import unet_param_keys, unet_train_step
+def cpu_baseline(workload="unet", size=256, channels=1, classes=1, batch=32, steps=3):
+    """CPU oracle (torch-CPU restatement of the reference) timed per BASELINE.md's protocol: the bench
+    geometry at ``batch`` (c2: 32, the GPU batch), seeded weights (0) and input (1), 1 warm-up step,
+    then the median of ``steps`` steps, on every host core this process may use; the UNet step is
+    reported with and without its clip+SGD update.  The reference's CPU path is fp32 only, so the c5
+    (bf16) sample is fp32."""
+    from oracle.unet_ref import sgd_clip_step, unet_param_keys, unet_train_step
     from oracle.probunet_ref import probunet_train_step
     threads, host = host_cpu()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     g = torch.Generator().manual_seed(1)
-    B = 2
+    B = batch
     x = torch.rand(B, channels, size, size, generator=g)
     if workload == "unet":
         from model import UNet
@@ -226,10 +229,17 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
             t = (torch.rand(B, 1, size, size, generator=g) > 0.5).float()
         else:
             t = torch.randint(0, classes, (B, 1, size, size), generator=g)
-        bufs = {k: torch.zeros_like(sd[k]) for k in unet_param_keys(sd)}
+        keys = unet_param_keys(sd)
+        bufs = {k: torch.zeros_like(sd[k]) for k in keys}
 
         def one():
-            unet_train_step(sd, x, t, 5, classes, lr=1e-3, bufs=bufs)
+            t0 = time.perf_counter()
+            _, _, grads = unet_train_step(sd, x, t, 5, classes)
+            t1 = time.perf_counter()
+            cur = {k: sd[k].detach() for k in keys}
+            sgd_clip_step(cur, grads, bufs, 1e-3)
+            sd.update(cur)
+            return t1 - t0, time.perf_counter() - t0
         what = "UNet fwd+loss+bwd+clip+SGD steps"
     else:
         from model import ProbabilisticUnet
@@ -240,23 +250,22 @@ def cpu_baseline(max_seconds=25.0, workload="unet", size=256, channels=1, classe
         eps = torch.randn(B, 6, generator=g)
 
         def one():
+            t0 = time.perf_counter()
             probunet_train_step(sd, x, segm, eps, 5, 6, classes, 4, 10.0)
+            dt = time.perf_counter() - t0
+            return dt, dt
         what = "ProbabilisticUnet fwd+elbo+bwd steps (no optimizer, no eval samples)"
     one()  # warm-up
-    times = []
-    t_end = time.perf_counter() + max_seconds
-    while True:
-        t0 = time.perf_counter()
-        one()
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() > t_end or len(times) >= 5:
-            break
-    times.sort()
-    med = times[len(times) // 2]
-    res = {"value": round(B / med, 4), "unit": "slices/s", "cores": threads, "kind": "port",
+    times = sorted(one() for _ in range(steps))
+    fb = sorted(t[0] for t in times)[len(times) // 2]
+    full = sorted(t[1] for t in times)[len(times) // 2]
+    res = {"value": round(B / full, 4), "unit": "slices/s", "cores": threads, "kind": "port",
            "sample": f"oracle/{'unet' if workload == 'unet' else 'probunet'}_ref.py torch-CPU fp32, "
                      f"{size}x{size}x{channels}, {classes} class(es), filters {FILTERS}, batch {B}, median of "
-                     f"{len(times)} {what} after 1 warm-up, {threads} threads"}
+                     f"{steps} {what} after 1 warm-up, {threads} threads",
+           "ms_per_step": round(full * 1e3, 1)}
+    if workload == "unet":
+        res["value_without_sgd"] = round(B / fb, 4)
     res.update(host)
     return res
 
@@ -271,8 +280,12 @@ def cpu_leg(args, step):
         dvr = dice_vs_ref(step.net, xb, tb, args.classes, args.precision)
     else:
         dvr = dice_vs_ref_probunet(step.net, *step.batch())
+    # c2: BASELINE.md's protocol (batch 32, median of 3); c4 / c5 at a bounded batch (a batch-32 c4 or
+    # batch-16 c5 step takes 30-40 s on the box's 16 host threads)
+    cpu_batch = {"unet": 32, "probunet": 8, "c5": 2}[args.workload] if args.batch >= 8 else args.batch
     cpu = cpu_baseline(workload="probunet" if args.workload == "probunet" else "unet", size=args.size,
-                       channels=args.channels, classes=3 if args.workload == "probunet" else args.classes)
+                       channels=args.channels, classes=3 if args.workload == "probunet" else args.classes,
+                       batch=cpu_batch)
     return cpu, dvr
 
 
@@ -340,8 +353,17 @@ def dice_vs_ref(net, x, t, classes, precision):
     per = [d(lab == k, labr == k) for k in ks]
     to_t = [d(lab == k, tgt == k) for k in ks]
     to_tr = [d(labr == k, tgt == k) for k in ks]
+    # label flips, and how many of them sit at an fp32 tie (the oracle's decision margin below 1e-5:
+    # |p - 0.5| for one class, the top-two logit gap otherwise), where either evaluation order may win
+    flip = lab != labr
+    if classes == 1:
+        margin = (yr[:, 0] - 0.5).abs()
+    else:
+        top = torch.topk(yr, 2, dim=1).values
+        margin = top[:, 0] - top[:, 1]
     return {"classes": ks, "dice_hip_vs_oracle_labels": [round(v, 6) for v in per],
             "label_agreement": round(float((lab == labr).float().mean()), 7),
+            "label_flips": int(flip.sum()), "label_flips_at_fp32_ties": int((flip & (margin < 1e-5)).sum()),
             "dice_to_target_hip": [round(v, 6) for v in to_t], "dice_to_target_oracle": [round(v, 6) for v in to_tr],
             "max_abs_dice_delta": float(max(abs(a - b) for a, b in zip(to_t, to_tr))),
             "max_abs_output_delta": float((y - yr).abs().max()),

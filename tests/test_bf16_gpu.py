@@ -391,7 +391,7 @@ def test_c5_bf16_dice_gap_vs_fp32_oracle(dev):
     oracle (the reference's arithmetic), the HIP fp32 path, and the HIP bf16 path (torch.autocast
     bf16).  Then the eval-mode argmax maps of all three on the batch: the fp32 HIP path must match
     the oracle within the parity contract (Dice 1e-3, argmax agreement >= 0.999); the bf16 path's
-    gap is reported and bounded (argmax agreement >= 0.98, per-class Dice gap <= 0.02)."""
+    gap is held to the same Dice contract (argmax agreement >= 0.99, per-class Dice gap <= 1e-3)."""
     import json
     import os
     from model import UNet
@@ -447,7 +447,72 @@ def test_c5_bf16_dice_gap_vs_fp32_oracle(dev):
     for m in modes:
         assert res["fp32"][f"argmax_agreement_vs_oracle_{m}"] >= 0.999, m
         assert max(res["fp32"][f"dice_gap_{m}"]) <= 1e-3, m
-        assert res["bf16"][f"argmax_agreement_vs_oracle_{m}"] >= 0.98, m
-        assert max(res["bf16"][f"dice_gap_{m}"]) <= 0.02, m
+        # the north star's Dice contract holds for the bf16 mode too (measured: agreement 0.99988,
+        # Dice gap <= 1.7e-4; profiles/r02/c5_bf16_dice_gap.json)
+        assert res["bf16"][f"argmax_agreement_vs_oracle_{m}"] >= 0.99, m
+        assert max(res["bf16"][f"dice_gap_{m}"]) <= 1e-3, m
     # the phantom is learnable: the reference itself segments it after 12 steps
     assert min(res["oracle"]["dice_to_target_train"]) > 0.5, res["oracle"]
+
+
+@pytest.mark.timeout(900)
+def test_c5_geometry_bf16_step_vs_oracle(dev):
+    """Config c5's geometry and arithmetic: UNet(3, 3, [64..1024]) on 512x512x3 slices under
+    torch.autocast(bfloat16), one training step (forward, CE, backward) at batch 2 vs the oracle's
+    autocast arithmetic (Bf16Conv3x3 / Bf16ConvT2x2) evaluated in fp64 — the bench's grid sizes,
+    split-K slab counts and operand layouts at 512^2 (PMU/model/unet/unet_model.py:31-54).
+
+    Tolerances: bf16 rounds every conv operand, so an fp32 evaluation of the very same arithmetic
+    flips operands across bf16 rounding boundaries: the oracle in fp32 is itself 6.1e-3 (output,
+    relative to max|out|) and 3.2e-3 (gradients) away from its fp64 evaluation at this geometry
+    (tools/parity_diag.py).  Outputs, loss and gradients are therefore held to max(1e-3, 2 x that
+    floor), measured on the spot; the label map and the Dice — the contract's bf16 quantities — to
+    argmax agreement >= 0.99 and per-class Dice within 1e-3 of the fp64 oracle's (measured 0.9977,
+    1.6e-4)."""
+    import os
+    from helpers import grad_err
+    from model import UNet
+    from oracle.unet_ref import trainer_dice, unet_forward, unet_loss, unet_param_keys
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    torch.manual_seed(0)
+    net = UNet(3, 3, [64, 128, 256, 512, 1024])
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    g = torch.Generator().manual_seed(2)
+    N, S = 2, 512
+    x = torch.rand(N, 3, S, S, generator=g)
+    tgt = torch.randint(0, 3, (N, 1, S, S), generator=g)
+    keys = unet_param_keys(sd)
+
+    def oracle(dt):
+        sdd = {k: (v.to(dt) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+        params = {k: sdd[k].clone().requires_grad_(True) for k in keys}
+        work = dict(sdd)
+        work.update(params)
+        o = unet_forward(work, x.to(dt), 5, 3, bf16=True)
+        lo = unet_loss(o, tgt, 3)
+        lo.backward()
+        return o.detach(), float(lo), {k: params[k].grad for k in keys}, work
+
+    ref, lref, gref, work = oracle(torch.float64)
+    o32, l32, g32, _ = oracle(torch.float32)
+    tol_out = max(1e-3, 2 * _rel(o32, ref))
+    tol_loss = max(1e-3, 2 * abs(l32 - lref) / abs(lref))
+    tol_g = max(1e-3, 2 * grad_err(g32, gref)[0])
+    net = net.to(dev).train()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = net(x.to(dev))
+    loss = unet_loss(out, tgt.to(dev), 3)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert _rel(out, ref) <= tol_out, (_rel(out, ref), tol_out)
+    assert abs(float(loss) - lref) <= tol_loss * abs(lref)
+    named = dict(net.named_parameters())
+    err, worst = grad_err({k: named[k].grad for k in keys}, gref)
+    assert err <= tol_g, (err, worst, tol_g)
+    lab, lab_ref = out.detach().argmax(1).cpu(), ref.argmax(1)
+    assert float((lab == lab_ref).float().mean()) >= 0.99
+    dh, dr = trainer_dice(out.detach().cpu(), tgt, 3), trainer_dice(ref, tgt, 3)
+    assert max(abs(a - b) for a, b in zip(dh, dr)) <= 1e-3, (dh, dr)
+    for k, v in net.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            assert float((v.double().cpu() - work[k]).abs().max()) <= 1e-3 * max(1.0, float(work[k].abs().max())), k

@@ -166,14 +166,31 @@ def test_train_net_and_predict_volume_end_to_end(dev, tmp_path):
     assert all(torch.isfinite(v.float()).all() for v in after.values())
     assert os.path.exists(os.path.join(str(tmp_path), "unet_checkpoint0.pt"))
     res = predict_volume(tr.net, ds, 0, batch_size=8)
-    from oracle.data_ref import class_dice, fuse
-    probs = [torch.softmax(s, 1) for s in res["stacks"]]
+    from oracle.data_ref import fuse
+    probs = [torch.softmax(s, 1).cpu() for s in res["stacks"]]
     vols = fuse(*probs)
-    truth = res["truth"]
+    truth = res["truth"].cpu()
     for v in range(4):
         for k in (1, 2):
-            ref = class_dice(vols[v].cpu(), truth.cpu(), k)
-            assert abs(float(res["dice"][v, k]) - ref) <= 5e-3   # softmax in-kernel: a few fp32 near-ties may flip
+            lo, hi, n_tie = _dice_bounds(vols[v], truth, k)
+            got = float(res["dice"][v, k])
+            assert lo - 1e-3 <= got <= hi + 1e-3, (v, k, got, lo, hi, n_tie)
+
+
+def _dice_bounds(vol, truth, k, tie=1e-5):
+    """eval.py's dice(volume, truth, k) (:42-49) as an interval over the fp32 near-ties: voxels whose
+    top-two probabilities are within ``tie`` (softmax / averaging rounding can order them either
+    way) may take either of those two labels.  Without near-ties lo == hi == the reference's Dice."""
+    s = 1e-6
+    top = torch.topk(vol, 2, dim=1)
+    amb = (top.values[:, 0] - top.values[:, 1]) < tie
+    lab = top.indices[:, 0]
+    t = truth.reshape(lab.shape) == k
+    sure = (lab == k) & ~amb
+    cand = amb & ((top.indices[:, 0] == k) | (top.indices[:, 1] == k))
+    i0, p0, tt = float((sure & t).sum()), float(sure.sum()), float(t.sum())
+    a, b = float((cand & t).sum()), float((cand & ~t).sum())
+    return (2 * i0 + s) / (p0 + b + tt + s), (2 * (i0 + a) + s) / (p0 + a + tt + s), int(amb.sum())
 
 
 @pytest.mark.gpu
