@@ -388,6 +388,17 @@ int pmu_occupancy_conv3x3_raw(int* blocks_per_cu);
 int pmu_occupancy_wgrad3x3_bf16(int* blocks_per_cu);
 int pmu_occupancy_conv3x3_pipe(int* blocks_per_cu);
 
+/* ---- build identity and the bounds-checked debug build ------------------------------------ */
+/* Bit 0: experiments build (make EXPERIMENTS=1: kernel-variant A/B switches honoured); bit 1:
+ * bounds-checked debug build (make DEBUG=1 -> libpmunet_hip_debug.so, PMU_DCHECK in the kernels). */
+int pmu_build_flags(void);
+/* Debug build: synchronises the device and returns the first recorded index-bound violation,
+ * out[0..4] = {code (PMU_DBG_* in csrc/pmu_common.h; 0 = none), source line, workgroup, set,
+ * translation unit}; *tu_name (may be NULL) receives the source file.  Release build: out all 0.
+ * pmu_debug_reset clears the records. */
+int pmu_debug_read(int* out, const char** tu_name);
+int pmu_debug_reset(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -631,6 +631,7 @@ __device__ __forceinline__ float sgd_one(float& p, float g, float b, float gscal
 __global__ __launch_bounds__(256) void sgd_clip_kernel(const pmu_sgd_chunk* __restrict__ chunks, void* const* __restrict__ ptrs,
                                                        float gscale, float lr, float momentum, float clip) {
   const pmu_sgd_chunk ck = chunks[blockIdx.x];
+  PMU_DCHECK(ck.tensor >= 0 && ck.start >= 0 && ck.len > 0 && ck.len <= 16384, PMU_DBG_INDEX);  // pmu_hip.optim.CHUNK
   float* p = (float*)ptrs[3 * ck.tensor + 0] + ck.start;
   float* g = (float*)ptrs[3 * ck.tensor + 1] + ck.start;
   float* b = (float*)ptrs[3 * ck.tensor + 2] + ck.start;
@@ -1019,5 +1020,65 @@ extern "C" int pmu_bnrelu_apply(const float* z, const float* coef, long long P, 
   hipLaunchKernelGGL(bnrelu_apply_kernel, dim3(grid_for(total4)), dim3(256), 0, (hipStream_t)stream, z, coef, total4,
                      C, out);
   PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+// ---- build identity and the debug-build violation records (pmu_common.h) ----------------------
+#ifdef PMU_DEBUG
+namespace {
+struct DbgTu {
+  const char* name;
+  int (*rd)(int*);
+  int (*rs)();
+};
+DbgTu g_dbg_tus[64];   // zero-initialised before any dynamic initialiser registers into it
+int g_dbg_ntu = 0;
+}  // namespace
+int pmu_dbg_register(const char* tu, int (*rd)(int*), int (*rs)()) {
+  if (g_dbg_ntu < 64) g_dbg_tus[g_dbg_ntu++] = DbgTu{tu, rd, rs};
+  return g_dbg_ntu;
+}
+#endif
+
+extern "C" int pmu_build_flags(void) {
+  int f = 0;
+#ifdef PMU_EXPERIMENTS
+  f |= 1;
+#endif
+#ifdef PMU_DEBUG
+  f |= 2;
+#endif
+  return f;
+}
+
+extern "C" int pmu_debug_read(int* out, const char** tu_name) {
+  PMU_REQUIRE(out);
+  for (int i = 0; i < 5; ++i) out[i] = 0;
+  if (tu_name) *tu_name = nullptr;
+#ifdef PMU_DEBUG
+  const hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  for (int t = 0; t < g_dbg_ntu; ++t) {
+    int rec[4];
+    const int rc = g_dbg_tus[t].rd(rec);
+    if (rc) return rc;
+    if (rec[3]) {
+      for (int i = 0; i < 4; ++i) out[i] = rec[i];
+      out[4] = t;
+      if (tu_name) *tu_name = g_dbg_tus[t].name;
+      return PMU_OK;
+    }
+  }
+#endif
+  return PMU_OK;
+}
+
+extern "C" int pmu_debug_reset(void) {
+#ifdef PMU_DEBUG
+  for (int t = 0; t < g_dbg_ntu; ++t) {
+    const int rc = g_dbg_tus[t].rs();
+    if (rc) return rc;
+  }
+#endif
   return PMU_OK;
 }

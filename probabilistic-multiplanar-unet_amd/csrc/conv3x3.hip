@@ -434,7 +434,7 @@ static int pick_twl(int W) {
 // MFMAs cover each block's commit phase).  PMU_CONV_IMPL=sync|pipe1 selects the others.
 static int pipe_mode() {
   static const int v = [] {
-    const char* e = getenv("PMU_CONV_IMPL");
+    const char* e = pmu_variant_env("PMU_CONV_IMPL");
     if (e && strcmp(e, "sync") == 0) return 0;
     if (e && strcmp(e, "pipe1") == 0) return 1;
     return 2;

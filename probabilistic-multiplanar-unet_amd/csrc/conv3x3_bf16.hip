@@ -535,7 +535,7 @@ static int launch_bf16(const pmu_frame* in, const unsigned short* wp, const floa
                        (!two || (long long)s1.C * s1.H * s1.W * in->N < (1LL << 31)) &&
                        (long long)in->N * in->H * in->W < (1LL << 31);
     const bool split_ok = !dgrad || split % 32 == 0 || split == NOUT;
-    if (ok && modes_ok && small && split_ok && pool == PMU_POOL_NONE && !getenv("PMU_BF16_NOPIPE")) {
+    if (ok && modes_ok && small && split_ok && pool == PMU_POOL_NONE && !pmu_variant_env("PMU_BF16_NOPIPE")) {
 #define PMU_BP(D, P, T)                                                                    \
   if (dgrad == D && pool == P && twl == T) {                                               \
     hipLaunchKernelGGL((conv3x3_bf16_pipe_kernel<D, P, T>), grid, dim3(256), 0, st, a);    \

@@ -99,6 +99,7 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
   const int n = t;
   const int h0 = th * TH, w0 = tw * TW;
   const int j0 = cb * BNT;
+  PMU_DCHECK(n < a.N && j0 < a.NOUT, PMU_DBG_GRID);
 
   // A units: halo pixel hp = it >> 2, 8-channel unit q = it & 3; tile-constant 32-bit offsets
   int eo[NA], dsta[NA];
@@ -116,6 +117,7 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
     vm |= v ? (1u << i) : 0u;
     okm |= ok ? (1u << i) : 0u;
     eo[i] = ok ? ((n * a.H + h) * a.W + w) * a.Cp + 8 * q : 0;
+    PMU_DCHECK(!ok || ((long long)(n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
     dsta[i] = hp * LS + 8 * q;
   }
   const int hsel = (lane >> 5) * 8;
@@ -251,6 +253,7 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
         const int h = h0 + (q >> TWL), w = w0 + (q & (TW - 1));
         if (!full && (!jok || h >= a.H || w >= a.W)) continue;
         const unsigned pix = (unsigned)((n * a.H + h) * a.W + w);
+        PMU_DCHECK(pix < (unsigned)(a.N * a.H * a.W) && j < a.NOUT, PMU_DBG_OUTPUT);
         const float v = acc[fm][fn][r] + b;
         dstp[(size_t)pix * (unsigned)ld] = v;
         if (!DGRAD) {
@@ -280,6 +283,7 @@ __global__ __launch_bounds__(BMT, 2) void conv3x3_raw_kernel(RawArgs a) {
           t1 += red[(v * BNT + tid) * 2 + 0];
           t2 += red[(v * BNT + tid) * 2 + 1];
         }
+        PMU_DCHECK(tsp < a.N * a.tiles_h * a.tiles_w, PMU_DBG_WORKSPACE);
         a.part[((long long)tsp * 2 + 0) * a.NOUT + j] = t1;
         a.part[((long long)tsp * 2 + 1) * a.NOUT + j] = t2;
       }
@@ -296,7 +300,7 @@ static int pick_twl(int W) {
 // pixels per tile: PMU_RAW_BMT=256|512 forces one (A/B measurements); default 256
 static int raw_bmt(int N, int H, int W, int TW, int ncb) {
   static const int forced = [] {
-    const char* e = getenv("PMU_RAW_BMT");
+    const char* e = pmu_variant_env("PMU_RAW_BMT");
     return e ? atoi(e) : 0;
   }();
   if (forced == 256 || forced == 512) return forced;
@@ -324,7 +328,7 @@ static int launch_raw(const unsigned short* x, int Cp, int N, int H, int W, cons
   a.tiles_w = pmu_cdiv(W, TW);
   a.tiles_h = pmu_cdiv(H, TH);
   static const int xcd = [] {
-    const char* e = getenv("PMU_RAW_XCD");
+    const char* e = pmu_variant_env("PMU_RAW_XCD");
     return e ? atoi(e) : 1;
   }();
   a.ncb = ncb;

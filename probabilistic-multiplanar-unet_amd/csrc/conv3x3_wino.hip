@@ -247,6 +247,7 @@ __device__ __forceinline__ WinoGeo wino_geo(const WinoArgs& a) {
   const int tw = sp % a.tiles_w; sp /= a.tiles_w;
   const int th = sp % a.tiles_h; sp /= a.tiles_h;
   g.n = sp;
+  PMU_DCHECK(g.n < a.in.N && g.cob_blk < a.nco, PMU_DBG_GRID);
   g.h0 = th * OH; g.w0 = tw * OW;
   g.j0 = g.cob_blk * CO;
   g.tg = wave & 3;   // tiles 16*tg .. 16*tg+15 (tile rows 2tg, 2tg+1)
@@ -311,6 +312,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& a, const WinoGeo& 
         const float y = q ? y1 : y0;
         if (!jok || hh >= F.H || ww >= F.W) continue;
         const long long pix = ((long long)g.n * F.H + hh) * F.W + ww;
+        PMU_DCHECK(pix < (long long)F.N * F.H * F.W && j < a.NOUT, PMU_DBG_OUTPUT);
         if (!DGRAD) {
           a.out0[pix * a.NOUT + j] = y;
           s1 += y;
@@ -343,6 +345,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& a, const WinoGeo& 
           t1 += red[((4 * hf + tg) * 16 + l) * 2 + 0];
           t2 += red[((4 * hf + tg) * 16 + l) * 2 + 1];
         }
+        PMU_DCHECK(g.spatial < (long long)F.N * a.tiles_h * a.tiles_w, PMU_DBG_WORKSPACE);
         a.part[((long long)g.spatial * 2 + 0) * a.NOUT + jj] = t1;
         a.part[((long long)g.spatial * 2 + 1) * a.NOUT + jj] = t2;
       }
@@ -521,6 +524,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
     const int h = g.h0 - 1 + hr, w = g.w0 - 1 + hc;
     const bool in = data && h >= 0 && w >= 0 && h < F.H && w < F.W;
     goff[r] = in ? (unsigned)(((((long long)g.n * F.H + h) * F.W + w) * KC + 4 * q) * 4) : 0u;
+    PMU_DCHECK(!in || (((long long)g.n * F.H + h) * F.W + w) < (long long)F.N * F.H * F.W, PMU_DBG_OPERAND);
     gin |= in ? (1u << r) : 0u;
     if (data && !in) {  // zero padding, in both stages, once
       *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -541,6 +545,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
   {                                                                                                        \
     const int p_ = (GI) / nchunks;                                                                         \
     const int k0_ = ((GI) - p_ * nchunks) * BK;                                                            \
+    PMU_DCHECK(k0_ + BK <= KC, PMU_DBG_OPERAND);                                                           \
     float* b_ = (BUF);                                                                                     \
     const char* xb_ = reinterpret_cast<const char*>(x + k0_);                                              \
     for (int r = 0; r < R_NGL; ++r)                                                                        \
@@ -626,7 +631,16 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_raw_kernel(WinoArgs a) {
 int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
                     float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
   PMU_REQUIRE(x && wp && out0 && KC > 0 && KC % BK == 0 && NOUT > 0 && N > 0 && H > 0 && W > 0);
-  PMU_REQUIRE((long long)N * H * W * KC * 4 < (1LL << 32));  // 32-bit DMA byte offsets
+  const long long img_bytes = (long long)H * W * (KC > NOUT ? KC : NOUT) * 4;
+  if ((long long)N * img_bytes >= (1LL << 32)) {  // 32-bit DMA byte offsets: split over images
+    const long long tiles = (long long)pmu_cdiv(W, OW) * pmu_cdiv(H, OH);
+    return pmu_image_chunks(N, img_bytes, [&](int n0, int nn) {
+      const long long px = (long long)n0 * H * W;
+      return launch_wino_raw(x + px * KC, KC, nn, H, W, wp, bias, NOUT, out0 + px * split,
+                  out1 ? out1 + px * (NOUT - split) : nullptr, split,
+                  part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream);
+    });
+  }
   WinoArgs a;
   memset(&a, 0, sizeof(a));
   a.in.s0.x = x; a.in.s0.C = KC; a.in.s0.H = H; a.in.s0.W = W;
@@ -637,7 +651,7 @@ int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp
   a.tiles_h = pmu_cdiv(H, OH);
   a.nco = pmu_cdiv(NOUT, CO);
   static const int prio = [] {  // PMU_WINO_PRIO=0|1 (A/B of static wave priority)
-    const char* e = getenv("PMU_WINO_PRIO");
+    const char* e = pmu_variant_env("PMU_WINO_PRIO");
     return e ? atoi(e) : 0;
   }();
   a.prio = prio;
@@ -649,7 +663,7 @@ int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp
   }();
   const long long spatial = (long long)a.tiles_w * a.tiles_h * N;
   static const bool fwd_multi = [] {  // PMU_WINO_FWD_MULTI=0: one pass per forward workgroup (A/B)
-    const char* e = getenv("PMU_WINO_FWD_MULTI");
+    const char* e = pmu_variant_env("PMU_WINO_FWD_MULTI");
     return !(e && atoi(e) == 0);
   }();
   int cpb = 1;
@@ -686,7 +700,7 @@ static bool wino_pipe_src_ok(const pmu_src& s) {
 // timing experiments (EXP 1-3, 6, 7 compute wrong results): only in `make EXPERIMENTS=1` builds
 static int wino_exp() {
   static const int v = [] {
-    const char* e = getenv("PMU_WINO_EXP");
+    const char* e = pmu_variant_env("PMU_WINO_EXP");
     return e ? atoi(e) : 0;
   }();
   return v;
@@ -695,7 +709,7 @@ static int wino_exp() {
 
 static bool wino_sync_forced() {
   static const bool v = [] {
-    const char* e = getenv("PMU_WINO_IMPL");
+    const char* e = pmu_variant_env("PMU_WINO_IMPL");
     return e && strcmp(e, "sync") == 0;
   }();
   return v;

@@ -60,6 +60,7 @@ struct W2Args {
   float* out1;
   float* part;        // [spatial blocks][2][NOUT] BN partial sums (fwd) or null
   int H, W, KC, NOUT, split, bw, bh, nco, cpb;
+  int N;              // images (bounds checks of the debug build)
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -284,6 +285,7 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
           if (!jok || hh >= a.H || ww >= a.W) continue;
           const float v = y + bias;
           const long long pix = ((long long)n * a.H + hh) * a.W + ww;
+          PMU_DCHECK(pix < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
           if (!DGRAD) {
             a.out0[pix * a.NOUT + j] = v;
             s1 += v;
@@ -316,6 +318,7 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
           t1 += red[(wv * 16 + l) * 2 + 0];
           t2 += red[(wv * 16 + l) * 2 + 1];
         }
+        PMU_DCHECK(spatial < (long long)a.N * a.bh * a.bw, PMU_DBG_WORKSPACE);
         a.part[((long long)spatial * 2 + 0) * a.NOUT + jj] = t1;
         a.part[((long long)spatial * 2 + 1) * a.NOUT + jj] = t2;
       }
@@ -348,6 +351,7 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
   {                                                                                                        \
     const int p_ = (GI) / nchunks;                                                                         \
     const int k0_ = ((GI) - p_ * nchunks) * BK;                                                            \
+    PMU_DCHECK(k0_ + BK <= a.KC, PMU_DBG_OPERAND);                                                         \
     float* b_ = (BUF);                                                                                     \
     const char* xb_ = reinterpret_cast<const char*>(a.x + k0_);                                            \
     _Pragma("unroll") for (int r = 0; r < NGL; ++r)                                                        \
@@ -422,6 +426,7 @@ __global__ __launch_bounds__(16 * CO_, 1) void conv3x3_wino2h_kernel(W2Args a) {
   const int KC = a.KC;
   B.nchunks = KC / BK;
   B.npass = a.cpb < a.nco - B.cob0 ? a.cpb : a.nco - B.cob0;
+  PMU_DCHECK(B.n < a.N && B.cob0 < a.nco, PMU_DBG_GRID);
   unsigned goff[NGL];
   unsigned gin = 0u, gzero = 0u;
 #pragma unroll
@@ -434,6 +439,7 @@ __global__ __launch_bounds__(16 * CO_, 1) void conv3x3_wino2h_kernel(W2Args a) {
     const int h = B.h0 - 1 + hr, w = B.w0 - 1 + px;
     const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
     goff[r] = in ? (unsigned)(((((long long)B.n * a.H + h) * a.W + w) * KC + 4 * (w5 & 1)) * 4) : 0u;
+    PMU_DCHECK(!in || (((long long)B.n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
     gin |= in ? (1u << r) : 0u;
     gzero |= (data && !in) ? (1u << r) : 0u;
     if (data && !in) {
@@ -450,7 +456,7 @@ __global__ __launch_bounds__(16 * CO_, 1) void conv3x3_wino2h_kernel(W2Args a) {
 // output channels per block (PMU_WINO2H_CO=32: 512-thread blocks, two per CU; A/B)
 static int w2h_co() {
   static const int v = [] {
-    const char* e = getenv("PMU_WINO2H_CO");
+    const char* e = pmu_variant_env("PMU_WINO2H_CO");
     return (e && atoi(e) == 32) ? 32 : 64;
   }();
   return v;
@@ -459,11 +465,21 @@ static int w2h_co() {
 int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
                   float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
   PMU_REQUIRE(x && wp && out0 && KC > 0 && KC % BK == 0 && NOUT > 0 && N > 0 && H > 0 && W > 0);
-  PMU_REQUIRE((long long)N * H * W * KC * 4 < (1LL << 32));  // 32-bit DMA byte offsets
+  const long long img_bytes = (long long)H * W * (KC > NOUT ? KC : NOUT) * 4;
+  if ((long long)N * img_bytes >= (1LL << 32)) {  // 32-bit DMA byte offsets: split over images
+    const long long tiles = (long long)pmu_cdiv(W, OW) * pmu_cdiv(H, OH);
+    return pmu_image_chunks(N, img_bytes, [&](int n0, int nn) {
+      const long long px = (long long)n0 * H * W;
+      return launch_wino2h(x + px * KC, KC, nn, H, W, wp, bias, NOUT, out0 + px * split,
+                  out1 ? out1 + px * (NOUT - split) : nullptr, split,
+                  part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream);
+    });
+  }
   W2Args a;
   memset(&a, 0, sizeof(a));
   a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
   a.H = H; a.W = W; a.KC = KC; a.NOUT = NOUT; a.split = split;
+  a.N = N;
   a.bw = pmu_cdiv(W, OW);
   a.bh = pmu_cdiv(H, OH);
   const int CO = w2h_co();

@@ -59,6 +59,7 @@ struct W4Args {
   int H, W, KC, NOUT, split, bw, bh, nco, cpb;
   int prio;           // 1: waves of component half 1 run at s_setprio 1 (PMU_WINO4_PRIO)
   int ts, tc;         // 2-D workgroup grouping (spatial x co-groups per group; tc = 0: co-groups fastest)
+  int N;              // images (bounds checks of the debug build)
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -382,6 +383,7 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
           if (!jok || hh2 >= a.H || ww >= a.W) continue;
           const float v = y + bias;
           const long long pix = ((long long)n * a.H + hh2) * a.W + ww;
+          PMU_DCHECK(pix < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
           if (!DGRAD) {
             a.out0[pix * a.NOUT + j] = v;
             s1 += v;
@@ -414,6 +416,7 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
           t1 += red[((4 * hf + g) * 16 + l) * 2 + 0];
           t2 += red[((4 * hf + g) * 16 + l) * 2 + 1];
         }
+        PMU_DCHECK(spatial < (long long)a.N * a.bh * a.bw, PMU_DBG_WORKSPACE);
         a.part[((long long)spatial * 2 + 0) * a.NOUT + jj] = t1;
         a.part[((long long)spatial * 2 + 1) * a.NOUT + jj] = t2;
       }
@@ -446,6 +449,7 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
   {                                                                                                        \
     const int p_ = (GI) / nchunks;                                                                         \
     const int k0_ = ((GI) - p_ * nchunks) * BK;                                                            \
+    PMU_DCHECK(k0_ + BK <= a.KC, PMU_DBG_OPERAND);                                                         \
     float* b_ = (BUF);                                                                                     \
     const char* xb_ = reinterpret_cast<const char*>(a.x + k0_);                                            \
     _Pragma("unroll") for (int r = 0; r < NGL; ++r)                                                        \
@@ -537,6 +541,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   const int KC = a.KC;
   B.nchunks = KC / BK;
   B.npass = a.cpb < a.nco - B.cob0 ? a.cpb : a.nco - B.cob0;
+  PMU_DCHECK(B.n < a.N && B.cob0 < a.nco, PMU_DBG_GRID);
 
   // this thread's operand units: byte offset of chunk 0 (< 2^32, host-checked) and whether the unit
   // is inside the input; units of the image outside it are zeroed in both stages once
@@ -552,6 +557,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
     const int h = B.h0 - 1 + hr, w = B.w0 - 1 + px;
     const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
     goff[r] = in ? (unsigned)(((((long long)B.n * a.H + h) * a.W + w) * KC + 4 * (w9 & 1)) * 4) : 0u;
+    PMU_DCHECK(!in || (((long long)B.n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
     gin |= in ? (1u << r) : 0u;
     gzero |= (data && !in) ? (1u << r) : 0u;
     if (data && !in) {
@@ -569,11 +575,21 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
 int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
                  float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
   PMU_REQUIRE(x && wp && out0 && KC > 0 && KC % BK == 0 && NOUT > 0 && N > 0 && H > 0 && W > 0);
-  PMU_REQUIRE((long long)N * H * W * KC * 4 < (1LL << 32));  // 32-bit DMA byte offsets
+  const long long img_bytes = (long long)H * W * (KC > NOUT ? KC : NOUT) * 4;
+  if ((long long)N * img_bytes >= (1LL << 32)) {  // 32-bit DMA byte offsets: split over images
+    const long long tiles = (long long)pmu_cdiv(W, OW) * pmu_cdiv(H, OH);
+    return pmu_image_chunks(N, img_bytes, [&](int n0, int nn) {
+      const long long px = (long long)n0 * H * W;
+      return launch_wino4(x + px * KC, KC, nn, H, W, wp, bias, NOUT, out0 + px * split,
+                  out1 ? out1 + px * (NOUT - split) : nullptr, split,
+                  part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream);
+    });
+  }
   W4Args a;
   memset(&a, 0, sizeof(a));
   a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
   a.H = H; a.W = W; a.KC = KC; a.NOUT = NOUT; a.split = split;
+  a.N = N;
   a.bw = pmu_cdiv(W, OW);
   a.bh = pmu_cdiv(H, OH);
   a.nco = pmu_cdiv(NOUT, CO);
@@ -596,16 +612,16 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
   }
   a.cpb = cpb;
   static const int pf = [] {
-    const char* e = getenv("PMU_WINO4_PF");
+    const char* e = pmu_variant_env("PMU_WINO4_PF");
     return e ? atoi(e) : 0;
   }();
   static const int prio = [] {  // PMU_WINO4_PRIO=1: waves of component half 1 at s_setprio 1 (A/B)
-    const char* e = getenv("PMU_WINO4_PRIO");
+    const char* e = pmu_variant_env("PMU_WINO4_PRIO");
     return e ? atoi(e) : 0;
   }();
   a.prio = prio;
   static const int grp = [] {  // PMU_WINO4_GROUP=0: co-groups fastest (A/B)
-    const char* e = getenv("PMU_WINO4_GROUP");
+    const char* e = pmu_variant_env("PMU_WINO4_GROUP");
     return e ? atoi(e) : 1;
   }();
   {

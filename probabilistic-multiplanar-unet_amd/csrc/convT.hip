@@ -739,7 +739,7 @@ static void convT_wgrad_geometry(int N, int H, int W, int Cin, int Cout, int* tw
 
 static void pipe_grid(PipeArgs& p, int nnb) {
   static const int xcd = [] {
-    const char* e = getenv("PMU_CONVT_XCD");
+    const char* e = pmu_variant_env("PMU_CONVT_XCD");
     return e ? atoi(e) : 1;
   }();
   p.nnb = nnb;
@@ -777,7 +777,7 @@ extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float
 #ifdef PMU_EXPERIMENTS
     // timing experiments (wrong results): only in `make EXPERIMENTS=1` builds
     static const int exp = [] {
-      const char* e = getenv("PMU_CONVT_EXP");
+      const char* e = pmu_variant_env("PMU_CONVT_EXP");
       return e ? atoi(e) : 0;
     }();
     if (exp == 1) hipLaunchKernelGGL((convT_pipe_kernel<false, 1>), grid, dim3(256), 0, (hipStream_t)stream, p);

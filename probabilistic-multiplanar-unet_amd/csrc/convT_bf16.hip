@@ -465,7 +465,7 @@ constexpr int DB_G = 2048;  // dbias partial rows (blocks of the partial-sum pas
 
 static void set_grid(TArgs& p, int nnb) {
   static const int xcd = [] {
-    const char* e = getenv("PMU_CONVT_XCD");
+    const char* e = pmu_variant_env("PMU_CONVT_XCD");
     return e ? atoi(e) : 1;
   }();
   p.nnb = nnb;

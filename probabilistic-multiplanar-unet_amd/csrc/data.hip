@@ -100,6 +100,7 @@ __global__ __launch_bounds__(256) void gather_slices_kernel(const long long* __r
                                                             float* __restrict__ out) {
   const int b = blockIdx.y;
   const int id = ids[b];
+  PMU_DCHECK(id >= 0 && addr[id] != 0, PMU_DBG_INDEX);
   const double* s = reinterpret_cast<const double*>(addr[id]);
   const double m = maxv ? maxv[id] : 0.0;
   const bool div = normalize && m != 0.0;

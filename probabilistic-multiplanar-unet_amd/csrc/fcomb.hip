@@ -1039,7 +1039,7 @@ extern "C" size_t pmu_fcomb_bwd_ws(int N, int H, int W) {
 static int fcomb_bwd_impl() {  // PMU_FCOMB_BWD=tile selects the LDS-tile kernel (A/B)
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("PMU_FCOMB_BWD");
+    const char* e = pmu_variant_env("PMU_FCOMB_BWD");
     v = (e && e[0] == 't') ? 0 : 1;
   }
   return v;

@@ -113,8 +113,11 @@ __global__ __launch_bounds__(LT) void ce_fwd_kernel(const float* __restrict__ x,
       for (int k = 0; k < K; ++k) m = fmaxf(m, xp[k * HW]);
       float se = 0.f;
       for (int k = 0; k < K; ++k) se += expf(xp[k * HW] - m);
-      const int tk = (int)tv;
-      l = (m + logf(se)) - ((tk >= 0 && tk < K) ? xp[(long long)tk * HW] : 0.f);
+      // a target outside [0, K) that is not ignore_index: torch raises; no host sync here, so the
+      // pixel's loss (and the reduced loss) is NaN and the debug build records the index
+      const bool tok = tv >= 0 && tv < K;
+      PMU_DCHECK(tok, PMU_DBG_INDEX);
+      l = tok ? (m + logf(se)) - xp[(long long)tv * HW] : __builtin_nanf("");
       c += 1.0;
     }
     if (each) each[i] = l;
@@ -137,6 +140,10 @@ __global__ __launch_bounds__(LT) void ce_bwd_kernel(const float* __restrict__ x,
     const long long tv = tgt[i];
     if (tv == ignore) {
       for (int k = 0; k < K; ++k) dp[k * HW] = 0.f;
+      continue;
+    }
+    if (tv < 0 || tv >= K) {  // out-of-range target (see ce_fwd_kernel): NaN gradient
+      for (int k = 0; k < K; ++k) dp[k * HW] = __builtin_nanf("");
       continue;
     }
     const float g = reduction == 0 ? gout[i] : gs;

@@ -76,6 +76,7 @@ __device__ __forceinline__ void tile_load(const WgbArgs& a, int tile, int co0, i
   const int tw = t % a.tiles_w; t /= a.tiles_w;
   const int th = t % a.tiles_h; t /= a.tiles_h;
   const int n = t, h0 = th * TH, w0 = tw * TW;
+  PMU_DCHECK(n < a.N, PMU_DBG_GRID);
   r.okd = 0u;
   r.okx = 0u;
 #pragma unroll
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_bf16_kernel(WgbArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int co = co0 + cbase + 32 * f + acc_row(r, lane);
+          PMU_DCHECK(split < a.nsplit && ci < a.Cin, PMU_DBG_WORKSPACE);
           if (co < a.Cout) a.ws[(((long long)split * 9 + tap) * a.Cout + co) * a.Cin + ci] = acc[f][kw][r];
         }
       }

@@ -55,6 +55,7 @@ __device__ __forceinline__ void wgw_origin(const WgwArgs& a, int tile, int& n, i
   const int tw = t % a.tiles_w; t /= a.tiles_w;
   const int th = t % a.tiles_h; t /= a.tiles_h;
   n = t; h0 = th * TH; w0 = tw * TW;
+  PMU_DCHECK(n < a.N, PMU_DBG_GRID);
 }
 
 // LDS-DMA staging of one K-tile: the slot is the dz image (128 px x 8 units) followed by the
@@ -100,6 +101,7 @@ __device__ __forceinline__ void wgw_dma(const WgwArgs& a, int tile, int co0, int
     const bool data = isd ? qd < C::WCO / 4 : (u < C::W_UNITS && qx < WCI / 4);
     const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
     const long long pix = ((long long)n * a.H + h) * a.W + w;
+    PMU_DCHECK(!in || pix < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
     const float* src = isd ? a.dz + pix * a.Cout + co0 + 4 * qd : a.x + pix * a.Cin + ci0 + 4 * qx;
     if (in)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -219,6 +221,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad3x3_wino_kernel(WgwArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = co0 + cf * 16 + 4 * (lane >> 4) + r;
+      PMU_DCHECK(split < a.nsplit && co < a.Cout && ci < a.Cin, PMU_DBG_WORKSPACE);
       a.ws[(((long long)split * 16 + c) * a.Cout + co) * a.Cin + ci] = acc[c][r];
     }
 }
@@ -354,6 +357,7 @@ __global__ __launch_bounds__(16 * WCO_, 1) void wgrad3x3_wino32_kernel(WgwArgs a
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + 32 * cg + acc_row(r, lane);
+      PMU_DCHECK(split < a.nsplit && co < a.Cout && ci < a.Cin, PMU_DBG_WORKSPACE);
       a.ws[(((long long)split * 16 + 4 * row + k) * a.Cout + co) * a.Cin + ci] = acc[k][r];
     }
 }
@@ -410,16 +414,16 @@ __global__ __launch_bounds__(256) void wgrad_wino_reduce_kernel(const float* __r
 // 64-channel blocks when Cout allows (PMU_WGW64=0: the 32-channel, 512-thread blocks everywhere)
 static bool wgw_v16() {  // PMU_WGRAD_WINO=16x16: the 16x16x4 layout (all components per wave)
   static const bool v = [] {
-    const char* e = getenv("PMU_WGRAD_WINO");
+    const char* e = pmu_variant_env("PMU_WGRAD_WINO");
     return e && strcmp(e, "16x16") == 0;
   }();
   return v;
 }
 static int wgw_wco(int Cout) {
   static const bool w64 = [] {
-    const char* e = getenv("PMU_WGW64");
+    const char* e = pmu_variant_env("PMU_WGW64");
 #ifdef PMU_EXPERIMENTS
-    if (getenv("PMU_WINO_EXP")) return false;  // the timing experiments are 32-channel kernels
+    if (pmu_variant_env("PMU_WINO_EXP")) return false;  // the timing experiments are 32-channel kernels
 #endif
     return !(e && atoi(e) == 0);
   }();
@@ -457,7 +461,7 @@ extern "C" size_t pmu_conv3x3_wgrad_ws_wino(int N, int H, int W, int Cin, int Co
 
 static int wino_prio() {  // PMU_WINO_PRIO=0|1 (A/B of static wave priority)
   static const int v = [] {
-    const char* e = getenv("PMU_WINO_PRIO");
+    const char* e = pmu_variant_env("PMU_WINO_PRIO");
     return e ? atoi(e) : 0;
   }();
   return v;
@@ -478,7 +482,7 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
 #ifdef PMU_EXPERIMENTS
   // timing experiments (wrong results for EXP != 0): only in `make EXPERIMENTS=1` builds
   static const int exp_ = [] {
-    const char* e = getenv("PMU_WINO_EXP");
+    const char* e = pmu_variant_env("PMU_WINO_EXP");
     return e ? atoi(e) : 0;
   }();
   if (exp_ == 1 || exp_ == 3) {

@@ -12,7 +12,8 @@ from ctypes import POINTER, c_double, c_float, c_int, c_longlong, c_size_t, c_vo
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-LIB_NAME = "libpmunet_hip.so"
+# PMU_LIB=debug selects the bounds-checked debug build (csrc: make DEBUG=1; see pmu_debug_read)
+LIB_NAME = "libpmunet_hip_debug.so" if os.environ.get("PMU_LIB") == "debug" else "libpmunet_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 HEADER_PATH = os.path.normpath(
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "include", "pmunet_hip.h"))
@@ -161,6 +162,9 @@ SIGNATURES = {
                               c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                               c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_void_p, c_void_p, c_void_p,
                               c_size_t, c_void_p]),
+    "pmu_build_flags": (c_int, []),
+    "pmu_debug_read": (c_int, [POINTER(c_int), POINTER(ctypes.c_char_p)]),
+    "pmu_debug_reset": (c_int, []),
 }
 
 _LIB = None
@@ -232,3 +236,39 @@ def ptr(t) -> int | None:
     if t is None:
         return None
     return t.data_ptr()
+
+
+BUILD_EXPERIMENTS, BUILD_DEBUG = 1, 2
+
+
+def build_flags() -> int:
+    return int(lib().pmu_build_flags())
+
+
+def experiments_build() -> bool:
+    """True for a `make EXPERIMENTS=1` library (kernel-variant A/B switches honoured)."""
+    return bool(build_flags() & BUILD_EXPERIMENTS)
+
+
+def debug_build() -> bool:
+    """True when the bounds-checked debug library (PMU_LIB=debug) is loaded."""
+    return bool(build_flags() & BUILD_DEBUG)
+
+
+DBG_CODES = {1: "operand read outside the operand tensor", 2: "store outside the output tensor",
+             3: "workgroup mapped outside the problem", 4: "data-dependent index out of range",
+             5: "workspace row out of range"}
+
+
+def debug_check(reset: bool = True) -> None:
+    """Debug build: raise if any kernel recorded an index-bound violation since the last reset
+    (synchronises the device).  No-op with the release library."""
+    out = (c_int * 5)()
+    tu = ctypes.c_char_p()
+    check(lib().pmu_debug_read(out, ctypes.byref(tu)), "pmu_debug_read")
+    if out[3]:
+        if reset:
+            check(lib().pmu_debug_reset(), "pmu_debug_reset")
+        where = tu.value.decode() if tu.value else "?"
+        raise RuntimeError(f"PMU debug build: {DBG_CODES.get(out[0], out[0])} at {os.path.basename(where)}:{out[1]} "
+                           f"(workgroup {out[2]})")

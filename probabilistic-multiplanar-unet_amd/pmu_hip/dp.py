@@ -12,7 +12,9 @@ all-reduces the whole buffer once after the backward, and then re-lays the buffe
 order (``functions.set_grad_order``).  From the second step on, bucket b holds the b-th stretch
 of gradients the backward emits, so when a bucket is complete its all-reduce is issued at once
 (RCCL's stream waits on an event of the compute stream at that point) and crosses xGMI while the
-rest of the backward still computes.  Buckets go out strictly in index order on every rank (the
+rest of the backward still computes (one micro-batch per rank and step, config c3's layout: with
+several, autograd adds each backward's gradients into .grad only after the node's kernels have
+run, so the exchange waits for the last backward and goes out whole in ``finish``).  Buckets go out strictly in index order on every rank (the
 collective order must match across ranks).  Parameters the backward never reported (e.g. the
 Probabilistic U-Net's ``unet.outc``, which gets no gradient) sit after the last bucket in a small
 tail that ``finish`` always exchanges, so every rank issues the same collectives.  The learned
@@ -91,6 +93,24 @@ class BucketAllReduce:
         self.sizes = [0] * len(self.buckets)
         for b in self.bucket_of.values():
             self.sizes[b] += 1
+        self._stale = True
+
+    def _zero_stale(self):
+        """Once after a relayout: the buffer still holds the old layout's values where the new one has
+        pads and the slots of parameters without a gradient (the tail is SUM-all-reduced every step,
+        so stale values there would grow by ~world per step).  Zero everything but the live
+        gradients' [off, off + numel) ranges (the optimizer has consumed the old-layout views)."""
+        self._stale = False
+        buf = flat_grad_buffer(self.net, self.plist)
+        offs = _offsets(self.net, self.plist)
+        lo, hi = buf.data_ptr(), buf.data_ptr() + buf.numel() * buf.element_size()
+        keep = sorted((offs[id(p)], offs[id(p)] + p.numel()) for p in self.plist
+                      if p.grad is not None and lo <= p.grad.data_ptr() < hi)
+        pos = 0
+        for a, b in keep + [(buf.numel(), buf.numel())]:
+            if a > pos:
+                buf[pos:a].zero_()
+            pos = max(pos, b)
 
     def _add(self, lo, hi, members):
         b = len(self.buckets)
@@ -103,6 +123,8 @@ class BucketAllReduce:
         self.works = []
         self.flushes = 0
         self.active = True
+        if getattr(self, "_stale", False):
+            self._zero_stale()
         if self.buckets is None:
             self.recording = []
             return

@@ -461,20 +461,45 @@ def pack_weights_wino4(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wp
 
 
+@dataclass
+class EngineConfig:
+    """Implementation choices of the fp32 3x3 convs, read ONCE from the environment at import (never
+    on the per-call hot path).  Tests switch them by assigning ``CFG``'s fields.
+
+    fp32_conv: "wino" (default: Winograd on materialised operands), "wino_fused" (the fused-staging
+        Winograd kernels everywhere) or "direct" (direct-sum MFMA kernels) — PMU_FP32_CONV;
+    wino2h: the 1024-thread F(2x2) kernels (default) or the 512-thread ones — PMU_WINO2H=0;
+    wino4: where F(4x4,3x3) runs — "dgrad" (default: the input gradient of maps >= 32x32) or "0"
+        (nowhere) — PMU_WINO4.  "1" (the forward too) breaks the model-level 1e-3 contract (see
+        wino4_ok) and is honoured only by an experiments build of the library (make EXPERIMENTS=1)."""
+    fp32_conv: str = "wino"
+    wino2h: bool = True
+    wino4: str = "dgrad"
+
+    @classmethod
+    def from_env(cls):
+        return cls(fp32_conv=os.environ.get("PMU_FP32_CONV", "wino"), wino2h=os.environ.get("PMU_WINO2H", "1") != "0",
+                   wino4=os.environ.get("PMU_WINO4", "dgrad"))
+
+
+CFG = EngineConfig.from_env()
+
+
 def wino4_ok(C: int, H: int, W: int, kind: str) -> bool:
     """Winograd F(4x4,3x3) on a materialised operand (pmu_conv3x3_*_wino4): reduction channels C % 8 == 0
     and images of at least 32 x 32 (its blocks are 32 x 32 output pixels; smaller maps keep F(2x2)).
 
-    Default (PMU_WINO4 unset or "dgrad"): the input gradient only.  F(4x4)'s fp32 rounding (~1e-6
-    relative rms, 5-10x the direct sum's; tools/wino_err.py) is harmless in the input gradient (c5
-    12-step Dice gap 2.7e-4 vs 2.2e-4 with F(2x2)), but in the forward it enters the BatchNorm
-    statistics: BN's backward amplifies it by |z|/sigma per element (UNet at batch 2 of 64x48: weight
-    gradients 2.6e-3 of their max, F(2x2) 7.9e-4) and the running statistics carry it into eval mode
-    (c5 12-step eval Dice gap 1.13e-3 > the 1e-3 contract).  PMU_WINO4=1 also runs the forward on
-    F(4x4) (A/B; kernel parity in tests/test_wino4_gpu.py), PMU_WINO4=0 keeps F(2x2) everywhere."""
-    mode = os.environ.get("PMU_WINO4", "dgrad")
-    return (C % 8 == 0 and H >= 32 and W >= 32 and (mode == "1" or mode == kind)
-            and os.environ.get("PMU_FP32_CONV", "wino") == "wino")
+    Default: the input gradient only.  F(4x4)'s fp32 rounding (~1e-6 relative rms, 5-10x the direct
+    sum's; tools/wino_err.py) is harmless in the input gradient (c5 12-step Dice gap 2.7e-4 vs 2.2e-4
+    with F(2x2)), but in the forward it enters the BatchNorm statistics: BN's backward amplifies it by
+    |z|/sigma per element (UNet at batch 2 of 64x48: weight gradients 2.6e-3 of their max, F(2x2)
+    7.9e-4) and the running statistics carry it into eval mode (c5 12-step eval Dice gap 1.13e-3 > the
+    1e-3 contract).  The forward on F(4x4) (CFG.wino4 == "1") is therefore an experiments-build A/B
+    only (kernel parity in tests/test_wino4_gpu.py)."""
+    mode = CFG.wino4
+    if mode == "1" and not L.experiments_build():
+        mode = "dgrad"
+    return C % 8 == 0 and H >= 32 and W >= 32 and (mode == "1" or mode == kind) and CFG.fp32_conv == "wino"
 
 
 def pack_weights_wino2h(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
@@ -489,19 +514,19 @@ def pack_weights_wino2h(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
 def wino2h_ok(C: int) -> bool:
     """The 1024-thread F(2x2) kernels (pmu_conv3x3_{fwd,dgrad}_wino2h; four waves per SIMD where the
     512-thread raw kernel runs two): C % 8 == 0.  kbench on the c2 shapes: forward 11.57 -> 10.98 ms
-    (256x256 layers 1.04 -> 0.90 ms).  PMU_WINO2H=0: the 512-thread raw kernels (A/B)."""
-    return C % 8 == 0 and os.environ.get("PMU_WINO2H", "1") != "0"
+    (256x256 layers 1.04 -> 0.90 ms).  CFG.wino2h False: the 512-thread raw kernels."""
+    return C % 8 == 0 and CFG.wino2h
 
 
 def use_wino() -> bool:
-    """fp32 3x3 convs (fwd and input gradient) by Winograd F(2x2,3x3) (PMU_FP32_CONV=direct: direct sum)."""
-    return os.environ.get("PMU_FP32_CONV", "wino") != "direct"
+    """fp32 3x3 convs (fwd and input gradient) by Winograd F(2x2,3x3) (CFG.fp32_conv "direct": direct sum)."""
+    return CFG.fp32_conv != "direct"
 
 
 def wino_raw_ok(C: int) -> bool:
-    """Winograd on a materialised operand (pmu_conv3x3_*_wino_raw): C % 16 == 0 (PMU_FP32_CONV=wino_fused
-    keeps the fused-staging Winograd kernels)."""
-    return C % 16 == 0 and os.environ.get("PMU_FP32_CONV", "wino") == "wino"
+    """Winograd on a materialised operand (pmu_conv3x3_*_wino_raw): C % 16 == 0 (CFG.fp32_conv
+    "wino_fused" keeps the fused-staging Winograd kernels)."""
+    return C % 16 == 0 and CFG.fp32_conv == "wino"
 
 
 def frame_to_f32(srcs, N, H, W) -> torch.Tensor:

@@ -294,6 +294,10 @@ def train_net(trainer, device, epochs=5, batch_size=1, lr=0.001, lrf=0.1, lrp=2,
                 with precision():
                     masks_pred = trainer.predict(imgs, true_masks)
                 loss = trainer.loss(imgs, true_masks, masks_pred) * scale
+                # the prediction's own graph is not the loss's for ProbUNetTrainer (the loss
+                # reconstructs from the posterior sample): drop it before the backward so its pending
+                # Fcomb node does not turn the reconstruction's gradients into non-flat tensors
+                del masks_pred
                 if sync is not None and i == len(step_mbs) - 1:
                     sync.begin()      # the last micro-batch's backward issues the bucket all-reduces
                 loss.backward()

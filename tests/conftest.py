@@ -28,3 +28,14 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _debug_build_bounds_check(request):
+    """PMU_LIB=debug (the bounds-checked debug library, csrc `make DEBUG=1`): after every GPU test,
+    fail it if any kernel recorded an index-bound violation (pmu_debug_read)."""
+    yield
+    if os.environ.get("PMU_LIB") == "debug" and request.node.get_closest_marker("gpu") is not None:
+        from pmu_hip import _lib as L
+        if L._LIB is not None:
+            L.debug_check()

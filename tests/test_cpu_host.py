@@ -184,3 +184,22 @@ def test_bench_roofline_peak_by_kernel_family():
     for k in ("pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw", "pmu_conv3x3_wgrad_wino",
               "pmu_convT2x2_wgrad", "pmu_fcomb_bwd"):
         assert bench.roofline_peak(k) == bench.FP32_MFMA_PEAK_TF, k
+
+
+def test_debug_build_exports_and_identifies_itself():
+    """The bounds-checked debug library (csrc `make DEBUG=1`, selected by PMU_LIB=debug) exports the
+    same C ABI and reports its build flags; the shipped library is neither a debug nor an experiments
+    build (kernel-variant A/B switches ignored)."""
+    import ctypes
+    from pmu_hip import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    rel = _lib.load_library(os.path.join(os.path.dirname(_lib.LIB_PATH), "libpmunet_hip.so"))
+    assert rel.pmu_build_flags() == 0
+    out = (ctypes.c_int * 5)(*([7] * 5))
+    assert rel.pmu_debug_read(out, None) == 0 and list(out) == [0] * 5
+    dbg_path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libpmunet_hip_debug.so")
+    if not os.path.exists(dbg_path):
+        pytest.skip("debug library not built (make -C csrc DEBUG=1)")
+    dbg = _lib.load_library(dbg_path)   # every SIGNATURES export must resolve
+    assert dbg.pmu_build_flags() == _lib.BUILD_DEBUG

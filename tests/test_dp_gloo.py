@@ -174,7 +174,12 @@ def _bucket_worker(rank, world, port, q, mode, acc):
                         len(sync.buckets or [])))
             sync.finish(idle=g is None)
             out = {k: p.grad.detach().numpy().copy() for k, p in named.items()}
-        q.put((rank, out, log))
+        # after the relayout the buffer's pads (and slots without a gradient) hold zeros, not the
+        # first layout's stale values
+        from pmu_hip.functions import _offsets, _slot, flat_grad_buffer
+        buf, offs = flat_grad_buffer(net, plist), _offsets(net, plist)
+        pad = sum(float(buf[offs[id(p)] + p.numel():offs[id(p)] + _slot(p.numel())].abs().sum()) for p in plist)
+        q.put((rank, out, log + [pad]))
     finally:
         dist.destroy_process_group()
 
@@ -189,6 +194,8 @@ def test_dp_bucketed_overlap_matches_reference_accumulation(mode, world, acc):
     for rank, out, log in res:
         err, key = grad_err({k: torch.from_numpy(out[k]) for k in ref}, ref)
         assert err <= 1e-5, (mode, rank, err, key)
+        log, pad = log[:-1], log[-1]
+        assert pad == 0.0, (mode, rank, pad)
         issued0, _, _, nb0 = log[0]
         assert issued0 == 0 and nb0 == 0            # round 0 records the report order
         for issued, first, flushes, nb in log[1:]:

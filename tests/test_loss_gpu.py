@@ -60,3 +60,25 @@ def test_losses_refuse_cpu_and_unused_options():
         BCELoss()(torch.rand(2, 2), torch.rand(2, 2))
     with pytest.raises(NotImplementedError):
         CrossEntropyLoss(label_smoothing=0.1)(torch.rand(2, 3), torch.zeros(2, dtype=torch.long))
+
+
+def test_cross_entropy_out_of_range_target_is_loud(dev):
+    """A class target outside [0, K) that is not ignore_index: torch raises; the HIP loss (no host
+    synchronisation on the hot path) returns NaN for the loss and that pixel's gradient, and the
+    bounds-checked debug build records the index (pmu_debug_read)."""
+    from pmu_hip import _lib as L
+    from pmu_hip.loss import CrossEntropyLoss
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 3, 8, 8, generator=g)
+    t = torch.randint(0, 3, (2, 8, 8), generator=g)
+    t[0, 0, 0] = 3
+    with pytest.raises(IndexError):
+        nn.CrossEntropyLoss()(x, t)
+    xd = x.to(dev).requires_grad_(True)
+    got = CrossEntropyLoss()(xd, t.to(dev))
+    got.backward()
+    assert torch.isnan(got).item()
+    assert torch.isnan(xd.grad[0, :, 0, 0]).all() and torch.isfinite(xd.grad[1]).all()
+    if L.debug_build():
+        with pytest.raises(RuntimeError, match="index out of range"):
+            L.debug_check()

@@ -201,7 +201,8 @@ def test_unet_wino_matches_direct(dev, monkeypatch, fused):
     xd, td = x.to(dev), target.to(dev)
 
     def step(mode):
-        monkeypatch.setenv("PMU_FP32_CONV", mode)
+        from pmu_hip import engine
+        monkeypatch.setattr(engine.CFG, "fp32_conv", mode)
         net.load_state_dict(sd0)
         for p in net.parameters():
             p.grad = None
