@@ -177,6 +177,18 @@ int pmu_conv3x3_fwd_raw(const unsigned short* xt, int Cp, int N, int H, int W, c
 int pmu_conv3x3_tiles_raw(int N, int H, int W, int Cout);
 int pmu_conv3x3_dgrad_raw(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                           int Cin, int Csplit, float* dx0, float* dx1, void* stream);
+/* The same convolutions with both operands staged by LDS-DMA (512-thread workgroups, 512- or
+ * 1024-pixel tiles, 16-channel chunks), for maps at least 32 wide: Cp % 16 == 0, Csplit == Cin or
+ * Csplit % 32 == 0 (pmu_conv3x3_dma_ok).  Weights packed by pmu_conv3x3_pack_dma (its own layout);
+ * part rows = pmu_conv3x3_tiles_dma().  Launches whose operand reaches 4 GiB are split over images. */
+int pmu_conv3x3_dma_ok(int H, int W, int Cp, int NOUT, int split);
+int pmu_conv3x3_tiles_dma(int N, int H, int W, int Cout);
+size_t pmu_conv3x3_packed_size_dma(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_dma(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream);
+int pmu_conv3x3_fwd_dma(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
+                        const float* bias, int Cout, float* z, float* part, void* stream);
+int pmu_conv3x3_dgrad_dma(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                          int Cin, int Csplit, float* dx0, float* dx1, void* stream);
 /* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels
  * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz
  * that pmu_conv3x3_wgrad_bf16 multiplies. */

@@ -1,0 +1,329 @@
+// 3x3 / pad 1 convolution of a materialised bf16 NHWC operand on bf16 MFMA, both operands staged by
+// LDS-DMA: config c5's forward and input gradient (nn.Conv2d at PMU/model/unet/unet_parts.py:15,18
+// under torch.autocast(bfloat16)), for maps at least 32 pixels wide.
+//
+// GEMM view per workgroup: BM output pixels (a TH x 32 tile of one image) x BN output channels, K =
+// 9 taps x channels in chunks of 16 (one v_mfma_f32_32x32x16_bf16 k-step per tap).  Per chunk the
+// (TH+2) x 34 halo image (16 channels) and the chunk's 9 x BN x 16 packed weights arrive by
+// global_load_lds (16 B per lane) in one of two LDS stages while the other stage feeds the MFMAs: no
+// staging registers, no ds_write, no transform.  The halo image serves all 9 taps from LDS.
+//
+// 512 threads = 8 waves (two per SIMD); a wave owns 128 pixels (4 tile rows = 4 32-row fragments) x
+// 64 channels (2 32-column fragments): 8 accumulators of 16, 6 ds_read_b128 per 8 MFMAs.  Two
+// shapes: BN = 128 (TH = 16, 512 pixels) and, for 64 output channels, BN = 64 (TH = 32, 1024 pixels).
+//
+// LDS-DMA writes each wave-instruction's 64 x 16 B contiguously, so the conflict-free layout is a
+// permutation of 16-B units, not a padded row: unit (pixel p, channel half q) sits at 2p + (q XOR
+// bit 3 of p).  A 32-lane fragment read (32 consecutive pixels, one half) then hits 16 distinct
+// 4-bank groups in each ds_read_b128 lane group, for any starting pixel (every tap).  The weights are
+// packed in the same order (channel co in place of the pixel), so their DMA is a straight copy.
+#include <cstdlib>
+
+#include "pmu_common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BK = 16;              // channels per chunk
+constexpr int TW = 32, HW2 = 34;    // tile width (one 32-pixel fragment per tile row), halo width
+constexpr int NT = 512, NWV = 8;
+
+template <int WN>
+struct DG {
+  static constexpr int BN = 64 * WN;
+  static constexpr int WM = NWV / WN;
+  static constexpr int TH = 4 * WM;
+  static constexpr int HP = (TH + 2) * HW2;
+  static constexpr int A_UNITS = 2 * HP;
+  static constexpr int B_UNITS = 18 * BN;       // 9 taps x BN channels x 2 halves
+  static constexpr int NGA = (A_UNITS + NT - 1) / NT;
+  static constexpr int NGB = (B_UNITS + NT - 1) / NT;
+  static constexpr int A_BYTES = 16 * A_UNITS;
+  static constexpr int STAGE = A_BYTES + 16 * B_UNITS;
+  static_assert(2 * STAGE <= 160 * 1024, "LDS");
+  static_assert(NGA <= 8, "gin / gzero masks");
+};
+
+struct DmaArgs {
+  const unsigned short* x;   // operand [N][H][W][Cp] bf16
+  const unsigned short* wp;  // packed [co block][chunk][tap][unit][8] bf16
+  const float* bias;
+  float* out0;
+  float* out1;
+  float* part;
+  int N, H, W, Cp, NOUT, split, tiles_w, tiles_h, nch, ncb;
+};
+
+__device__ __forceinline__ int swz(int p, int q) { return 2 * p + (q ^ ((p >> 3) & 1)); }
+__device__ __forceinline__ unsigned short bf16_bits(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
+
+// wp[jb][ch][tap][u][e]: unit u = swz(co, q) holds B[tap][k = 16 ch + 8 q + e][j = BN jb + co], zero
+// padded, bf16 RNE.  Forward: B[tap][ci][co] = w[co][ci][tap]; dgrad: B[tap][co][ci] = w[co][ci][8 - tap].
+__global__ __launch_bounds__(256) void pack_dma_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, int BN,
+                                                       unsigned short* __restrict__ wp) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  const int nch = (KC + BK - 1) / BK, njb = (NOUT + BN - 1) / BN;
+  const long long total = (long long)njb * nch * 9 * 2 * BN * 8;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int el = (int)(e & 7);
+    long long r = e >> 3;
+    const int u = (int)(r % (2 * BN)); r /= 2 * BN;
+    const int tap = (int)(r % 9); r /= 9;
+    const int ch = (int)(r % nch);
+    const int jb = (int)(r / nch);
+    const int co = u >> 1, q = (u & 1) ^ ((co >> 3) & 1);
+    const int j = jb * BN + co, k = ch * BK + 8 * q + el;
+    float v = 0.f;
+    if (j < NOUT && k < KC)
+      v = dgrad ? w[((long long)k * Cin + j) * 9 + (8 - tap)] : w[((long long)j * Cin + k) * 9 + tap];
+    wp[e] = bf16_bits(v);
+  }
+}
+
+template <bool DGRAD, int WN>
+__global__ __launch_bounds__(NT, 1) void conv3x3_dma_kernel(DmaArgs a) {
+  using G = DG<WN>;
+  constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (spatial tile, channel block), channel blocks fastest in XCD order: the channel blocks of one
+  // tile share its halo image through their XCD's L2
+  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+  const int cb = lb % a.ncb;
+  int t = lb / a.ncb;
+  const int tsp = t;
+  const int tw = t % a.tiles_w;
+  t /= a.tiles_w;
+  const int th = t % a.tiles_h;
+  const int n = t / a.tiles_h;
+  const int h0 = th * TH, w0 = tw * TW, j0 = cb * BN;
+  PMU_DCHECK(n < a.N && j0 < a.NOUT, PMU_DBG_GRID);
+
+  // operand units of this thread (DMA round r: unit (r * 8 + wave) * 64 + lane): 32-bit byte offset
+  // of chunk 0 and whether the unit is inside the image; units outside it are zero in both stages
+  unsigned goff[G::NGA];
+  unsigned gin = 0u;
+#pragma unroll
+  for (int r = 0; r < G::NGA; ++r) {
+    const int u = (r * NWV + wave) * 64 + lane;
+    const bool data = u < G::A_UNITS;
+    const int hp = u >> 1, q = (u & 1) ^ ((hp >> 3) & 1);
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    const int h = h0 - 1 + hr, w = w0 - 1 + hc;
+    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    goff[r] = in ? (unsigned)(((((long long)n * a.H + h) * a.W + w) * a.Cp + 8 * q) * 2) : 0u;
+    PMU_DCHECK(!in || (((long long)n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
+    gin |= in ? (1u << r) : 0u;
+    if (data && !in) {
+      *reinterpret_cast<uint4*>(smem + 16 * u) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(smem + G::STAGE + 16 * u) = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  const char* wsrc = reinterpret_cast<const char*>(a.wp) + (long long)cb * a.nch * G::B_UNITS * 16 + 16 * lane;
+
+#define PMU_GLDS(S, D)                                                                                      \
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
+                                   (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
+#define PMU_FETCH(CH, STG)                                                                                  \
+  {                                                                                                        \
+    PMU_DCHECK((CH) * BK + BK <= a.Cp, PMU_DBG_OPERAND);                                                   \
+    const char* xa_ = reinterpret_cast<const char*>(a.x) + (CH) * BK * 2;                                  \
+    unsigned char* st_ = (STG);                                                                            \
+    _Pragma("unroll") for (int r = 0; r < G::NGA; ++r)                                                     \
+      if ((gin >> r) & 1u) PMU_GLDS(xa_ + goff[r], st_ + (r * NWV + wave) * 1024)                         \
+    const char* wb_ = wsrc + (long long)(CH) * G::B_UNITS * 16;                                            \
+    _Pragma("unroll") for (int r = 0; r < G::NGB; ++r)                                                     \
+      if ((r + 1) * NT <= G::B_UNITS || (r * NWV + wave) * 64 + lane < G::B_UNITS)                          \
+        PMU_GLDS(wb_ + (r * NWV + wave) * 1024, st_ + G::A_BYTES + (r * NWV + wave) * 1024)               \
+  }
+
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int q = lane >> 5, li = lane & 31;
+  const int hpb = 4 * wm * HW2 + li;           // halo pixel of fragment 0, tap (0, 0)
+  int ub[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) ub[fn] = G::A_BYTES + 16 * swz(wn * 64 + fn * 32 + li, q);
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  PMU_FETCH(0, smem)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ch = 0; ch < a.nch; ++ch) {
+    const unsigned char* cur = smem + (ch & 1) * G::STAGE;
+    if (ch + 1 < a.nch) PMU_FETCH(ch + 1, smem + ((ch + 1) & 1) * G::STAGE)
+    bf16x8 op[2][FM + FN];
+    auto load_tap = [&](int tap, bf16x8 (&o)[FM + FN]) {
+      const int dy = tap / 3, dx = tap - 3 * (tap / 3);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int hp = hpb + (fm + dy) * HW2 + dx;
+        o[fm] = *reinterpret_cast<const bf16x8*>(cur + 16 * swz(hp, q));
+      }
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) o[FM + fn] = *reinterpret_cast<const bf16x8*>(cur + ub[fn] + tap * (32 * BN));
+    };
+    load_tap(0, op[0]);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) load_tap(tap + 1, op[(tap + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[tap & 1][fm], op[tap & 1][FM + fn], acc[fm][fn],
+                                                                 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
+    __syncthreads();
+  }
+#undef PMU_FETCH
+#undef PMU_GLDS
+
+  // epilogue: accumulator (fm, fn, r) = output pixel (tile row 4 wm + fm, column acc_row(r, lane)),
+  // channel j0 + 64 wn + 32 fn + (lane & 31); a 32-channel destination is uniform (split % 32 == 0)
+  float* red = reinterpret_cast<float*>(smem);  // [8 waves][64][2] (the stages are free now)
+  float s1[FN], s2[FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    s1[fn] = 0.f;
+    s2[fn] = 0.f;
+    const int jb = j0 + wn * 64 + fn * 32;
+    const int j = jb + li;
+    const bool jok = j < a.NOUT;
+    const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+    float* dstp;
+    int ld;
+    if (!DGRAD) { dstp = a.out0 + j; ld = a.NOUT; }
+    else if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
+    else { dstp = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int h = h0 + 4 * wm + fm;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int w = w0 + acc_row(r, lane);
+        if (!jok || h >= a.H || w >= a.W) continue;
+        const long long pix = ((long long)n * a.H + h) * a.W + w;
+        PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+        const float v = acc[fm][fn][r] + b;
+        dstp[pix * ld] = v;
+        if (!DGRAD) {
+          s1[fn] += v;
+          s2[fn] = fmaf(v, v, s2[fn]);
+        }
+      }
+    }
+  }
+  if (!DGRAD && a.part) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] += __shfl_xor(s1[fn], 32, 64);
+      s2[fn] += __shfl_xor(s2[fn], 32, 64);
+      if (lane < 32) {
+        red[(wave * 64 + fn * 32 + lane) * 2 + 0] = s1[fn];
+        red[(wave * 64 + fn * 32 + lane) * 2 + 1] = s2[fn];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {  // channel tid = 64 wn + c: summed over the WM waves of column group wn, in order
+      const int j = j0 + tid, wnn = tid >> 6, c = tid & 63;
+      if (j < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int m = 0; m < WM; ++m) {
+          t1 += red[((m * WN + wnn) * 64 + c) * 2 + 0];
+          t2 += red[((m * WN + wnn) * 64 + c) * 2 + 1];
+        }
+        PMU_DCHECK(tsp < a.N * a.tiles_h * a.tiles_w, PMU_DBG_WORKSPACE);
+        a.part[((long long)tsp * 2 + 0) * a.NOUT + j] = t1;
+        a.part[((long long)tsp * 2 + 1) * a.NOUT + j] = t2;
+      }
+    }
+  }
+}
+
+// channel-block width: 64 for <= 64 output channels (1024-pixel tiles), else 128 (512-pixel tiles)
+static int dma_wn(int NOUT) { return NOUT <= 64 ? 1 : 2; }
+static int dma_th(int NOUT) { return dma_wn(NOUT) == 1 ? 32 : 16; }
+
+static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, const unsigned short* wp, const float* bias,
+                      int NOUT, float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
+  PMU_REQUIRE(x && wp && out0 && N > 0 && H > 0 && W >= 32 && Cp > 0 && Cp % BK == 0 && NOUT > 0);
+  PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && out1));
+  const long long img_bytes = (long long)H * W * Cp * 2;
+  if ((long long)N * img_bytes >= (1LL << 32)) {  // 32-bit DMA byte offsets: split over images
+    const long long tiles = (long long)pmu_cdiv(W, TW) * pmu_cdiv(H, dma_th(NOUT));
+    return pmu_image_chunks(N, img_bytes, [&](int n0, int nn) {
+      const long long px = (long long)n0 * H * W;
+      return launch_dma(x + px * Cp, Cp, nn, H, W, wp, bias, NOUT, out0 + px * (dgrad ? split : NOUT),
+                        out1 ? out1 + px * (NOUT - split) : nullptr, split,
+                        part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream);
+    });
+  }
+  DmaArgs a;
+  a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
+  a.N = N; a.H = H; a.W = W; a.Cp = Cp; a.NOUT = NOUT; a.split = dgrad ? split : NOUT;
+  a.nch = Cp / BK;
+  const int wn = dma_wn(NOUT);
+  a.ncb = pmu_cdiv(NOUT, 64 * wn);
+  a.tiles_w = pmu_cdiv(W, TW);
+  a.tiles_h = pmu_cdiv(H, dma_th(NOUT));
+  const long long blocks = (long long)a.tiles_w * a.tiles_h * N * a.ncb;
+  PMU_REQUIRE(blocks < (1LL << 31));
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)blocks);
+  if (wn == 1 && dgrad) hipLaunchKernelGGL((conv3x3_dma_kernel<true, 1>), grid, dim3(NT), 0, st, a);
+  else if (wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<false, 1>), grid, dim3(NT), 0, st, a);
+  else if (dgrad) hipLaunchKernelGGL((conv3x3_dma_kernel<true, 2>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_dma_kernel<false, 2>), grid, dim3(NT), 0, st, a);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+}  // namespace
+
+extern "C" int pmu_conv3x3_dma_ok(int H, int W, int Cp, int NOUT, int split) {
+  return W >= 32 && H >= 1 && Cp % BK == 0 && NOUT > 0 && (split == NOUT || split % 32 == 0);
+}
+
+extern "C" int pmu_conv3x3_tiles_dma(int N, int H, int W, int Cout) {
+  return N * pmu_cdiv(H, dma_th(Cout)) * pmu_cdiv(W, TW);
+}
+
+extern "C" size_t pmu_conv3x3_packed_size_dma(int Cout, int Cin, int dgrad) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  const int BN = 64 * dma_wn(NOUT);
+  return (size_t)pmu_cdiv(NOUT, BN) * pmu_cdiv(KC, BK) * 9 * 2 * BN * 8 * sizeof(unsigned short);
+}
+
+extern "C" int pmu_conv3x3_pack_dma(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream) {
+  PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
+  const int NOUT = dgrad ? Cin : Cout;
+  const long long total = (long long)(pmu_conv3x3_packed_size_dma(Cout, Cin, dgrad) / sizeof(unsigned short));
+  long long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(pack_dma_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad,
+                     64 * dma_wn(NOUT), wp);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_conv3x3_fwd_dma(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                   const float* bias, int Cout, float* z, float* part, void* stream) {
+  return launch_dma(xt, Cp, N, H, W, wp, bias, Cout, z, nullptr, Cout, part, false, stream);
+}
+
+extern "C" int pmu_conv3x3_dgrad_dma(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                     int Cin, int Csplit, float* dx0, float* dx1, void* stream) {
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
+}

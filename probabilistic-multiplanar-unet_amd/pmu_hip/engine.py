@@ -208,10 +208,20 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
                z.data_ptr(), L.ptr(part), s)
     elif bf16:
         Cp = _pad8(sum(sr.C for sr in srcs))
-        use_raw = raw_ok(N, H, W, Cp)
-        R = lb.pmu_conv3x3_tiles_raw(N, H, W, Cout) if use_raw else lb.pmu_conv3x3_tiles(N, H, W)
+        use_dma = dma_ok(H, W, Cp, Cout, Cout)
+        use_raw = use_dma or raw_ok(N, H, W, Cp)
+        R = (lb.pmu_conv3x3_tiles_dma(N, H, W, Cout) if use_dma else
+             lb.pmu_conv3x3_tiles_raw(N, H, W, Cout) if use_raw else lb.pmu_conv3x3_tiles(N, H, W))
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
-        if use_raw:
+        if use_dma:
+            # both operands by LDS-DMA (maps >= 32 wide): the operand written once in bf16, as below
+            xt = frame_to_bf16(srcs, N, H, W)
+            wp = pack_weights_dma(conv.weight, dgrad=False)
+            L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), Cp, N, H, W, wp.data_ptr(), L.ptr(conv.bias), Cout,
+                   z.data_ptr(), L.ptr(part), s)
+            if not keep:
+                xt = None
+        elif use_raw:
             # the operand (BN+ReLU / max-pool / F.pad+cat applied) written once in bf16; the GEMM
             # streams it, and the weight gradient reuses it
             xt = frame_to_bf16(srcs, N, H, W)
@@ -407,7 +417,11 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split):
         sp = Cin if split is None else split
         dx0 = _empty(N, H, W, sp, device=dev)
         dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin else None
-        if raw_ok(N, H, W, dzt.shape[3]) and (sp == Cin or sp % 32 == 0):
+        if dma_ok(H, W, dzt.shape[3], Cin, sp):
+            wp = pack_weights_dma(conv.weight, dgrad=True)
+            L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
+                   dx0.data_ptr(), L.ptr(dx1), s)
+        elif raw_ok(N, H, W, dzt.shape[3]) and (sp == Cin or sp % 32 == 0):
             wp = pack_weights_raw(conv.weight, dgrad=True)
             L.call("pmu_conv3x3_dgrad_raw", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
                    dx0.data_ptr(), L.ptr(dx1), s)
@@ -423,6 +437,21 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split):
     L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(), ws.data_ptr(),
            wsb, s)
     return res
+
+
+def dma_ok(H, W, Cp, NOUT, split) -> bool:
+    """Shapes of the LDS-DMA bf16 conv (pmu_conv3x3_{fwd,dgrad}_dma): maps >= 32 wide, Cp % 16 == 0,
+    a concat split on a 32-channel boundary."""
+    return bool(L.lib().pmu_conv3x3_dma_ok(H, W, Cp, NOUT, split))
+
+
+def pack_weights_dma(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """Weights rounded to bf16 in the LDS-DMA conv's swizzled unit order (pmu_conv3x3_pack_dma)."""
+    Cout, Cin = w.shape[0], w.shape[1]
+    n = L.lib().pmu_conv3x3_packed_size_dma(Cout, Cin, int(dgrad)) // 2
+    wp = torch.empty(n, dtype=torch.int16, device=w.device)
+    L.call("pmu_conv3x3_pack_dma", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
 
 
 def pack_weights_raw(w: torch.Tensor, dgrad: bool) -> torch.Tensor:

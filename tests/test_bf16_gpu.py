@@ -516,3 +516,58 @@ def test_c5_geometry_bf16_step_vs_oracle(dev):
     for k, v in net.state_dict().items():
         if k.endswith("running_mean") or k.endswith("running_var"):
             assert float((v.double().cpu() - work[k]).abs().max()) <= 1e-3 * max(1.0, float(work[k].abs().max())), k
+
+
+def _pack_dma(w, dgrad):
+    from pmu_hip import _lib as L
+    n = L.lib().pmu_conv3x3_packed_size_dma(w.shape[0], w.shape[1], int(dgrad)) // 2
+    wp = torch.empty(n, dtype=torch.int16, device=w.device)
+    L.call("pmu_conv3x3_pack_dma", w.data_ptr(), w.shape[0], w.shape[1], int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 40, 40, 64, 96), (1, 33, 64, 32, 64), (2, 32, 32, 128, 128),
+                                            (1, 17, 45, 48, 200), (4, 64, 96, 64, 64), (2, 16, 33, 16, 256)])
+def test_conv3x3_fwd_dma(dev, N, H, W, Cin, Cout):
+    """The LDS-DMA bf16 conv (both operands by global_load_lds, swizzled units) == conv of the rounded
+    operand: partial tiles in both directions, ragged channel blocks, both block shapes (64 / 128
+    output channels), BN partial sums."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    g = torch.Generator().manual_seed(71 + H + Cout)
+    z0 = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    coef = torch.cat([torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.2]).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    xt = _to_bf16([Src(z0, L.SRC_BNRELU, coef)], N, H, W, Cin)
+    assert L.lib().pmu_conv3x3_dma_ok(H, W, xt.shape[3], Cout, Cout) == 1
+    z = torch.empty(N, H, W, Cout, device=dev)
+    part = torch.full((L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cout), 2 * Cout), float("nan"), device=dev)
+    L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), xt.shape[3], N, H, W, _pack_dma(w, False).data_ptr(), b.data_ptr(),
+           Cout, z.data_ptr(), part.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = _ref_conv(_bf16_values(xt, Cin), w, b)
+    assert _rel(z, ref) <= TOL
+    s = part.view(-1, 2, Cout).double().sum(0).cpu()
+    assert _rel(s[0], z.double().cpu().reshape(-1, Cout).sum(0)) <= 1e-4
+    assert _rel(s[1], (z.double().cpu().reshape(-1, Cout) ** 2).sum(0)) <= 1e-4
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 36, 40, 128, 64, 64), (1, 32, 48, 96, 128, 32),
+                                                  (2, 20, 64, 64, 32, 64), (3, 40, 32, 256, 128, 128)])
+def test_conv3x3_dgrad_dma(dev, N, H, W, Cin, Cout, split):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    g = torch.Generator().manual_seed(81 + H)
+    dz = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    dzt = _to_bf16([Src(dz)], N, H, W, Cout)
+    dx0 = torch.empty(N, H, W, split, device=dev)
+    dx1 = torch.empty(N, H, W, Cin - split, device=dev) if split < Cin else None
+    L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), dzt.shape[3], N, H, W, _pack_dma(w, True).data_ptr(), Cin, split,
+           dx0.data_ptr(), L.ptr(dx1), L.stream())
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, W), _rb(w).double().cpu(), _nchw(_rb(dz)).double().cpu(),
+                                     padding=1).permute(0, 2, 3, 1)
+    got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
+    assert _rel(got, ref) <= TOL

@@ -42,7 +42,13 @@ def main():
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--only", default=None, help="H,Cin,Cout of a single shape")
     ap.add_argument("--unpacked", action="store_true", help="stage weights from the PyTorch layout")
+    ap.add_argument("--c5", action="store_true", help="config c5's layer shapes (512x512 input) at batch 16")
     args = ap.parse_args()
+    if args.c5:
+        global SHAPES
+        SHAPES = [(2 * h, ci, co) for (h, ci, co) in SHAPES]
+        if "--N" not in sys.argv:
+            args.N = 16
     dev = torch.device("cuda")
     N = args.N
     s = L.stream()
@@ -106,7 +112,18 @@ def main():
         part4 = torch.empty(L.lib().pmu_conv3x3_tiles_wino4(N, H, W), 2 * Cout, device=dev)
         from pmu_hip.engine import pack_weights_wino2h
         w2f, w2d = pack_weights_wino2h(w, False), pack_weights_wino2h(w, True)
+        def packd(wt, dg):
+            n = L.lib().pmu_conv3x3_packed_size_dma(wt.shape[0], wt.shape[1], int(dg)) // 2
+            t = torch.empty(n, dtype=torch.int16, device=dev)
+            L.call("pmu_conv3x3_pack_dma", wt.data_ptr(), wt.shape[0], wt.shape[1], int(dg), t.data_ptr(), s)
+            return t
+        wdf, wdd = packd(w, False), packd(w, True)
+        partd = torch.empty(L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cout), 2 * Cout, device=dev)
         ops = {
+            "fwd_dma": lambda: L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), cpi, N, H, W, wdf.data_ptr(), b.data_ptr(),
+                                      Cout, out.data_ptr(), partd.data_ptr(), s),
+            "dgrad_dma": lambda: L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), cpo, N, H, W, wdd.data_ptr(), Cin, Cin,
+                                        dx.data_ptr(), None, s),
             "fwd_raw": lambda: L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), cpi, N, H, W, wrf.data_ptr(), b.data_ptr(),
                                       Cout, out.data_ptr(), partr.data_ptr(), s),
             "dgrad_raw": lambda: L.call("pmu_conv3x3_dgrad_raw", dzt.data_ptr(), cpo, N, H, W, wrd.data_ptr(), Cin, Cin,
@@ -159,7 +176,7 @@ def main():
             tot.setdefault(op, [0.0, 0.0])
             tot[op][0] += ms
             tot[op][1] += flops
-            peak = 2516.0 if (op.endswith("bf16") or op.endswith("raw")) else 157.3
+            peak = 2516.0 if (op.endswith("bf16") or op.endswith("raw") or op.endswith("dma")) else 157.3
             print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / peak * 100:5.1f}%)",
                   flush=True)
     for op, (ms, fl) in tot.items():
