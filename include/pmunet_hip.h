@@ -182,7 +182,7 @@ int pmu_conv3x3_dgrad_raw(const unsigned short* dzt, int Cp, int N, int H, int W
  * Csplit % 32 == 0 (pmu_conv3x3_dma_ok).  Weights packed by pmu_conv3x3_pack_dma (its own layout);
  * part rows = pmu_conv3x3_tiles_dma().  Launches whose operand reaches 4 GiB are split over images. */
 int pmu_conv3x3_dma_ok(int H, int W, int Cp, int NOUT, int split);
-int pmu_conv3x3_tiles_dma(int N, int H, int W, int Cout);
+int pmu_conv3x3_tiles_dma(int N, int H, int W, int Cout, int Cp);
 size_t pmu_conv3x3_packed_size_dma(int Cout, int Cin, int dgrad);
 int pmu_conv3x3_pack_dma(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream);
 int pmu_conv3x3_fwd_dma(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
@@ -213,6 +213,18 @@ int pmu_convT2x2_dgrad_bf16(const float* du, int Hd, int Wd, int off_h, int off_
                             int N, int H, int W, int Cin, int Cout, float* dx, void* stream);
 /* Weight gradient from materialised bf16 operands: xt [N][H][W][pad8(Cin)] (the convT input after BN+ReLU)
  * and dut [N][Hd][Wd][pad8(Cout)] (du); dbias (nullable) sums the fp32 du over the output region. */
+/* The same forward / input gradient with both GEMM operands staged by LDS-DMA from materialised bf16
+ * tensors: xt = the BN+ReLU operand [N][H][W][Cip] (pmu_frame_to_bf16), dut = du [N][Hd][Wd][Cop];
+ * weights packed by pmu_convT2x2_pack_dma (2 * 4*Cin*Cout bytes).  Cin % 32 == 0, Cout % 32 == 0 and
+ * the GEMM column count (forward 4*Cout, dgrad Cin) % 128 == 0 (pmu_convT2x2_dma_ok). */
+int pmu_convT2x2_dma_ok(int Cin, int Cout, int dgrad);
+size_t pmu_convT2x2_packed_size_dma(int Cin, int Cout);
+int pmu_convT2x2_pack_dma(const float* w, int Cin, int Cout, int dgrad, unsigned short* wp, void* stream);
+int pmu_convT2x2_fwd_dma(const unsigned short* xt, int Cip, int N, int H, int W, const unsigned short* wp,
+                         const float* bias, int Cin, int Cout, float* u, void* stream);
+int pmu_convT2x2_dgrad_dma(const unsigned short* dut, int Cop, int Hd, int Wd, int off_h, int off_w,
+                           const unsigned short* wp, int N, int H, int W, int Cin, int Cout, float* dx,
+                           void* stream);
 size_t pmu_convT2x2_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);
 int pmu_convT2x2_wgrad_bf16(const unsigned short* xt, const unsigned short* dut, const float* du, int N, int H,
                             int W, int Hd, int Wd, int off_h, int off_w, int Cin, int Cout, float* dw,

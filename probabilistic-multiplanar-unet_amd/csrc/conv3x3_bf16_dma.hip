@@ -8,9 +8,10 @@
 // global_load_lds (16 B per lane) in one of two LDS stages while the other stage feeds the MFMAs: no
 // staging registers, no ds_write, no transform.  The halo image serves all 9 taps from LDS.
 //
-// 512 threads = 8 waves (two per SIMD); a wave owns 128 pixels (4 tile rows = 4 32-row fragments) x
-// 64 channels (2 32-column fragments): 8 accumulators of 16, 6 ds_read_b128 per 8 MFMAs.  Two
-// shapes: BN = 128 (TH = 16, 512 pixels) and, for 64 output channels, BN = 64 (TH = 32, 1024 pixels).
+// A wave owns 128 pixels (4 tile rows = 4 32-row fragments) x 64 channels (2 32-column fragments): 8
+// accumulators of 16, 6 ds_read_b128 per 8 MFMAs, ~236 VGPRs (two waves per SIMD).  Two workgroup
+// shapes (dma_shape): 512 pixels x 128 channels in 8 waves (one workgroup per CU), and 512 pixels x
+// 64 channels in 4 waves (two per CU) for <= 64 output channels or reductions of <= 128 channels.
 //
 // LDS-DMA writes each wave-instruction's 64 x 16 B contiguously, so the conflict-free layout is a
 // permutation of 16-B units, not a padded row: unit (pixel p, channel half q) sits at 2p + (q XOR
@@ -27,10 +28,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BK = 16;              // channels per chunk
 constexpr int TW = 32, HW2 = 34;    // tile width (one 32-pixel fragment per tile row), halo width
-constexpr int NT = 512, NWV = 8;
 
-template <int WN>
+// NWV waves per workgroup (8: one workgroup per CU; 4: two per CU, one's prologue / epilogue under
+// the other's MFMAs), WN of them across the BN = 64 WN output channels
+template <int WN, int NWV>
 struct DG {
+  static constexpr int NT = 64 * NWV;
   static constexpr int BN = 64 * WN;
   static constexpr int WM = NWV / WN;
   static constexpr int TH = 4 * WM;
@@ -81,10 +84,10 @@ __global__ __launch_bounds__(256) void pack_dma_kernel(const float* __restrict__
   }
 }
 
-template <bool DGRAD, int WN>
-__global__ __launch_bounds__(NT, 1) void conv3x3_dma_kernel(DmaArgs a) {
-  using G = DG<WN>;
-  constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH;
+template <bool DGRAD, int WN, int NWV>
+__global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs a) {
+  using G = DG<WN, NWV>;
+  constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH, NT = G::NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // (spatial tile, channel block), channel blocks fastest in XCD order: the channel blocks of one
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_dma_kernel(DmaArgs a) {
 
   // epilogue: accumulator (fm, fn, r) = output pixel (tile row 4 wm + fm, column acc_row(r, lane)),
   // channel j0 + 64 wn + 32 fn + (lane & 31); a 32-channel destination is uniform (split % 32 == 0)
-  float* red = reinterpret_cast<float*>(smem);  // [8 waves][64][2] (the stages are free now)
+  float* red = reinterpret_cast<float*>(smem);  // [NWV waves][64][2] (the stages are free now)
   float s1[FN], s2[FN];
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
@@ -252,17 +255,25 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_dma_kernel(DmaArgs a) {
   }
 }
 
-// channel-block width: 64 for <= 64 output channels (1024-pixel tiles), else 128 (512-pixel tiles)
-static int dma_wn(int NOUT) { return NOUT <= 64 ? 1 : 2; }
-static int dma_th(int NOUT) { return dma_wn(NOUT) == 1 ? 32 : 16; }
+// Workgroup shape: 64 output channels x 512 pixels in 4 waves (two workgroups per CU) for <= 64
+// output channels or a short reduction (K <= 128 channels: a few chunks per tile, the prologue and
+// the output stores are a large share); else 128 channels x 512 pixels in 8 waves
+struct Shape {
+  int wn, nwv, th;
+};
+static Shape dma_shape(int NOUT, int KC) {
+  if (NOUT <= 64 || KC <= 128) return {1, 4, 16};
+  return {2, 8, 16};
+}
 
 static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, const unsigned short* wp, const float* bias,
                       int NOUT, float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
   PMU_REQUIRE(x && wp && out0 && N > 0 && H > 0 && W >= 32 && Cp > 0 && Cp % BK == 0 && NOUT > 0);
   PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && out1));
+  const Shape sh = dma_shape(NOUT, Cp);
   const long long img_bytes = (long long)H * W * Cp * 2;
   if ((long long)N * img_bytes >= (1LL << 32)) {  // 32-bit DMA byte offsets: split over images
-    const long long tiles = (long long)pmu_cdiv(W, TW) * pmu_cdiv(H, dma_th(NOUT));
+    const long long tiles = (long long)pmu_cdiv(W, TW) * pmu_cdiv(H, sh.th);
     return pmu_image_chunks(N, img_bytes, [&](int n0, int nn) {
       const long long px = (long long)n0 * H * W;
       return launch_dma(x + px * Cp, Cp, nn, H, W, wp, bias, NOUT, out0 + px * (dgrad ? split : NOUT),
@@ -274,18 +285,17 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
   a.N = N; a.H = H; a.W = W; a.Cp = Cp; a.NOUT = NOUT; a.split = dgrad ? split : NOUT;
   a.nch = Cp / BK;
-  const int wn = dma_wn(NOUT);
-  a.ncb = pmu_cdiv(NOUT, 64 * wn);
+  a.ncb = pmu_cdiv(NOUT, 64 * sh.wn);
   a.tiles_w = pmu_cdiv(W, TW);
-  a.tiles_h = pmu_cdiv(H, dma_th(NOUT));
+  a.tiles_h = pmu_cdiv(H, sh.th);
   const long long blocks = (long long)a.tiles_w * a.tiles_h * N * a.ncb;
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((unsigned)blocks);
-  if (wn == 1 && dgrad) hipLaunchKernelGGL((conv3x3_dma_kernel<true, 1>), grid, dim3(NT), 0, st, a);
-  else if (wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<false, 1>), grid, dim3(NT), 0, st, a);
-  else if (dgrad) hipLaunchKernelGGL((conv3x3_dma_kernel<true, 2>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((conv3x3_dma_kernel<false, 2>), grid, dim3(NT), 0, st, a);
+  const dim3 grid((unsigned)blocks), blk(64 * sh.nwv);
+  if (sh.wn == 1 && dgrad) hipLaunchKernelGGL((conv3x3_dma_kernel<true, 1, 4>), grid, blk, 0, st, a);
+  else if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<false, 1, 4>), grid, blk, 0, st, a);
+  else if (dgrad) hipLaunchKernelGGL((conv3x3_dma_kernel<true, 2, 8>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_dma_kernel<false, 2, 8>), grid, blk, 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -296,24 +306,24 @@ extern "C" int pmu_conv3x3_dma_ok(int H, int W, int Cp, int NOUT, int split) {
   return W >= 32 && H >= 1 && Cp % BK == 0 && NOUT > 0 && (split == NOUT || split % 32 == 0);
 }
 
-extern "C" int pmu_conv3x3_tiles_dma(int N, int H, int W, int Cout) {
-  return N * pmu_cdiv(H, dma_th(Cout)) * pmu_cdiv(W, TW);
+extern "C" int pmu_conv3x3_tiles_dma(int N, int H, int W, int Cout, int Cp) {
+  return N * pmu_cdiv(H, dma_shape(Cout, Cp).th) * pmu_cdiv(W, TW);
 }
 
 extern "C" size_t pmu_conv3x3_packed_size_dma(int Cout, int Cin, int dgrad) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
-  const int BN = 64 * dma_wn(NOUT);
+  const int BN = 64 * dma_shape(NOUT, (KC + BK - 1) / BK * BK).wn;
   return (size_t)pmu_cdiv(NOUT, BN) * pmu_cdiv(KC, BK) * 9 * 2 * BN * 8 * sizeof(unsigned short);
 }
 
 extern "C" int pmu_conv3x3_pack_dma(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream) {
   PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
-  const int NOUT = dgrad ? Cin : Cout;
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
   const long long total = (long long)(pmu_conv3x3_packed_size_dma(Cout, Cin, dgrad) / sizeof(unsigned short));
   long long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(pack_dma_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad,
-                     64 * dma_wn(NOUT), wp);
+                     64 * dma_shape(NOUT, (KC + BK - 1) / BK * BK).wn, wp);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

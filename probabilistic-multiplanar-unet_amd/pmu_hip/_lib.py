@@ -163,13 +163,20 @@ SIGNATURES = {
                               c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_void_p, c_void_p, c_void_p,
                               c_size_t, c_void_p]),
     "pmu_conv3x3_dma_ok": (c_int, [c_int, c_int, c_int, c_int, c_int]),
-    "pmu_conv3x3_tiles_dma": (c_int, [c_int, c_int, c_int, c_int]),
+    "pmu_conv3x3_tiles_dma": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_conv3x3_packed_size_dma": (c_size_t, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_fwd_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                       c_void_p, c_void_p]),
+    "pmu_convT2x2_dma_ok": (c_int, [c_int, c_int, c_int]),
+    "pmu_convT2x2_packed_size_dma": (c_size_t, [c_int, c_int]),
+    "pmu_convT2x2_pack_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_fwd_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                                     c_void_p, c_void_p]),
+    "pmu_convT2x2_dgrad_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int,
+                                       c_int, c_int, c_void_p, c_void_p]),
     "pmu_build_flags": (c_int, []),
     "pmu_debug_read": (c_int, [POINTER(c_int), POINTER(ctypes.c_char_p)]),
     "pmu_debug_reset": (c_int, []),

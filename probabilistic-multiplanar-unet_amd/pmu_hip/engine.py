@@ -210,7 +210,7 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         Cp = _pad8(sum(sr.C for sr in srcs))
         use_dma = dma_ok(H, W, Cp, Cout, Cout)
         use_raw = use_dma or raw_ok(N, H, W, Cp)
-        R = (lb.pmu_conv3x3_tiles_dma(N, H, W, Cout) if use_dma else
+        R = (lb.pmu_conv3x3_tiles_dma(N, H, W, Cout, Cp) if use_dma else
              lb.pmu_conv3x3_tiles_raw(N, H, W, Cout) if use_raw else lb.pmu_conv3x3_tiles(N, H, W))
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
         if use_dma:
@@ -576,6 +576,14 @@ def pack_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wp
 
 
+def pack_convT_weights_dma(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """ConvT weights rounded to bf16 in the LDS-DMA GEMMs' swizzled unit order (pmu_convT2x2_pack_dma)."""
+    Cin, Cout = w.shape[0], w.shape[1]
+    wp = torch.empty(L.lib().pmu_convT2x2_packed_size_dma(Cin, Cout) // 2, dtype=torch.int16, device=w.device)
+    L.call("pmu_convT2x2_pack_dma", w.data_ptr(), Cin, Cout, int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
 def pack_convT_weights_bf16(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     """ConvT weights rounded to bf16 in pmu_convT2x2_pack's layouts (pmu_convT2x2_pack_bf16)."""
     Cin, Cout = w.shape[0], w.shape[1]
@@ -609,6 +617,7 @@ class UpState:
     c1: ConvBNOut
     c2: ConvBNOut
     bf16: bool = False       # convT input gradient on bf16 MFMA where its shapes allow
+    xt: torch.Tensor | None = None   # bf16: the convT operand the forward materialised (weight gradient)
 
 
 class UNetState:
@@ -679,7 +688,18 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         Cup = convT.out_channels
         u = _empty(N, 2 * hi, 2 * wi, Cup, device=dev)
         fin = frame_of([cur.act()], N, hi, wi)
-        if bf16 and L.lib().pmu_convT2x2_bf16_ok(fin, Cup):
+        Cin_t = cur.z.shape[3]
+        xtT = None
+        if bf16 and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 0):
+            # the BN+ReLU operand written once in bf16 (the weight gradient's operand too), both GEMM
+            # operands by LDS-DMA
+            xtT = frame_to_bf16([cur.act()], N, hi, wi)
+            wpt = pack_convT_weights_dma(convT.weight, dgrad=False)
+            L.call("pmu_convT2x2_fwd_dma", xtT.data_ptr(), xtT.shape[3], N, hi, wi, wpt.data_ptr(), L.ptr(convT.bias),
+                   Cin_t, Cup, u.data_ptr(), L.stream())
+            if not keep:
+                xtT = None
+        elif bf16 and L.lib().pmu_convT2x2_bf16_ok(fin, Cup):
             wpt = pack_convT_weights_bf16(convT.weight, dgrad=False)
             L.call("pmu_convT2x2_fwd_bf16", fin, wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
         else:
@@ -693,7 +713,7 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         srcs = [skip.act(), Src(u, L.SRC_RAW, off=off)]
         o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev, bf16=bf16, keep=keep)
         o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev, bf16=bf16, keep=keep)
-        st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2, bf16=bf16))
+        st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2, bf16=bf16, xt=xtT))
         cur = o2
     st.feat_src = cur
     if net.apply_last_layer:
@@ -754,7 +774,12 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         Hd, Wd = dup.shape[1], dup.shape[2]
         Cup = convT.out_channels
         dx = _empty(N, hi, wi, Cin_t, device=dev)
-        if us.bf16 and Cin_t % 128 == 0 and Cup % 32 == 0:
+        dut = frame_to_bf16([Src(dup)], N, Hd, Wd) if us.bf16 else None
+        if us.bf16 and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 1):
+            wpt = pack_convT_weights_dma(convT.weight, dgrad=True)
+            L.call("pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd, Wd, us.off[0], us.off[1], wpt.data_ptr(),
+                   N, hi, wi, Cin_t, Cup, dx.data_ptr(), s)
+        elif us.bf16 and Cin_t % 128 == 0 and Cup % 32 == 0:
             wpt = pack_convT_weights_bf16(convT.weight, dgrad=True)
             L.call("pmu_convT2x2_dgrad_bf16", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], wpt.data_ptr(), N, hi, wi,
                    Cin_t, Cup, dx.data_ptr(), s)
@@ -766,8 +791,8 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         dbt = grads.new(convT.bias) if convT.bias is not None else None
         if us.bf16:
             # bf16 operands materialised (the convT input after BN+ReLU, du); the bias gradient sums fp32 du
-            xt = frame_to_bf16([prev.act()], N, hi, wi)
-            dut = frame_to_bf16([Src(dup)], N, Hd, Wd)
+            xt = us.xt if us.xt is not None else frame_to_bf16([prev.act()], N, hi, wi)
+            us.xt = None
             wsb = L.lib().pmu_convT2x2_wgrad_ws_bf16(N, hi, wi, Cin_t, Cup)
             ws = _empty(max(1, (wsb + 3) // 4), device=dev)
             L.call("pmu_convT2x2_wgrad_bf16", xt.data_ptr(), dut.data_ptr(), dup.data_ptr(), N, hi, wi, Hd, Wd,

@@ -542,7 +542,7 @@ def test_conv3x3_fwd_dma(dev, N, H, W, Cin, Cout):
     xt = _to_bf16([Src(z0, L.SRC_BNRELU, coef)], N, H, W, Cin)
     assert L.lib().pmu_conv3x3_dma_ok(H, W, xt.shape[3], Cout, Cout) == 1
     z = torch.empty(N, H, W, Cout, device=dev)
-    part = torch.full((L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cout), 2 * Cout), float("nan"), device=dev)
+    part = torch.full((L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cout, xt.shape[3]), 2 * Cout), float("nan"), device=dev)
     L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), xt.shape[3], N, H, W, _pack_dma(w, False).data_ptr(), b.data_ptr(),
            Cout, z.data_ptr(), part.data_ptr(), L.stream())
     torch.cuda.synchronize()
@@ -571,3 +571,54 @@ def test_conv3x3_dgrad_dma(dev, N, H, W, Cin, Cout, split):
                                      padding=1).permute(0, 2, 3, 1)
     got = dx0 if dx1 is None else torch.cat([dx0, dx1], dim=3)
     assert _rel(got, ref) <= TOL
+
+
+def _packT_dma(w, dgrad):
+    from pmu_hip import _lib as L
+    wp = torch.empty(L.lib().pmu_convT2x2_packed_size_dma(w.shape[0], w.shape[1]) // 2, dtype=torch.int16,
+                     device=w.device)
+    L.call("pmu_convT2x2_pack_dma", w.data_ptr(), w.shape[0], w.shape[1], int(dgrad), wp.data_ptr(), L.stream())
+    return wp
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 16, 16, 128, 64), (3, 9, 7, 64, 32), (1, 32, 24, 256, 128),
+                                            (2, 13, 11, 96, 256)])
+def test_convT_fwd_dma(dev, N, H, W, Cin, Cout):
+    """ConvT forward with both GEMM operands by LDS-DMA (the bf16 BN+ReLU operand materialised once):
+    == conv_transpose2d of the rounded operand and weights; ragged M tiles, both tile shapes."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    g = torch.Generator().manual_seed(91 + H)
+    z = torch.randn(N, H, W, Cin, generator=g).to(dev)
+    coef = torch.cat([torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.2]).to(dev)
+    w = (torch.randn(Cin, Cout, 2, 2, generator=g) * 0.1).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    assert L.lib().pmu_convT2x2_dma_ok(Cin, Cout, 0) == 1
+    xt = _to_bf16([Src(z, L.SRC_BNRELU, coef)], N, H, W, Cin)
+    u = torch.empty(N, 2 * H, 2 * W, Cout, device=dev)
+    L.call("pmu_convT2x2_fwd_dma", xt.data_ptr(), xt.shape[3], N, H, W, _packT_dma(w, False).data_ptr(), b.data_ptr(),
+           Cin, Cout, u.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = TF.conv_transpose2d(_nchw(_bf16_values(xt, Cin)).double().cpu(), _rb(w).double().cpu(), b.double().cpu(),
+                              stride=2).permute(0, 2, 3, 1)
+    assert _rel(u, ref) <= TOL
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,oh,ow", [(2, 16, 16, 128, 64, 0, 0), (2, 10, 9, 256, 32, 1, 0),
+                                                  (1, 8, 12, 128, 128, 0, 1), (3, 5, 7, 384, 96, 1, 1)])
+def test_convT_dgrad_dma(dev, N, H, W, Cin, Cout, oh, ow):
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src
+    g = torch.Generator().manual_seed(97 + H)
+    Hd, Wd = 2 * H + oh + (1 if oh else 0), 2 * W + ow + (1 if ow else 0)
+    du = torch.randn(N, Hd, Wd, Cout, generator=g).to(dev)
+    w = (torch.randn(Cin, Cout, 2, 2, generator=g) * 0.1).to(dev)
+    assert L.lib().pmu_convT2x2_dma_ok(Cin, Cout, 1) == 1
+    dut = _to_bf16([Src(du)], N, Hd, Wd, Cout)
+    dx = torch.empty(N, H, W, Cin, device=dev)
+    L.call("pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd, Wd, oh, ow, _packT_dma(w, True).data_ptr(), N, H,
+           W, Cin, Cout, dx.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    dui = du[:, oh:oh + 2 * H, ow:ow + 2 * W]
+    ref = TF.conv2d(_nchw(_rb(dui)).double().cpu(), _rb(w).double().cpu(), stride=2).permute(0, 2, 3, 1)
+    assert _rel(dx, ref) <= TOL

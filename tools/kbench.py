@@ -118,7 +118,7 @@ def main():
             L.call("pmu_conv3x3_pack_dma", wt.data_ptr(), wt.shape[0], wt.shape[1], int(dg), t.data_ptr(), s)
             return t
         wdf, wdd = packd(w, False), packd(w, True)
-        partd = torch.empty(L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cout), 2 * Cout, device=dev)
+        partd = torch.empty(L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cout, cpi), 2 * Cout, device=dev)
         ops = {
             "fwd_dma": lambda: L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), cpi, N, H, W, wdf.data_ptr(), b.data_ptr(),
                                       Cout, out.data_ptr(), partd.data_ptr(), s),

@@ -26,7 +26,13 @@ def main():
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--N", type=int, default=32)
+    ap.add_argument("--c5", action="store_true", help="config c5's decoder shapes (512x512 input), batch 16")
     args = ap.parse_args()
+    global SHAPES
+    if args.c5:
+        SHAPES = [(2 * h, ci, co) for (h, ci, co) in SHAPES]
+        if "--N" not in sys.argv:
+            args.N = 16
     dev = torch.device("cuda")
     N, s = args.N, L.stream()
     tot = {}
@@ -46,7 +52,23 @@ def main():
         wsb = L.lib().pmu_convT2x2_wgrad_ws(N, H, W, Cin, Cout)
         ws = torch.empty(max(1, (wsb + 3) // 4), device=dev)
         flops = 2.0 * N * H * W * Cin * Cout * 4
+        from pmu_hip.engine import frame_to_bf16, pack_convT_weights_bf16, pack_convT_weights_dma
+        xt = frame_to_bf16([Src(z, L.SRC_BNRELU, coef)], N, H, W)
+        dut = frame_to_bf16([Src(du)], N, Hd, Wd)
+        wbf, wbd = pack_convT_weights_bf16(w, False), pack_convT_weights_bf16(w, True)
+        wdf, wdd = pack_convT_weights_dma(w, False), pack_convT_weights_dma(w, True)
+        wsbb = L.lib().pmu_convT2x2_wgrad_ws_bf16(N, H, W, Cin, Cout)
+        wsb16 = torch.empty(max(1, (wsbb + 3) // 4), device=dev)
         ops = {
+            "fwd_bf16": lambda: L.call("pmu_convT2x2_fwd_bf16", fin, wbf.data_ptr(), b.data_ptr(), Cout, u.data_ptr(), s),
+            "fwd_dma": lambda: L.call("pmu_convT2x2_fwd_dma", xt.data_ptr(), xt.shape[3], N, H, W, wdf.data_ptr(),
+                                      b.data_ptr(), Cin, Cout, u.data_ptr(), s),
+            "dgrad_bf16": lambda: L.call("pmu_convT2x2_dgrad_bf16", du.data_ptr(), Hd, Wd, 0, 0, wbd.data_ptr(), N, H, W,
+                                         Cin, Cout, dx.data_ptr(), s),
+            "dgrad_dma": lambda: L.call("pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd, Wd, 0, 0,
+                                        wdd.data_ptr(), N, H, W, Cin, Cout, dx.data_ptr(), s),
+            "wgrad_bf16": lambda: L.call("pmu_convT2x2_wgrad_bf16", xt.data_ptr(), dut.data_ptr(), du.data_ptr(), N, H, W,
+                                         Hd, Wd, 0, 0, Cin, Cout, dw.data_ptr(), db.data_ptr(), wsb16.data_ptr(), wsbb, s),
             "fwd": lambda: L.call("pmu_convT2x2_fwd", fin, w.data_ptr(), wpf.data_ptr(), b.data_ptr(), Cout,
                                   u.data_ptr(), s),
             "dgrad": lambda: L.call("pmu_convT2x2_dgrad", du.data_ptr(), Hd, Wd, 0, 0, w.data_ptr(), wpd.data_ptr(),
@@ -62,7 +84,8 @@ def main():
             tot.setdefault(op, [0.0, 0.0])
             tot[op][0] += ms
             tot[op][1] += flops
-            print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / 157.3 * 100:5.1f}%)",
+            peak = 2516.0 if ("bf16" in op or "dma" in op) else 157.3
+            print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / peak * 100:5.1f}%)",
                   flush=True)
     for op, (ms, fl) in tot.items():
         print(f"TOTAL {op:6s} {ms:8.3f} ms  {fl / (ms * 1e-3) / 1e12:7.2f} TF")
