@@ -128,6 +128,13 @@ int pmu_conv3x3_fwd_wino2h(const float* xt, int Cin, int N, int H, int W, const 
                            int Cout, float* z, float* part, void* stream);
 int pmu_conv3x3_dgrad_wino2h(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
                              int Csplit, float* dx0, float* dx1, void* stream);
+/* The input gradient fused with the BatchNorm+ReLU backward reduction of the layer that produced this
+ * conv's operand (dx is that layer's da, no concat split): part[pmu_conv3x3_tiles_wino2h rows][2][Cin]
+ * = (sum g, sum g*xhat), g = dx * (z*coef[c]+coef[Cin+c] > 0), xhat = (z-mean)*invstd — the sums
+ * pmu_bn_bwd_reduce(dx, z, ...) computes, without reading dx back (PMU/model/unet/unet_parts.py:16-17). */
+int pmu_conv3x3_dgrad_wino2h_bnr(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                                 float* dx, const float* z, const float* coef, const float* mean,
+                                 const float* invstd, float* part, void* stream);
 /* ---- fp32 Winograd F(4x4,3x3) on a materialised operand (images >= 32 x 32: the c2 fp32 default) --
  * Replaces the same nn.Conv2d forward / input gradient (PMU/model/unet/unet_parts.py:15,18; autograd of
  * PMU/model/unet/unet_model.py:31-54) as pmu_conv3x3_*_wino_raw: 36 per-component GEMMs of
@@ -142,6 +149,10 @@ int pmu_conv3x3_fwd_wino4(const float* xt, int Cin, int N, int H, int W, const f
                           int Cout, float* z, float* part, void* stream);
 int pmu_conv3x3_dgrad_wino4(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
                             int Csplit, float* dx0, float* dx1, void* stream);
+/* as pmu_conv3x3_dgrad_wino2h_bnr (part rows = pmu_conv3x3_tiles_wino4) */
+int pmu_conv3x3_dgrad_wino4_bnr(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                                float* dx, const float* z, const float* coef, const float* mean,
+                                const float* invstd, float* part, void* stream);
 /* dw[Cout][Cin][3][3] from the teed operands dzt [N][H][W][Cout] and xt [N][H][W][Cin] (fp32), by
  * Winograd F(2x2,3x3): dw = G^T [sum over 2x2 tiles of (A dY A^T) .* (B^T X B)] G.  Cout % 32 == 0,
  * Cin % 64 == 0 (pmu_conv3x3_wgrad_ws_wino returns 0 otherwise); ws must hold that many bytes. */
@@ -189,6 +200,10 @@ int pmu_conv3x3_fwd_dma(const unsigned short* xt, int Cp, int N, int H, int W, c
                         const float* bias, int Cout, float* z, float* part, void* stream);
 int pmu_conv3x3_dgrad_dma(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                           int Cin, int Csplit, float* dx0, float* dx1, void* stream);
+/* as pmu_conv3x3_dgrad_wino2h_bnr (part rows = pmu_conv3x3_tiles_dma(N, H, W, Cin, Cp)) */
+int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                              int Cin, float* dx, const float* z, const float* coef, const float* mean,
+                              const float* invstd, float* part, void* stream);
 /* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels
  * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz
  * that pmu_conv3x3_wgrad_bf16 multiplies. */

@@ -56,6 +56,12 @@ struct DmaArgs {
   float* out1;
   float* part;
   int N, H, W, Cp, NOUT, split, tiles_w, tiles_h, nch, ncb;
+  // input gradient only: the producer layer's BatchNorm+ReLU backward partial sums (see
+  // pmu_conv3x3_dgrad_wino4_bnr); null: none
+  const float* bz;
+  const float* bcoef;
+  const float* bmean;
+  const float* binv;
 };
 
 __device__ __forceinline__ int swz(int p, int q) { return 2 * p + (q ^ ((p >> 3) & 1)); }
@@ -204,6 +210,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     const int j = jb + li;
     const bool jok = j < a.NOUT;
     const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+    const bool bnr = DGRAD && a.bz && jok;
+    const float bsc = bnr ? a.bcoef[j] : 0.f, bsh = bnr ? a.bcoef[a.NOUT + j] : 0.f;
+    const float bmu = bnr ? a.bmean[j] : 0.f, bis = bnr ? a.binv[j] : 0.f;
     float* dstp;
     int ld;
     if (!DGRAD) { dstp = a.out0 + j; ld = a.NOUT; }
@@ -223,11 +232,16 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
         if (!DGRAD) {
           s1[fn] += v;
           s2[fn] = fmaf(v, v, s2[fn]);
+        } else if (bnr) {
+          const float zz = a.bz[pix * a.NOUT + j];
+          const float gg = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
+          s1[fn] += gg;
+          s2[fn] = fmaf(gg, (zz - bmu) * bis, s2[fn]);
         }
       }
     }
   }
-  if (!DGRAD && a.part) {
+  if (a.part) {  // forward: BN partial sums of the output; input gradient: of the producer's BN backward
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       s1[fn] += __shfl_xor(s1[fn], 32, 64);
@@ -267,7 +281,9 @@ static Shape dma_shape(int NOUT, int KC) {
 }
 
 static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, const unsigned short* wp, const float* bias,
-                      int NOUT, float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
+                      int NOUT, float* out0, float* out1, int split, float* part, bool dgrad, void* stream,
+                      const float* bz = nullptr, const float* bcoef = nullptr, const float* bmean = nullptr,
+                      const float* binv = nullptr) {
   PMU_REQUIRE(x && wp && out0 && N > 0 && H > 0 && W >= 32 && Cp > 0 && Cp % BK == 0 && NOUT > 0);
   PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && out1));
   const Shape sh = dma_shape(NOUT, Cp);
@@ -278,13 +294,15 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
       const long long px = (long long)n0 * H * W;
       return launch_dma(x + px * Cp, Cp, nn, H, W, wp, bias, NOUT, out0 + px * (dgrad ? split : NOUT),
                         out1 ? out1 + px * (NOUT - split) : nullptr, split,
-                        part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream);
+                        part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream,
+                        bz ? bz + px * NOUT : nullptr, bcoef, bmean, binv);
     });
   }
   DmaArgs a;
   a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
   a.N = N; a.H = H; a.W = W; a.Cp = Cp; a.NOUT = NOUT; a.split = dgrad ? split : NOUT;
   a.nch = Cp / BK;
+  a.bz = bz; a.bcoef = bcoef; a.bmean = bmean; a.binv = binv;
   a.ncb = pmu_cdiv(NOUT, 64 * sh.wn);
   a.tiles_w = pmu_cdiv(W, TW);
   a.tiles_h = pmu_cdiv(H, sh.th);
@@ -336,4 +354,12 @@ extern "C" int pmu_conv3x3_fwd_dma(const unsigned short* xt, int Cp, int N, int 
 extern "C" int pmu_conv3x3_dgrad_dma(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                                      int Cin, int Csplit, float* dx0, float* dx1, void* stream) {
   return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
+}
+
+// As pmu_conv3x3_dgrad_wino4_bnr (part rows = pmu_conv3x3_tiles_dma(N, H, W, Cin, Cp)).
+extern "C" int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                         int Cin, float* dx, const float* z, const float* coef, const float* mean,
+                                         const float* invstd, float* part, void* stream) {
+  PMU_REQUIRE(z && coef && mean && invstd && part);
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream, z, coef, mean, invstd);
 }

@@ -60,6 +60,13 @@ struct W4Args {
   int prio;           // 1: waves of component half 1 run at s_setprio 1 (PMU_WINO4_PRIO)
   int ts, tc;         // 2-D workgroup grouping (spatial x co-groups per group; tc = 0: co-groups fastest)
   int N;              // images (bounds checks of the debug build)
+  // input gradient only: BatchNorm+ReLU backward partial sums of the layer that produced the operand
+  // of this conv (dx is that layer's da): part[spatial][2][NOUT] += (sum g, sum g*xhat) with
+  // g = dx * (z*scale+shift > 0), xhat = (z-mean)*invstd (pmu_bn_bwd_reduce's sums); null: none
+  const float* bz;
+  const float* bcoef;
+  const float* bmean;
+  const float* binv;
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -355,6 +362,13 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
   const int j = j0 + 16 * CH + (lane & 15);
   const bool jok = j < a.NOUT;
   float s1 = 0.f, s2 = 0.f;
+  float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
+  if (DGRAD && a.bz && jok) {
+    bsc = a.bcoef[j];
+    bsh = a.bcoef[a.NOUT + j];
+    bmu = a.bmean[j];
+    bis = a.binv[j];
+  }
 #pragma unroll
   for (int rho = 0; rho < 2; ++rho) {
     if (rho) __syncthreads();  // round 0's reads are done before xb is rewritten
@@ -390,6 +404,12 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
             s2 = fmaf(v, v, s2);
           } else if (j < a.split) {
             a.out0[pix * a.split + j] = v;
+            if (a.bz) {
+              const float zz = a.bz[pix * a.NOUT + j];
+              const float g = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
+              s1 += g;
+              s2 = fmaf(g, (zz - bmu) * bis, s2);
+            }
           } else {
             a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
           }
@@ -397,7 +417,7 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
       }
     }
   }
-  if (!DGRAD && a.part) {
+  if (a.part) {  // forward: BN partial sums of the output; input gradient: of the producer's BN backward
     s1 += __shfl_xor(s1, 16, 64);
     s2 += __shfl_xor(s2, 16, 64);
     s1 += __shfl_xor(s1, 32, 64);
@@ -573,7 +593,9 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
 }
 
 int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
-                 float* out0, float* out1, int split, float* part, bool dgrad, void* stream) {
+                 float* out0, float* out1, int split, float* part, bool dgrad, void* stream,
+                 const float* bz = nullptr, const float* bcoef = nullptr, const float* bmean = nullptr,
+                 const float* binv = nullptr) {
   PMU_REQUIRE(x && wp && out0 && KC > 0 && KC % BK == 0 && NOUT > 0 && N > 0 && H > 0 && W > 0);
   const long long img_bytes = (long long)H * W * (KC > NOUT ? KC : NOUT) * 4;
   if ((long long)N * img_bytes >= (1LL << 32)) {  // 32-bit DMA byte offsets: split over images
@@ -582,7 +604,8 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
       const long long px = (long long)n0 * H * W;
       return launch_wino4(x + px * KC, KC, nn, H, W, wp, bias, NOUT, out0 + px * split,
                   out1 ? out1 + px * (NOUT - split) : nullptr, split,
-                  part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream);
+                  part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream,
+                  bz ? bz + px * NOUT : nullptr, bcoef, bmean, binv);
     });
   }
   W4Args a;
@@ -590,6 +613,7 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
   a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
   a.H = H; a.W = W; a.KC = KC; a.NOUT = NOUT; a.split = split;
   a.N = N;
+  a.bz = bz; a.bcoef = bcoef; a.bmean = bmean; a.binv = binv;
   a.bw = pmu_cdiv(W, OW);
   a.bh = pmu_cdiv(H, OH);
   a.nco = pmu_cdiv(NOUT, CO);
@@ -671,4 +695,15 @@ extern "C" int pmu_conv3x3_dgrad_wino4(const float* dzt, int Cout, int N, int H,
                                        int Csplit, float* dx0, float* dx1, void* stream) {
   PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
   return launch_wino4(dzt, Cout, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
+}
+
+// The input gradient fused with the BatchNorm+ReLU backward reduction of the layer whose output
+// this conv consumed (dx = that layer's da): part[pmu_conv3x3_tiles_wino4 rows][2][Cin] as
+// pmu_bn_bwd_reduce would compute them from (dx, z) — dx is not read back.
+extern "C" int pmu_conv3x3_dgrad_wino4_bnr(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
+                                           float* dx, const float* z, const float* coef, const float* mean,
+                                           const float* invstd, float* part, void* stream) {
+  PMU_REQUIRE(z && coef && mean && invstd && part);
+  return launch_wino4(dzt, Cout, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream, z, coef, mean,
+                      invstd);
 }

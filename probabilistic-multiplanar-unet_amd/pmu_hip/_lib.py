@@ -177,6 +177,12 @@ SIGNATURES = {
                                      c_void_p, c_void_p]),
     "pmu_convT2x2_dgrad_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int,
                                        c_int, c_int, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_wino2h_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_wino4_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_build_flags": (c_int, []),
     "pmu_debug_read": (c_int, [POINTER(c_int), POINTER(ctypes.c_char_p)]),
     "pmu_debug_reset": (c_int, []),

@@ -35,6 +35,7 @@ class Src:
     z: torch.Tensor | None = None    # BNBWD only
     pool: int = L.POOL_NONE
     off: tuple = (0, 0)
+    prod: object = None              # the ConvBNOut whose activation this is (SRC_BNRELU sources)
 
     @property
     def C(self) -> int:
@@ -142,17 +143,23 @@ def bn_forward(part, R: int, C: int, count: int, bn: torch.nn.BatchNorm2d, train
     return BNState(coef=coef, mean=mean, invstd=invstd, count=float(count))
 
 
-def bn_backward(da: torch.Tensor, z: torch.Tensor, st: BNState, bn: torch.nn.BatchNorm2d, grads, conv_bias=None):
-    """Returns (bcoef, dgamma, dbeta, dbias) for BN+ReLU backward given da = dL/d relu(bn(z))."""
+def bn_backward(da: torch.Tensor, z: torch.Tensor, st: BNState, bn: torch.nn.BatchNorm2d, grads, conv_bias=None,
+                pre=None):
+    """Returns (bcoef, dgamma, dbeta, dbias) for BN+ReLU backward given da = dL/d relu(bn(z)).
+    pre: (part, R) — the partial sums (sum g, sum g*xhat) already formed by the kernel that produced
+    da (a *_bnr input gradient); else pmu_bn_bwd_reduce reads da and z for them."""
     s = L.stream()
     dev = z.device
     N, H, W, C = z.shape
     P = N * H * W
     lb = L.lib()
-    R = lb.pmu_bn_bwd_tiles(P, C)
-    part = _empty(R, 2 * C, device=dev)
-    L.call("pmu_bn_bwd_reduce", da.data_ptr(), z.data_ptr(), st.coef.data_ptr(), st.mean.data_ptr(),
-           st.invstd.data_ptr(), P, C, part.data_ptr(), s)
+    if pre is not None:
+        part, R = pre
+    else:
+        R = lb.pmu_bn_bwd_tiles(P, C)
+        part = _empty(R, 2 * C, device=dev)
+        L.call("pmu_bn_bwd_reduce", da.data_ptr(), z.data_ptr(), st.coef.data_ptr(), st.mean.data_ptr(),
+               st.invstd.data_ptr(), P, C, part.data_ptr(), s)
     G = lb.pmu_colsum_groups(R)
     acc = _empty(G, 2 * C, dtype=torch.float64, device=dev)
     L.call("pmu_colsum_f64", part.data_ptr(), R, 2 * C, acc.data_ptr(), G, s)
@@ -178,9 +185,10 @@ class ConvBNOut:
     bf16: bool = False                          # computed on the bf16-MFMA kernels
     xt: torch.Tensor | None = None              # bf16: the operand copy the forward kernel wrote (for wgrad)
     xt32: torch.Tensor | None = None            # fp32: the same, teed by pmu_conv3x3_fwd (RAW wgrad operand)
+    bnr: tuple | None = None                    # (da, part, R): BN-backward partials formed by the consumer's dgrad
 
     def act(self, pool=L.POOL_NONE) -> Src:
-        return Src(self.z, L.SRC_BNRELU, self.bn.coef, pool=pool)
+        return Src(self.z, L.SRC_BNRELU, self.bn.coef, pool=pool, prod=self)
 
 
 def first_layer_ok(cin: int, cout: int) -> bool:
@@ -283,6 +291,18 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
                      xt32=None if (bf16 or planes is not None) else xt32)
 
 
+def _bnr_producer(out: ConvBNOut, need_dx: bool, split):
+    """The ConvBNOut whose BatchNorm+ReLU backward partial sums this conv's input gradient can form in
+    its epilogue: the operand is that layer's unpooled activation alone and its batch statistics exist."""
+    if not need_dx or split is not None or len(out.srcs) != 1:
+        return None
+    sr = out.srcs[0]
+    p = sr.prod
+    if sr.mode != L.SRC_BNRELU or sr.pool != L.POOL_NONE or p is None or p.bn.mean is None or sr.x is not p.z:
+        return None
+    return p
+
+
 def tee32_ok(cin: int, cout: int) -> bool:
     """Channel counts for which the fp32 weight gradient runs on teed RAW operands (its 64x64 blocks)."""
     return cin % 64 == 0 and cout % 64 == 0
@@ -297,15 +317,20 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     z = out.z
     N, H, W, Cout = z.shape
     dev = z.device
-    bcoef, _, _, _ = bn_backward(da, z, out.bn, bn, grads, conv.bias)
+    pre = None
+    if out.bnr is not None and out.bnr[0] is da:
+        pre = out.bnr[1:]
+    out.bnr = None
+    bcoef, _, _, _ = bn_backward(da, z, out.bn, bn, grads, conv.bias, pre=pre)
     dz_src = Src(da, L.SRC_BNBWD, bcoef, z=z)
     dzf = frame_of([dz_src], N, H, W)
     dw = grads.new(conv.weight)
     lb = L.lib()
+    prod = _bnr_producer(out, need_dx, split)
     if out.bf16:
-        return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split)
+        return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split, prod)
     if out.xt32 is not None and need_dx:
-        return _conv_backward_tee32(out, dz_src, conv, dw, split)
+        return _conv_backward_tee32(out, dz_src, conv, dw, split, prod)
     if out.planes is not None:
         Cin = len(out.planes)
         wsb = lb.pmu_conv_first_wgrad_ws(N, H, W, Cin, Cout)
@@ -319,12 +344,23 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
         L.call("pmu_conv3x3_wgrad", dzf, frame_of(out.srcs, N, H, W), Cout, dw.data_ptr(), ws.data_ptr(), wsb, s)
     if not need_dx or out.planes is not None:
         return None
-    return _dgrad32(dz_src, conv, N, H, W, split, None)
+    return _dgrad32(dz_src, conv, N, H, W, split, None, prod)
 
 
-def _dgrad32(dz_src, conv, N, H, W, split, tee):
+def _bnr_call(name, prod, R, lead, dx, s):
+    """Launch a *_bnr input gradient (lead: its leading arguments up to Cin) and leave the producer's
+    BN-backward partials on it for its own conv_bn_backward."""
+    C = prod.z.shape[3]
+    part = _empty(R, 2 * C, device=dx.device)
+    L.call(name, *lead, dx.data_ptr(), prod.z.data_ptr(), prod.bn.coef.data_ptr(), prod.bn.mean.data_ptr(),
+           prod.bn.invstd.data_ptr(), part.data_ptr(), s)
+    prod.bnr = (dx, part, R)
+
+
+def _dgrad32(dz_src, conv, N, H, W, split, tee, prod=None):
     """fp32 input gradient of a 3x3 conv (Winograd or direct); dx, or (dx0, dx1) split at ``split``.
-    tee: receives dz (the BN+ReLU backward applied) for the weight gradient."""
+    tee: receives dz (the BN+ReLU backward applied) for the weight gradient.  prod: the layer whose
+    BN-backward partial sums the Winograd kernels form in their epilogue (see _bnr_producer)."""
     s = L.stream()
     dev = conv.weight.device
     Cin, Cout = conv.in_channels, conv.out_channels
@@ -332,18 +368,27 @@ def _dgrad32(dz_src, conv, N, H, W, split, tee):
     dx0 = _empty(N, H, W, sp, device=dev)
     dx1 = _empty(N, H, W, Cin - sp, device=dev) if split is not None else None
     dzf = frame_of([dz_src], N, H, W)
+    lb = L.lib()
     if use_wino() and wino4_ok(Cout, H, W, "dgrad"):
         dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
         L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
         wp = pack_weights_wino4(conv.weight, dgrad=True)
-        L.call("pmu_conv3x3_dgrad_wino4", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
-               L.ptr(dx1), s)
+        if prod is not None:
+            _bnr_call("pmu_conv3x3_dgrad_wino4_bnr", prod, lb.pmu_conv3x3_tiles_wino4(N, H, W),
+                      (dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin), dx0, s)
+        else:
+            L.call("pmu_conv3x3_dgrad_wino4", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
+                   L.ptr(dx1), s)
     elif use_wino() and wino_raw_ok(Cout) and wino2h_ok(Cout):
         dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
         L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
         wp = pack_weights_wino2h(conv.weight, dgrad=True)
-        L.call("pmu_conv3x3_dgrad_wino2h", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
-               L.ptr(dx1), s)
+        if prod is not None:
+            _bnr_call("pmu_conv3x3_dgrad_wino2h_bnr", prod, lb.pmu_conv3x3_tiles_wino2h(N, H, W),
+                      (dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin), dx0, s)
+        else:
+            L.call("pmu_conv3x3_dgrad_wino2h", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
+                   L.ptr(dx1), s)
     elif use_wino() and wino_raw_ok(Cout):
         dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
         L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
@@ -360,7 +405,7 @@ def _dgrad32(dz_src, conv, N, H, W, split, tee):
     return dx0 if split is None else (dx0, dx1)
 
 
-def _conv_backward_tee32(out: ConvBNOut, dz_src, conv, dw, split):
+def _conv_backward_tee32(out: ConvBNOut, dz_src, conv, dw, split, prod=None):
     """fp32 backward with materialised operands: the input-gradient kernel tees dz (BN+ReLU backward
     applied) as it stages it, and the weight gradient multiplies that with the operand the forward
     teed — both RAW frames, so its staging is a plain copy."""
@@ -370,7 +415,7 @@ def _conv_backward_tee32(out: ConvBNOut, dz_src, conv, dw, split):
     dev = out.z.device
     Cin = conv.in_channels
     dzt = _empty(N, H, W, Cout, device=dev)
-    res = _dgrad32(dz_src, conv, N, H, W, split, dzt)
+    res = _dgrad32(dz_src, conv, N, H, W, split, dzt, prod)
     wsb = lb.pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout) if use_wino() else 0
     if wsb:
         ws = _empty((wsb + 3) // 4, device=dev)
@@ -402,7 +447,7 @@ def raw_ok(N, H, W, Cp) -> bool:
     return N * H * W * Cp < 2 ** 31
 
 
-def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split):
+def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, prod=None):
     """bf16-MFMA backward of one conv layer (torch.autocast(bfloat16) arithmetic).  dz after the
     BN+ReLU backward is written once in bf16 (dzt); the input gradient streams it (or, for a concat
     split that is not a multiple of 32, stages dz's frame in the fused kernel) and the weight
@@ -419,8 +464,12 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split):
         dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin else None
         if dma_ok(H, W, dzt.shape[3], Cin, sp):
             wp = pack_weights_dma(conv.weight, dgrad=True)
-            L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
-                   dx0.data_ptr(), L.ptr(dx1), s)
+            if prod is not None:
+                _bnr_call("pmu_conv3x3_dgrad_dma_bnr", prod, L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3]),
+                          (dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin), dx0, s)
+            else:
+                L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
+                       dx0.data_ptr(), L.ptr(dx1), s)
         elif raw_ok(N, H, W, dzt.shape[3]) and (sp == Cin or sp % 32 == 0):
             wp = pack_weights_raw(conv.weight, dgrad=True)
             L.call("pmu_conv3x3_dgrad_raw", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
