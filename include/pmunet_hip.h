@@ -427,6 +427,28 @@ int pmu_occupancy_conv3x3_raw(int* blocks_per_cu);
 int pmu_occupancy_wgrad3x3_bf16(int* blocks_per_cu);
 int pmu_occupancy_conv3x3_pipe(int* blocks_per_cu);
 
+/* ---- batched weight packing ------------------------------------------------------------------
+ * One launch re-packs the weights of many layers into one layout after an optimizer step
+ * (pmu_hip.optim.FusedSGD -> pmu_hip.engine.repack): jobs[] in DEVICE memory, job j = one tensor w
+ * [Cout][Cin][3][3] (ConvTranspose2d: [Cin][Cout][2][2]) packed into dst as the single-tensor pack
+ * function of that layout would, using workgroups [block0, block0 + nblocks) of a grid of `blocks`
+ * (nblocks from the matching *_blocks query).  dgrad is uniform over the jobs of one call. */
+typedef struct {
+  const float* w;
+  void* dst;
+  int Cout, Cin, block0, nblocks;
+} pmu_pack_job;
+int pmu_conv3x3_pack_wino2h_blocks(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_wino2h_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream);
+int pmu_conv3x3_pack_wino4_blocks(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_wino4_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream);
+int pmu_convT2x2_pack_blocks(int Cin, int Cout, int dgrad);
+int pmu_convT2x2_pack_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream);
+int pmu_conv3x3_pack_dma_blocks(int Cout, int Cin, int dgrad);
+int pmu_conv3x3_pack_dma_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream);
+int pmu_convT2x2_pack_dma_blocks(int Cin, int Cout, int dgrad);
+int pmu_convT2x2_pack_dma_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream);
+
 /* ---- build identity and the bounds-checked debug build ------------------------------------ */
 /* Bit 0: experiments build (make EXPERIMENTS=1: kernel-variant A/B switches honoured); bit 1:
  * bounds-checked debug build (make DEBUG=1 -> libpmunet_hip_debug.so, PMU_DCHECK in the kernels). */

@@ -69,12 +69,12 @@ __device__ __forceinline__ unsigned short bf16_bits(float v) { return __builtin_
 
 // wp[jb][ch][tap][u][e]: unit u = swz(co, q) holds B[tap][k = 16 ch + 8 q + e][j = BN jb + co], zero
 // padded, bf16 RNE.  Forward: B[tap][ci][co] = w[co][ci][tap]; dgrad: B[tap][co][ci] = w[co][ci][8 - tap].
-__global__ __launch_bounds__(256) void pack_dma_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, int BN,
-                                                       unsigned short* __restrict__ wp) {
+__device__ __forceinline__ void pack_dma_body(const float* __restrict__ w, int Cout, int Cin, int dgrad, int BN,
+                                              unsigned short* __restrict__ wp, int bid, int nblk) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
   const int nch = (KC + BK - 1) / BK, njb = (NOUT + BN - 1) / BN;
   const long long total = (long long)njb * nch * 9 * 2 * BN * 8;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+  for (long long e = (long long)bid * blockDim.x + threadIdx.x; e < total; e += (long long)nblk * blockDim.x) {
     const int el = (int)(e & 7);
     long long r = e >> 3;
     const int u = (int)(r % (2 * BN)); r /= 2 * BN;
@@ -88,6 +88,19 @@ __global__ __launch_bounds__(256) void pack_dma_kernel(const float* __restrict__
       v = dgrad ? w[((long long)k * Cin + j) * 9 + (8 - tap)] : w[((long long)j * Cin + k) * 9 + tap];
     wp[e] = bf16_bits(v);
   }
+}
+__global__ __launch_bounds__(256) void pack_dma_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, int BN,
+                                                       unsigned short* __restrict__ wp) {
+  pack_dma_body(w, Cout, Cin, dgrad, BN, wp, blockIdx.x, gridDim.x);
+}
+// workgroup channel width of a conv (see dma_shape): 64 for <= 64 outputs or a <= 128-channel reduction
+__host__ __device__ __forceinline__ int dma_bn(int NOUT, int KC) {
+  return (NOUT <= 64 || (KC + BK - 1) / BK * BK <= 128) ? 64 : 128;
+}
+__global__ __launch_bounds__(256) void pack_dma_multi_kernel(const pmu_pack_job* __restrict__ jobs, int njobs, int dgrad) {
+  const pmu_pack_job& j = jobs[pmu_job_of(jobs, njobs, blockIdx.x)];
+  const int NOUT = dgrad ? j.Cin : j.Cout, KC = dgrad ? j.Cout : j.Cin;
+  pack_dma_body(j.w, j.Cout, j.Cin, dgrad, dma_bn(NOUT, KC), (unsigned short*)j.dst, blockIdx.x - j.block0, j.nblocks);
 }
 
 template <bool DGRAD, int WN, int NWV>
@@ -276,7 +289,7 @@ struct Shape {
   int wn, nwv, th;
 };
 static Shape dma_shape(int NOUT, int KC) {
-  if (NOUT <= 64 || KC <= 128) return {1, 4, 16};
+  if (dma_bn(NOUT, KC) == 64) return {1, 4, 16};
   return {2, 8, 16};
 }
 
@@ -330,7 +343,7 @@ extern "C" int pmu_conv3x3_tiles_dma(int N, int H, int W, int Cout, int Cp) {
 
 extern "C" size_t pmu_conv3x3_packed_size_dma(int Cout, int Cin, int dgrad) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
-  const int BN = 64 * dma_shape(NOUT, (KC + BK - 1) / BK * BK).wn;
+  const int BN = dma_bn(NOUT, KC);
   return (size_t)pmu_cdiv(NOUT, BN) * pmu_cdiv(KC, BK) * 9 * 2 * BN * 8 * sizeof(unsigned short);
 }
 
@@ -341,7 +354,7 @@ extern "C" int pmu_conv3x3_pack_dma(const float* w, int Cout, int Cin, int dgrad
   long long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(pack_dma_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad,
-                     64 * dma_shape(NOUT, (KC + BK - 1) / BK * BK).wn, wp);
+                     dma_bn(NOUT, KC), wp);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -362,4 +375,19 @@ extern "C" int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int 
                                          const float* invstd, float* part, void* stream) {
   PMU_REQUIRE(z && coef && mean && invstd && part);
   return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream, z, coef, mean, invstd);
+}
+
+static int pack_dma_grid(int Cout, int Cin, int dgrad) {
+  const long long total = (long long)(pmu_conv3x3_packed_size_dma(Cout, Cin, dgrad) / sizeof(unsigned short));
+  const long long g = (total + 255) / 256;
+  return (int)(g > 4096 ? 4096 : g);
+}
+
+extern "C" int pmu_conv3x3_pack_dma_blocks(int Cout, int Cin, int dgrad) { return pack_dma_grid(Cout, Cin, dgrad); }
+
+extern "C" int pmu_conv3x3_pack_dma_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream) {
+  PMU_REQUIRE(jobs && njobs > 0 && blocks > 0);
+  hipLaunchKernelGGL(pack_dma_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs, dgrad);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
 }

@@ -94,11 +94,12 @@ __device__ __forceinline__ void wino2_u(const float (&g)[3][3], float (&u)[16]) 
 // channel, co) writes its 16 components (c = 4a + b) as 4 float4 (input-gradient packing: consecutive
 // threads read consecutive filters w[co][ci..])
 template <int CO>
-__global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, float* __restrict__ wp) {
+__device__ __forceinline__ void pack_wino2h_body(const float* __restrict__ w, int Cout, int Cin, int dgrad,
+                                                 float* __restrict__ wp, int bid, int nblk) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
   const int nch = (KC + BK - 1) / BK, ncob = (NOUT + CO - 1) / CO;
   const long long total = (long long)ncob * nch * BK * CO;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+  for (long long e = (long long)bid * blockDim.x + threadIdx.x; e < total; e += (long long)nblk * blockDim.x) {
     const int col = (int)(e % CO);
     long long r = e / CO;
     const int kl = (int)(r % BK); r /= BK;
@@ -121,17 +122,21 @@ __global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Ci
     *reinterpret_cast<float4*>(dst + 16) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
+template <int CO>
+__global__ void pack_wino2h_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, float* __restrict__ wp) {
+  pack_wino2h_body<CO>(w, Cout, Cin, dgrad, wp, blockIdx.x, gridDim.x);
+}
 
 // Forward packing, one workgroup per (co block, chunk): the 8 x CO filters w[co][ci0..ci0+7] are read
 // along ci (8 lanes cover 288 contiguous bytes), transformed into LDS in the packed order, and the
 // workgroup's contiguous BK x CO x NCP segment is stored with consecutive float4s.
 template <int CO>
-__global__ __launch_bounds__(256) void pack_wino2h_fwd_kernel(const float* __restrict__ w, int Cout, int Cin,
-                                                              float* __restrict__ wp) {
+__device__ __forceinline__ void pack_wino2h_fwd_body(const float* __restrict__ w, int Cout, int Cin,
+                                                     float* __restrict__ wp, int bid) {
   constexpr int SEG = BK * CO * NCP;
   __shared__ float4 seg4[SEG / 4];
   const int nch = (Cin + BK - 1) / BK;
-  const int ch = blockIdx.x % nch, jb = blockIdx.x / nch;
+  const int ch = bid % nch, jb = bid / nch;
   for (int f = threadIdx.x; f < BK * CO; f += blockDim.x) {
     const int kl = f % BK, col = f / BK;
     const int j = jb * CO + col, k = ch * BK + kl;
@@ -145,8 +150,20 @@ __global__ __launch_bounds__(256) void pack_wino2h_fwd_kernel(const float* __res
     d[4] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
-  float4* dst = reinterpret_cast<float4*>(wp + (long long)blockIdx.x * SEG);
+  float4* dst = reinterpret_cast<float4*>(wp + (long long)bid * SEG);
   for (int i = threadIdx.x; i < SEG / 4; i += blockDim.x) dst[i] = seg4[i];
+}
+template <int CO>
+__global__ __launch_bounds__(256) void pack_wino2h_fwd_kernel(const float* __restrict__ w, int Cout, int Cin,
+                                                              float* __restrict__ wp) {
+  pack_wino2h_fwd_body<CO>(w, Cout, Cin, wp, blockIdx.x);
+}
+__global__ __launch_bounds__(256) void pack_wino2h_multi_kernel(const pmu_pack_job* __restrict__ jobs, int njobs,
+                                                                int dgrad) {
+  const pmu_pack_job& j = jobs[pmu_job_of(jobs, njobs, blockIdx.x)];
+  const int bid = blockIdx.x - j.block0;
+  if (dgrad) pack_wino2h_body<64>(j.w, j.Cout, j.Cin, 1, (float*)j.dst, bid, j.nblocks);
+  else pack_wino2h_fwd_body<64>(j.w, j.Cout, j.Cin, (float*)j.dst, bid);
 }
 
 template <int OFF>
@@ -582,4 +599,20 @@ extern "C" int pmu_conv3x3_dgrad_wino2h_bnr(const float* dzt, int Cout, int N, i
   PMU_REQUIRE(z && coef && mean && invstd && part);
   return launch_wino2h(dzt, Cout, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream, z, coef, mean,
                        invstd);
+}
+
+static int pack_wino2h_grid(int Cout, int Cin, int dgrad) {
+  if (!dgrad) return pmu_cdiv(Cout, w2h_co()) * pmu_cdiv(Cin, BK);
+  const long long total = (long long)pmu_conv3x3_packed_size_wino2h(Cout, Cin, dgrad) / sizeof(float) / NCP;
+  return (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+}
+
+extern "C" int pmu_conv3x3_pack_wino2h_blocks(int Cout, int Cin, int dgrad) { return pack_wino2h_grid(Cout, Cin, dgrad); }
+
+extern "C" int pmu_conv3x3_pack_wino2h_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream) {
+  PMU_REQUIRE(jobs && njobs > 0 && blocks > 0 && w2h_co() == 64);
+  hipLaunchKernelGGL(pack_wino2h_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs,
+                     dgrad);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
 }

@@ -90,13 +90,13 @@ __device__ __forceinline__ void g6(const double (&g)[3], double (&t)[6]) {
 // order and the contiguous BK x CO x 36 segment is stored with consecutive float4s. Consecutive
 // threads read consecutive filters: along the output channel for the input gradient (w[k][j..]),
 // along the reduction channel for the forward (w[j][k..]).
-__global__ __launch_bounds__(256) void pack_wino4_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
-                                                         float* __restrict__ wp) {
+__device__ __forceinline__ void pack_wino4_body(const float* __restrict__ w, int Cout, int Cin, int dgrad,
+                                                float* __restrict__ wp, int bid) {
   constexpr int SEG = BK * CO * NC;
   __shared__ float4 seg4[SEG / 4];
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
   const int nch = (KC + BK - 1) / BK;
-  const int ch = blockIdx.x % nch, jb = blockIdx.x / nch;
+  const int ch = bid % nch, jb = bid / nch;
   for (int f = threadIdx.x; f < BK * CO; f += blockDim.x) {
     const int col = dgrad ? f % CO : f / BK, kl = dgrad ? f / CO : f % BK;
     const int j = jb * CO + col, k = ch * BK + kl;
@@ -128,8 +128,17 @@ __global__ __launch_bounds__(256) void pack_wino4_kernel(const float* __restrict
     for (int q = 0; q < 9; ++q) d[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
   }
   __syncthreads();
-  float4* dst = reinterpret_cast<float4*>(wp + (long long)blockIdx.x * SEG);
+  float4* dst = reinterpret_cast<float4*>(wp + (long long)bid * SEG);
   for (int i = threadIdx.x; i < SEG / 4; i += blockDim.x) dst[i] = seg4[i];
+}
+__global__ __launch_bounds__(256) void pack_wino4_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad,
+                                                         float* __restrict__ wp) {
+  pack_wino4_body(w, Cout, Cin, dgrad, wp, blockIdx.x);
+}
+__global__ __launch_bounds__(256) void pack_wino4_multi_kernel(const pmu_pack_job* __restrict__ jobs, int njobs,
+                                                               int dgrad) {
+  const pmu_pack_job& j = jobs[pmu_job_of(jobs, njobs, blockIdx.x)];
+  pack_wino4_body(j.w, j.Cout, j.Cin, dgrad, (float*)j.dst, blockIdx.x - j.block0);
 }
 
 // B^T row on d0..d5, B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
@@ -706,4 +715,17 @@ extern "C" int pmu_conv3x3_dgrad_wino4_bnr(const float* dzt, int Cout, int N, in
   PMU_REQUIRE(z && coef && mean && invstd && part);
   return launch_wino4(dzt, Cout, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream, z, coef, mean,
                       invstd);
+}
+
+extern "C" int pmu_conv3x3_pack_wino4_blocks(int Cout, int Cin, int dgrad) {
+  const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
+  return pmu_cdiv(NOUT, CO) * pmu_cdiv(KC, BK);
+}
+
+extern "C" int pmu_conv3x3_pack_wino4_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream) {
+  PMU_REQUIRE(jobs && njobs > 0 && blocks > 0);
+  hipLaunchKernelGGL(pack_wino4_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs,
+                     dgrad);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
 }

@@ -698,8 +698,8 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
 }
 
 // packed B operands (see above); e over Cin*Cout*4
-__global__ void convT_pack_kernel(const float* __restrict__ w, int Cin, int Cout, int dgrad, float* __restrict__ wp) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void convT_pack_one(const float* __restrict__ w, int Cin, int Cout, int dgrad,
+                                               float* __restrict__ wp, long long e) {
   const long long E = 4LL * Cin * Cout;
   if (e >= E) return;
   // read-coalesced: e = (ci*Cout + co)*4 + ab
@@ -709,6 +709,14 @@ __global__ void convT_pack_kernel(const float* __restrict__ w, int Cin, int Cout
   const float v = w[e];
   if (dgrad) wp[(long long)ci * 4 * Cout + ab * Cout + co] = v;
   else wp[((long long)ab * Cout + co) * Cin + ci] = v;
+}
+__global__ void convT_pack_kernel(const float* __restrict__ w, int Cin, int Cout, int dgrad, float* __restrict__ wp) {
+  convT_pack_one(w, Cin, Cout, dgrad, wp, (long long)blockIdx.x * blockDim.x + threadIdx.x);
+}
+// job: Cout = the ConvTranspose2d's Cin, Cin = its Cout (w [Cin][Cout][2][2])
+__global__ void convT_pack_multi_kernel(const pmu_pack_job* __restrict__ jobs, int njobs, int dgrad) {
+  const pmu_pack_job& j = jobs[pmu_job_of(jobs, njobs, blockIdx.x)];
+  convT_pack_one(j.w, j.Cout, j.Cin, dgrad, (float*)j.dst, (long long)(blockIdx.x - j.block0) * blockDim.x + threadIdx.x);
 }
 
 static bool pipe_ok_fwd(const pmu_frame* in, int Cout) {
@@ -865,5 +873,19 @@ extern "C" int pmu_convT2x2_wgrad(const float* du, int Hd, int Wd, int off_h, in
                        (const float*)a.bws, a.nsplit, Cout, dbias);
     PMU_CHECK_LAUNCH();
   }
+  return PMU_OK;
+}
+
+extern "C" int pmu_convT2x2_pack_blocks(int Cin, int Cout, int dgrad) {
+  (void)dgrad;
+  return pmu_cdiv(4LL * Cin * Cout, 256);
+}
+
+// jobs[]: .Cout = the ConvTranspose2d's in_channels, .Cin = its out_channels (w [Cin][Cout][2][2])
+extern "C" int pmu_convT2x2_pack_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream) {
+  PMU_REQUIRE(jobs && njobs > 0 && blocks > 0);
+  hipLaunchKernelGGL(convT_pack_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, jobs, njobs,
+                     dgrad);
+  PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -46,12 +46,12 @@ struct TG {
   static_assert(NSTAGE * STAGE <= 160 * 1024, "LDS");
 };
 
-__global__ __launch_bounds__(256) void convT_pack_dma_kernel(const float* __restrict__ w, int Cin, int Cout, int dgrad,
-                                                             int BN, unsigned short* __restrict__ wp) {
+__device__ __forceinline__ void convT_pack_dma_body(const float* __restrict__ w, int Cin, int Cout, int dgrad, int BN,
+                                                    unsigned short* __restrict__ wp, int bid, int nblk) {
   const int Ncols = dgrad ? Cin : 4 * Cout, K = dgrad ? 4 * Cout : Cin;
   const int nkc = K / BK;
   const long long total = (long long)Ncols * K;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+  for (long long e = (long long)bid * blockDim.x + threadIdx.x; e < total; e += (long long)nblk * blockDim.x) {
     const int el = (int)(e & 7);
     long long r = e >> 3;
     const int p = (int)(r % (BN * 4));
@@ -64,6 +64,19 @@ __global__ __launch_bounds__(256) void convT_pack_dma_kernel(const float* __rest
     else { ci = k; ab = n / Cout; co = n - ab * Cout; }
     wp[e] = __builtin_bit_cast(unsigned short, (__bf16)w[((long long)ci * Cout + co) * 4 + ab]);
   }
+}
+__host__ __device__ __forceinline__ int convT_dma_bn(int Ncols) { return Ncols % 256 == 0 ? 256 : 128; }
+__global__ __launch_bounds__(256) void convT_pack_dma_kernel(const float* __restrict__ w, int Cin, int Cout, int dgrad,
+                                                             int BN, unsigned short* __restrict__ wp) {
+  convT_pack_dma_body(w, Cin, Cout, dgrad, BN, wp, blockIdx.x, gridDim.x);
+}
+// job: .Cout = the ConvTranspose2d's in_channels, .Cin = its out_channels (as pmu_convT2x2_pack_multi)
+__global__ __launch_bounds__(256) void convT_pack_dma_multi_kernel(const pmu_pack_job* __restrict__ jobs, int njobs,
+                                                                   int dgrad) {
+  const pmu_pack_job& j = jobs[pmu_job_of(jobs, njobs, blockIdx.x)];
+  const int cin = j.Cout, cout = j.Cin;
+  convT_pack_dma_body(j.w, cin, cout, dgrad, convT_dma_bn(dgrad ? cin : 4 * cout), (unsigned short*)j.dst,
+                      blockIdx.x - j.block0, j.nblocks);
 }
 
 template <bool DGRAD, int WN>
@@ -205,7 +218,7 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
   }
 }
 
-static int dma_wn(int Ncols) { return Ncols % 256 == 0 ? 4 : 2; }
+static int dma_wn(int Ncols) { return convT_dma_bn(Ncols) / 64; }
 
 template <bool DGRAD>
 static int launch(GArgs& g, void* stream) {
@@ -265,4 +278,23 @@ extern "C" int pmu_convT2x2_dgrad_dma(const unsigned short* dut, int Cop, int Hd
   g.M = N * H * W; g.Ncols = Cin; g.K = 4 * Cout; g.lda = Cop;
   g.H = H; g.W = W; g.Cout = Cout; g.Hd = Hd; g.Wd = Wd; g.oh = off_h; g.ow = off_w;
   return launch<true>(g, stream);
+}
+
+static int convT_pack_dma_grid(int Cin, int Cout) {
+  const long long g = (4LL * Cin * Cout + 255) / 256;
+  return (int)(g > 4096 ? 4096 : g);
+}
+
+extern "C" int pmu_convT2x2_pack_dma_blocks(int Cin, int Cout, int dgrad) {
+  (void)dgrad;
+  return convT_pack_dma_grid(Cin, Cout);
+}
+
+// jobs[]: .Cout = the ConvTranspose2d's in_channels, .Cin = its out_channels
+extern "C" int pmu_convT2x2_pack_dma_multi(const pmu_pack_job* jobs, int njobs, int blocks, int dgrad, void* stream) {
+  PMU_REQUIRE(jobs && njobs > 0 && blocks > 0);
+  hipLaunchKernelGGL(convT_pack_dma_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, jobs,
+                     njobs, dgrad);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
 }

@@ -46,6 +46,14 @@ static inline int pmu_image_chunks(int N, long long bytes_per_image, F&& f) {
   return 0;
 }
 
+// Batched weight packing (pmu_*_pack_*_multi): one launch packs many tensors of one layout; job j owns
+// workgroups [block0, block0 + nblocks) of the grid.
+__device__ __forceinline__ int pmu_job_of(const pmu_pack_job* jobs, int njobs, int bid) {
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].block0 <= bid) ++j;
+  return j;
+}
+
 // XCD-aware logical block order: the hardware deals consecutive workgroups round-robin over the 8
 // XCDs (each with its own L2); the logical id gives every XCD a contiguous range of the nb blocks,
 // so a kernel that walks its column blocks fastest re-reads a row block's operand from its own L2.

@@ -33,6 +33,11 @@ class PmuFrame(ctypes.Structure):
     _fields_ = [("src", PmuSrc * 2), ("nsrc", c_int), ("N", c_int), ("H", c_int), ("W", c_int)]
 
 
+class PmuPackJob(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("dst", c_void_p), ("Cout", c_int), ("Cin", c_int), ("block0", c_int),
+                ("nblocks", c_int)]
+
+
 class PmuSgdChunk(ctypes.Structure):
     _fields_ = [("tensor", c_int), ("len", c_int), ("start", c_longlong)]
 
@@ -183,6 +188,16 @@ SIGNATURES = {
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_dma_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_pack_wino2h_blocks": (c_int, [c_int, c_int, c_int]),
+    "pmu_conv3x3_pack_wino2h_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "pmu_conv3x3_pack_wino4_blocks": (c_int, [c_int, c_int, c_int]),
+    "pmu_conv3x3_pack_wino4_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "pmu_convT2x2_pack_blocks": (c_int, [c_int, c_int, c_int]),
+    "pmu_convT2x2_pack_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "pmu_conv3x3_pack_dma_blocks": (c_int, [c_int, c_int, c_int]),
+    "pmu_conv3x3_pack_dma_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "pmu_convT2x2_pack_dma_blocks": (c_int, [c_int, c_int, c_int]),
+    "pmu_convT2x2_pack_dma_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "pmu_build_flags": (c_int, []),
     "pmu_debug_read": (c_int, [POINTER(c_int), POINTER(ctypes.c_char_p)]),
     "pmu_debug_reset": (c_int, []),

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass, field
 
 import torch
@@ -494,7 +495,7 @@ def dma_ok(H, W, Cp, NOUT, split) -> bool:
     return bool(L.lib().pmu_conv3x3_dma_ok(H, W, Cp, NOUT, split))
 
 
-def pack_weights_dma(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+def _pack_weights_dma_now(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     """Weights rounded to bf16 in the LDS-DMA conv's swizzled unit order (pmu_conv3x3_pack_dma)."""
     Cout, Cin = w.shape[0], w.shape[1]
     n = L.lib().pmu_conv3x3_packed_size_dma(Cout, Cin, int(dgrad)) // 2
@@ -530,7 +531,7 @@ def pack_weights_wino(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wp
 
 
-def pack_weights_wino4(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+def _pack_weights_wino4_now(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     """F(4x4,3x3) weights U = G g G^T in the F(4x4) kernel's blocks (pmu_conv3x3_pack_wino4)."""
     Cout, Cin = w.shape[0], w.shape[1]
     n = L.lib().pmu_conv3x3_packed_size_wino4(Cout, Cin, int(dgrad)) // 4
@@ -580,7 +581,7 @@ def wino4_ok(C: int, H: int, W: int, kind: str) -> bool:
     return C % 8 == 0 and H >= 32 and W >= 32 and (mode == "1" or mode == kind) and CFG.fp32_conv == "wino"
 
 
-def pack_weights_wino2h(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+def _pack_weights_wino2h_now(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     """F(2x2,3x3) weights in the 1024-thread kernel's 64-channel blocks (pmu_conv3x3_pack_wino2h)."""
     Cout, Cin = w.shape[0], w.shape[1]
     n = L.lib().pmu_conv3x3_packed_size_wino2h(Cout, Cin, int(dgrad)) // 4
@@ -625,7 +626,7 @@ def pack_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wp
 
 
-def pack_convT_weights_dma(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+def _pack_convT_weights_dma_now(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     """ConvT weights rounded to bf16 in the LDS-DMA GEMMs' swizzled unit order (pmu_convT2x2_pack_dma)."""
     Cin, Cout = w.shape[0], w.shape[1]
     wp = torch.empty(L.lib().pmu_convT2x2_packed_size_dma(Cin, Cout) // 2, dtype=torch.int16, device=w.device)
@@ -641,7 +642,7 @@ def pack_convT_weights_bf16(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     return wp
 
 
-def pack_convT_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+def _pack_convT_weights_now(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
     """ConvT weights [Cin][Cout][2][2] re-laid out k-contiguous for the pipelined GEMMs (pmu_convT2x2_pack)."""
     Cin, Cout = w.shape[0], w.shape[1]
     wp = _empty(L.lib().pmu_convT2x2_packed_size(Cin, Cout) // 4, device=w.device)
@@ -897,3 +898,114 @@ def unet_report_order(net) -> list:
         c1w, b1, c2w, b2 = _dc_layers(dc)
         groups += [conv_group(c2w, b2), conv_group(c1w, b1)]
     return groups
+
+
+# ----------------------------------------------------------------------------------------
+# packed weights: cached across calls, re-packed in one launch per layout by the optimizer
+# ----------------------------------------------------------------------------------------
+# A conv's weights are re-laid out (Winograd U = G g G^T, bf16 tiles, ...) for its kernels.  They only
+# change in the optimizer step, so each pack is kept and reused until its tensor changes: the entry
+# records the parameter's storage, torch's in-place version counter and a pack epoch that
+# pmu_hip.optim.FusedSGD bumps (its kernel writes the parameters through raw pointers, which torch's
+# version counter does not see).  After its update FusedSGD calls repack(), which refreshes every
+# cached pack of the updated parameters in one batched launch per layout (pmu_*_pack_*_multi): the
+# forward and backward then launch no pack kernel.  (Writes through ``param.data`` bypass the version
+# counter: call invalidate_packs() after them.)
+class _Pack:
+    __slots__ = ("w", "ptr", "ver", "epoch", "t")
+
+
+_PACKS: dict = {}
+_TABLES: dict = {}
+# layout -> (single-tensor packer, batched-launch C entries (blocks query, multi launch))
+_LAYOUTS = {
+    "dma": (_pack_weights_dma_now, ("pmu_conv3x3_pack_dma_blocks", "pmu_conv3x3_pack_dma_multi")),
+    "wino4": (_pack_weights_wino4_now, ("pmu_conv3x3_pack_wino4_blocks", "pmu_conv3x3_pack_wino4_multi")),
+    "wino2h": (_pack_weights_wino2h_now, ("pmu_conv3x3_pack_wino2h_blocks", "pmu_conv3x3_pack_wino2h_multi")),
+    "convT_dma": (_pack_convT_weights_dma_now, ("pmu_convT2x2_pack_dma_blocks", "pmu_convT2x2_pack_dma_multi")),
+    "convT": (_pack_convT_weights_now, ("pmu_convT2x2_pack_blocks", "pmu_convT2x2_pack_multi")),
+}
+
+
+def _cached_pack(layout: str, w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    key = (id(w), layout, bool(dgrad))
+    e = _PACKS.get(key)
+    ep = getattr(w, "_pmu_epoch", 0)
+    if e is not None and e.w() is w and e.ptr == w.data_ptr() and e.ver == w._version and e.epoch == ep:
+        return e.t
+    e = _Pack()
+    e.w = weakref.ref(w, lambda _r, k=key: _PACKS.pop(k, None))
+    e.ptr, e.ver, e.epoch = w.data_ptr(), w._version, ep
+    e.t = _LAYOUTS[layout][0](w, dgrad)
+    _PACKS[key] = e
+    return e.t
+
+
+def invalidate_packs() -> None:
+    """Forget every cached pack (after writing parameters through ``.data``)."""
+    _PACKS.clear()
+    _TABLES.clear()
+
+
+def repack(params) -> int:
+    """After an optimizer step that wrote ``params`` in place: bump their pack epoch and refresh all
+    their cached packs, one batched launch per (layout, direction).  Returns the launch count."""
+    ids = set()
+    for p in params:
+        p._pmu_epoch = getattr(p, "_pmu_epoch", 0) + 1
+        ids.add(id(p))
+    groups = {}
+    for key, e in list(_PACKS.items()):
+        w = e.w()
+        if w is None or id(w) not in ids or e.ptr != w.data_ptr() or e.ver != w._version:
+            continue   # not updated here, or changed elsewhere: re-packed on its next use
+        groups.setdefault((key[1], key[2]), []).append((w, e))
+    launches = 0
+    s = L.stream()
+    lb = L.lib()
+    for (layout, dgrad), items in groups.items():
+        blocks_fn, multi = _LAYOUTS[layout][1]
+        sig = tuple((w.data_ptr(), e.t.data_ptr(), w.shape[0], w.shape[1]) for w, e in items)
+        tab = _TABLES.get((layout, dgrad, sig))
+        if tab is None:
+            jobs = (L.PmuPackJob * len(items))()
+            b0 = 0
+            for i, (w, e) in enumerate(items):
+                nb = getattr(lb, blocks_fn)(w.shape[0], w.shape[1], int(dgrad))
+                jobs[i] = L.PmuPackJob(w.data_ptr(), e.t.data_ptr(), w.shape[0], w.shape[1], b0, nb)
+                b0 += nb
+            dev_jobs = torch.frombuffer(bytearray(jobs), dtype=torch.uint8).to(items[0][0].device)
+            tab = (dev_jobs, len(items), b0)
+            if len(_TABLES) > 64:
+                _TABLES.clear()
+            _TABLES[(layout, dgrad, sig)] = tab
+        L.call(multi, tab[0].data_ptr(), tab[1], tab[2], int(dgrad), s)
+        launches += 1
+        for w, e in items:
+            e.epoch = w._pmu_epoch
+    return launches
+
+
+def pack_weights_dma(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """Weights rounded to bf16 in the LDS-DMA conv's swizzled unit order (cached; pmu_conv3x3_pack_dma)."""
+    return _cached_pack("dma", w, dgrad)
+
+
+def pack_weights_wino4(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """F(4x4,3x3) weights U = G g G^T in the F(4x4) kernel's blocks (cached; pmu_conv3x3_pack_wino4)."""
+    return _cached_pack("wino4", w, dgrad)
+
+
+def pack_weights_wino2h(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """F(2x2,3x3) weights in the 1024-thread kernel's 64-channel blocks (cached; pmu_conv3x3_pack_wino2h)."""
+    return _cached_pack("wino2h", w, dgrad)
+
+
+def pack_convT_weights_dma(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """ConvT weights rounded to bf16 in the LDS-DMA GEMMs' unit order (cached; pmu_convT2x2_pack_dma)."""
+    return _cached_pack("convT_dma", w, dgrad)
+
+
+def pack_convT_weights(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
+    """ConvT weights [Cin][Cout][2][2] k-contiguous for the pipelined GEMMs (cached; pmu_convT2x2_pack)."""
+    return _cached_pack("convT", w, dgrad)

@@ -16,6 +16,7 @@ import ctypes
 import torch
 
 from . import _lib as L
+from . import engine
 
 CHUNK = 16384   # elements per block: 16 per thread, 4 float4 loads of p, g and buf in flight
 
@@ -69,4 +70,7 @@ class FusedSGD(torch.optim.Optimizer):
             ptr_t, ck_t, nck, _ = self._table(plist, dev)
             L.call("pmu_sgd_clip", ck_t.data_ptr(), nck, ptr_t.data_ptr(), float(grad_scale), float(group["lr"]),
                    float(group["momentum"]), float(group["clip"]), L.stream())
+            # the kernel wrote the parameters: refresh their packed layouts in one batched launch per
+            # layout, so the next forward / backward launches no pack kernel
+            engine.repack(plist)
         return loss

@@ -72,3 +72,44 @@ def test_pack_wino4(dev, Cout, Cin, dgrad):
     assert ref.numel() == n
     # U is computed in double and rounded once: equal to the fp64 restatement rounded to fp32
     assert float((wp.double().cpu() - ref.float().double()).abs().max()) <= 1e-7 * float(ref.abs().max())
+
+
+def test_packs_cached_and_batch_repacked_after_fused_sgd(dev):
+    """Packed weights are reused until their tensor changes; FusedSGD re-packs every cached layout of
+    the parameters it updated in one batched launch per (layout, direction) — the result equals a
+    fresh single-tensor pack of the new weights bit for bit, and a second forward/backward launches no
+    pack kernel (ragged widths exercise every batched layout's tail blocks)."""
+    from model import UNet
+    from pmu_hip import engine
+    from pmu_hip.optim import FusedSGD
+    torch.manual_seed(0)
+    net = UNet(1, 1, [32, 48, 64]).to(dev).train()
+    opt = FusedSGD(net.parameters(), lr=0.05, momentum=0.9, clip=0.1)
+    x = torch.rand(2, 1, 64, 48, device=dev)
+    t = (torch.rand(2, 1, 64, 48, device=dev) > 0.5).float()
+    calls = []
+    orig = dict(engine._LAYOUTS)
+    try:
+        for k, (fn, multi) in orig.items():
+            engine._LAYOUTS[k] = ((lambda f, kk: (lambda w, d: (calls.append(kk), f(w, d))[1]))(fn, k), multi)
+        for step in range(3):
+            opt.zero_grad()
+            torch.nn.functional.binary_cross_entropy(net(x), t).backward()
+            opt.step()
+            if step == 0:
+                first = len(calls)
+        assert first > 0 and len(calls) == first, (first, len(calls))   # steps 1, 2: all packs from the cache
+    finally:
+        engine._LAYOUTS.update(orig)
+    torch.cuda.synchronize()
+    n = 0
+    for (wid, layout, dgrad), e in list(engine._PACKS.items()):
+        w = e.w()
+        if w is None or not any(w is p for p in net.parameters()):
+            continue
+        assert e.epoch == w._pmu_epoch and e.ver == w._version
+        fresh = orig[layout][0](w, dgrad)
+        torch.cuda.synchronize()
+        assert torch.equal(e.t, fresh), (layout, dgrad, tuple(w.shape))
+        n += 1
+    assert n >= 8
