@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib as L
-from .engine import Src, _dc_layers, _empty, conv_bn_backward, conv_bn_forward, frame_of, pack_convT_weights
+from .engine import Src, _check_channels, _dc_layers, _empty, conv_bn_backward, conv_bn_forward, frame_of, pack_convT_weights
 from .functions import LiveNode, _NO_CPU, grad_sink_for, use_bf16
 
 
@@ -141,6 +141,7 @@ class UpRunner:
         N, hi, wi, Cin = x1h.shape
         hs, ws_ = x2h.shape[1], x2h.shape[2]
         convT = self.module.up
+        _check_channels(Cin, convT)
         Cup = convT.out_channels
         dY, dX = hs - 2 * hi, ws_ - 2 * wi
         if dY < 0 or dX < 0:

@@ -197,9 +197,18 @@ def first_layer_ok(cin: int, cout: int) -> bool:
     return 1 <= cin <= 4 and cout % 4 == 0 and 4 <= cout <= 1024 and 256 % (cout // 4) == 0 and cout <= 256
 
 
+def _check_channels(cin: int, layer) -> None:
+    """The kernels take channel counts from the operand frame and index the weight by them, so an
+    operand whose channel count differs from the layer's is refused here, as torch's conv would."""
+    if cin != layer.in_channels:
+        raise RuntimeError(f"{type(layer).__name__}: operand has {cin} channels, the layer expects "
+                           f"{layer.in_channels} (weight {tuple(layer.weight.shape)})")
+
+
 def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H, W, training, dev,
                     planes=None, bf16=False, keep=False) -> ConvBNOut:
     Cout = conv.out_channels
+    _check_channels(len(planes) if planes is not None else sum(sr.C for sr in srcs), conv)
     s = L.stream()
     lb = L.lib()
     z = _empty(N, H, W, Cout, device=dev)
@@ -739,6 +748,7 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         u = _empty(N, 2 * hi, 2 * wi, Cup, device=dev)
         fin = frame_of([cur.act()], N, hi, wi)
         Cin_t = cur.z.shape[3]
+        _check_channels(Cin_t, convT)
         xtT = None
         if bf16 and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 0):
             # the BN+ReLU operand written once in bf16 (the weight gradient's operand too), both GEMM
@@ -768,6 +778,7 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
     st.feat_src = cur
     if net.apply_last_layer:
         K = net.outc.conv.out_channels
+        _check_channels(cur.z.shape[3], net.outc.conv)
         y = _empty(N, K, H, W, device=dev)
         L.call("pmu_head1x1_fwd", frame_of([cur.act()], N, H, W), net.outc.conv.weight.data_ptr(),
                L.ptr(net.outc.conv.bias), K, int(net.n_classes == 1), y.data_ptr(), L.stream())

@@ -83,7 +83,7 @@ def test_packs_cached_and_batch_repacked_after_fused_sgd(dev):
     from pmu_hip import engine
     from pmu_hip.optim import FusedSGD
     torch.manual_seed(0)
-    net = UNet(1, 1, [32, 48, 64]).to(dev).train()
+    net = UNet(1, 1, [32, 64, 128]).to(dev).train()
     opt = FusedSGD(net.parameters(), lr=0.05, momentum=0.9, clip=0.1)
     x = torch.rand(2, 1, 64, 48, device=dev)
     t = (torch.rand(2, 1, 64, 48, device=dev) > 0.5).float()
@@ -113,3 +113,14 @@ def test_packs_cached_and_batch_repacked_after_fused_sgd(dev):
         assert torch.equal(e.t, fresh), (layout, dgrad, tuple(w.shape))
         n += 1
     assert n >= 8
+
+
+def test_channel_mismatch_refused(dev):
+    """A filter list that does not double per level makes the decoder's concatenation (skip + up)
+    differ from the DoubleConv's in_channels: torch's conv raises there, and so does the engine —
+    before any kernel indexes the weight by the operand's channel count."""
+    from model import UNet
+    net = UNet(1, 1, [32, 48, 64]).to(dev).train()
+    with pytest.raises(RuntimeError, match="channels"):
+        net(torch.rand(2, 1, 64, 48, device=dev))
+    torch.cuda.synchronize()
