@@ -57,6 +57,9 @@ enum {
                          scale*g + kx*(z-mean) + kc                   coef = [scale|shift|mean|kx|kc] */
 };
 enum { PMU_POOL_NONE = 0, PMU_POOL_MAX2 = 1, PMU_POOL_AVG2CEIL = 2 };
+/* Storage type of a source's tensors (pmu_src.dtype bits; 0 = both fp32).  bf16 storage is what
+ * torch.autocast(bfloat16) keeps a conv output in (config c5): the pre-BN z of the bf16 path. */
+enum { PMU_DT_X_BF16 = 1, PMU_DT_Z_BF16 = 2 };
 
 typedef struct pmu_src {
   const float* x;    /* NHWC [N][H][W][C]: raw values, pre-BN z, or upstream gradient */
@@ -65,6 +68,9 @@ typedef struct pmu_src {
   int mode, pool;
   int C, H, W;       /* stored tensor dims                                            */
   int off_h, off_w;  /* top/left offset of the (pooled) source inside the frame (F.pad) */
+  int dtype;         /* PMU_DT_* bits: x / z stored as bf16 (read as fp32 exactly).  Only the
+                        materialising and streaming calls take bf16 sources (pmu_frame_to_bf16,
+                        pmu_frame_to_f32, pmu_head1x1_fwd, pmu_wgrad1x1); the others refuse them */
 } pmu_src;
 
 /* A conv operand: one frame of N x H x W pixels whose channels are the concatenation
@@ -157,6 +163,13 @@ int pmu_conv3x3_dgrad_wino4_bnr(const float* dzt, int Cout, int N, int H, int W,
  * Winograd F(2x2,3x3): dw = G^T [sum over 2x2 tiles of (A dY A^T) .* (B^T X B)] G.  Cout % 32 == 0,
  * Cin % 64 == 0 (pmu_conv3x3_wgrad_ws_wino returns 0 otherwise); ws must hold that many bytes. */
 size_t pmu_conv3x3_wgrad_ws_wino(int N, int H, int W, int Cin, int Cout);
+/* The same weight gradient by Winograd F(4x4,3x3): 36 products per 4x4 tile and channel pair (2.25
+ * per output pixel vs F(2x2)'s 4), output transform in fp64; fp32 rounding ~1.3e-6 of rms |dw|
+ * (tools/wgrad_err.py).  Cout % 32 == 0, Cin % 64 == 0 (pmu_conv3x3_wgrad_ws_wino4 returns 0
+ * otherwise); ws must hold that many bytes. */
+size_t pmu_conv3x3_wgrad_ws_wino4(int N, int H, int W, int Cin, int Cout);
+int pmu_conv3x3_wgrad_wino4(const float* dzt, const float* xt, int N, int H, int W, int Cout, int Cin,
+                            float* dw, float* ws, size_t ws_bytes, void* stream);
 int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, int H, int W, int Cout, int Cin,
                            float* dw, float* ws, size_t ws_bytes, void* stream);
 
@@ -204,6 +217,19 @@ int pmu_conv3x3_dgrad_dma(const unsigned short* dzt, int Cp, int N, int H, int W
 int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                               int Cin, float* dx, const float* z, const float* coef, const float* mean,
                               const float* invstd, float* part, void* stream);
+/* bf16 storage of z (config c5: torch.autocast keeps a conv's output in bf16, unet_parts.py:15,18 under
+ * autocast), centred: the forward stores bf16(z - zoff[c]) (RNE; zoff = the BN running mean, null: 0)
+ * with the BN partial sums of stored + zoff; every consumer then applies the centred coefficients of
+ * pmu_bn_center.  The input gradient's BN-backward partials read such a z. */
+int pmu_conv3x3_fwd_dma_zb(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
+                           const float* bias, int Cout, unsigned short* z, const float* zoff, float* part,
+                           void* stream);
+/* coef_out = [scale | shift + off*scale], mean_out = mean - off (in place allowed; mean may be NULL) */
+int pmu_bn_center(const float* coef, const float* mean, const float* off, int C, float* coef_out,
+                  float* mean_out, void* stream);
+int pmu_conv3x3_dgrad_dma_bnr_zb(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                 int Cin, float* dx, const unsigned short* z, const float* coef, const float* mean,
+                                 const float* invstd, float* part, void* stream);
 /* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels
  * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz
  * that pmu_conv3x3_wgrad_bf16 multiplies. */
@@ -269,6 +295,9 @@ int pmu_bn_eval_coef(const float* running_mean, const float* running_var, const 
 /* BN+ReLU backward reduction over da (NHWC) and z: part[tile][2][C] = (sum g, sum g*xhat). */
 int pmu_bn_bwd_reduce(const float* da, const float* z, const float* coef, const float* mean,
                       const float* invstd, int P, int C, float* part, void* stream);
+/* the same over a bf16-stored z (C % 4 == 0) */
+int pmu_bn_bwd_reduce_zb(const float* da, const unsigned short* z, const float* coef, const float* mean,
+                         const float* invstd, int P, int C, float* part, void* stream);
 int pmu_bn_bwd_tiles(int P, int C);
 /* From acc[G][2][C]: dgamma, dbeta, dbias(conv bias feeding BN) and the BNBWD coef block
  * [scale|shift|mean|kx|kc]. */
@@ -285,6 +314,9 @@ int pmu_bnrelu_apply(const float* z, const float* coef, long long P, int C, floa
  * accumulate=0 overwrites dx (zeros outside windows). */
 int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int N, int H, int W,
                      int C, float* dx, int accumulate, void* stream);
+/* the same over a bf16-stored z (coef required, C % 4 == 0) */
+int pmu_maxpool2_bwd_zb(const float* dpool, const unsigned short* z, const float* coef, int N, int H, int W,
+                        int C, float* dx, int accumulate, void* stream);
 /* AvgPool2d(2,2,ceil_mode=True) backward: dx = dpool/count(window), overwrite. */
 int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream);
 

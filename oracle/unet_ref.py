@@ -30,6 +30,23 @@ def _rb(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
 
+# torch.autocast(bfloat16) returns a conv's output in bf16.  BF16_Z models the HIP path's storage of
+# it (include/pmunet_hip.h pmu_conv3x3_fwd_dma_zb, engine CFG.bf16_z): the convs that run on the
+# LDS-DMA kernel (maps >= 32 wide, padded Cin % 16 == 0, Cout % 8 == 0) keep z as bf16(z - rm) + rm,
+# rm the BN running mean before the step's update (straight-through gradient).  False: fp32 z.
+BF16_Z = False
+
+
+def _dma_zb(x, cin, cout):
+    return BF16_Z and x.shape[3] >= 32 and ((cin + 7) // 8 * 8) % 16 == 0 and cout % 8 == 0
+
+
+def _round_centered(y, off):
+    """bf16(y - off) + off per channel, gradient passed straight through (autocast's cast)."""
+    o = off.to(y.dtype).view(1, -1, 1, 1)
+    return y + (_rb(y - o) + o - y).detach()
+
+
 class Bf16Conv3x3(torch.autograd.Function):
     """conv3x3(pad 1) with torch.autocast(bfloat16) arithmetic as the HIP bf16 kernels implement it
     (include/pmunet_hip.h, bf16 section): the operand x and the weights are rounded to bf16, the
@@ -85,7 +102,11 @@ def double_conv(x, sd, pre, training, bf16=False, first_fp32=False):
     HIP path's Cin <= 4 first-layer kernel)."""
     for i in (0, 3):
         use = bf16 and not (first_fp32 and i == 0)
-        x = _conv3x3(x, sd[f"{pre}double_conv.{i}.weight"], sd[f"{pre}double_conv.{i}.bias"], use)
+        w = sd[f"{pre}double_conv.{i}.weight"]
+        zb = use and _dma_zb(x, w.shape[1], w.shape[0])
+        x = _conv3x3(x, w, sd[f"{pre}double_conv.{i}.bias"], use)
+        if zb:
+            x = _round_centered(x, sd[f"{pre}double_conv.{i + 1}.running_mean"].clone())
         x = F.relu(_bn(x, sd, f"{pre}double_conv.{i + 1}.", training))
     return x
 

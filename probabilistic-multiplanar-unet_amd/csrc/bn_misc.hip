@@ -93,7 +93,8 @@ __global__ void bn_eval_coef_kernel(const float* rm, const float* rv, const floa
 // ---------------- BN + ReLU backward reduction ----------------
 // part[tile][2][C] = (sum g, sum g*xhat), g = da * (z*scale+shift > 0), xhat = (z-mean)*invstd
 constexpr int BNR_BYTES = 65536;  // bytes of one tensor per block
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ da, const float* __restrict__ z,
+template <class ZT>  // z stored as float or bf16 (unsigned short)
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ da, const ZT* __restrict__ z,
                                                             const float* __restrict__ coef, const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long long P, int C,
                                                             int ppb, float* __restrict__ part) {
@@ -118,12 +119,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
       const long long pend = min(P, p0 + ppb);
       const int nit = pend > p0 + pg ? (int)((pend - p0 - pg + npg - 1) / npg) : 0;
       const float* dp = da + (p0 + pg) * C + c;
-      const float* zp = z + (p0 + pg) * C + c;
+      const ZT* zp = z + (p0 + pg) * C + c;
       const long long step = (long long)npg * C;
 #pragma unroll 4
       for (int it = 0; it < nit; ++it) {
         const float4 d = *reinterpret_cast<const float4*>(dp + it * step);
-        const float4 zz = *reinterpret_cast<const float4*>(zp + it * step);
+        const float4 zz = pmu_ld4(zp + it * step);
         const float dv[4] = {d.x, d.y, d.z, d.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
         const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
         const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
@@ -238,8 +239,8 @@ __global__ __launch_bounds__(256) void maxpool2_bwd1_kernel(const float* __restr
 
 // ---------------- pooling backward ----------------
 // grid-stride over dx elements in channel quads
-template <bool RAW>
-__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restrict__ dpool, const float* __restrict__ z,
+template <bool RAW, class ZT>  // z stored as float or bf16 (unsigned short)
+__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restrict__ dpool, const ZT* __restrict__ z,
                                                            const float* __restrict__ coef, int N, int H, int W, int C,
                                                            float* __restrict__ dx, int accumulate) {
   const int CQ = C >> 2;
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restri
       float best[4];
       int arg[4] = {0, 0, 0, 0};
       {
-        const float4 v = *reinterpret_cast<const float4*>(z + b);
+        const float4 v = pmu_ld4(z + b);
         if (RAW) {
           best[0] = v.x; best[1] = v.y; best[2] = v.z; best[3] = v.w;
         } else {
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restri
       }
 #pragma unroll
       for (int k = 1; k < 4; ++k) {
-        const float4 v = *reinterpret_cast<const float4*>(z + b + off[k]);
+        const float4 v = pmu_ld4(z + b + off[k]);
         const float a0 = RAW ? v.x : fmaxf(0.f, fmaf(v.x, sc.x, sh.x)), a1 = RAW ? v.y : fmaxf(0.f, fmaf(v.y, sc.y, sh.y));
         const float a2 = RAW ? v.z : fmaxf(0.f, fmaf(v.z, sc.z, sh.z)), a3 = RAW ? v.w : fmaxf(0.f, fmaf(v.w, sc.w, sh.w));
         if (a0 > best[0]) { best[0] = a0; arg[0] = k; }
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const fl
   }
   const unsigned pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
   for (unsigned p = blockIdx.x * HPPB + pg; p < pend; p += PG) {  // 32-bit decode (P < 2^31)
-    const float4 a = pmu_bnrelu4(*reinterpret_cast<const float4*>(f.s0.x + (size_t)p * C + 4 * cq), sc, sh);
+    const float4 a = pmu_bnrelu4(src_x4(f.s0, (long long)p * C + 4 * cq), sc, sh);
     const unsigned n = p / HWu, pix = p - n * HWu;
 #pragma unroll
     for (int k = 0; k < HEAD_KMAX; ++k) {
@@ -551,7 +552,7 @@ __global__ __launch_bounds__(256) void wgrad1x1_fast_kernel(const float* __restr
   const unsigned HWu = (unsigned)HW, pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
   for (unsigned p = blockIdx.x * HPPB + pg; p < pend; p += PG) {  // 32-bit decode (P < 2^31)
     const unsigned n = p / HWu, pix = p - n * HWu;
-    const float4 a = pmu_bnrelu4(*reinterpret_cast<const float4*>(f.s0.x + (size_t)p * C + 4 * cq), sc, sh);
+    const float4 a = pmu_bnrelu4(src_x4(f.s0, (long long)p * C + 4 * cq), sc, sh);
 #pragma unroll
     for (int k = 0; k < HEAD_KMAX; ++k) {
       if (k >= K) break;
@@ -812,6 +813,29 @@ extern "C" int pmu_bn_eval_coef(const float* running_mean, const float* running_
   return PMU_OK;
 }
 
+// Centring of a bf16-stored z (pmu_conv3x3_fwd_dma_zb stores z - off): the coefficients every
+// consumer applies to the stored value — scale, shift + off*scale (BN+ReLU: (zs + off)*scale + shift),
+// mean - off (xhat = (zs + off - mean)*invstd).  In place allowed.
+__global__ __launch_bounds__(256) void bn_center_kernel(const float* __restrict__ coef, const float* mean,
+                                                        const float* __restrict__ off, int C, float* coef_out,
+                                                        float* mean_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float sc = coef[c], sh = coef[C + c], o = off[c];
+  coef_out[c] = sc;
+  coef_out[C + c] = fmaf(o, sc, sh);
+  if (mean && mean_out) mean_out[c] = mean[c] - o;
+}
+
+extern "C" int pmu_bn_center(const float* coef, const float* mean, const float* off, int C, float* coef_out,
+                             float* mean_out, void* stream) {
+  PMU_REQUIRE(coef && off && coef_out && C > 0 && (!mean || mean_out));
+  hipLaunchKernelGGL(bn_center_kernel, dim3((unsigned)pmu_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, coef, mean,
+                     off, C, coef_out, mean_out);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
 static int bn_bwd_ppb(int C) {
   int ppb = BNR_BYTES / (C * 4);
   return ppb < 1 ? 1 : ppb;
@@ -829,8 +853,18 @@ extern "C" int pmu_bn_bwd_reduce(const float* da, const float* z, const float* c
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0, (hipStream_t)stream,
                      da, z, coef, mean, invstd, (long long)P, C, ppb, part);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_bn_bwd_reduce_zb(const float* da, const unsigned short* z, const float* coef, const float* mean,
+                                    const float* invstd, int P, int C, float* part, void* stream) {
+  PMU_REQUIRE(da && z && coef && mean && invstd && part && P > 0 && C > 0 && C % 4 == 0);
+  const int ppb = bn_bwd_ppb(C);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel<unsigned short>, dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0,
+                     (hipStream_t)stream, da, z, coef, mean, invstd, (long long)P, C, ppb, part);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -866,11 +900,20 @@ extern "C" int pmu_maxpool2_bwd(const float* dpool, const float* z, const float*
     return PMU_OK;
   }
   if (coef)
-    hipLaunchKernelGGL(maxpool2_bwd_kernel<false>, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0,
-                       (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+    hipLaunchKernelGGL((maxpool2_bwd_kernel<false, float>), dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256),
+                       0, (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
   else
-    hipLaunchKernelGGL(maxpool2_bwd_kernel<true>, dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256), 0,
-                       (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+    hipLaunchKernelGGL((maxpool2_bwd_kernel<true, float>), dim3(grid_for((long long)N * H * W * (C / 4))), dim3(256),
+                       0, (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_maxpool2_bwd_zb(const float* dpool, const unsigned short* z, const float* coef, int N, int H, int W,
+                                   int C, float* dx, int accumulate, void* stream) {
+  PMU_REQUIRE(dpool && z && coef && dx && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
+  hipLaunchKernelGGL((maxpool2_bwd_kernel<false, unsigned short>), dim3(grid_for((long long)N * H * W * (C / 4))),
+                     dim3(256), 0, (hipStream_t)stream, dpool, z, coef, N, H, W, C, dx, accumulate);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -901,7 +944,7 @@ static bool host_head_fast(const pmu_frame* in) {
 
 extern "C" int pmu_head1x1_fwd(const pmu_frame* in, const float* w, const float* b, int K, int do_sigmoid,
                                float* y, void* stream) {
-  PMU_REQUIRE(valid_frame(in) && w && y && K >= 1 && K <= HEAD_KMAX);
+  PMU_REQUIRE(valid_frame(in, true) && w && y && K >= 1 && K <= HEAD_KMAX);
   const DevFrame f = make_dev_frame(in);
   const long long P = (long long)in->N * in->H * in->W;
   if (host_head_fast(in) && P < (1LL << 31)) {
@@ -940,7 +983,7 @@ extern "C" size_t pmu_wgrad1x1_ws(int P, int K, int C) {
 
 extern "C" int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float* dw, float* db, float* ws,
                             size_t ws_bytes, void* stream) {
-  PMU_REQUIRE(dl && valid_frame(act) && dw && ws && K >= 1 && K <= HEAD_KMAX);
+  PMU_REQUIRE(dl && valid_frame(act, true) && dw && ws && K >= 1 && K <= HEAD_KMAX);
   const DevFrame f = make_dev_frame(act);
   PMU_REQUIRE(f.C <= 256);
   const long long P = (long long)act->N * act->H * act->W;

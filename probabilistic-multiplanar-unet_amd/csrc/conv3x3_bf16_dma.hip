@@ -62,6 +62,12 @@ struct DmaArgs {
   const float* bcoef;
   const float* bmean;
   const float* binv;
+  // bf16 z (torch.autocast's conv output dtype), centred: forward — z stored as bf16(z - zoff[c]) (RNE;
+  // zoff = the BN's running mean, so the stored value keeps bf16's relative precision against the
+  // channel's spread, not its mean) and the BN partial sums taken over the stored values + zoff;
+  // input gradient — bz holds such values (its consumer passes the correspondingly shifted coef/mean)
+  int zbf;
+  const float* zoff;
 };
 
 __device__ __forceinline__ int swz(int p, int q) { return 2 * p + (q ^ ((p >> 3) & 1)); }
@@ -223,6 +229,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     const int j = jb + li;
     const bool jok = j < a.NOUT;
     const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
+    const float zo = (!DGRAD && jok && a.zoff) ? a.zoff[j] : 0.f;
     const bool bnr = DGRAD && a.bz && jok;
     const float bsc = bnr ? a.bcoef[j] : 0.f, bsh = bnr ? a.bcoef[a.NOUT + j] : 0.f;
     const float bmu = bnr ? a.bmean[j] : 0.f, bis = bnr ? a.binv[j] : 0.f;
@@ -234,19 +241,37 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
       const int h = h0 + 4 * wm + fm;
+      // the producer's z under this row's 16 outputs, loaded together before the stores (clamped
+      // addresses: every lane loads, no branch per load; unused values are ignored)
+      float zt[16];
+      if (DGRAD && a.bz) {
+        const int jc = min(j, a.NOUT - 1);
+        const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const long long zi = (row + min(w0 + acc_row(r, lane), a.W - 1)) * a.NOUT + jc;
+          zt[r] = a.zbf == 1 ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int w = w0 + acc_row(r, lane);
         if (!jok || h >= a.H || w >= a.W) continue;
         const long long pix = ((long long)n * a.H + h) * a.W + w;
         PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-        const float v = acc[fm][fn][r] + b;
-        dstp[pix * ld] = v;
+        float v = acc[fm][fn][r] + b;
+        if (!DGRAD && a.zbf) {
+          const unsigned short vb = bf16_bits(v - zo);
+          reinterpret_cast<unsigned short*>(a.out0)[pix * ld + j] = vb;
+          v = pmu_bf16_f32(vb) + zo;
+        } else {
+          dstp[pix * ld] = v;
+        }
         if (!DGRAD) {
           s1[fn] += v;
           s2[fn] = fmaf(v, v, s2[fn]);
         } else if (bnr) {
-          const float zz = a.bz[pix * a.NOUT + j];
+          const float zz = zt[r];
           const float gg = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
           s1[fn] += gg;
           s2[fn] = fmaf(gg, (zz - bmu) * bis, s2[fn]);
@@ -296,7 +321,7 @@ static Shape dma_shape(int NOUT, int KC) {
 static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, const unsigned short* wp, const float* bias,
                       int NOUT, float* out0, float* out1, int split, float* part, bool dgrad, void* stream,
                       const float* bz = nullptr, const float* bcoef = nullptr, const float* bmean = nullptr,
-                      const float* binv = nullptr) {
+                      const float* binv = nullptr, int zbf = 0, const float* zoff = nullptr) {
   PMU_REQUIRE(x && wp && out0 && N > 0 && H > 0 && W >= 32 && Cp > 0 && Cp % BK == 0 && NOUT > 0);
   PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && out1));
   const Shape sh = dma_shape(NOUT, Cp);
@@ -305,10 +330,15 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
     const long long tiles = (long long)pmu_cdiv(W, TW) * pmu_cdiv(H, sh.th);
     return pmu_image_chunks(N, img_bytes, [&](int n0, int nn) {
       const long long px = (long long)n0 * H * W;
-      return launch_dma(x + px * Cp, Cp, nn, H, W, wp, bias, NOUT, out0 + px * (dgrad ? split : NOUT),
-                        out1 ? out1 + px * (NOUT - split) : nullptr, split,
-                        part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream,
-                        bz ? bz + px * NOUT : nullptr, bcoef, bmean, binv);
+      // bf16 z (forward output / input-gradient bz): element offsets of 2-byte values
+      float* o0 = (!dgrad && zbf == 1) ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(out0) + px * NOUT)
+                                  : out0 + px * (dgrad ? split : NOUT);
+      const float* bzc = !bz ? nullptr
+                             : zbf == 1 ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(bz) + px * NOUT)
+                                   : bz + px * NOUT;
+      return launch_dma(x + px * Cp, Cp, nn, H, W, wp, bias, NOUT, o0, out1 ? out1 + px * (NOUT - split) : nullptr,
+                        split, part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream, bzc, bcoef,
+                        bmean, binv, zbf, zoff);
     });
   }
   DmaArgs a;
@@ -316,6 +346,8 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   a.N = N; a.H = H; a.W = W; a.Cp = Cp; a.NOUT = NOUT; a.split = dgrad ? split : NOUT;
   a.nch = Cp / BK;
   a.bz = bz; a.bcoef = bcoef; a.bmean = bmean; a.binv = binv;
+  a.zbf = zbf;
+  a.zoff = zoff;
   a.ncb = pmu_cdiv(NOUT, 64 * sh.wn);
   a.tiles_w = pmu_cdiv(W, TW);
   a.tiles_h = pmu_cdiv(H, sh.th);
@@ -375,6 +407,25 @@ extern "C" int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int 
                                          const float* invstd, float* part, void* stream) {
   PMU_REQUIRE(z && coef && mean && invstd && part);
   return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream, z, coef, mean, invstd);
+}
+
+// bf16 storage of z (config c5's autocast dtype), centred on zoff (the BN running mean; null: 0): the
+// forward stores bf16(z - zoff) (RNE) with the BN partial sums of stored + zoff; the input gradient's
+// BN-backward partials read such a z with the centred coefficients (shift + zoff*scale, mean - zoff).
+extern "C" int pmu_conv3x3_fwd_dma_zb(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                      const float* bias, int Cout, unsigned short* z, const float* zoff, float* part,
+                                      void* stream) {
+  return launch_dma(xt, Cp, N, H, W, wp, bias, Cout, reinterpret_cast<float*>(z), nullptr, Cout, part, false, stream,
+                    nullptr, nullptr, nullptr, nullptr, 1, zoff);
+}
+
+extern "C" int pmu_conv3x3_dgrad_dma_bnr_zb(const unsigned short* dzt, int Cp, int N, int H, int W,
+                                            const unsigned short* wp, int Cin, float* dx, const unsigned short* z,
+                                            const float* coef, const float* mean, const float* invstd, float* part,
+                                            void* stream) {
+  PMU_REQUIRE(z && coef && mean && invstd && part);
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream,
+                    reinterpret_cast<const float*>(z), coef, mean, invstd, 1);
 }
 
 static int pack_dma_grid(int Cout, int Cin, int dgrad) {

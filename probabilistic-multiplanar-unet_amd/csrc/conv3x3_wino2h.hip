@@ -303,10 +303,21 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
       const int r = 2 * rho + rr;
-      float P[4];
-      w2_partial<CH>(acc, CH, r, P);
       const int t = 4 * kk + r;
       const int oh = h0 + 2 * (2 * tg + (t >> 3)), ow = w0 + 2 * (t & 7);
+      // the producer's z under this tile's 4 outputs, loaded together ahead of the output transform
+      // (clamped addresses: every lane loads, no branch per load; unused values are ignored)
+      float zt[4];
+      if (DGRAD && a.bz) {
+        const int jc = min(j, a.NOUT - 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const long long pix = ((long long)n * a.H + min(oh + (e >> 1), a.H - 1)) * a.W + min(ow + (e & 1), a.W - 1);
+          zt[e] = a.bz[pix * a.NOUT + jc];
+        }
+      }
+      float P[4];
+      w2_partial<CH>(acc, CH, r, P);
 #pragma unroll
       for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -324,7 +335,7 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
           } else if (j < a.split) {
             a.out0[pix * a.split + j] = v;
             if (a.bz) {
-              const float zz = a.bz[pix * a.NOUT + j];
+              const float zz = zt[2 * p + q];
               const float g = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
               s1 += g;
               s2 = fmaf(g, (zz - bmu) * bis, s2);

@@ -392,10 +392,22 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
       const int r = 2 * rho + rr;
-      float P[16];
-      w4_partial<CH>(acc, CH, r, P);
       const int t = 4 * kk + r;  // tile within the group
       const int oh = h0 + 4 * (2 * tg + (t >> 3)), ow = w0 + 4 * (t & 7);
+      // the producer's z under this tile's 16 outputs, loaded before the output transform so the
+      // loads are in flight together (issued one per store, each waited for on its own)
+      float zt[16];
+      if (DGRAD && a.bz) {
+        const int jc = min(j, a.NOUT - 1);  // clamped: every lane loads (no branch per load), unused ones ignored
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int hh2 = oh + (e >> 2), ww = ow + (e & 3);
+          const long long pix = ((long long)n * a.H + min(hh2, a.H - 1)) * a.W + min(ww, a.W - 1);
+          zt[e] = a.bz[pix * a.NOUT + jc];
+        }
+      }
+      float P[16];
+      w4_partial<CH>(acc, CH, r, P);
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int hh2 = oh + p;
@@ -414,7 +426,7 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
           } else if (j < a.split) {
             a.out0[pix * a.split + j] = v;
             if (a.bz) {
-              const float zz = a.bz[pix * a.NOUT + j];
+              const float zz = zt[4 * p + q];
               const float g = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
               s1 += g;
               s2 = fmaf(g, (zz - bmu) * bis, s2);

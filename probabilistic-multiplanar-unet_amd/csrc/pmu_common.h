@@ -78,11 +78,26 @@ __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (
 // Positions outside the frame or the source read as 0 (conv zero padding is applied
 // in operand space, i.e. after BN+ReLU, as in the reference).
 // ---------------------------------------------------------------------------------
+// bf16 storage (pmu_src.dtype): a stored bf16 is read as the fp32 it denotes (exact); conv outputs
+// kept in bf16 are rounded to nearest-even
+__device__ __forceinline__ float pmu_bf16_f32(unsigned short u) { return __uint_as_float((unsigned)u << 16); }
+__device__ __forceinline__ unsigned short pmu_f32_bf16(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
+__device__ __forceinline__ float pmu_round_bf16(float v) { return pmu_bf16_f32(pmu_f32_bf16(v)); }
+__device__ __forceinline__ float4 pmu_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 pmu_ld4(const unsigned short* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ float pmu_ld1(const float* p) { return *p; }
+__device__ __forceinline__ float pmu_ld1(const unsigned short* p) { return pmu_bf16_f32(*p); }
+
 struct DevSrc {
   const float* x;
   const float* z;
   const float* coef;
   int mode, pool, C, H, W, off_h, off_w;
+  int xbf, zbf;  // x / z stored as bf16
 };
 struct DevFrame {
   DevSrc s0, s1;
@@ -93,12 +108,14 @@ struct DevFrame {
 static inline DevFrame make_dev_frame(const pmu_frame* f) {
   DevFrame d;
   const pmu_src* a = &f->src[0];
-  d.s0 = DevSrc{a->x, a->z, a->coef, a->mode, a->pool, a->C, a->H, a->W, a->off_h, a->off_w};
+  d.s0 = DevSrc{a->x, a->z, a->coef, a->mode, a->pool, a->C, a->H, a->W, a->off_h, a->off_w,
+                a->dtype & PMU_DT_X_BF16, (a->dtype & PMU_DT_Z_BF16) >> 1};
   if (f->nsrc > 1) {
     const pmu_src* b = &f->src[1];
-    d.s1 = DevSrc{b->x, b->z, b->coef, b->mode, b->pool, b->C, b->H, b->W, b->off_h, b->off_w};
+    d.s1 = DevSrc{b->x, b->z, b->coef, b->mode, b->pool, b->C, b->H, b->W, b->off_h, b->off_w,
+                  b->dtype & PMU_DT_X_BF16, (b->dtype & PMU_DT_Z_BF16) >> 1};
   } else {
-    d.s1 = DevSrc{nullptr, nullptr, nullptr, 0, 0, 0, 0, 0, 0, 0};
+    d.s1 = DevSrc{nullptr, nullptr, nullptr, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   }
   d.nsrc = f->nsrc;
   d.N = f->N; d.H = f->H; d.W = f->W;
@@ -113,13 +130,17 @@ static inline bool valid_src(const pmu_src& s, int N) {
   if (s.mode == PMU_SRC_BNRELU && !s.coef) return false;
   if (s.mode == PMU_SRC_BNBWD && (!s.coef || !s.z)) return false;
   if (s.mode < 0 || s.mode > 2 || s.pool < 0 || s.pool > 2) return false;
+  if (s.dtype < 0 || s.dtype > 3) return false;
   (void)N;
   return true;
 }
-static inline bool valid_frame(const pmu_frame* f) {
+// bf16: the frame may hold bf16-stored sources (only the calls whose kernels read sources through
+// src_xform / src_xform4 pass true; the fused-staging kernels read fp32 and refuse them)
+static inline bool valid_frame(const pmu_frame* f, bool bf16 = false) {
   if (!f || f->nsrc < 1 || f->nsrc > 2 || f->N <= 0 || f->H <= 0 || f->W <= 0) return false;
   for (int i = 0; i < f->nsrc; ++i) {
     if (!valid_src(f->src[i], f->N)) return false;
+    if (!bf16 && f->src[i].dtype != 0) return false;
     const pmu_src& s = f->src[i];
     if (s.pool == PMU_POOL_MAX2 && (s.H / 2 + s.off_h > f->H || s.W / 2 + s.off_w > f->W)) return false;
   }
@@ -127,17 +148,24 @@ static inline bool valid_frame(const pmu_frame* f) {
 }
 
 // transform of one stored element (index i into x/z, channel c of the source)
+__device__ __forceinline__ float src_x1(const DevSrc& s, long long i) {
+  return s.xbf ? pmu_ld1(reinterpret_cast<const unsigned short*>(s.x) + i) : s.x[i];
+}
+__device__ __forceinline__ float4 src_x4(const DevSrc& s, long long i) {
+  return s.xbf ? pmu_ld4(reinterpret_cast<const unsigned short*>(s.x) + i) : pmu_ld4(s.x + i);
+}
 __device__ __forceinline__ float src_xform(const DevSrc& s, long long i, int c) {
-  if (s.mode == PMU_SRC_RAW) return s.x[i];
-  if (s.mode == PMU_SRC_BNRELU) return fmaxf(0.f, fmaf(s.x[i], s.coef[c], s.coef[s.C + c]));
+  const float x = src_x1(s, i);
+  if (s.mode == PMU_SRC_RAW) return x;
+  if (s.mode == PMU_SRC_BNRELU) return fmaxf(0.f, fmaf(x, s.coef[c], s.coef[s.C + c]));
   // BNBWD
-  const float z = s.z[i];
+  const float z = s.zbf ? pmu_ld1(reinterpret_cast<const unsigned short*>(s.z) + i) : s.z[i];
   const float sc = s.coef[c];
-  const float g = (fmaf(z, sc, s.coef[s.C + c]) > 0.f) ? s.x[i] : 0.f;
+  const float g = (fmaf(z, sc, s.coef[s.C + c]) > 0.f) ? x : 0.f;
   return fmaf(sc, g, fmaf(s.coef[3 * s.C + c], z - s.coef[2 * s.C + c], s.coef[4 * s.C + c]));
 }
 __device__ __forceinline__ float4 src_xform4(const DevSrc& s, long long i, int c) {
-  const float4 x = *reinterpret_cast<const float4*>(s.x + i);
+  const float4 x = src_x4(s, i);
   if (s.mode == PMU_SRC_RAW) return x;
   const float4 sc = *reinterpret_cast<const float4*>(s.coef + c);
   const float4 sh = *reinterpret_cast<const float4*>(s.coef + s.C + c);
@@ -145,7 +173,7 @@ __device__ __forceinline__ float4 src_xform4(const DevSrc& s, long long i, int c
     return make_float4(fmaxf(0.f, fmaf(x.x, sc.x, sh.x)), fmaxf(0.f, fmaf(x.y, sc.y, sh.y)),
                        fmaxf(0.f, fmaf(x.z, sc.z, sh.z)), fmaxf(0.f, fmaf(x.w, sc.w, sh.w)));
   }
-  const float4 z = *reinterpret_cast<const float4*>(s.z + i);
+  const float4 z = s.zbf ? pmu_ld4(reinterpret_cast<const unsigned short*>(s.z) + i) : pmu_ld4(s.z + i);
   const float4 mu = *reinterpret_cast<const float4*>(s.coef + 2 * s.C + c);
   const float4 kx = *reinterpret_cast<const float4*>(s.coef + 3 * s.C + c);
   const float4 kc = *reinterpret_cast<const float4*>(s.coef + 4 * s.C + c);

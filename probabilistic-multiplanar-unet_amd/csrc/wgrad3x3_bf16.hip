@@ -324,7 +324,7 @@ static void geometry(int N, int H, int W, int Cin, int Cout, int* wco, int* twl,
 }  // namespace
 
 extern "C" int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* out, void* stream) {
-  PMU_REQUIRE(valid_frame(f) && out && Cpad % 4 == 0);
+  PMU_REQUIRE(valid_frame(f, true) && out && Cpad % 4 == 0);
   const int C = f->src[0].C + (f->nsrc > 1 ? f->src[1].C : 0);
   PMU_REQUIRE(Cpad >= C);
   const long long units = (long long)f->N * f->H * f->W * (Cpad / 8);
@@ -348,7 +348,7 @@ extern "C" int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* o
 }
 
 extern "C" int pmu_frame_to_f32(const pmu_frame* f, float* out, void* stream) {
-  PMU_REQUIRE(valid_frame(f) && out);
+  PMU_REQUIRE(valid_frame(f, true) && out);
   const DevFrame d = make_dev_frame(f);
   const long long units = (long long)d.N * d.H * d.W * (d.C / 4);
   if (d.vec && units < (1LL << 31)) {

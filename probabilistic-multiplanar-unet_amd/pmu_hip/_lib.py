@@ -22,11 +22,12 @@ PMU_OK = 0
 PMU_ERR_ARG = 1001
 SRC_RAW, SRC_BNRELU, SRC_BNBWD = 0, 1, 2
 POOL_NONE, POOL_MAX2, POOL_AVG2CEIL = 0, 1, 2
+DT_X_BF16, DT_Z_BF16 = 1, 2
 
 
 class PmuSrc(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("z", c_void_p), ("coef", c_void_p), ("mode", c_int), ("pool", c_int),
-                ("C", c_int), ("H", c_int), ("W", c_int), ("off_h", c_int), ("off_w", c_int)]
+                ("C", c_int), ("H", c_int), ("W", c_int), ("off_h", c_int), ("off_w", c_int), ("dtype", c_int)]
 
 
 class PmuFrame(ctypes.Structure):
@@ -118,12 +119,16 @@ SIGNATURES = {
     "pmu_bn_eval_coef": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p]),
     "pmu_bn_bwd_reduce": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                   c_void_p]),
+    "pmu_bn_bwd_reduce_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                     c_void_p]),
     "pmu_bn_bwd_tiles": (c_int, [c_int, c_int]),
     "pmu_bn_bwd_finalize": (c_int, [c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_bnrelu_apply": (c_int, [c_void_p, c_void_p, c_longlong, c_int, c_void_p, c_void_p]),
     "pmu_maxpool2_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                  c_void_p]),
+    "pmu_maxpool2_bwd_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                    c_void_p]),
     "pmu_avgpool2_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_packed_size": (c_size_t, [c_int, c_int]),
     "pmu_convT2x2_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
@@ -188,6 +193,14 @@ SIGNATURES = {
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_dma_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_fwd_dma_zb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                       c_void_p, c_void_p, c_void_p]),
+    "pmu_bn_center": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_wgrad_ws_wino4": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_conv3x3_wgrad_wino4": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                        c_size_t, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_bnr_zb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_pack_wino2h_blocks": (c_int, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_wino2h_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "pmu_conv3x3_pack_wino4_blocks": (c_int, [c_int, c_int, c_int]),

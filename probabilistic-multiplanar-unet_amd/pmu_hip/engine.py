@@ -22,6 +22,7 @@ import torch
 from . import _lib as L
 
 F32 = torch.float32
+BF16S = torch.int16   # bf16 values kept as their 16-bit patterns (the kernels' unsigned short)
 
 
 # ----------------------------------------------------------------------------------------
@@ -57,10 +58,12 @@ def make_frame(srcs, N: int, H: int, W: int) -> L.PmuFrame:
     f.N, f.H, f.W = N, H, W
     for i, s in enumerate(srcs):
         t = s.x
-        assert t.is_contiguous() and t.dtype == F32 and t.dim() == 4, "operand must be contiguous NHWC fp32"
+        assert t.is_contiguous() and t.dtype in (F32, BF16S) and t.dim() == 4, \
+            "operand must be contiguous NHWC fp32 (or bf16 bits)"
         c = f.src[i]
         c.x = t.data_ptr()
         c.z = s.z.data_ptr() if s.z is not None else None
+        c.dtype = (L.DT_X_BF16 if t.dtype == BF16S else 0) | (L.DT_Z_BF16 if s.z is not None and s.z.dtype == BF16S else 0)
         c.coef = s.coef.data_ptr() if s.coef is not None else None
         c.mode, c.pool = s.mode, s.pool
         c.C, c.H, c.W = t.shape[3], t.shape[1], t.shape[2]
@@ -70,6 +73,14 @@ def make_frame(srcs, N: int, H: int, W: int) -> L.PmuFrame:
 
 def frame_of(srcs, N, H, W):
     return ctypes.byref(make_frame(srcs, N, H, W))
+
+
+def _f32_srcs(srcs, N, H, W):
+    """srcs for a call that stages fp32 frames itself (the fused-staging kernels): unchanged when every
+    source is stored in fp32, else the frame's values materialised once in fp32 as one RAW source."""
+    if all(sr.x.dtype == F32 and (sr.z is None or sr.z.dtype == F32) for sr in srcs):
+        return srcs
+    return [Src(frame_to_f32(srcs, N, H, W))]
 
 
 def _empty(*shape, dtype=F32, device=None):
@@ -159,8 +170,8 @@ def bn_backward(da: torch.Tensor, z: torch.Tensor, st: BNState, bn: torch.nn.Bat
     else:
         R = lb.pmu_bn_bwd_tiles(P, C)
         part = _empty(R, 2 * C, device=dev)
-        L.call("pmu_bn_bwd_reduce", da.data_ptr(), z.data_ptr(), st.coef.data_ptr(), st.mean.data_ptr(),
-               st.invstd.data_ptr(), P, C, part.data_ptr(), s)
+        L.call("pmu_bn_bwd_reduce_zb" if z.dtype == BF16S else "pmu_bn_bwd_reduce", da.data_ptr(), z.data_ptr(),
+               st.coef.data_ptr(), st.mean.data_ptr(), st.invstd.data_ptr(), P, C, part.data_ptr(), s)
     G = lb.pmu_colsum_groups(R)
     acc = _empty(G, 2 * C, dtype=torch.float64, device=dev)
     L.call("pmu_colsum_f64", part.data_ptr(), R, 2 * C, acc.data_ptr(), G, s)
@@ -206,13 +217,21 @@ def _check_channels(cin: int, layer) -> None:
 
 
 def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H, W, training, dev,
-                    planes=None, bf16=False, keep=False) -> ConvBNOut:
+                    planes=None, bf16=False, keep=False, zb=False) -> ConvBNOut:
+    """relu(bn(conv(operand))) forward: z (pre-BN conv output, NHWC) + batch statistics.
+
+    zb (bf16 mode, unet_forward with CFG.bf16_z): the LDS-DMA conv stores z in bf16, as torch.autocast
+    keeps a conv's output, centred on the BN running mean (pmu_conv3x3_fwd_dma_zb: bf16(z - rm), so
+    the rounding is relative to the channel's spread, not its mean); the layer's coefficients are
+    then the centred ones (pmu_bn_center) and its consumers read z through bf16-aware frames,
+    pmu_bn_bwd_reduce_zb, pmu_maxpool2_bwd_zb and the *_bnr_zb input gradient."""
     Cout = conv.out_channels
     _check_channels(len(planes) if planes is not None else sum(sr.C for sr in srcs), conv)
     s = L.stream()
     lb = L.lib()
     z = _empty(N, H, W, Cout, device=dev)
     xt = None
+    zoff = None
     need_stats = training or not bn.track_running_stats
     if planes is not None and not first_layer_ok(len(planes), Cout):
         # channel counts outside the first-layer kernel: the generic 3x3 path on a raw NHWC frame
@@ -235,8 +254,16 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             # both operands by LDS-DMA (maps >= 32 wide): the operand written once in bf16, as below
             xt = frame_to_bf16(srcs, N, H, W)
             wp = pack_weights_dma(conv.weight, dgrad=False)
-            L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), Cp, N, H, W, wp.data_ptr(), L.ptr(conv.bias), Cout,
-                   z.data_ptr(), L.ptr(part), s)
+            if zb and Cout % 8 == 0:   # (the bf16-z consumers take channel quads)
+                z = _empty(N, H, W, Cout, dtype=BF16S, device=dev)
+                # the running mean before this step's update (bn_forward below moves it)
+                zoff = (bn.running_mean.detach().clone() if bn.track_running_stats and bn.running_mean is not None
+                        else torch.zeros(Cout, device=dev))
+                L.call("pmu_conv3x3_fwd_dma_zb", xt.data_ptr(), Cp, N, H, W, wp.data_ptr(), L.ptr(conv.bias), Cout,
+                       z.data_ptr(), zoff.data_ptr(), L.ptr(part), s)
+            else:
+                L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), Cp, N, H, W, wp.data_ptr(), L.ptr(conv.bias), Cout,
+                       z.data_ptr(), L.ptr(part), s)
             if not keep:
                 xt = None
         elif use_raw:
@@ -252,8 +279,8 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             wp = pack_weights_bf16(conv.weight, dgrad=False)
             xt = (torch.empty(N, H, W, Cp, dtype=torch.int16, device=dev)
                   if keep else None)   # the weight gradient's operand, teed by the fused kernel
-            L.call("pmu_conv3x3_fwd_bf16", frame_of(srcs, N, H, W), wp.data_ptr(), L.ptr(conv.bias), Cout,
-                   z.data_ptr(), L.ptr(part), L.ptr(xt), s)
+            L.call("pmu_conv3x3_fwd_bf16", frame_of(_f32_srcs(srcs, N, H, W), N, H, W), wp.data_ptr(),
+                   L.ptr(conv.bias), Cout, z.data_ptr(), L.ptr(part), L.ptr(xt), s)
     else:
         Cin = sum(sr.C for sr in srcs)
         # the weight gradient reads the operand the kernel staged (RAW) instead of re-deriving it
@@ -296,6 +323,9 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             L.call("pmu_conv3x3_fwd", frame_of(srcs, N, H, W), conv.weight.data_ptr(), wp.data_ptr(),
                    L.ptr(conv.bias), Cout, z.data_ptr(), L.ptr(part), L.ptr(xt32), s)
     st = bn_forward(part, R, Cout, N * H * W, bn, training, dev)
+    if zoff is not None:   # consumers apply the coefficients to the centred stored z
+        L.call("pmu_bn_center", st.coef.data_ptr(), L.ptr(st.mean), zoff.data_ptr(), Cout, st.coef.data_ptr(),
+               L.ptr(st.mean), s)
     bfl = bf16 and planes is None
     return ConvBNOut(z=z, bn=st, srcs=list(srcs), planes=planes, bf16=bfl, xt=xt if bfl else None,
                      xt32=None if (bf16 or planes is not None) else xt32)
@@ -377,6 +407,9 @@ def _dgrad32(dz_src, conv, N, H, W, split, tee, prod=None):
     sp = Cin if split is None else split
     dx0 = _empty(N, H, W, sp, device=dev)
     dx1 = _empty(N, H, W, Cin - sp, device=dev) if split is not None else None
+    if prod is not None and prod.z.dtype != F32:
+        prod = None   # the fp32 kernels' BN-backward epilogue reads an fp32 z
+    dz_src = _f32_srcs([dz_src], N, H, W)[0]
     dzf = frame_of([dz_src], N, H, W)
     lb = L.lib()
     if use_wino() and wino4_ok(Cout, H, W, "dgrad"):
@@ -426,8 +459,13 @@ def _conv_backward_tee32(out: ConvBNOut, dz_src, conv, dw, split, prod=None):
     Cin = conv.in_channels
     dzt = _empty(N, H, W, Cout, device=dev)
     res = _dgrad32(dz_src, conv, N, H, W, split, dzt, prod)
-    wsb = lb.pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout) if use_wino() else 0
-    if wsb:
+    wsb4 = lb.pmu_conv3x3_wgrad_ws_wino4(N, H, W, Cin, Cout) if (use_wino() and CFG.wgrad4) else 0
+    wsb = 0 if wsb4 else (lb.pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout) if use_wino() else 0)
+    if wsb4:
+        ws = _empty((wsb4 + 3) // 4, device=dev)
+        L.call("pmu_conv3x3_wgrad_wino4", dzt.data_ptr(), out.xt32.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(),
+               ws.data_ptr(), wsb4, s)
+    elif wsb:
         ws = _empty((wsb + 3) // 4, device=dev)
         L.call("pmu_conv3x3_wgrad_wino", dzt.data_ptr(), out.xt32.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(),
                ws.data_ptr(), wsb, s)
@@ -475,7 +513,8 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
         if dma_ok(H, W, dzt.shape[3], Cin, sp):
             wp = pack_weights_dma(conv.weight, dgrad=True)
             if prod is not None:
-                _bnr_call("pmu_conv3x3_dgrad_dma_bnr", prod, L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3]),
+                _bnr_call("pmu_conv3x3_dgrad_dma_bnr_zb" if prod.z.dtype == BF16S else "pmu_conv3x3_dgrad_dma_bnr",
+                          prod, L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3]),
                           (dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin), dx0, s)
             else:
                 L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
@@ -486,8 +525,8 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
                    dx0.data_ptr(), L.ptr(dx1), s)
         else:
             wp = pack_weights_bf16(conv.weight, dgrad=True)
-            L.call("pmu_conv3x3_dgrad_bf16", frame_of([dz_src], N, H, W), wp.data_ptr(), Cin, sp, dx0.data_ptr(),
-                   L.ptr(dx1), None, s)
+            L.call("pmu_conv3x3_dgrad_bf16", frame_of(_f32_srcs([dz_src], N, H, W), N, H, W), wp.data_ptr(), Cin,
+                   sp, dx0.data_ptr(), L.ptr(dx1), None, s)
         res = dx0 if split is None else (dx0, dx1)
     xt = out.xt if out.xt is not None else frame_to_bf16(out.srcs, N, H, W)
     out.xt = None
@@ -559,18 +598,29 @@ class EngineConfig:
     wino2h: the 1024-thread F(2x2) kernels (default) or the 512-thread ones — PMU_WINO2H=0;
     wino4: where F(4x4,3x3) runs — "dgrad" (default: the input gradient of maps >= 32x32) or "0"
         (nowhere) — PMU_WINO4.  "1" (the forward too) breaks the model-level 1e-3 contract (see
-        wino4_ok) and is honoured only by an experiments build of the library (make EXPERIMENTS=1)."""
+        wino4_ok) and is honoured only by an experiments build of the library (make EXPERIMENTS=1);
+    bf16_z: bf16 mode (unet_forward) stores the LDS-DMA convs' pre-BN output z in bf16, centred on the
+        BN running mean — the dtype torch.autocast gives a conv's output.  Off by default: it breaks
+        the c5 Dice contract (eval Dice gap 6.8e-3 centred / 5.4e-3 uncentred vs 2.2e-4 with fp32 z,
+        tests/test_bf16_gpu.py::test_c5_bf16_dice_gap_vs_fp32_oracle; DESIGN.md §3b), so PMU_BF16_Z=1
+        is honoured only by an experiments build of the library, as PMU_WINO4=1;
+    wgrad4: the fp32 weight gradient by Winograd F(4x4,3x3) where its shapes allow (PMU_WGRAD4=1; off by
+        default: measured equal to F(2x2) over the c2 shapes, 10.29 vs 10.29 ms — LDS-read bound)."""
     fp32_conv: str = "wino"
     wino2h: bool = True
     wino4: str = "dgrad"
+    bf16_z: bool = False
+    wgrad4: bool = False
 
     @classmethod
     def from_env(cls):
         return cls(fp32_conv=os.environ.get("PMU_FP32_CONV", "wino"), wino2h=os.environ.get("PMU_WINO2H", "1") != "0",
-                   wino4=os.environ.get("PMU_WINO4", "dgrad"))
+                   wino4=os.environ.get("PMU_WINO4", "dgrad"), bf16_z=os.environ.get("PMU_BF16_Z", "0") == "1",
+                   wgrad4=os.environ.get("PMU_WGRAD4", "0") == "1")
 
 
 CFG = EngineConfig.from_env()
+_BF16_Z_FORCED = False   # tests: exercise the bf16-z path on the shipped library (monkeypatched)
 
 
 def wino4_ok(C: int, H: int, W: int, kind: str) -> bool:
@@ -717,8 +767,9 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         first_srcs = [Src(xc.permute(0, 2, 3, 1).contiguous())]
     # ---- encoder
     c1w, b1, c2w, b2 = _dc_layers(net.inc)
-    o1 = conv_bn_forward(first_srcs, c1w, b1, N, H, W, training, dev, planes=planes, bf16=bf16, keep=keep)
-    o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev, bf16=bf16, keep=keep)
+    zb = bf16 and CFG.bf16_z and (_BF16_Z_FORCED or L.experiments_build())
+    o1 = conv_bn_forward(first_srcs, c1w, b1, N, H, W, training, dev, planes=planes, bf16=bf16, keep=keep, zb=zb)
+    o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev, bf16=bf16, keep=keep, zb=zb)
     st.enc.append((o1, o2))
     h, w = H, W
     for down in net.down_blocks:
@@ -733,8 +784,8 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
             pooled = _empty(N, h, w, prev.z.shape[3], device=dev)
             L.call("pmu_frame_to_f32", frame_of(srcs, N, h, w), pooled.data_ptr(), L.stream())
             srcs = [Src(pooled)]
-        o1 = conv_bn_forward(srcs, c1w, b1, N, h, w, training, dev, bf16=bf16, keep=keep)
-        o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev, bf16=bf16, keep=keep)
+        o1 = conv_bn_forward(srcs, c1w, b1, N, h, w, training, dev, bf16=bf16, keep=keep, zb=zb)
+        o2 = conv_bn_forward([o1.act()], c2w, b2, N, h, w, training, dev, bf16=bf16, keep=keep, zb=zb)
         st.enc.append((o1, o2))
     # ---- decoder
     cur = st.enc[-1][1]
@@ -759,20 +810,20 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
                    Cin_t, Cup, u.data_ptr(), L.stream())
             if not keep:
                 xtT = None
-        elif bf16 and L.lib().pmu_convT2x2_bf16_ok(fin, Cup):
+        elif bf16 and L.lib().pmu_convT2x2_bf16_ok(fin, Cup):   # (refuses bf16-stored sources)
             wpt = pack_convT_weights_bf16(convT.weight, dgrad=False)
             L.call("pmu_convT2x2_fwd_bf16", fin, wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
         else:
             wpt = pack_convT_weights(convT.weight, dgrad=False)
-            L.call("pmu_convT2x2_fwd", fin, convT.weight.data_ptr(), wpt.data_ptr(), L.ptr(convT.bias), Cup,
-                   u.data_ptr(), L.stream())
+            L.call("pmu_convT2x2_fwd", frame_of(_f32_srcs([cur.act()], N, hi, wi), N, hi, wi), convT.weight.data_ptr(),
+                   wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
         dY, dX = hs - 2 * hi, ws_ - 2 * wi
         assert dY >= 0 and dX >= 0, "decoder feature map larger than skip (unsupported by reference too)"
         off = (dY // 2, dX // 2)
         c1w, b1, c2w, b2 = _dc_layers(up.conv)
         srcs = [skip.act(), Src(u, L.SRC_RAW, off=off)]
-        o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev, bf16=bf16, keep=keep)
-        o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev, bf16=bf16, keep=keep)
+        o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev, bf16=bf16, keep=keep, zb=zb)
+        o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev, bf16=bf16, keep=keep, zb=zb)
         st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2, bf16=bf16, xt=xtT))
         cur = o2
     st.feat_src = cur
@@ -785,6 +836,8 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         st.y = y
         return y, st
     C = cur.z.shape[3]
+    if cur.z.dtype != F32:
+        return frame_to_f32([cur.act()], N, H, W).permute(0, 3, 1, 2), st
     feat = _empty(N, H, W, C, device=dev)
     L.call("pmu_bnrelu_apply", cur.z.data_ptr(), cur.bn.coef.data_ptr(), N * H * W, C, feat.data_ptr(), L.stream())
     return feat.permute(0, 3, 1, 2), st
@@ -863,7 +916,8 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             wsb = L.lib().pmu_convT2x2_wgrad_ws(N, hi, wi, Cin_t, Cup)
             ws = _empty(max(1, (wsb + 3) // 4), device=dev)
             L.call("pmu_convT2x2_wgrad", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1],
-                   frame_of([prev.act()], N, hi, wi), Cup, dwt.data_ptr(), L.ptr(dbt), ws.data_ptr(), wsb, s)
+                   frame_of(_f32_srcs([prev.act()], N, hi, wi), N, hi, wi), Cup, dwt.data_ptr(), L.ptr(dbt),
+                   ws.data_ptr(), wsb, s)
         grads.flush()
         da = dx
     # ---- encoder, deepest first; da = gradient w.r.t. the deepest encoder output
@@ -883,8 +937,8 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             prev = st.enc[lev - 1][1]
             hp, wp = prev.z.shape[1], prev.z.shape[2]
             Cp = prev.z.shape[3]
-            L.call("pmu_maxpool2_bwd", dpool.data_ptr(), prev.z.data_ptr(), prev.bn.coef.data_ptr(), N, hp, wp, Cp,
-                   dskip[lev - 1].data_ptr(), 1, s)
+            L.call("pmu_maxpool2_bwd_zb" if prev.z.dtype == BF16S else "pmu_maxpool2_bwd", dpool.data_ptr(),
+                   prev.z.data_ptr(), prev.bn.coef.data_ptr(), N, hp, wp, Cp, dskip[lev - 1].data_ptr(), 1, s)
     return grads
 
 

@@ -1,0 +1,21 @@
+# F(4x4) weight gradient + bf16 z: new kernel tests first, kbench of both wgrads, then the full GPU
+# suite, c2 / c5 benches and rocprof stats into gpurun_out/wg4.
+set -u
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-wg4}; mkdir -p $O
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_wgrad4_gpu.py tests/test_zb_gpu.py -q -m gpu -p no:cacheprovider --timeout 240 --timeout-method thread > $O/tests_new.log 2>&1; rc=$?
+tail -3 $O/tests_new.log
+if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" $O/tests_new.log | head -30; exit $rc; fi
+true
+true
+timeout -k 10 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -x > $O/tests_gpu.log 2>&1; rc=$?
+tail -3 $O/tests_gpu.log
+if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" $O/tests_gpu.log | head -30; exit $rc; fi
+timeout -k 10 600 python bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err || exit $?
+cut -c 1-200 $O/bench_c2.json
+timeout -k 10 600 python bench.py --workload c5 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err || exit $?
+cut -c 1-200 $O/bench_c5.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2 -o bench -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing > $O/prof_c2.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o bench -- python3 $R/bench.py --workload c5 --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing --no-eval > $O/prof_c5.log 2>&1 || exit $?
+echo done

@@ -104,6 +104,8 @@ def main():
         dzt32 = torch.randn(N, H, W, Cout, device=dev)
         wsbw = L.lib().pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout)
         wsw = torch.empty(max(wsbw, 4) // 4, device=dev)
+        wsb4 = L.lib().pmu_conv3x3_wgrad_ws_wino4(N, H, W, Cin, Cout)
+        ws4 = torch.empty(max(wsb4, 4) // 4, device=dev)
         from pmu_hip.engine import pack_weights_wino
         wwf, wwd = pack_weights_wino(w, False), pack_weights_wino(w, True)
         partw = torch.empty(L.lib().pmu_conv3x3_tiles_wino(N, H, W), 2 * Cout, device=dev)
@@ -119,7 +121,23 @@ def main():
             return t
         wdf, wdd = packd(w, False), packd(w, True)
         partd = torch.empty(L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cout, cpi), 2 * Cout, device=dev)
+        # a producer of the Cin channels for the *_bnr input gradients (BN-backward partials in the epilogue)
+        zp = torch.randn(N, H, W, Cin, device=dev)
+        cp = torch.cat([torch.rand(Cin, device=dev) + 0.5, torch.randn(Cin, device=dev) * 0.1])
+        mp, ip = torch.randn(Cin, device=dev) * 0.1, torch.rand(Cin, device=dev) + 0.5
+        def bnr(tiles):
+            pp = torch.empty(tiles, 2 * Cin, device=dev)
+            return (dx.data_ptr(), zp.data_ptr(), cp.data_ptr(), mp.data_ptr(), ip.data_ptr(), pp.data_ptr(), s)
+        bnr4 = bnr(L.lib().pmu_conv3x3_tiles_wino4(N, H, W))
+        bnr2 = bnr(L.lib().pmu_conv3x3_tiles_wino2h(N, H, W))
+        bnrd = bnr(L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, cpo))
         ops = {
+            "dgrad_w4b": lambda: L.call("pmu_conv3x3_dgrad_wino4_bnr", dzt32.data_ptr(), Cout, N, H, W, w4d.data_ptr(),
+                                        Cin, *bnr4),
+            "dgrad_w2hb": lambda: L.call("pmu_conv3x3_dgrad_wino2h_bnr", dzt32.data_ptr(), Cout, N, H, W,
+                                         w2d.data_ptr(), Cin, *bnr2),
+            "dgrad_dmab": lambda: L.call("pmu_conv3x3_dgrad_dma_bnr", dzt.data_ptr(), cpo, N, H, W, wdd.data_ptr(), Cin,
+                                         *bnrd),
             "fwd_dma": lambda: L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), cpi, N, H, W, wdf.data_ptr(), b.data_ptr(),
                                       Cout, out.data_ptr(), partd.data_ptr(), s),
             "dgrad_dma": lambda: L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), cpo, N, H, W, wdd.data_ptr(), Cin, Cin,
@@ -163,6 +181,8 @@ def main():
                                        out.data_ptr(), partw.data_ptr(), None, s),
             "dgrad_wino": lambda: L.call("pmu_conv3x3_dgrad_wino", fdz, wwd.data_ptr(), Cin, Cin, dx.data_ptr(),
                                          None, None, s),
+            "wgrad_w4": lambda: L.call("pmu_conv3x3_wgrad_wino4", dzt32.data_ptr(), xt32.data_ptr(), N, H, W, Cout,
+                                       Cin, dw.data_ptr(), ws4.data_ptr(), wsb4, s),
             "wgrad_wino": lambda: L.call("pmu_conv3x3_wgrad_wino", dzt32.data_ptr(), xt32.data_ptr(), N, H, W, Cout,
                                          Cin, dw.data_ptr(), wsw.data_ptr(), wsbw, s),
             "pack": lambda: pack_weights(w, False),
@@ -176,7 +196,7 @@ def main():
             tot.setdefault(op, [0.0, 0.0])
             tot[op][0] += ms
             tot[op][1] += flops
-            peak = 2516.0 if (op.endswith("bf16") or op.endswith("raw") or op.endswith("dma")) else 157.3
+            peak = 2516.0 if (op.endswith("bf16") or op.endswith("raw") or "dma" in op) else 157.3
             print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / peak * 100:5.1f}%)",
                   flush=True)
     for op, (ms, fl) in tot.items():
