@@ -72,13 +72,37 @@ class KernelTimer:
             "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16",
             "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino", "pmu_conv3x3_wgrad_wino",
             "pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw", "pmu_conv3x3_fwd_wino4",
-            "pmu_conv3x3_dgrad_wino4", "pmu_conv3x3_fwd_wino2h", "pmu_conv3x3_dgrad_wino2h")
+            "pmu_conv3x3_dgrad_wino4", "pmu_conv3x3_fwd_wino2h", "pmu_conv3x3_dgrad_wino2h",
+            "pmu_conv3x3_dgrad_wino4_bnr", "pmu_conv3x3_dgrad_wino2h_bnr", "pmu_conv3x3_wgrad_wino4",
+            "pmu_conv3x3_fwd_dma", "pmu_conv3x3_fwd_dma_zb", "pmu_conv3x3_dgrad_dma", "pmu_conv3x3_dgrad_dma_bnr",
+            "pmu_conv3x3_dgrad_dma_bnr_zb", "pmu_convT2x2_fwd_dma", "pmu_convT2x2_dgrad_dma")
+
+    @staticmethod
+    def _base(name):
+        """The call family of a fused variant (the BN-backward epilogue / bf16-z forms do the same MFMA work)."""
+        for suf in ("_bnr_zb", "_bnr", "_zb"):
+            if name.endswith(suf):
+                return name[: -len(suf)]
+        return name
 
     def __init__(self):
         self.rec = []
 
     @staticmethod
     def _flops(name, args):
+        name = KernelTimer._base(name)
+        if name == "pmu_conv3x3_wgrad_wino4":
+            N, H, W, cout, cin = args[2], args[3], args[4], args[5], args[6]
+            return 2.0 * 36 * N * ((H + 3) // 4) * ((W + 3) // 4) * cin * cout
+        if name in ("pmu_conv3x3_fwd_dma", "pmu_conv3x3_dgrad_dma"):
+            cp, N, H, W, nout = args[1], args[2], args[3], args[4], args[7] if name.endswith("fwd_dma") else args[6]
+            return 2.0 * N * H * W * cp * nout * 9
+        if name == "pmu_convT2x2_fwd_dma":
+            N, H, W, cin, cout = args[2], args[3], args[4], args[7], args[8]
+            return 2.0 * N * H * W * cin * cout * 4
+        if name == "pmu_convT2x2_dgrad_dma":
+            N, H, W, cin, cout = args[7], args[8], args[9], args[10], args[11]
+            return 2.0 * N * H * W * cin * cout * 4
         if name in ("pmu_conv3x3_fwd_wino4", "pmu_conv3x3_dgrad_wino4"):
             # Winograd F(4x4,3x3): 36 products per 4x4 output tile per channel pair
             cin, N, H, W = args[1], args[2], args[3], args[4]
@@ -148,6 +172,7 @@ class KernelTimer:
     def _direct(name, args, fl):
         """The direct-sum FLOPs of a launch: a Winograd F(2x2,3x3) launch executes 16
         products per 2x2 output tile and channel pair where the direct sum takes 9 per pixel."""
+        name = KernelTimer._base(name)
         if "_wino" not in name or not fl:
             return fl
         if name.endswith("_wino4"):
@@ -388,6 +413,12 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_wgrad_bf16": r"wgrad3x3_bf16_kernel<", "pmu_conv3x3_fwd_raw": r"conv3x3_raw_kernel<false",
     "pmu_conv3x3_dgrad_raw": r"conv3x3_raw_kernel<true", "pmu_convT2x2_fwd_bf16": r"convT_bf16_kernel<false>",
     "pmu_convT2x2_dgrad_bf16": r"convT_bf16_kernel<true>", "pmu_convT2x2_wgrad_bf16": r"convT_wgrad_bf16_kernel",
+    "pmu_conv3x3_dgrad_wino4_bnr": r"conv3x3_wino4_kernel<true", "pmu_conv3x3_dgrad_wino2h_bnr": r"conv3x3_wino2h_kernel<true",
+    "pmu_conv3x3_wgrad_wino4": (r"wgrad3x3_wino4_kernel", r"wgrad_wino4_reduce_kernel"),
+    "pmu_conv3x3_fwd_dma": r"conv3x3_dma_kernel<false", "pmu_conv3x3_fwd_dma_zb": r"conv3x3_dma_kernel<false",
+    "pmu_conv3x3_dgrad_dma": r"conv3x3_dma_kernel<true", "pmu_conv3x3_dgrad_dma_bnr": r"conv3x3_dma_kernel<true",
+    "pmu_conv3x3_dgrad_dma_bnr_zb": r"conv3x3_dma_kernel<true",
+    "pmu_convT2x2_fwd_dma": r"convT_dma_kernel<false", "pmu_convT2x2_dgrad_dma": r"convT_dma_kernel<true",
 }
 
 
@@ -537,9 +568,10 @@ def phantom_batches(S, B, rank, world, dev):
 
 
 def roofline_peak(kernel):
-    """Dense MFMA peak (TFLOP/s) for a C-ABI kernel family: bf16 for the *_bf16 family and the bf16
-    raw GEMMs (pmu_conv3x3_{fwd,dgrad}_raw), fp32 otherwise (the Winograd raw kernels are *_wino_raw)."""
-    bf16 = kernel.endswith("_bf16") or (kernel.endswith("_raw") and "_wino" not in kernel)
+    """Dense MFMA peak (TFLOP/s) for a C-ABI kernel family: bf16 for the *_bf16 family, the LDS-DMA
+    bf16 GEMMs (*_dma*) and the bf16 raw GEMMs (pmu_conv3x3_{fwd,dgrad}_raw), fp32 otherwise (the
+    Winograd raw kernels are *_wino_raw)."""
+    bf16 = (kernel.endswith("_bf16") or "_dma" in kernel or (kernel.endswith("_raw") and "_wino" not in kernel))
     return BF16_MFMA_PEAK_TF if bf16 else FP32_MFMA_PEAK_TF
 
 

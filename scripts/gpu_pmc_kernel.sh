@@ -8,7 +8,7 @@ i=0
 IFS=';' read -ra PS <<< "$PASSES"
 for P in "${PS[@]}"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace -d $O/p$i -o p$i --output-format csv -- python tools/kbench.py --ops ${OPS:-fwd_wr} --only ${SHAPE:-256,64,64} --iters 3 > $O/p$i.log 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc $P --kernel-trace -d $O/p$i -o p$i --output-format csv -- python tools/kbench.py --ops ${OPS:-fwd_wr} --only ${SHAPE:-256,64,64} --iters 3 ${KB_EXTRA:-} > $O/p$i.log 2>&1 || exit $?
 done
 python tools/pmc_summary.py $(find $O -name "*counter_collection.csv") > $O/summary.txt
 cat $O/summary.txt
