@@ -317,6 +317,14 @@ int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int 
 /* the same over a bf16-stored z (coef required, C % 4 == 0) */
 int pmu_maxpool2_bwd_zb(const float* dpool, const unsigned short* z, const float* coef, int N, int H, int W,
                         int C, float* dx, int accumulate, void* stream);
+/* pmu_maxpool2_bwd (BN+ReLU coef, C % 4 == 0) fused with the BatchNorm+ReLU backward reduction of
+ * the pooled layer over the resulting dx (= that layer's da; replaces pmu_bn_bwd_reduce for it):
+ * part[pmu_maxpool2_bwd_bnr_tiles rows][2][C] = (sum g, sum g*xhat), g = dx*(z*scale+shift > 0),
+ * xhat = (z-mean)*invstd.  MaxPool2d(2) backward, unet_parts.py:33; BN backward, unet_parts.py:16,19. */
+int pmu_maxpool2_bwd_bnr_tiles(int N, int H, int W, int C);
+int pmu_maxpool2_bwd_bnr(const float* dpool, const float* z, const float* coef, const float* mean,
+                         const float* invstd, int N, int H, int W, int C, float* dx, int accumulate,
+                         float* part, void* stream);
 /* AvgPool2d(2,2,ceil_mode=True) backward: dx = dpool/count(window), overwrite. */
 int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream);
 
@@ -344,6 +352,15 @@ int pmu_head1x1_fwd(const pmu_frame* in, const float* w, const float* b, int K, 
 /* dl = dy * s*(1-s) (do_sigmoid) or dy; da[N][H][W][C] = w^T dl (NHWC); dl written (NCHW). */
 int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
                     int N, int H, int W, float* dl, float* da, void* stream);
+/* pmu_head1x1_bwd fused with the BatchNorm+ReLU backward reduction of the layer feeding the head
+ * (da is its gradient; replaces pmu_bn_bwd_reduce for it): part[pmu_head1x1_bwd_tiles rows][2][C]
+ * as pmu_maxpool2_bwd_bnr.  Shapes: pmu_head1x1_bwd_bnr_ok (C = 4q, q a power of two <= 64).
+ * OutConv backward, unet_parts.py:70-76; BN backward of the last DoubleConv, unet_parts.py:19. */
+int pmu_head1x1_bwd_bnr_ok(int N, int H, int W, int C);
+int pmu_head1x1_bwd_tiles(int N, int H, int W);
+int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
+                        int N, int H, int W, float* dl, float* da, const float* z, const float* coef,
+                        const float* mean, const float* invstd, float* part, void* stream);
 size_t pmu_wgrad1x1_ws(int P, int K, int C);
 /* dw[K][C] = sum_p dl[p][k] act[p][c], db[k] = sum_p dl[p][k]; dl NCHW [N][K][H][W]. */
 int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float* dw, float* db, float* ws,

@@ -293,6 +293,113 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restri
   }
 }
 
+// MaxPool2d(2) backward into the skip gradient fused with the BatchNorm+ReLU backward partial sums
+// of the pooled layer (its da is complete once the pooled gradient has been routed): a thread owns one
+// channel quad of one 2x2 window (ceil-sized, so the odd last row / column of an odd map is covered
+// for the sums), reads its four z quads once (maxpool2_bwd_kernel re-reads the window per output
+// element), adds dpool to the first max, writes da and accumulates (sum g, sum g*xhat),
+// g = da * (z*scale+shift > 0), xhat = (z-mean)*invstd — the part[block][2][C] slab bn_bwd_reduce
+// would compute from a second pass over da and z.  Block = 256 threads over wpb windows.
+__global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __restrict__ dpool,
+                                                               const float* __restrict__ z,
+                                                               const float* __restrict__ coef,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd, int N, int H, int W,
+                                                               int C, int wpb, float* __restrict__ dx, int accumulate,
+                                                               float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int tid = threadIdx.x;
+  const int CQ = C >> 2;
+  const int npg = CQ >= 256 ? 1 : 256 / CQ;
+  const int qstride = CQ >= 256 ? 256 : CQ;
+  const int pg = tid / qstride, q0 = tid % qstride;
+  const int Hp = H / 2, Wp = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const long long nwin = (long long)N * Hc * Wc;
+  const long long w0 = (long long)blockIdx.x * wpb;
+  const long long wend = min(nwin, w0 + wpb);
+  for (int q = q0; q < CQ; q += qstride) {
+    const int c = 4 * q;
+    const float4 sc = *reinterpret_cast<const float4*>(coef + c);
+    const float4 sh = *reinterpret_cast<const float4*>(coef + C + c);
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+    const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+    float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
+    if (pg < npg) {
+      for (long long wi = w0 + pg; wi < wend; wi += npg) {
+        const int wc = (int)(wi % Wc);
+        const long long r = wi / Wc;
+        const int hc = (int)(r % Hc);
+        const int n = (int)(r / Hc);
+        float zv[4][4], dv[4][4];
+        bool ok[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int h = 2 * hc + (k >> 1), w = 2 * wc + (k & 1);
+          ok[k] = h < H && w < W;
+          const long long off = ((((long long)n * H + (ok[k] ? h : 0)) * W + (ok[k] ? w : 0)) * C + c);
+          PMU_DCHECK(off + 4 <= (long long)N * H * W * C, PMU_DBG_OPERAND);
+          float4 zz = make_float4(0.f, 0.f, 0.f, 0.f), dd = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok[k]) {
+            zz = *reinterpret_cast<const float4*>(z + off);
+            if (accumulate) dd = *reinterpret_cast<const float4*>(dx + off);
+          }
+          zv[k][0] = zz.x; zv[k][1] = zz.y; zv[k][2] = zz.z; zv[k][3] = zz.w;
+          dv[k][0] = dd.x; dv[k][1] = dd.y; dv[k][2] = dd.z; dv[k][3] = dd.w;
+        }
+        if (hc < Hp && wc < Wp) {  // a full window: route dpool to the first max of relu(z*sc+sh)
+          const float4 g = *reinterpret_cast<const float4*>(dpool + (((long long)n * Hp + hc) * Wp + wc) * C + c);
+          const float gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float best = fmaxf(0.f, fmaf(zv[0][e], scv[e], shv[e]));
+            int arg = 0;
+#pragma unroll
+            for (int k = 1; k < 4; ++k) {
+              const float a = fmaxf(0.f, fmaf(zv[k][e], scv[e], shv[e]));
+              if (a > best) { best = a; arg = k; }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (arg == k) dv[k][e] += gv[e];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!ok[k]) continue;
+          const int h = 2 * hc + (k >> 1), w = 2 * wc + (k & 1);
+          const long long off = (((long long)n * H + h) * W + w) * C + c;
+          *reinterpret_cast<float4*>(dx + off) = make_float4(dv[k][0], dv[k][1], dv[k][2], dv[k][3]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gg = fmaf(zv[k][e], scv[e], shv[e]) > 0.f ? dv[k][e] : 0.f;
+            sg[e] += gg;
+            sgx[e] = fmaf(gg, (zv[k][e] - muv[e]) * isv[e], sgx[e]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { red[tid * 8 + e] = sg[e]; red[tid * 8 + 4 + e] = sgx[e]; }
+    __syncthreads();
+    if (pg == 0) {
+      float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
+      for (int l = 0; l < npg; ++l) {
+        const int src = l * qstride + q0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { t1[e] += red[src * 8 + e]; t2[e] += red[src * 8 + 4 + e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        part[((long long)blockIdx.x * 2 + 0) * C + c + e] = t1[e];
+        part[((long long)blockIdx.x * 2 + 1) * C + c + e] = t2[e];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void avgpool2_bwd_kernel(const float* __restrict__ dpool, int N, int H, int W, int C,
                                                            float* __restrict__ dx) {
   const int Hp = (H + 1) / 2, Wp = (W + 1) / 2;
@@ -504,21 +611,44 @@ __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const fl
   }
 }
 
+// BNR: also the BatchNorm+ReLU backward partial sums of the layer feeding the head (da is its
+// gradient): part[block][2][C] = (sum g, sum g*xhat), g = da * (z*scale+shift > 0),
+// xhat = (z-mean)*invstd — what bn_bwd_reduce would read da and z again for
+struct HeadBnr {
+  const float* z;
+  const float* coef;
+  const float* mean;
+  const float* invstd;
+  float* part;
+};
+
+template <bool BNR>
 __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                                                             int do_sigmoid, const float* __restrict__ w, int K, int C,
                                                             long long HW, long long P, float* __restrict__ dl,
-                                                            float* __restrict__ da) {
-  const int tid = threadIdx.x;
+                                                            float* __restrict__ da, HeadBnr bn) {
+  __shared__ float red[BNR ? 4 * 2 * 256 : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int CQ = C >> 2, PG = 256 / CQ;
   const int cq = tid & (CQ - 1), pg = tid / CQ;
   float4 wq[HEAD_KMAX];
 #pragma unroll
   for (int k = 0; k < HEAD_KMAX; ++k)
     wq[k] = k < K ? *reinterpret_cast<const float4*>(w + k * C + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 sc, sh, mu, is;
+  float s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  if (BNR) {
+    sc = *reinterpret_cast<const float4*>(bn.coef + 4 * cq);
+    sh = *reinterpret_cast<const float4*>(bn.coef + C + 4 * cq);
+    mu = *reinterpret_cast<const float4*>(bn.mean + 4 * cq);
+    is = *reinterpret_cast<const float4*>(bn.invstd + 4 * cq);
+  }
   // 32-bit pixel decode (P < 2^31, host-checked): 64-bit divisions per pixel dominated
   const unsigned HWu = (unsigned)HW, pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
   for (unsigned p = blockIdx.x * HPPB + pg; p < pend; p += PG) {
     const unsigned n = p / HWu, pix = p - n * HWu;
+    float4 zz;
+    if (BNR) zz = *reinterpret_cast<const float4*>(bn.z + (size_t)p * C + 4 * cq);  // in flight with dy
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < HEAD_KMAX; ++k) {
@@ -531,6 +661,39 @@ __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restr
       o.z = fmaf(g, wq[k].z, o.z); o.w = fmaf(g, wq[k].w, o.w);
     }
     *reinterpret_cast<float4*>(da + (size_t)p * C + 4 * cq) = o;
+    if (BNR) {
+      const float ov[4] = {o.x, o.y, o.z, o.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
+      const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+      const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = fmaf(zv[e], scv[e], shv[e]) > 0.f ? ov[e] : 0.f;
+        s1[e] += g;
+        s2[e] = fmaf(g, (zv[e] - muv[e]) * isv[e], s2[e]);
+      }
+    }
+  }
+  if (BNR) {  // the wave's pixel groups by xor shuffles, then the 4 waves in order
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      for (int o = CQ; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    if (lane < CQ) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[(wave * 2 + 0) * 256 + 4 * cq + e] = s1[e];
+        red[(wave * 2 + 1) * 256 + 4 * cq + e] = s2[e];
+      }
+    }
+    __syncthreads();
+    for (int o = tid; o < 2 * C; o += 256) {
+      const int r = o / C, c = o - r * C;
+      float t = 0.f;
+      for (int wv = 0; wv < 4; ++wv) t += red[(wv * 2 + r) * 256 + c];
+      bn.part[(long long)blockIdx.x * 2 * C + o] = t;
+    }
   }
 }
 
@@ -918,6 +1081,27 @@ extern "C" int pmu_maxpool2_bwd_zb(const float* dpool, const unsigned short* z, 
   return PMU_OK;
 }
 
+// windows per block of the fused max-pool backward: about 128 KB of z per block
+static int mpb_wpb(int C) {
+  const int w = 8192 / C;
+  return w < 1 ? 1 : w;
+}
+
+extern "C" int pmu_maxpool2_bwd_bnr_tiles(int N, int H, int W, int C) {
+  return (int)pmu_cdiv((long long)N * ((H + 1) / 2) * ((W + 1) / 2), mpb_wpb(C));
+}
+
+extern "C" int pmu_maxpool2_bwd_bnr(const float* dpool, const float* z, const float* coef, const float* mean,
+                                    const float* invstd, int N, int H, int W, int C, float* dx, int accumulate,
+                                    float* part, void* stream) {
+  PMU_REQUIRE(dpool && z && coef && mean && invstd && dx && part && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
+  const int R = pmu_maxpool2_bwd_bnr_tiles(N, H, W, C);
+  hipLaunchKernelGGL(maxpool2_bwd_bnr_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dpool, z, coef,
+                     mean, invstd, N, H, W, C, mpb_wpb(C), dx, accumulate, part);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
 extern "C" int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream) {
   PMU_REQUIRE(dpool && dx && N > 0 && H > 0 && W > 0 && C > 0);
   const long long units = (long long)N * H * W * (C / 4);
@@ -965,13 +1149,34 @@ extern "C" int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, 
   const long long P = (long long)N * H * W;
   const int CQ = C >> 2;
   if ((C & 3) == 0 && CQ <= 64 && (CQ & (CQ - 1)) == 0 && P < (1LL << 31)) {
-    hipLaunchKernelGGL(head_bwd_fast_kernel, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
-                       dy, y, do_sigmoid, w, K, C, (long long)H * W, P, dl, da);
+    const HeadBnr nob{nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipLaunchKernelGGL(head_bwd_fast_kernel<false>, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0,
+                       (hipStream_t)stream, dy, y, do_sigmoid, w, K, C, (long long)H * W, P, dl, da, nob);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }
   hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)pmu_cdiv(P, 256)), dim3(256), 0, (hipStream_t)stream,
                      dy, y, do_sigmoid, w, K, C, N, H, W, dl, da);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_head1x1_bwd_bnr_ok(int N, int H, int W, int C) {
+  const int CQ = C >> 2;
+  return (C & 3) == 0 && CQ <= 64 && (CQ & (CQ - 1)) == 0 && (long long)N * H * W < (1LL << 31);
+}
+
+extern "C" int pmu_head1x1_bwd_tiles(int N, int H, int W) { return (int)pmu_cdiv((long long)N * H * W, HPPB); }
+
+extern "C" int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
+                                   int N, int H, int W, float* dl, float* da, const float* z, const float* coef,
+                                   const float* mean, const float* invstd, float* part, void* stream) {
+  PMU_REQUIRE(dy && w && dl && da && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y) && N > 0 && H > 0 &&
+              W > 0 && z && coef && mean && invstd && part && pmu_head1x1_bwd_bnr_ok(N, H, W, C));
+  const long long P = (long long)N * H * W;
+  const HeadBnr bn{z, coef, mean, invstd, part};
+  hipLaunchKernelGGL(head_bwd_fast_kernel<true>, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
+                     dy, y, do_sigmoid, w, K, C, (long long)H * W, P, dl, da, bn);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -129,6 +129,9 @@ SIGNATURES = {
                                  c_void_p]),
     "pmu_maxpool2_bwd_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                     c_void_p]),
+    "pmu_maxpool2_bwd_bnr_tiles": (c_int, [c_int, c_int, c_int, c_int]),
+    "pmu_maxpool2_bwd_bnr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                     c_void_p, c_int, c_void_p, c_void_p]),
     "pmu_avgpool2_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_packed_size": (c_size_t, [c_int, c_int]),
     "pmu_convT2x2_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
@@ -141,6 +144,10 @@ SIGNATURES = {
     "pmu_head1x1_fwd": (c_int, [_FP, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pmu_head1x1_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                 c_void_p, c_void_p, c_void_p]),
+    "pmu_head1x1_bwd_bnr_ok": (c_int, [c_int, c_int, c_int, c_int]),
+    "pmu_head1x1_bwd_tiles": (c_int, [c_int, c_int, c_int]),
+    "pmu_head1x1_bwd_bnr": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_wgrad1x1_ws": (c_size_t, [c_int, c_int, c_int]),
     "pmu_wgrad1x1": (c_int, [c_void_p, _FP, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_sgd_clip": (c_int, [c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_void_p]),

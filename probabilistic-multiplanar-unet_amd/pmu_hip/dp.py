@@ -135,13 +135,17 @@ class BucketAllReduce:
     def _issue_range(self, lo, hi):
         self.works.append(dist.all_reduce(self.buf[lo:hi], group=self.group, async_op=True))
 
-    def _ready(self, params):
-        """GradSink.flush callback: ``params``' gradient kernels are enqueued."""
+    def _ready(self, params, flat=True):
+        """GradSink.flush callback: ``params``' gradient kernels are enqueued.  ``flat``: into the flat
+        buffer (else into tensors autograd adds to .grad later: order recorded, no bucket issued —
+        those gradients are copied into their slots in ``finish``)."""
         if not self.active:
             return
         if self.recording is not None:
             seen = {id(p) for p in self.recording}
             self.recording += [p for p in params if id(p) not in seen]
+            return
+        if not flat:
             return
         self.flushes += 1
         for p in params:

@@ -92,15 +92,16 @@ class GradSink(dict):
     of the network's persistent flat gradient buffer when one is attached (stable pointers for
     the fused optimizer / one-shot all-reduce), else a fresh tensor.
 
-    ``on_ready`` (flat-buffer sinks only): called by ``flush()`` with the parameters whose
+    ``on_ready``: called by ``flush()`` as ``on_ready(params, flat)`` with the parameters whose
     gradient kernels have been enqueued on the stream since the previous flush, so a
-    data-parallel reducer (pmu_hip.dp) can start a bucket's all-reduce while the rest of the
-    backward still runs."""
+    data-parallel reducer (pmu_hip.dp) can learn the backward order and, for a flat-buffer sink
+    (``flat``), start a bucket's all-reduce while the rest of the backward still runs."""
 
     def __init__(self, views=None, on_ready=None):
         super().__init__()
         self.views = views
-        self.on_ready = on_ready if views is not None else None
+        self.flat = views is not None
+        self.on_ready = on_ready
         self._pending = []
 
     def new(self, p):
@@ -115,7 +116,7 @@ class GradSink(dict):
     def flush(self):
         if self.on_ready is not None and self._pending:
             ready, self._pending = self._pending, []
-            self.on_ready(ready)
+            self.on_ready(ready, self.flat)
 
 
 # ----------------------------------------------------------------------------------------
@@ -857,8 +858,18 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         dyc = dy.contiguous()
         dl = _empty(N, K, H, W, device=dev)
         da = _empty(N, H, W, C, device=dev)
-        L.call("pmu_head1x1_bwd", dyc.data_ptr(), st.y.data_ptr(), int(net.n_classes == 1),
-               net.outc.conv.weight.data_ptr(), K, C, N, H, W, dl.data_ptr(), da.data_ptr(), s)
+        lb = L.lib()
+        if last.z.dtype == F32 and last.bn.mean is not None and lb.pmu_head1x1_bwd_bnr_ok(N, H, W, C):
+            # the head's input gradient also forms the last layer's BN-backward partial sums
+            R = lb.pmu_head1x1_bwd_tiles(N, H, W)
+            part = _empty(R, 2 * C, device=dev)
+            L.call("pmu_head1x1_bwd_bnr", dyc.data_ptr(), st.y.data_ptr(), int(net.n_classes == 1),
+                   net.outc.conv.weight.data_ptr(), K, C, N, H, W, dl.data_ptr(), da.data_ptr(), last.z.data_ptr(),
+                   last.bn.coef.data_ptr(), last.bn.mean.data_ptr(), last.bn.invstd.data_ptr(), part.data_ptr(), s)
+            last.bnr = (da, part, R)
+        else:
+            L.call("pmu_head1x1_bwd", dyc.data_ptr(), st.y.data_ptr(), int(net.n_classes == 1),
+                   net.outc.conv.weight.data_ptr(), K, C, N, H, W, dl.data_ptr(), da.data_ptr(), s)
         dwo = grads.new(net.outc.conv.weight)
         dbo = grads.new(net.outc.conv.bias) if net.outc.conv.bias is not None else _empty(K, device=dev)
         wsb = L.lib().pmu_wgrad1x1_ws(N * H * W, K, C)
@@ -937,8 +948,18 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             prev = st.enc[lev - 1][1]
             hp, wp = prev.z.shape[1], prev.z.shape[2]
             Cp = prev.z.shape[3]
-            L.call("pmu_maxpool2_bwd_zb" if prev.z.dtype == BF16S else "pmu_maxpool2_bwd", dpool.data_ptr(),
-                   prev.z.data_ptr(), prev.bn.coef.data_ptr(), N, hp, wp, Cp, dskip[lev - 1].data_ptr(), 1, s)
+            if prev.z.dtype == F32 and prev.bn.mean is not None and Cp % 4 == 0:
+                # routed into the skip gradient, which completes the pooled layer's da: the same pass
+                # forms that layer's BN-backward partial sums (no pmu_bn_bwd_reduce for it)
+                R = L.lib().pmu_maxpool2_bwd_bnr_tiles(N, hp, wp, Cp)
+                part = _empty(R, 2 * Cp, device=dev)
+                L.call("pmu_maxpool2_bwd_bnr", dpool.data_ptr(), prev.z.data_ptr(), prev.bn.coef.data_ptr(),
+                       prev.bn.mean.data_ptr(), prev.bn.invstd.data_ptr(), N, hp, wp, Cp, dskip[lev - 1].data_ptr(),
+                       1, part.data_ptr(), s)
+                prev.bnr = (dskip[lev - 1], part, R)
+            else:
+                L.call("pmu_maxpool2_bwd_zb" if prev.z.dtype == BF16S else "pmu_maxpool2_bwd", dpool.data_ptr(),
+                       prev.z.data_ptr(), prev.bn.coef.data_ptr(), N, hp, wp, Cp, dskip[lev - 1].data_ptr(), 1, s)
     return grads
 
 

@@ -90,10 +90,7 @@ def _offsets(root, plist):
 
 class LiveNode:
     """Marks one pending autograd node of ``module`` (created in forward, released when its backward
-    has run or its graph was freed).  While two nodes of one module are pending — the module applied
-    twice in one graph, e.g. loss(net(x1)) + loss(net(x2)) — their gradients must not both be views
-    of the same flat-buffer slots: autograd sums the two node outputs before AccumulateGrad, and
-    aliased views would give 2*g2 instead of g1 + g2."""
+    has run or its graph was freed); ``module._pmu_live`` counts them (diagnostics and tests)."""
     __slots__ = ("d",)
 
     def __init__(self, module):
@@ -112,11 +109,25 @@ class LiveNode:
 def grad_sink_for(module, params) -> GradSink:
     """Destination of this node's parameter gradients (fresh flat-buffer views, see module doc).
     The views are created per backward and not retained, so autograd can adopt them as .grad.
-    Plain tensors instead when a .grad already exists (autograd accumulates into it) or another
-    node of the same module is still pending (see LiveNode)."""
-    if not all(p.grad is None for p in params) or module.__dict__.get("_pmu_live", 0) > 1:
-        return GradSink()
+
+    Plain tensors instead when a .grad already exists (autograd accumulates into it), or when
+    another node of the same module already received the views in this same backward pass (the
+    module applied twice in one graph, e.g. loss(net(x1)) + loss(net(x2))): autograd sums the two
+    node outputs before AccumulateGrad, and aliased views would give 2*g2 instead of g1 + g2.  A
+    second node that is pending but never reached by the backward (the Probabilistic U-Net's prior
+    sample ``masks_pred``, alive while -elbo backpropagates) does not count: the test is per
+    autograd graph task, not per pending node.
+
+    Either way the sink reports its layers to the root's data-parallel reducer (``on_ready``), so
+    the backward order is learned even from a step whose last backward accumulates into existing
+    .grad tensors (several micro-batches per rank); only flat-buffer sinks let it issue buckets."""
     root = grad_root(module)
+    ready = root.__dict__.get("_pmu_grad_ready")
+    task = torch._C._current_graph_task_id()
+    d = module.__dict__
+    if not all(p.grad is None for p in params) or (task >= 0 and d.get("_pmu_views_task") == task):
+        return GradSink(on_ready=ready)
+    d["_pmu_views_task"] = task
     plist = list(root.parameters())
     buf = flat_grad_buffer(root, plist)
     offs = _offsets(root, plist)
@@ -125,7 +136,7 @@ def grad_sink_for(module, params) -> GradSink:
         o = offs.get(id(p))
         if o is not None:
             views[p] = buf[o:o + p.numel()].view_as(p)
-    return GradSink(views, on_ready=root.__dict__.get("_pmu_grad_ready"))
+    return GradSink(views, on_ready=ready)
 
 
 # ----------------------------------------------------------------------------------------

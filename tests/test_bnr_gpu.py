@@ -90,3 +90,56 @@ def test_dgrad_bnr_dma(dev, N, H, W, Cin, Cout):
     torch.cuda.synchronize()
     assert torch.equal(dx, plain)
     _check(dx, part, z, coef, mean, invstd, dev)
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 64, 64, 64), (1, 33, 45, 32), (2, 16, 16, 512), (1, 7, 9, 1040)])
+def test_maxpool2_bwd_bnr(dev, N, H, W, C):
+    """pmu_maxpool2_bwd_bnr: dx bit-equal to pmu_maxpool2_bwd accumulated onto the same skip gradient
+    (odd maps: the last row / column gets the skip gradient only), and the partials of the result."""
+    from pmu_hip import _lib as L
+    g = torch.Generator().manual_seed(31 + H + C)
+    z, coef, mean, invstd = _bn_inputs(N, H, W, C, g, dev)
+    z[:, ::3, ::2, :5] = -coef[C:C + 5].cpu().to(dev) / coef[:5]   # a few exact ties of the activation at 0
+    dpool = torch.randn(N, H // 2, W // 2, C, generator=g).to(dev)
+    skip = torch.randn(N, H, W, C, generator=g).to(dev)
+    dx = skip.clone()
+    R = L.lib().pmu_maxpool2_bwd_bnr_tiles(N, H, W, C)
+    part = torch.full((R, 2 * C), float("nan"), device=dev)
+    L.call("pmu_maxpool2_bwd_bnr", dpool.data_ptr(), z.data_ptr(), coef.data_ptr(), mean.data_ptr(),
+           invstd.data_ptr(), N, H, W, C, dx.data_ptr(), 1, part.data_ptr(), L.stream())
+    ref = skip.clone()
+    L.call("pmu_maxpool2_bwd", dpool.data_ptr(), z.data_ptr(), coef.data_ptr(), N, H, W, C, ref.data_ptr(), 1,
+           L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref)
+    # against torch's max_pool2d backward on the activation (first max of each window)
+    act = torch.relu(z.double().cpu() * coef[:C].double().cpu() + coef[C:].double().cpu()).permute(0, 3, 1, 2)
+    act.requires_grad_(True)
+    torch.nn.functional.max_pool2d(act, 2).backward(dpool.double().cpu().permute(0, 3, 1, 2))
+    want = skip.double().cpu() + act.grad.permute(0, 2, 3, 1)
+    assert float((dx.double().cpu() - want).abs().max()) <= 1e-6 * float(want.abs().max())
+    _check(dx, part, z, coef, mean, invstd, dev)
+
+
+@pytest.mark.parametrize("N,H,W,C,K,sig", [(2, 64, 64, 64, 1, 1), (3, 37, 45, 32, 3, 0), (1, 16, 16, 256, 2, 0)])
+def test_head1x1_bwd_bnr(dev, N, H, W, C, K, sig):
+    """pmu_head1x1_bwd_bnr: dl and da bit-equal to pmu_head1x1_bwd, and the partials of da."""
+    from pmu_hip import _lib as L
+    g = torch.Generator().manual_seed(41 + H + C)
+    z, coef, mean, invstd = _bn_inputs(N, H, W, C, g, dev)
+    dy = torch.randn(N, K, H, W, generator=g).to(dev)
+    y = torch.rand(N, K, H, W, generator=g).to(dev)
+    w = (torch.randn(K, C, generator=g) * 0.1).to(dev)
+    assert L.lib().pmu_head1x1_bwd_bnr_ok(N, H, W, C)
+    R = L.lib().pmu_head1x1_bwd_tiles(N, H, W)
+    part = torch.full((R, 2 * C), float("nan"), device=dev)
+    dl, da = torch.empty(N, K, H, W, device=dev), torch.empty(N, H, W, C, device=dev)
+    L.call("pmu_head1x1_bwd_bnr", dy.data_ptr(), y.data_ptr(), sig, w.data_ptr(), K, C, N, H, W, dl.data_ptr(),
+           da.data_ptr(), z.data_ptr(), coef.data_ptr(), mean.data_ptr(), invstd.data_ptr(), part.data_ptr(),
+           L.stream())
+    dl2, da2 = torch.empty_like(dl), torch.empty_like(da)
+    L.call("pmu_head1x1_bwd", dy.data_ptr(), y.data_ptr(), sig, w.data_ptr(), K, C, N, H, W, dl2.data_ptr(),
+           da2.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dl, dl2) and torch.equal(da, da2)
+    _check(da, part, z, coef, mean, invstd, dev)

@@ -162,6 +162,20 @@ def _bucket_worker(rank, world, port, q, mode, acc):
                 if mode == "foreign":
                     for p in plist:
                         p.grad = g[name_of[id(p)]].clone()   # accumulated outside the flat buffer
+                elif mode == "accumulated":
+                    # several micro-batches per rank: the earlier backward left flat-buffer .grad views
+                    # (here zeros), so the last one's sink hands out plain tensors that autograd adds in
+                    first = grad_sink_for(net, plist)
+                    for p in plist:
+                        p.grad = first.new(p).zero_()
+                    sink = grad_sink_for(net, plist)
+                    assert not sink.flat
+                    for grp in groups:
+                        for p in grp:
+                            v = sink.new(p)
+                            v.copy_(g[name_of[id(p)]])
+                            p.grad.add_(v)
+                        sink.flush()                         # reports the order, issues nothing
                 else:
                     sink = grad_sink_for(net, plist)
                     for grp in groups:
@@ -185,6 +199,7 @@ def _bucket_worker(rank, world, port, q, mode, acc):
 
 
 @pytest.mark.parametrize("mode,world,acc", [("backward_order", 2, 8), ("forward_order", 2, 8), ("foreign", 2, 8),
+                                            ("accumulated", 2, 8),
                                             ("backward_order", 4, 8), ("backward_order", 8, 8),
                                             ("backward_order", 4, 2)])
 def test_dp_bucketed_overlap_matches_reference_accumulation(mode, world, acc):
@@ -209,6 +224,8 @@ def test_dp_bucketed_overlap_matches_reference_accumulation(mode, world, acc):
                 assert first is not None and first < flushes // 2   # bucket 0 long before the end
             elif mode == "forward_order" and busy:
                 assert issued == nb                   # the layout follows the learned (reversed) order too
+            elif mode == "accumulated":
+                assert issued == 0                    # learned from plain-sink reports; exchanged at finish()
             else:
                 assert issued == 0                    # foreign grads / idle rank: all at finish()
 

@@ -244,12 +244,21 @@ def test_probunet_flat_grad_buffer(dev):
     x = torch.rand(2, 1, 32, 32, device=dev)
     segm = torch.randint(0, 3, (2, 1, 32, 32), device=dev).float()
     net.forward(x, segm, training=True)
-    (-net.elbo(segm)).backward()
+    # the trainer's step: a prior sample (masks_pred, with grad) stays alive while -elbo backpropagates,
+    # so a second Fcomb node is pending but never reached: Fcomb still gets the flat-buffer views
+    masks_pred = net.sample(testing=False)
+    loss = -net.elbo(segm)
+    assert net.fcomb.__dict__["_pmu_live"] == 2
+    loss.backward()
     buf = flat_grad_buffer(net)
     lo, hi = buf.data_ptr(), buf.data_ptr() + buf.numel() * 4
+    seen = 0
     for k, p in net.named_parameters():
         if p.grad is not None:
             assert lo <= p.grad.data_ptr() < hi, k
+            seen += k.startswith("fcomb.")
+    assert seen == len(list(net.fcomb.parameters()))
+    del masks_pred
 
 
 def test_probunet_odd_filters_vs_oracle(dev):

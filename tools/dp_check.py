@@ -52,7 +52,7 @@ def main():
     # the backward's real report order, seen through the reducer's flush callback
     reports = []
     orig = net.__dict__["_pmu_grad_ready"]
-    net.__dict__["_pmu_grad_ready"] = lambda ps: (reports.append([id(p) for p in ps]), orig(ps))
+    net.__dict__["_pmu_grad_ready"] = lambda ps, flat=True: (reports.append([id(p) for p in ps]), orig(ps, flat))
     ok = True
     for it in range(3):
         for p in plist:
