@@ -109,12 +109,15 @@ __global__ __launch_bounds__(256) void pack_dma_multi_kernel(const pmu_pack_job*
   pack_dma_body(j.w, j.Cout, j.Cin, dgrad, dma_bn(NOUT, KC), (unsigned short*)j.dst, blockIdx.x - j.block0, j.nblocks);
 }
 
-template <bool DGRAD, int WN, int NWV>
+// ZB: z stored in bf16 (the experiments-build bf16-z mode: the forward writes it, the input gradient's
+// BN-backward epilogue reads it)
+template <bool DGRAD, bool ZB, int WN, int NWV>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs a) {
   using G = DG<WN, NWV>;
   constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH, NT = G::NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index as a uniform (SGPR) value: the epilogue's row pointers derive from it
+  const int tid = threadIdx.x, lane = tid & 63, wave = DGRAD ? tid >> 6 : __builtin_amdgcn_readfirstlane(tid >> 6);
   // (spatial tile, channel block), channel blocks fastest in XCD order: the channel blocks of one
   // tile share its halo image through their XCD's L2
   const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
@@ -218,63 +221,103 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
 #undef PMU_GLDS
 
   // epilogue: accumulator (fm, fn, r) = output pixel (tile row 4 wm + fm, column acc_row(r, lane)),
-  // channel j0 + 64 wn + 32 fn + (lane & 31); a 32-channel destination is uniform (split % 32 == 0)
+  // channel j0 + 64 wn + 32 fn + (lane & 31); a 32-channel destination is uniform (split % 32 == 0).
   float* red = reinterpret_cast<float*>(smem);  // [NWV waves][64][2] (the stages are free now)
   float s1[FN], s2[FN];
-#pragma unroll
-  for (int fn = 0; fn < FN; ++fn) {
-    s1[fn] = 0.f;
-    s2[fn] = 0.f;
-    const int jb = j0 + wn * 64 + fn * 32;
-    const int j = jb + li;
-    const bool jok = j < a.NOUT;
-    const float b = (!DGRAD && jok && a.bias) ? a.bias[j] : 0.f;
-    const float zo = (!DGRAD && jok && a.zoff) ? a.zoff[j] : 0.f;
-    const bool bnr = DGRAD && a.bz && jok;
-    const float bsc = bnr ? a.bcoef[j] : 0.f, bsh = bnr ? a.bcoef[a.NOUT + j] : 0.f;
-    const float bmu = bnr ? a.bmean[j] : 0.f, bis = bnr ? a.binv[j] : 0.f;
-    float* dstp;
-    int ld;
-    if (!DGRAD) { dstp = a.out0 + j; ld = a.NOUT; }
-    else if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
-    else { dstp = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
-#pragma unroll
+  if constexpr (!DGRAD) {
+    // Forward: values and BN sums formed unconditionally (masked), only the stores predicated.  With the
+    // bias first consumed inside a per-output branch the compiler waited vmcnt(0) in every branch,
+    // i.e. for all earlier stores of the epilogue (one store in flight at a time: 112 waits for 128
+    // stores).  Store addresses: a uniform row base per (fm, fn) + a 32-bit column offset.
+    bool jok[FN];
+    float bv[FN], zov[FN];
+  #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] = 0.f;
+      s2[fn] = 0.f;
+      const int j = j0 + wn * 64 + fn * 32 + li;
+      jok[fn] = j < a.NOUT;
+      const int jc = jok[fn] ? j : a.NOUT - 1;
+      bv[fn] = a.bias ? a.bias[jc] : 0.f;
+      zov[fn] = (ZB && a.zoff) ? a.zoff[jc] : 0.f;
+    }
+  #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
       const int h = h0 + 4 * wm + fm;
-      // the producer's z under this row's 16 outputs, loaded together before the stores (clamped
-      // addresses: every lane loads, no branch per load; unused values are ignored)
-      float zt[16];
-      if (DGRAD && a.bz) {
-        const int jc = min(j, a.NOUT - 1);
-        const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
-#pragma unroll
+      const long long rowpix = ((long long)n * a.H + (h < a.H ? h : a.H - 1)) * a.W;
+      float* drow = a.out0 + rowpix * a.NOUT;
+      unsigned short* drowb = reinterpret_cast<unsigned short*>(a.out0) + rowpix * a.NOUT;
+  #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int j = j0 + wn * 64 + fn * 32 + li;
+  #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const long long zi = (row + min(w0 + acc_row(r, lane), a.W - 1)) * a.NOUT + jc;
-          zt[r] = a.zbf == 1 ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
+          const int w = w0 + acc_row(r, lane);
+          const bool ok = jok[fn] && h < a.H && w < a.W;
+          float v = acc[fm][fn][r] + bv[fn];
+          unsigned short vb = 0;
+          if (ZB) {
+            vb = bf16_bits(v - zov[fn]);
+            v = pmu_bf16_f32(vb) + zov[fn];
+          }
+          const float m = ok ? v : 0.f;
+          s1[fn] += m;
+          s2[fn] = fmaf(m, m, s2[fn]);
+          if (!ok) continue;
+          PMU_DCHECK(((long long)n * a.H + h) * a.W + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+          const unsigned oo = (unsigned)(w * a.NOUT + j);
+          if (ZB) drowb[oo] = vb;
+          else drow[oo] = v;
         }
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int w = w0 + acc_row(r, lane);
-        if (!jok || h >= a.H || w >= a.W) continue;
-        const long long pix = ((long long)n * a.H + h) * a.W + w;
-        PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-        float v = acc[fm][fn][r] + b;
-        if (!DGRAD && a.zbf) {
-          const unsigned short vb = bf16_bits(v - zo);
-          reinterpret_cast<unsigned short*>(a.out0)[pix * ld + j] = vb;
-          v = pmu_bf16_f32(vb) + zo;
-        } else {
-          dstp[pix * ld] = v;
+    }
+  } else {
+    // the input gradient keeps per-output branches around its (optional, a.bz) z uses: the straight-line
+    // form above with the producer's BN-backward sums spilled 18-140 VGPRs in every arrangement tried
+    // (compile-time variant, masked sums, half rows, fm-outer order)
+  #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] = 0.f;
+      s2[fn] = 0.f;
+      const int jb = j0 + wn * 64 + fn * 32;
+      const int j = jb + li;
+      const bool jok = j < a.NOUT;
+      const bool bnr = a.bz && jok;
+      const float bsc = bnr ? a.bcoef[j] : 0.f, bsh = bnr ? a.bcoef[a.NOUT + j] : 0.f;
+      const float bmu = bnr ? a.bmean[j] : 0.f, bis = bnr ? a.binv[j] : 0.f;
+      float* dstp;
+      int ld;
+      if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
+      else { dstp = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
+  #pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int h = h0 + 4 * wm + fm;
+        // the producer's z under this row's 16 outputs, loaded together before the stores (clamped
+        // addresses: every lane loads, no branch per load; unused values are ignored)
+        float zt[16];
+        if (a.bz) {
+          const int jc = min(j, a.NOUT - 1);
+          const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const long long zi = (row + min(w0 + acc_row(r, lane), a.W - 1)) * a.NOUT + jc;
+            zt[r] = ZB ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
+          }
         }
-        if (!DGRAD) {
-          s1[fn] += v;
-          s2[fn] = fmaf(v, v, s2[fn]);
-        } else if (bnr) {
-          const float zz = zt[r];
-          const float gg = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
-          s1[fn] += gg;
-          s2[fn] = fmaf(gg, (zz - bmu) * bis, s2[fn]);
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int w = w0 + acc_row(r, lane);
+          if (!jok || h >= a.H || w >= a.W) continue;
+          const long long pix = ((long long)n * a.H + h) * a.W + w;
+          PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+          const float v = acc[fm][fn][r];
+          dstp[pix * ld] = v;
+          if (bnr) {
+            const float zz = zt[r];
+            const float gg = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
+            s1[fn] += gg;
+            s2[fn] = fmaf(gg, (zz - bmu) * bis, s2[fn]);
+          }
         }
       }
     }
@@ -355,10 +398,17 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks), blk(64 * sh.nwv);
-  if (sh.wn == 1 && dgrad) hipLaunchKernelGGL((conv3x3_dma_kernel<true, 1, 4>), grid, blk, 0, st, a);
-  else if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<false, 1, 4>), grid, blk, 0, st, a);
-  else if (dgrad) hipLaunchKernelGGL((conv3x3_dma_kernel<true, 2, 8>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((conv3x3_dma_kernel<false, 2, 8>), grid, blk, 0, st, a);
+  const bool zb = zbf == 1;
+#define PMU_DMA_LAUNCH(D, Z)                                                                              \
+  {                                                                                                       \
+    if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 4>), grid, blk, 0, st, a);            \
+    else hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 2, 8>), grid, blk, 0, st, a);                       \
+  }
+  if (dgrad && zb) PMU_DMA_LAUNCH(true, true)
+  else if (dgrad) PMU_DMA_LAUNCH(true, false)
+  else if (zb) PMU_DMA_LAUNCH(false, true)
+  else PMU_DMA_LAUNCH(false, false)
+#undef PMU_DMA_LAUNCH
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -274,7 +274,7 @@ __device__ __forceinline__ void w2_partial(const f32x4 (&acc)[2][8], int h, int 
 // epilogue: lane holds M[comp (half CH)][tile 4*kk + r of the group][co j0 + 32 cg + 16 h + (lane & 15)];
 // the two component halves of (tg, cg) swap the partial outputs of the co half the other finishes
 // through xb (a free LDS stage), in two rounds of two tiles per lane
-template <bool DGRAD, int CH, int CO>
+template <bool DGRAD, bool BNR, int CH, int CO>
 __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, int w0, int j0, int spatial,
                                                 const f32x4 (&acc)[2][8], float* xb, float* red, float bias) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kk = lane >> 4;
@@ -283,7 +283,7 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
   const bool jok = j < a.NOUT;
   float s1 = 0.f, s2 = 0.f;
   float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
-  if (DGRAD && a.bz && jok) {
+  if (BNR && jok) {
     bsc = a.bcoef[j];
     bsh = a.bcoef[a.NOUT + j];
     bmu = a.bmean[j];
@@ -308,7 +308,7 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
       // the producer's z under this tile's 4 outputs, loaded together ahead of the output transform
       // (clamped addresses: every lane loads, no branch per load; unused values are ignored)
       float zt[4];
-      if (DGRAD && a.bz) {
+      if (BNR) {
         const int jc = min(j, a.NOUT - 1);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -318,31 +318,33 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
       }
       float P[4];
       w2_partial<CH>(acc, CH, r, P);
+      // Values, masks and BN sums are formed unconditionally and only the stores are predicated: a
+      // global-memory value (bias, z) first consumed inside a per-output branch made the compiler
+      // wait vmcnt(0) in every branch, i.e. for every earlier store of the epilogue to complete.
+      const long long pix0 = ((long long)n * a.H + oh) * a.W + ow;
 #pragma unroll
       for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int hh = oh + p, ww = ow + q;
-          const float y = P[2 * p + q] + xb[((partner * 2 + rr) * 4 + 2 * p + q) * 64 + lane];
-          if (!jok || hh >= a.H || ww >= a.W) continue;
-          const float v = y + bias;
-          const long long pix = ((long long)n * a.H + hh) * a.W + ww;
-          PMU_DCHECK(pix < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
+          const float v = P[2 * p + q] + xb[((partner * 2 + rr) * 4 + 2 * p + q) * 64 + lane] + bias;
+          const bool ok = jok && hh < a.H && ww < a.W;
+          const long long pix = pix0 + (long long)p * a.W + q;
           if (!DGRAD) {
-            a.out0[pix * a.NOUT + j] = v;
-            s1 += v;
-            s2 = fmaf(v, v, s2);
-          } else if (j < a.split) {
-            a.out0[pix * a.split + j] = v;
-            if (a.bz) {
-              const float zz = zt[2 * p + q];
-              const float g = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
-              s1 += g;
-              s2 = fmaf(g, (zz - bmu) * bis, s2);
-            }
-          } else {
-            a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+            const float m = ok ? v : 0.f;
+            s1 += m;
+            s2 = fmaf(m, m, s2);
+          } else if (BNR) {
+            const float zz = zt[2 * p + q];
+            const float g = (ok && fmaf(zz, bsc, bsh) > 0.f) ? v : 0.f;
+            s1 += g;
+            s2 = fmaf(g, (zz - bmu) * bis, s2);
           }
+          if (!ok) continue;
+          PMU_DCHECK(pix < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
+          if (!DGRAD) a.out0[pix * a.NOUT + j] = v;
+          else if (j < a.split) a.out0[pix * a.split + j] = v;
+          else a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
         }
     }
   }
@@ -380,7 +382,7 @@ struct W2Block {
   unsigned gin, gzero;
 };
 
-template <bool DGRAD, int CH, int CO_>
+template <bool DGRAD, bool BNR, int CH, int CO_>
 __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, const unsigned (&goff)[W2Cfg<CO_>::NGL],
                                             float* smem) {
   using C = W2Cfg<CO_>;
@@ -438,7 +440,7 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
     int ne = B.n, h0e = B.h0, w0e = B.w0;
     asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
     float* xb = smem + ((gi - 1) & 1) * STAGE;
-    wino2h_epilogue<DGRAD, CH, CO>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    wino2h_epilogue<DGRAD, BNR, CH, CO>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
     if (p + 1 < B.npass) {  // block-uniform: restore the zero units the exchange overwrote
 #pragma unroll
       for (int r = 0; r < NGL; ++r)
@@ -454,7 +456,9 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
 #undef PMU_GLDS
 }
 
-template <bool DGRAD, int CO_>
+// BNR (input gradient only): the producer's BN-backward partial sums in the epilogue (a.bz set) — a
+// compile-time choice, so the z loads and their uses sit in straight-line code
+template <bool DGRAD, bool BNR, int CO_>
 __global__ __launch_bounds__(16 * CO_, 1) void conv3x3_wino2h_kernel(W2Args a) {
   using C = W2Cfg<CO_>;
   constexpr int NT = C::NT, NGL = C::NGL, STAGE = C::STAGE;
@@ -497,8 +501,8 @@ __global__ __launch_bounds__(16 * CO_, 1) void conv3x3_wino2h_kernel(W2Args a) {
   }
   B.gin = gin;
   B.gzero = gzero;
-  if ((tid >> 8) & 1) wino2h_main<DGRAD, 1, CO_>(a, B, goff, smem);
-  else wino2h_main<DGRAD, 0, CO_>(a, B, goff, smem);
+  if ((tid >> 8) & 1) wino2h_main<DGRAD, BNR, 1, CO_>(a, B, goff, smem);
+  else wino2h_main<DGRAD, BNR, 0, CO_>(a, B, goff, smem);
 }
 
 // output channels per block (PMU_WINO2H_CO=32: 512-thread blocks, two per CU; A/B)
@@ -556,10 +560,13 @@ int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, 
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks);
-  if (CO == 32 && dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, 32>), grid, dim3(512), 0, st, a);
-  else if (CO == 32) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, 32>), grid, dim3(512), 0, st, a);
-  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, 64>), grid, dim3(1024), 0, st, a);
-  else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, 64>), grid, dim3(1024), 0, st, a);
+  const bool bnr = dgrad && bz;
+  if (CO == 32 && bnr) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, true, 32>), grid, dim3(512), 0, st, a);
+  else if (CO == 32 && dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, false, 32>), grid, dim3(512), 0, st, a);
+  else if (CO == 32) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 32>), grid, dim3(512), 0, st, a);
+  else if (bnr) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, true, 64>), grid, dim3(1024), 0, st, a);
+  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, false, 64>), grid, dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64>), grid, dim3(1024), 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

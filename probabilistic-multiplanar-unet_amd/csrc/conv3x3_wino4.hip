@@ -363,7 +363,7 @@ __device__ __forceinline__ void w4_partial(const f32x4 (&acc)[2][18], int h, int
 // in acc[h][cl][r].  The two waves of a tile group (halves 0 and 1) swap the partial outputs of the
 // co half the other one finishes through xb (a free LDS stage), in two rounds of two tiles per lane;
 // wave (tg, CH) then finishes co half CH: bias, store, BN partial sums.
-template <bool DGRAD, int CH>
+template <bool DGRAD, bool BNR, int CH>
 __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, int w0, int j0, int spatial,
                                                const f32x4 (&acc)[2][18], float* xb, float* red, float bias) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kk = lane >> 4;
@@ -372,7 +372,7 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
   const bool jok = j < a.NOUT;
   float s1 = 0.f, s2 = 0.f;
   float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
-  if (DGRAD && a.bz && jok) {
+  if (BNR && jok) {
     bsc = a.bcoef[j];
     bsh = a.bcoef[a.NOUT + j];
     bmu = a.bmean[j];
@@ -397,7 +397,7 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
       // the producer's z under this tile's 16 outputs, loaded before the output transform so the
       // loads are in flight together (issued one per store, each waited for on its own)
       float zt[16];
-      if (DGRAD && a.bz) {
+      if (BNR) {
         const int jc = min(j, a.NOUT - 1);  // clamped: every lane loads (no branch per load), unused ones ignored
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -408,32 +408,33 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
       }
       float P[16];
       w4_partial<CH>(acc, CH, r, P);
+      // values, masks and BN sums unconditional, only the stores predicated (see conv3x3_wino2h.hip:
+      // a global value first consumed inside a per-output branch cost a vmcnt(0) per store)
+      const long long pix0 = ((long long)n * a.H + oh) * a.W + ow;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int hh2 = oh + p;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int ww = ow + q;
-          const float y = P[4 * p + q] + xb[((partner * 2 + rr) * 16 + 4 * p + q) * 64 + lane];
-          if (!jok || hh2 >= a.H || ww >= a.W) continue;
-          const float v = y + bias;
-          const long long pix = ((long long)n * a.H + hh2) * a.W + ww;
-          PMU_DCHECK(pix < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
+          const float v = P[4 * p + q] + xb[((partner * 2 + rr) * 16 + 4 * p + q) * 64 + lane] + bias;
+          const bool ok = jok && hh2 < a.H && ww < a.W;
+          const long long pix = pix0 + (long long)p * a.W + q;
           if (!DGRAD) {
-            a.out0[pix * a.NOUT + j] = v;
-            s1 += v;
-            s2 = fmaf(v, v, s2);
-          } else if (j < a.split) {
-            a.out0[pix * a.split + j] = v;
-            if (a.bz) {
-              const float zz = zt[4 * p + q];
-              const float g = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
-              s1 += g;
-              s2 = fmaf(g, (zz - bmu) * bis, s2);
-            }
-          } else {
-            a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+            const float m = ok ? v : 0.f;
+            s1 += m;
+            s2 = fmaf(m, m, s2);
+          } else if (BNR) {
+            const float zz = zt[4 * p + q];
+            const float g = (ok && fmaf(zz, bsc, bsh) > 0.f) ? v : 0.f;
+            s1 += g;
+            s2 = fmaf(g, (zz - bmu) * bis, s2);
           }
+          if (!ok) continue;
+          PMU_DCHECK(pix < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
+          if (!DGRAD) a.out0[pix * a.NOUT + j] = v;
+          else if (j < a.split) a.out0[pix * a.split + j] = v;
+          else a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
         }
       }
     }
@@ -473,7 +474,7 @@ struct W4Block {
 };
 
 // the pass / chunk pipeline of a wave of component half CH (waves 4 CH .. 4 CH + 3)
-template <bool DGRAD, int CH, bool PF>
+template <bool DGRAD, bool BNR, int CH, bool PF>
 __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, const unsigned (&goff)[NGL],
                                            float* smem) {
   float* red = smem + 2 * STAGE;
@@ -530,7 +531,7 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
     int ne = B.n, h0e = B.h0, w0e = B.w0;
     asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
     float* xb = smem + ((gi - 1) & 1) * STAGE;
-    wino4_epilogue<DGRAD, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    wino4_epilogue<DGRAD, BNR, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
     if (p + 1 < B.npass) {  // block-uniform: every wave takes the barrier
       // the exchange overwrote xb's stage: restore its zero units (each thread its own) before the
       // next pass reads it
@@ -552,7 +553,9 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
 // (pass, chunk) sequence is one DMA pipeline, so the next pass's first chunk lands under this
 // pass's epilogue.  Waves 0-3 compute components 0..17 (rows 0-2 of the 6x6 grid), waves 4-7 the
 // rest, each for its tile group's 16 tiles x all 32 output channels.
-template <bool DGRAD, bool PF>
+// BNR (input gradient only): the producer's BN-backward partial sums in the epilogue (a.bz set) — a
+// compile-time choice, so the z loads and their uses sit in straight-line code
+template <bool DGRAD, bool BNR, bool PF>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
   const int tid = threadIdx.x;
@@ -609,8 +612,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   B.gin = gin;
   B.gzero = gzero;
   if (a.prio && (tid >> 8)) __builtin_amdgcn_s_setprio(1);
-  if (tid >> 8) wino4_main<DGRAD, 1, PF>(a, B, goff, smem);
-  else wino4_main<DGRAD, 0, PF>(a, B, goff, smem);
+  if (tid >> 8) wino4_main<DGRAD, BNR, 1, PF>(a, B, goff, smem);
+  else wino4_main<DGRAD, BNR, 0, PF>(a, B, goff, smem);
 }
 
 int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
@@ -681,10 +684,11 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks);
-  if (dgrad && pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true>), grid, dim3(NT), 0, st, a);
-  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false>), grid, dim3(NT), 0, st, a);
-  else if (pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<false, true>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false>), grid, dim3(NT), 0, st, a);
+  if (dgrad && bz) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, false>), grid, dim3(NT), 0, st, a);
+  else if (dgrad && pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, true>), grid, dim3(NT), 0, st, a);
+  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, false>), grid, dim3(NT), 0, st, a);
+  else if (pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, true>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, false>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
