@@ -213,6 +213,11 @@ int pmu_conv3x3_fwd_dma(const unsigned short* xt, int Cp, int N, int H, int W, c
                         const float* bias, int Cout, float* z, float* part, void* stream);
 int pmu_conv3x3_dgrad_dma(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                           int Cin, int Csplit, float* dx0, float* dx1, void* stream);
+/* the same with a concat split (Csplit < Cin, (Cin - Csplit) % 8 == 0) that also writes dx1b, a bf16
+ * (RNE) copy of dx1 [N][H][W][Cin-Csplit]: the up-sampled part's gradient is the transposed conv's
+ * bf16 operand (unet_parts.py:52,66 under autocast) — no separate pmu_frame_to_bf16 pass over dx1 */
+int pmu_conv3x3_dgrad_dma_x1b(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                              int Cin, int Csplit, float* dx0, float* dx1, unsigned short* dx1b, void* stream);
 /* as pmu_conv3x3_dgrad_wino2h_bnr (part rows = pmu_conv3x3_tiles_dma(N, H, W, Cin, Cp)) */
 int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                               int Cin, float* dx, const float* z, const float* coef, const float* mean,
@@ -354,13 +359,16 @@ int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, const float
                     int N, int H, int W, float* dl, float* da, void* stream);
 /* pmu_head1x1_bwd fused with the BatchNorm+ReLU backward reduction of the layer feeding the head
  * (da is its gradient; replaces pmu_bn_bwd_reduce for it): part[pmu_head1x1_bwd_tiles rows][2][C]
- * as pmu_maxpool2_bwd_bnr.  Shapes: pmu_head1x1_bwd_bnr_ok (C = 4q, q a power of two <= 64).
+ * as pmu_maxpool2_bwd_bnr.  With dw non-NULL the same pass also forms the head's weight gradient
+ * (pmu_wgrad1x1's dw[K][C] and db[K] from act = relu(z*scale+shift); ws of pmu_wgrad1x1_ws bytes) and
+ * dl is not written (may be NULL).  Shapes: pmu_head1x1_bwd_bnr_ok (C = 4q, q a power of two <= 64).
  * OutConv backward, unet_parts.py:70-76; BN backward of the last DoubleConv, unet_parts.py:19. */
 int pmu_head1x1_bwd_bnr_ok(int N, int H, int W, int C);
 int pmu_head1x1_bwd_tiles(int N, int H, int W);
 int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
                         int N, int H, int W, float* dl, float* da, const float* z, const float* coef,
-                        const float* mean, const float* invstd, float* part, void* stream);
+                        const float* mean, const float* invstd, float* part, float* dw, float* db, float* ws,
+                        size_t ws_bytes, void* stream);
 size_t pmu_wgrad1x1_ws(int P, int K, int C);
 /* dw[K][C] = sum_p dl[p][k] act[p][c], db[k] = sum_p dl[p][k]; dl NCHW [N][K][H][W]. */
 int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float* dw, float* db, float* ws,

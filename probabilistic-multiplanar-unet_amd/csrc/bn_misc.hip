@@ -614,20 +614,25 @@ __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const fl
 // BNR: also the BatchNorm+ReLU backward partial sums of the layer feeding the head (da is its
 // gradient): part[block][2][C] = (sum g, sum g*xhat), g = da * (z*scale+shift > 0),
 // xhat = (z-mean)*invstd — what bn_bwd_reduce would read da and z again for
+// WG (with BNR): also the head's weight / bias gradient partials ws[block][K][C+1] from the same z
+// reads, a = relu(z*scale+shift) — wgrad1x1_fast_kernel's block, thread mapping and summation order, so
+// rows_sum_split4_kernel turns them into the same dw, db; dl is then not written
 struct HeadBnr {
   const float* z;
   const float* coef;
   const float* mean;
   const float* invstd;
   float* part;
+  float* ws;
 };
 
-template <bool BNR>
+template <bool BNR, bool WG = false>
 __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                                                             int do_sigmoid, const float* __restrict__ w, int K, int C,
                                                             long long HW, long long P, float* __restrict__ dl,
                                                             float* __restrict__ da, HeadBnr bn) {
   __shared__ float red[BNR ? 4 * 2 * 256 : 1];
+  __shared__ float redw[WG ? 4 * HEAD_KMAX * 260 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int CQ = C >> 2, PG = 256 / CQ;
   const int cq = tid & (CQ - 1), pg = tid / CQ;
@@ -637,6 +642,10 @@ __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restr
     wq[k] = k < K ? *reinterpret_cast<const float4*>(w + k * C + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
   float4 sc, sh, mu, is;
   float s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  float4 wacc[HEAD_KMAX];
+  float waccb[HEAD_KMAX];
+#pragma unroll
+  for (int k = 0; k < HEAD_KMAX; ++k) { wacc[k] = make_float4(0.f, 0.f, 0.f, 0.f); waccb[k] = 0.f; }
   if (BNR) {
     sc = *reinterpret_cast<const float4*>(bn.coef + 4 * cq);
     sh = *reinterpret_cast<const float4*>(bn.coef + C + 4 * cq);
@@ -650,15 +659,22 @@ __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restr
     float4 zz;
     if (BNR) zz = *reinterpret_cast<const float4*>(bn.z + (size_t)p * C + 4 * cq);  // in flight with dy
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 av;
+    if (WG) av = pmu_bnrelu4(zz, sc, sh);
 #pragma unroll
     for (int k = 0; k < HEAD_KMAX; ++k) {
       if (k >= K) break;
       const size_t i = (size_t)(n * K + k) * HWu + pix;
       float g = dy[i];
       if (do_sigmoid) { const float sg = y[i]; g = g * (sg * (1.f - sg)); }
-      if (cq == 0) dl[i] = g;
+      if (!WG && cq == 0) dl[i] = g;
       o.x = fmaf(g, wq[k].x, o.x); o.y = fmaf(g, wq[k].y, o.y);
       o.z = fmaf(g, wq[k].z, o.z); o.w = fmaf(g, wq[k].w, o.w);
+      if (WG) {
+        wacc[k].x = fmaf(g, av.x, wacc[k].x); wacc[k].y = fmaf(g, av.y, wacc[k].y);
+        wacc[k].z = fmaf(g, av.z, wacc[k].z); wacc[k].w = fmaf(g, av.w, wacc[k].w);
+        waccb[k] += g;
+      }
     }
     *reinterpret_cast<float4*>(da + (size_t)p * C + 4 * cq) = o;
     if (BNR) {
@@ -693,6 +709,29 @@ __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restr
       float t = 0.f;
       for (int wv = 0; wv < 4; ++wv) t += red[(wv * 2 + r) * 256 + c];
       bn.part[(long long)blockIdx.x * 2 * C + o] = t;
+    }
+  }
+  if (WG) {  // as wgrad1x1_fast_kernel
+    const int CW = C + 1;
+#pragma unroll
+    for (int k = 0; k < HEAD_KMAX; ++k) {
+      if (k >= K) break;
+      float v[5] = {wacc[k].x, wacc[k].y, wacc[k].z, wacc[k].w, waccb[k]};
+#pragma unroll
+      for (int e = 0; e < 5; ++e)
+        for (int o = CQ; o < 64; o <<= 1) v[e] += __shfl_xor(v[e], o, 64);
+      if (lane < CQ) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) redw[(wave * HEAD_KMAX + k) * 260 + 4 * cq + e] = v[e];
+        if (cq == 0) redw[(wave * HEAD_KMAX + k) * 260 + C] = v[4];
+      }
+    }
+    __syncthreads();
+    for (int o = tid; o < K * CW; o += 256) {
+      const int k = o / CW, c = o - k * CW;
+      float t = 0.f;
+      for (int wv = 0; wv < 4; ++wv) t += redw[(wv * HEAD_KMAX + k) * 260 + c];
+      bn.ws[(long long)blockIdx.x * K * CW + o] = t;
     }
   }
 }
@@ -1149,7 +1188,7 @@ extern "C" int pmu_head1x1_bwd(const float* dy, const float* y, int do_sigmoid, 
   const long long P = (long long)N * H * W;
   const int CQ = C >> 2;
   if ((C & 3) == 0 && CQ <= 64 && (CQ & (CQ - 1)) == 0 && P < (1LL << 31)) {
-    const HeadBnr nob{nullptr, nullptr, nullptr, nullptr, nullptr};
+    const HeadBnr nob{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     hipLaunchKernelGGL(head_bwd_fast_kernel<false>, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0,
                        (hipStream_t)stream, dy, y, do_sigmoid, w, K, C, (long long)H * W, P, dl, da, nob);
     PMU_CHECK_LAUNCH();
@@ -1170,13 +1209,25 @@ extern "C" int pmu_head1x1_bwd_tiles(int N, int H, int W) { return (int)pmu_cdiv
 
 extern "C" int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
                                    int N, int H, int W, float* dl, float* da, const float* z, const float* coef,
-                                   const float* mean, const float* invstd, float* part, void* stream) {
-  PMU_REQUIRE(dy && w && dl && da && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y) && N > 0 && H > 0 &&
+                                   const float* mean, const float* invstd, float* part, float* dw, float* db,
+                                   float* ws, size_t ws_bytes, void* stream) {
+  PMU_REQUIRE(dy && w && da && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y) && N > 0 && H > 0 &&
               W > 0 && z && coef && mean && invstd && part && pmu_head1x1_bwd_bnr_ok(N, H, W, C));
+  PMU_REQUIRE(dw ? (ws != nullptr) : (dl != nullptr));
   const long long P = (long long)N * H * W;
-  const HeadBnr bn{z, coef, mean, invstd, part};
-  hipLaunchKernelGGL(head_bwd_fast_kernel<true>, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
-                     dy, y, do_sigmoid, w, K, C, (long long)H * W, P, dl, da, bn);
+  const int R = pmu_cdiv(P, HPPB);
+  const HeadBnr bn{z, coef, mean, invstd, part, ws};
+  if (dw) {  // the head's weight gradient from the same pass (pmu_wgrad1x1's dw, db; dl not written)
+    PMU_REQUIRE(ws_bytes >= (size_t)R * K * (C + 1) * sizeof(float));
+    hipLaunchKernelGGL((head_bwd_fast_kernel<true, true>), dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dy, y,
+                       do_sigmoid, w, K, C, (long long)H * W, P, dl, da, bn);
+    PMU_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rows_sum_split4_kernel, dim3((unsigned)pmu_cdiv(K * (C + 1), 64)), dim3(256), 0,
+                       (hipStream_t)stream, (const float*)ws, R, K, C, dw, db);
+  } else {
+    hipLaunchKernelGGL((head_bwd_fast_kernel<true, false>), dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dy, y,
+                       do_sigmoid, w, K, C, (long long)H * W, P, dl, da, bn);
+  }
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

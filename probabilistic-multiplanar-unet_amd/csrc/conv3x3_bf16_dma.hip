@@ -54,6 +54,7 @@ struct DmaArgs {
   const float* bias;
   float* out0;
   float* out1;
+  unsigned short* out1b;  // input gradient, nullable: a bf16 (RNE) copy of out1 (the convT's bf16 operand)
   float* part;
   int N, H, W, Cp, NOUT, split, tiles_w, tiles_h, nch, ncb;
   // input gradient only: the producer layer's BatchNorm+ReLU backward partial sums (see
@@ -272,9 +273,10 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       }
     }
   } else {
-    // the input gradient keeps per-output branches around its (optional, a.bz) z uses: the straight-line
-    // form above with the producer's BN-backward sums spilled 18-140 VGPRs in every arrangement tried
-    // (compile-time variant, masked sums, half rows, fm-outer order)
+    // Input gradient: all stores first, then (a.bz) the producer's BN-backward sums from the still-live
+    // accumulators and the z under them, a row at a time.  z loads interleaved with the stores made
+    // every consumption of a z value wait for all earlier stores (vmcnt counts both, in order); the
+    // straight-line masked form of the forward above spilled 18-140 VGPRs here.
   #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       s1[fn] = 0.f;
@@ -282,41 +284,53 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       const int jb = j0 + wn * 64 + fn * 32;
       const int j = jb + li;
       const bool jok = j < a.NOUT;
-      const bool bnr = a.bz && jok;
-      const float bsc = bnr ? a.bcoef[j] : 0.f, bsh = bnr ? a.bcoef[a.NOUT + j] : 0.f;
-      const float bmu = bnr ? a.bmean[j] : 0.f, bis = bnr ? a.binv[j] : 0.f;
       float* dstp;
       int ld;
+      unsigned short* dstb = nullptr;  // (uniform per fragment)
       if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
-      else { dstp = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
+      else {
+        dstp = a.out1 + (j - a.split);
+        ld = a.NOUT - a.split;
+        if (a.out1b) dstb = a.out1b + (j - a.split);
+      }
   #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
         const int h = h0 + 4 * wm + fm;
-        // the producer's z under this row's 16 outputs, loaded together before the stores (clamped
-        // addresses: every lane loads, no branch per load; unused values are ignored)
-        float zt[16];
-        if (a.bz) {
-          const int jc = min(j, a.NOUT - 1);
-          const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const long long zi = (row + min(w0 + acc_row(r, lane), a.W - 1)) * a.NOUT + jc;
-            zt[r] = ZB ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
-          }
-        }
   #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int w = w0 + acc_row(r, lane);
           if (!jok || h >= a.H || w >= a.W) continue;
           const long long pix = ((long long)n * a.H + h) * a.W + w;
           PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-          const float v = acc[fm][fn][r];
-          dstp[pix * ld] = v;
-          if (bnr) {
-            const float zz = zt[r];
-            const float gg = fmaf(zz, bsc, bsh) > 0.f ? v : 0.f;
+          dstp[pix * ld] = acc[fm][fn][r];
+          if (dstb) dstb[pix * ld] = bf16_bits(acc[fm][fn][r]);
+        }
+      }
+    }
+    if (a.bz) {
+  #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int j = j0 + wn * 64 + fn * 32 + li;
+        const bool jok = j < a.NOUT;
+        const int jc = jok ? j : a.NOUT - 1;
+        const float bsc = a.bcoef[jc], bsh = a.bcoef[a.NOUT + jc], bmu = a.bmean[jc], bis = a.binv[jc];
+  #pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int h = h0 + 4 * wm + fm;
+          const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
+          float zt[16];
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {  // clamped addresses: every lane loads, masked values ignored
+            const long long zi = (row + min(w0 + acc_row(r, lane), a.W - 1)) * a.NOUT + jc;
+            zt[r] = ZB ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
+          }
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int w = w0 + acc_row(r, lane);
+            const bool ok = jok && h < a.H && w < a.W;
+            const float gg = (ok && fmaf(zt[r], bsc, bsh) > 0.f) ? acc[fm][fn][r] : 0.f;
             s1[fn] += gg;
-            s2[fn] = fmaf(gg, (zz - bmu) * bis, s2[fn]);
+            s2[fn] = fmaf(gg, (zt[r] - bmu) * bis, s2[fn]);
           }
         }
       }
@@ -364,8 +378,10 @@ static Shape dma_shape(int NOUT, int KC) {
 static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, const unsigned short* wp, const float* bias,
                       int NOUT, float* out0, float* out1, int split, float* part, bool dgrad, void* stream,
                       const float* bz = nullptr, const float* bcoef = nullptr, const float* bmean = nullptr,
-                      const float* binv = nullptr, int zbf = 0, const float* zoff = nullptr) {
+                      const float* binv = nullptr, int zbf = 0, const float* zoff = nullptr,
+                      unsigned short* out1b = nullptr) {
   PMU_REQUIRE(x && wp && out0 && N > 0 && H > 0 && W >= 32 && Cp > 0 && Cp % BK == 0 && NOUT > 0);
+  PMU_REQUIRE(!out1b || (dgrad && out1));
   PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && out1));
   const Shape sh = dma_shape(NOUT, Cp);
   const long long img_bytes = (long long)H * W * Cp * 2;
@@ -381,11 +397,11 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
                                    : bz + px * NOUT;
       return launch_dma(x + px * Cp, Cp, nn, H, W, wp, bias, NOUT, o0, out1 ? out1 + px * (NOUT - split) : nullptr,
                         split, part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream, bzc, bcoef,
-                        bmean, binv, zbf, zoff);
+                        bmean, binv, zbf, zoff, out1b ? out1b + px * (NOUT - split) : nullptr);
     });
   }
   DmaArgs a;
-  a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.part = part;
+  a.x = x; a.wp = wp; a.bias = bias; a.out0 = out0; a.out1 = out1; a.out1b = out1b; a.part = part;
   a.N = N; a.H = H; a.W = W; a.Cp = Cp; a.NOUT = NOUT; a.split = dgrad ? split : NOUT;
   a.nch = Cp / BK;
   a.bz = bz; a.bcoef = bcoef; a.bmean = bmean; a.binv = binv;
@@ -449,6 +465,16 @@ extern "C" int pmu_conv3x3_fwd_dma(const unsigned short* xt, int Cp, int N, int 
 extern "C" int pmu_conv3x3_dgrad_dma(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                                      int Cin, int Csplit, float* dx0, float* dx1, void* stream) {
   return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
+}
+
+// The concat split input gradient with a bf16 copy of its second part (the transposed conv's bf16
+// input gradient operand, which pmu_frame_to_bf16 would otherwise make from dx1 in another pass).
+extern "C" int pmu_conv3x3_dgrad_dma_x1b(const unsigned short* dzt, int Cp, int N, int H, int W,
+                                         const unsigned short* wp, int Cin, int Csplit, float* dx0, float* dx1,
+                                         unsigned short* dx1b, void* stream) {
+  PMU_REQUIRE(dx1 && dx1b && Csplit < Cin && (Cin - Csplit) % 8 == 0);
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream, nullptr, nullptr,
+                    nullptr, nullptr, 0, nullptr, dx1b);
 }
 
 // As pmu_conv3x3_dgrad_wino4_bnr (part rows = pmu_conv3x3_tiles_dma(N, H, W, Cin, Cp)).

@@ -663,7 +663,10 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
         }
     } else {
       const int ab = col / p.Cout, co = col - ab * p.Cout;
-      const float b = p.bias ? p.bias[co] : 0.f;
+      float b = p.bias ? p.bias[co] : 0.f;
+      // consumed here, unconditionally: first consumed inside the per-output store branches (the compiler
+      // sinks the add into them), the bias made each branch wait vmcnt(0), i.e. for every earlier store
+      asm volatile("" : "+v"(b));
       const unsigned Wu = (unsigned)p.W, Hu = (unsigned)p.H;  // 32-bit decode (M < 2^31, host-checked)
       float* outc = p.out + (long long)(ab >> 1) * 2 * p.W * p.Cout + (ab & 1) * p.Cout + co;
       const bool full = m0 + PM <= p.M;
@@ -674,10 +677,13 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
           for (int r = 0; r < 16; ++r) {
             const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
             if (EXP == 1 && acc[fm][fn][r] != -1.2345f) continue;
+            // the bias added outside the store's branch: first consumed inside it, it made the
+            // compiler wait vmcnt(0) — for every earlier store — in each branch
+            const float v = acc[fm][fn][r] + b;
             if (full || m < (unsigned)p.M) {
               const unsigned j = m & (Wu - 1), t = m >> p.lw;
               const unsigned i = t & (Hu - 1), n = t >> p.lh;
-              outc[(size_t)(((n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j)) * (unsigned)p.Cout] = acc[fm][fn][r] + b;
+              outc[(size_t)(((n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j)) * (unsigned)p.Cout] = v;
             }
           }
       } else {
@@ -686,10 +692,11 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const unsigned m = (unsigned)(m0 + wm * 64 + fm * 32 + acc_row(r, lane));
+            const float v = acc[fm][fn][r] + b;
             if (m < (unsigned)p.M) {
               const unsigned t = m / Wu, j = m - t * Wu;
               const unsigned n = t / Hu, i = t - n * Hu;
-              outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * p.Cout] = acc[fm][fn][r] + b;
+              outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * p.Cout] = v;
             }
           }
       }

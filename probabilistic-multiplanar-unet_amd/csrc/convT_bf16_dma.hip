@@ -201,7 +201,10 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
         }
     } else {
       const int ab = col / g.Cout, co = col - ab * g.Cout;
-      const float b = g.bias ? g.bias[co] : 0.f;
+      float b = g.bias ? g.bias[co] : 0.f;
+      // consumed here, unconditionally (see convT.hip: first consumed inside the per-output store
+      // branches, the bias cost a vmcnt(0) — a wait for every earlier store — per store)
+      asm volatile("" : "+v"(b));
       float* outc = g.out + (long long)(ab >> 1) * 2 * g.W * g.Cout + (ab & 1) * g.Cout + co;
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm)

@@ -147,7 +147,8 @@ SIGNATURES = {
     "pmu_head1x1_bwd_bnr_ok": (c_int, [c_int, c_int, c_int, c_int]),
     "pmu_head1x1_bwd_tiles": (c_int, [c_int, c_int, c_int]),
     "pmu_head1x1_bwd_bnr": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
-                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_wgrad1x1_ws": (c_size_t, [c_int, c_int, c_int]),
     "pmu_wgrad1x1": (c_int, [c_void_p, _FP, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_sgd_clip": (c_int, [c_void_p, c_int, c_void_p, c_float, c_float, c_float, c_float, c_void_p]),
@@ -187,6 +188,8 @@ SIGNATURES = {
                                     c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                       c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_x1b": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                          c_void_p, c_void_p, c_void_p]),
     "pmu_convT2x2_dma_ok": (c_int, [c_int, c_int, c_int]),
     "pmu_convT2x2_packed_size_dma": (c_size_t, [c_int, c_int]),
     "pmu_convT2x2_pack_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -517,6 +517,13 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
                 _bnr_call("pmu_conv3x3_dgrad_dma_bnr_zb" if prod.z.dtype == BF16S else "pmu_conv3x3_dgrad_dma_bnr",
                           prod, L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3]),
                           (dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin), dx0, s)
+            elif dx1 is not None and (Cin - sp) % 8 == 0:
+                # the up-sampled part's gradient also in bf16: the transposed conv's operand, kept on the
+                # fp32 tensor (unet_backward uses it instead of a pmu_frame_to_bf16 pass over dx1)
+                dx1b = torch.empty(N, H, W, Cin - sp, dtype=BF16S, device=dev)
+                L.call("pmu_conv3x3_dgrad_dma_x1b", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
+                       dx0.data_ptr(), dx1.data_ptr(), dx1b.data_ptr(), s)
+                dx1._pmu_bf16 = dx1b
             else:
                 L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
                        dx0.data_ptr(), L.ptr(dx1), s)
@@ -859,23 +866,25 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         dl = _empty(N, K, H, W, device=dev)
         da = _empty(N, H, W, C, device=dev)
         lb = L.lib()
+        dwo = grads.new(net.outc.conv.weight)
+        dbo = grads.new(net.outc.conv.bias) if net.outc.conv.bias is not None else _empty(K, device=dev)
+        wsb = lb.pmu_wgrad1x1_ws(N * H * W, K, C)
+        ws = _empty(max(1, (wsb + 3) // 4), device=dev)
         if last.z.dtype == F32 and last.bn.mean is not None and lb.pmu_head1x1_bwd_bnr_ok(N, H, W, C):
-            # the head's input gradient also forms the last layer's BN-backward partial sums
+            # one pass over z: the head's input gradient, its weight / bias gradient and the last
+            # layer's BN-backward partial sums
             R = lb.pmu_head1x1_bwd_tiles(N, H, W)
             part = _empty(R, 2 * C, device=dev)
             L.call("pmu_head1x1_bwd_bnr", dyc.data_ptr(), st.y.data_ptr(), int(net.n_classes == 1),
-                   net.outc.conv.weight.data_ptr(), K, C, N, H, W, dl.data_ptr(), da.data_ptr(), last.z.data_ptr(),
-                   last.bn.coef.data_ptr(), last.bn.mean.data_ptr(), last.bn.invstd.data_ptr(), part.data_ptr(), s)
+                   net.outc.conv.weight.data_ptr(), K, C, N, H, W, None, da.data_ptr(), last.z.data_ptr(),
+                   last.bn.coef.data_ptr(), last.bn.mean.data_ptr(), last.bn.invstd.data_ptr(), part.data_ptr(),
+                   dwo.data_ptr(), dbo.data_ptr(), ws.data_ptr(), wsb, s)
             last.bnr = (da, part, R)
         else:
             L.call("pmu_head1x1_bwd", dyc.data_ptr(), st.y.data_ptr(), int(net.n_classes == 1),
                    net.outc.conv.weight.data_ptr(), K, C, N, H, W, dl.data_ptr(), da.data_ptr(), s)
-        dwo = grads.new(net.outc.conv.weight)
-        dbo = grads.new(net.outc.conv.bias) if net.outc.conv.bias is not None else _empty(K, device=dev)
-        wsb = L.lib().pmu_wgrad1x1_ws(N * H * W, K, C)
-        ws = _empty(max(1, (wsb + 3) // 4), device=dev)
-        L.call("pmu_wgrad1x1", dl.data_ptr(), frame_of([last.act()], N, H, W), K, dwo.data_ptr(), dbo.data_ptr(),
-               ws.data_ptr(), wsb, s)
+            L.call("pmu_wgrad1x1", dl.data_ptr(), frame_of([last.act()], N, H, W), K, dwo.data_ptr(), dbo.data_ptr(),
+                   ws.data_ptr(), wsb, s)
         grads.flush()
     else:
         da = dy.permute(0, 2, 3, 1).contiguous()   # NCHW-shaped channels-last view -> NHWC
@@ -899,7 +908,10 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         Hd, Wd = dup.shape[1], dup.shape[2]
         Cup = convT.out_channels
         dx = _empty(N, hi, wi, Cin_t, device=dev)
-        dut = frame_to_bf16([Src(dup)], N, Hd, Wd) if us.bf16 else None
+        dut = None
+        if us.bf16:   # the concat dgrad's bf16 copy of dup when it wrote one (pmu_conv3x3_dgrad_dma_x1b)
+            dut = getattr(dup, "_pmu_bf16", None)
+            dut = dut if dut is not None else frame_to_bf16([Src(dup)], N, Hd, Wd)
         if us.bf16 and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 1):
             wpt = pack_convT_weights_dma(convT.weight, dgrad=True)
             L.call("pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd, Wd, us.off[0], us.off[1], wpt.data_ptr(),

@@ -92,6 +92,31 @@ def test_dgrad_bnr_dma(dev, N, H, W, Cin, Cout):
     _check(dx, part, z, coef, mean, invstd, dev)
 
 
+@pytest.mark.parametrize("N,H,W,Cskip,Cup,Cout", [(2, 64, 64, 64, 64, 64), (1, 33, 45, 128, 64, 96)])
+def test_dgrad_dma_split_bf16_copy(dev, N, H, W, Cskip, Cup, Cout):
+    """pmu_conv3x3_dgrad_dma_x1b: dx0 / dx1 bit-equal to pmu_conv3x3_dgrad_dma with the same split, and
+    dx1b the bf16 (RNE) rounding of dx1 — what pmu_frame_to_bf16 makes of it (unet_parts.py:52,66)."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_to_bf16, pack_weights_dma
+    g = torch.Generator().manual_seed(23 + H + Cskip)
+    Cin = Cskip + Cup
+    dz = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    dzt = frame_to_bf16([Src(dz)], N, H, W)
+    wp = pack_weights_dma(w, True)
+    dx0, dx1 = torch.empty(N, H, W, Cskip, device=dev), torch.empty(N, H, W, Cup, device=dev)
+    dx1b = torch.empty(N, H, W, Cup, dtype=torch.int16, device=dev)
+    L.call("pmu_conv3x3_dgrad_dma_x1b", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, Cskip,
+           dx0.data_ptr(), dx1.data_ptr(), dx1b.data_ptr(), L.stream())
+    r0, r1 = torch.empty_like(dx0), torch.empty_like(dx1)
+    L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, Cskip, r0.data_ptr(),
+           r1.data_ptr(), L.stream())
+    ref_b = frame_to_bf16([Src(r1)], N, H, W)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, r0) and torch.equal(dx1, r1)
+    assert torch.equal(dx1b, ref_b)
+
+
 @pytest.mark.parametrize("N,H,W,C", [(2, 64, 64, 64), (1, 33, 45, 32), (2, 16, 16, 512), (1, 7, 9, 1040)])
 def test_maxpool2_bwd_bnr(dev, N, H, W, C):
     """pmu_maxpool2_bwd_bnr: dx bit-equal to pmu_maxpool2_bwd accumulated onto the same skip gradient
@@ -122,24 +147,41 @@ def test_maxpool2_bwd_bnr(dev, N, H, W, C):
 
 
 @pytest.mark.parametrize("N,H,W,C,K,sig", [(2, 64, 64, 64, 1, 1), (3, 37, 45, 32, 3, 0), (1, 16, 16, 256, 2, 0)])
-def test_head1x1_bwd_bnr(dev, N, H, W, C, K, sig):
-    """pmu_head1x1_bwd_bnr: dl and da bit-equal to pmu_head1x1_bwd, and the partials of da."""
+@pytest.mark.parametrize("fused_wgrad", [False, True])
+def test_head1x1_bwd_bnr(dev, N, H, W, C, K, sig, fused_wgrad):
+    """pmu_head1x1_bwd_bnr: da (and dl) bit-equal to pmu_head1x1_bwd, the BN-backward partials of da,
+    and (fused_wgrad) the head's dw / db bit-equal to pmu_wgrad1x1 on the BN+ReLU activation of z."""
     from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_of
     g = torch.Generator().manual_seed(41 + H + C)
     z, coef, mean, invstd = _bn_inputs(N, H, W, C, g, dev)
     dy = torch.randn(N, K, H, W, generator=g).to(dev)
     y = torch.rand(N, K, H, W, generator=g).to(dev)
     w = (torch.randn(K, C, generator=g) * 0.1).to(dev)
-    assert L.lib().pmu_head1x1_bwd_bnr_ok(N, H, W, C)
-    R = L.lib().pmu_head1x1_bwd_tiles(N, H, W)
+    lb = L.lib()
+    assert lb.pmu_head1x1_bwd_bnr_ok(N, H, W, C)
+    R = lb.pmu_head1x1_bwd_tiles(N, H, W)
     part = torch.full((R, 2 * C), float("nan"), device=dev)
     dl, da = torch.empty(N, K, H, W, device=dev), torch.empty(N, H, W, C, device=dev)
-    L.call("pmu_head1x1_bwd_bnr", dy.data_ptr(), y.data_ptr(), sig, w.data_ptr(), K, C, N, H, W, dl.data_ptr(),
-           da.data_ptr(), z.data_ptr(), coef.data_ptr(), mean.data_ptr(), invstd.data_ptr(), part.data_ptr(),
-           L.stream())
+    wsb = lb.pmu_wgrad1x1_ws(N * H * W, K, C)
+    ws = torch.empty(wsb // 4 + 1, device=dev)
+    dw, db = torch.full((K, C), float("nan"), device=dev), torch.full((K,), float("nan"), device=dev)
+    L.call("pmu_head1x1_bwd_bnr", dy.data_ptr(), y.data_ptr(), sig, w.data_ptr(), K, C, N, H, W,
+           None if fused_wgrad else dl.data_ptr(), da.data_ptr(), z.data_ptr(), coef.data_ptr(), mean.data_ptr(),
+           invstd.data_ptr(), part.data_ptr(), dw.data_ptr() if fused_wgrad else None,
+           db.data_ptr() if fused_wgrad else None, ws.data_ptr(), wsb, L.stream())
     dl2, da2 = torch.empty_like(dl), torch.empty_like(da)
     L.call("pmu_head1x1_bwd", dy.data_ptr(), y.data_ptr(), sig, w.data_ptr(), K, C, N, H, W, dl2.data_ptr(),
            da2.data_ptr(), L.stream())
     torch.cuda.synchronize()
-    assert torch.equal(dl, dl2) and torch.equal(da, da2)
+    assert torch.equal(da, da2)
+    if fused_wgrad:
+        dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
+        ws2 = torch.empty_like(ws)
+        L.call("pmu_wgrad1x1", dl2.data_ptr(), frame_of([Src(z, L.SRC_BNRELU, coef)], N, H, W), K, dw2.data_ptr(),
+               db2.data_ptr(), ws2.data_ptr(), wsb, L.stream())
+        torch.cuda.synchronize()
+        assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    else:
+        assert torch.equal(dl, dl2)
     _check(da, part, z, coef, mean, invstd, dev)
