@@ -736,6 +736,118 @@ __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restr
   }
 }
 
+// The fused head backward (BNR + WG of head_bwd_fast_kernel) with KT classes and the sigmoid as
+// compile-time constants and the pixel loop in batches of 4: every load of a batch (z, dy, y; clamped
+// addresses, out-of-range pixels masked to 0) is issued before its da stores.  One pixel per
+// iteration made each iteration's loads wait for the previous iteration's store (vmcnt counts loads
+// and stores in order): 2.2 TB/s.  Same per-thread summation order as head_bwd_fast_kernel /
+// wgrad1x1_fast_kernel (masked terms add exact zeros), so the results are bit-identical.
+template <int KT, bool SIG>
+__global__ __launch_bounds__(256) void head_bwd_fused_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                             const float* __restrict__ w, int C, long long HW,
+                                                             long long P, float* __restrict__ da, HeadBnr bn) {
+  constexpr int B = 4;
+  __shared__ float red[4 * 2 * 256];
+  __shared__ float redw[4 * KT * 260];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int CQ = C >> 2, PG = 256 / CQ;
+  const int cq = tid & (CQ - 1), pg = tid / CQ;
+  float4 wq[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) wq[k] = *reinterpret_cast<const float4*>(w + k * C + 4 * cq);
+  const float4 sc = *reinterpret_cast<const float4*>(bn.coef + 4 * cq);
+  const float4 sh = *reinterpret_cast<const float4*>(bn.coef + C + 4 * cq);
+  const float4 mu = *reinterpret_cast<const float4*>(bn.mean + 4 * cq);
+  const float4 is = *reinterpret_cast<const float4*>(bn.invstd + 4 * cq);
+  const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+  const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+  float s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  float4 wacc[KT];
+  float waccb[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) { wacc[k] = make_float4(0.f, 0.f, 0.f, 0.f); waccb[k] = 0.f; }
+  const unsigned HWu = (unsigned)HW, pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
+  for (unsigned p0 = blockIdx.x * HPPB + pg; p0 < pend; p0 += B * PG) {
+    float4 zz[B];
+    float g[B][KT];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const unsigned p = min(p0 + b * PG, pend - 1);
+      const unsigned n = p / HWu, pix = p - n * HWu;
+      zz[b] = *reinterpret_cast<const float4*>(bn.z + (size_t)p * C + 4 * cq);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        const size_t i = (size_t)(n * KT + k) * HWu + pix;
+        g[b][k] = dy[i];
+        if (SIG) { const float sg = y[i]; g[b][k] = g[b][k] * (sg * (1.f - sg)); }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const unsigned p = p0 + b * PG;
+      const bool ok = p < pend;
+      const float4 av = pmu_bnrelu4(zz[b], sc, sh);
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        const float gk = ok ? g[b][k] : 0.f;
+        o.x = fmaf(gk, wq[k].x, o.x); o.y = fmaf(gk, wq[k].y, o.y);
+        o.z = fmaf(gk, wq[k].z, o.z); o.w = fmaf(gk, wq[k].w, o.w);
+        wacc[k].x = fmaf(gk, av.x, wacc[k].x); wacc[k].y = fmaf(gk, av.y, wacc[k].y);
+        wacc[k].z = fmaf(gk, av.z, wacc[k].z); wacc[k].w = fmaf(gk, av.w, wacc[k].w);
+        waccb[k] += gk;
+      }
+      const float ov[4] = {o.x, o.y, o.z, o.w}, zv[4] = {zz[b].x, zz[b].y, zz[b].z, zz[b].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float gg = fmaf(zv[e], scv[e], shv[e]) > 0.f ? ov[e] : 0.f;
+        s1[e] += gg;
+        s2[e] = fmaf(gg, (zv[e] - muv[e]) * isv[e], s2[e]);
+      }
+      if (ok) *reinterpret_cast<float4*>(da + (size_t)p * C + 4 * cq) = o;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    for (int o = CQ; o < 64; o <<= 1) {
+      s1[e] += __shfl_xor(s1[e], o, 64);
+      s2[e] += __shfl_xor(s2[e], o, 64);
+    }
+  if (lane < CQ) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[(wave * 2 + 0) * 256 + 4 * cq + e] = s1[e];
+      red[(wave * 2 + 1) * 256 + 4 * cq + e] = s2[e];
+    }
+  }
+  const int CW = C + 1;
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    float v[5] = {wacc[k].x, wacc[k].y, wacc[k].z, wacc[k].w, waccb[k]};
+#pragma unroll
+    for (int e = 0; e < 5; ++e)
+      for (int o = CQ; o < 64; o <<= 1) v[e] += __shfl_xor(v[e], o, 64);
+    if (lane < CQ) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) redw[(wave * KT + k) * 260 + 4 * cq + e] = v[e];
+      if (cq == 0) redw[(wave * KT + k) * 260 + C] = v[4];
+    }
+  }
+  __syncthreads();
+  for (int o = tid; o < 2 * C; o += 256) {
+    const int r = o / C, c = o - r * C;
+    float t = 0.f;
+    for (int wv = 0; wv < 4; ++wv) t += red[(wv * 2 + r) * 256 + c];
+    bn.part[(long long)blockIdx.x * 2 * C + o] = t;
+  }
+  for (int o = tid; o < KT * CW; o += 256) {
+    const int k = o / CW, c = o - k * CW;
+    float t = 0.f;
+    for (int wv = 0; wv < 4; ++wv) t += redw[(wv * KT + k) * 260 + c];
+    bn.ws[(long long)blockIdx.x * KT * CW + o] = t;
+  }
+}
+
 // dw[k][c] / db[k] partials per block: ws[block][k][C+1]; shuffles over the wave's pixel groups,
 // LDS over the 4 waves (fixed order)
 __global__ __launch_bounds__(256) void wgrad1x1_fast_kernel(const float* __restrict__ dl, DevFrame f, int K,
@@ -1219,8 +1331,21 @@ extern "C" int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmo
   const HeadBnr bn{z, coef, mean, invstd, part, ws};
   if (dw) {  // the head's weight gradient from the same pass (pmu_wgrad1x1's dw, db; dl not written)
     PMU_REQUIRE(ws_bytes >= (size_t)R * K * (C + 1) * sizeof(float));
-    hipLaunchKernelGGL((head_bwd_fast_kernel<true, true>), dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dy, y,
-                       do_sigmoid, w, K, C, (long long)H * W, P, dl, da, bn);
+    hipStream_t st = (hipStream_t)stream;
+    const long long HW = (long long)H * W;
+#define PMU_HEAD_FUSED(KV)                                                                                   \
+  case KV:                                                                                                  \
+    if (do_sigmoid) hipLaunchKernelGGL((head_bwd_fused_kernel<KV, true>), dim3((unsigned)R), dim3(256), 0, st,  \
+                                       dy, y, w, C, HW, P, da, bn);                                         \
+    else hipLaunchKernelGGL((head_bwd_fused_kernel<KV, false>), dim3((unsigned)R), dim3(256), 0, st, dy, y, w, \
+                            C, HW, P, da, bn);                                                              \
+    break;
+    switch (K) {
+      PMU_HEAD_FUSED(1) PMU_HEAD_FUSED(2) PMU_HEAD_FUSED(3) PMU_HEAD_FUSED(4)
+      PMU_HEAD_FUSED(5) PMU_HEAD_FUSED(6) PMU_HEAD_FUSED(7) PMU_HEAD_FUSED(8)
+      default: return PMU_ERR_ARG;
+    }
+#undef PMU_HEAD_FUSED
     PMU_CHECK_LAUNCH();
     hipLaunchKernelGGL(rows_sum_split4_kernel, dim3((unsigned)pmu_cdiv(K * (C + 1), 64)), dim3(256), 0,
                        (hipStream_t)stream, (const float*)ws, R, K, C, dw, db);
