@@ -459,7 +459,9 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
 // BNR (input gradient only): the producer's BN-backward partial sums in the epilogue (a.bz set) — a
 // compile-time choice, so the z loads and their uses sit in straight-line code
 template <bool DGRAD, bool BNR, int CO_>
-__global__ __launch_bounds__(16 * CO_, 1) void conv3x3_wino2h_kernel(W2Args a) {
+// 64 channels: 1024 threads = four waves per SIMD (<= 128 VGPRs implied); 32 channels: 512 threads,
+// capped at 128 VGPRs (four waves per SIMD) so two workgroups share a CU (at 132 VGPRs only one fit)
+__global__ __launch_bounds__(16 * CO_, CO_ == 32 ? 4 : 1) void conv3x3_wino2h_kernel(W2Args a) {
   using C = W2Cfg<CO_>;
   constexpr int NT = C::NT, NGL = C::NGL, STAGE = C::STAGE;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + C::RED_FLOATS];

@@ -12,8 +12,11 @@ from ctypes import POINTER, c_double, c_float, c_int, c_longlong, c_size_t, c_vo
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-# PMU_LIB=debug selects the bounds-checked debug build (csrc: make DEBUG=1; see pmu_debug_read)
-LIB_NAME = "libpmunet_hip_debug.so" if os.environ.get("PMU_LIB") == "debug" else "libpmunet_hip.so"
+# PMU_LIB=debug selects the bounds-checked debug build (csrc: make DEBUG=1; see pmu_debug_read);
+# PMU_LIB=exp a kernel-variant A/B build (csrc: make EXPERIMENTS=1 BLD=build_exp
+# OUT=../pmu_hip/libpmunet_hip_exp.so; not shipped, tools/ and scripts/ only)
+LIB_NAME = {"debug": "libpmunet_hip_debug.so", "exp": "libpmunet_hip_exp.so"}.get(os.environ.get("PMU_LIB", ""),
+                                                                                  "libpmunet_hip.so")
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 HEADER_PATH = os.path.normpath(
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "include", "pmunet_hip.h"))
