@@ -241,6 +241,11 @@ int pmu_conv3x3_dgrad_dma_bnr_zb(const unsigned short* dzt, int Cp, int N, int H
 int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* out, void* stream);
 /* out[N][H][W][C] = the frame's fp32 operand values (e.g. MaxPool2d of BN+ReLU, unet_parts.py:33). */
 int pmu_frame_to_f32(const pmu_frame* f, float* out, void* stream);
+/* the frame into the first channels of a wider NHWC tensor (output pixel stride ldo elements): the
+ * skip half of an Up block's concat operand, whose other half pmu_convT2x2_fwd_ld /
+ * pmu_convT2x2_fwd_dma_ldb write in place (unet_parts.py:66).  Channel counts of 4 (fp32) / 8 (bf16). */
+int pmu_frame_to_f32_ld(const pmu_frame* f, float* out, int ldo, void* stream);
+int pmu_frame_to_bf16_ld(const pmu_frame* f, int Cpad, unsigned short* out, int ldo, void* stream);
 /* dw[Cout][Cin][3][3] from dzt [N][H][W][pad8(Cout)] and xt [N][H][W][pad8(Cin)] (bf16, pad8(c) =
  * c rounded up to a multiple of 8); ws must hold pmu_conv3x3_wgrad_ws_bf16() bytes. */
 size_t pmu_conv3x3_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);
@@ -268,6 +273,10 @@ size_t pmu_convT2x2_packed_size_dma(int Cin, int Cout);
 int pmu_convT2x2_pack_dma(const float* w, int Cin, int Cout, int dgrad, unsigned short* wp, void* stream);
 int pmu_convT2x2_fwd_dma(const unsigned short* xt, int Cip, int N, int H, int W, const unsigned short* wp,
                          const float* bias, int Cin, int Cout, float* u, void* stream);
+/* the same written as bf16 into channels [0, Cout) of a wider NHWC bf16 tensor (pixel stride ldo):
+ * the up-sampled half of the Up block's bf16 concat operand — no fp32 u (unet_parts.py:52,66) */
+int pmu_convT2x2_fwd_dma_ldb(const unsigned short* xt, int Cip, int N, int H, int W, const unsigned short* wp,
+                             const float* bias, int Cin, int Cout, unsigned short* ub, int ldo, void* stream);
 int pmu_convT2x2_dgrad_dma(const unsigned short* dut, int Cop, int Hd, int Wd, int off_h, int off_w,
                            const unsigned short* wp, int N, int H, int W, int Cin, int Cout, float* dx,
                            void* stream);
@@ -342,6 +351,11 @@ int pmu_convT2x2_pack(const float* w, int Cin, int Cout, int dgrad, float* wp, v
  * forward weights; used when the frame is one unpooled BN+ReLU source and Cin%16 == Cout%32 == 0. */
 int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout,
                      float* u, void* stream);
+/* the same into channels [0, Cout) of a wider NHWC tensor (pixel stride ldo floats), the up-sampled
+ * half of the Up block's fp32 concat operand; pipelined path only (wp given, pmu_convT2x2_fwd_ld_ok) */
+int pmu_convT2x2_fwd_ld_ok(const pmu_frame* in, int Cout);
+int pmu_convT2x2_fwd_ld(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout,
+                        float* u, int ldo, void* stream);
 /* dx[N][H][W][Cin] from du (NHWC [N][Hd][Wd][Cout], convT output placed at (off_h,off_w)). */
 int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, int off_w, const float* w,
                        const float* wp, int N, int H, int W, int Cin, int Cout, float* dx, void* stream);

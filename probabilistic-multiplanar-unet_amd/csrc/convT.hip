@@ -505,6 +505,7 @@ struct PipeArgs {
   int Hd, Wd, off_h, off_w;
   int lw, lh;          // fwd: log2 W, log2 H when powers of two, else -1
   int nnb, xcd;        // column blocks; 1: 1-D XCD-ordered grid, column blocks fastest
+  int ldo;             // fwd: output pixel stride (floats; Cout, or the concat operand's width)
 };
 
 template <int OFF>
@@ -668,7 +669,8 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
       // sinks the add into them), the bias made each branch wait vmcnt(0), i.e. for every earlier store
       asm volatile("" : "+v"(b));
       const unsigned Wu = (unsigned)p.W, Hu = (unsigned)p.H;  // 32-bit decode (M < 2^31, host-checked)
-      float* outc = p.out + (long long)(ab >> 1) * 2 * p.W * p.Cout + (ab & 1) * p.Cout + co;
+      const int ldo = p.ldo;
+      float* outc = p.out + (long long)(ab >> 1) * 2 * p.W * ldo + (ab & 1) * ldo + co;
       const bool full = m0 + PM <= p.M;
       if (p.lw >= 0 && p.lh >= 0) {  // power-of-two H, W: shift/mask decode
 #pragma unroll
@@ -683,7 +685,7 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
             if (full || m < (unsigned)p.M) {
               const unsigned j = m & (Wu - 1), t = m >> p.lw;
               const unsigned i = t & (Hu - 1), n = t >> p.lh;
-              outc[(size_t)(((n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j)) * (unsigned)p.Cout] = v;
+              outc[(size_t)(((n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j)) * (unsigned)ldo] = v;
             }
           }
       } else {
@@ -696,7 +698,7 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
             if (m < (unsigned)p.M) {
               const unsigned t = m / Wu, j = m - t * Wu;
               const unsigned n = t / Hu, i = t - n * Hu;
-              outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * p.Cout] = v;
+              outc[((long long)(n * 2 * Hu + 2 * i) * (2 * Wu) + 2 * j) * ldo] = v;
             }
           }
       }
@@ -774,19 +776,19 @@ extern "C" int pmu_convT2x2_pack(const float* w, int Cin, int Cout, int dgrad, f
   return PMU_OK;
 }
 
-extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout,
-                                float* u, void* stream) {
-  PMU_REQUIRE(valid_frame(in) && w && u && Cout > 0);
+static int convT_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout, float* u,
+                     int ldo, void* stream) {
+  PMU_REQUIRE(valid_frame(in) && w && u && Cout > 0 && ldo >= Cout);
   const long long M = (long long)in->N * in->H * in->W;
   if (wp && pipe_ok_fwd(in, Cout) && M < (1LL << 31)) {
     PipeArgs p{};
     p.a = in->src[0].x; p.coef = in->src[0].coef; p.bp = wp; p.bias = bias; p.out = u;
     p.M = M; p.Ncols = 4 * Cout; p.K = in->src[0].C;
-    p.H = in->H; p.W = in->W; p.Cin = in->src[0].C; p.Cout = Cout;
+    p.H = in->H; p.W = in->W; p.Cin = in->src[0].C; p.Cout = Cout; p.ldo = ldo;
     auto log2_or = [](int v) { return (v & (v - 1)) == 0 ? __builtin_ctz((unsigned)v) : -1; };
     p.lw = log2_or(in->W); p.lh = log2_or(in->H);
     // the output index (((n*2H + 2i)*2W + 2j)*Cout + co) stays 32-bit in the shift path
-    if (4LL * M * Cout >= (1LL << 32)) p.lw = -1;
+    if (4LL * M * ldo >= (1LL << 32)) p.lw = -1;
     pipe_grid(p, p.Ncols / PN);
     const dim3 grid = p.xcd ? dim3((unsigned)(pmu_cdiv(M, PM) * p.nnb)) : dim3((unsigned)pmu_cdiv(M, PM), (unsigned)p.nnb);
 #ifdef PMU_EXPERIMENTS
@@ -803,6 +805,7 @@ extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }
+  PMU_REQUIRE(ldo == Cout);  // (the strided output is the pipelined kernel's)
   ActRowA al{make_dev_frame(in), PixDecode{in->H, in->W}};
   const int Cin = al.f.C;
   WKN_B bl{w, 4 * Cout};
@@ -814,6 +817,23 @@ extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float
                      N, (long long)Cin, (int)nch);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
+}
+
+extern "C" int pmu_convT2x2_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout,
+                                float* u, void* stream) {
+  return convT_fwd(in, w, wp, bias, Cout, u, Cout, stream);
+}
+
+// The transposed conv written straight into channels [0, Cout) of a wider NHWC tensor whose pixels are
+// ldo floats apart: the up-sampled half of the Up block's concat operand (unet_parts.py:52,66), so
+// the operand materialisation copies only the skip half.  Pipelined path only (wp, pmu_convT2x2_fwd_ld_ok).
+extern "C" int pmu_convT2x2_fwd_ld_ok(const pmu_frame* in, int Cout) {
+  return valid_frame(in) && pipe_ok_fwd(in, Cout) && (long long)in->N * in->H * in->W < (1LL << 31);
+}
+extern "C" int pmu_convT2x2_fwd_ld(const pmu_frame* in, const float* w, const float* wp, const float* bias, int Cout,
+                                   float* u, int ldo, void* stream) {
+  PMU_REQUIRE(wp && pmu_convT2x2_fwd_ld_ok(in, Cout));
+  return convT_fwd(in, w, wp, bias, Cout, u, ldo, stream);
 }
 
 extern "C" int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, int off_w, const float* w,

@@ -34,6 +34,8 @@ struct GArgs {
   int M, Ncols, K, lda;
   int H, W, Cout, Hd, Wd, oh, ow;
   int nnb;
+  int ldo;                    // fwd: output pixel stride (Cout, or the concat operand's width)
+  unsigned short* outb;       // fwd, nullable: write bf16(u) here (pixel stride ldo) instead of out
 };
 
 template <int WN>
@@ -205,7 +207,10 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
       // consumed here, unconditionally (see convT.hip: first consumed inside the per-output store
       // branches, the bias cost a vmcnt(0) — a wait for every earlier store — per store)
       asm volatile("" : "+v"(b));
-      float* outc = g.out + (long long)(ab >> 1) * 2 * g.W * g.Cout + (ab & 1) * g.Cout + co;
+      const int ldo = g.ldo;
+      const long long cbase = (long long)(ab >> 1) * 2 * g.W * ldo + (ab & 1) * ldo + co;
+      float* outc = g.out + cbase;
+      unsigned short* outcb = g.outb + cbase;
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
@@ -214,7 +219,9 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
           if (m < g.M) {
             const unsigned t = (unsigned)m / (unsigned)g.W, j = (unsigned)m - t * (unsigned)g.W;
             const unsigned n = t / (unsigned)g.H, i = t - n * (unsigned)g.H;
-            outc[((long long)(n * 2 * g.H + 2 * i) * (2 * g.W) + 2 * j) * g.Cout] = acc[fm][fn][r] + b;
+            const long long o = ((long long)(n * 2 * g.H + 2 * i) * (2 * g.W) + 2 * j) * ldo;
+            if (g.outb) outcb[o] = __builtin_bit_cast(unsigned short, (__bf16)(acc[fm][fn][r] + b));
+            else outc[o] = acc[fm][fn][r] + b;
           }
         }
     }
@@ -266,7 +273,22 @@ extern "C" int pmu_convT2x2_fwd_dma(const unsigned short* xt, int Cip, int N, in
   GArgs g{};
   g.a = xt; g.bp = wp; g.bias = bias; g.out = u;
   g.M = N * H * W; g.Ncols = 4 * Cout; g.K = Cin; g.lda = Cip;
-  g.H = H; g.W = W; g.Cout = Cout;
+  g.H = H; g.W = W; g.Cout = Cout; g.ldo = Cout;
+  return launch<false>(g, stream);
+}
+
+// The forward written as bf16 (RNE) into channels [0, Cout) of a wider NHWC bf16 tensor (pixel stride
+// ldo): the up-sampled half of the Up block's bf16 concat operand (unet_parts.py:52,66 under autocast),
+// so the operand materialisation copies only the skip half and no fp32 u is written at all.
+extern "C" int pmu_convT2x2_fwd_dma_ldb(const unsigned short* xt, int Cip, int N, int H, int W,
+                                        const unsigned short* wp, const float* bias, int Cin, int Cout,
+                                        unsigned short* ub, int ldo, void* stream) {
+  PMU_REQUIRE(xt && wp && ub && N > 0 && H > 0 && W > 0 && Cip >= Cin && Cip % 8 == 0 && ldo >= Cout);
+  PMU_REQUIRE(pmu_convT2x2_dma_ok(Cin, Cout, 0) && (long long)N * H * W < (1LL << 31));
+  GArgs g{};
+  g.a = xt; g.bp = wp; g.bias = bias; g.out = nullptr; g.outb = ub;
+  g.M = N * H * W; g.Ncols = 4 * Cout; g.K = Cin; g.lda = Cip;
+  g.H = H; g.W = W; g.Cout = Cout; g.ldo = ldo;
   return launch<false>(g, stream);
 }
 

@@ -237,8 +237,9 @@ __global__ __launch_bounds__(256) void frame_to_bf16_kernel(DevFrame f, int Cpad
 
 // Fast path: one 16-B unit (8 channels) per thread, 32-bit pixel decode; every source's channel
 // count is a multiple of 8 (a unit never straddles the concat) and the output has < 2^31 units.
+// (ldo: output pixel stride in elements, >= Cpad — a wider tensor's first Cpad channels)
 __global__ __launch_bounds__(256) void frame_to_bf16_fast_kernel(DevFrame f, int Cpad, unsigned total,
-                                                                 unsigned short* __restrict__ out) {
+                                                                 unsigned short* __restrict__ out, int ldo) {
   const unsigned nu = (unsigned)Cpad / 8u, Wu = (unsigned)f.W, Hu = (unsigned)f.H;
   for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const unsigned pix = e / nu, cu = e - pix * nu;
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(256) void frame_to_bf16_fast_kernel(DevFrame f, int
       a = src_value4(s, (int)n, hs, ws, cs);
       b = src_value4(s, (int)n, hs, ws, cs + 4);
     }
-    *reinterpret_cast<uint4*>(out + (size_t)pix * Cpad + c) =
+    *reinterpret_cast<uint4*>(out + (size_t)pix * ldo + c) =
         make_uint4(pmu_pk_bf16(a.x, a.y), pmu_pk_bf16(a.z, a.w), pmu_pk_bf16(b.x, b.y), pmu_pk_bf16(b.z, b.w));
   }
 }
@@ -284,7 +285,8 @@ __global__ __launch_bounds__(256) void frame_to_f32_kernel(DevFrame f, float* __
 
 // Fast path of the fp32 materialisation: one float4 (4 channels) per thread, 32-bit pixel decode;
 // every source's channel count is a multiple of 4 and the output has < 2^31 units.
-__global__ __launch_bounds__(256) void frame_to_f32_fast_kernel(DevFrame f, unsigned total, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void frame_to_f32_fast_kernel(DevFrame f, unsigned total, float* __restrict__ out,
+                                                                int ldo) {
   const unsigned nu = (unsigned)f.C / 4u, Wu = (unsigned)f.W, Hu = (unsigned)f.H;
   for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const unsigned pix = e / nu, cu = e - pix * nu;
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(256) void frame_to_f32_fast_kernel(DevFrame f, unsi
     const bool second = f.nsrc > 1 && c >= f.C0;
     const DevSrc& s = second ? f.s1 : f.s0;
     const int cs = c - (second ? f.C0 : 0);
-    *reinterpret_cast<float4*>(out + (size_t)pix * f.C + c) =
+    *reinterpret_cast<float4*>(out + (size_t)pix * ldo + c) =
         src_value4(s, (int)n, (int)h - s.off_h, (int)w - s.off_w, cs);
   }
 }
@@ -334,7 +336,7 @@ extern "C" int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* o
     long long g = (units + 255) / 256;
     if (g > 16384) g = 16384;
     hipLaunchKernelGGL(frame_to_bf16_fast_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
-                       make_dev_frame(f), Cpad, (unsigned)units, out);
+                       make_dev_frame(f), Cpad, (unsigned)units, out, Cpad);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }
@@ -355,7 +357,7 @@ extern "C" int pmu_frame_to_f32(const pmu_frame* f, float* out, void* stream) {
     long long g = (units + 255) / 256;
     if (g > 16384) g = 16384;
     hipLaunchKernelGGL(frame_to_f32_fast_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, d,
-                       (unsigned)units, out);
+                       (unsigned)units, out, d.C);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }
@@ -406,5 +408,37 @@ extern "C" int pmu_occupancy_wgrad3x3_bf16(int* blocks_per_cu) {
   const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(wgrad3x3_bf16_kernel<128, 4>), 768, 0);
   if (e != hipSuccess) return (int)e;
   *blocks_per_cu = n;
+  return PMU_OK;
+}
+
+// The frame written into the first channels of a wider NHWC tensor (pixel stride ldo): the skip half
+// of the Up block's concat operand, whose other half the transposed conv writes in place
+// (pmu_convT2x2_fwd_ld / pmu_convT2x2_fwd_dma_ld).  Vector paths only (channel counts of 4 / 8).
+extern "C" int pmu_frame_to_f32_ld(const pmu_frame* f, float* out, int ldo, void* stream) {
+  PMU_REQUIRE(valid_frame(f, true) && out);
+  const DevFrame d = make_dev_frame(f);
+  const long long units = (long long)d.N * d.H * d.W * (d.C / 4);
+  PMU_REQUIRE(d.vec && units < (1LL << 31) && ldo >= d.C && ldo % 4 == 0 && (long long)d.N * d.H * d.W * ldo < (1LL << 32));
+  long long g = (units + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(frame_to_f32_fast_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, d,
+                     (unsigned)units, out, ldo);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_frame_to_bf16_ld(const pmu_frame* f, int Cpad, unsigned short* out, int ldo, void* stream) {
+  PMU_REQUIRE(valid_frame(f, true) && out && Cpad % 8 == 0 && ldo >= Cpad && ldo % 8 == 0);
+  const int C = f->src[0].C + (f->nsrc > 1 ? f->src[1].C : 0);
+  PMU_REQUIRE(Cpad >= C);
+  const long long units = (long long)f->N * f->H * f->W * (Cpad / 8);
+  bool fast = units < (1LL << 31);
+  for (int i = 0; i < f->nsrc; ++i) fast = fast && f->src[i].C % 8 == 0;
+  PMU_REQUIRE(fast);
+  long long g = (units + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(frame_to_bf16_fast_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
+                     make_dev_frame(f), Cpad, (unsigned)units, out, ldo);
+  PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

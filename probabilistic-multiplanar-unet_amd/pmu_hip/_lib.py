@@ -95,6 +95,8 @@ SIGNATURES = {
                                       c_void_p, c_void_p]),
     "pmu_frame_to_bf16": (c_int, [_FP, c_int, c_void_p, c_void_p]),
     "pmu_frame_to_f32": (c_int, [_FP, c_void_p, c_void_p]),
+    "pmu_frame_to_f32_ld": (c_int, [_FP, c_void_p, c_int, c_void_p]),
+    "pmu_frame_to_bf16_ld": (c_int, [_FP, c_int, c_void_p, c_int, c_void_p]),
     "pmu_conv3x3_wgrad_ws_bf16": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_conv3x3_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                        c_size_t, c_void_p]),
@@ -139,6 +141,8 @@ SIGNATURES = {
     "pmu_convT2x2_packed_size": (c_size_t, [c_int, c_int]),
     "pmu_convT2x2_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_fwd": (c_int, [_FP, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_fwd_ld_ok": (c_int, [_FP, c_int]),
+    "pmu_convT2x2_fwd_ld": (c_int, [_FP, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "pmu_convT2x2_dgrad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                    c_int, c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_wgrad_ws": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
@@ -198,6 +202,8 @@ SIGNATURES = {
     "pmu_convT2x2_pack_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_fwd_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
                                      c_void_p, c_void_p]),
+    "pmu_convT2x2_fwd_dma_ldb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                                         c_void_p, c_int, c_void_p]),
     "pmu_convT2x2_dgrad_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int,
                                        c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_wino2h_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,

@@ -83,6 +83,19 @@ def _f32_srcs(srcs, N, H, W):
     return [Src(frame_to_f32(srcs, N, H, W))]
 
 
+def _materialised(srcs, dtype):
+    """The operand tensor itself when the frame is one RAW, unpooled, unshifted source already stored
+    in the dtype the GEMM reads (fp32, or bf16 with channels padded to 8): no copy is needed."""
+    if len(srcs) != 1:
+        return None
+    sr = srcs[0]
+    if sr.mode != L.SRC_RAW or sr.pool != L.POOL_NONE or sr.off != (0, 0) or sr.x.dtype != dtype:
+        return None
+    if dtype == BF16S and sr.C % 8 != 0:
+        return None
+    return sr.x
+
+
 def _empty(*shape, dtype=F32, device=None):
     return torch.empty(shape, dtype=dtype, device=device)
 
@@ -253,7 +266,8 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         part = _empty(R, 2 * Cout, device=dev) if need_stats else None
         if use_dma:
             # both operands by LDS-DMA (maps >= 32 wide): the operand written once in bf16, as below
-            xt = frame_to_bf16(srcs, N, H, W)
+            xt = _materialised(srcs, BF16S)
+            xt = xt if xt is not None else frame_to_bf16(srcs, N, H, W)
             wp = pack_weights_dma(conv.weight, dgrad=False)
             if zb and Cout % 8 == 0:   # (the bf16-z consumers take channel quads)
                 z = _empty(N, H, W, Cout, dtype=BF16S, device=dev)
@@ -270,7 +284,8 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
         elif use_raw:
             # the operand (BN+ReLU / max-pool / F.pad+cat applied) written once in bf16; the GEMM
             # streams it, and the weight gradient reuses it
-            xt = frame_to_bf16(srcs, N, H, W)
+            xt = _materialised(srcs, BF16S)
+            xt = xt if xt is not None else frame_to_bf16(srcs, N, H, W)
             wp = pack_weights_raw(conv.weight, dgrad=False)
             L.call("pmu_conv3x3_fwd_raw", xt.data_ptr(), Cp, N, H, W, wp.data_ptr(), L.ptr(conv.bias), Cout,
                    z.data_ptr(), L.ptr(part), s)
@@ -291,7 +306,8 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             R = lb.pmu_conv3x3_tiles_wino4(N, H, W)
             part = _empty(R, 2 * Cout, device=dev) if need_stats else None
             wp = pack_weights_wino4(conv.weight, dgrad=False)
-            xm = frame_to_f32(srcs, N, H, W)
+            xm = _materialised(srcs, F32)
+            xm = xm if xm is not None else frame_to_f32(srcs, N, H, W)
             L.call("pmu_conv3x3_fwd_wino4", xm.data_ptr(), Cin, N, H, W, wp.data_ptr(), L.ptr(conv.bias),
                    Cout, z.data_ptr(), L.ptr(part), s)
             xt32 = xm if xt32 is not None else None
@@ -300,7 +316,8 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
             part = _empty(R, 2 * Cout, device=dev) if need_stats else None
             if wino_raw_ok(Cin) and wino2h_ok(Cin):
                 # 1024-thread F(2x2) workgroups (four waves per SIMD) on the materialised operand
-                xm = frame_to_f32(srcs, N, H, W)
+                xm = _materialised(srcs, F32)
+                xm = xm if xm is not None else frame_to_f32(srcs, N, H, W)
                 wp2 = pack_weights_wino2h(conv.weight, dgrad=False)
                 L.call("pmu_conv3x3_fwd_wino2h", xm.data_ptr(), Cin, N, H, W, wp2.data_ptr(), L.ptr(conv.bias),
                        Cout, z.data_ptr(), L.ptr(part), s)
@@ -309,7 +326,8 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
                 # the operand materialised once (the weight gradient's operand anyway), then a
                 # DMA-staged Winograd GEMM on it
                 wp = pack_weights_wino(conv.weight, dgrad=False)
-                xm = frame_to_f32(srcs, N, H, W)
+                xm = _materialised(srcs, F32)
+                xm = xm if xm is not None else frame_to_f32(srcs, N, H, W)
                 L.call("pmu_conv3x3_fwd_wino_raw", xm.data_ptr(), Cin, N, H, W, wp.data_ptr(), L.ptr(conv.bias),
                        Cout, z.data_ptr(), L.ptr(part), s)
                 xt32 = xm if xt32 is not None else None
@@ -728,13 +746,14 @@ def _dc_layers(dc):
 
 @dataclass
 class UpState:
-    u: torch.Tensor          # convT output, NHWC [N][2h][2w][Cup]
+    u: torch.Tensor | None   # convT output, NHWC [N][2h][2w][Cup] (None: written into the concat operand)
     off: tuple               # (pad_top, pad_left) inside the skip frame
     prev: ConvBNOut          # convT input producer
     c1: ConvBNOut
     c2: ConvBNOut
     bf16: bool = False       # convT input gradient on bf16 MFMA where its shapes allow
     xt: torch.Tensor | None = None   # bf16: the convT operand the forward materialised (weight gradient)
+    cskip: int = 0                   # channels of the skip half of the concat operand (backward split)
 
 
 class UNetState:
@@ -804,35 +823,66 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         hi, wi = cur.z.shape[1], cur.z.shape[2]
         convT = up.up
         Cup = convT.out_channels
-        u = _empty(N, 2 * hi, 2 * wi, Cup, device=dev)
         fin = frame_of([cur.act()], N, hi, wi)
         Cin_t = cur.z.shape[3]
         _check_channels(Cin_t, convT)
         xtT = None
-        if bf16 and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 0):
-            # the BN+ReLU operand written once in bf16 (the weight gradient's operand too), both GEMM
-            # operands by LDS-DMA
-            xtT = frame_to_bf16([cur.act()], N, hi, wi)
-            wpt = pack_convT_weights_dma(convT.weight, dgrad=False)
-            L.call("pmu_convT2x2_fwd_dma", xtT.data_ptr(), xtT.shape[3], N, hi, wi, wpt.data_ptr(), L.ptr(convT.bias),
-                   Cin_t, Cup, u.data_ptr(), L.stream())
-            if not keep:
-                xtT = None
-        elif bf16 and L.lib().pmu_convT2x2_bf16_ok(fin, Cup):   # (refuses bf16-stored sources)
-            wpt = pack_convT_weights_bf16(convT.weight, dgrad=False)
-            L.call("pmu_convT2x2_fwd_bf16", fin, wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
-        else:
-            wpt = pack_convT_weights(convT.weight, dgrad=False)
-            L.call("pmu_convT2x2_fwd", frame_of(_f32_srcs([cur.act()], N, hi, wi), N, hi, wi), convT.weight.data_ptr(),
-                   wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
         dY, dX = hs - 2 * hi, ws_ - 2 * wi
         assert dY >= 0 and dX >= 0, "decoder feature map larger than skip (unsupported by reference too)"
         off = (dY // 2, dX // 2)
         c1w, b1, c2w, b2 = _dc_layers(up.conv)
-        srcs = [skip.act(), Src(u, L.SRC_RAW, off=off)]
+        Cskip = skip.z.shape[3]
+        Ccat = Cskip + Cup
+        lb = L.lib()
+        # The concat operand built in place: the transposed conv writes its half (channels Cskip..) of
+        # the materialised operand directly and only the skip half is copied (no u tensor, one pass over
+        # it less) — when the halves need no F.pad and the conv will stage a materialised operand.
+        direct = dY == 0 and dX == 0 and Cskip % 8 == 0 and Cup % 8 == 0 and skip.z.dtype == F32
+        if bf16:
+            direct = (direct and bool(lb.pmu_convT2x2_dma_ok(Cin_t, Cup, 0)) and
+                      dma_ok(hs, ws_, Ccat, c1w.out_channels, c1w.out_channels))
+        else:
+            direct = (direct and use_wino() and (wino4_ok(Ccat, hs, ws_, "fwd") or wino_raw_ok(Ccat)) and
+                      bool(lb.pmu_convT2x2_fwd_ld_ok(fin, Cup)))
+        if direct and bf16:
+            xcat = torch.empty(N, hs, ws_, Ccat, dtype=BF16S, device=dev)
+            xtT = frame_to_bf16([cur.act()], N, hi, wi)
+            wpt = pack_convT_weights_dma(convT.weight, dgrad=False)
+            L.call("pmu_convT2x2_fwd_dma_ldb", xtT.data_ptr(), xtT.shape[3], N, hi, wi, wpt.data_ptr(),
+                   L.ptr(convT.bias), Cin_t, Cup, xcat.data_ptr() + 2 * Cskip, Ccat, L.stream())
+            L.call("pmu_frame_to_bf16_ld", frame_of([skip.act()], N, hs, ws_), Cskip, xcat.data_ptr(), Ccat, L.stream())
+            if not keep:
+                xtT = None
+            u, srcs = None, [Src(xcat)]
+        elif direct:
+            xcat = _empty(N, hs, ws_, Ccat, device=dev)
+            wpt = pack_convT_weights(convT.weight, dgrad=False)
+            L.call("pmu_convT2x2_fwd_ld", fin, convT.weight.data_ptr(), wpt.data_ptr(), L.ptr(convT.bias), Cup,
+                   xcat.data_ptr() + 4 * Cskip, Ccat, L.stream())
+            L.call("pmu_frame_to_f32_ld", frame_of([skip.act()], N, hs, ws_), xcat.data_ptr(), Ccat, L.stream())
+            u, srcs = None, [Src(xcat)]
+        else:
+            u = _empty(N, 2 * hi, 2 * wi, Cup, device=dev)
+            if bf16 and lb.pmu_convT2x2_dma_ok(Cin_t, Cup, 0):
+                # the BN+ReLU operand written once in bf16 (the weight gradient's operand too), both GEMM
+                # operands by LDS-DMA
+                xtT = frame_to_bf16([cur.act()], N, hi, wi)
+                wpt = pack_convT_weights_dma(convT.weight, dgrad=False)
+                L.call("pmu_convT2x2_fwd_dma", xtT.data_ptr(), xtT.shape[3], N, hi, wi, wpt.data_ptr(),
+                       L.ptr(convT.bias), Cin_t, Cup, u.data_ptr(), L.stream())
+                if not keep:
+                    xtT = None
+            elif bf16 and lb.pmu_convT2x2_bf16_ok(fin, Cup):   # (refuses bf16-stored sources)
+                wpt = pack_convT_weights_bf16(convT.weight, dgrad=False)
+                L.call("pmu_convT2x2_fwd_bf16", fin, wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
+            else:
+                wpt = pack_convT_weights(convT.weight, dgrad=False)
+                L.call("pmu_convT2x2_fwd", frame_of(_f32_srcs([cur.act()], N, hi, wi), N, hi, wi),
+                       convT.weight.data_ptr(), wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
+            srcs = [skip.act(), Src(u, L.SRC_RAW, off=off)]
         o1 = conv_bn_forward(srcs, c1w, b1, N, hs, ws_, training, dev, bf16=bf16, keep=keep, zb=zb)
         o2 = conv_bn_forward([o1.act()], c2w, b2, N, hs, ws_, training, dev, bf16=bf16, keep=keep, zb=zb)
-        st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2, bf16=bf16, xt=xtT))
+        st.ups.append(UpState(u=u, off=off, prev=cur, c1=o1, c2=o2, bf16=bf16, xt=xtT, cskip=Cskip))
         cur = o2
     st.feat_src = cur
     if net.apply_last_layer:
@@ -898,7 +948,7 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         c1w, b1, c2w, b2 = _dc_layers(up.conv)
         da1 = conv_bn_backward(us.c2, da, c2w, b2, grads)
         grads.flush()
-        Cskip = us.c1.srcs[0].C
+        Cskip = us.cskip
         dsk, dup = conv_bn_backward(us.c1, da1, c1w, b1, grads, split=Cskip)
         grads.flush()
         dskip[nlev - 2 - j] = dsk
