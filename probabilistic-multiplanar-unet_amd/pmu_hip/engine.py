@@ -89,7 +89,8 @@ def _materialised(srcs, dtype):
     if len(srcs) != 1:
         return None
     sr = srcs[0]
-    if sr.mode != L.SRC_RAW or sr.pool != L.POOL_NONE or sr.off != (0, 0) or sr.x.dtype != dtype:
+    if (sr.mode != L.SRC_RAW or sr.pool != L.POOL_NONE or sr.off != (0, 0) or sr.x.dtype != dtype
+            or not sr.x.is_contiguous() or sr.x.dim() != 4):
         return None
     if dtype == BF16S and sr.C % 8 != 0:
         return None
