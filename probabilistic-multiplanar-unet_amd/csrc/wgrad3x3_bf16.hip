@@ -301,6 +301,241 @@ __global__ __launch_bounds__(256) void frame_to_f32_fast_kernel(DevFrame f, unsi
   }
 }
 
+// ---- streaming materialisation ------------------------------------------------------------
+// The frame_to_* passes are HBM-bound (c5: 38 per step, 19% of its kernel time; c2: 34, 7%).  The
+// generic kernels above take one 8-channel unit per thread per step, re-load the unit's BN
+// coefficients every step, and (vmcnt counts loads and stores in order) wait for a step's stores
+// before the next step's loads can be consumed: 4.8-5.2 TB/s, 3.3-3.8 TB/s max-pooled.  This path
+// takes the common frames — one fp32 source, no offset, C = Cpad a multiple of 8 with C / 8 a power
+// of two up to 256 (every UNet width) — with a thread owning one channel unit for the whole launch
+// (coefficients loaded once) and U pixels per step, the next step's loads issued before this step's
+// stores.  Same per-element arithmetic as src_xform4 / src_value4: bit-identical output.  Measured
+// (profiles/r03/kbench_frame_c5.txt): max-pooled 3.7-4.0 -> 5.2-6.6 TB/s; the flat passes over
+// the 512^2 / 256^2 maps gain only from the nontemporal policy below (about 5.0 -> 5.5 TB/s).
+struct StreamArgs {
+  const float* x;
+  const float* z;
+  const float* coef;
+  void* out;
+  int C, lg;         // channels; log2(C / 8)
+  int H, W, SH, SW;  // frame H x W; source SH x SW (POOL: the 2x2 windows' map, floor mode)
+  unsigned P;        // frame pixels N * H * W
+  int ldo;           // output pixel stride in elements
+};
+
+template <int MODE, bool POOL>
+struct StreamLd {
+  static constexpr int NV = POOL ? 8 : (MODE == PMU_SRC_BNBWD ? 4 : 2);
+  float4 v[NV];
+};
+
+typedef float stream_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned stream_u4 __attribute__((ext_vector_type(4)));
+template <int NT>
+__device__ __forceinline__ float4 stream_ld4(const float* p) {
+  if (NT & 1) {
+    const stream_f4 v = __builtin_nontemporal_load(reinterpret_cast<const stream_f4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return pmu_ld4(p);
+}
+
+template <int MODE, bool POOL, int NT>
+__device__ __forceinline__ void stream_load(const StreamArgs& a, unsigned p, int c, StreamLd<MODE, POOL>& d) {
+  if (!POOL) {
+    const size_t o = (size_t)p * a.C + c;
+    d.v[0] = stream_ld4<NT>(a.x + o);
+    d.v[1] = stream_ld4<NT>(a.x + o + 4);
+    if constexpr (MODE == PMU_SRC_BNBWD) {
+      d.v[2] = stream_ld4<NT>(a.z + o);
+      d.v[3] = stream_ld4<NT>(a.z + o + 4);
+    }
+  } else {
+    const unsigned t = p / (unsigned)a.W, w = p - t * (unsigned)a.W;
+    const unsigned n = t / (unsigned)a.H, h = t - n * (unsigned)a.H;
+    const size_t b = (((size_t)n * a.SH + 2 * h) * a.SW + 2 * w) * a.C + c;
+    const size_t rs = (size_t)a.SW * a.C;
+    const size_t o[4] = {b, b + a.C, b + rs, b + rs + a.C};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      d.v[2 * k] = stream_ld4<NT>(a.x + o[k]);
+      d.v[2 * k + 1] = stream_ld4<NT>(a.x + o[k] + 4);
+    }
+  }
+}
+
+__device__ __forceinline__ float4 bnrelu4(float4 x, float4 sc, float4 sh) {
+  return make_float4(fmaxf(0.f, fmaf(x.x, sc.x, sh.x)), fmaxf(0.f, fmaf(x.y, sc.y, sh.y)),
+                     fmaxf(0.f, fmaf(x.z, sc.z, sh.z)), fmaxf(0.f, fmaf(x.w, sc.w, sh.w)));
+}
+__device__ __forceinline__ float4 max4(float4 a, float4 t) {
+  return make_float4(fmaxf(a.x, t.x), fmaxf(a.y, t.y), fmaxf(a.z, t.z), fmaxf(a.w, t.w));
+}
+__device__ __forceinline__ float bnbwd1(float x, float z, float sc, float sh, float mu, float kx, float kc) {
+  return fmaf(sc, fmaf(z, sc, sh) > 0.f ? x : 0.f, fmaf(kx, z - mu, kc));
+}
+__device__ __forceinline__ float4 bnbwd4(float4 x, float4 z, float4 sc, float4 sh, float4 mu, float4 kx, float4 kc) {
+  return make_float4(bnbwd1(x.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x), bnbwd1(x.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y),
+                     bnbwd1(x.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z), bnbwd1(x.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w));
+}
+
+template <int MODE, bool POOL, bool BF, int U, int NT>
+__global__ __launch_bounds__(256) void frame_stream_kernel(StreamArgs a) {
+  const int tid = threadIdx.x;
+  const int c = 8 * (tid & ((1 << a.lg) - 1));
+  const unsigned pb = 256u >> a.lg;  // pixels per U-slice of a block step
+  // this thread's channel unit is fixed: its coefficients in registers for the whole launch
+  float4 sc[2], sh[2], mu[2], kx[2], kc[2];
+  if (MODE != PMU_SRC_RAW) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      sc[k] = pmu_ld4(a.coef + c + 4 * k);
+      sh[k] = pmu_ld4(a.coef + a.C + c + 4 * k);
+      if (MODE == PMU_SRC_BNBWD) {
+        mu[k] = pmu_ld4(a.coef + 2 * a.C + c + 4 * k);
+        kx[k] = pmu_ld4(a.coef + 3 * a.C + c + 4 * k);
+        kc[k] = pmu_ld4(a.coef + 4 * a.C + c + 4 * k);
+      }
+    }
+  }
+  const unsigned span = pb * U, stride = span * gridDim.x;
+  const unsigned pr = (unsigned)(tid >> a.lg), plast = a.P - 1;
+  // Two register sets in ping-pong (a copy between them would wait for the loads it copies): the
+  // loads of step s+1 are in flight while step s stores.  Loads are unconditional, the pixel clamped
+  // to the last one (a load under a branch makes the compiler wait for every outstanding load before
+  // the first store), and the loop runs on the block's uniform base.
+  StreamLd<MODE, POOL> A[U], B[U];
+  auto load = [&](StreamLd<MODE, POOL>* d, unsigned base) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) stream_load<MODE, POOL, NT>(a, min(base + pr + j * pb, plast), c, d[j]);
+  };
+  auto store = [&](const StreamLd<MODE, POOL>* d, unsigned base) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      // past the end: the clamped pixel's own value rewritten to it (identical bytes), so the stores
+      // are unconditional too and the compiler can count the loads still in flight at each store
+      const unsigned p = min(base + pr + j * pb, plast);
+      float4 r[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (POOL) {
+          float4 m = d[j].v[k];
+          if (MODE == PMU_SRC_BNRELU) m = bnrelu4(m, sc[k], sh[k]);
+#pragma unroll
+          for (int q = 1; q < 4; ++q) {
+            float4 t = d[j].v[2 * q + k];
+            if (MODE == PMU_SRC_BNRELU) t = bnrelu4(t, sc[k], sh[k]);
+            m = max4(m, t);
+          }
+          r[k] = m;
+        } else if (MODE == PMU_SRC_BNRELU) {
+          r[k] = bnrelu4(d[j].v[k], sc[k], sh[k]);
+        } else if (MODE == PMU_SRC_BNBWD) {
+          r[k] = bnbwd4(d[j].v[k], d[j].v[2 + k], sc[k], sh[k], mu[k], kx[k], kc[k]);
+        } else {
+          r[k] = d[j].v[k];
+        }
+      }
+      if (BF) {
+        uint4* o = reinterpret_cast<uint4*>(static_cast<unsigned short*>(a.out) + (size_t)p * a.ldo + c);
+        const uint4 v = make_uint4(pmu_pk_bf16(r[0].x, r[0].y), pmu_pk_bf16(r[0].z, r[0].w),
+                                   pmu_pk_bf16(r[1].x, r[1].y), pmu_pk_bf16(r[1].z, r[1].w));
+        if (NT & 2) __builtin_nontemporal_store(stream_u4{v.x, v.y, v.z, v.w}, reinterpret_cast<stream_u4*>(o));
+        else *o = v;
+      } else {
+        float4* o = reinterpret_cast<float4*>(static_cast<float*>(a.out) + (size_t)p * a.ldo + c);
+        if (NT & 2) {
+          __builtin_nontemporal_store(stream_f4{r[0].x, r[0].y, r[0].z, r[0].w}, reinterpret_cast<stream_f4*>(o));
+          __builtin_nontemporal_store(stream_f4{r[1].x, r[1].y, r[1].z, r[1].w}, reinterpret_cast<stream_f4*>(o + 1));
+        } else {
+          o[0] = r[0];
+          o[1] = r[1];
+        }
+      }
+    }
+  };
+  unsigned base = blockIdx.x * span;
+  load(A, base);
+  // (sched_barrier: keeps the scheduler from hoisting a step's arithmetic, which waits for its loads,
+  // above the issue of the next step's loads)
+  for (; base < a.P; base += 2 * stride) {
+    load(B, base + stride);
+    __builtin_amdgcn_sched_barrier(0);
+    store(A, base);
+    // no exit between the halves (a step past the end rewrites the last pixel): a mid-loop exit
+    // shares the latch, and the compiler then waits at the loop head for loads that path left pending
+    load(A, base + 2 * stride);
+    __builtin_amdgcn_sched_barrier(0);
+    store(B, base + stride);
+  }
+}
+
+// A frame the streaming path takes (see above); PMU_FRAME_STREAM=0 forces the generic kernels (the
+// tests compare the two).
+static bool stream_ok(const pmu_frame* f, int Cout) {
+  if (f->nsrc != 1) return false;
+  const pmu_src& s = f->src[0];
+  if (s.dtype != 0 || s.off_h != 0 || s.off_w != 0 || s.C != Cout || s.C % 8 != 0) return false;
+  const int nu = s.C / 8;
+  if (nu > 256 || (nu & (nu - 1)) != 0) return false;
+  if (s.pool == PMU_POOL_AVG2CEIL || (s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNBWD)) return false;
+  if (s.pool == PMU_POOL_NONE && (s.H != f->H || s.W != f->W)) return false;
+  if (s.pool == PMU_POOL_MAX2 && (s.H / 2 != f->H || s.W / 2 != f->W)) return false;
+  if ((long long)f->N * f->H * f->W >= (1LL << 31)) return false;
+  const char* e = getenv("PMU_FRAME_STREAM");
+  return !(e && e[0] == '0');
+}
+
+template <bool BF, int NT, int U_POOL, int U_FLAT, int U_BWD>
+static void launch_stream_nt(const pmu_src& s, dim3 grid, dim3 blk, hipStream_t st, const StreamArgs& a) {
+  if (s.pool == PMU_POOL_MAX2) {
+    if (s.mode == PMU_SRC_BNRELU) hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_BNRELU, true, BF, U_POOL, NT>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_RAW, true, BF, U_POOL, NT>), grid, blk, 0, st, a);
+  } else if (s.mode == PMU_SRC_BNRELU) {
+    hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_BNRELU, false, BF, U_FLAT, NT>), grid, blk, 0, st, a);
+  } else if (s.mode == PMU_SRC_BNBWD) {
+    hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_BNBWD, false, BF, U_BWD, NT>), grid, blk, 0, st, a);
+  } else {
+    hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_RAW, false, BF, U_FLAT, NT>), grid, blk, 0, st, a);
+  }
+}
+
+template <bool BF>
+static int launch_stream(const pmu_frame* f, void* out, int ldo, hipStream_t st) {
+  const pmu_src& s = f->src[0];
+  StreamArgs a;
+  a.x = s.x; a.z = s.z; a.coef = s.coef; a.out = out;
+  a.C = s.C;
+  a.lg = 0;
+  while ((8 << a.lg) < s.C) ++a.lg;
+  a.H = f->H; a.W = f->W; a.SH = s.H; a.SW = s.W;
+  a.P = (unsigned)((long long)f->N * f->H * f->W);
+  a.ldo = ldo;
+  static const int max_blocks = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return 8 * cus;
+  }();
+  constexpr int U_POOL = 1, U_FLAT = 2, U_BWD = 2;
+  const int U = s.pool == PMU_POOL_MAX2 ? U_POOL : s.mode == PMU_SRC_BNBWD ? U_BWD : U_FLAT;
+  const long long span = (256LL >> a.lg) * U;
+  long long g = ((long long)a.P + span - 1) / span;
+  if (g > max_blocks) g = max_blocks;
+  const dim3 grid((unsigned)g), blk(256);
+  // cache policy (measured per shape, tools/kbench_frame.py, and per step): nontemporal loads and
+  // stores for the bf16 passes over sources larger than the 256 MB last-level cache's share they
+  // would thrash (c5 512^2 / 256^2 levels: -8..-10%), plain below it and for the fp32 passes (c2:
+  // nontemporal measured +18% there)
+  const char* ne = pmu_variant_env("PMU_FRAME_NT");
+  const size_t xbytes = (size_t)f->N * s.H * s.W * s.C * sizeof(float);
+  const bool nt = ne ? (atoi(ne) & 3) == 3 : (BF && xbytes >= ((size_t)128 << 20));
+  if (nt) launch_stream_nt<BF, 3, U_POOL, U_FLAT, U_BWD>(s, grid, blk, st, a);
+  else launch_stream_nt<BF, 0, U_POOL, U_FLAT, U_BWD>(s, grid, blk, st, a);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
 static int pad8(int c) { return (c + 7) & ~7; }
 
 static void geometry(int N, int H, int W, int Cin, int Cout, int* wco, int* twl, int* tiles_w, int* tiles_h,
@@ -329,6 +564,7 @@ extern "C" int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* o
   PMU_REQUIRE(valid_frame(f, true) && out && Cpad % 4 == 0);
   const int C = f->src[0].C + (f->nsrc > 1 ? f->src[1].C : 0);
   PMU_REQUIRE(Cpad >= C);
+  if (stream_ok(f, Cpad)) return launch_stream<true>(f, out, Cpad, (hipStream_t)stream);
   const long long units = (long long)f->N * f->H * f->W * (Cpad / 8);
   bool fast = Cpad % 8 == 0 && units < (1LL << 31);
   for (int i = 0; i < f->nsrc; ++i) fast = fast && f->src[i].C % 8 == 0;
@@ -351,6 +587,7 @@ extern "C" int pmu_frame_to_bf16(const pmu_frame* f, int Cpad, unsigned short* o
 
 extern "C" int pmu_frame_to_f32(const pmu_frame* f, float* out, void* stream) {
   PMU_REQUIRE(valid_frame(f, true) && out);
+  if (stream_ok(f, f->src[0].C)) return launch_stream<false>(f, out, f->src[0].C, (hipStream_t)stream);
   const DevFrame d = make_dev_frame(f);
   const long long units = (long long)d.N * d.H * d.W * (d.C / 4);
   if (d.vec && units < (1LL << 31)) {
@@ -419,6 +656,7 @@ extern "C" int pmu_frame_to_f32_ld(const pmu_frame* f, float* out, int ldo, void
   const DevFrame d = make_dev_frame(f);
   const long long units = (long long)d.N * d.H * d.W * (d.C / 4);
   PMU_REQUIRE(d.vec && units < (1LL << 31) && ldo >= d.C && ldo % 4 == 0 && (long long)d.N * d.H * d.W * ldo < (1LL << 32));
+  if (stream_ok(f, d.C) && ldo % 8 == 0) return launch_stream<false>(f, out, ldo, (hipStream_t)stream);
   long long g = (units + 255) / 256;
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(frame_to_f32_fast_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, d,
@@ -435,6 +673,7 @@ extern "C" int pmu_frame_to_bf16_ld(const pmu_frame* f, int Cpad, unsigned short
   bool fast = units < (1LL << 31);
   for (int i = 0; i < f->nsrc; ++i) fast = fast && f->src[i].C % 8 == 0;
   PMU_REQUIRE(fast);
+  if (stream_ok(f, Cpad)) return launch_stream<true>(f, out, ldo, (hipStream_t)stream);
   long long g = (units + 255) / 256;
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(frame_to_bf16_fast_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
