@@ -112,7 +112,13 @@ __global__ __launch_bounds__(256) void pack_dma_multi_kernel(const pmu_pack_job*
 
 // ZB: z stored in bf16 (the experiments-build bf16-z mode: the forward writes it, the input gradient's
 // BN-backward epilogue reads it)
-template <bool DGRAD, bool ZB, int WN, int NWV>
+// EXP (timing experiments, experiments build only, PMU_DMA_EXP; wrong results on purpose): bit 0 = no
+// epilogue output stores, bit 1 = no MFMAs.  512^2 x 64 -> 64 (c5, tools/kbench.py --c5): 0.52 ms; no
+// stores 0.33; no MFMAs 0.36; neither 0.17 — the z stores (1.07 GB fp32) and the MFMAs add up instead
+// of overlapping.  Measured and dropped: a phase offset between the two workgroups of a CU (s_sleep
+// before the first round: no change) and 16-B stores through an LDS transpose (-2..5% on K <= 128
+// only).
+template <bool DGRAD, bool ZB, int WN, int NWV, int EXP = 0>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs a) {
   using G = DG<WN, NWV>;
   constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH, NT = G::NT;
@@ -211,8 +217,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[tap & 1][fm], op[tap & 1][FM + fn], acc[fm][fn],
-                                                                 0, 0, 0);
+          if constexpr (!(EXP & 2))
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[tap & 1][fm], op[tap & 1][FM + fn], acc[fm][fn],
+                                                                   0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
@@ -264,7 +271,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
           const float m = ok ? v : 0.f;
           s1[fn] += m;
           s2[fn] = fmaf(m, m, s2[fn]);
-          if (!ok) continue;
+          if (!ok || (EXP & 1)) continue;
           PMU_DCHECK(((long long)n * a.H + h) * a.W + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
           const unsigned oo = (unsigned)(w * a.NOUT + j);
           if (ZB) drowb[oo] = vb;
@@ -420,6 +427,25 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
     if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 4>), grid, blk, 0, st, a);            \
     else hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 2, 8>), grid, blk, 0, st, a);                       \
   }
+#ifdef PMU_EXPERIMENTS
+  {
+    const char* e = pmu_variant_env("PMU_DMA_EXP");
+    const int x = e ? atoi(e) : 0;
+    if (!dgrad && !zb && x >= 1 && x <= 3) {
+      if (sh.wn == 1) {
+        if (x == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<false, false, 1, 4, 1>), grid, blk, 0, st, a);
+        if (x == 2) hipLaunchKernelGGL((conv3x3_dma_kernel<false, false, 1, 4, 2>), grid, blk, 0, st, a);
+        if (x == 3) hipLaunchKernelGGL((conv3x3_dma_kernel<false, false, 1, 4, 3>), grid, blk, 0, st, a);
+      } else {
+        if (x == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<false, false, 2, 8, 1>), grid, blk, 0, st, a);
+        if (x == 2) hipLaunchKernelGGL((conv3x3_dma_kernel<false, false, 2, 8, 2>), grid, blk, 0, st, a);
+        if (x == 3) hipLaunchKernelGGL((conv3x3_dma_kernel<false, false, 2, 8, 3>), grid, blk, 0, st, a);
+      }
+      PMU_CHECK_LAUNCH();
+      return PMU_OK;
+    }
+  }
+#endif
   if (dgrad && zb) PMU_DMA_LAUNCH(true, true)
   else if (dgrad) PMU_DMA_LAUNCH(true, false)
   else if (zb) PMU_DMA_LAUNCH(false, true)
