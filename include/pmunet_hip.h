@@ -246,6 +246,15 @@ int pmu_frame_to_f32(const pmu_frame* f, float* out, void* stream);
  * pmu_convT2x2_fwd_dma_ldb write in place (unet_parts.py:66).  Channel counts of 4 (fp32) / 8 (bf16). */
 int pmu_frame_to_f32_ld(const pmu_frame* f, float* out, int ldo, void* stream);
 int pmu_frame_to_bf16_ld(const pmu_frame* f, int Cpad, unsigned short* out, int ldo, void* stream);
+/* One pass over a level's BN+ReLU activation for both of its consumers (unet_parts.py:33 MaxPool2d
+ * and :66 torch.cat): f is the max-pooled frame (one fp32 BNRELU source, even source dims, C a
+ * power-of-two multiple of 8 up to 2048; pmu_frame_pool_skip_ok); out[N][H][W][C] receives the
+ * pooled operand and skip (pixel stride ldo_skip >= C, a multiple of 8) the unpooled activation in
+ * its first C channels.  Bit-identical to pmu_frame_to_* + pmu_frame_to_*_ld. */
+int pmu_frame_pool_skip_ok(const pmu_frame* f);
+int pmu_frame_to_bf16_pool_skip(const pmu_frame* f, unsigned short* out, unsigned short* skip, int ldo_skip,
+                                void* stream);
+int pmu_frame_to_f32_pool_skip(const pmu_frame* f, float* out, float* skip, int ldo_skip, void* stream);
 /* dw[Cout][Cin][3][3] from dzt [N][H][W][pad8(Cout)] and xt [N][H][W][pad8(Cin)] (bf16, pad8(c) =
  * c rounded up to a multiple of 8); ws must hold pmu_conv3x3_wgrad_ws_bf16() bytes. */
 size_t pmu_conv3x3_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);

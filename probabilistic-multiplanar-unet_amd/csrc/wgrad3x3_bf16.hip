@@ -321,6 +321,8 @@ struct StreamArgs {
   int H, W, SH, SW;  // frame H x W; source SH x SW (POOL: the 2x2 windows' map, floor mode)
   unsigned P;        // frame pixels N * H * W
   int ldo;           // output pixel stride in elements
+  void* out2;        // SKIP: the unpooled values (each 2x2 window's four), pixel stride ldo2
+  int ldo2;
 };
 
 template <int MODE, bool POOL>
@@ -379,7 +381,31 @@ __device__ __forceinline__ float4 bnbwd4(float4 x, float4 z, float4 sc, float4 s
                      bnbwd1(x.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z), bnbwd1(x.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w));
 }
 
-template <int MODE, bool POOL, bool BF, int U, int NT>
+// 8 channels (r0, r1) at element offset e of a bf16 / fp32 NHWC tensor
+template <bool BF, int NT>
+__device__ __forceinline__ void stream_st8(void* out, size_t e, float4 r0, float4 r1) {
+  if (BF) {
+    uint4* o = reinterpret_cast<uint4*>(static_cast<unsigned short*>(out) + e);
+    const uint4 v = make_uint4(pmu_pk_bf16(r0.x, r0.y), pmu_pk_bf16(r0.z, r0.w), pmu_pk_bf16(r1.x, r1.y),
+                               pmu_pk_bf16(r1.z, r1.w));
+    if (NT & 2) __builtin_nontemporal_store(stream_u4{v.x, v.y, v.z, v.w}, reinterpret_cast<stream_u4*>(o));
+    else *o = v;
+  } else {
+    float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + e);
+    if (NT & 2) {
+      __builtin_nontemporal_store(stream_f4{r0.x, r0.y, r0.z, r0.w}, reinterpret_cast<stream_f4*>(o));
+      __builtin_nontemporal_store(stream_f4{r1.x, r1.y, r1.z, r1.w}, reinterpret_cast<stream_f4*>(o + 1));
+    } else {
+      o[0] = r0;
+      o[1] = r1;
+    }
+  }
+}
+
+// SKIP (POOL only, even source dims): the four values of each window also written unpooled to out2 —
+// the skip half of the Up block's concat operand, made in the same pass as the max-pooled operand of
+// the next level's first conv (one read of the activation instead of two)
+template <int MODE, bool POOL, bool BF, int U, int NT, bool SKIP = false>
 __global__ __launch_bounds__(256) void frame_stream_kernel(StreamArgs a) {
   const int tid = threadIdx.x;
   const int c = 8 * (tid & ((1 << a.lg) - 1));
@@ -415,18 +441,18 @@ __global__ __launch_bounds__(256) void frame_stream_kernel(StreamArgs a) {
       // past the end: the clamped pixel's own value rewritten to it (identical bytes), so the stores
       // are unconditional too and the compiler can count the loads still in flight at each store
       const unsigned p = min(base + pr + j * pb, plast);
-      float4 r[2];
+      float4 r[2], tq[4][2];
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         if (POOL) {
-          float4 m = d[j].v[k];
-          if (MODE == PMU_SRC_BNRELU) m = bnrelu4(m, sc[k], sh[k]);
 #pragma unroll
-          for (int q = 1; q < 4; ++q) {
-            float4 t = d[j].v[2 * q + k];
-            if (MODE == PMU_SRC_BNRELU) t = bnrelu4(t, sc[k], sh[k]);
-            m = max4(m, t);
+          for (int q = 0; q < 4; ++q) {
+            tq[q][k] = d[j].v[2 * q + k];
+            if (MODE == PMU_SRC_BNRELU) tq[q][k] = bnrelu4(tq[q][k], sc[k], sh[k]);
           }
+          float4 m = tq[0][k];
+#pragma unroll
+          for (int q = 1; q < 4; ++q) m = max4(m, tq[q][k]);
           r[k] = m;
         } else if (MODE == PMU_SRC_BNRELU) {
           r[k] = bnrelu4(d[j].v[k], sc[k], sh[k]);
@@ -436,21 +462,14 @@ __global__ __launch_bounds__(256) void frame_stream_kernel(StreamArgs a) {
           r[k] = d[j].v[k];
         }
       }
-      if (BF) {
-        uint4* o = reinterpret_cast<uint4*>(static_cast<unsigned short*>(a.out) + (size_t)p * a.ldo + c);
-        const uint4 v = make_uint4(pmu_pk_bf16(r[0].x, r[0].y), pmu_pk_bf16(r[0].z, r[0].w),
-                                   pmu_pk_bf16(r[1].x, r[1].y), pmu_pk_bf16(r[1].z, r[1].w));
-        if (NT & 2) __builtin_nontemporal_store(stream_u4{v.x, v.y, v.z, v.w}, reinterpret_cast<stream_u4*>(o));
-        else *o = v;
-      } else {
-        float4* o = reinterpret_cast<float4*>(static_cast<float*>(a.out) + (size_t)p * a.ldo + c);
-        if (NT & 2) {
-          __builtin_nontemporal_store(stream_f4{r[0].x, r[0].y, r[0].z, r[0].w}, reinterpret_cast<stream_f4*>(o));
-          __builtin_nontemporal_store(stream_f4{r[1].x, r[1].y, r[1].z, r[1].w}, reinterpret_cast<stream_f4*>(o + 1));
-        } else {
-          o[0] = r[0];
-          o[1] = r[1];
-        }
+      stream_st8<BF, NT>(a.out, (size_t)p * a.ldo + c, r[0], r[1]);
+      if constexpr (POOL && SKIP) {
+        const unsigned t = p / (unsigned)a.W, w = p - t * (unsigned)a.W;
+        const unsigned n = t / (unsigned)a.H, h = t - n * (unsigned)a.H;
+        const size_t sp = ((size_t)n * a.SH + 2 * h) * a.SW + 2 * w;
+        const size_t so[4] = {sp, sp + 1, sp + a.SW, sp + a.SW + 1};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) stream_st8<BF, NT>(a.out2, so[q] * a.ldo2 + c, tq[q][0], tq[q][1]);
       }
     }
   };
@@ -488,7 +507,9 @@ static bool stream_ok(const pmu_frame* f, int Cout) {
 
 template <bool BF, int NT, int U_POOL, int U_FLAT, int U_BWD>
 static void launch_stream_nt(const pmu_src& s, dim3 grid, dim3 blk, hipStream_t st, const StreamArgs& a) {
-  if (s.pool == PMU_POOL_MAX2) {
+  if (a.out2) {  // (pool_skip_ok: BNRELU, max-pooled)
+    hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_BNRELU, true, BF, U_POOL, NT, true>), grid, blk, 0, st, a);
+  } else if (s.pool == PMU_POOL_MAX2) {
     if (s.mode == PMU_SRC_BNRELU) hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_BNRELU, true, BF, U_POOL, NT>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_RAW, true, BF, U_POOL, NT>), grid, blk, 0, st, a);
   } else if (s.mode == PMU_SRC_BNRELU) {
@@ -501,10 +522,11 @@ static void launch_stream_nt(const pmu_src& s, dim3 grid, dim3 blk, hipStream_t 
 }
 
 template <bool BF>
-static int launch_stream(const pmu_frame* f, void* out, int ldo, hipStream_t st) {
+static int launch_stream(const pmu_frame* f, void* out, int ldo, hipStream_t st, void* out2 = nullptr, int ldo2 = 0) {
   const pmu_src& s = f->src[0];
   StreamArgs a;
   a.x = s.x; a.z = s.z; a.coef = s.coef; a.out = out;
+  a.out2 = out2; a.ldo2 = ldo2;
   a.C = s.C;
   a.lg = 0;
   while ((8 << a.lg) < s.C) ++a.lg;
@@ -680,4 +702,26 @@ extern "C" int pmu_frame_to_bf16_ld(const pmu_frame* f, int Cpad, unsigned short
                      make_dev_frame(f), Cpad, (unsigned)units, out, ldo);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
+}
+
+// The max-pooled BN+ReLU operand of a down block's first conv and, in the same pass, the unpooled
+// activation into the first channels of the Up block's concat operand (pixel stride ldo_skip; see
+// pmu_frame_to_bf16_ld): one read of the activation instead of two.  f: the pooled frame (one fp32
+// BN+ReLU source, max-pooled, even source dims, channels a power-of-two multiple of 8 up to 2048).
+extern "C" int pmu_frame_pool_skip_ok(const pmu_frame* f) {
+  if (!valid_frame(f, true) || !stream_ok(f, f->src[0].C)) return 0;
+  const pmu_src& s = f->src[0];
+  return s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNRELU && s.H == 2 * f->H && s.W == 2 * f->W &&
+         (long long)f->N * s.H * s.W < (1LL << 31);
+}
+
+extern "C" int pmu_frame_to_bf16_pool_skip(const pmu_frame* f, unsigned short* out, unsigned short* skip, int ldo_skip,
+                                           void* stream) {
+  PMU_REQUIRE(out && skip && pmu_frame_pool_skip_ok(f) && ldo_skip >= f->src[0].C && ldo_skip % 8 == 0);
+  return launch_stream<true>(f, out, f->src[0].C, (hipStream_t)stream, skip, ldo_skip);
+}
+
+extern "C" int pmu_frame_to_f32_pool_skip(const pmu_frame* f, float* out, float* skip, int ldo_skip, void* stream) {
+  PMU_REQUIRE(out && skip && pmu_frame_pool_skip_ok(f) && ldo_skip >= f->src[0].C && ldo_skip % 8 == 0);
+  return launch_stream<false>(f, out, f->src[0].C, (hipStream_t)stream, skip, ldo_skip);
 }

@@ -97,6 +97,9 @@ SIGNATURES = {
     "pmu_frame_to_f32": (c_int, [_FP, c_void_p, c_void_p]),
     "pmu_frame_to_f32_ld": (c_int, [_FP, c_void_p, c_int, c_void_p]),
     "pmu_frame_to_bf16_ld": (c_int, [_FP, c_int, c_void_p, c_int, c_void_p]),
+    "pmu_frame_pool_skip_ok": (c_int, [_FP]),
+    "pmu_frame_to_bf16_pool_skip": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p]),
+    "pmu_frame_to_f32_pool_skip": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p]),
     "pmu_conv3x3_wgrad_ws_bf16": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_conv3x3_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                        c_size_t, c_void_p]),

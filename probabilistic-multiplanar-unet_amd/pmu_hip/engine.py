@@ -761,12 +761,44 @@ class UNetState:
     """Everything the backward needs from one forward."""
 
     def __init__(self):
+        self.xcat = {}          # level -> Up-block concat operand whose skip half the encoder wrote
         self.x = None
         self.planes = None
         self.enc: list = []     # per level: (c1, c2) ConvBNOut
         self.ups: list = []     # per up block: UpState
         self.y = None           # head output (NCHW)
         self.feat_src = None    # last DoubleConv output producer
+
+
+def _pool_skip(up, prev: ConvBNOut, srcs, N, h, w, bf16):
+    """(pooled operand, concat operand) from one pass over prev's activation
+    (pmu_frame_to_*_pool_skip), when the Up block that takes prev as its skip will build its concat
+    operand in place (see unet_forward's decoder: no F.pad, 8-channel halves, the conv staging a
+    materialised operand); else None.  The concat tensor's other half is the transposed conv's."""
+    if prev.z.dtype != F32 or 2 * h != prev.z.shape[1] or 2 * w != prev.z.shape[2]:
+        return None
+    Cskip, Cup = prev.z.shape[3], up.up.out_channels
+    Ccat, Cout1 = Cskip + Cup, _dc_layers(up.conv)[0].out_channels
+    hs, ws_ = 2 * h, 2 * w
+    if Cskip % 8 or Cup % 8:
+        return None
+    lb = L.lib()
+    if bf16:
+        if not (lb.pmu_convT2x2_dma_ok(up.up.in_channels, Cup, 0) and dma_ok(hs, ws_, Ccat, Cout1, Cout1)
+                and (dma_ok(h, w, Cskip, Cout1, Cout1) or raw_ok(N, h, w, Cskip))):
+            return None
+    elif not (use_wino() and (wino4_ok(Ccat, hs, ws_, "fwd") or wino_raw_ok(Ccat))):
+        return None
+    f = frame_of(srcs, N, h, w)
+    if not lb.pmu_frame_pool_skip_ok(f):
+        return None
+    dev = prev.z.device
+    dt = BF16S if bf16 else F32
+    pooled = torch.empty(N, h, w, Cskip, dtype=dt, device=dev)
+    xcat = torch.empty(N, hs, ws_, Ccat, dtype=dt, device=dev)
+    L.call("pmu_frame_to_bf16_pool_skip" if bf16 else "pmu_frame_to_f32_pool_skip", f, pooled.data_ptr(),
+           xcat.data_ptr(), Ccat, L.stream())
+    return pooled, xcat
 
 
 def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep: bool = False):
@@ -800,13 +832,19 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
     o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev, bf16=bf16, keep=keep, zb=zb)
     st.enc.append((o1, o2))
     h, w = H, W
+    nlev = len(net.down_blocks) + 1
     for down in net.down_blocks:
         dc = down.maxpool_conv[1]
         c1w, b1, c2w, b2 = _dc_layers(dc)
         prev = st.enc[-1][1]
         h, w = h // 2, w // 2
         srcs = [prev.act(L.POOL_MAX2)]
-        if bf16 and not raw_ok(N, h, w, _pad8(prev.z.shape[3])):
+        pre = _pool_skip(net.up_blocks[nlev - 2 - (len(st.enc) - 1)], prev, srcs, N, h, w, bf16)
+        if pre is not None:
+            # the pooled operand and the Up block's concat operand (skip half) in one pass over prev
+            srcs = [Src(pre[0])]
+            st.xcat[len(st.enc) - 1] = pre[1]
+        elif bf16 and not raw_ok(N, h, w, _pad8(prev.z.shape[3])):
             # fused bf16 fallback: the max-pooled activation materialised once, read raw by every
             # column block (the pipelined fused kernel has no pooled staging)
             pooled = _empty(N, h, w, prev.z.shape[3], device=dev)
@@ -820,6 +858,7 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
     nlev = len(st.enc)
     for j, up in enumerate(net.up_blocks):
         skip = st.enc[nlev - 2 - j][1]
+        xpre = st.xcat.pop(nlev - 2 - j, None)
         hs, ws_ = skip.z.shape[1], skip.z.shape[2]
         hi, wi = cur.z.shape[1], cur.z.shape[2]
         convT = up.up
@@ -845,22 +884,27 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         else:
             direct = (direct and use_wino() and (wino4_ok(Ccat, hs, ws_, "fwd") or wino_raw_ok(Ccat)) and
                       bool(lb.pmu_convT2x2_fwd_ld_ok(fin, Cup)))
+        # (xpre: the encoder already wrote the skip half, with the next level's pooled operand)
+        ready = xpre is not None and xpre.shape == (N, hs, ws_, Ccat) and xpre.dtype == (BF16S if bf16 else F32)
         if direct and bf16:
-            xcat = torch.empty(N, hs, ws_, Ccat, dtype=BF16S, device=dev)
+            xcat = xpre if ready else torch.empty(N, hs, ws_, Ccat, dtype=BF16S, device=dev)
             xtT = frame_to_bf16([cur.act()], N, hi, wi)
             wpt = pack_convT_weights_dma(convT.weight, dgrad=False)
             L.call("pmu_convT2x2_fwd_dma_ldb", xtT.data_ptr(), xtT.shape[3], N, hi, wi, wpt.data_ptr(),
                    L.ptr(convT.bias), Cin_t, Cup, xcat.data_ptr() + 2 * Cskip, Ccat, L.stream())
-            L.call("pmu_frame_to_bf16_ld", frame_of([skip.act()], N, hs, ws_), Cskip, xcat.data_ptr(), Ccat, L.stream())
+            if not ready:
+                L.call("pmu_frame_to_bf16_ld", frame_of([skip.act()], N, hs, ws_), Cskip, xcat.data_ptr(), Ccat,
+                       L.stream())
             if not keep:
                 xtT = None
             u, srcs = None, [Src(xcat)]
         elif direct:
-            xcat = _empty(N, hs, ws_, Ccat, device=dev)
+            xcat = xpre if ready else _empty(N, hs, ws_, Ccat, device=dev)
             wpt = pack_convT_weights(convT.weight, dgrad=False)
             L.call("pmu_convT2x2_fwd_ld", fin, convT.weight.data_ptr(), wpt.data_ptr(), L.ptr(convT.bias), Cup,
                    xcat.data_ptr() + 4 * Cskip, Ccat, L.stream())
-            L.call("pmu_frame_to_f32_ld", frame_of([skip.act()], N, hs, ws_), xcat.data_ptr(), Ccat, L.stream())
+            if not ready:
+                L.call("pmu_frame_to_f32_ld", frame_of([skip.act()], N, hs, ws_), xcat.data_ptr(), Ccat, L.stream())
             u, srcs = None, [Src(xcat)]
         else:
             u = _empty(N, 2 * hi, 2 * wi, Cup, device=dev)

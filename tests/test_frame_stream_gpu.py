@@ -92,3 +92,36 @@ def test_frame_stream_ld(dev, bf, kind, C, ldo):
     gen = _run(src, N, H, W, C, bf, ldo, generic=True)
     assert torch.equal(got, gen)
     assert (got[..., C:] == -7).all()
+
+
+@pytest.mark.parametrize("bf", [True, False])
+@pytest.mark.parametrize("N,H,W,C,Ccat", [(2, 8, 8, 64, 128), (3, 5, 7, 128, 192), (1, 16, 4, 8, 16)])
+def test_frame_pool_skip(dev, bf, N, H, W, C, Ccat):
+    """pmu_frame_to_*_pool_skip: the max-pooled operand and the unpooled skip half of the concat operand
+    from one pass, bit-equal to pmu_frame_to_* of the pooled frame + pmu_frame_to_*_ld of the unpooled
+    one (unet_parts.py:33 and :66); the concat's other channels untouched."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_of
+    src, _ = _frame("pool", N, H, W, C, dev)
+    dt = torch.int16 if bf else torch.float32
+    f = frame_of([src], N, H, W)
+    assert L.lib().pmu_frame_pool_skip_ok(f)
+    pooled = torch.full((N, H, W, C), -3, dtype=dt, device=dev)
+    xcat = torch.full((N, 2 * H, 2 * W, Ccat), -7, dtype=dt, device=dev)
+    L.call("pmu_frame_to_bf16_pool_skip" if bf else "pmu_frame_to_f32_pool_skip", f, pooled.data_ptr(),
+           xcat.data_ptr(), Ccat, L.stream())
+    torch.cuda.synchronize()
+    ref_pool = _run(src, N, H, W, C, bf, C, generic=True)
+    unpooled = Src(src.x, src.mode, src.coef)
+    ref_skip = _run(unpooled, N, 2 * H, 2 * W, C, bf, Ccat, generic=True)
+    assert torch.equal(pooled, ref_pool)
+    assert torch.equal(xcat[..., :C], ref_skip[..., :C])
+    assert (xcat[..., C:] == -7).all()
+
+
+def test_frame_pool_skip_refuses_odd_sources(dev):
+    """Floor-mode pooling of an odd map leaves a row / column outside every window: not this path."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import frame_of
+    src, _ = _frame("pool", 1, 5, 5, 64, dev, odd=True)
+    assert not L.lib().pmu_frame_pool_skip_ok(frame_of([src], 1, 5, 5))
