@@ -218,6 +218,16 @@ int pmu_conv3x3_dgrad_dma(const unsigned short* dzt, int Cp, int N, int H, int W
  * bf16 operand (unet_parts.py:52,66 under autocast) — no separate pmu_frame_to_bf16 pass over dx1 */
 int pmu_conv3x3_dgrad_dma_x1b(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                               int Cin, int Csplit, float* dx0, float* dx1, unsigned short* dx1b, void* stream);
+/* the same without the fp32 dx1 (only dx1b), plus part[tile][0][Cin] = per-tile column sums of dx
+ * (part[tile][1][*] = 0; tiles = pmu_conv3x3_tiles_dma(N, H, W, Cin, Cp)): the transposed conv's bias
+ * gradient (unet_parts.py:52 backward) is the sum over tiles of channels [Csplit, Cin)
+ * (pmu_convT2x2_dbias_rows). */
+int pmu_conv3x3_dgrad_dma_x1b_sum(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                  int Cin, int Csplit, float* dx0, unsigned short* dx1b, float* part, void* stream);
+/* dbias[c] = sum over r < R of part[r * ld + c], c < Cout, in a fixed order; ws holds
+ * pmu_convT2x2_dbias_rows_ws(Cout) bytes. */
+size_t pmu_convT2x2_dbias_rows_ws(int Cout);
+int pmu_convT2x2_dbias_rows(const float* part, int R, long long ld, int Cout, float* dbias, float* ws, void* stream);
 /* as pmu_conv3x3_dgrad_wino2h_bnr (part rows = pmu_conv3x3_tiles_dma(N, H, W, Cin, Cp)) */
 int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                               int Cin, float* dx, const float* z, const float* coef, const float* mean,

@@ -118,7 +118,10 @@ __global__ __launch_bounds__(256) void pack_dma_multi_kernel(const pmu_pack_job*
 // of overlapping.  Measured and dropped: a phase offset between the two workgroups of a CU (s_sleep
 // before the first round: no change) and 16-B stores through an LDS transpose (-2..5% on K <= 128
 // only).
-template <bool DGRAD, bool ZB, int WN, int NWV, int EXP = 0>
+// CS (input gradient): per-tile column sums of dx into a.part instead of the BN-backward partials
+// (pmu_conv3x3_dgrad_dma_x1b_sum; a compile-time variant: as a runtime branch beside the a.bz one it
+// spilled 89 VGPRs)
+template <bool DGRAD, bool ZB, int WN, int NWV, int EXP = 0, bool CS = false>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs a) {
   using G = DG<WN, NWV>;
   constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH, NT = G::NT;
@@ -295,8 +298,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       int ld;
       unsigned short* dstb = nullptr;  // (uniform per fragment)
       if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
-      else {
-        dstp = a.out1 + (j - a.split);
+      else {  // (out1 null: only the bf16 copy, pmu_conv3x3_dgrad_dma_x1b_sum)
+        dstp = a.out1 ? a.out1 + (j - a.split) : nullptr;
         ld = a.NOUT - a.split;
         if (a.out1b) dstb = a.out1b + (j - a.split);
       }
@@ -309,12 +312,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
           if (!jok || h >= a.H || w >= a.W) continue;
           const long long pix = ((long long)n * a.H + h) * a.W + w;
           PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-          dstp[pix * ld] = acc[fm][fn][r];
+          if (!CS || dstp) dstp[pix * ld] = acc[fm][fn][r];  // (only the CS variant has a null out1)
           if (dstb) dstb[pix * ld] = bf16_bits(acc[fm][fn][r]);
         }
       }
     }
-    if (a.bz) {
+    if (!CS && a.bz) {
   #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const int j = j0 + wn * 64 + fn * 32 + li;
@@ -338,6 +341,20 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
             const float gg = (ok && fmaf(zt[r], bsc, bsh) > 0.f) ? acc[fm][fn][r] : 0.f;
             s1[fn] += gg;
             s2[fn] = fmaf(gg, (zt[r] - bmu) * bis, s2[fn]);
+          }
+        }
+      }
+    } else if (CS) {  // per-tile column sums of dx (x1b_sum: the transposed conv's bias gradient)
+  #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const bool jok = j0 + wn * 64 + fn * 32 + li < a.NOUT;
+  #pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int h = h0 + 4 * wm + fm;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const bool ok = jok && h < a.H && w0 + acc_row(r, lane) < a.W;
+            s1[fn] += ok ? acc[fm][fn][r] : 0.f;
           }
         }
       }
@@ -388,8 +405,8 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
                       const float* binv = nullptr, int zbf = 0, const float* zoff = nullptr,
                       unsigned short* out1b = nullptr) {
   PMU_REQUIRE(x && wp && out0 && N > 0 && H > 0 && W >= 32 && Cp > 0 && Cp % BK == 0 && NOUT > 0);
-  PMU_REQUIRE(!out1b || (dgrad && out1));
-  PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && out1));
+  PMU_REQUIRE(!out1b || dgrad);
+  PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && (out1 || out1b)));
   const Shape sh = dma_shape(NOUT, Cp);
   const long long img_bytes = (long long)H * W * Cp * 2;
   if ((long long)N * img_bytes >= (1LL << 32)) {  // 32-bit DMA byte offsets: split over images
@@ -446,7 +463,10 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
     }
   }
 #endif
-  if (dgrad && zb) PMU_DMA_LAUNCH(true, true)
+  if (dgrad && part && !bz) {  // column sums (pmu_conv3x3_dgrad_dma_x1b_sum)
+    if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, true>), grid, blk, 0, st, a);
+  } else if (dgrad && zb) PMU_DMA_LAUNCH(true, true)
   else if (dgrad) PMU_DMA_LAUNCH(true, false)
   else if (zb) PMU_DMA_LAUNCH(false, true)
   else PMU_DMA_LAUNCH(false, false)
@@ -500,6 +520,18 @@ extern "C" int pmu_conv3x3_dgrad_dma_x1b(const unsigned short* dzt, int Cp, int 
                                          unsigned short* dx1b, void* stream) {
   PMU_REQUIRE(dx1 && dx1b && Csplit < Cin && (Cin - Csplit) % 8 == 0);
   return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream, nullptr, nullptr,
+                    nullptr, nullptr, 0, nullptr, dx1b);
+}
+
+// As pmu_conv3x3_dgrad_dma_x1b with dx1 kept only in bf16, plus per-tile column sums of dx in
+// part[tile][0][Cin] (part[tile][1][*] = 0; tiles = pmu_conv3x3_tiles_dma(N, H, W, Cin, Cp)): the
+// transposed conv's bias gradient is the sum over tiles of channels [Csplit, Cin)
+// (pmu_convT2x2_dbias_rows), so its fp32 du is neither written nor re-read.
+extern "C" int pmu_conv3x3_dgrad_dma_x1b_sum(const unsigned short* dzt, int Cp, int N, int H, int W,
+                                             const unsigned short* wp, int Cin, int Csplit, float* dx0,
+                                             unsigned short* dx1b, float* part, void* stream) {
+  PMU_REQUIRE(dx1b && part && Csplit < Cin && (Cin - Csplit) % 8 == 0);
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx0, nullptr, Csplit, part, true, stream, nullptr, nullptr,
                     nullptr, nullptr, 0, nullptr, dx1b);
 }
 

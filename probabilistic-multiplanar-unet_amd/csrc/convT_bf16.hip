@@ -431,16 +431,17 @@ __global__ __launch_bounds__(256) void convT_dbias_part1_kernel(const float* __r
     part[(long long)blockIdx.x * Cout + c] = s;
   }
 }
-// db[c] = sum of the G partial rows: 64 channels per block, 4 row groups summed in a fixed order
+// db[c] = sum of the G partial rows (row stride ld): 64 channels per block, 4 row groups summed in a
+// fixed order
 __global__ __launch_bounds__(256) void convT_dbias_sum_kernel(const float* __restrict__ part, int G, int Cout,
-                                                              float* __restrict__ db) {
+                                                              long long ld, float* __restrict__ db) {
   __shared__ float red[256];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
   float s = 0.f;
   if (c < Cout) {
     const int g0 = (G * grp) / 4, g1 = (G * (grp + 1)) / 4;
 #pragma unroll 4
-    for (int gidx = g0; gidx < g1; ++gidx) s += part[(long long)gidx * Cout + c];
+    for (int gidx = g0; gidx < g1; ++gidx) s += part[(long long)gidx * ld + c];
   }
   red[threadIdx.x] = s;
   __syncthreads();
@@ -559,8 +560,46 @@ extern "C" int pmu_convT2x2_wgrad_bf16(const unsigned short* xt, const unsigned 
                          off_w, Cout, part);
     PMU_CHECK_LAUNCH();
     hipLaunchKernelGGL(convT_dbias_sum_kernel, dim3((unsigned)pmu_cdiv(Cout, 64)), dim3(256), 0, st, (const float*)part,
-                       DB_G, Cout, dbias);
+                       DB_G, Cout, (long long)Cout, dbias);
     PMU_CHECK_LAUNCH();
   }
+  return PMU_OK;
+}
+
+// dbias[c] = sum over r < R of part[r * ld + c] (c < Cout), fixed order: the bias gradient from the
+// per-tile column sums of pmu_conv3x3_dgrad_dma_x1b_sum (part + Csplit, ld = 2 Cin).  Two passes: the
+// rows in DB_RG contiguous groups (one block per 64 channels x group: thousands of rows per channel
+// are a latency chain for one block) into ws[DB_RG][Cout], then those rows in order.
+static constexpr int DB_RG = 64;
+static __global__ __launch_bounds__(256) void dbias_rows_part_kernel(const float* __restrict__ part, int R, int Cout,
+                                                              long long ld, float* __restrict__ ws) {
+  const int g = blockIdx.y, r0 = (int)((long long)R * g / DB_RG), r1 = (int)((long long)R * (g + 1) / DB_RG);
+  // (the one-block sum kernel over this group's rows, its 4 row sub-groups in order)
+  __shared__ float red[256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < Cout) {
+    const int a0 = r0 + ((r1 - r0) * grp) / 4, a1 = r0 + ((r1 - r0) * (grp + 1)) / 4;
+#pragma unroll 4
+    for (int r = a0; r < a1; ++r) s += part[(long long)r * ld + c];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (grp == 0 && c < Cout)
+    ws[(long long)g * Cout + c] = ((red[threadIdx.x] + red[64 + threadIdx.x]) + red[128 + threadIdx.x]) + red[192 + threadIdx.x];
+}
+
+extern "C" size_t pmu_convT2x2_dbias_rows_ws(int Cout) { return (size_t)DB_RG * Cout * sizeof(float); }
+
+extern "C" int pmu_convT2x2_dbias_rows(const float* part, int R, long long ld, int Cout, float* dbias, float* ws,
+                                       void* stream) {
+  PMU_REQUIRE(part && dbias && ws && R > 0 && Cout > 0 && ld >= Cout);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(dbias_rows_part_kernel, dim3((unsigned)pmu_cdiv(Cout, 64), DB_RG), dim3(256), 0, st, part, R,
+                     Cout, ld, ws);
+  PMU_CHECK_LAUNCH();
+  hipLaunchKernelGGL(convT_dbias_sum_kernel, dim3((unsigned)pmu_cdiv(Cout, 64)), dim3(256), 0, st, (const float*)ws,
+                     DB_RG, Cout, (long long)Cout, dbias);
+  PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -200,6 +200,10 @@ SIGNATURES = {
                                       c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_dma_x1b": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                           c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_x1b_sum": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                              c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_convT2x2_dbias_rows_ws": (c_size_t, [c_int]),
+    "pmu_convT2x2_dbias_rows": (c_int, [c_void_p, c_int, c_longlong, c_int, c_void_p, c_void_p, c_void_p]),
     "pmu_convT2x2_dma_ok": (c_int, [c_int, c_int, c_int]),
     "pmu_convT2x2_packed_size_dma": (c_size_t, [c_int, c_int]),
     "pmu_convT2x2_pack_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

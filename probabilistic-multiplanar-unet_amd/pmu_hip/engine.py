@@ -368,11 +368,13 @@ def tee32_ok(cin: int, cout: int) -> bool:
     return cin % 64 == 0 and cout % 64 == 0
 
 
-def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, need_dx=True, split=None):
+def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, need_dx=True, split=None,
+                     x1_bf16_only=False):
     """Backward of relu(bn(conv(operand))) given da (NHWC).  Writes conv/bn grads into ``grads``.
 
     Returns the operand gradient(s): one NHWC tensor, or (dx0, dx1) when ``split`` is given
-    (channel split of a concatenated operand)."""
+    (channel split of a concatenated operand).  x1_bf16_only (bf16 convs): the caller needs dx1 only as
+    the transposed conv's bf16 operand and its column sums (see _conv_backward_bf16)."""
     s = L.stream()
     z = out.z
     N, H, W, Cout = z.shape
@@ -388,7 +390,7 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     lb = L.lib()
     prod = _bnr_producer(out, need_dx, split)
     if out.bf16:
-        return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split, prod)
+        return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split, prod, x1_bf16_only)
     if out.xt32 is not None and need_dx:
         return _conv_backward_tee32(out, dz_src, conv, dw, split, prod)
     if out.planes is not None:
@@ -515,7 +517,7 @@ def raw_ok(N, H, W, Cp) -> bool:
     return N * H * W * Cp < 2 ** 31
 
 
-def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, prod=None):
+def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, prod=None, x1_bf16_only=False):
     """bf16-MFMA backward of one conv layer (torch.autocast(bfloat16) arithmetic).  dz after the
     BN+ReLU backward is written once in bf16 (dzt); the input gradient streams it (or, for a concat
     split that is not a multiple of 32, stages dz's frame in the fused kernel) and the weight
@@ -529,8 +531,19 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
     if need_dx:
         sp = Cin if split is None else split
         dx0 = _empty(N, H, W, sp, device=dev)
-        dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin else None
-        if dma_ok(H, W, dzt.shape[3], Cin, sp):
+        x1only = x1_bf16_only and sp < Cin and (Cin - sp) % 8 == 0 and dma_ok(H, W, dzt.shape[3], Cin, sp)
+        dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin and not x1only else None
+        if x1only:
+            # dx1 only in bf16 (the transposed conv's operand) with per-tile column sums (its bias gradient):
+            # the fp32 dx1 is neither written nor re-read
+            wp = pack_weights_dma(conv.weight, dgrad=True)
+            R = L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3])
+            part = _empty(R, 2 * Cin, device=dev)
+            dx1 = torch.empty(N, H, W, Cin - sp, dtype=BF16S, device=dev)
+            L.call("pmu_conv3x3_dgrad_dma_x1b_sum", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
+                   dx0.data_ptr(), dx1.data_ptr(), part.data_ptr(), s)
+            dx1._pmu_dbpart = (part, R, sp)
+        elif dma_ok(H, W, dzt.shape[3], Cin, sp):
             wp = pack_weights_dma(conv.weight, dgrad=True)
             if prod is not None:
                 _bnr_call("pmu_conv3x3_dgrad_dma_bnr_zb" if prod.z.dtype == BF16S else "pmu_conv3x3_dgrad_dma_bnr",
@@ -994,17 +1007,23 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         da1 = conv_bn_backward(us.c2, da, c2w, b2, grads)
         grads.flush()
         Cskip = us.cskip
-        dsk, dup = conv_bn_backward(us.c1, da1, c1w, b1, grads, split=Cskip)
-        grads.flush()
-        dskip[nlev - 2 - j] = dsk
         convT = up.up
         prev = us.prev
         hi, wi, Cin_t = prev.z.shape[1], prev.z.shape[2], prev.z.shape[3]
-        Hd, Wd = dup.shape[1], dup.shape[2]
         Cup = convT.out_channels
+        # bf16 with the LDS-DMA transposed-conv input gradient and no F.pad: dup is needed only in bf16 and
+        # for the bias gradient's column sums, which the concat input gradient forms in its epilogue
+        x1only = bool(us.bf16 and us.off == (0, 0) and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 1))
+        dsk, dup = conv_bn_backward(us.c1, da1, c1w, b1, grads, split=Cskip, x1_bf16_only=x1only)
+        grads.flush()
+        dskip[nlev - 2 - j] = dsk
+        Hd, Wd = dup.shape[1], dup.shape[2]
         dx = _empty(N, hi, wi, Cin_t, device=dev)
         dut = None
-        if us.bf16:   # the concat dgrad's bf16 copy of dup when it wrote one (pmu_conv3x3_dgrad_dma_x1b)
+        dbpart = getattr(dup, "_pmu_dbpart", None)
+        if dbpart is not None:
+            dut = dup
+        elif us.bf16:   # the concat dgrad's bf16 copy of dup when it wrote one (pmu_conv3x3_dgrad_dma_x1b)
             dut = getattr(dup, "_pmu_bf16", None)
             dut = dut if dut is not None else frame_to_bf16([Src(dup)], N, Hd, Wd)
         if us.bf16 and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 1):
@@ -1027,8 +1046,17 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             us.xt = None
             wsb = L.lib().pmu_convT2x2_wgrad_ws_bf16(N, hi, wi, Cin_t, Cup)
             ws = _empty(max(1, (wsb + 3) // 4), device=dev)
-            L.call("pmu_convT2x2_wgrad_bf16", xt.data_ptr(), dut.data_ptr(), dup.data_ptr(), N, hi, wi, Hd, Wd,
-                   us.off[0], us.off[1], Cin_t, Cup, dwt.data_ptr(), L.ptr(dbt), ws.data_ptr(), wsb, s)
+            if dbpart is not None:
+                L.call("pmu_convT2x2_wgrad_bf16", xt.data_ptr(), dut.data_ptr(), None, N, hi, wi, Hd, Wd,
+                       0, 0, Cin_t, Cup, dwt.data_ptr(), None, ws.data_ptr(), wsb, s)
+                if dbt is not None:
+                    part, R, sp = dbpart
+                    wsd = _empty(L.lib().pmu_convT2x2_dbias_rows_ws(Cup) // 4, device=dev)
+                    L.call("pmu_convT2x2_dbias_rows", part.data_ptr() + 4 * sp, R, part.shape[1], Cup,
+                           dbt.data_ptr(), wsd.data_ptr(), s)
+            else:
+                L.call("pmu_convT2x2_wgrad_bf16", xt.data_ptr(), dut.data_ptr(), dup.data_ptr(), N, hi, wi, Hd, Wd,
+                       us.off[0], us.off[1], Cin_t, Cup, dwt.data_ptr(), L.ptr(dbt), ws.data_ptr(), wsb, s)
             del xt, dut
         else:
             wsb = L.lib().pmu_convT2x2_wgrad_ws(N, hi, wi, Cin_t, Cup)

@@ -117,6 +117,39 @@ def test_dgrad_dma_split_bf16_copy(dev, N, H, W, Cskip, Cup, Cout):
     assert torch.equal(dx1b, ref_b)
 
 
+@pytest.mark.parametrize("N,H,W,Cskip,Cup,Cout", [(2, 64, 64, 64, 64, 64), (1, 33, 45, 128, 64, 96)])
+def test_dgrad_dma_split_bf16_colsum(dev, N, H, W, Cskip, Cup, Cout):
+    """pmu_conv3x3_dgrad_dma_x1b_sum: dx0 / dx1b bit-equal to pmu_conv3x3_dgrad_dma_x1b, no fp32 dx1, and
+    pmu_convT2x2_dbias_rows over its per-tile column sums = the transposed conv's bias gradient, the
+    sum of dx1 over all pixels (unet_parts.py:52 backward), to fp32 summation rounding."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_to_bf16, pack_weights_dma
+    g = torch.Generator().manual_seed(29 + H + Cskip)
+    Cin = Cskip + Cup
+    dz = torch.randn(N, H, W, Cout, generator=g).to(dev)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).to(dev)
+    dzt = frame_to_bf16([Src(dz)], N, H, W)
+    wp = pack_weights_dma(w, True)
+    dx0, dx1b = torch.empty(N, H, W, Cskip, device=dev), torch.empty(N, H, W, Cup, dtype=torch.int16, device=dev)
+    R = L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3])
+    part = torch.full((R, 2 * Cin), float("nan"), device=dev)
+    L.call("pmu_conv3x3_dgrad_dma_x1b_sum", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, Cskip,
+           dx0.data_ptr(), dx1b.data_ptr(), part.data_ptr(), L.stream())
+    db = torch.empty(Cup, device=dev)
+    wsd = torch.empty(L.lib().pmu_convT2x2_dbias_rows_ws(Cup) // 4, device=dev)
+    L.call("pmu_convT2x2_dbias_rows", part.data_ptr() + 4 * Cskip, R, 2 * Cin, Cup, db.data_ptr(), wsd.data_ptr(),
+           L.stream())
+    r0, r1 = torch.empty_like(dx0), torch.empty(N, H, W, Cup, device=dev)
+    rb = torch.empty_like(dx1b)
+    L.call("pmu_conv3x3_dgrad_dma_x1b", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, Cskip,
+           r0.data_ptr(), r1.data_ptr(), rb.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, r0) and torch.equal(dx1b, rb)
+    ref = r1.double().sum(dim=(0, 1, 2))
+    assert ((db.double() - ref).abs() <= 1e-5 * (r1.double().abs().sum(dim=(0, 1, 2)) + 1)).all()
+    assert (part[:, Cin:] == 0).all()
+
+
 @pytest.mark.parametrize("N,H,W,C", [(2, 64, 64, 64), (1, 33, 45, 32), (2, 16, 16, 512), (1, 7, 9, 1040)])
 def test_maxpool2_bwd_bnr(dev, N, H, W, C):
     """pmu_maxpool2_bwd_bnr: dx bit-equal to pmu_maxpool2_bwd accumulated onto the same skip gradient
