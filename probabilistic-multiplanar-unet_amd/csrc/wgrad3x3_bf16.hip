@@ -24,9 +24,13 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int WCI = 64;     // ci per block
-constexpr int WPIX = 64;    // pixels per K tile
 constexpr int NT = 768;     // 12 waves
-constexpr int MAX_HPX = 108;
+// pixels per K tile: 128 for 64-channel blocks (the 512^2 / 64-channel shapes are load-latency-bound
+// per tile: 0.49 -> 0.42 ms at 64 -> 64, 0.79 -> 0.70 ms at 128 -> 64), 64 for 128-channel blocks
+// (at 128 they spill past the 3-waves-per-SIMD register cap and lose 15%)
+__host__ __device__ constexpr int wpix_of(int wco) { return wco == 64 ? 128 : 64; }
+// the tile's halo image: (TH + 2) x (TW + 2) pixels, TW = 16 or 8
+__host__ __device__ constexpr int hpx_of(int px) { return px == 128 ? 180 : 108; }
 constexpr int XS = WCI + 32;  // X row stride (bf16): 192 B = 64 mod 256 -> tr reads conflict-free
 
 struct WgbArgs {
@@ -39,12 +43,15 @@ struct WgbArgs {
 
 template <int WCO>
 struct Geo {
+  static constexpr int WPIX = wpix_of(WCO);
+  static constexpr int MAX_HPX = hpx_of(WPIX);
   static constexpr int DS = WCO + 32;                 // D row stride (bf16): 320 B / 192 B
   static constexpr int D_ELEMS = WPIX * DS;
   static constexpr int SLOT = D_ELEMS + MAX_HPX * XS;  // one ring slot (bf16 elements)
   static constexpr int DU = WPIX * WCO / 8;            // 16-B units of a D tile
   static constexpr int ND = (DU + NT - 1) / NT;
   static constexpr int NX = (MAX_HPX * WCI / 8 + NT - 1) / NT;
+  static_assert(2 * SLOT * 2 <= 160 * 1024, "two ring slots in LDS");
   static constexpr int FCO = WCO / 64;                 // co fragments per wave (12 waves)
 };
 
@@ -71,7 +78,7 @@ struct TileIO {
 template <int WCO, int TWL>
 __device__ __forceinline__ void tile_load(const WgbArgs& a, int tile, int co0, int ci0, int tid, TileIO<WCO, TWL>& r) {
   using G = Geo<WCO>;
-  constexpr int TW = 1 << TWL, TH = WPIX >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
+  constexpr int TW = 1 << TWL, TH = G::WPIX >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
   int t = tile;
   const int tw = t % a.tiles_w; t /= a.tiles_w;
   const int th = t % a.tiles_h; t /= a.tiles_h;
@@ -107,7 +114,7 @@ __device__ __forceinline__ void tile_load(const WgbArgs& a, int tile, int co0, i
 template <int WCO, int TWL>
 __device__ __forceinline__ void tile_store(const TileIO<WCO, TWL>& r, int tid, unsigned short* slot) {
   using G = Geo<WCO>;
-  constexpr int TW = 1 << TWL, TH = WPIX >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
+  constexpr int TW = 1 << TWL, TH = G::WPIX >> TWL, HW2 = TW + 2, HP = (TH + 2) * HW2;
   unsigned short* Ds = slot;
   unsigned short* Xs = slot + G::D_ELEMS;
 #pragma unroll
@@ -172,7 +179,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_bf16_kernel(WgbArgs a) {
     const unsigned short* Ds = smem + cur * G::SLOT;
     const unsigned short* Xs = Ds + G::D_ELEMS;
 #pragma unroll
-    for (int ks = 0; ks < WPIX / 16; ++ks) {
+    for (int ks = 0; ks < G::WPIX / 16; ++ks) {
       bf16x8 af[FCO], bf[3];
       s16x4 lo, hi;
       // pixel rows of this lane's two reads: 16ks + 8h + 4t + q, t = 0, 1 (same tile row: TW >= 8)
@@ -564,7 +571,7 @@ static void geometry(int N, int H, int W, int Cin, int Cout, int* wco, int* twl,
                      int* ntiles, int* nsplit) {
   *wco = Cout > 64 ? 128 : 64;
   *twl = (W > 8) ? 4 : 3;
-  const int TW = 1 << *twl, TH = WPIX / TW;
+  const int TW = 1 << *twl, TH = wpix_of(*wco) / TW;
   *tiles_w = pmu_cdiv(W, TW);
   *tiles_h = pmu_cdiv(H, TH);
   *ntiles = N * *tiles_w * *tiles_h;
