@@ -30,6 +30,8 @@ for p in (PKG, ROOT):
 
 import torch  # noqa: E402
 
+from pmu_hip._lib import MFMA_ENTRY_POINTS  # noqa: E402  (the table only; the library loads lazily)
+
 METRIC = "2D slices/sec fwd+bwd, 256×256×1 batch32 U-Net; Dice vs ref"
 METRIC_C5 = "2D slices/sec fwd+bwd, 512×512×3 batch16 U-Net bf16 (BASELINE.json configs[4])"
 METRIC_C4 = ("2D slices/sec ProbabilisticUnet train step (prior+posterior, latent 6, KL+CE) + 16 fcomb samples, "
@@ -66,21 +68,14 @@ def conv_flops_per_slice(H, W, filters, n_ch=1, n_cls=1):
 class KernelTimer:
     """HIP-event timing of every launch, with algorithmic FLOPs for the MFMA kernels."""
 
-    MFMA = ("pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad", "pmu_convT2x2_fwd",
-            "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad", "pmu_fcomb_fwd", "pmu_fcomb_bwd",
-            "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16", "pmu_convT2x2_fwd_bf16",
-            "pmu_convT2x2_dgrad_bf16", "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw", "pmu_convT2x2_wgrad_bf16",
-            "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino", "pmu_conv3x3_wgrad_wino",
-            "pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw", "pmu_conv3x3_fwd_wino4",
-            "pmu_conv3x3_dgrad_wino4", "pmu_conv3x3_fwd_wino2h", "pmu_conv3x3_dgrad_wino2h",
-            "pmu_conv3x3_dgrad_wino4_bnr", "pmu_conv3x3_dgrad_wino2h_bnr", "pmu_conv3x3_wgrad_wino4",
-            "pmu_conv3x3_fwd_dma", "pmu_conv3x3_fwd_dma_zb", "pmu_conv3x3_dgrad_dma", "pmu_conv3x3_dgrad_dma_bnr",
-            "pmu_conv3x3_dgrad_dma_bnr_zb", "pmu_convT2x2_fwd_dma", "pmu_convT2x2_dgrad_dma")
+    MFMA = MFMA_ENTRY_POINTS   # pmu_hip._lib: every C-ABI entry whose kernels issue MFMAs
 
     @staticmethod
     def _base(name):
-        """The call family of a fused variant (the BN-backward epilogue / bf16-z forms do the same MFMA work)."""
-        for suf in ("_bnr_zb", "_bnr", "_zb"):
+        """The call family of a fused variant: the BN-backward epilogue (_bnr), bf16-z (_zb), concat-split
+        bf16 copy / column-sum (_x1b, _x1b_sum) and in-place concat (_ld, _ldb) forms take the same
+        leading arguments and do the same MFMA work as the plain call."""
+        for suf in ("_bnr_zb", "_x1b_sum", "_x1b", "_bnr", "_zb", "_ldb", "_ld"):
             if name.endswith(suf):
                 return name[: -len(suf)]
         return name
@@ -419,6 +414,8 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_dgrad_dma": r"conv3x3_dma_kernel<true", "pmu_conv3x3_dgrad_dma_bnr": r"conv3x3_dma_kernel<true",
     "pmu_conv3x3_dgrad_dma_bnr_zb": r"conv3x3_dma_kernel<true",
     "pmu_convT2x2_fwd_dma": r"convT_dma_kernel<false", "pmu_convT2x2_dgrad_dma": r"convT_dma_kernel<true",
+    "pmu_conv3x3_dgrad_dma_x1b": r"conv3x3_dma_kernel<true", "pmu_conv3x3_dgrad_dma_x1b_sum": r"conv3x3_dma_kernel<true",
+    "pmu_convT2x2_fwd_ld": r"convT_pipe_kernel<false", "pmu_convT2x2_fwd_dma_ldb": r"convT_dma_kernel<false",
 }
 
 
@@ -481,6 +478,8 @@ def build_unet(args, dev, world, rank):
     if world > 1:  # identical replicas: broadcast rank 0's weights
         for t in list(net.parameters()) + list(net.buffers()):
             dist.broadcast(t.data, 0)
+        from pmu_hip.engine import invalidate_packs
+        invalidate_packs()   # written through .data: invisible to the packed-weight cache
     opt = FusedSGD(net.parameters(), lr=1e-3, momentum=0.9, clip=0.1)
     sync = dp_sync(net, world)
     g = torch.Generator(device="cpu").manual_seed(1 + rank)
@@ -639,6 +638,8 @@ def build_probunet(args, dev, world, rank):
     if world > 1:
         for t in list(net.parameters()) + list(net.buffers()):
             dist.broadcast(t.data, 0)
+        from pmu_hip.engine import invalidate_packs
+        invalidate_packs()   # written through .data: invisible to the packed-weight cache
     opt = FusedSGD(net.parameters(), lr=1e-3, momentum=0.9, clip=0.1)
     sync = dp_sync(net, world)
     g = torch.Generator(device="cpu").manual_seed(1 + rank)

@@ -106,15 +106,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   const int pg = tid / qstride;
   const int q0 = tid % qstride;
   const long long p0 = (long long)blockIdx.x * ppb;
-  // each thread owns channel quads q0, q0+qstride, ... (only >1 when CQ > 256)
-  for (int q = q0; q < CQ; q += qstride) {
-    const int c = 4 * q;
+  // each thread owns channel quads q0, q0+qstride, ... (only >1 when CQ > 256); every thread runs the
+  // same number of rounds (the barriers below are block-wide), a quad past C only joins the barriers
+  for (int qb = 0; qb < CQ; qb += qstride) {
+    const int q = qb + q0;
+    const int c = 4 * (q < CQ ? q : 0);
     const float4 sc = *reinterpret_cast<const float4*>(coef + c);
     const float4 sh = *reinterpret_cast<const float4*>(coef + C + c);
     const float4 mu = *reinterpret_cast<const float4*>(mean + c);
     const float4 is = *reinterpret_cast<const float4*>(invstd + c);
     float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
-    if (pg < npg) {
+    if (pg < npg && q < CQ) {
       // the block's pixels of this thread, in order; unrolled so 8 loads are in flight per thread
       const long long pend = min(P, p0 + ppb);
       const int nit = pend > p0 + pg ? (int)((pend - p0 - pg + npg - 1) / npg) : 0;
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
 #pragma unroll
     for (int e = 0; e < 4; ++e) { red[tid * 8 + e] = sg[e]; red[tid * 8 + 4 + e] = sgx[e]; }
     __syncthreads();
-    if (pg == 0) {
+    if (pg == 0 && q < CQ) {
       float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
       for (int l = 0; l < npg; ++l) {
         const int src = l * qstride + q0;
@@ -317,8 +319,11 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __re
   const long long nwin = (long long)N * Hc * Wc;
   const long long w0 = (long long)blockIdx.x * wpb;
   const long long wend = min(nwin, w0 + wpb);
-  for (int q = q0; q < CQ; q += qstride) {
-    const int c = 4 * q;
+  // every thread runs the same number of channel-quad rounds (the barriers below are block-wide);
+  // a thread whose quad lies past C in the last round only joins the barriers
+  for (int qb = 0; qb < CQ; qb += qstride) {
+    const int q = qb + q0;
+    const int c = 4 * (q < CQ ? q : 0);
     const float4 sc = *reinterpret_cast<const float4*>(coef + c);
     const float4 sh = *reinterpret_cast<const float4*>(coef + C + c);
     const float4 mu = *reinterpret_cast<const float4*>(mean + c);
@@ -326,7 +331,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __re
     const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
     const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
     float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
-    if (pg < npg) {
+    if (pg < npg && q < CQ) {
       for (long long wi = w0 + pg; wi < wend; wi += npg) {
         const int wc = (int)(wi % Wc);
         const long long r = wi / Wc;
@@ -383,7 +388,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __re
 #pragma unroll
     for (int e = 0; e < 4; ++e) { red[tid * 8 + e] = sg[e]; red[tid * 8 + 4 + e] = sgx[e]; }
     __syncthreads();
-    if (pg == 0) {
+    if (pg == 0 && q < CQ) {
       float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
       for (int l = 0; l < npg; ++l) {
         const int src = l * qstride + q0;

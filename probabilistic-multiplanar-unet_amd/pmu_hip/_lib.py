@@ -242,6 +242,29 @@ SIGNATURES = {
     "pmu_debug_reset": (c_int, []),
 }
 
+# The entry points whose kernels issue MFMAs (every other entry is VALU / memory work).  bench.py's
+# KernelTimer counts exactly these, each with a FLOP formula; tests/test_cpu_host.py checks that every
+# one of them has a non-zero formula and is declared in SIGNATURES.
+MFMA_ENTRY_POINTS = (
+    # fp32 direct-sum and Winograd 3x3 convs (conv3x3*.hip, wgrad3x3*.hip)
+    "pmu_conv3x3_fwd", "pmu_conv3x3_dgrad", "pmu_conv3x3_wgrad",
+    "pmu_conv3x3_fwd_wino", "pmu_conv3x3_dgrad_wino", "pmu_conv3x3_wgrad_wino",
+    "pmu_conv3x3_fwd_wino_raw", "pmu_conv3x3_dgrad_wino_raw",
+    "pmu_conv3x3_fwd_wino2h", "pmu_conv3x3_dgrad_wino2h", "pmu_conv3x3_dgrad_wino2h_bnr",
+    "pmu_conv3x3_fwd_wino4", "pmu_conv3x3_dgrad_wino4", "pmu_conv3x3_dgrad_wino4_bnr", "pmu_conv3x3_wgrad_wino4",
+    # bf16 3x3 convs
+    "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16",
+    "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw",
+    "pmu_conv3x3_fwd_dma", "pmu_conv3x3_fwd_dma_zb", "pmu_conv3x3_dgrad_dma", "pmu_conv3x3_dgrad_dma_bnr",
+    "pmu_conv3x3_dgrad_dma_bnr_zb", "pmu_conv3x3_dgrad_dma_x1b", "pmu_conv3x3_dgrad_dma_x1b_sum",
+    # transposed convs
+    "pmu_convT2x2_fwd", "pmu_convT2x2_fwd_ld", "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad",
+    "pmu_convT2x2_fwd_bf16", "pmu_convT2x2_dgrad_bf16", "pmu_convT2x2_wgrad_bf16",
+    "pmu_convT2x2_fwd_dma", "pmu_convT2x2_fwd_dma_ldb", "pmu_convT2x2_dgrad_dma",
+    # the Probabilistic U-Net's Fcomb
+    "pmu_fcomb_fwd", "pmu_fcomb_bwd",
+)
+
 _LIB = None
 
 

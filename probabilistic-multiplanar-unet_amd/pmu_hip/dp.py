@@ -98,14 +98,23 @@ class BucketAllReduce:
     def _zero_stale(self):
         """Once after a relayout: the buffer still holds the old layout's values where the new one has
         pads and the slots of parameters without a gradient (the tail is SUM-all-reduced every step,
-        so stale values there would grow by ~world per step).  Zero everything but the live
-        gradients' [off, off + numel) ranges (the optimizer has consumed the old-layout views)."""
+        so stale values there would grow by ~world per step).  A .grad that survived the relayout
+        (zero_grad(set_to_none=False), a caller holding .grad across the first step) is still an
+        old-layout view: it is first moved out of the buffer (a copy, exchanged like any gradient
+        autograd kept outside it), so every in-buffer gradient sits at its new slot; then everything
+        but those slots is zeroed."""
         self._stale = False
         buf = flat_grad_buffer(self.net, self.plist)
         offs = _offsets(self.net, self.plist)
-        lo, hi = buf.data_ptr(), buf.data_ptr() + buf.numel() * buf.element_size()
-        keep = sorted((offs[id(p)], offs[id(p)] + p.numel()) for p in self.plist
-                      if p.grad is not None and lo <= p.grad.data_ptr() < hi)
+        es = buf.element_size()
+        lo, hi = buf.data_ptr(), buf.data_ptr() + buf.numel() * es
+        inbuf = [p for p in self.plist if p.grad is not None and lo <= p.grad.data_ptr() < hi]
+        moved = [p for p in inbuf if (p.grad.data_ptr() - lo) // es != offs[id(p)]]
+        copies = [p.grad.detach().clone() for p in moved]   # all read before any slot is touched
+        for p, c in zip(moved, copies):
+            p.grad = c
+        moved_ids = {id(p) for p in moved}
+        keep = sorted((offs[id(p)], offs[id(p)] + p.numel()) for p in inbuf if id(p) not in moved_ids)
         pos = 0
         for a, b in keep + [(buf.numel(), buf.numel())]:
             if a > pos:

@@ -783,6 +783,19 @@ class UNetState:
         self.feat_src = None    # last DoubleConv output producer
 
 
+def _convT_ld_ok(N, h, w, cin, cout, ptr) -> bool:
+    """The decoder's in-place fp32 transposed conv (pmu_convT2x2_fwd_ld) takes an N x h x w x cin
+    BN+ReLU input producing cout channels — the test unet_forward's decoder applies to its actual
+    input frame, asked ahead of time by the encoder (ptr: any device pointer; not dereferenced)."""
+    f = L.PmuFrame()
+    f.nsrc, f.N, f.H, f.W = 1, N, h, w
+    c = f.src[0]
+    c.x = c.coef = ptr
+    c.mode, c.pool, c.dtype = L.SRC_BNRELU, L.POOL_NONE, 0
+    c.C, c.H, c.W = cin, h, w
+    return bool(L.lib().pmu_convT2x2_fwd_ld_ok(ctypes.byref(f), cout))
+
+
 def _pool_skip(up, prev: ConvBNOut, srcs, N, h, w, bf16):
     """(pooled operand, concat operand) from one pass over prev's activation
     (pmu_frame_to_*_pool_skip), when the Up block that takes prev as its skip will build its concat
@@ -800,8 +813,9 @@ def _pool_skip(up, prev: ConvBNOut, srcs, N, h, w, bf16):
         if not (lb.pmu_convT2x2_dma_ok(up.up.in_channels, Cup, 0) and dma_ok(hs, ws_, Ccat, Cout1, Cout1)
                 and (dma_ok(h, w, Cskip, Cout1, Cout1) or raw_ok(N, h, w, Cskip))):
             return None
-    elif not (use_wino() and (wino4_ok(Ccat, hs, ws_, "fwd") or wino_raw_ok(Ccat))):
-        return None
+    elif not (use_wino() and (wino4_ok(Ccat, hs, ws_, "fwd") or wino_raw_ok(Ccat))
+              and _convT_ld_ok(N, h, w, up.up.in_channels, Cup, prev.z.data_ptr())):
+        return None   # (the decoder then builds its concat operand from u: the skip half would go unread)
     f = frame_of(srcs, N, h, w)
     if not lb.pmu_frame_pool_skip_ok(f):
         return None

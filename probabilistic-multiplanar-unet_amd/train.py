@@ -502,6 +502,8 @@ def main(argv=None):
     if world > 1:  # identical replicas
         for t in list(trainer.net.parameters()) + list(trainer.net.buffers()):
             dist.broadcast(t.data, 0)
+        from pmu_hip.engine import invalidate_packs
+        invalidate_packs()   # written through .data: invisible to the packed-weight cache
     if args.dir is not None:
         dir_img = os.path.join(args.dir, "images")
         dir_mask = os.path.join(args.dir, "labels")

@@ -36,3 +36,5 @@ def load_checkpoint(net, load_model, device):
     loader (weights only: a state_dict is plain tensors)."""
     import torch
     net.load_state_dict(torch.load(load_model, map_location=device, weights_only=True), strict=False)
+    from pmu_hip.engine import invalidate_packs
+    invalidate_packs()   # (load_state_dict bumps the version counters the pack cache checks; belt and braces)

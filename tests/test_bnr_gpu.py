@@ -150,7 +150,8 @@ def test_dgrad_dma_split_bf16_colsum(dev, N, H, W, Cskip, Cup, Cout):
     assert (part[:, Cin:] == 0).all()
 
 
-@pytest.mark.parametrize("N,H,W,C", [(2, 64, 64, 64), (1, 33, 45, 32), (2, 16, 16, 512), (1, 7, 9, 1040)])
+@pytest.mark.parametrize("N,H,W,C", [(2, 64, 64, 64), (1, 33, 45, 32), (2, 16, 16, 512), (1, 7, 9, 1040), (2, 9, 11, 192),
+                                     (1, 6, 8, 2064)])
 def test_maxpool2_bwd_bnr(dev, N, H, W, C):
     """pmu_maxpool2_bwd_bnr: dx bit-equal to pmu_maxpool2_bwd accumulated onto the same skip gradient
     (odd maps: the last row / column gets the skip gradient only), and the partials of the result."""

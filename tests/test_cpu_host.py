@@ -186,6 +186,49 @@ def test_bench_roofline_peak_by_kernel_family():
         assert bench.roofline_peak(k) == bench.FP32_MFMA_PEAK_TF, k
 
 
+def _fake_args(name):
+    """Arguments of the ctypes signature of ``name`` as bench.KernelTimer sees them: every int 64, every
+    frame a 2-image 64x64 frame of one 64-channel source, pointers None."""
+    import ctypes
+    from pmu_hip import _lib
+    res, types = _lib.SIGNATURES[name]
+    args = []
+    for t in types:
+        if t is ctypes.c_int or t is ctypes.c_longlong or t is ctypes.c_size_t:
+            args.append(64)
+        elif t is _lib._FP:
+            f = _lib.PmuFrame()
+            f.nsrc, f.N, f.H, f.W = 1, 2, 64, 64
+            f.src[0].C, f.src[0].H, f.src[0].W = 64, 64, 64
+            args.append(ctypes.byref(f))
+        else:
+            args.append(None)
+    return args
+
+
+def test_bench_counts_every_mfma_entry_point():
+    """Every C-ABI entry whose kernels issue MFMAs (pmu_hip._lib.MFMA_ENTRY_POINTS, next to the ctypes
+    table) is declared in the table, counted by bench.KernelTimer and has a non-zero FLOP formula — no
+    MFMA kernel prints "tflops": null and step_mfma_busy_frac sees all of them."""
+    import bench
+    from pmu_hip import _lib
+    assert bench.KernelTimer.MFMA is _lib.MFMA_ENTRY_POINTS
+    for name in _lib.MFMA_ENTRY_POINTS:
+        assert name in _lib.SIGNATURES, name
+        fl = bench.KernelTimer._flops(name, _fake_args(name))
+        assert fl > 0, name
+        # the direct-sum basis of a Winograd launch is larger than its executed products, never zero
+        assert bench.KernelTimer._direct(name, _fake_args(name), fl) >= fl, name
+    # the fused variants count as their base call (same shapes, same MFMA work)
+    for v, base in (("pmu_conv3x3_dgrad_dma_x1b_sum", "pmu_conv3x3_dgrad_dma"),
+                    ("pmu_conv3x3_dgrad_dma_x1b", "pmu_conv3x3_dgrad_dma"),
+                    ("pmu_convT2x2_fwd_dma_ldb", "pmu_convT2x2_fwd_dma"), ("pmu_convT2x2_fwd_ld", "pmu_convT2x2_fwd")):
+        assert bench.KernelTimer._flops(v, _fake_args(v)) == bench.KernelTimer._flops(base, _fake_args(base)), v
+    # and each has a kernel family for the PMC traffic lookup
+    for name in _lib.MFMA_ENTRY_POINTS:
+        assert name in bench.KERNEL_FAMILY, name
+
+
 def test_debug_build_exports_and_identifies_itself():
     """The bounds-checked debug library (csrc `make DEBUG=1`, selected by PMU_LIB=debug) exports the
     same C ABI and reports its build flags; the shipped library is neither a debug nor an experiments

@@ -132,6 +132,38 @@ def test_fusion_large_vs_restatement(dev):
             assert float(r["counts"][v, c, 2]) == float((truth == c).sum())
 
 
+@pytest.mark.parametrize("D0,D1,D2", [(512, 64, 48), (40, 512, 56)])
+def test_fusion_512_edge_vs_restatement(dev, D0, D1, D2):
+    """Config c5's eval volume has 512-voxel edges (PMU/eval.py:157-203 on a 512^3 scan; the bench runs
+    512^3 on random-init weights only): a 512-edge volume along the view-0 slice axis and along a
+    transposed axis, 3 classes, vs the restatement.  Probabilities in: average, label map and counts
+    exact.  Logits in (the predictor's path, softmax inside the kernel): average within 1e-6 and labels
+    equal but at fp32 near-ties of the top two classes."""
+    from oracle.data_ref import fuse
+    from pmu_hip.fusion import fuse_views
+    g = torch.Generator(device="cpu").manual_seed(D0 + 3 * D1 + 7 * D2)
+    C = 3
+    logits = [torch.randn(n, C, a, b, generator=g) * 3.0 for n, a, b in ((D0, D1, D2), (D1, D0, D2), (D2, D0, D1))]
+    st = [torch.softmax(t, 1) for t in logits]
+    truth = torch.randint(0, C, (D0, D1, D2), generator=g).float()
+    vols = fuse(*st)
+    r = fuse_views(*[t.to(dev) for t in st], truth.to(dev))
+    assert torch.equal(r["avg"].cpu(), vols[3])
+    lab = torch.argmax(vols[3], 1).int()
+    assert torch.equal(r["label"].cpu(), lab)
+    for v in range(4):
+        am = torch.argmax(vols[v], 1)
+        for c in range(C):
+            assert float(r["counts"][v, c, 0]) == float(((am == c) & (truth == c)).sum())
+            assert float(r["counts"][v, c, 1]) == float((am == c).sum())
+            assert float(r["counts"][v, c, 2]) == float((truth == c).sum())
+    r2 = fuse_views(*[t.to(dev) for t in logits], truth.to(dev), logits=True)
+    assert float((r2["avg"].cpu() - vols[3]).abs().max()) <= 1e-6
+    top = torch.topk(vols[3], 2, dim=1).values
+    flips = r2["label"].cpu() != lab
+    assert bool(((top[:, 0] - top[:, 1])[flips] < 1e-5).all()), int(flips.sum())
+
+
 def _synthetic_scans(n, shape, seed):
     g = np.random.default_rng(seed)
     out = {}

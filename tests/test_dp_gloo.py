@@ -156,10 +156,22 @@ def _bucket_worker(rank, world, port, q, mode, acc):
         # 3 rounds: round 0 learns the layout, later rounds reuse buffer and bucket state
         for rnd in range(3):
             for p in plist:
-                p.grad = None
+                if mode == "kept" and p.grad is not None:
+                    p.grad.zero_()       # zero_grad(set_to_none=False): round 0's old-layout views survive
+                else:
+                    p.grad = None
             sync.begin()
             if g is not None:
-                if mode == "foreign":
+                if mode == "kept" and rnd > 0:
+                    sink = grad_sink_for(net, plist)
+                    assert not sink.flat                     # .grad exists: autograd accumulates into it
+                    for grp in groups:
+                        for p in grp:
+                            v = sink.new(p)
+                            v.copy_(g[name_of[id(p)]])
+                            p.grad.add_(v)
+                        sink.flush()
+                elif mode == "foreign":
                     for p in plist:
                         p.grad = g[name_of[id(p)]].clone()   # accumulated outside the flat buffer
                 elif mode == "accumulated":
@@ -199,7 +211,7 @@ def _bucket_worker(rank, world, port, q, mode, acc):
 
 
 @pytest.mark.parametrize("mode,world,acc", [("backward_order", 2, 8), ("forward_order", 2, 8), ("foreign", 2, 8),
-                                            ("accumulated", 2, 8),
+                                            ("accumulated", 2, 8), ("kept", 2, 8),
                                             ("backward_order", 4, 8), ("backward_order", 8, 8),
                                             ("backward_order", 4, 2)])
 def test_dp_bucketed_overlap_matches_reference_accumulation(mode, world, acc):
@@ -224,7 +236,7 @@ def test_dp_bucketed_overlap_matches_reference_accumulation(mode, world, acc):
                 assert first is not None and first < flushes // 2   # bucket 0 long before the end
             elif mode == "forward_order" and busy:
                 assert issued == nb                   # the layout follows the learned (reversed) order too
-            elif mode == "accumulated":
+            elif mode in ("accumulated", "kept"):
                 assert issued == 0                    # learned from plain-sink reports; exchanged at finish()
             else:
                 assert issued == 0                    # foreign grads / idle rank: all at finish()

@@ -124,3 +124,40 @@ def test_channel_mismatch_refused(dev):
     with pytest.raises(RuntimeError, match="channels"):
         net(torch.rand(2, 1, 64, 48, device=dev))
     torch.cuda.synchronize()
+
+
+def test_data_write_needs_invalidate_packs(dev):
+    """The pack cache keys on storage, torch's version counter and the FusedSGD epoch.  A write through
+    ``.data`` (a custom optimizer, a raw broadcast) bumps none of them: the forward then still runs the
+    old packs — the documented hazard — and after invalidate_packs() it runs the new weights, equal to a
+    fresh model built from them.  load_state_dict writes in place through the version counter, so a
+    checkpoint load is seen without help."""
+    from model import UNet
+    from pmu_hip import engine
+    torch.manual_seed(0)
+    net = UNet(1, 1, [32, 64]).to(dev).eval()
+    x = torch.rand(2, 1, 64, 48, device=dev)
+    sd0 = {k: v.clone() for k, v in net.state_dict().items()}
+    # the packed weights (every 3x3 conv but the first layer, which reads its weight raw, and the
+    # transposed conv); the head reads its weight raw too
+    packed = [k for k, v in sd0.items() if v.dim() == 4 and k not in ("inc.double_conv.0.weight", "outc.conv.weight")]
+    assert len(packed) >= 5
+    with torch.no_grad():
+        y0 = net(x).clone()
+        new = {k: (v * 0.5 if k in packed else v) for k, v in sd0.items()}
+        for k, p in net.named_parameters():
+            p.data.copy_(new[k])                          # not seen by the cache
+        y_stale = net(x).clone()
+        engine.invalidate_packs()
+        y1 = net(x).clone()
+        torch.manual_seed(0)
+        ref = UNet(1, 1, [32, 64]).to(dev).eval()
+        ref.load_state_dict(new)
+        y_ref = ref(x).clone()
+        net.load_state_dict(sd0)                          # a checkpoint load: in place, version counter bumped
+        y2 = net(x)
+    torch.cuda.synchronize()
+    assert torch.equal(y_stale, y0)                       # the hazard: old packs
+    assert not torch.equal(y1, y0)
+    assert torch.equal(y1, y_ref)                         # after invalidate_packs(): the new weights
+    assert torch.equal(y2, y0)                            # the load is seen without invalidate_packs()
