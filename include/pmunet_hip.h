@@ -360,6 +360,12 @@ int pmu_maxpool2_bwd_bnr(const float* dpool, const float* z, const float* coef, 
                          float* part, void* stream);
 /* AvgPool2d(2,2,ceil_mode=True) backward: dx = dpool/count(window), overwrite. */
 int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream);
+/* The same (bit-equal dx, here da: N x H x W x C at the pooled layer's resolution) fused with the BN+ReLU
+ * backward partial sums of the layer whose activation was pooled (probabilistic_unet.py:36 AvgPool2d,
+ * :30-32 BN+ReLU): part[pmu_bn_bwd_tiles(N*H*W, C) rows][2][C] as pmu_bn_bwd_reduce forms them from
+ * (da, z).  C % 4 == 0. */
+int pmu_avgpool2_bwd_bnr(const float* dpool, const float* z, const float* coef, const float* mean,
+                         const float* invstd, int N, int H, int W, int C, float* da, float* part, void* stream);
 
 /* ---- ConvTranspose2d(k=2, s=2) ---------------------------------------------------- */
 /* Optional packed weights (wp, pmu_convT2x2_packed_size bytes): k-contiguous B operands for the
@@ -483,6 +489,10 @@ int pmu_spatial_mean(const float* z, const float* coef, int N, int H, int W, int
                      void* stream);
 /* da[N][H][W][C] = dmean[N][C] / (H*W). */
 int pmu_spatial_mean_bwd(const float* dmean, int N, int H, int W, int C, float* da, void* stream);
+/* The same fused with the BN+ReLU backward partial sums of the averaged layer (:39 mean over the
+ * encoder's last activation): part as pmu_avgpool2_bwd_bnr.  C % 4 == 0. */
+int pmu_spatial_mean_bwd_bnr(const float* dmean, const float* z, const float* coef, const float* mean,
+                             const float* invstd, int N, int H, int W, int C, float* da, float* part, void* stream);
 /* y[N][M] = x[N][K] . w[M][K]^T + b  (a 1x1 conv on a 1x1 map, probabilistic_unet.py:72,101). */
 int pmu_linear_fwd(const float* x, const float* w, const float* b, int N, int K, int M, float* y,
                    void* stream);

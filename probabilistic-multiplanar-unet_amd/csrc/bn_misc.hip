@@ -158,6 +158,92 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   }
 }
 
+// The two encoder passes that complete a layer's da (probabilistic_unet.py:26-44, the prior /
+// posterior nets): AvgPool2d(2, ceil_mode) backward (SRC 1: da[n][h][w] = dpool[n][h/2][w/2] / count of
+// the window's valid pixels, avgpool2_bwd's arithmetic) and the spatial mean's backward (SRC 2:
+// da[n][p] = dmean[n] / (H*W), :39 torch.mean over dims 2,3), each writing da and forming the layer's
+// BatchNorm+ReLU backward partial sums in the same pass — the part[tile][2][C] slab of
+// bn_bwd_reduce_kernel (same blocks, same per-thread pixel order), so the layer's bn_backward takes
+// them instead of a second pass over da and z.
+template <int SRC>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_src_kernel(const float* __restrict__ g,
+                                                                const float* __restrict__ z,
+                                                                const float* __restrict__ coef,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd, int N, int H, int W,
+                                                                int C, int ppb, float* __restrict__ da,
+                                                                float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int tid = threadIdx.x;
+  const int CQ = C >> 2;
+  const int npg = CQ >= 256 ? 1 : 256 / CQ;
+  const int qstride = CQ >= 256 ? 256 : CQ;
+  const int pg = tid / qstride;
+  const int q0 = tid % qstride;
+  const long long P = (long long)N * H * W;
+  const long long p0 = (long long)blockIdx.x * ppb;
+  const int Hp = (H + 1) / 2, Wp = (W + 1) / 2;
+  const float hw = (float)(H * W);
+  for (int qb = 0; qb < CQ; qb += qstride) {  // uniform trip count: the barriers below are block-wide
+    const int q = qb + q0;
+    const int c = 4 * (q < CQ ? q : 0);
+    const float4 sc = *reinterpret_cast<const float4*>(coef + c);
+    const float4 sh = *reinterpret_cast<const float4*>(coef + C + c);
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+    const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+    float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
+    if (pg < npg && q < CQ) {
+      const int pend = (int)min(P, p0 + ppb);   // P < 2^31 (host-checked)
+#pragma unroll 4
+      for (int p = (int)p0 + pg; p < pend; p += npg) {
+        const int w = p % W;
+        const int t = p / W;
+        const int h = t % H;
+        const int n = t / H;
+        float4 d;
+        if (SRC == 1) {
+          const int hp = h >> 1, wp = w >> 1;
+          const float cnt = (float)((min(2 * hp + 2, H) - 2 * hp) * (min(2 * wp + 2, W) - 2 * wp));
+          const float4 gg = *reinterpret_cast<const float4*>(g + (((long long)n * Hp + hp) * Wp + wp) * C + c);
+          d = make_float4(gg.x / cnt, gg.y / cnt, gg.z / cnt, gg.w / cnt);
+        } else {
+          const float4 gg = *reinterpret_cast<const float4*>(g + (long long)n * C + c);
+          d = make_float4(gg.x / hw, gg.y / hw, gg.z / hw, gg.w / hw);
+        }
+        PMU_DCHECK(p < P, PMU_DBG_OUTPUT);
+        const float4 zz = *reinterpret_cast<const float4*>(z + (long long)p * C + c);
+        *reinterpret_cast<float4*>(da + (long long)p * C + c) = d;
+        const float dv[4] = {d.x, d.y, d.z, d.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = fmaf(zv[e], scv[e], shv[e]) > 0.f ? dv[e] : 0.f;
+          sg[e] += gv;
+          sgx[e] = fmaf(gv, (zv[e] - muv[e]) * isv[e], sgx[e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { red[tid * 8 + e] = sg[e]; red[tid * 8 + 4 + e] = sgx[e]; }
+    __syncthreads();
+    if (pg == 0 && q < CQ) {
+      float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
+      for (int l = 0; l < npg; ++l) {
+        const int src = l * qstride + q0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { t1[e] += red[src * 8 + e]; t2[e] += red[src * 8 + 4 + e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        part[((long long)blockIdx.x * 2 + 0) * C + c + e] = t1[e];
+        part[((long long)blockIdx.x * 2 + 1) * C + c + e] = t2[e];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ acc, int G, int C,
                                                               double count, const float* __restrict__ gamma,
                                                               const float* __restrict__ coef,
@@ -1161,6 +1247,37 @@ static int bn_bwd_ppb(int C) {
 }
 
 extern "C" int pmu_bn_bwd_tiles(int P, int C) { return pmu_cdiv(P, bn_bwd_ppb(C)); }
+
+// AvgPool2d(2, ceil_mode) backward into da (N x H x W x C, the pooled layer's resolution) fused with
+// that layer's BN+ReLU backward partial sums (part rows = pmu_bn_bwd_tiles(N*H*W, C)); da bit-equal to
+// pmu_avgpool2_bwd, part to pmu_bn_bwd_reduce on it.  C % 4 == 0.
+extern "C" int pmu_avgpool2_bwd_bnr(const float* dpool, const float* z, const float* coef, const float* mean,
+                                    const float* invstd, int N, int H, int W, int C, float* da, float* part,
+                                    void* stream) {
+  PMU_REQUIRE(dpool && z && coef && mean && invstd && da && part && N > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0);
+  const long long P = (long long)N * H * W;
+  PMU_REQUIRE(P < (1LL << 31));
+  const int ppb = bn_bwd_ppb(C);
+  hipLaunchKernelGGL(bn_bwd_reduce_src_kernel<1>, dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0, (hipStream_t)stream,
+                     dpool, z, coef, mean, invstd, N, H, W, C, ppb, da, part);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+// The spatial mean's backward (da[n][h][w][c] = dmean[n][c] / (H*W), pmu_spatial_mean_bwd's arithmetic)
+// fused with the BN+ReLU backward partial sums of the layer it averaged (part as above).  C % 4 == 0.
+extern "C" int pmu_spatial_mean_bwd_bnr(const float* dmean, const float* z, const float* coef, const float* mean,
+                                        const float* invstd, int N, int H, int W, int C, float* da, float* part,
+                                        void* stream) {
+  PMU_REQUIRE(dmean && z && coef && mean && invstd && da && part && N > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0);
+  const long long P = (long long)N * H * W;
+  PMU_REQUIRE(P < (1LL << 31));
+  const int ppb = bn_bwd_ppb(C);
+  hipLaunchKernelGGL(bn_bwd_reduce_src_kernel<2>, dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0, (hipStream_t)stream,
+                     dmean, z, coef, mean, invstd, N, H, W, C, ppb, da, part);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
 
 extern "C" int pmu_bn_bwd_reduce(const float* da, const float* z, const float* coef, const float* mean,
                                  const float* invstd, int P, int C, float* part, void* stream) {

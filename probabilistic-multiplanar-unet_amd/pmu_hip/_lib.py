@@ -141,6 +141,10 @@ SIGNATURES = {
     "pmu_maxpool2_bwd_bnr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                      c_void_p, c_int, c_void_p, c_void_p]),
     "pmu_avgpool2_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_avgpool2_bwd_bnr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                     c_void_p, c_void_p, c_void_p]),
+    "pmu_spatial_mean_bwd_bnr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                         c_int, c_void_p, c_void_p, c_void_p]),
     "pmu_convT2x2_packed_size": (c_size_t, [c_int, c_int]),
     "pmu_convT2x2_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_fwd": (c_int, [_FP, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),

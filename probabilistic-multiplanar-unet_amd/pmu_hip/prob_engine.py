@@ -105,7 +105,24 @@ def gaussian_backward(g, st: GaussState, dmls: torch.Tensor, grads):
            dwl.data_ptr(), L.ptr(dbl), s)
     h, w = st.hw
     da = _empty(N, h, w, C, device=dev)
-    L.call("pmu_spatial_mean_bwd", dmean.data_ptr(), N, h, w, C, da.data_ptr(), s)
+    lb = L.lib()
+
+    def fused(o):   # the pass that completes o's da can form o's BN-backward partial sums (fp32 z, C % 4)
+        return o.z.dtype == torch.float32 and o.bn.mean is not None and o.z.shape[3] % 4 == 0
+
+    def bnr_call(name, g, o, da):
+        Np, hp, wp, Cp = o.z.shape
+        R = lb.pmu_bn_bwd_tiles(Np * hp * wp, Cp)
+        part = _empty(R, 2 * Cp, device=dev)
+        L.call(name, g.data_ptr(), o.z.data_ptr(), o.bn.coef.data_ptr(), o.bn.mean.data_ptr(),
+               o.bn.invstd.data_ptr(), Np, hp, wp, Cp, da.data_ptr(), part.data_ptr(), s)
+        o.bnr = (da, part, R)
+
+    last = st.layers[-1]
+    if fused(last):
+        bnr_call("pmu_spatial_mean_bwd_bnr", dmean, last, da)
+    else:
+        L.call("pmu_spatial_mean_bwd", dmean.data_ptr(), N, h, w, C, da.data_ptr(), s)
     for idx in reversed(range(len(layers))):
         conv, bn, pooled = layers[idx]
         o = st.layers[idx]
@@ -113,10 +130,14 @@ def gaussian_backward(g, st: GaussState, dmls: torch.Tensor, grads):
         if idx == 0:
             break
         if pooled:
-            p = st.layers[idx - 1].z
-            hp, wp, Cp = p.shape[1], p.shape[2], p.shape[3]
+            prev = st.layers[idx - 1]
+            hp, wp, Cp = prev.z.shape[1], prev.z.shape[2], prev.z.shape[3]
             da = _empty(N, hp, wp, Cp, device=dev)
-            L.call("pmu_avgpool2_bwd", dx.data_ptr(), N, hp, wp, Cp, da.data_ptr(), s)
+            if fused(prev):
+                # the pooled layer's da is complete here: its BN-backward partials in the same pass
+                bnr_call("pmu_avgpool2_bwd_bnr", dx, prev, da)
+            else:
+                L.call("pmu_avgpool2_bwd", dx.data_ptr(), N, hp, wp, Cp, da.data_ptr(), s)
         else:
             da = dx
     return grads

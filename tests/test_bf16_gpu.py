@@ -494,9 +494,12 @@ def _c5_step_vs_oracle(dev, N, say=print, odev="cpu"):
         params = {k: sdd[k].clone().requires_grad_(True) for k in keys}
         work = dict(sdd)
         work.update(params)
-        o = unet_forward(work, x.to(odev, dt), 5, 3, bf16=True)
-        lo = unet_loss(o, tgt.to(odev), 3)
-        lo.backward()
+        # on the GPU, torch's own im2col + rocBLAS GEMM convolutions (MIOpen off: it would compile a
+        # kernel per shape on first use, minutes of silence on a fresh box)
+        with torch.backends.cudnn.flags(enabled=False):
+            o = unet_forward(work, x.to(odev, dt), 5, 3, bf16=True)
+            lo = unet_loss(o, tgt.to(odev), 3)
+            lo.backward()
         res = (o.detach().cpu(), float(lo.detach()), {k: params[k].grad.cpu() for k in keys},
                {k: v.detach().cpu() for k, v in work.items()})
         del o, lo, params, work, sdd

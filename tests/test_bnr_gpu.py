@@ -219,3 +219,38 @@ def test_head1x1_bwd_bnr(dev, N, H, W, C, K, sig, fused_wgrad):
     else:
         assert torch.equal(dl, dl2)
     _check(da, part, z, coef, mean, invstd, dev)
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 64, 64, 64), (3, 33, 45, 128), (2, 16, 16, 1040), (1, 7, 9, 192)])
+@pytest.mark.parametrize("kind", ["avgpool", "mean"])
+def test_encoder_bwd_bnr(dev, N, H, W, C, kind):
+    """The Probabilistic U-Net encoder's passes that complete a layer's da (probabilistic_unet.py:36
+    AvgPool2d(2, ceil_mode) backward, :39 spatial-mean backward) fused with that layer's BN+ReLU backward
+    partials: da bit-equal to pmu_avgpool2_bwd / pmu_spatial_mean_bwd, the partials equal to
+    pmu_bn_bwd_reduce's on the same (da, z) bit for bit (same blocks, same pixel order) and to fp64."""
+    from pmu_hip import _lib as L
+    g = torch.Generator().manual_seed(41 + H + C)
+    z, coef, mean, invstd = _bn_inputs(N, H, W, C, g, dev)
+    if kind == "avgpool":
+        src = torch.randn(N, (H + 1) // 2, (W + 1) // 2, C, generator=g).to(dev)
+        ref = torch.empty(N, H, W, C, device=dev)
+        L.call("pmu_avgpool2_bwd", src.data_ptr(), N, H, W, C, ref.data_ptr(), L.stream())
+        name = "pmu_avgpool2_bwd_bnr"
+    else:
+        src = torch.randn(N, C, generator=g).to(dev)
+        ref = torch.empty(N, H, W, C, device=dev)
+        L.call("pmu_spatial_mean_bwd", src.data_ptr(), N, H, W, C, ref.data_ptr(), L.stream())
+        name = "pmu_spatial_mean_bwd_bnr"
+    P = N * H * W
+    R = L.lib().pmu_bn_bwd_tiles(P, C)
+    da = torch.full((N, H, W, C), float("nan"), device=dev)
+    part = torch.full((R, 2 * C), float("nan"), device=dev)
+    L.call(name, src.data_ptr(), z.data_ptr(), coef.data_ptr(), mean.data_ptr(), invstd.data_ptr(), N, H, W, C,
+           da.data_ptr(), part.data_ptr(), L.stream())
+    ref_part = torch.empty(R, 2 * C, device=dev)
+    L.call("pmu_bn_bwd_reduce", ref.data_ptr(), z.data_ptr(), coef.data_ptr(), mean.data_ptr(), invstd.data_ptr(), P, C,
+           ref_part.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(da, ref)
+    assert torch.equal(part, ref_part)
+    _check(da, part, z, coef, mean, invstd, dev)
