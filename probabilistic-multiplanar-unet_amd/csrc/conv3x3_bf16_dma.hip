@@ -19,6 +19,7 @@
 // 4-bank groups in each ds_read_b128 lane group, for any starting pixel (every tap).  The weights are
 // packed in the same order (channel co in place of the pixel), so their DMA is a straight copy.
 #include <cstdlib>
+#include <type_traits>
 
 #include "pmu_common.h"
 
@@ -197,37 +198,62 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
   PMU_FETCH(0, smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int ch = 0; ch < a.nch; ++ch) {
+  // One operand set per tap in two register buffers; tap t+1's reads are issued during tap t's MFMAs,
+  // and the next chunk's tap 0 during this chunk's tap 8: the chunk barrier (its DMA landed, every
+  // wave done reading the stage the following fetch overwrites) sits between two taps' MFMA groups,
+  // not between a barrier and the first LDS round trip of a chunk.  9 taps per chunk flip the buffer
+  // parity every chunk, so chunks run in compile-time-parity pairs.
+  bf16x8 op[2][FM + FN];
+  auto load_tap = [&](const unsigned char* cur, int tap, bf16x8 (&o)[FM + FN]) {
+    const int dy = tap / 3, dx = tap - 3 * (tap / 3);
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int hp = hpb + (fm + dy) * HW2 + dx;
+      o[fm] = *reinterpret_cast<const bf16x8*>(cur + 16 * swz(hp, q));
+    }
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) o[FM + fn] = *reinterpret_cast<const bf16x8*>(cur + ub[fn] + tap * (32 * BN));
+  };
+  auto run_chunk = [&](int ch, auto par) {
+    constexpr int P = decltype(par)::value;
     const unsigned char* cur = smem + (ch & 1) * G::STAGE;
-    if (ch + 1 < a.nch) PMU_FETCH(ch + 1, smem + ((ch + 1) & 1) * G::STAGE)
-    bf16x8 op[2][FM + FN];
-    auto load_tap = [&](int tap, bf16x8 (&o)[FM + FN]) {
-      const int dy = tap / 3, dx = tap - 3 * (tap / 3);
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm) {
-        const int hp = hpb + (fm + dy) * HW2 + dx;
-        o[fm] = *reinterpret_cast<const bf16x8*>(cur + 16 * swz(hp, q));
-      }
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) o[FM + fn] = *reinterpret_cast<const bf16x8*>(cur + ub[fn] + tap * (32 * BN));
-    };
-    load_tap(0, op[0]);
+    const unsigned char* nxt = smem + ((ch + 1) & 1) * G::STAGE;
+    const bool more = ch + 1 < a.nch;
+    if (more) PMU_FETCH(ch + 1, smem + ((ch + 1) & 1) * G::STAGE)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      if (tap + 1 < 9) load_tap(tap + 1, op[(tap + 1) & 1]);
+      // this tap's operands (read during the previous tap's MFMAs) have landed: wait for them BEFORE
+      // the next reads are issued (left to the compiler, an lgkmcnt(0) after those reads drained them
+      // too: an LDS round trip with the MFMA pipe idle every other tap)
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt at their maxima
+      __builtin_amdgcn_sched_barrier(0);
+      if (tap + 1 < 9) {
+        load_tap(cur, tap + 1, op[(tap + 1 + P) & 1]);
+      } else if (more) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's share of chunk ch + 1 landed
+        __builtin_amdgcn_s_barrier();                      // everyone's, and every read of chunk ch - 1 done
+        __builtin_amdgcn_sched_barrier(0);
+        load_tap(nxt, 0, op[(9 + P) & 1]);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
           if constexpr (!(EXP & 2))
-            acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[tap & 1][fm], op[tap & 1][FM + fn], acc[fm][fn],
-                                                                   0, 0, 0);
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[(tap + P) & 1][fm], op[(tap + P) & 1][FM + fn],
+                                                                   acc[fm][fn], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
-    __syncthreads();
+  };
+  load_tap(smem, 0, op[0]);
+  int ch = 0;
+  for (; ch + 1 < a.nch; ch += 2) {
+    run_chunk(ch, std::integral_constant<int, 0>{});
+    run_chunk(ch + 1, std::integral_constant<int, 1>{});
   }
+  if (ch < a.nch) run_chunk(ch, std::integral_constant<int, 0>{});
+  __syncthreads();  // every wave's last reads are done before the epilogue reuses the stages
 #undef PMU_FETCH
 #undef PMU_GLDS
 

@@ -281,6 +281,12 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
   const int tg = wave & 3, cg = wave >> 3, partner = tg + 4 * (1 - CH) + 8 * cg;
   const int j = j0 + 32 * cg + 16 * CH + (lane & 15);
   const bool jok = j < a.NOUT;
+  // this lane's output column: the forward's z, or the input gradient's dx0 / dx1 side of the split
+  float* dst;
+  int ld;
+  if (!DGRAD) { dst = a.out0 + j; ld = a.NOUT; }
+  else if (j < a.split) { dst = a.out0 + j; ld = a.split; }
+  else { dst = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
   float s1 = 0.f, s2 = 0.f;
   float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
   if (BNR && jok) {
@@ -318,18 +324,26 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
       }
       float P[4];
       w2_partial<CH>(acc, CH, r, P);
-      // Values, masks and BN sums are formed unconditionally and only the stores are predicated: a
-      // global-memory value (bias, z) first consumed inside a per-output branch made the compiler
-      // wait vmcnt(0) in every branch, i.e. for every earlier store of the epilogue to complete.
-      const long long pix0 = ((long long)n * a.H + oh) * a.W + ow;
+      // the partner's partial outputs read together and held in registers before any store branch (read
+      // where used, the plain input gradient's ds_reads sank into the store branches, each followed by
+      // an lgkmcnt(0): serial LDS round trips).  Values, masks and BN sums are formed unconditionally
+      // and only the stores are predicated: a global-memory value (bias, z) first consumed inside a
+      // per-output branch made the compiler wait vmcnt(0) in every branch, i.e. for every earlier store
+      // of the epilogue to complete.
+      float xv[4];
 #pragma unroll
-      for (int p = 0; p < 2; ++p)
+      for (int e = 0; e < 4; ++e) xv[e] = xb[((partner * 2 + rr) * 4 + e) * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(xv[e]));
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int hh = oh + p;
+        float* rowp = dst + (long long)((long long)n * a.H + min(hh, a.H - 1)) * a.W * ld;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const int hh = oh + p, ww = ow + q;
-          const float v = P[2 * p + q] + xb[((partner * 2 + rr) * 4 + 2 * p + q) * 64 + lane] + bias;
+          const int ww = ow + q;
+          const float v = P[2 * p + q] + xv[2 * p + q] + bias;
           const bool ok = jok && hh < a.H && ww < a.W;
-          const long long pix = pix0 + (long long)p * a.W + q;
           if (!DGRAD) {
             const float m = ok ? v : 0.f;
             s1 += m;
@@ -341,11 +355,10 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
             s2 = fmaf(g, (zz - bmu) * bis, s2);
           }
           if (!ok) continue;
-          PMU_DCHECK(pix < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
-          if (!DGRAD) a.out0[pix * a.NOUT + j] = v;
-          else if (j < a.split) a.out0[pix * a.split + j] = v;
-          else a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+          PMU_DCHECK((((long long)n * a.H + hh) * a.W + ww) < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
+          rowp[(unsigned)(ww * ld)] = v;
         }
+      }
     }
   }
   if (a.part) {  // forward: BN partial sums of the output; input gradient: of the producer's BN backward

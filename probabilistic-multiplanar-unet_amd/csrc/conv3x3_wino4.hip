@@ -370,6 +370,12 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
   const int tg = wave & 3, partner = tg + 4 * (1 - CH);
   const int j = j0 + 16 * CH + (lane & 15);
   const bool jok = j < a.NOUT;
+  // this lane's output column: the forward's z, or the input gradient's dx0 / dx1 side of the split
+  float* dst;
+  int ld;
+  if (!DGRAD) { dst = a.out0 + j; ld = a.NOUT; }
+  else if (j < a.split) { dst = a.out0 + j; ld = a.split; }
+  else { dst = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
   float s1 = 0.f, s2 = 0.f;
   float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
   if (BNR && jok) {
@@ -408,18 +414,27 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
       }
       float P[16];
       w4_partial<CH>(acc, CH, r, P);
+      // the partner's 16 partial outputs read together and held in registers before any store branch:
+      // read where they are used, the compiler sank each ds_read into its output's store branch (the
+      // plain input gradient uses v only there) and waited lgkmcnt(0) right behind it — 16 serial LDS
+      // round trips per tile
+      float xv[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) xv[e] = xb[((partner * 2 + rr) * 16 + e) * 64 + lane];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) asm volatile("" : "+v"(xv[e]));
       // values, masks and BN sums unconditional, only the stores predicated (see conv3x3_wino2h.hip:
-      // a global value first consumed inside a per-output branch cost a vmcnt(0) per store)
-      const long long pix0 = ((long long)n * a.H + oh) * a.W + ow;
+      // a global value first consumed inside a per-output branch cost a vmcnt(0) per store); one row
+      // pointer per output row, 32-bit column offsets
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int hh2 = oh + p;
+        float* rowp = dst + (long long)((long long)n * a.H + min(hh2, a.H - 1)) * a.W * ld;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int ww = ow + q;
-          const float v = P[4 * p + q] + xb[((partner * 2 + rr) * 16 + 4 * p + q) * 64 + lane] + bias;
+          const float v = P[4 * p + q] + xv[4 * p + q] + bias;
           const bool ok = jok && hh2 < a.H && ww < a.W;
-          const long long pix = pix0 + (long long)p * a.W + q;
           if (!DGRAD) {
             const float m = ok ? v : 0.f;
             s1 += m;
@@ -431,10 +446,8 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
             s2 = fmaf(g, (zz - bmu) * bis, s2);
           }
           if (!ok) continue;
-          PMU_DCHECK(pix < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
-          if (!DGRAD) a.out0[pix * a.NOUT + j] = v;
-          else if (j < a.split) a.out0[pix * a.split + j] = v;
-          else a.out1[pix * (a.NOUT - a.split) + (j - a.split)] = v;
+          PMU_DCHECK((((long long)n * a.H + hh2) * a.W + ww) < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
+          rowp[(unsigned)(ww * ld)] = v;
         }
       }
     }

@@ -152,37 +152,56 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nkc) fetch(s);
-  for (int kc = 0; kc < nkc; ++kc) {
-    // chunk kc has landed once at most min(NS - 2, nkc - 1 - kc) later chunks are outstanding
-    const int later = (nkc - 1 - kc) < (NS - 2) ? (nkc - 1 - kc) : (NS - 2);
+  // wait until chunk c has landed (this thread's DMAs: at most min(NS - 2, nkc - 1 - c) later chunks may
+  // stay outstanding), then a plain barrier: everyone's have, and every read of the chunk before c is
+  // done.  (__syncthreads()' release fence would wait for every DMA in flight, the later chunks' too.)
+  auto chunk_ready = [&](int c) {
+    const int later = (nkc - 1 - c) < (NS - 2) ? (nkc - 1 - c) : (NS - 2);
     if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NDMA) : "memory");
     else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // a plain barrier: __syncthreads()' release fence would wait for every DMA in flight (vmcnt(0)),
-    // the later chunks' included; this thread's chunk-kc DMAs are counted in above, and the previous
-    // chunk's LDS reads have been consumed by its MFMAs
-    asm volatile("s_barrier" ::: "memory");
-    if (kc + NS - 1 < nkc) fetch(kc + NS - 1);
-    const unsigned char* cur = smem + (kc % NS) * G::STAGE;
-    bf16x8 op[2][FM + FN];
-    auto load = [&](int s, bf16x8 (&o)[FM + FN]) {
-      const int q = 2 * s + hq;
+    __builtin_amdgcn_s_barrier();
+  };
+  bf16x8 op[2][FM + FN];
+  auto load = [&](const unsigned char* cur, int s, bf16x8 (&o)[FM + FN]) {
+    const int q = 2 * s + hq;
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm) o[fm] = *reinterpret_cast<const bf16x8*>(cur + 16 * tpos(aro[fm], q));
+    for (int fm = 0; fm < FM; ++fm) o[fm] = *reinterpret_cast<const bf16x8*>(cur + 16 * tpos(aro[fm], q));
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn)
+      o[FM + fn] = *reinterpret_cast<const bf16x8*>(cur + G::A_BYTES + 16 * tpos(bro[fn], q));
+  };
+  auto mfmas = [&](const bf16x8 (&o)[FM + FN]) {
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn)
-        o[FM + fn] = *reinterpret_cast<const bf16x8*>(cur + G::A_BYTES + 16 * tpos(bro[fn], q));
-    };
-    load(0, op[0]);
-    load(1, op[1]);
+        acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o[fm], o[FM + fn], acc[fm][fn], 0, 0, 0);
+  };
+  // Each k-step's operands are read during the previous k-step's MFMAs — the next chunk's first one
+  // during this chunk's second, after the chunk barrier — so no LDS round trip sits between a barrier
+  // and the MFMAs (with the reads of both k-steps issued after the barrier, every chunk paid one).
+  chunk_ready(0);
+  load(smem, 0, op[0]);
+  for (int kc = 0; kc < nkc; ++kc) {
+    if (kc + NS - 1 < nkc) fetch(kc + NS - 1);   // into chunk kc - 1's stage: read by everyone (barrier)
+    const unsigned char* cur = smem + (kc % NS) * G::STAGE;
+    __builtin_amdgcn_s_waitcnt(0xC07F);           // lgkmcnt(0): k-step 0's operands
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[s][fm], op[s][FM + fn], acc[fm][fn], 0, 0, 0);
+    load(cur, 1, op[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(op[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);           // k-step 1's operands: this chunk's last reads
+    __builtin_amdgcn_sched_barrier(0);
+    if (kc + 1 < nkc) {
+      chunk_ready(kc + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      load(smem + ((kc + 1) % NS) * G::STAGE, 0, op[0]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(op[1]);
+    __builtin_amdgcn_sched_barrier(0);
   }
 #undef PMU_GLDS
 
