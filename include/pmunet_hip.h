@@ -81,24 +81,8 @@ typedef struct pmu_frame {
   int N, H, W;
 } pmu_frame;
 
-/* ---- 3x3 convolution (implicit GEMM on MFMA, LDS halo tiles) -------------------- */
-/* z[N][H][W][Cout] = conv3x3(frame, w) + bias.  If part != NULL, per-tile BN partial
- * sums (sum z, sum z^2) are written to part[tile][2][Cout]; pmu_conv3x3_tiles() gives
- * the tile count.  tee (nullable): receives the operand the kernel multiplied (the frame after
- * BN+ReLU / pooling / concatenation), [N][H][W][Cin] fp32 — a RAW source for pmu_conv3x3_wgrad. */
-int pmu_conv3x3_fwd(const pmu_frame* in, const float* w, const float* wp, const float* bias,
-                    int Cout, float* z, float* part, float* tee, void* stream);
-int pmu_conv3x3_tiles(int N, int H, int W);
-/* Optional pre-packed weights (wp != NULL replaces w): the per-block/chunk B tiles laid out
- * contiguously in LDS order, so staging is a straight copy.  dgrad=1 packs the flipped,
- * transposed operand of pmu_conv3x3_dgrad. */
-size_t pmu_conv3x3_packed_size(int Cout, int Cin, int dgrad);
-int pmu_conv3x3_pack(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream);
-/* dx = dL/d(frame) for frame channels [0,Csplit) -> dx0 (NHWC, Csplit ch) and
- * [Csplit,Cin) -> dx1 (NHWC, Cin-Csplit ch).  dz is a frame whose single source is
- * normally PMU_SRC_BNBWD. */
-int pmu_conv3x3_dgrad(const pmu_frame* dz, const float* w, const float* wp, int Cin, int Csplit,
-                      float* dx0, float* dx1, float* tee, void* stream);  /* tee: dz after BN backward, [N][H][W][Cout] */
+/* ---- 3x3 convolution: direct-sum weight gradient (channel counts the Winograd weight gradient
+ * does not take: Cout % 32 or Cin % 64 != 0) ------------------------------------------------ */
 /* dw[Cout][Cin][3][3] = dL/dw; ws must hold pmu_conv3x3_wgrad_ws() bytes. */
 size_t pmu_conv3x3_wgrad_ws(int N, int H, int W, int Cin, int Cout);
 int pmu_conv3x3_wgrad(const pmu_frame* dz, const pmu_frame* act, int Cout, float* dw,
@@ -117,12 +101,6 @@ int pmu_conv3x3_fwd_wino(const pmu_frame* in, const float* wp, const float* bias
                          float* part, float* tee, void* stream);
 int pmu_conv3x3_dgrad_wino(const pmu_frame* dz, const float* wp, int Cin, int Csplit, float* dx0, float* dx1,
                            float* tee, void* stream);
-/* The same on a materialised operand (pmu_frame_to_f32 of the frame; the default fp32 path): xt /
- * dzt [N][H][W][C] fp32 with C % 16 == 0, staged by LDS-DMA.  part rows = pmu_conv3x3_tiles_wino(). */
-int pmu_conv3x3_fwd_wino_raw(const float* xt, int Cin, int N, int H, int W, const float* wp, const float* bias,
-                             int Cout, float* z, float* part, void* stream);
-int pmu_conv3x3_dgrad_wino_raw(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
-                               int Csplit, float* dx0, float* dx1, void* stream);
 /* The same F(2x2,3x3) operators on a materialised operand in 1024-thread workgroups (16 waves, four per
  * SIMD; 64 output channels x 16 x 16 pixels per block; waves split the 16 components in halves).
  * C % 8 == 0; weights by pmu_conv3x3_pack_wino2h ([64 output rows][8 channels][16 components]);
@@ -151,8 +129,6 @@ int pmu_conv3x3_dgrad_wino2h_bnr(const float* dzt, int Cout, int N, int H, int W
 size_t pmu_conv3x3_packed_size_wino4(int Cout, int Cin, int dgrad);
 int pmu_conv3x3_pack_wino4(const float* w, int Cout, int Cin, int dgrad, float* wp, void* stream);
 int pmu_conv3x3_tiles_wino4(int N, int H, int W);
-int pmu_conv3x3_fwd_wino4(const float* xt, int Cin, int N, int H, int W, const float* wp, const float* bias,
-                          int Cout, float* z, float* part, void* stream);
 int pmu_conv3x3_dgrad_wino4(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
                             int Csplit, float* dx0, float* dx1, void* stream);
 /* as pmu_conv3x3_dgrad_wino2h_bnr (part rows = pmu_conv3x3_tiles_wino4) */
@@ -163,13 +139,6 @@ int pmu_conv3x3_dgrad_wino4_bnr(const float* dzt, int Cout, int N, int H, int W,
  * Winograd F(2x2,3x3): dw = G^T [sum over 2x2 tiles of (A dY A^T) .* (B^T X B)] G.  Cout % 32 == 0,
  * Cin % 64 == 0 (pmu_conv3x3_wgrad_ws_wino returns 0 otherwise); ws must hold that many bytes. */
 size_t pmu_conv3x3_wgrad_ws_wino(int N, int H, int W, int Cin, int Cout);
-/* The same weight gradient by Winograd F(4x4,3x3): 36 products per 4x4 tile and channel pair (2.25
- * per output pixel vs F(2x2)'s 4), output transform in fp64; fp32 rounding ~1.3e-6 of rms |dw|
- * (tools/wgrad_err.py).  Cout % 32 == 0, Cin % 64 == 0 (pmu_conv3x3_wgrad_ws_wino4 returns 0
- * otherwise); ws must hold that many bytes. */
-size_t pmu_conv3x3_wgrad_ws_wino4(int N, int H, int W, int Cin, int Cout);
-int pmu_conv3x3_wgrad_wino4(const float* dzt, const float* xt, int N, int H, int W, int Cout, int Cin,
-                            float* dw, float* ws, size_t ws_bytes, void* stream);
 int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, int H, int W, int Cout, int Cin,
                            float* dw, float* ws, size_t ws_bytes, void* stream);
 
@@ -181,7 +150,10 @@ int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, int H, int 
  * Weights are always pre-packed (bf16, [row block of 64][chunk of 16][tap][64][16]). */
 size_t pmu_conv3x3_packed_size_bf16(int Cout, int Cin, int dgrad);
 int pmu_conv3x3_pack_bf16(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream);
-/* as pmu_conv3x3_fwd / _dgrad (part uses the same pmu_conv3x3_tiles() tile count).  tee (nullable):
+/* rows of the fused-staging convs' BN partial sums (256-pixel tiles) */
+int pmu_conv3x3_tiles(int N, int H, int W);
+/* z = conv3x3(frame) + bias / dx as the direct-sum fp32 conv of pmu_hip_experiments.h (part rows =
+ * pmu_conv3x3_tiles()).  tee (nullable):
  * receives the bf16 operand the kernel multiplied, [N][H][W][pad8(K channels)] as pmu_frame_to_bf16
  * would write it (padding channels untouched) — the input of pmu_conv3x3_wgrad_bf16, for free. */
 int pmu_conv3x3_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int Cout,
@@ -232,19 +204,6 @@ int pmu_convT2x2_dbias_rows(const float* part, int R, long long ld, int Cout, fl
 int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                               int Cin, float* dx, const float* z, const float* coef, const float* mean,
                               const float* invstd, float* part, void* stream);
-/* bf16 storage of z (config c5: torch.autocast keeps a conv's output in bf16, unet_parts.py:15,18 under
- * autocast), centred: the forward stores bf16(z - zoff[c]) (RNE; zoff = the BN running mean, null: 0)
- * with the BN partial sums of stored + zoff; every consumer then applies the centred coefficients of
- * pmu_bn_center.  The input gradient's BN-backward partials read such a z. */
-int pmu_conv3x3_fwd_dma_zb(const unsigned short* xt, int Cp, int N, int H, int W, const unsigned short* wp,
-                           const float* bias, int Cout, unsigned short* z, const float* zoff, float* part,
-                           void* stream);
-/* coef_out = [scale | shift + off*scale], mean_out = mean - off (in place allowed; mean may be NULL) */
-int pmu_bn_center(const float* coef, const float* mean, const float* off, int C, float* coef_out,
-                  float* mean_out, void* stream);
-int pmu_conv3x3_dgrad_dma_bnr_zb(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
-                                 int Cin, float* dx, const unsigned short* z, const float* coef, const float* mean,
-                                 const float* invstd, float* part, void* stream);
 /* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels
  * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz
  * that pmu_conv3x3_wgrad_bf16 multiplies. */
@@ -271,16 +230,6 @@ size_t pmu_conv3x3_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);
 int pmu_conv3x3_wgrad_bf16(const unsigned short* dzt, const unsigned short* xt, int N, int H, int W,
                            int Cout, int Cin, float* dw, float* ws, size_t ws_bytes, void* stream);
 
-/* ConvTranspose2d(k2,s2) forward / input gradient with bf16 operands (fp32 sums and outputs), weights
- * packed as pmu_convT2x2_pack's layouts in bf16 (4*Cin*Cout elements).  The forward takes one unpooled
- * BN+ReLU source with Cin % 32 == 0, Cout % 32 == 0 (pmu_convT2x2_bf16_ok), dgrad Cin % 128 == 0 and
- * Cout % 32 == 0. */
-int pmu_convT2x2_pack_bf16(const float* w, int Cin, int Cout, int dgrad, unsigned short* wp, void* stream);
-int pmu_convT2x2_bf16_ok(const pmu_frame* in, int Cout);
-int pmu_convT2x2_fwd_bf16(const pmu_frame* in, const unsigned short* wp, const float* bias, int Cout,
-                          float* u, void* stream);
-int pmu_convT2x2_dgrad_bf16(const float* du, int Hd, int Wd, int off_h, int off_w, const unsigned short* wp,
-                            int N, int H, int W, int Cin, int Cout, float* dx, void* stream);
 /* Weight gradient from materialised bf16 operands: xt [N][H][W][pad8(Cin)] (the convT input after BN+ReLU)
  * and dut [N][Hd][Wd][pad8(Cout)] (du); dbias (nullable) sums the fp32 du over the output region. */
 /* The same forward / input gradient with both GEMM operands staged by LDS-DMA from materialised bf16
@@ -328,9 +277,6 @@ int pmu_bn_eval_coef(const float* running_mean, const float* running_var, const 
 /* BN+ReLU backward reduction over da (NHWC) and z: part[tile][2][C] = (sum g, sum g*xhat). */
 int pmu_bn_bwd_reduce(const float* da, const float* z, const float* coef, const float* mean,
                       const float* invstd, int P, int C, float* part, void* stream);
-/* the same over a bf16-stored z (C % 4 == 0) */
-int pmu_bn_bwd_reduce_zb(const float* da, const unsigned short* z, const float* coef, const float* mean,
-                         const float* invstd, int P, int C, float* part, void* stream);
 int pmu_bn_bwd_tiles(int P, int C);
 /* From acc[G][2][C]: dgamma, dbeta, dbias(conv bias feeding BN) and the BNBWD coef block
  * [scale|shift|mean|kx|kc]. */
@@ -347,9 +293,6 @@ int pmu_bnrelu_apply(const float* z, const float* coef, long long P, int C, floa
  * accumulate=0 overwrites dx (zeros outside windows). */
 int pmu_maxpool2_bwd(const float* dpool, const float* z, const float* coef, int N, int H, int W,
                      int C, float* dx, int accumulate, void* stream);
-/* the same over a bf16-stored z (coef required, C % 4 == 0) */
-int pmu_maxpool2_bwd_zb(const float* dpool, const unsigned short* z, const float* coef, int N, int H, int W,
-                        int C, float* dx, int accumulate, void* stream);
 /* pmu_maxpool2_bwd (BN+ReLU coef, C % 4 == 0) fused with the BatchNorm+ReLU backward reduction of
  * the pooled layer over the resulting dx (= that layer's da; replaces pmu_bn_bwd_reduce for it):
  * part[pmu_maxpool2_bwd_bnr_tiles rows][2][C] = (sum g, sum g*xhat), g = dx*(z*scale+shift > 0),
@@ -525,7 +468,6 @@ int pmu_fcomb_bwd(const float* feat, const float* z, const float* zb, const floa
 /* ---- diagnostics: resident blocks per CU of the main GEMM kernels (hipOccupancy API) ---- */
 int pmu_occupancy_conv3x3_raw(int* blocks_per_cu);
 int pmu_occupancy_wgrad3x3_bf16(int* blocks_per_cu);
-int pmu_occupancy_conv3x3_pipe(int* blocks_per_cu);
 
 /* ---- batched weight packing ------------------------------------------------------------------
  * One launch re-packs the weights of many layers into one layout after an optimizer step

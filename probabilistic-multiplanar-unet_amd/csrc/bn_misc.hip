@@ -1218,6 +1218,8 @@ extern "C" int pmu_bn_eval_coef(const float* running_mean, const float* running_
   return PMU_OK;
 }
 
+#ifdef PMU_EXPERIMENTS
+// bf16-stored z (experiments build only: it breaks the c5 Dice contract)
 // Centring of a bf16-stored z (pmu_conv3x3_fwd_dma_zb stores z - off): the coefficients every
 // consumer applies to the stored value — scale, shift + off*scale (BN+ReLU: (zs + off)*scale + shift),
 // mean - off (xhat = (zs + off - mean)*invstd).  In place allowed.
@@ -1241,6 +1243,7 @@ extern "C" int pmu_bn_center(const float* coef, const float* mean, const float* 
   return PMU_OK;
 }
 
+#endif  // PMU_EXPERIMENTS
 static int bn_bwd_ppb(int C) {
   int ppb = BNR_BYTES / (C * 4);
   return ppb < 1 ? 1 : ppb;
@@ -1295,6 +1298,8 @@ extern "C" int pmu_bn_bwd_reduce(const float* da, const float* z, const float* c
   return PMU_OK;
 }
 
+#ifdef PMU_EXPERIMENTS
+// bf16-stored z (experiments build only: it breaks the c5 Dice contract)
 extern "C" int pmu_bn_bwd_reduce_zb(const float* da, const unsigned short* z, const float* coef, const float* mean,
                                     const float* invstd, int P, int C, float* part, void* stream) {
   PMU_REQUIRE(da && z && coef && mean && invstd && part && P > 0 && C > 0 && C % 4 == 0);
@@ -1305,6 +1310,7 @@ extern "C" int pmu_bn_bwd_reduce_zb(const float* da, const unsigned short* z, co
   return PMU_OK;
 }
 
+#endif  // PMU_EXPERIMENTS
 extern "C" int pmu_bn_bwd_finalize(const double* acc, int G, int C, double count, const float* gamma,
                                    const float* coef, const float* mean, const float* invstd, float* dgamma,
                                    float* dbeta, float* dbias, float* bcoef, void* stream) {
@@ -1345,6 +1351,8 @@ extern "C" int pmu_maxpool2_bwd(const float* dpool, const float* z, const float*
   return PMU_OK;
 }
 
+#ifdef PMU_EXPERIMENTS
+// bf16-stored z (experiments build only: it breaks the c5 Dice contract)
 extern "C" int pmu_maxpool2_bwd_zb(const float* dpool, const unsigned short* z, const float* coef, int N, int H, int W,
                                    int C, float* dx, int accumulate, void* stream) {
   PMU_REQUIRE(dpool && z && coef && dx && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
@@ -1354,6 +1362,7 @@ extern "C" int pmu_maxpool2_bwd_zb(const float* dpool, const unsigned short* z, 
   return PMU_OK;
 }
 
+#endif  // PMU_EXPERIMENTS
 // windows per block of the fused max-pool backward: about 128 KB of z per block
 static int mpb_wpb(int C) {
   const int w = 8192 / C;

@@ -24,6 +24,11 @@
 
 #include "pmu_stage.h"
 
+// The direct-sum fp32 conv is the engine's PMU_FP32_CONV=direct A/B only (the default fp32 path is
+// Winograd on every shape: conv3x3_wino2h.hip, conv3x3_wino4.hip, and conv3x3_wino.hip's fused
+// kernels for channel counts off the 16 grid): experiments build only.
+#ifdef PMU_EXPERIMENTS
+
 namespace {
 
 constexpr int BM = 256;     // pixels per tile
@@ -505,11 +510,7 @@ static int launch_conv(const pmu_frame* in, const float* w, const float* wp, con
 
 }  // namespace
 
-extern "C" int pmu_conv3x3_tiles(int N, int H, int W) {
-  const int twl = pick_twl(W);
-  const int TW = 1 << twl, TH = BM / TW;
-  return N * pmu_cdiv(H, TH) * pmu_cdiv(W, TW);
-}
+// (pmu_conv3x3_tiles: defined in conv3x3_bf16.hip, same 256-pixel tile geometry)
 
 extern "C" size_t pmu_conv3x3_packed_size(int Cout, int Cin, int dgrad) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
@@ -552,3 +553,4 @@ extern "C" int pmu_occupancy_conv3x3_pipe(int* blocks_per_cu) {
   *blocks_per_cu = n;
   return PMU_OK;
 }
+#endif  // PMU_EXPERIMENTS

@@ -561,6 +561,14 @@ static int launch_bf16(const pmu_frame* in, const unsigned short* wp, const floa
 
 }  // namespace
 
+// rows of the fused-staging convs' BN partial sums part[tile][2][Cout]: tiles of BM = 256 pixels, 32, 16 or
+// 8 wide (pick_twl) — the bf16 kernels here, and the experiments build's fp32 direct-sum conv
+extern "C" int pmu_conv3x3_tiles(int N, int H, int W) {
+  const int twl = pick_twl(W);
+  const int TW = 1 << twl, TH = BM / TW;
+  return N * pmu_cdiv(H, TH) * pmu_cdiv(W, TW);
+}
+
 extern "C" size_t pmu_conv3x3_packed_size_bf16(int Cout, int Cin, int dgrad) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
   return (size_t)packed_row_blocks(NOUT) * pmu_cdiv(KC, BK) * 9 * PJ * BK * sizeof(unsigned short);

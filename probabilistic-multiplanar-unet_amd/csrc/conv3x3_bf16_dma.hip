@@ -492,9 +492,14 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   if (dgrad && part && !bz) {  // column sums (pmu_conv3x3_dgrad_dma_x1b_sum)
     if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, true>), grid, blk, 0, st, a);
-  } else if (dgrad && zb) PMU_DMA_LAUNCH(true, true)
-  else if (dgrad) PMU_DMA_LAUNCH(true, false)
+  }
+#ifdef PMU_EXPERIMENTS
+  else if (dgrad && zb) PMU_DMA_LAUNCH(true, true)
   else if (zb) PMU_DMA_LAUNCH(false, true)
+#else
+  else if (zb) return PMU_ERR_ARG;  // bf16-stored z: experiments build only
+#endif
+  else if (dgrad) PMU_DMA_LAUNCH(true, false)
   else PMU_DMA_LAUNCH(false, false)
 #undef PMU_DMA_LAUNCH
   PMU_CHECK_LAUNCH();
@@ -569,6 +574,8 @@ extern "C" int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int 
   return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream, z, coef, mean, invstd);
 }
 
+#ifdef PMU_EXPERIMENTS
+// (experiments build only: bf16 z breaks the c5 Dice contract)
 // bf16 storage of z (config c5's autocast dtype), centred on zoff (the BN running mean; null: 0): the
 // forward stores bf16(z - zoff) (RNE) with the BN partial sums of stored + zoff; the input gradient's
 // BN-backward partials read such a z with the centred coefficients (shift + zoff*scale, mean - zoff).
@@ -587,6 +594,8 @@ extern "C" int pmu_conv3x3_dgrad_dma_bnr_zb(const unsigned short* dzt, int Cp, i
   return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream,
                     reinterpret_cast<const float*>(z), coef, mean, invstd, 1);
 }
+
+#endif  // PMU_EXPERIMENTS
 
 static int pack_dma_grid(int Cout, int Cin, int dgrad) {
   const long long total = (long long)(pmu_conv3x3_packed_size_dma(Cout, Cin, dgrad) / sizeof(unsigned short));

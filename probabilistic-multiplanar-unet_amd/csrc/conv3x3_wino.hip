@@ -479,8 +479,11 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino_pipe_kernel(WinoArgs a) {
   wino_epilogue<DGRAD>(a, g, acc, smem, wino_bias<DGRAD>(a, g));
 }
 
+#ifdef PMU_EXPERIMENTS
+// (the 512-thread raw kernels: superseded by the 1024-thread conv3x3_wino2h.hip kernels on every shape
+// they take; experiments build only, PMU_WINO2H=0 A/B)
 // ---------------------------------------------------------------------------------------------
-// RAW-operand variant (the default fp32 path): the operand was materialised once (BN+ReLU / pool /
+// RAW-operand variant: the operand was materialised once (BN+ReLU / pool /
 // F.pad+cat applied, or the BN backward of dz) — the tensor the weight gradient reads anyway — so
 // the staging is a copy done by LDS-DMA (global_load_lds, no registers, no VALU), and each lane reads
 // its 4x4 patch once per chunk as 16 ds_read_b128 (4 channels: channel 4*kk + ks feeds step ks).
@@ -688,6 +691,7 @@ int launch_wino_raw(const float* x, int KC, int N, int H, int W, const float* wp
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
+#endif  // PMU_EXPERIMENTS
 
 // a source the pipelined staging takes: float4 channels, chunks never straddle sources
 static bool wino_pipe_src_ok(const pmu_src& s) {
@@ -811,6 +815,7 @@ extern "C" int pmu_conv3x3_dgrad_wino(const pmu_frame* dz, const float* wp, int 
   return launch_wino(dz, wp, nullptr, Cin, Cout, dx0, dx1, Csplit, nullptr, tee, true, stream);
 }
 
+#ifdef PMU_EXPERIMENTS
 extern "C" int pmu_conv3x3_fwd_wino_raw(const float* xt, int Cin, int N, int H, int W, const float* wp,
                                         const float* bias, int Cout, float* z, float* part, void* stream) {
   return launch_wino_raw(xt, Cin, N, H, W, wp, bias, Cout, z, nullptr, Cout, part, false, stream);
@@ -821,3 +826,4 @@ extern "C" int pmu_conv3x3_dgrad_wino_raw(const float* dzt, int Cout, int N, int
   PMU_REQUIRE(Csplit > 0 && Csplit <= Cin && (Csplit == Cin || dx1));
   return launch_wino_raw(dzt, Cout, N, H, W, wp, nullptr, Cin, dx0, dx1, Csplit, nullptr, true, stream);
 }
+#endif  // PMU_EXPERIMENTS

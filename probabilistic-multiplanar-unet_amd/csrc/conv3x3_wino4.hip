@@ -700,8 +700,12 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
   if (dgrad && bz) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, false>), grid, dim3(NT), 0, st, a);
   else if (dgrad && pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, true>), grid, dim3(NT), 0, st, a);
   else if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, false>), grid, dim3(NT), 0, st, a);
+#ifdef PMU_EXPERIMENTS
   else if (pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, true>), grid, dim3(NT), 0, st, a);
   else hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, false>), grid, dim3(NT), 0, st, a);
+#else
+  else return PMU_ERR_ARG;  // the F(4x4) forward is an experiments-build kernel (see pmu_conv3x3_fwd_wino4)
+#endif
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -724,10 +728,15 @@ extern "C" int pmu_conv3x3_pack_wino4(const float* w, int Cout, int Cin, int dgr
   return PMU_OK;
 }
 
+#ifdef PMU_EXPERIMENTS
+// The F(4x4) forward: built, tested (tests/test_wino4_gpu.py) and measured (+41 slices/s on c2), but its
+// fp32 rounding enters the BatchNorm statistics and breaks the model-level 1e-3 / Dice contract
+// (DESIGN.md §3a), so it ships only in the experiments build (include/pmunet_hip_experiments.h).
 extern "C" int pmu_conv3x3_fwd_wino4(const float* xt, int Cin, int N, int H, int W, const float* wp, const float* bias,
                                      int Cout, float* z, float* part, void* stream) {
   return launch_wino4(xt, Cin, N, H, W, wp, bias, Cout, z, nullptr, Cout, part, false, stream);
 }
+#endif
 
 extern "C" int pmu_conv3x3_dgrad_wino4(const float* dzt, int Cout, int N, int H, int W, const float* wp, int Cin,
                                        int Csplit, float* dx0, float* dx1, void* stream) {

@@ -29,6 +29,9 @@ struct TArgs {
   int nnb, xcd;               // column blocks; 1: 1-D XCD-ordered grid, column blocks fastest
 };
 
+#ifdef PMU_EXPERIMENTS
+// (register-staged ConvT forward / input gradient: their shapes are exactly the LDS-DMA kernels'
+// (convT_bf16_dma.hip), which the engine always takes; experiments build only)
 __global__ void convT_pack_bf16_kernel(const float* __restrict__ w, int Cin, int Cout, int dgrad,
                                        unsigned short* __restrict__ wp) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -200,6 +203,8 @@ __global__ __launch_bounds__(256, 2) void convT_bf16_kernel(TArgs p) {
     }
   }
 }
+
+#endif  // PMU_EXPERIMENTS
 
 // ---------------------------------------------------------------------------------------------
 // Weight gradient on bf16 MFMA: dW[ci][co][a][b] = sum_p xt[p][ci] * dut[pix_ab(p)][co]
@@ -464,6 +469,7 @@ constexpr int DB_G = 2048;  // dbias partial rows (blocks of the partial-sum pas
 
 }  // namespace
 
+#ifdef PMU_EXPERIMENTS
 static void set_grid(TArgs& p, int nnb) {
   static const int xcd = [] {
     const char* e = pmu_variant_env("PMU_CONVT_XCD");
@@ -522,6 +528,8 @@ extern "C" int pmu_convT2x2_dgrad_bf16(const float* du, int Hd, int Wd, int off_
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
+
+#endif  // PMU_EXPERIMENTS
 
 extern "C" size_t pmu_convT2x2_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout) {
   int nt, ns;

@@ -15,11 +15,14 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 # PMU_LIB=debug selects the bounds-checked debug build (csrc: make DEBUG=1; see pmu_debug_read);
 # PMU_LIB=exp a kernel-variant A/B build (csrc: make EXPERIMENTS=1 BLD=build_exp
 # OUT=../pmu_hip/libpmunet_hip_exp.so; not shipped, tools/ and scripts/ only)
-LIB_NAME = {"debug": "libpmunet_hip_debug.so", "exp": "libpmunet_hip_exp.so"}.get(os.environ.get("PMU_LIB", ""),
-                                                                                  "libpmunet_hip.so")
+# PMU_LIB=prev: a previous revision's release build placed there by an A/B script (scripts/gpu_r4_dma.sh)
+LIB_NAME = {"debug": "libpmunet_hip_debug.so", "exp": "libpmunet_hip_exp.so",
+            "prev": "libpmunet_hip_prev.so"}.get(os.environ.get("PMU_LIB", ""), "libpmunet_hip.so")
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 HEADER_PATH = os.path.normpath(
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "include", "pmunet_hip.h"))
+EXP_HEADER_PATH = os.path.join(os.path.dirname(HEADER_PATH), "pmunet_hip_experiments.h")
+EXP_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpmunet_hip_exp.so")
 
 PMU_OK = 0
 PMU_ERR_ARG = 1001
@@ -49,11 +52,7 @@ class PmuSgdChunk(ctypes.Structure):
 _FP = POINTER(PmuFrame)
 # name -> (restype, argtypes)
 SIGNATURES = {
-    "pmu_conv3x3_fwd": (c_int, [_FP, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "pmu_conv3x3_packed_size": (c_size_t, [c_int, c_int, c_int]),
-    "pmu_conv3x3_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_tiles": (c_int, [c_int, c_int, c_int]),
-    "pmu_conv3x3_dgrad": (c_int, [_FP, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_wgrad_ws": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_conv3x3_wgrad": (c_int, [_FP, _FP, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_conv3x3_packed_size_wino": (c_size_t, [c_int, c_int, c_int]),
@@ -61,10 +60,6 @@ SIGNATURES = {
     "pmu_conv3x3_tiles_wino": (c_int, [c_int, c_int, c_int]),
     "pmu_conv3x3_fwd_wino": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_wino": (c_int, [_FP, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "pmu_conv3x3_fwd_wino_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                                         c_void_p, c_void_p]),
-    "pmu_conv3x3_dgrad_wino_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-                                           c_void_p, c_void_p]),
     "pmu_conv3x3_packed_size_wino2h": (c_size_t, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_wino2h": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_tiles_wino2h": (c_int, [c_int, c_int, c_int]),
@@ -75,8 +70,6 @@ SIGNATURES = {
     "pmu_conv3x3_packed_size_wino4": (c_size_t, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_wino4": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_tiles_wino4": (c_int, [c_int, c_int, c_int]),
-    "pmu_conv3x3_fwd_wino4": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                                      c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_wino4": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                         c_void_p, c_void_p]),
     "pmu_conv3x3_wgrad_ws_wino": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
@@ -103,17 +96,11 @@ SIGNATURES = {
     "pmu_conv3x3_wgrad_ws_bf16": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_conv3x3_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                        c_size_t, c_void_p]),
-    "pmu_convT2x2_pack_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
-    "pmu_convT2x2_bf16_ok": (c_int, [_FP, c_int]),
-    "pmu_convT2x2_fwd_bf16": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
-    "pmu_convT2x2_dgrad_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
-                                        c_int, c_void_p, c_void_p]),
     "pmu_convT2x2_wgrad_ws_bf16": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_convT2x2_wgrad_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                         c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pmu_occupancy_conv3x3_raw": (c_int, [POINTER(c_int)]),
     "pmu_occupancy_wgrad3x3_bf16": (c_int, [POINTER(c_int)]),
-    "pmu_occupancy_conv3x3_pipe": (c_int, [POINTER(c_int)]),
     "pmu_conv_first_fwd": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p, c_void_p]),
     "pmu_conv_first_tiles": (c_int, [c_int, c_int, c_int]),
@@ -127,16 +114,12 @@ SIGNATURES = {
     "pmu_bn_eval_coef": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p]),
     "pmu_bn_bwd_reduce": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                   c_void_p]),
-    "pmu_bn_bwd_reduce_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
-                                     c_void_p]),
     "pmu_bn_bwd_tiles": (c_int, [c_int, c_int]),
     "pmu_bn_bwd_finalize": (c_int, [c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_bnrelu_apply": (c_int, [c_void_p, c_void_p, c_longlong, c_int, c_void_p, c_void_p]),
     "pmu_maxpool2_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                  c_void_p]),
-    "pmu_maxpool2_bwd_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
-                                    c_void_p]),
     "pmu_maxpool2_bwd_bnr_tiles": (c_int, [c_int, c_int, c_int, c_int]),
     "pmu_maxpool2_bwd_bnr": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                      c_void_p, c_int, c_void_p, c_void_p]),
@@ -223,14 +206,6 @@ SIGNATURES = {
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_dma_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "pmu_conv3x3_fwd_dma_zb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                                       c_void_p, c_void_p, c_void_p]),
-    "pmu_bn_center": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
-    "pmu_conv3x3_wgrad_ws_wino4": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
-    "pmu_conv3x3_wgrad_wino4": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
-                                        c_size_t, c_void_p]),
-    "pmu_conv3x3_dgrad_dma_bnr_zb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
-                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_pack_wino2h_blocks": (c_int, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_wino2h_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "pmu_conv3x3_pack_wino4_blocks": (c_int, [c_int, c_int, c_int]),
@@ -244,6 +219,38 @@ SIGNATURES = {
     "pmu_build_flags": (c_int, []),
     "pmu_debug_read": (c_int, [POINTER(c_int), POINTER(ctypes.c_char_p)]),
     "pmu_debug_reset": (c_int, []),
+}
+# The experiments build's extra entries (include/pmunet_hip_experiments.h; csrc make EXPERIMENTS=1): bound
+# when the loaded library exports them, never by the shipped one.
+EXP_SIGNATURES = {
+    "pmu_conv3x3_fwd": (c_int, [_FP, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_packed_size": (c_size_t, [c_int, c_int, c_int]),
+    "pmu_conv3x3_pack": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad": (c_int, [_FP, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_fwd_wino_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                         c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_wino_raw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                           c_void_p, c_void_p]),
+    "pmu_conv3x3_fwd_wino4": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                      c_void_p, c_void_p]),
+    "pmu_convT2x2_pack_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_bf16_ok": (c_int, [_FP, c_int]),
+    "pmu_convT2x2_fwd_bf16": (c_int, [_FP, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_dgrad_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                                        c_int, c_void_p, c_void_p]),
+    "pmu_occupancy_conv3x3_pipe": (c_int, [POINTER(c_int)]),
+    "pmu_bn_bwd_reduce_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                     c_void_p]),
+    "pmu_maxpool2_bwd_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                    c_void_p]),
+    "pmu_conv3x3_fwd_dma_zb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                       c_void_p, c_void_p, c_void_p]),
+    "pmu_bn_center": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_wgrad_ws_wino4": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_conv3x3_wgrad_wino4": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                        c_size_t, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_bnr_zb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 # The entry points whose kernels issue MFMAs (every other entry is VALU / memory work).  bench.py's
@@ -283,6 +290,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(cdll, name)  # AttributeError if the export is missing
         fn.restype = res
         fn.argtypes = args
+    for name, (res, args) in EXP_SIGNATURES.items():
+        if hasattr(cdll, name):
+            fn = getattr(cdll, name)
+            fn.restype = res
+            fn.argtypes = args
     return cdll
 
 
@@ -344,7 +356,13 @@ BUILD_EXPERIMENTS, BUILD_DEBUG = 1, 2
 
 
 def build_flags() -> int:
-    return int(lib().pmu_build_flags())
+    """pmu_build_flags() of the loaded library (cached on it: the engine asks per conv)."""
+    cdll = lib()
+    f = cdll.__dict__.get("_pmu_flags")
+    if f is None:
+        f = int(cdll.pmu_build_flags())
+        cdll.__dict__["_pmu_flags"] = f
+    return f
 
 
 def experiments_build() -> bool:

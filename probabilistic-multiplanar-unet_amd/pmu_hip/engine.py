@@ -481,7 +481,8 @@ def _conv_backward_tee32(out: ConvBNOut, dz_src, conv, dw, split, prod=None):
     Cin = conv.in_channels
     dzt = _empty(N, H, W, Cout, device=dev)
     res = _dgrad32(dz_src, conv, N, H, W, split, dzt, prod)
-    wsb4 = lb.pmu_conv3x3_wgrad_ws_wino4(N, H, W, Cin, Cout) if (use_wino() and CFG.wgrad4) else 0
+    wsb4 = (lb.pmu_conv3x3_wgrad_ws_wino4(N, H, W, Cin, Cout)
+            if (use_wino() and CFG.wgrad4 and L.experiments_build()) else 0)
     wsb = 0 if wsb4 else (lb.pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout) if use_wino() else 0)
     if wsb4:
         ws = _empty((wsb4 + 3) // 4, device=dev)
@@ -660,7 +661,6 @@ class EngineConfig:
 
 
 CFG = EngineConfig.from_env()
-_BF16_Z_FORCED = False   # tests: exercise the bf16-z path on the shipped library (monkeypatched)
 
 
 def wino4_ok(C: int, H: int, W: int, kind: str) -> bool:
@@ -677,7 +677,7 @@ def wino4_ok(C: int, H: int, W: int, kind: str) -> bool:
     mode = CFG.wino4
     if mode == "1" and not L.experiments_build():
         mode = "dgrad"
-    return C % 8 == 0 and H >= 32 and W >= 32 and (mode == "1" or mode == kind) and CFG.fp32_conv == "wino"
+    return C % 8 == 0 and H >= 32 and W >= 32 and (mode == "1" or mode == kind) and fp32_mode() == "wino"
 
 
 def _pack_weights_wino2h_now(w: torch.Tensor, dgrad: bool) -> torch.Tensor:
@@ -693,18 +693,26 @@ def wino2h_ok(C: int) -> bool:
     """The 1024-thread F(2x2) kernels (pmu_conv3x3_{fwd,dgrad}_wino2h; four waves per SIMD where the
     512-thread raw kernel runs two): C % 8 == 0.  kbench on the c2 shapes: forward 11.57 -> 10.98 ms
     (256x256 layers 1.04 -> 0.90 ms).  CFG.wino2h False: the 512-thread raw kernels."""
-    return C % 8 == 0 and CFG.wino2h
+    return C % 8 == 0 and (CFG.wino2h or not L.experiments_build())
+
+
+def fp32_mode() -> str:
+    """CFG.fp32_conv as honoured by the loaded library: "direct" (the direct-sum kernels) exists only in an
+    experiments build; the shipped library runs the default Winograd path instead."""
+    if CFG.fp32_conv == "direct" and not L.experiments_build():
+        return "wino"
+    return CFG.fp32_conv
 
 
 def use_wino() -> bool:
-    """fp32 3x3 convs (fwd and input gradient) by Winograd F(2x2,3x3) (CFG.fp32_conv "direct": direct sum)."""
-    return CFG.fp32_conv != "direct"
+    """fp32 3x3 convs (fwd and input gradient) by Winograd (fp32_mode() "direct": the direct sum)."""
+    return fp32_mode() != "direct"
 
 
 def wino_raw_ok(C: int) -> bool:
     """Winograd on a materialised operand (pmu_conv3x3_*_wino_raw): C % 16 == 0 (CFG.fp32_conv
     "wino_fused" keeps the fused-staging Winograd kernels)."""
-    return C % 16 == 0 and CFG.fp32_conv == "wino"
+    return C % 16 == 0 and fp32_mode() == "wino"
 
 
 def frame_to_f32(srcs, N, H, W) -> torch.Tensor:
@@ -854,7 +862,7 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
         first_srcs = [Src(xc.permute(0, 2, 3, 1).contiguous())]
     # ---- encoder
     c1w, b1, c2w, b2 = _dc_layers(net.inc)
-    zb = bf16 and CFG.bf16_z and (_BF16_Z_FORCED or L.experiments_build())
+    zb = bf16 and CFG.bf16_z and L.experiments_build()
     o1 = conv_bn_forward(first_srcs, c1w, b1, N, H, W, training, dev, planes=planes, bf16=bf16, keep=keep, zb=zb)
     o2 = conv_bn_forward([o1.act()], c2w, b2, N, H, W, training, dev, bf16=bf16, keep=keep, zb=zb)
     st.enc.append((o1, o2))
@@ -944,7 +952,7 @@ def unet_forward(net, x: torch.Tensor, training: bool, bf16: bool = False, keep:
                        L.ptr(convT.bias), Cin_t, Cup, u.data_ptr(), L.stream())
                 if not keep:
                     xtT = None
-            elif bf16 and lb.pmu_convT2x2_bf16_ok(fin, Cup):   # (refuses bf16-stored sources)
+            elif bf16 and L.experiments_build() and lb.pmu_convT2x2_bf16_ok(fin, Cup):   # (same shapes as the DMA one)
                 wpt = pack_convT_weights_bf16(convT.weight, dgrad=False)
                 L.call("pmu_convT2x2_fwd_bf16", fin, wpt.data_ptr(), L.ptr(convT.bias), Cup, u.data_ptr(), L.stream())
             else:
@@ -1044,7 +1052,7 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             wpt = pack_convT_weights_dma(convT.weight, dgrad=True)
             L.call("pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd, Wd, us.off[0], us.off[1], wpt.data_ptr(),
                    N, hi, wi, Cin_t, Cup, dx.data_ptr(), s)
-        elif us.bf16 and Cin_t % 128 == 0 and Cup % 32 == 0:
+        elif us.bf16 and Cin_t % 128 == 0 and Cup % 32 == 0 and L.experiments_build():
             wpt = pack_convT_weights_bf16(convT.weight, dgrad=True)
             L.call("pmu_convT2x2_dgrad_bf16", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], wpt.data_ptr(), N, hi, wi,
                    Cin_t, Cup, dx.data_ptr(), s)

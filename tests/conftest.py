@@ -39,3 +39,24 @@ def _debug_build_bounds_check(request):
         from pmu_hip import _lib as L
         if L._LIB is not None:
             L.debug_check()
+
+
+_EXP = {}
+
+
+@pytest.fixture
+def exp_lib(dev):
+    """The experiments library (csrc `make EXPERIMENTS=1`, include/pmunet_hip_experiments.h) in place of
+    the shipped one for this test: the kernels the default dispatch does not reach are tested against
+    it (the shipped library does not export them).  Skips when it is not built."""
+    from pmu_hip import _lib as L
+    if not os.path.exists(L.EXP_LIB_PATH):
+        pytest.skip("experiments library not built (make -C csrc EXPERIMENTS=1)")
+    prev = L.lib()
+    if "lib" not in _EXP:
+        _EXP["lib"] = L.load_library(L.EXP_LIB_PATH)
+    L._LIB = _EXP["lib"]
+    try:
+        yield _EXP["lib"]
+    finally:
+        L._LIB = prev

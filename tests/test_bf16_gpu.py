@@ -257,7 +257,7 @@ def _packT(w, dgrad):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 16, 16, 128, 64), (3, 9, 7, 64, 32), (1, 32, 24, 256, 128)])
-def test_convT_fwd_bf16(dev, N, H, W, Cin, Cout):
+def test_convT_fwd_bf16(dev, exp_lib, N, H, W, Cin, Cout):
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src, frame_of
     g = torch.Generator().manual_seed(21 + H)
@@ -277,7 +277,7 @@ def test_convT_fwd_bf16(dev, N, H, W, Cin, Cout):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,oh,ow", [(2, 16, 16, 128, 64, 0, 0), (2, 10, 9, 256, 32, 1, 0),
                                                   (1, 8, 12, 128, 128, 0, 1)])
-def test_convT_dgrad_bf16(dev, N, H, W, Cin, Cout, oh, ow):
+def test_convT_dgrad_bf16(dev, exp_lib, N, H, W, Cin, Cout, oh, ow):
     from pmu_hip import _lib as L
     g = torch.Generator().manual_seed(31 + H)
     Hd, Wd = 2 * H + oh + (1 if oh else 0), 2 * W + ow + (1 if ow else 0)

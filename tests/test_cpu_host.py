@@ -144,23 +144,35 @@ def test_bilinear_up_rejected_like_reference():
 
 
 # ----------------------------------------------------------------------------- C ABI
-def _header_functions():
+def _header_functions(path=None):
     from pmu_hip._lib import HEADER_PATH
-    src = open(HEADER_PATH).read()
+    src = open(path or HEADER_PATH).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(pmu_[A-Za-z0-9_]+)\s*\(", src)))
 
 
 def test_library_exports_every_header_symbol():
-    from pmu_hip._lib import LIB_PATH, SIGNATURES, load_library
+    """The shipped library exports exactly include/pmunet_hip.h (every declaration resolves, the ctypes
+    table mirrors it, and none of include/pmunet_hip_experiments.h is exported); the experiments library
+    exports both headers."""
+    from pmu_hip._lib import EXP_HEADER_PATH, EXP_LIB_PATH, EXP_SIGNATURES, LIB_PATH, SIGNATURES, load_library
     if not os.path.exists(LIB_PATH):
         pytest.skip("libpmunet_hip.so not built (run __graft_entry__.build())")
     cdll = load_library()
     names = _header_functions()
-    assert len(names) >= 25
+    exp_names = _header_functions(EXP_HEADER_PATH)
+    assert len(names) >= 25 and len(exp_names) >= 10
+    assert not set(names) & set(exp_names)
     for n in names:
         assert hasattr(cdll, n), f"{n} declared in include/pmunet_hip.h but not exported"
     assert set(SIGNATURES) == set(names), "ctypes SIGNATURES out of sync with the header"
+    assert set(EXP_SIGNATURES) == set(exp_names), "ctypes EXP_SIGNATURES out of sync with the experiments header"
+    shipped_exp = [n for n in exp_names if hasattr(cdll, n)]
+    assert not shipped_exp, f"experiments entries exported by the shipped library: {shipped_exp}"
+    if os.path.exists(EXP_LIB_PATH):
+        exp = load_library(EXP_LIB_PATH)
+        for n in names + exp_names:
+            assert hasattr(exp, n), f"{n} not exported by the experiments library"
 
 
 def test_library_rejects_bad_arguments_without_gpu():
@@ -170,7 +182,8 @@ def test_library_rejects_bad_arguments_without_gpu():
     if not os.path.exists(LIB_PATH):
         pytest.skip("library not built")
     cdll = load_library()
-    assert cdll.pmu_conv3x3_fwd(None, None, None, None, 0, None, None, None, None) == PMU_ERR_ARG
+    assert cdll.pmu_conv3x3_fwd_wino(None, None, None, 0, None, None, None, None) == PMU_ERR_ARG
+    assert cdll.pmu_conv3x3_fwd_dma(None, 16, 1, 32, 32, None, None, 64, None, None, None) == PMU_ERR_ARG
     assert cdll.pmu_sgd_clip(None, 0, None, ctypes.c_float(1), ctypes.c_float(1), ctypes.c_float(0.9),
                              ctypes.c_float(0.1), None) == PMU_ERR_ARG
     assert cdll.pmu_conv3x3_tiles(32, 256, 256) == 32 * 32 * 8
@@ -191,7 +204,7 @@ def _fake_args(name):
     frame a 2-image 64x64 frame of one 64-channel source, pointers None."""
     import ctypes
     from pmu_hip import _lib
-    res, types = _lib.SIGNATURES[name]
+    res, types = {**_lib.SIGNATURES, **_lib.EXP_SIGNATURES}[name]
     args = []
     for t in types:
         if t is ctypes.c_int or t is ctypes.c_longlong or t is ctypes.c_size_t:
@@ -214,7 +227,7 @@ def test_bench_counts_every_mfma_entry_point():
     from pmu_hip import _lib
     assert bench.KernelTimer.MFMA is _lib.MFMA_ENTRY_POINTS
     for name in _lib.MFMA_ENTRY_POINTS:
-        assert name in _lib.SIGNATURES, name
+        assert name in _lib.SIGNATURES or name in _lib.EXP_SIGNATURES, name
         fl = bench.KernelTimer._flops(name, _fake_args(name))
         assert fl > 0, name
         # the direct-sum basis of a Winograd launch is larger than its executed products, never zero

@@ -52,7 +52,7 @@ def _frames(kind, N, H, W, g, dev):
 
 @pytest.mark.parametrize("kind,N,H,W", [("bnrelu", 2, 40, 36), ("maxpool", 2, 24, 20), ("concat", 2, 33, 17),
                                         ("narrow", 1, 16, 16), ("bnrelu", 1, 7, 9)])
-def test_conv3x3_fwd_tee32(dev, kind, N, H, W):
+def test_conv3x3_fwd_tee32(dev, exp_lib, kind, N, H, W):
     from pmu_hip import _lib as L
     from pmu_hip.engine import frame_of, pack_weights
     g = torch.Generator().manual_seed(5 + H)
@@ -76,7 +76,7 @@ def test_conv3x3_fwd_tee32(dev, kind, N, H, W):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 40, 36, 128, 64, 64), (2, 17, 33, 64, 128, 64),
                                                   (1, 8, 8, 64, 64, 64)])
-def test_conv3x3_dgrad_tee32_and_raw_wgrad(dev, N, H, W, Cin, Cout, split):
+def test_conv3x3_dgrad_tee32_and_raw_wgrad(dev, exp_lib, N, H, W, Cin, Cout, split):
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src, frame_of, pack_weights
     g = torch.Generator().manual_seed(17 + W)

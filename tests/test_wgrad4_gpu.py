@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 32, 32, 64, 32), (1, 37, 45, 64, 64), (2, 16, 16, 128, 64),
                                             (2, 64, 48, 64, 96), (3, 9, 13, 64, 32), (1, 8, 8, 256, 128)])
-def test_wgrad_wino4_vs_fp64(dev, N, H, W, Cin, Cout):
+def test_wgrad_wino4_vs_fp64(dev, exp_lib, N, H, W, Cin, Cout):
     from pmu_hip import _lib as L
     g = torch.Generator().manual_seed(11 + H + Cin)
     x = torch.relu(torch.randn(N, H, W, Cin, generator=g))
@@ -39,7 +39,7 @@ def test_wgrad_wino4_vs_fp64(dev, N, H, W, Cin, Cout):
     assert rms <= 1e-5, rms
 
 
-def test_wgrad_wino4_ws_size_rules(dev):
+def test_wgrad_wino4_ws_size_rules(dev, exp_lib):
     from pmu_hip import _lib as L
     assert L.lib().pmu_conv3x3_wgrad_ws_wino4(2, 16, 16, 64, 48) == 0    # Cout % 32
     assert L.lib().pmu_conv3x3_wgrad_ws_wino4(2, 16, 16, 96, 32) == 0    # Cin % 64

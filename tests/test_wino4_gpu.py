@@ -28,7 +28,7 @@ def _rel(a, b):
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 32, 32, 64, 64), (1, 37, 45, 16, 40), (1, 70, 33, 48, 32),
                                             (2, 64, 64, 128, 96), (1, 33, 40, 8, 24), (1, 256, 64, 64, 64),
                                             (4, 64, 64, 64, 256)])  # last: 2-D grouped grid (8 co-groups x 4)
-def test_conv3x3_fwd_wino4(dev, N, H, W, Cin, Cout):
+def test_conv3x3_fwd_wino4(dev, exp_lib, N, H, W, Cin, Cout):
     from pmu_hip import _lib as L
     from pmu_hip.engine import pack_weights_wino4
     g = torch.Generator().manual_seed(43 + H + Cin)
@@ -126,7 +126,10 @@ def test_wino4_multipass(cpb):
     input gradient with Cin = 160 (5 co-blocks, concat split inside a pass) and forward with
     Cout = 160 (bias and BN partial sums per pass)."""
     pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "probabilistic-multiplanar-unet_amd")
-    env = dict(os.environ, PMU_WINO4_CPB=str(cpb))
+    from pmu_hip import _lib as L
+    if not os.path.exists(L.EXP_LIB_PATH):
+        pytest.skip("experiments library not built (make -C csrc EXPERIMENTS=1)")
+    env = dict(os.environ, PMU_WINO4_CPB=str(cpb), PMU_LIB="exp")   # the forward half: experiments build
     out = subprocess.run([sys.executable, "-c", _MULTIPASS4, pkg], env=env, capture_output=True, text=True,
                          timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]

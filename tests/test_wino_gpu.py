@@ -134,7 +134,7 @@ def test_conv3x3_wgrad_wino(dev, N, H, W, Cin, Cout):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 32, 32, 64, 64), (1, 37, 45, 16, 40), (3, 16, 16, 512, 96),
                                             (2, 9, 7, 32, 10), (1, 70, 20, 48, 32)])
-def test_conv3x3_fwd_wino_raw(dev, N, H, W, Cin, Cout):
+def test_conv3x3_fwd_wino_raw(dev, exp_lib, N, H, W, Cin, Cout):
     from pmu_hip import _lib as L
     from pmu_hip.engine import pack_weights_wino
     g = torch.Generator().manual_seed(41 + H + Cin)
@@ -156,7 +156,7 @@ def test_conv3x3_fwd_wino_raw(dev, N, H, W, Cin, Cout):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 40, 36, 64, 64, 64), (2, 17, 33, 128, 64, 64),
                                                   (1, 16, 16, 96, 128, 32), (2, 9, 7, 12, 16, 12)])
-def test_conv3x3_dgrad_wino_raw(dev, N, H, W, Cin, Cout, split):
+def test_conv3x3_dgrad_wino_raw(dev, exp_lib, N, H, W, Cin, Cout, split):
     from pmu_hip import _lib as L
     from pmu_hip.engine import pack_weights_wino
     g = torch.Generator().manual_seed(5 + H + Cout)
@@ -175,7 +175,7 @@ def test_conv3x3_dgrad_wino_raw(dev, N, H, W, Cin, Cout, split):
 
 
 @pytest.mark.parametrize("fused", [False, True])
-def test_unet_wino_matches_direct(dev, monkeypatch, fused):
+def test_unet_wino_matches_direct(dev, exp_lib, monkeypatch, fused):
     """The whole c2 architecture, one training step, with the Winograd kernels (default: materialised
     operands; or the fused-staging variant) and with the direct-sum kernels, both against the fp64
     CPU oracle: the Winograd gradients are as close to fp64 as the direct ones (within 2x of the
@@ -269,7 +269,10 @@ def test_wino_raw_multipass(cpb):
     import subprocess
     import sys
     pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "probabilistic-multiplanar-unet_amd")
-    env = dict(os.environ, PMU_WINO_CPB=str(cpb))
+    from pmu_hip import _lib as L
+    if not os.path.exists(L.EXP_LIB_PATH):
+        pytest.skip("experiments library not built (make -C csrc EXPERIMENTS=1)")
+    env = dict(os.environ, PMU_WINO_CPB=str(cpb), PMU_LIB="exp")   # the raw kernels: experiments build
     out = subprocess.run([sys.executable, "-c", _MULTIPASS, pkg], env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     assert float(out.stdout.strip().splitlines()[-1]) <= TOL

@@ -15,7 +15,7 @@ def _bits(t):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 40, 64, 64, 64), (1, 33, 45, 128, 96), (2, 32, 32, 256, 128)])
-def test_fwd_dma_zb_is_rounded_fp32(dev, N, H, W, Cin, Cout):
+def test_fwd_dma_zb_is_rounded_fp32(dev, exp_lib, N, H, W, Cin, Cout):
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src, frame_to_bf16, pack_weights_dma
     g = torch.Generator().manual_seed(3 + H + Cin)
@@ -46,7 +46,7 @@ def test_fwd_dma_zb_is_rounded_fp32(dev, N, H, W, Cin, Cout):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 40, 64, 64, 64), (1, 33, 45, 128, 96)])
-def test_dgrad_dma_bnr_zb(dev, N, H, W, Cin, Cout):
+def test_dgrad_dma_bnr_zb(dev, exp_lib, N, H, W, Cin, Cout):
     """The *_bnr_zb partials equal the fp32-z kernel's on z rounded to bf16 bit for bit (same arithmetic
     on the same values), and dx is unchanged."""
     from pmu_hip import _lib as L
@@ -72,7 +72,7 @@ def test_dgrad_dma_bnr_zb(dev, N, H, W, Cin, Cout):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-def test_bn_bwd_reduce_and_maxpool_bwd_zb(dev):
+def test_bn_bwd_reduce_and_maxpool_bwd_zb(dev, exp_lib):
     from pmu_hip import _lib as L
     g = torch.Generator().manual_seed(41)
     N, H, W, C = 2, 34, 50, 64
@@ -100,7 +100,7 @@ def test_bn_bwd_reduce_and_maxpool_bwd_zb(dev):
 
 
 @pytest.mark.parametrize("mode", ["bnrelu", "bnrelu_pool", "concat", "bnbwd"])
-def test_frames_with_bf16_sources(dev, mode):
+def test_frames_with_bf16_sources(dev, exp_lib, mode):
     """pmu_frame_to_bf16 / _f32 over bf16-stored sources = over the same values stored in fp32."""
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src, frame_of, frame_to_bf16, frame_to_f32
@@ -167,7 +167,7 @@ def test_head_with_bf16_source(dev):
 
 
 @pytest.mark.parametrize("bf16_z", [True, False])
-def test_unet_bf16_z_modes_vs_oracle(dev, monkeypatch, bf16_z):
+def test_unet_bf16_z_modes_vs_oracle(dev, exp_lib, monkeypatch, bf16_z):
     """Model level, both z modes against the oracle's autocast arithmetic with the same z rounding
     (oracle.unet_ref.BF16_Z): one training step of UNet(3, 3, [64, 128, 256]) at 64 x 64 (DMA convs
     with bf16-stored z at 64 and 32 wide, raw convs with rounded fp32 z at 16 wide).  Tolerance as
@@ -177,7 +177,6 @@ def test_unet_bf16_z_modes_vs_oracle(dev, monkeypatch, bf16_z):
     from model import UNet
     from pmu_hip import engine
     monkeypatch.setattr(engine.CFG, "bf16_z", bf16_z)
-    monkeypatch.setattr(engine, "_BF16_Z_FORCED", True)
     monkeypatch.setattr(U, "BF16_Z", bf16_z)
     torch.manual_seed(0)
     net = UNet(3, 3, [64, 128, 256])
@@ -215,7 +214,7 @@ def test_unet_bf16_z_modes_vs_oracle(dev, monkeypatch, bf16_z):
     assert err <= tol_g, (err, worst, tol_g)
 
 
-def test_bn_center(dev):
+def test_bn_center(dev, exp_lib):
     from pmu_hip import _lib as L
     g = torch.Generator().manual_seed(71)
     C = 96
