@@ -20,3 +20,4 @@ timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/ben
 timeout -k 10 300 python bench.py --workload c5 --no-cpu-baseline --no-eval > $O/bench_c5.json 2> $O/bench_c5.err || exit $?
 cut -c 1-200 $O/bench_c2.json $O/bench_c5.json
 bash scripts/gpu_mfma_calib.sh || exit $?
+bash scripts/gpu_sq_dma.sh || exit $?

@@ -76,8 +76,9 @@ def main():
         wsb = L.lib().pmu_conv3x3_wgrad_ws(N, H, W, Cin, Cout)
         ws = torch.empty(wsb // 4 + 1, device=dev)
         from pmu_hip.engine import pack_weights
-        wpf = pack_weights(w, False) if not args.unpacked else None
-        wpd = pack_weights(w, True) if not args.unpacked else None
+        exp = hasattr(L.lib(), "pmu_conv3x3_fwd")   # the direct-sum conv: experiments library (PMU_LIB=exp)
+        wpf = pack_weights(w, False) if exp and not args.unpacked else None
+        wpd = pack_weights(w, True) if exp and not args.unpacked else None
         def packb(wt, dg):
             n = L.lib().pmu_conv3x3_packed_size_bf16(wt.shape[0], wt.shape[1], int(dg)) // 2
             t = torch.empty(n, dtype=torch.int16, device=dev)
@@ -104,7 +105,7 @@ def main():
         dzt32 = torch.randn(N, H, W, Cout, device=dev)
         wsbw = L.lib().pmu_conv3x3_wgrad_ws_wino(N, H, W, Cin, Cout)
         wsw = torch.empty(max(wsbw, 4) // 4, device=dev)
-        wsb4 = L.lib().pmu_conv3x3_wgrad_ws_wino4(N, H, W, Cin, Cout)
+        wsb4 = L.lib().pmu_conv3x3_wgrad_ws_wino4(N, H, W, Cin, Cout) if exp else 0
         ws4 = torch.empty(max(wsb4, 4) // 4, device=dev)
         from pmu_hip.engine import pack_weights_wino
         wwf, wwd = pack_weights_wino(w, False), pack_weights_wino(w, True)

@@ -55,7 +55,8 @@ def main():
         from pmu_hip.engine import frame_to_bf16, pack_convT_weights_bf16, pack_convT_weights_dma
         xt = frame_to_bf16([Src(z, L.SRC_BNRELU, coef)], N, H, W)
         dut = frame_to_bf16([Src(du)], N, Hd, Wd)
-        wbf, wbd = pack_convT_weights_bf16(w, False), pack_convT_weights_bf16(w, True)
+        exp = hasattr(L.lib(), "pmu_convT2x2_pack_bf16")   # register-staged bf16 ConvT: experiments library
+        wbf, wbd = (pack_convT_weights_bf16(w, False), pack_convT_weights_bf16(w, True)) if exp else (None, None)
         wdf, wdd = pack_convT_weights_dma(w, False), pack_convT_weights_dma(w, True)
         wsbb = L.lib().pmu_convT2x2_wgrad_ws_bf16(N, H, W, Cin, Cout)
         wsb16 = torch.empty(max(1, (wsbb + 3) // 4), device=dev)
