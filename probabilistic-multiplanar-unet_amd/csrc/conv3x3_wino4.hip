@@ -500,16 +500,21 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
                                    (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
+  // Passes walk the chunks in alternating (serpentine) order: a pass starts on the chunks the previous
+  // pass fetched last, which are still in the XCD's L2 (~3 of a workgroup's 37-KB chunk images fit its
+  // share), instead of on chunk 0, fetched longest ago.
 #define PMU_FETCH4(GI, BUF)                                                                                 \
   {                                                                                                        \
     const int p_ = (GI) / nchunks;                                                                         \
-    const int k0_ = ((GI) - p_ * nchunks) * BK;                                                            \
+    const int c_ = (GI) - p_ * nchunks;                                                                    \
+    const int cs_ = (p_ & 1) ? nchunks - 1 - c_ : c_;                                                      \
+    const int k0_ = cs_ * BK;                                                                              \
     PMU_DCHECK(k0_ + BK <= a.KC, PMU_DBG_OPERAND);                                                         \
     float* b_ = (BUF);                                                                                     \
     const char* xb_ = reinterpret_cast<const char*>(a.x + k0_);                                            \
     _Pragma("unroll") for (int r = 0; r < NGL; ++r)                                                        \
       if ((gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                           \
-    const char* s_ = reinterpret_cast<const char*>(wsrc + (long long)(GI) * U_FLOATS) + uoff;              \
+    const char* s_ = reinterpret_cast<const char*>(wsrc + ((long long)p_ * nchunks + cs_) * U_FLOATS) + uoff; \
     float* d_ = b_ + A_FLOATS + wave_off;                                                                  \
     _Pragma("unroll") for (int r = 0; r < UGL; ++r)                                                        \
       if (r * NT * 4 + (wave + 1) * 256 <= U_FLOATS) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)          \

@@ -224,8 +224,11 @@ __global__ __launch_bounds__(256, 2) void convT_wgrad_kernel(TwArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int TW = 1 << a.twl, TH = TPIX >> a.twl;
   const int nci = (a.Cin + TB - 1) / TB;
-  const int ci0 = (blockIdx.x % nci) * TB, co0 = (blockIdx.x / nci) * TB;
-  const int split = blockIdx.y;
+  // (channel block, split) in XCD order, channel blocks fastest (see wgrad3x3_bf16.hip)
+  const int nblk = gridDim.x;
+  const int lbk = pmu_xcd_block(blockIdx.y * nblk + blockIdx.x, nblk * gridDim.y);
+  const int ci0 = (lbk % nblk % nci) * TB, co0 = (lbk % nblk / nci) * TB;
+  const int split = lbk / nblk;
   const int cif = wave >> 1, cof = wave & 1;
   const bool do_bias = (a.bws != nullptr) && ci0 == 0;
   const bool vec = (a.Cout & 3) == 0;

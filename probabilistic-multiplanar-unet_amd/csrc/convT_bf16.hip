@@ -243,8 +243,13 @@ __global__ __launch_bounds__(256, 2) void convT_wgrad_bf16_kernel(TwbArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Ds[4 * WPX * DSW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nco = pmu_cdiv_dev(a.Cout, WCO);
-  const int co0 = (blockIdx.x % nco) * WCO, ci0 = (blockIdx.x / nco) * WCI;
-  const int split = blockIdx.y;
+  // (channel block, split) in XCD order, channel blocks fastest: the blocks of one split read the same
+  // pixel rows at the same time through one XCD's L2 (see wgrad3x3_bf16.hip)
+  const int nblk = gridDim.x;
+  const int lbk = pmu_xcd_block(blockIdx.y * nblk + blockIdx.x, nblk * gridDim.y);
+  const int blk = lbk % nblk;
+  const int co0 = (blk % nco) * WCO, ci0 = (blk / nco) * WCI;
+  const int split = lbk / nblk;
   const long long P = (long long)a.N * a.H * a.W;
   const int t_beg = (int)(((long long)a.ntiles * split) / a.nsplit);
   const int t_end = (int)(((long long)a.ntiles * (split + 1)) / a.nsplit);

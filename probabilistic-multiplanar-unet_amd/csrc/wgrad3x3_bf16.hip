@@ -141,8 +141,14 @@ __global__ __launch_bounds__(NT, 3) void wgrad3x3_bf16_kernel(WgbArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * G::SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nco = pmu_cdiv_dev(a.Cout, WCO);
-  const int co0 = (blockIdx.x % nco) * WCO, ci0 = (blockIdx.x / nco) * WCI;
-  const int split = blockIdx.y;
+  // (channel block, split) in XCD order, channel blocks fastest: the blocks of one split walk the same
+  // pixel tiles in step on one XCD, so its L2 serves each tile to all of them (in launch order they
+  // sat on different XCDs and each fetched every tile from HBM)
+  const int nblk = gridDim.x;
+  const int lbk = pmu_xcd_block(blockIdx.y * nblk + blockIdx.x, nblk * gridDim.y);
+  const int blk = lbk % nblk;
+  const int co0 = (blk % nco) * WCO, ci0 = (blk / nco) * WCI;
+  const int split = lbk / nblk;
   // wave -> (co group, ci fragment, kernel row)
   const int kh = wave % 3, cif = (wave / 3) & 1, cog = wave / 6;  // cog < 2
   // WCO = 64: 2 co groups of one fragment; WCO = 128: 2 co groups of two fragments
