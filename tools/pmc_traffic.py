@@ -52,6 +52,16 @@ def main():
     meta = {"formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes per dispatch (gfx950 FETCH_SIZE counts half "
                        "of 16B/lane reads; counters in KiB)",
             "fetch_dir": fdir, "write_dir": wdir}
+    steps = 0
+    if "--steps" in sys.argv:
+        steps = int(sys.argv[sys.argv.index("--steps") + 1])
+    if steps > 0:
+        # every dispatch of the profiled command (timed + warm-up steps, plus the one-time setup launches:
+        # weight init, the first packs) divided by the steps it ran: an upper bound on the per-step bytes
+        tot = sum(v["hbm_bytes_per_dispatch"] * max(v["dispatches_fetch_pass"], 1) for v in res.values())
+        meta["steps_profiled"] = steps
+        meta["hbm_gb_per_step"] = tot / steps / 1e9
+        print(f"HBM per step: {tot / steps / 1e9:.2f} GB ({steps} steps profiled, setup launches included)")
     json.dump({"meta": meta, "kernels": res}, open(out, "w"), indent=1)
     top = sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_dispatch"] * max(1, kv[1]["dispatches_fetch_pass"]))
     for k, v in top[:12]:
