@@ -388,12 +388,93 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const float* __restri
 // element), adds dpool to the first max, writes da and accumulates (sum g, sum g*xhat),
 // g = da * (z*scale+shift > 0), xhat = (z-mean)*invstd — the part[block][2][C] slab bn_bwd_reduce
 // would compute from a second pass over da and z.  Block = 256 threads over wpb windows.
+// Streaming form (as frame_stream_kernel): a thread's windows run in ping-pong pairs, the next
+// window's nine float4 loads in flight while this one is routed and stored; every load is
+// unconditional (addresses clamped into the map, the values of outside pixels / partial windows
+// masked afterwards) and only the stores are predicated — loads under per-window branches, consumed
+// right after, left one global round trip exposed per window (4.9 TB/s at c5's 512^2 level).
+struct MpWin {
+  float4 z[4], d[4], g;
+};
+
+template <bool ACC>
+__device__ __forceinline__ void mp_load(const float* __restrict__ dpool, const float* __restrict__ z,
+                                        const float* __restrict__ dx, long long wi, int H, int W, int C, int c,
+                                        MpWin& m) {
+  const int Hp = H / 2, Wp = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const int wc = (int)(wi % Wc);
+  const long long r = wi / Wc;
+  const int hc = (int)(r % Hc);
+  const int n = (int)(r / Hc);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int h = min(2 * hc + (k >> 1), H - 1), w = min(2 * wc + (k & 1), W - 1);
+    const long long off = (((long long)n * H + h) * W + w) * C + c;
+    m.z[k] = *reinterpret_cast<const float4*>(z + off);
+    if (ACC) m.d[k] = *reinterpret_cast<const float4*>(dx + off);
+  }
+  const long long po = (((long long)n * Hp + min(hc, Hp - 1)) * Wp + min(wc, Wp - 1)) * C + c;
+  m.g = *reinterpret_cast<const float4*>(dpool + po);
+}
+
+template <bool ACC>
+__device__ __forceinline__ void mp_route(const MpWin& m, long long wi, bool valid, int H, int W, int C, int c,
+                                         const float (&scv)[4], const float (&shv)[4], const float (&muv)[4],
+                                         const float (&isv)[4], float* __restrict__ dx, float (&sg)[4], float (&sgx)[4]) {
+  const int Hp = H / 2, Wp = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const int wc = (int)(wi % Wc);
+  const long long r = wi / Wc;
+  const int hc = (int)(r % Hc);
+  const int n = (int)(r / Hc);
+  const bool full = hc < Hp && wc < Wp;
+  float zv[4][4], dv[4][4];
+  bool ok[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    ok[k] = valid && 2 * hc + (k >> 1) < H && 2 * wc + (k & 1) < W;
+    zv[k][0] = m.z[k].x; zv[k][1] = m.z[k].y; zv[k][2] = m.z[k].z; zv[k][3] = m.z[k].w;
+    if (ACC) { dv[k][0] = m.d[k].x; dv[k][1] = m.d[k].y; dv[k][2] = m.d[k].z; dv[k][3] = m.d[k].w; }
+    else { dv[k][0] = 0.f; dv[k][1] = 0.f; dv[k][2] = 0.f; dv[k][3] = 0.f; }
+  }
+  const float gv[4] = {full ? m.g.x : 0.f, full ? m.g.y : 0.f, full ? m.g.z : 0.f, full ? m.g.w : 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {  // route dpool to the first max of relu(z*sc+sh) (a full window only: gv = 0 else)
+    float best = fmaxf(0.f, fmaf(zv[0][e], scv[e], shv[e]));
+    int arg = 0;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float a = fmaxf(0.f, fmaf(zv[k][e], scv[e], shv[e]));
+      if (a > best) { best = a; arg = k; }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dv[k][e] += arg == k ? gv[e] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gg = (ok[k] && fmaf(zv[k][e], scv[e], shv[e]) > 0.f) ? dv[k][e] : 0.f;
+      sg[e] += gg;
+      sgx[e] = fmaf(gg, (zv[k][e] - muv[e]) * isv[e], sgx[e]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (!ok[k]) continue;
+    const int h = 2 * hc + (k >> 1), w = 2 * wc + (k & 1);
+    const long long off = (((long long)n * H + h) * W + w) * C + c;
+    PMU_DCHECK(off + 4 <= (long long)n * H * W * C + (long long)H * W * C, PMU_DBG_OUTPUT);
+    *reinterpret_cast<float4*>(dx + off) = make_float4(dv[k][0], dv[k][1], dv[k][2], dv[k][3]);
+  }
+}
+
+template <bool ACC>
 __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __restrict__ dpool,
                                                                const float* __restrict__ z,
                                                                const float* __restrict__ coef,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ invstd, int N, int H, int W,
-                                                               int C, int wpb, float* __restrict__ dx, int accumulate,
+                                                               int C, int wpb, float* __restrict__ dx,
                                                                float* __restrict__ part) {
   __shared__ float red[256 * 8];
   const int tid = threadIdx.x;
@@ -401,7 +482,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __re
   const int npg = CQ >= 256 ? 1 : 256 / CQ;
   const int qstride = CQ >= 256 ? 256 : CQ;
   const int pg = tid / qstride, q0 = tid % qstride;
-  const int Hp = H / 2, Wp = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;
   const long long nwin = (long long)N * Hc * Wc;
   const long long w0 = (long long)blockIdx.x * wpb;
   const long long wend = min(nwin, w0 + wpb);
@@ -418,57 +499,20 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __re
     const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
     float sg[4] = {0, 0, 0, 0}, sgx[4] = {0, 0, 0, 0};
     if (pg < npg && q < CQ) {
-      for (long long wi = w0 + pg; wi < wend; wi += npg) {
-        const int wc = (int)(wi % Wc);
-        const long long r = wi / Wc;
-        const int hc = (int)(r % Hc);
-        const int n = (int)(r / Hc);
-        float zv[4][4], dv[4][4];
-        bool ok[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int h = 2 * hc + (k >> 1), w = 2 * wc + (k & 1);
-          ok[k] = h < H && w < W;
-          const long long off = ((((long long)n * H + (ok[k] ? h : 0)) * W + (ok[k] ? w : 0)) * C + c);
-          PMU_DCHECK(off + 4 <= (long long)N * H * W * C, PMU_DBG_OPERAND);
-          float4 zz = make_float4(0.f, 0.f, 0.f, 0.f), dd = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (ok[k]) {
-            zz = *reinterpret_cast<const float4*>(z + off);
-            if (accumulate) dd = *reinterpret_cast<const float4*>(dx + off);
-          }
-          zv[k][0] = zz.x; zv[k][1] = zz.y; zv[k][2] = zz.z; zv[k][3] = zz.w;
-          dv[k][0] = dd.x; dv[k][1] = dd.y; dv[k][2] = dd.z; dv[k][3] = dd.w;
-        }
-        if (hc < Hp && wc < Wp) {  // a full window: route dpool to the first max of relu(z*sc+sh)
-          const float4 g = *reinterpret_cast<const float4*>(dpool + (((long long)n * Hp + hc) * Wp + wc) * C + c);
-          const float gv[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float best = fmaxf(0.f, fmaf(zv[0][e], scv[e], shv[e]));
-            int arg = 0;
-#pragma unroll
-            for (int k = 1; k < 4; ++k) {
-              const float a = fmaxf(0.f, fmaf(zv[k][e], scv[e], shv[e]));
-              if (a > best) { best = a; arg = k; }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              if (arg == k) dv[k][e] += gv[e];
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (!ok[k]) continue;
-          const int h = 2 * hc + (k >> 1), w = 2 * wc + (k & 1);
-          const long long off = (((long long)n * H + h) * W + w) * C + c;
-          *reinterpret_cast<float4*>(dx + off) = make_float4(dv[k][0], dv[k][1], dv[k][2], dv[k][3]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float gg = fmaf(zv[k][e], scv[e], shv[e]) > 0.f ? dv[k][e] : 0.f;
-            sg[e] += gg;
-            sgx[e] = fmaf(gg, (zv[k][e] - muv[e]) * isv[e], sgx[e]);
-          }
-        }
+      const long long last = wend - 1;
+      MpWin A, B;
+      long long wi = w0 + pg;
+      mp_load<ACC>(dpool, z, dx, min(wi, last), H, W, C, c, A);
+      for (; wi < wend; wi += 2 * npg) {
+        const long long wb = wi + npg, wa = wi + 2 * npg;
+        mp_load<ACC>(dpool, z, dx, min(wb, last), H, W, C, c, B);
+        __builtin_amdgcn_sched_barrier(0);
+        mp_route<ACC>(A, wi, true, H, W, C, c, scv, shv, muv, isv, dx, sg, sgx);
+        __builtin_amdgcn_sched_barrier(0);
+        mp_load<ACC>(dpool, z, dx, min(wa, last), H, W, C, c, A);
+        __builtin_amdgcn_sched_barrier(0);
+        mp_route<ACC>(B, min(wb, last), wb < wend, H, W, C, c, scv, shv, muv, isv, dx, sg, sgx);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 #pragma unroll
@@ -667,6 +711,8 @@ constexpr int HPPB = 2048;  // pixels per block in the fast head kernels
 // loads of a pixel's quads coalesce into its whole C-channel row; per class the quad dot products
 // are summed over the pixel's CQ lanes by xor shuffles and lane cq == 0 writes y[n][k][pix].
 // (One thread per pixel read a 16-B piece of 64 different rows per load instruction.)
+template <bool XBF>  // the source's x in bf16 (a compile-time choice: a load under the storage-type branch
+                    // would be waited for on its own)
 __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const float* __restrict__ w,
                                                             const float* __restrict__ b, int K, int do_sigmoid,
                                                             float* __restrict__ y) {
@@ -684,19 +730,33 @@ __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const fl
     wq[k] = k < K ? *reinterpret_cast<const float4*>(w + k * C + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
     bk[k] = (k < K && b) ? b[k] : 0.f;
   }
+  // HU pixels per thread per round, their loads issued together (address clamped to the block's last
+  // pixel, only the stores predicated): one pixel per round left a global round trip exposed per
+  // pixel (c5 512^2: 0.30 ms for 1.07 GB)
+  constexpr int HU = 4;
   const unsigned pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
-  for (unsigned p = blockIdx.x * HPPB + pg; p < pend; p += PG) {  // 32-bit decode (P < 2^31)
-    const float4 a = pmu_bnrelu4(src_x4(f.s0, (long long)p * C + 4 * cq), sc, sh);
-    const unsigned n = p / HWu, pix = p - n * HWu;
+  for (unsigned p0 = blockIdx.x * HPPB + pg; p0 < pend; p0 += HU * PG) {  // 32-bit decode (P < 2^31)
+    float4 zx[HU];
 #pragma unroll
-    for (int k = 0; k < HEAD_KMAX; ++k) {
-      if (k >= K) break;
-      float v = fmaf(a.x, wq[k].x, fmaf(a.y, wq[k].y, fmaf(a.z, wq[k].z, a.w * wq[k].w)));
-      for (int o = 1; o < CQ; o <<= 1) v += __shfl_xor(v, o, 64);
-      if (cq == 0) {
+    for (int u = 0; u < HU; ++u) {
+      const unsigned p = min(p0 + u * PG, pend - 1);
+      const long long i = (long long)p * C + 4 * cq;
+      zx[u] = XBF ? pmu_ld4(reinterpret_cast<const unsigned short*>(f.s0.x) + i) : pmu_ld4(f.s0.x + i);
+    }
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const unsigned p = p0 + u * PG;
+      const float4 a = pmu_bnrelu4(zx[u], sc, sh);
+      const unsigned pc = min(p, pend - 1);
+      const unsigned n = pc / HWu, pix = pc - n * HWu;
+#pragma unroll
+      for (int k = 0; k < HEAD_KMAX; ++k) {
+        if (k >= K) break;
+        float v = fmaf(a.x, wq[k].x, fmaf(a.y, wq[k].y, fmaf(a.z, wq[k].z, a.w * wq[k].w)));
+        for (int o = 1; o < CQ; o <<= 1) v += __shfl_xor(v, o, 64);
         v += bk[k];
         if (do_sigmoid) v = 1.f / (1.f + expf(-v));
-        y[(size_t)(n * K + k) * HWu + pix] = v;
+        if (cq == 0 && p < pend) y[(size_t)(n * K + k) * HWu + pix] = v;
       }
     }
   }
@@ -1378,8 +1438,12 @@ extern "C" int pmu_maxpool2_bwd_bnr(const float* dpool, const float* z, const fl
                                     float* part, void* stream) {
   PMU_REQUIRE(dpool && z && coef && mean && invstd && dx && part && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
   const int R = pmu_maxpool2_bwd_bnr_tiles(N, H, W, C);
-  hipLaunchKernelGGL(maxpool2_bwd_bnr_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dpool, z, coef,
-                     mean, invstd, N, H, W, C, mpb_wpb(C), dx, accumulate, part);
+  if (accumulate)
+    hipLaunchKernelGGL(maxpool2_bwd_bnr_kernel<true>, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dpool, z,
+                       coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part);
+  else
+    hipLaunchKernelGGL(maxpool2_bwd_bnr_kernel<false>, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dpool, z,
+                       coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -1414,7 +1478,8 @@ extern "C" int pmu_head1x1_fwd(const pmu_frame* in, const float* w, const float*
   const DevFrame f = make_dev_frame(in);
   const long long P = (long long)in->N * in->H * in->W;
   if (host_head_fast(in) && P < (1LL << 31)) {
-    hipLaunchKernelGGL(head_fwd_fast_kernel, dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(f.s0.xbf ? head_fwd_fast_kernel<true> : head_fwd_fast_kernel<false>,
+                       dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
                        f, w, b, K, do_sigmoid, y);
     PMU_CHECK_LAUNCH();
     return PMU_OK;

@@ -15,7 +15,9 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+#ifdef PMU_EXPERIMENTS
 constexpr int TM = 128, TN = 128, TK = 32, TLS = 40;  // LDS row stride (bf16)
+#endif
 
 struct TArgs {
   const float* a;             // fwd: z [M][Cin] (pre-BN);  dgrad: du [N][Hd][Wd][Cout]

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void convT_pack_dma_multi_kernel(const pmu_pac
 template <bool DGRAD, int WN>
 __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
   using G = TG<WN>;
-  constexpr int NS = G::NSTAGE, WM = G::WM, BN = G::BN, NUA = G::NUA, NUB = G::NUB, NDMA = NUA + NUB;
+  constexpr int NS = G::NSTAGE, BN = G::BN, NUA = G::NUA, NUB = G::NUB, NDMA = NUA + NUB;
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);

@@ -18,37 +18,49 @@ struct FirstArgs {
   float* part;
 };
 
-// Tiled forward: block = 8 x 32 output pixels of one image x all Cout.  The (8+2) x (32+2) x CIN
-// input patch is staged in LDS once (zero halo), each thread keeps its channel quad's 9*CIN
-// weight float4 in registers, and per pixel reads the 9*CIN inputs from LDS (one address per pixel:
-// broadcast over the quad lanes) into packed 2-wide FMAs.  The per-pixel global loads of the
-// untiled kernel (27 per pixel at CIN = 3) and its LDS weight reads made it ~5x slower than the
-// z write it must do.
+// Tiled forward: a block walks FT_TPB consecutive 8 x 32 output-pixel tiles of one image row band x
+// all Cout.  Each tile's (8+2) x (32+2) x CIN input patch is staged in LDS (zero halo; the next tile's
+// patch values are loaded into registers under the current tile's FMAs, so only a block's first
+// patch load is exposed), each thread keeps its channel quad's 9*CIN weight float4 in registers, and
+// per pixel reads the 9*CIN inputs from LDS (one address per pixel: broadcast over the quad lanes)
+// into packed 2-wide FMAs.  BN partial sums: one row per tile (pmu_conv_first_tiles rows).
 constexpr int FT_H = 8, FT_W = 32, FT_PH = FT_H + 2, FT_PW = FT_W + 2;
+constexpr int FT_TPB = 4;  // tiles per forward block (one block per tile exposed each patch load: 0.35 ms at c5)
 
 typedef float pmu_f2 __attribute__((ext_vector_type(2)));
 
+// the (8+2) x (32+2) x CIN patch values of one tile this thread stages (zero outside the image)
 template <int CIN>
-__global__ __launch_bounds__(256) void conv_first_fwd_tile_kernel(FirstArgs a, int tiles_w, int tiles_h) {
-  __shared__ float patch[CIN * FT_PH * FT_PW];
-  __shared__ float red[256 * 8];
-  const int tid = threadIdx.x;
-  const int CQ = a.Cout >> 2, npl = 256 / CQ;
-  const int cq = tid % CQ, pl = tid / CQ;
-  int t = blockIdx.x;
+__device__ __forceinline__ void first_patch_load(const float* const (&planes)[4], int tile, int tiles_w, int tiles_h,
+                                                 int H, int W, float (&pv)[(CIN * FT_PH * FT_PW + 255) / 256]) {
+  constexpr int PE = CIN * FT_PH * FT_PW, NPE = (PE + 255) / 256;
+  int t = tile;
   const int tw = t % tiles_w; t /= tiles_w;
   const int th = t % tiles_h;
   const int n = t / tiles_h;
   const int h0 = th * FT_H, w0 = tw * FT_W;
-  const unsigned HW = (unsigned)a.H * (unsigned)a.W;
-  for (int e = tid; e < CIN * FT_PH * FT_PW; e += 256) {
+  const unsigned HW = (unsigned)H * (unsigned)W;
+#pragma unroll
+  for (int q = 0; q < NPE; ++q) {
+    const int e = threadIdx.x + 256 * q;
     const int ci = e / (FT_PH * FT_PW), r = e - ci * (FT_PH * FT_PW);
     const int ph = r / FT_PW, pw = r - ph * FT_PW;
     const int h = h0 - 1 + ph, w = w0 - 1 + pw;
     float v = 0.f;
-    if (h >= 0 && h < a.H && w >= 0 && w < a.W) v = a.planes[ci][(unsigned)n * HW + (unsigned)(h * a.W + w)];
-    patch[e] = v;
+    if (e < PE && h >= 0 && h < H && w >= 0 && w < W) v = planes[ci][(unsigned)n * HW + (unsigned)(h * W + w)];
+    pv[q] = v;
   }
+}
+
+template <int CIN>
+__global__ __launch_bounds__(256, 3) void conv_first_fwd_tile_kernel(FirstArgs a, int tiles_w, int tiles_h, int ntiles) {
+  constexpr int PE = CIN * FT_PH * FT_PW, NPE = (PE + 255) / 256;
+  __shared__ float patch[PE];
+  __shared__ float red[256 * 8];
+  const int tid = threadIdx.x;
+  const int CQ = a.Cout >> 2, npl = 256 / CQ;
+  const int cq = tid % CQ, pl = tid / CQ;
+  const unsigned HW = (unsigned)a.H * (unsigned)a.W;
   pmu_f2 wlo[CIN * 9], whi[CIN * 9];  // w[co = 4cq + {0,1}], w[4cq + {2,3}] per (ci, tap)
 #pragma unroll
   for (int k = 0; k < CIN * 9; ++k) {
@@ -60,43 +72,59 @@ __global__ __launch_bounds__(256) void conv_first_fwd_tile_kernel(FirstArgs a, i
     blo = pmu_f2{a.bias[4 * cq], a.bias[4 * cq + 1]};
     bhi = pmu_f2{a.bias[4 * cq + 2], a.bias[4 * cq + 3]};
   }
-  __syncthreads();
-  pmu_f2 s1lo = {0.f, 0.f}, s1hi = {0.f, 0.f}, s2lo = {0.f, 0.f}, s2hi = {0.f, 0.f};
-  for (int i = pl; i < FT_H * FT_W; i += npl) {
-    const int r = i / FT_W, c = i - r * FT_W;
-    const int h = h0 + r, w = w0 + c;
-    if (h >= a.H || w >= a.W) continue;
-    pmu_f2 olo = blo, ohi = bhi;
+  const int t_beg = blockIdx.x * FT_TPB, t_end = min(ntiles, t_beg + FT_TPB);
+  float pv[NPE];
+  first_patch_load<CIN>(a.planes, t_beg, tiles_w, tiles_h, a.H, a.W, pv);
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    __syncthreads();  // the previous tile's patch and partial-sum reads are done
 #pragma unroll
-    for (int ci = 0; ci < CIN; ++ci)
+    for (int q = 0; q < NPE; ++q)
+      if (tid + 256 * q < PE) patch[tid + 256 * q] = pv[q];
+    __syncthreads();
+    if (tile + 1 < t_end) first_patch_load<CIN>(a.planes, tile + 1, tiles_w, tiles_h, a.H, a.W, pv);
+    int t = tile;
+    const int tw = t % tiles_w; t /= tiles_w;
+    const int th = t % tiles_h;
+    const int n = t / tiles_h;
+    const int h0 = th * FT_H, w0 = tw * FT_W;
+    pmu_f2 s1lo = {0.f, 0.f}, s1hi = {0.f, 0.f}, s2lo = {0.f, 0.f}, s2hi = {0.f, 0.f};
+    for (int i = pl; i < FT_H * FT_W; i += npl) {
+      const int r = i / FT_W, c = i - r * FT_W;
+      const int h = h0 + r, w = w0 + c;
+      if (h >= a.H || w >= a.W) continue;
+      pmu_f2 olo = blo, ohi = bhi;
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const float x = patch[(ci * FT_PH + r + tap / 3) * FT_PW + c + tap % 3];
-        const pmu_f2 x2 = {x, x};
-        olo = __builtin_elementwise_fma(x2, wlo[ci * 9 + tap], olo);
-        ohi = __builtin_elementwise_fma(x2, whi[ci * 9 + tap], ohi);
-      }
-    const unsigned p = (unsigned)n * HW + (unsigned)(h * a.W + w);
-    *reinterpret_cast<float4*>(a.z + (size_t)p * a.Cout + 4 * cq) = make_float4(olo.x, olo.y, ohi.x, ohi.y);
-    s1lo += olo; s1hi += ohi;
-    s2lo = __builtin_elementwise_fma(olo, olo, s2lo);
-    s2hi = __builtin_elementwise_fma(ohi, ohi, s2hi);
-  }
-  if (!a.part) return;
-  red[tid * 8 + 0] = s1lo.x; red[tid * 8 + 1] = s1lo.y; red[tid * 8 + 2] = s1hi.x; red[tid * 8 + 3] = s1hi.y;
-  red[tid * 8 + 4] = s2lo.x; red[tid * 8 + 5] = s2lo.y; red[tid * 8 + 6] = s2hi.x; red[tid * 8 + 7] = s2hi.y;
-  __syncthreads();
-  if (tid < CQ) {
-    float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
-    for (int l = 0; l < npl; ++l) {
-      const int src = l * CQ + tid;
+      for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { t1[e] += red[src * 8 + e]; t2[e] += red[src * 8 + 4 + e]; }
+        for (int tap = 0; tap < 9; ++tap) {
+          const float x = patch[(ci * FT_PH + r + tap / 3) * FT_PW + c + tap % 3];
+          const pmu_f2 x2 = {x, x};
+          olo = __builtin_elementwise_fma(x2, wlo[ci * 9 + tap], olo);
+          ohi = __builtin_elementwise_fma(x2, whi[ci * 9 + tap], ohi);
+        }
+      const unsigned p = (unsigned)n * HW + (unsigned)(h * a.W + w);
+      *reinterpret_cast<float4*>(a.z + (size_t)p * a.Cout + 4 * cq) = make_float4(olo.x, olo.y, ohi.x, ohi.y);
+      s1lo += olo; s1hi += ohi;
+      s2lo = __builtin_elementwise_fma(olo, olo, s2lo);
+      s2hi = __builtin_elementwise_fma(ohi, ohi, s2hi);
     }
+    if (!a.part) continue;  // (block-uniform)
+    // BN partial sums of this tile: one row per tile, in the one-tile-per-block order
+    red[tid * 8 + 0] = s1lo.x; red[tid * 8 + 1] = s1lo.y; red[tid * 8 + 2] = s1hi.x; red[tid * 8 + 3] = s1hi.y;
+    red[tid * 8 + 4] = s2lo.x; red[tid * 8 + 5] = s2lo.y; red[tid * 8 + 6] = s2hi.x; red[tid * 8 + 7] = s2hi.y;
+    __syncthreads();
+    if (tid < CQ) {
+      float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
+      for (int l = 0; l < npl; ++l) {
+        const int src = l * CQ + tid;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      a.part[((long long)blockIdx.x * 2 + 0) * a.Cout + 4 * tid + e] = t1[e];
-      a.part[((long long)blockIdx.x * 2 + 1) * a.Cout + 4 * tid + e] = t2[e];
+        for (int e = 0; e < 4; ++e) { t1[e] += red[src * 8 + e]; t2[e] += red[src * 8 + 4 + e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a.part[((long long)tile * 2 + 0) * a.Cout + 4 * tid + e] = t1[e];
+        a.part[((long long)tile * 2 + 1) * a.Cout + 4 * tid + e] = t2[e];
+      }
     }
   }
 }
@@ -184,24 +212,54 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_tile_kernel(FirstWgArgs 
   for (int k = 0; k < K9; ++k) { acc[0][k] = pmu_f2{0.f, 0.f}; acc[1][k] = pmu_f2{0.f, 0.f}; }
   const int t_beg = blockIdx.x * FW_TPB, t_end = min(ntiles, t_beg + FW_TPB);
   float pv[NPE];
-  auto load_patch = [&](int tile) {
-    int t = tile;
+  auto load_patch = [&](int tile) { first_patch_load<CIN>(a.planes, tile, tiles_w, tiles_h, H, W, pv); };
+  // da / z of the thread's pixels two iterations ahead (flat (tile, pixel) order, crossing tile
+  // boundaries): a pixel's float4 loads were consumed right after issue, one global round trip per
+  // pixel with two waves per SIMD to cover it (0.61 ms at c5 for 2.1 GB)
+  const int per_tile = (FT_H * FT_W) / PG;  // PG divides 256
+  const int nj = (t_end - t_beg) * per_tile;
+  auto pixel_of = [&](int j, size_t& p, int& r, int& cc, bool& ok) {
+    const int jj = j < nj ? j : nj - 1;
+    int t = t_beg + jj / per_tile;
+    const int i = pg + (jj - (jj / per_tile) * per_tile) * PG;
+    r = i / FT_W;
+    cc = i - r * FT_W;
     const int tw = t % tiles_w; t /= tiles_w;
     const int th = t % tiles_h;
     const int n = t / tiles_h;
-    const int h0 = th * FT_H, w0 = tw * FT_W;
-#pragma unroll
-    for (int q = 0; q < NPE; ++q) {
-      const int e = tid + 256 * q;
-      const int ci = e / (FT_PH * FT_PW), r = e - ci * (FT_PH * FT_PW);
-      const int ph = r / FT_PW, pw = r - ph * FT_PW;
-      const int h = h0 - 1 + ph, w = w0 - 1 + pw;
-      float v = 0.f;
-      if (e < PE && h >= 0 && h < H && w >= 0 && w < W) v = a.planes[ci][(unsigned)n * HW + (unsigned)(h * W + w)];
-      pv[q] = v;
-    }
+    const int h = th * FT_H + r, w = tw * FT_W + cc;
+    ok = j < nj && h < H && w < W;
+    p = (size_t)((unsigned)n * HW + (unsigned)(min(h, H - 1) * W + min(w, W - 1)));
   };
-  if (t_beg < t_end) load_patch(t_beg);
+  float4 dq[2], zq[2];
+  auto issue = [&](int j, int slot) {
+    size_t p; int r, cc; bool ok;
+    pixel_of(j, p, r, cc, ok);
+    dq[slot] = *reinterpret_cast<const float4*>(s.x + p * Cout + c);
+    zq[slot] = *reinterpret_cast<const float4*>(s.z + p * Cout + c);
+  };
+  auto consume = [&](int j, int slot) {
+    size_t p; int r, cc; bool ok;
+    pixel_of(j, p, r, cc, ok);
+    const float4 d = dq[slot], z = zq[slot];
+    pmu_f2 glo = {pmu_bnbwd1(d.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x), pmu_bnbwd1(d.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y)};
+    pmu_f2 ghi = {pmu_bnbwd1(d.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z), pmu_bnbwd1(d.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w)};
+    if (!ok) { glo = pmu_f2{0.f, 0.f}; ghi = pmu_f2{0.f, 0.f}; }
+#pragma unroll
+    for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const float x = patch[(ci * FT_PH + r + tap / 3) * FT_PW + cc + tap % 3];
+        const pmu_f2 x2 = {x, x};
+        acc[0][ci * 9 + tap] = __builtin_elementwise_fma(glo, x2, acc[0][ci * 9 + tap]);
+        acc[1][ci * 9 + tap] = __builtin_elementwise_fma(ghi, x2, acc[1][ci * 9 + tap]);
+      }
+  };
+  if (t_beg < t_end) {
+    load_patch(t_beg);
+    issue(0, 0);
+    issue(1, 1);
+  }
   for (int tile = t_beg; tile < t_end; ++tile) {
     __syncthreads();  // the previous tile's patch reads are done
 #pragma unroll
@@ -209,29 +267,13 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_tile_kernel(FirstWgArgs 
       if (tid + 256 * q < PE) patch[tid + 256 * q] = pv[q];
     __syncthreads();
     if (tile + 1 < t_end) load_patch(tile + 1);  // in flight under this tile's FMAs
-    int t = tile;
-    const int tw = t % tiles_w; t /= tiles_w;
-    const int th = t % tiles_h;
-    const int n = t / tiles_h;
-    const int h0 = th * FT_H, w0 = tw * FT_W;
-    for (int i = pg; i < FT_H * FT_W; i += PG) {
-      const int r = i / FT_W, cc = i - r * FT_W;
-      const int h = h0 + r, w = w0 + cc;
-      if (h >= H || w >= W) continue;
-      const size_t p = (size_t)((unsigned)n * HW + (unsigned)(h * W + w));
-      const float4 d = *reinterpret_cast<const float4*>(s.x + p * Cout + c);
-      const float4 z = *reinterpret_cast<const float4*>(s.z + p * Cout + c);
-      const pmu_f2 glo = {pmu_bnbwd1(d.x, z.x, sc.x, sh.x, mu.x, kx.x, kc.x), pmu_bnbwd1(d.y, z.y, sc.y, sh.y, mu.y, kx.y, kc.y)};
-      const pmu_f2 ghi = {pmu_bnbwd1(d.z, z.z, sc.z, sh.z, mu.z, kx.z, kc.z), pmu_bnbwd1(d.w, z.w, sc.w, sh.w, mu.w, kx.w, kc.w)};
-#pragma unroll
-      for (int ci = 0; ci < CIN; ++ci)
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const float x = patch[(ci * FT_PH + r + tap / 3) * FT_PW + cc + tap % 3];
-          const pmu_f2 x2 = {x, x};
-          acc[0][ci * 9 + tap] = __builtin_elementwise_fma(glo, x2, acc[0][ci * 9 + tap]);
-          acc[1][ci * 9 + tap] = __builtin_elementwise_fma(ghi, x2, acc[1][ci * 9 + tap]);
-        }
+    const int j0 = (tile - t_beg) * per_tile;
+    for (int ii = 0; ii < per_tile; ii += 2) {  // per_tile = Cout / 4 is even (first_wgrad_fast)
+      const int j = j0 + ii;
+      consume(j, 0);
+      issue(j + 2, 0);
+      consume(j + 1, 1);
+      issue(j + 3, 1);
     }
   }
   // reduce over the pixel groups inside the wave (lanes with equal cq are CQ apart), then waves
@@ -292,6 +334,7 @@ __global__ void rows_sum_kernel(const float* __restrict__ ws, int R, int Wd, flo
 
 }  // namespace
 
+// rows of the forward's BN partial sums: one per 8 x 32 tile
 extern "C" int pmu_conv_first_tiles(int N, int H, int W) {
   return N * pmu_cdiv(H, FT_H) * pmu_cdiv(W, FT_W);
 }
@@ -306,14 +349,14 @@ extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, in
   for (int i = 0; i < 4; ++i) a.planes[i] = i < Cin ? planes[i] : nullptr;
   for (int i = 0; i < Cin; ++i) PMU_REQUIRE(planes[i]);
   a.Cin = Cin; a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.w = w; a.bias = bias; a.z = z; a.part = part;
-  const int tw = pmu_cdiv(W, FT_W), th = pmu_cdiv(H, FT_H);
-  const dim3 grid((unsigned)pmu_conv_first_tiles(N, H, W));
+  const int tw = pmu_cdiv(W, FT_W), th = pmu_cdiv(H, FT_H), nt = N * tw * th;
+  const dim3 grid((unsigned)pmu_cdiv(nt, FT_TPB));
   hipStream_t st = (hipStream_t)stream;
   switch (Cin) {
-    case 1: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<1>, grid, dim3(256), 0, st, a, tw, th); break;
-    case 2: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<2>, grid, dim3(256), 0, st, a, tw, th); break;
-    case 3: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<3>, grid, dim3(256), 0, st, a, tw, th); break;
-    default: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<4>, grid, dim3(256), 0, st, a, tw, th); break;
+    case 1: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<1>, grid, dim3(256), 0, st, a, tw, th, nt); break;
+    case 2: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<2>, grid, dim3(256), 0, st, a, tw, th, nt); break;
+    case 3: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<3>, grid, dim3(256), 0, st, a, tw, th, nt); break;
+    default: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<4>, grid, dim3(256), 0, st, a, tw, th, nt); break;
   }
   PMU_CHECK_LAUNCH();
   return PMU_OK;
@@ -322,7 +365,8 @@ extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, in
 static bool first_wgrad_fast(const pmu_frame* dz, int Cout) {
   const pmu_src& s = dz->src[0];
   return s.mode == PMU_SRC_BNBWD && s.pool == PMU_POOL_NONE && s.off_h == 0 && s.off_w == 0 && s.H == dz->H &&
-         s.W == dz->W && Cout % 4 == 0 && Cout <= 256 && 256 % (Cout / 4) == 0;
+         s.W == dz->W && Cout % 8 == 0 && Cout <= 256 && 256 % (Cout / 4) == 0;  // (Cout / 4 pixels per tile
+                                                                                  // and thread: paired)
 }
 
 extern "C" size_t pmu_conv_first_wgrad_ws(int N, int H, int W, int Cin, int Cout) {

@@ -17,6 +17,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
   } while (0)
 
 static inline int pmu_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+// compute units of the current device (cached per process: one device per process)
+static inline int pmu_num_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n;
+  }();
+  return cus;
+}
 
 // Kernel-variant A/B switches (variants that compute the same result but measured slower, kept for
 // re-measurement): read only by `make EXPERIMENTS=1` builds; the shipped library ignores them and

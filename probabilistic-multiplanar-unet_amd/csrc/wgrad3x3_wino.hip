@@ -65,7 +65,7 @@ __device__ __forceinline__ void wgw_origin(const WgwArgs& a, int tile, int& n, i
 constexpr int D_UPX = DLS / 4, X_UPX = XLS / 4;
 constexpr int D_UNITS = TH * TW * D_UPX;
 constexpr int W_UNITS = D_UNITS + HH * HWD * X_UPX;
-constexpr int W_NGL = (W_UNITS + NT - 1) / NT;
+[[maybe_unused]] constexpr int W_NGL = (W_UNITS + NT - 1) / NT;
 static_assert(D_UNITS * 4 == D_FLOATS && W_UNITS * 4 == SLOT, "slot = dz image + x image");
 
 // block geometry by output-channel width: 32 (512 threads) or 64 (1024 threads: 4 waves per SIMD,

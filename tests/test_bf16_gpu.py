@@ -580,11 +580,14 @@ def _pack_dma(w, dgrad):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 40, 40, 64, 96), (1, 33, 64, 32, 64), (2, 32, 32, 128, 128),
-                                            (1, 17, 45, 48, 200), (4, 64, 96, 64, 64), (2, 16, 33, 16, 256)])
+                                            (1, 17, 45, 48, 200), (4, 64, 96, 64, 64), (2, 16, 33, 16, 256),
+                                            (32, 90, 70, 32, 64), (16, 40, 70, 160, 256)])
 def test_conv3x3_fwd_dma(dev, N, H, W, Cin, Cout):
     """The LDS-DMA bf16 conv (both operands by global_load_lds, swizzled units) == conv of the rounded
     operand: partial tiles in both directions, ragged channel blocks, both block shapes (64 / 128
-    output channels), BN partial sums."""
+    output channels), BN partial sums.  The last two have more tiles than resident workgroups, so
+    the persistent workgroups walk several tiles each (border tiles among them: their zero units
+    are rewritten per tile)."""
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src
     g = torch.Generator().manual_seed(71 + H + Cout)
@@ -607,7 +610,8 @@ def test_conv3x3_fwd_dma(dev, N, H, W, Cin, Cout):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 36, 40, 128, 64, 64), (1, 32, 48, 96, 128, 32),
-                                                  (2, 20, 64, 64, 32, 64), (3, 40, 32, 256, 128, 128)])
+                                                  (2, 20, 64, 64, 32, 64), (3, 40, 32, 256, 128, 128),
+                                                  (32, 90, 70, 96, 64, 64)])   # last: tiles > workgroups
 def test_conv3x3_dgrad_dma(dev, N, H, W, Cin, Cout, split):
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src

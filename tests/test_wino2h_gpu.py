@@ -24,7 +24,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 32, 32, 64, 64), (1, 37, 45, 16, 40), (1, 70, 33, 48, 32),
-                                            (2, 64, 64, 128, 96), (1, 33, 40, 8, 24), (1, 256, 64, 64, 64)])
+                                            (2, 64, 64, 128, 96), (1, 33, 40, 8, 24), (1, 256, 64, 64, 64),
+                                            (4, 100, 90, 64, 96)])  # last: more work items than workgroups
 def test_conv3x3_fwd_wino2h(dev, N, H, W, Cin, Cout):
     from pmu_hip import _lib as L
     from pmu_hip.engine import pack_weights_wino2h
@@ -48,7 +49,8 @@ def test_conv3x3_fwd_wino2h(dev, N, H, W, Cin, Cout):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 40, 36, 64, 64, 64), (2, 33, 64, 128, 64, 64),
-                                                  (1, 32, 48, 96, 128, 32), (1, 45, 37, 24, 16, 8)])
+                                                  (1, 32, 48, 96, 128, 32), (1, 45, 37, 24, 16, 8),
+                                                  (4, 100, 90, 96, 64, 64)])  # last: items > workgroups
 def test_conv3x3_dgrad_wino2h(dev, N, H, W, Cin, Cout, split):
     from pmu_hip import _lib as L
     from pmu_hip.engine import pack_weights_wino2h

@@ -52,7 +52,8 @@ def test_conv3x3_fwd_wino4(dev, exp_lib, N, H, W, Cin, Cout):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,split", [(2, 40, 36, 64, 64, 64), (2, 33, 64, 128, 64, 64),
                                                   (1, 32, 48, 96, 128, 32), (1, 45, 37, 24, 16, 8),
-                                                  (4, 64, 64, 256, 64, 128)])  # last: 2-D grouped grid
+                                                  (4, 64, 64, 256, 64, 128),   # 2-D grouped grid
+                                                  (24, 100, 90, 64, 64, 64)])  # more work items than workgroups
 def test_conv3x3_dgrad_wino4(dev, N, H, W, Cin, Cout, split):
     from pmu_hip import _lib as L
     from pmu_hip.engine import pack_weights_wino4
@@ -90,6 +91,8 @@ sys.path.insert(0, sys.argv[1])
 from pmu_hip import _lib as L
 from pmu_hip.engine import pack_weights_wino4
 N, H, W, Cin, Cout, split = 2, 40, 36, 160, 64, 96
+if len(sys.argv) > 2:  # several work items per persistent workgroup, each with several passes
+    N, H, W = 20, 100, 90
 g = torch.Generator().manual_seed(19)
 dz = torch.randn(N, H, W, Cout, generator=g).cuda()
 w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.1).cuda()
@@ -122,18 +125,20 @@ print(err)
 """
 
 
-@pytest.mark.parametrize("cpb", [2, 3, 5])
-def test_wino4_multipass(cpb):
+@pytest.mark.parametrize("cpb,big", [(2, False), (3, False), (5, False), (2, True)])
+def test_wino4_multipass(cpb, big):
     """Output-channel passes of the F(4x4) kernels (a workgroup walking cpb co-blocks of one spatial
     block, the next pass's first chunk fetched under this pass's MFMAs), forced through PMU_WINO4_CPB:
     input gradient with Cin = 160 (5 co-blocks, concat split inside a pass) and forward with
-    Cout = 160 (bias and BN partial sums per pass)."""
+    Cout = 160 (bias and BN partial sums per pass).  big: 720 work items for 256 persistent
+    workgroups, so a workgroup's flat pipeline crosses from a pass to the next pass and to the next
+    work item (new operand units, border blocks)."""
     pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "probabilistic-multiplanar-unet_amd")
     from pmu_hip import _lib as L
     if not os.path.exists(L.EXP_LIB_PATH):
         pytest.skip("experiments library not built (make -C csrc EXPERIMENTS=1)")
     env = dict(os.environ, PMU_WINO4_CPB=str(cpb), PMU_LIB="exp")   # the forward half: experiments build
-    out = subprocess.run([sys.executable, "-c", _MULTIPASS4, pkg], env=env, capture_output=True, text=True,
-                         timeout=240)
+    out = subprocess.run([sys.executable, "-c", _MULTIPASS4, pkg] + (["big"] if big else []), env=env,
+                         capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     assert float(out.stdout.strip().splitlines()[-1]) <= TOL4
