@@ -711,8 +711,12 @@ constexpr int HPPB = 2048;  // pixels per block in the fast head kernels
 // loads of a pixel's quads coalesce into its whole C-channel row; per class the quad dot products
 // are summed over the pixel's CQ lanes by xor shuffles and lane cq == 0 writes y[n][k][pix].
 // (One thread per pixel read a 16-B piece of 64 different rows per load instruction.)
-template <bool XBF>  // the source's x in bf16 (a compile-time choice: a load under the storage-type branch
-                    // would be waited for on its own)
+// XBF: the source's x in bf16 (a compile-time choice: a load under the storage-type branch would be
+// waited for on its own).  HU pixels per thread per round, their loads issued together (address
+// clamped to the block's last pixel, only the stores predicated): one pixel per round left a global
+// round trip exposed per pixel for one class (c2: 0.19 -> 0.14 ms); with three classes the batch of
+// four measured slower (c5: 0.31 -> 0.37 ms), so HU = 1 there
+template <bool XBF, int HU>
 __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const float* __restrict__ w,
                                                             const float* __restrict__ b, int K, int do_sigmoid,
                                                             float* __restrict__ y) {
@@ -730,10 +734,6 @@ __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const fl
     wq[k] = k < K ? *reinterpret_cast<const float4*>(w + k * C + 4 * cq) : make_float4(0.f, 0.f, 0.f, 0.f);
     bk[k] = (k < K && b) ? b[k] : 0.f;
   }
-  // HU pixels per thread per round, their loads issued together (address clamped to the block's last
-  // pixel, only the stores predicated): one pixel per round left a global round trip exposed per
-  // pixel (c5 512^2: 0.30 ms for 1.07 GB)
-  constexpr int HU = 4;
   const unsigned pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
   for (unsigned p0 = blockIdx.x * HPPB + pg; p0 < pend; p0 += HU * PG) {  // 32-bit decode (P < 2^31)
     float4 zx[HU];
@@ -1478,7 +1478,8 @@ extern "C" int pmu_head1x1_fwd(const pmu_frame* in, const float* w, const float*
   const DevFrame f = make_dev_frame(in);
   const long long P = (long long)in->N * in->H * in->W;
   if (host_head_fast(in) && P < (1LL << 31)) {
-    hipLaunchKernelGGL(f.s0.xbf ? head_fwd_fast_kernel<true> : head_fwd_fast_kernel<false>,
+    hipLaunchKernelGGL(f.s0.xbf ? (K == 1 ? head_fwd_fast_kernel<true, 4> : head_fwd_fast_kernel<true, 1>)
+                                : (K == 1 ? head_fwd_fast_kernel<false, 4> : head_fwd_fast_kernel<false, 1>),
                        dim3((unsigned)pmu_cdiv(P, HPPB)), dim3(256), 0, (hipStream_t)stream,
                        f, w, b, K, do_sigmoid, y);
     PMU_CHECK_LAUNCH();

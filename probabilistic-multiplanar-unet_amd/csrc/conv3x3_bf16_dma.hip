@@ -122,89 +122,59 @@ __global__ __launch_bounds__(256) void pack_dma_multi_kernel(const pmu_pack_job*
 // CS (input gradient): per-tile column sums of dx into a.part instead of the BN-backward partials
 // (pmu_conv3x3_dgrad_dma_x1b_sum; a compile-time variant: as a runtime branch beside the a.bz one it
 // spilled 89 VGPRs)
-// One (spatial tile, channel block) of the persistent kernel below: decoded from its flat index
-// (channel blocks fastest: the channel blocks of one tile share its halo image through one XCD's L2)
-struct DmaTile {
-  int n, h0, w0, j0, tsp;
-};
-
 template <bool DGRAD, bool ZB, int WN, int NWV, int EXP = 0, bool CS = false>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs a) {
   using G = DG<WN, NWV>;
   constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH, NT = G::NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
-  __shared__ float red[NWV * 64 * 2];  // epilogue partial sums [wave][64][2] (its own: the stages stay live)
   // the wave index as a uniform (SGPR) value: the epilogue's row pointers derive from it
   const int tid = threadIdx.x, lane = tid & 63, wave = DGRAD ? tid >> 6 : __builtin_amdgcn_readfirstlane(tid >> 6);
-  // Persistent: workgroup lb (XCD order) takes tiles lb, lb + G, lb + 2G, ... as one flat chunk
-  // pipeline, so the next tile's first chunk is fetched under this tile's last MFMAs and lands during
-  // its epilogue, whose stores drain under the next tile's first chunk.  (One tile per workgroup paid
-  // the operand latency before its first MFMA and left the MFMAs idle during its stores: at 512^2,
-  // 64 -> 64 the loads, the stores and the MFMAs added up.)
-  const int ntot = a.ncb * a.tiles_w * a.tiles_h * a.N;
-  const int gsz = gridDim.x;
-  const int lb = pmu_xcd_block(blockIdx.x, gsz);
-  const int nmine = (ntot - lb + gsz - 1) / gsz;
-  auto decode = [&](int L) __attribute__((always_inline)) {
-    DmaTile T;
-    const int cb = L % a.ncb;
-    int t = L / a.ncb;
-    T.tsp = t;
-    const int tw = t % a.tiles_w;
-    t /= a.tiles_w;
-    const int th = t % a.tiles_h;
-    T.n = t / a.tiles_h;
-    T.h0 = th * TH;
-    T.w0 = tw * TW;
-    T.j0 = cb * BN;
-    PMU_DCHECK(T.n < a.N && T.j0 < a.NOUT, PMU_DBG_GRID);
-    return T;
-  };
+  // (spatial tile, channel block), channel blocks fastest in XCD order: the channel blocks of one
+  // tile share its halo image through their XCD's L2
+  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+  const int cb = lb % a.ncb;
+  int t = lb / a.ncb;
+  const int tsp = t;
+  const int tw = t % a.tiles_w;
+  t /= a.tiles_w;
+  const int th = t % a.tiles_h;
+  const int n = t / a.tiles_h;
+  const int h0 = th * TH, w0 = tw * TW, j0 = cb * BN;
+  PMU_DCHECK(n < a.N && j0 < a.NOUT, PMU_DBG_GRID);
 
-  // operand units of this thread (DMA round r: unit (r * NWV + wave) * 64 + lane): 32-bit byte offset
-  // of chunk 0, whether the unit is inside the image (DMA'd) or an image unit outside it (zero)
+  // operand units of this thread (DMA round r: unit (r * 8 + wave) * 64 + lane): 32-bit byte offset
+  // of chunk 0 and whether the unit is inside the image; units outside it are zero in both stages
   unsigned goff[G::NGA];
-  unsigned gin = 0u, gzero = 0u;
-  auto setup = [&](const DmaTile& T) __attribute__((always_inline)) {
-    gin = 0u;
-    gzero = 0u;
-    // per-unit positions re-derived from a laundered thread id (hoisted out of the tile loop they were
-    // held, and spilled, across it)
-    int tid_s = threadIdx.x;
-    asm volatile("" : "+v"(tid_s));
-    const int lane_s = tid_s & 63, wave_s = tid_s >> 6;
+  unsigned gin = 0u;
 #pragma unroll
-    for (int r = 0; r < G::NGA; ++r) {
-      const int u = (r * NWV + wave_s) * 64 + lane_s;
-      const bool data = u < G::A_UNITS;
-      const int hp = u >> 1, q = (u & 1) ^ ((hp >> 3) & 1);
-      const int hr = hp / HW2, hc = hp - hr * HW2;
-      const int h = T.h0 - 1 + hr, w = T.w0 - 1 + hc;
-      const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
-      goff[r] = in ? (unsigned)(((((long long)T.n * a.H + h) * a.W + w) * a.Cp + 8 * q) * 2) : 0u;
-      PMU_DCHECK(!in || (((long long)T.n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
-      gin |= in ? (1u << r) : 0u;
-      gzero |= (data && !in) ? (1u << r) : 0u;
+  for (int r = 0; r < G::NGA; ++r) {
+    const int u = (r * NWV + wave) * 64 + lane;
+    const bool data = u < G::A_UNITS;
+    const int hp = u >> 1, q = (u & 1) ^ ((hp >> 3) & 1);
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    const int h = h0 - 1 + hr, w = w0 - 1 + hc;
+    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    goff[r] = in ? (unsigned)(((((long long)n * a.H + h) * a.W + w) * a.Cp + 8 * q) * 2) : 0u;
+    PMU_DCHECK(!in || (((long long)n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
+    gin |= in ? (1u << r) : 0u;
+    if (data && !in) {
+      *reinterpret_cast<uint4*>(smem + 16 * u) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(smem + G::STAGE + 16 * u) = make_uint4(0u, 0u, 0u, 0u);
     }
-  };
-  const char* wbase = reinterpret_cast<const char*>(a.wp) + 16 * lane;
+  }
+  const char* wsrc = reinterpret_cast<const char*>(a.wp) + (long long)cb * a.nch * G::B_UNITS * 16 + 16 * lane;
 
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
                                    (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
-  // chunk CH of tile T into stage STG; the image units outside the map are written as zeros (they
-  // may hold another tile's data: the write is ordered before the stage's readers by the chunk barrier)
-#define PMU_FETCH(T, CH, STG)                                                                               \
+#define PMU_FETCH(CH, STG)                                                                                  \
   {                                                                                                        \
     PMU_DCHECK((CH) * BK + BK <= a.Cp, PMU_DBG_OPERAND);                                                   \
     const char* xa_ = reinterpret_cast<const char*>(a.x) + (CH) * BK * 2;                                  \
     unsigned char* st_ = (STG);                                                                            \
-    _Pragma("unroll") for (int r = 0; r < G::NGA; ++r) {                                                   \
+    _Pragma("unroll") for (int r = 0; r < G::NGA; ++r)                                                     \
       if ((gin >> r) & 1u) PMU_GLDS(xa_ + goff[r], st_ + (r * NWV + wave) * 1024)                         \
-      if ((gzero >> r) & 1u)                                                                               \
-        *reinterpret_cast<uint4*>(st_ + 16 * ((r * NWV + wave) * 64 + lane)) = make_uint4(0u, 0u, 0u, 0u); \
-    }                                                                                                      \
-    const char* wb_ = wbase + ((long long)((T).j0 / BN) * a.nch + (CH)) * G::B_UNITS * 16;                 \
+    const char* wb_ = wsrc + (long long)(CH) * G::B_UNITS * 16;                                            \
     _Pragma("unroll") for (int r = 0; r < G::NGB; ++r)                                                     \
       if ((r + 1) * NT <= G::B_UNITS || (r * NWV + wave) * 64 + lane < G::B_UNITS)                          \
         PMU_GLDS(wb_ + (r * NWV + wave) * 1024, st_ + G::A_BYTES + (r * NWV + wave) * 1024)               \
@@ -225,212 +195,31 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  DmaTile T = decode(lb);   // the tile being computed
-  DmaTile Tn = T;           // the tile whose chunks are being fetched
-  setup(T);
-  PMU_FETCH(T, 0, smem)
+  PMU_FETCH(0, smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // One operand set per tap in two register buffers; tap t+1's reads are issued during tap t's MFMAs,
   // and the next chunk's tap 0 during this chunk's tap 8: the chunk barrier (its DMA landed, every
   // wave done reading the stage the following fetch overwrites) sits between two taps' MFMA groups,
   // not between a barrier and the first LDS round trip of a chunk.  9 taps per chunk flip the buffer
-  // parity every chunk, so chunks run in compile-time-parity pairs (flat over the tiles).
+  // parity every chunk, so chunks run in compile-time-parity pairs.
   bf16x8 op[2][FM + FN];
-  auto load_tap = [&](const unsigned char* cur, int tap, bf16x8 (&o)[FM + FN]) __attribute__((always_inline)) {
+  auto load_tap = [&](const unsigned char* cur, int tap, bf16x8 (&o)[FM + FN]) {
     const int dy = tap / 3, dx = tap - 3 * (tap / 3);
-    // the swizzled addresses recomputed per read (a few VALU under the MFMAs): hoisted, the 36 per
-    // stage were held across the loop and the persistent loop's extra state spilled
-    int hb = hpb;
-    asm volatile("" : "+v"(hb));
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
-      const int hp = hb + (fm + dy) * HW2 + dx;
+      const int hp = hpb + (fm + dy) * HW2 + dx;
       o[fm] = *reinterpret_cast<const bf16x8*>(cur + 16 * swz(hp, q));
     }
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) o[FM + fn] = *reinterpret_cast<const bf16x8*>(cur + ub[fn] + tap * (32 * BN));
   };
-  auto epilogue = [&](const DmaTile& E) __attribute__((always_inline)) {
-    const int n = E.n, h0 = E.h0, w0 = E.w0, j0 = E.j0;
-    // lane-derived values re-derived from a laundered thread id: without it the compiler hoisted the
-    // epilogue's tile-invariant address terms out of the tile loop, live (and spilled) across the MFMAs
-    int tid_e = threadIdx.x;
-    asm volatile("" : "+v"(tid_e));
-    const int lane = tid_e & 63, li = lane & 31;
-    const int wave = DGRAD ? tid_e >> 6 : __builtin_amdgcn_readfirstlane(tid_e >> 6);
-    const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-    // accumulator (fm, fn, r) = output pixel (tile row 4 wm + fm, column acc_row(r, lane)), channel
-    // j0 + 64 wn + 32 fn + (lane & 31); a 32-channel destination is uniform (split % 32 == 0).
-    float s1[FN], s2[FN];
-    if constexpr (!DGRAD) {
-      // Forward: values and BN sums formed unconditionally (masked), only the stores predicated.  With
-      // the bias first consumed inside a per-output branch the compiler waited vmcnt(0) in every
-      // branch, i.e. for all earlier stores of the epilogue (one store in flight at a time: 112 waits
-      // for 128 stores).  Store addresses: a uniform row base per (fm, fn) + a 32-bit column offset.
-      bool jok[FN];
-      float bv[FN], zov[FN];
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        s1[fn] = 0.f;
-        s2[fn] = 0.f;
-        const int j = j0 + wn * 64 + fn * 32 + li;
-        jok[fn] = j < a.NOUT;
-        const int jc = jok[fn] ? j : a.NOUT - 1;
-        bv[fn] = a.bias ? a.bias[jc] : 0.f;
-        zov[fn] = (ZB && a.zoff) ? a.zoff[jc] : 0.f;
-      }
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm) {
-        const int h = h0 + 4 * wm + fm;
-        const long long rowpix = ((long long)n * a.H + (h < a.H ? h : a.H - 1)) * a.W;
-        float* drow = a.out0 + rowpix * a.NOUT;
-        unsigned short* drowb = reinterpret_cast<unsigned short*>(a.out0) + rowpix * a.NOUT;
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int j = j0 + wn * 64 + fn * 32 + li;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int w = w0 + acc_row(r, lane);
-            const bool ok = jok[fn] && h < a.H && w < a.W;
-            float v = acc[fm][fn][r] + bv[fn];
-            unsigned short vb = 0;
-            if (ZB) {
-              vb = bf16_bits(v - zov[fn]);
-              v = pmu_bf16_f32(vb) + zov[fn];
-            }
-            const float m = ok ? v : 0.f;
-            s1[fn] += m;
-            s2[fn] = fmaf(m, m, s2[fn]);
-            if (!ok || (EXP & 1)) continue;
-            PMU_DCHECK(((long long)n * a.H + h) * a.W + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-            const unsigned oo = (unsigned)(w * a.NOUT + j);
-            if (ZB) drowb[oo] = vb;
-            else drow[oo] = v;
-          }
-        }
-      }
-    } else {
-      // Input gradient: all stores first, then (a.bz) the producer's BN-backward sums from the still-live
-      // accumulators and the z under them, a row at a time.  z loads interleaved with the stores made
-      // every consumption of a z value wait for all earlier stores (vmcnt counts both, in order); the
-      // straight-line masked form of the forward above spilled 18-140 VGPRs here.
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        s1[fn] = 0.f;
-        s2[fn] = 0.f;
-        const int jb = j0 + wn * 64 + fn * 32;
-        const int j = jb + li;
-        const bool jok = j < a.NOUT;
-        float* dstp;
-        int ld;
-        unsigned short* dstb = nullptr;  // (uniform per fragment)
-        if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
-        else {  // (out1 null: only the bf16 copy, pmu_conv3x3_dgrad_dma_x1b_sum)
-          dstp = a.out1 ? a.out1 + (j - a.split) : nullptr;
-          ld = a.NOUT - a.split;
-          if (a.out1b) dstb = a.out1b + (j - a.split);
-        }
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm) {
-          const int h = h0 + 4 * wm + fm;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int w = w0 + acc_row(r, lane);
-            if (!jok || h >= a.H || w >= a.W) continue;
-            const long long pix = ((long long)n * a.H + h) * a.W + w;
-            PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-            if (!CS || dstp) dstp[pix * ld] = acc[fm][fn][r];  // (only the CS variant has a null out1)
-            if (dstb) dstb[pix * ld] = bf16_bits(acc[fm][fn][r]);
-          }
-        }
-      }
-      if (!CS && a.bz) {
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int j = j0 + wn * 64 + fn * 32 + li;
-          const bool jok = j < a.NOUT;
-          const int jc = jok ? j : a.NOUT - 1;
-          const float bsc = a.bcoef[jc], bsh = a.bcoef[a.NOUT + jc], bmu = a.bmean[jc], bis = a.binv[jc];
-#pragma unroll
-          for (int fm = 0; fm < FM; ++fm) {
-            const int h = h0 + 4 * wm + fm;
-            const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
-            float zt[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {  // clamped addresses: every lane loads, masked values ignored
-              const long long zi = (row + min(w0 + acc_row(r, lane), a.W - 1)) * a.NOUT + jc;
-              zt[r] = ZB ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int w = w0 + acc_row(r, lane);
-              const bool ok = jok && h < a.H && w < a.W;
-              const float gg = (ok && fmaf(zt[r], bsc, bsh) > 0.f) ? acc[fm][fn][r] : 0.f;
-              s1[fn] += gg;
-              s2[fn] = fmaf(gg, (zt[r] - bmu) * bis, s2[fn]);
-            }
-          }
-        }
-      } else if (CS) {  // per-tile column sums of dx (x1b_sum: the transposed conv's bias gradient)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const bool jok = j0 + wn * 64 + fn * 32 + li < a.NOUT;
-#pragma unroll
-          for (int fm = 0; fm < FM; ++fm) {
-            const int h = h0 + 4 * wm + fm;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const bool ok = jok && h < a.H && w0 + acc_row(r, lane) < a.W;
-              s1[fn] += ok ? acc[fm][fn][r] : 0.f;
-            }
-          }
-        }
-      }
-    }
-    if (a.part) {  // forward: BN partial sums of the output; input gradient: of the producer's BN backward
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        s1[fn] += __shfl_xor(s1[fn], 32, 64);
-        s2[fn] += __shfl_xor(s2[fn], 32, 64);
-        if (lane < 32) {
-          red[(wave * 64 + fn * 32 + lane) * 2 + 0] = s1[fn];
-          red[(wave * 64 + fn * 32 + lane) * 2 + 1] = s2[fn];
-        }
-      }
-      __syncthreads();
-      if (tid_e < BN) {  // channel tid = 64 wn + c: summed over the WM waves of column group wn, in order
-        const int j = j0 + tid_e, wnn = tid_e >> 6, c = tid_e & 63;
-        if (j < a.NOUT) {
-          float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-          for (int m = 0; m < WM; ++m) {
-            t1 += red[((m * WN + wnn) * 64 + c) * 2 + 0];
-            t2 += red[((m * WN + wnn) * 64 + c) * 2 + 1];
-          }
-          PMU_DCHECK(E.tsp < a.N * a.tiles_h * a.tiles_w, PMU_DBG_WORKSPACE);
-          a.part[((long long)E.tsp * 2 + 0) * a.NOUT + j] = t1;
-          a.part[((long long)E.tsp * 2 + 1) * a.NOUT + j] = t2;
-        }
-      }
-      // (red is rewritten only after the next tile's chunk barriers: every reader is past this point)
-    }
-  };
-  // chunk ch of the tile kt being computed (flat chunk g = kt * nch + ch, stage and register parity P =
-  // g & 1); the last chunk of a tile fetches the next tile's first chunk
-  auto run_chunk = [&](int kt, int ch, auto par) __attribute__((always_inline)) {
+  auto run_chunk = [&](int ch, auto par) {
     constexpr int P = decltype(par)::value;
-    const unsigned char* cur = smem + P * G::STAGE;
-    unsigned char* nxt = smem + (1 - P) * G::STAGE;
-    const bool last = ch + 1 == a.nch;
-    const bool more = !last || kt + 1 < nmine;
-    if (!last) {
-      PMU_FETCH(T, ch + 1, nxt)
-    } else if (more) {  // every fetch of this tile is issued: goff may change
-      Tn = decode(lb + (kt + 1) * gsz);
-      setup(Tn);
-      PMU_FETCH(Tn, 0, nxt)
-    }
+    const unsigned char* cur = smem + (ch & 1) * G::STAGE;
+    const unsigned char* nxt = smem + ((ch + 1) & 1) * G::STAGE;
+    const bool more = ch + 1 < a.nch;
+    if (more) PMU_FETCH(ch + 1, smem + ((ch + 1) & 1) * G::STAGE)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       // this tap's operands (read during the previous tap's MFMAs) have landed: wait for them BEFORE
@@ -441,10 +230,10 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       if (tap + 1 < 9) {
         load_tap(cur, tap + 1, op[(tap + 1 + P) & 1]);
       } else if (more) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's share of the next chunk landed
-        __builtin_amdgcn_s_barrier();                      // everyone's, and every read of the chunk before done
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's share of chunk ch + 1 landed
+        __builtin_amdgcn_s_barrier();                      // everyone's, and every read of chunk ch - 1 done
         __builtin_amdgcn_sched_barrier(0);
-        if (!last) load_tap(nxt, 0, op[(9 + P) & 1]);
+        load_tap(nxt, 0, op[(9 + P) & 1]);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -457,37 +246,172 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  // the chunks of tile kt, in compile-time-parity pairs from start parity P0
-  auto run_tile = [&](int kt, auto par0) __attribute__((always_inline)) {
-    constexpr int P0 = decltype(par0)::value;
-    int ch = 0;
-    for (; ch + 1 < a.nch; ch += 2) {
-      run_chunk(kt, ch, std::integral_constant<int, P0>{});
-      run_chunk(kt, ch + 1, std::integral_constant<int, 1 - P0>{});
-    }
-    if (ch < a.nch) run_chunk(kt, ch, std::integral_constant<int, P0>{});
-  };
-  // every tile starts at stage / register parity 0: the host makes a workgroup take more than one
-  // tile only when the chunk count is even (a parity branch per tile made the register allocator
-  // copy the accumulators between the two paths' assignments and spill)
-  PMU_DCHECK(nmine == 1 || (a.nch & 1) == 0, PMU_DBG_GRID);
   load_tap(smem, 0, op[0]);
-  for (int kt = 0; kt < nmine; ++kt) {
-    run_tile(kt, std::integral_constant<int, 0>{});
-    epilogue(T);
-    if (kt + 1 < nmine) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-      T = Tn;
-      load_tap(smem, 0, op[0]);  // the next tile's first operands (its chunk landed before the last barrier)
-    }
+  int ch = 0;
+  for (; ch + 1 < a.nch; ch += 2) {
+    run_chunk(ch, std::integral_constant<int, 0>{});
+    run_chunk(ch + 1, std::integral_constant<int, 1>{});
   }
+  if (ch < a.nch) run_chunk(ch, std::integral_constant<int, 0>{});
+  __syncthreads();  // every wave's last reads are done before the epilogue reuses the stages
 #undef PMU_FETCH
 #undef PMU_GLDS
+
+  // epilogue: accumulator (fm, fn, r) = output pixel (tile row 4 wm + fm, column acc_row(r, lane)),
+  // channel j0 + 64 wn + 32 fn + (lane & 31); a 32-channel destination is uniform (split % 32 == 0).
+  float* red = reinterpret_cast<float*>(smem);  // [NWV waves][64][2] (the stages are free now)
+  float s1[FN], s2[FN];
+  if constexpr (!DGRAD) {
+    // Forward: values and BN sums formed unconditionally (masked), only the stores predicated.  With the
+    // bias first consumed inside a per-output branch the compiler waited vmcnt(0) in every branch,
+    // i.e. for all earlier stores of the epilogue (one store in flight at a time: 112 waits for 128
+    // stores).  Store addresses: a uniform row base per (fm, fn) + a 32-bit column offset.
+    bool jok[FN];
+    float bv[FN], zov[FN];
+  #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] = 0.f;
+      s2[fn] = 0.f;
+      const int j = j0 + wn * 64 + fn * 32 + li;
+      jok[fn] = j < a.NOUT;
+      const int jc = jok[fn] ? j : a.NOUT - 1;
+      bv[fn] = a.bias ? a.bias[jc] : 0.f;
+      zov[fn] = (ZB && a.zoff) ? a.zoff[jc] : 0.f;
+    }
+  #pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int h = h0 + 4 * wm + fm;
+      const long long rowpix = ((long long)n * a.H + (h < a.H ? h : a.H - 1)) * a.W;
+      float* drow = a.out0 + rowpix * a.NOUT;
+      unsigned short* drowb = reinterpret_cast<unsigned short*>(a.out0) + rowpix * a.NOUT;
+  #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int j = j0 + wn * 64 + fn * 32 + li;
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int w = w0 + acc_row(r, lane);
+          const bool ok = jok[fn] && h < a.H && w < a.W;
+          float v = acc[fm][fn][r] + bv[fn];
+          unsigned short vb = 0;
+          if (ZB) {
+            vb = bf16_bits(v - zov[fn]);
+            v = pmu_bf16_f32(vb) + zov[fn];
+          }
+          const float m = ok ? v : 0.f;
+          s1[fn] += m;
+          s2[fn] = fmaf(m, m, s2[fn]);
+          if (!ok || (EXP & 1)) continue;
+          PMU_DCHECK(((long long)n * a.H + h) * a.W + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+          const unsigned oo = (unsigned)(w * a.NOUT + j);
+          if (ZB) drowb[oo] = vb;
+          else drow[oo] = v;
+        }
+      }
+    }
+  } else {
+    // Input gradient: all stores first, then (a.bz) the producer's BN-backward sums from the still-live
+    // accumulators and the z under them, a row at a time.  z loads interleaved with the stores made
+    // every consumption of a z value wait for all earlier stores (vmcnt counts both, in order); the
+    // straight-line masked form of the forward above spilled 18-140 VGPRs here.
+  #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] = 0.f;
+      s2[fn] = 0.f;
+      const int jb = j0 + wn * 64 + fn * 32;
+      const int j = jb + li;
+      const bool jok = j < a.NOUT;
+      float* dstp;
+      int ld;
+      unsigned short* dstb = nullptr;  // (uniform per fragment)
+      if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
+      else {  // (out1 null: only the bf16 copy, pmu_conv3x3_dgrad_dma_x1b_sum)
+        dstp = a.out1 ? a.out1 + (j - a.split) : nullptr;
+        ld = a.NOUT - a.split;
+        if (a.out1b) dstb = a.out1b + (j - a.split);
+      }
+  #pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int h = h0 + 4 * wm + fm;
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int w = w0 + acc_row(r, lane);
+          if (!jok || h >= a.H || w >= a.W) continue;
+          const long long pix = ((long long)n * a.H + h) * a.W + w;
+          PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+          if (!CS || dstp) dstp[pix * ld] = acc[fm][fn][r];  // (only the CS variant has a null out1)
+          if (dstb) dstb[pix * ld] = bf16_bits(acc[fm][fn][r]);
+        }
+      }
+    }
+    if (!CS && a.bz) {
+  #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int j = j0 + wn * 64 + fn * 32 + li;
+        const bool jok = j < a.NOUT;
+        const int jc = jok ? j : a.NOUT - 1;
+        const float bsc = a.bcoef[jc], bsh = a.bcoef[a.NOUT + jc], bmu = a.bmean[jc], bis = a.binv[jc];
+  #pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int h = h0 + 4 * wm + fm;
+          const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
+          float zt[16];
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {  // clamped addresses: every lane loads, masked values ignored
+            const long long zi = (row + min(w0 + acc_row(r, lane), a.W - 1)) * a.NOUT + jc;
+            zt[r] = ZB ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
+          }
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int w = w0 + acc_row(r, lane);
+            const bool ok = jok && h < a.H && w < a.W;
+            const float gg = (ok && fmaf(zt[r], bsc, bsh) > 0.f) ? acc[fm][fn][r] : 0.f;
+            s1[fn] += gg;
+            s2[fn] = fmaf(gg, (zt[r] - bmu) * bis, s2[fn]);
+          }
+        }
+      }
+    } else if (CS) {  // per-tile column sums of dx (x1b_sum: the transposed conv's bias gradient)
+  #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const bool jok = j0 + wn * 64 + fn * 32 + li < a.NOUT;
+  #pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const int h = h0 + 4 * wm + fm;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const bool ok = jok && h < a.H && w0 + acc_row(r, lane) < a.W;
+            s1[fn] += ok ? acc[fm][fn][r] : 0.f;
+          }
+        }
+      }
+    }
+  }
+  if (a.part) {  // forward: BN partial sums of the output; input gradient: of the producer's BN backward
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      s1[fn] += __shfl_xor(s1[fn], 32, 64);
+      s2[fn] += __shfl_xor(s2[fn], 32, 64);
+      if (lane < 32) {
+        red[(wave * 64 + fn * 32 + lane) * 2 + 0] = s1[fn];
+        red[(wave * 64 + fn * 32 + lane) * 2 + 1] = s2[fn];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {  // channel tid = 64 wn + c: summed over the WM waves of column group wn, in order
+      const int j = j0 + tid, wnn = tid >> 6, c = tid & 63;
+      if (j < a.NOUT) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int m = 0; m < WM; ++m) {
+          t1 += red[((m * WN + wnn) * 64 + c) * 2 + 0];
+          t2 += red[((m * WN + wnn) * 64 + c) * 2 + 1];
+        }
+        PMU_DCHECK(tsp < a.N * a.tiles_h * a.tiles_w, PMU_DBG_WORKSPACE);
+        a.part[((long long)tsp * 2 + 0) * a.NOUT + j] = t1;
+        a.part[((long long)tsp * 2 + 1) * a.NOUT + j] = t2;
+      }
+    }
+  }
 }
 
 // Workgroup shape: 64 output channels x 512 pixels in 4 waves (two workgroups per CU) for <= 64
@@ -536,12 +460,8 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   a.ncb = pmu_cdiv(NOUT, 64 * sh.wn);
   a.tiles_w = pmu_cdiv(W, TW);
   a.tiles_h = pmu_cdiv(H, sh.th);
-  const long long tiles = (long long)a.tiles_w * a.tiles_h * N * a.ncb;
-  PMU_REQUIRE(tiles < (1LL << 31));
-  // persistent workgroups: as many as are resident at once (two 4-wave or one 8-wave per CU); an odd
-  // chunk count keeps one tile per workgroup (the kernel runs every tile from stage parity 0)
-  const long long cap = (long long)pmu_num_cus() * (sh.nwv == 4 ? 2 : 1);
-  const long long blocks = (tiles < cap || (a.nch & 1)) ? tiles : cap;
+  const long long blocks = (long long)a.tiles_w * a.tiles_h * N * a.ncb;
+  PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks), blk(64 * sh.nwv);
   const bool zb = zbf == 1;

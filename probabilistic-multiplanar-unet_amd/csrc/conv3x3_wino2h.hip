@@ -395,89 +395,35 @@ struct W2Block {
   unsigned gin, gzero;
 };
 
-// work item L (spatial block, co-block group) of the persistent kernel: co groups fastest
-template <int CO_>
-__device__ __forceinline__ W2Block w2_decode(const W2Args& a, int L) {
-  W2Block B;
-  const int ncog = (a.nco + a.cpb - 1) / a.cpb;
-  B.cob0 = (L % ncog) * a.cpb;
-  int sp = L / ncog;
-  B.spatial = sp;
-  const int bx = sp % a.bw; sp /= a.bw;
-  const int by = sp % a.bh;
-  B.n = sp / a.bh;
-  B.h0 = by * OH;
-  B.w0 = bx * OW;
-  B.nchunks = a.KC / BK;
-  B.npass = a.cpb < a.nco - B.cob0 ? a.cpb : a.nco - B.cob0;
-  PMU_DCHECK(B.n < a.N && B.cob0 < a.nco, PMU_DBG_GRID);
-  return B;
-}
-
-// this thread's operand units of block B: byte offset of chunk 0 (< 2^32, host-checked), inside the
-// input (DMA'd) or an image unit outside it (zero).  Positions from a laundered thread id, so they are
-// recomputed per work item instead of held across the loop.
-template <int CO_>
-__device__ __forceinline__ void w2_setup(const W2Args& a, W2Block& B, unsigned (&goff)[W2Cfg<CO_>::NGL]) {
-  using C = W2Cfg<CO_>;
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  unsigned gin = 0u, gzero = 0u;
-#pragma unroll
-  for (int r = 0; r < C::NGL; ++r) {
-    const int u = r * C::NT + tid;
-    const int hr = u / ROWU, wu = u - hr * ROWU;
-    const int g = wu / 5, w5 = wu - 5 * g;
-    const int px = 2 * g + (w5 >> 1);
-    const bool data = u < A_UNITS && w5 < 4 && px < HW;
-    const int h = B.h0 - 1 + hr, w = B.w0 - 1 + px;
-    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
-    goff[r] = in ? (unsigned)(((((long long)B.n * a.H + h) * a.W + w) * a.KC + 4 * (w5 & 1)) * 4) : 0u;
-    PMU_DCHECK(!in || (((long long)B.n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
-    gin |= in ? (1u << r) : 0u;
-    gzero |= (data && !in) ? (1u << r) : 0u;
-  }
-  B.gin = gin;
-  B.gzero = gzero;
-}
-
-// The persistent pipeline of a wave of component half CH: the workgroup walks work items lb, lb + G,
-// ... (G = the grid), each its co-block passes, each the chunks — one flat DMA sequence, so the next
-// pass's (or the next work item's) first chunk lands under this pass's last MFMAs and epilogue.
-// (One work item per workgroup left each workgroup's first DMA latency and its epilogue stores
-// without MFMAs beside them: one workgroup per CU, nothing else to overlap.)
 template <bool DGRAD, bool BNR, int CH, int CO_>
-__device__ __forceinline__ void wino2h_main(const W2Args& a, int lb, int gsz, int nitems, float* smem) {
+__device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, const unsigned (&goff)[W2Cfg<CO_>::NGL],
+                                            float* smem) {
   using C = W2Cfg<CO_>;
   constexpr int CO = C::CO, NT = C::NT, NGL = C::NGL, UGL = C::UGL, U_FLOATS = C::U_FLOATS, STAGE = C::STAGE;
   float* red = smem + 2 * STAGE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nchunks = a.KC / BK;
+  const int nchunks = B.nchunks, total = B.npass * nchunks;
+  const float* wsrc = a.wp + (long long)B.cob0 * nchunks * U_FLOATS;
   const unsigned uoff = 16u * tid;
   const int wave_off = wave * 256;
-  unsigned goff[NGL];
-  W2Block B = w2_decode<CO_>(a, lb);
-  w2_setup<CO_>(a, B, goff);
-  W2Block Bn = B;
+  const unsigned gin = B.gin;
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
                                    (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
-  // chunk C of pass P of block FB into BUF.  Serpentine chunk order over the passes (as
-  // conv3x3_wino4.hip): a pass begins on the chunks the previous one fetched last, still in L2;
-  // direction by co-block parity (independent of cpb).  Image units outside the map are written as
-  // zeros (the stage may hold another block's data; ordered before its readers by the chunk barrier).
-#define PMU_FETCH2(FB, GOFF, P, C, BUF)                                                                     \
+  // serpentine chunk order over the passes (as conv3x3_wino4.hip): a pass begins on the chunks the
+  // previous one fetched last, still in L2; direction by co-block parity (independent of cpb)
+#define PMU_FETCH2(GI, BUF)                                                                                 \
   {                                                                                                        \
-    const int cs_ = (((FB).cob0 + (P)) & 1) ? nchunks - 1 - (C) : (C);                                     \
+    const int p_ = (GI) / nchunks;                                                                         \
+    const int c_ = (GI) - p_ * nchunks;                                                                    \
+    const int cs_ = ((B.cob0 + p_) & 1) ? nchunks - 1 - c_ : c_;                                           \
     const int k0_ = cs_ * BK;                                                                              \
     PMU_DCHECK(k0_ + BK <= a.KC, PMU_DBG_OPERAND);                                                         \
     float* b_ = (BUF);                                                                                     \
     const char* xb_ = reinterpret_cast<const char*>(a.x + k0_);                                            \
-    _Pragma("unroll") for (int r = 0; r < NGL; ++r) {                                                      \
-      if (((FB).gin >> r) & 1u) PMU_GLDS(xb_ + (GOFF)[r], b_ + 4 * (r * NT) + wave_off)                   \
-      if (((FB).gzero >> r) & 1u) *reinterpret_cast<float4*>(b_ + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f); \
-    }                                                                                                      \
-    const char* s_ = reinterpret_cast<const char*>(a.wp + ((long long)((FB).cob0 + (P)) * nchunks + cs_) * U_FLOATS) + uoff; \
+    _Pragma("unroll") for (int r = 0; r < NGL; ++r)                                                        \
+      if ((gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                           \
+    const char* s_ = reinterpret_cast<const char*>(wsrc + ((long long)p_ * nchunks + cs_) * U_FLOATS) + uoff; \
     float* d_ = b_ + A_FLOATS + wave_off;                                                                  \
     _Pragma("unroll") for (int r = 0; r < UGL; ++r)                                                        \
       if (r * NT * 4 + (wave + 1) * 256 <= U_FLOATS) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)          \
@@ -491,55 +437,37 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, int lb, int gsz, in
 #pragma unroll
     for (int c = 0; c < 8; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  PMU_FETCH2(B, goff, 0, 0, smem)
-  PMU_FETCH2(B, goff, 0, 0, smem + STAGE)  // (zero units of the other stage; its data is overwritten before use)
+  PMU_FETCH2(0, smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int gi = 0;  // flat chunk index: stage parity
-  for (int k = 0; k < nitems; ++k) {
-    for (int p = 0; p < B.npass; ++p) {
-      const int j0 = (B.cob0 + p) * CO;
-      const int jb = j0 + 32 * cg + 16 * CH + t;
-      const float bias = (!DGRAD && a.bias && jb < a.NOUT) ? a.bias[jb] : 0.f;
-      for (int ch = 0; ch < nchunks; ++ch, ++gi) {
-        float* cur = smem + (gi & 1) * STAGE;
-        float* nxt = smem + ((gi + 1) & 1) * STAGE;
-        if (ch + 1 < nchunks) PMU_FETCH2(B, goff, p, ch + 1, nxt)
-        else if (p + 1 < B.npass) PMU_FETCH2(B, goff, p + 1, 0, nxt)
-        else if (k + 1 < nitems) {  // every fetch of this block is issued: goff may change
-          Bn = w2_decode<CO_>(a, lb + (k + 1) * gsz);
-          w2_setup<CO_>(a, Bn, goff);
-          PMU_FETCH2(Bn, goff, 0, 0, nxt)
-        }
-        const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
-        w2_step<CH>(pa, ua, acc);                          // channel 2*kk
-        w2_step<CH>(pa + 4, ua + CO * NCP * 4, acc);       // channel 2*kk + 1
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
-        __syncthreads();
-      }
-      // (block-uniform values: made scalar, and laundered so the epilogue's address arithmetic is not
-      // hoisted out of the loops and held across the MFMAs)
-      int ne = __builtin_amdgcn_readfirstlane(B.n), h0e = __builtin_amdgcn_readfirstlane(B.h0);
-      int w0e = __builtin_amdgcn_readfirstlane(B.w0);
-      asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
-      float* xb = smem + ((gi - 1) & 1) * STAGE;
-      wino2h_epilogue<DGRAD, BNR, CH, CO>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
-      // block-uniform: the exchange overwrote xb's stage, where the next chunk after the next one
-      // lands: restore the zero units of the block that chunk belongs to
-      const bool next_pass = p + 1 < B.npass, next_item = !next_pass && k + 1 < nitems;
-      if (next_pass || next_item) {
-        const unsigned gz = next_pass ? B.gzero : Bn.gzero;
-#pragma unroll
-        for (int r = 0; r < NGL; ++r)
-          if ((gz >> r) & 1u) *reinterpret_cast<float4*>(xb + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f);
-        __syncthreads();
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int c = 0; c < 8; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < B.npass; ++p) {
+    const int j0 = (B.cob0 + p) * CO;
+    const int jb = j0 + 32 * cg + 16 * CH + t;
+    const float bias = (!DGRAD && a.bias && jb < a.NOUT) ? a.bias[jb] : 0.f;
+    int gi = p * nchunks;
+    for (int ch = 0; ch < nchunks; ++ch, ++gi) {
+      float* cur = smem + (gi & 1) * STAGE;
+      if (gi + 1 < total) PMU_FETCH2(gi + 1, smem + ((gi + 1) & 1) * STAGE)
+      const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
+      w2_step<CH>(pa, ua, acc);                          // channel 2*kk
+      w2_step<CH>(pa + 4, ua + CO * NCP * 4, acc);       // channel 2*kk + 1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
+      __syncthreads();
     }
-    B = Bn;
+    int ne = B.n, h0e = B.h0, w0e = B.w0;
+    asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
+    float* xb = smem + ((gi - 1) & 1) * STAGE;
+    wino2h_epilogue<DGRAD, BNR, CH, CO>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    if (p + 1 < B.npass) {  // block-uniform: restore the zero units the exchange overwrote
+#pragma unroll
+      for (int r = 0; r < NGL; ++r)
+        if ((B.gzero >> r) & 1u) *reinterpret_cast<float4*>(xb + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #undef PMU_FETCH2
 #undef PMU_GLDS
@@ -552,16 +480,48 @@ template <bool DGRAD, bool BNR, int CO_>
 // capped at 128 VGPRs (four waves per SIMD) so two workgroups share a CU (at 132 VGPRs only one fit)
 __global__ __launch_bounds__(16 * CO_, CO_ == 32 ? 4 : 1) void conv3x3_wino2h_kernel(W2Args a) {
   using C = W2Cfg<CO_>;
-  constexpr int STAGE = C::STAGE;
+  constexpr int NT = C::NT, NGL = C::NGL, STAGE = C::STAGE;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + C::RED_FLOATS];
   const int tid = threadIdx.x;
-  const int gsz = gridDim.x;
-  const int lb = pmu_xcd_block(blockIdx.x, gsz);
+  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
   const int ncog = (a.nco + a.cpb - 1) / a.cpb;
-  const int ntot = ncog * a.bw * a.bh * a.N;
-  const int nitems = (ntot - lb + gsz - 1) / gsz;
-  if ((tid >> 8) & 1) wino2h_main<DGRAD, BNR, 1, CO_>(a, lb, gsz, nitems, smem);
-  else wino2h_main<DGRAD, BNR, 0, CO_>(a, lb, gsz, nitems, smem);
+  W2Block B;
+  B.cob0 = (lb % ncog) * a.cpb;
+  int sp = lb / ncog;
+  B.spatial = sp;
+  const int bx = sp % a.bw; sp /= a.bw;
+  const int by = sp % a.bh;
+  B.n = sp / a.bh;
+  B.h0 = by * OH;
+  B.w0 = bx * OW;
+  const int KC = a.KC;
+  B.nchunks = KC / BK;
+  B.npass = a.cpb < a.nco - B.cob0 ? a.cpb : a.nco - B.cob0;
+  PMU_DCHECK(B.n < a.N && B.cob0 < a.nco, PMU_DBG_GRID);
+  unsigned goff[NGL];
+  unsigned gin = 0u, gzero = 0u;
+#pragma unroll
+  for (int r = 0; r < NGL; ++r) {
+    const int u = r * NT + tid;
+    const int hr = u / ROWU, wu = u - hr * ROWU;
+    const int g = wu / 5, w5 = wu - 5 * g;
+    const int px = 2 * g + (w5 >> 1);
+    const bool data = u < A_UNITS && w5 < 4 && px < HW;
+    const int h = B.h0 - 1 + hr, w = B.w0 - 1 + px;
+    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    goff[r] = in ? (unsigned)(((((long long)B.n * a.H + h) * a.W + w) * KC + 4 * (w5 & 1)) * 4) : 0u;
+    PMU_DCHECK(!in || (((long long)B.n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
+    gin |= in ? (1u << r) : 0u;
+    gzero |= (data && !in) ? (1u << r) : 0u;
+    if (data && !in) {
+      *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(smem + STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  B.gin = gin;
+  B.gzero = gzero;
+  if ((tid >> 8) & 1) wino2h_main<DGRAD, BNR, 1, CO_>(a, B, goff, smem);
+  else wino2h_main<DGRAD, BNR, 0, CO_>(a, B, goff, smem);
 }
 
 // output channels per block (PMU_WINO2H_CO=32: 512-thread blocks, two per CU; A/B)
@@ -615,11 +575,8 @@ int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, 
     while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= min_wg) cpb *= 2;
   }
   a.cpb = cpb;
-  const long long items = (long long)pmu_cdiv(a.nco, cpb) * spatial;
-  PMU_REQUIRE(items < (1LL << 31));
-  // persistent workgroups: as many as are resident at once (one 1024-thread or two 512-thread per CU)
-  const long long cap = (long long)pmu_num_cus() * (CO == 32 ? 2 : 1);
-  const long long blocks = items < cap ? items : cap;
+  const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
+  PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks);
   const bool bnr = dgrad && bz;

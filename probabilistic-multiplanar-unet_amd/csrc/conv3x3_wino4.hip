@@ -486,100 +486,37 @@ struct W4Block {
   unsigned gzero;  // image units outside it (zero, written once; restored after an exchange in their stage)
 };
 
-// work item L (spatial block, co-block group) of the persistent kernel, in the grid order of the
-// one-item-per-workgroup kernel (2-D grouping when a.tc > 0)
-__device__ __forceinline__ W4Block w4_decode(const W4Args& a, int L) {
-  W4Block B;
-  const int ncog = (a.nco + a.cpb - 1) / a.cpb;
-  int cg, sp;
-  if (a.tc > 0) {
-    // 2-D grouping (the host checked ncog % tc == 0 and spatial % ts == 0): an XCD's consecutive
-    // work items cover ts spatial blocks x tc co-groups, so its L2 holds ts operand images and tc U
-    // slices at a time instead of 1 image and all U slices
-    const int gsz = a.ts * a.tc, g = L / gsz, i = L - g * gsz;
-    const int gpr = ncog / a.tc;
-    cg = (g % gpr) * a.tc + i % a.tc;
-    sp = (g / gpr) * a.ts + i / a.tc;
-  } else {
-    cg = L % ncog;
-    sp = L / ncog;
-  }
-  B.cob0 = cg * a.cpb;
-  B.spatial = sp;
-  const int bx = sp % a.bw; sp /= a.bw;
-  const int by = sp % a.bh;
-  B.n = sp / a.bh;
-  B.h0 = by * OH;
-  B.w0 = bx * OW;
-  B.nchunks = a.KC / BK;
-  B.npass = a.cpb < a.nco - B.cob0 ? a.cpb : a.nco - B.cob0;
-  PMU_DCHECK(B.n < a.N && B.cob0 < a.nco, PMU_DBG_GRID);
-  return B;
-}
-
-// this thread's operand units of block B (byte offset of chunk 0 < 2^32, host-checked; inside the
-// input: DMA'd; image units outside it: zero), from a laundered thread id so they are recomputed per
-// work item instead of held across the loop
-__device__ __forceinline__ void w4_setup(const W4Args& a, W4Block& B, unsigned (&goff)[NGL]) {
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  unsigned gin = 0u, gzero = 0u;
-#pragma unroll
-  for (int r = 0; r < NGL; ++r) {
-    const int u = r * NT + tid;
-    const int hr = u / ROWU, wu = u - hr * ROWU;
-    const int g = wu / 9, w9 = wu - 9 * g;
-    const int px = 4 * g + (w9 >> 1);
-    const bool data = u < A_UNITS && w9 < 8 && px < HW;
-    const int h = B.h0 - 1 + hr, w = B.w0 - 1 + px;
-    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
-    goff[r] = in ? (unsigned)(((((long long)B.n * a.H + h) * a.W + w) * a.KC + 4 * (w9 & 1)) * 4) : 0u;
-    PMU_DCHECK(!in || (((long long)B.n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
-    gin |= in ? (1u << r) : 0u;
-    gzero |= (data && !in) ? (1u << r) : 0u;
-  }
-  B.gin = gin;
-  B.gzero = gzero;
-}
-
-// The persistent pipeline of a wave of component half CH (waves 4 CH .. 4 CH + 3): the workgroup walks
-// work items lb, lb + G, ... (G = the grid), each its co-block passes, each the chunks — one flat DMA
-// sequence, so the next pass's (or the next work item's) first chunk lands under this pass's last
-// MFMAs and epilogue (one work item per workgroup left the first DMA latency and the epilogue stores
-// of every workgroup without MFMAs beside them: one workgroup per CU).
+// the pass / chunk pipeline of a wave of component half CH (waves 4 CH .. 4 CH + 3)
 template <bool DGRAD, bool BNR, int CH, bool PF>
-__device__ __forceinline__ void wino4_main(const W4Args& a, int lb, int gsz, int nitems, float* smem) {
+__device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, const unsigned (&goff)[NGL],
+                                           float* smem) {
   float* red = smem + 2 * STAGE;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nchunks = a.KC / BK;
+  const int nchunks = B.nchunks, total = B.npass * nchunks;
+  const float* wsrc = a.wp + (long long)B.cob0 * nchunks * U_FLOATS;
   const unsigned uoff = 16u * tid;
   const int wave_off = wave * 256;
-  unsigned goff[NGL];
-  W4Block B = w4_decode(a, lb);
-  w4_setup(a, B, goff);
-  W4Block Bn = B;
+  const unsigned gin = B.gin;
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
                                    (__attribute__((address_space(3))) void*)(D), 16, 0, 0);
-  // chunk C of pass P of block FB into BUF.  Passes walk the chunks in alternating (serpentine) order:
-  // a pass starts on the chunks the previous pass fetched last, which are still in the XCD's L2 (~3 of
-  // a workgroup's 37-KB chunk images fit its share), instead of on chunk 0, fetched longest ago.  The
-  // direction follows the co-block's parity, not the pass index, so an output's summation order does
-  // not depend on cpb (launches split over images stay bit-equal to whole ones).  Image units outside
-  // the map are written as zeros (the stage may hold another block's data; ordered before its readers
-  // by the chunk barrier).
-#define PMU_FETCH4(FB, P, C, BUF)                                                                           \
+  // Passes walk the chunks in alternating (serpentine) order: a pass starts on the chunks the previous
+  // pass fetched last, which are still in the XCD's L2 (~3 of a workgroup's 37-KB chunk images fit its
+  // share), instead of on chunk 0, fetched longest ago.  The direction follows the co-block's parity,
+  // not the pass index, so an output's summation order does not depend on cpb (launches split over
+  // images stay bit-equal to whole ones).
+#define PMU_FETCH4(GI, BUF)                                                                                 \
   {                                                                                                        \
-    const int cs_ = (((FB).cob0 + (P)) & 1) ? nchunks - 1 - (C) : (C);                                     \
+    const int p_ = (GI) / nchunks;                                                                         \
+    const int c_ = (GI) - p_ * nchunks;                                                                    \
+    const int cs_ = ((B.cob0 + p_) & 1) ? nchunks - 1 - c_ : c_;                                           \
     const int k0_ = cs_ * BK;                                                                              \
     PMU_DCHECK(k0_ + BK <= a.KC, PMU_DBG_OPERAND);                                                         \
     float* b_ = (BUF);                                                                                     \
     const char* xb_ = reinterpret_cast<const char*>(a.x + k0_);                                            \
-    _Pragma("unroll") for (int r = 0; r < NGL; ++r) {                                                      \
-      if (((FB).gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                      \
-      if (((FB).gzero >> r) & 1u) *reinterpret_cast<float4*>(b_ + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f); \
-    }                                                                                                      \
-    const char* s_ = reinterpret_cast<const char*>(a.wp + ((long long)((FB).cob0 + (P)) * nchunks + cs_) * U_FLOATS) + uoff; \
+    _Pragma("unroll") for (int r = 0; r < NGL; ++r)                                                        \
+      if ((gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                           \
+    const char* s_ = reinterpret_cast<const char*>(wsrc + ((long long)p_ * nchunks + cs_) * U_FLOATS) + uoff; \
     float* d_ = b_ + A_FLOATS + wave_off;                                                                  \
     _Pragma("unroll") for (int r = 0; r < UGL; ++r)                                                        \
       if (r * NT * 4 + (wave + 1) * 256 <= U_FLOATS) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)          \
@@ -593,73 +530,110 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, int lb, int gsz, int
 #pragma unroll
     for (int c = 0; c < 18; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  PMU_FETCH4(B, 0, 0, smem)
-  PMU_FETCH4(B, 0, 0, smem + STAGE)  // (zero units of the other stage; its data is overwritten before use)
+  PMU_FETCH4(0, smem)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int gi = 0;  // flat chunk index: stage parity
-  for (int k = 0; k < nitems; ++k) {
-    for (int p = 0; p < B.npass; ++p) {
-      const int j0 = (B.cob0 + p) * CO;
-      const int jb = j0 + 16 * CH + t;
-      const float bias = (!DGRAD && a.bias && jb < a.NOUT) ? a.bias[jb] : 0.f;
-      for (int ch = 0; ch < nchunks; ++ch, ++gi) {
-        float* cur = smem + (gi & 1) * STAGE;
-        float* nxt = smem + ((gi + 1) & 1) * STAGE;
-        if (ch + 1 < nchunks) PMU_FETCH4(B, p, ch + 1, nxt)
-        else if (p + 1 < B.npass) PMU_FETCH4(B, p + 1, 0, nxt)
-        else if (k + 1 < nitems) {  // every fetch of this block is issued: goff may change
-          Bn = w4_decode(a, lb + (k + 1) * gsz);
-          w4_setup(a, Bn, goff);
-          PMU_FETCH4(Bn, 0, 0, nxt)
-        }
-        const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
-        w4_chunk<CH, PF>(pa, ua, acc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
-        __syncthreads();
-      }
-      // launder the block origin (scalar) so the epilogue's address arithmetic is not hoisted out of
-      // the loops (it would be held, and spilled, across the MFMA loop)
-      int ne = __builtin_amdgcn_readfirstlane(B.n), h0e = __builtin_amdgcn_readfirstlane(B.h0);
-      int w0e = __builtin_amdgcn_readfirstlane(B.w0);
-      asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
-      float* xb = smem + ((gi - 1) & 1) * STAGE;
-      wino4_epilogue<DGRAD, BNR, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
-      // block-uniform: the exchange overwrote xb's stage, where the chunk after the next one lands:
-      // restore the zero units of the block that chunk belongs to
-      const bool next_pass = p + 1 < B.npass, next_item = !next_pass && k + 1 < nitems;
-      if (next_pass || next_item) {
-        const unsigned gz = next_pass ? B.gzero : Bn.gzero;
-#pragma unroll
-        for (int r = 0; r < NGL; ++r)
-          if ((gz >> r) & 1u) *reinterpret_cast<float4*>(xb + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f);
-        __syncthreads();
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int c = 0; c < 18; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < B.npass; ++p) {
+    const int j0 = (B.cob0 + p) * CO;
+    const int jb = j0 + 16 * CH + t;
+    const float bias = (!DGRAD && a.bias && jb < a.NOUT) ? a.bias[jb] : 0.f;
+    int gi = p * nchunks;
+    for (int ch = 0; ch < nchunks; ++ch, ++gi) {
+      float* cur = smem + (gi & 1) * STAGE;
+      if (gi + 1 < total) PMU_FETCH4(gi + 1, smem + ((gi + 1) & 1) * STAGE)
+      const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
+      w4_chunk<CH, PF>(pa, ua, acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
+      __syncthreads();
     }
-    B = Bn;
+    // launder the block origin so the epilogue's address arithmetic is not hoisted out of the pass
+    // loop (it would be held, and spilled, across the MFMA loop)
+    int ne = B.n, h0e = B.h0, w0e = B.w0;
+    asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
+    float* xb = smem + ((gi - 1) & 1) * STAGE;
+    wino4_epilogue<DGRAD, BNR, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    if (p + 1 < B.npass) {  // block-uniform: every wave takes the barrier
+      // the exchange overwrote xb's stage: restore its zero units (each thread its own) before the
+      // next pass reads it
+#pragma unroll
+      for (int r = 0; r < NGL; ++r)
+        if ((B.gzero >> r) & 1u) *reinterpret_cast<float4*>(xb + 4 * (r * NT + tid)) = make_float4(0.f, 0.f, 0.f, 0.f);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int c = 0; c < 18; ++c) acc[h][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #undef PMU_FETCH4
 #undef PMU_GLDS
 }
 
+// A workgroup walks a.cpb output-channel blocks of one spatial block in passes; the flat
+// (pass, chunk) sequence is one DMA pipeline, so the next pass's first chunk lands under this
+// pass's epilogue.  Waves 0-3 compute components 0..17 (rows 0-2 of the 6x6 grid), waves 4-7 the
+// rest, each for its tile group's 16 tiles x all 32 output channels.
 // BNR (input gradient only): the producer's BN-backward partial sums in the epilogue (a.bz set) — a
 // compile-time choice, so the z loads and their uses sit in straight-line code
 template <bool DGRAD, bool BNR, bool PF>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
   const int tid = threadIdx.x;
-  const int gsz = gridDim.x;
-  const int lb = pmu_xcd_block(blockIdx.x, gsz);
+  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
   const int ncog = (a.nco + a.cpb - 1) / a.cpb;
-  const int ntot = ncog * a.bw * a.bh * a.N;
-  const int nitems = (ntot - lb + gsz - 1) / gsz;
+  W4Block B;
+  int cg, sp;
+  if (a.tc > 0) {
+    // 2-D grouping (the host checked ncog % tc == 0 and spatial % ts == 0): an XCD's consecutive
+    // workgroups cover ts spatial blocks x tc co-groups, so its L2 holds ts operand images and tc U
+    // slices at a time instead of 1 image and all U slices
+    const int gsz = a.ts * a.tc, g = lb / gsz, i = lb - g * gsz;
+    const int gpr = ncog / a.tc;
+    cg = (g % gpr) * a.tc + i % a.tc;
+    sp = (g / gpr) * a.ts + i / a.tc;
+  } else {
+    cg = lb % ncog;
+    sp = lb / ncog;
+  }
+  B.cob0 = cg * a.cpb;
+  B.spatial = sp;
+  const int bx = sp % a.bw; sp /= a.bw;
+  const int by = sp % a.bh;
+  B.n = sp / a.bh;
+  B.h0 = by * OH;
+  B.w0 = bx * OW;
+  const int KC = a.KC;
+  B.nchunks = KC / BK;
+  B.npass = a.cpb < a.nco - B.cob0 ? a.cpb : a.nco - B.cob0;
+  PMU_DCHECK(B.n < a.N && B.cob0 < a.nco, PMU_DBG_GRID);
+
+  // this thread's operand units: byte offset of chunk 0 (< 2^32, host-checked) and whether the unit
+  // is inside the input; units of the image outside it are zeroed in both stages once
+  unsigned goff[NGL];
+  unsigned gin = 0u, gzero = 0u;
+#pragma unroll
+  for (int r = 0; r < NGL; ++r) {
+    const int u = r * NT + tid;
+    const int hr = u / ROWU, wu = u - hr * ROWU;
+    const int g = wu / 9, w9 = wu - 9 * g;
+    const int px = 4 * g + (w9 >> 1);
+    const bool data = u < A_UNITS && w9 < 8 && px < HW;
+    const int h = B.h0 - 1 + hr, w = B.w0 - 1 + px;
+    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+    goff[r] = in ? (unsigned)(((((long long)B.n * a.H + h) * a.W + w) * KC + 4 * (w9 & 1)) * 4) : 0u;
+    PMU_DCHECK(!in || (((long long)B.n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
+    gin |= in ? (1u << r) : 0u;
+    gzero |= (data && !in) ? (1u << r) : 0u;
+    if (data && !in) {
+      *reinterpret_cast<float4*>(smem + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(smem + STAGE + 4 * u) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  B.gin = gin;
+  B.gzero = gzero;
   if (a.prio && (tid >> 8)) __builtin_amdgcn_s_setprio(1);
-  if (tid >> 8) wino4_main<DGRAD, BNR, 1, PF>(a, lb, gsz, nitems, smem);
-  else wino4_main<DGRAD, BNR, 0, PF>(a, lb, gsz, nitems, smem);
+  if (tid >> 8) wino4_main<DGRAD, BNR, 1, PF>(a, B, goff, smem);
+  else wino4_main<DGRAD, BNR, 0, PF>(a, B, goff, smem);
 }
 
 int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
@@ -726,11 +700,8 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
       if (ncog % tc == 0 && spatial % ts == 0 && tc > 1 && ts > 1) { a.tc = tc; a.ts = ts; }
     }
   }
-  const long long items = (long long)pmu_cdiv(a.nco, cpb) * spatial;
-  PMU_REQUIRE(items < (1LL << 31));
-  // persistent workgroups: one per CU (the resident limit of this kernel)
-  const long long cap = pmu_num_cus();
-  const long long blocks = items < cap ? items : cap;
+  const long long blocks = (long long)pmu_cdiv(a.nco, cpb) * spatial;
+  PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks);
   if (dgrad && bz) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, false>), grid, dim3(NT), 0, st, a);

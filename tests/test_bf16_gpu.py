@@ -585,9 +585,8 @@ def _pack_dma(w, dgrad):
 def test_conv3x3_fwd_dma(dev, N, H, W, Cin, Cout):
     """The LDS-DMA bf16 conv (both operands by global_load_lds, swizzled units) == conv of the rounded
     operand: partial tiles in both directions, ragged channel blocks, both block shapes (64 / 128
-    output channels), BN partial sums.  The last two have more tiles than resident workgroups, so
-    the persistent workgroups walk several tiles each (border tiles among them: their zero units
-    are rewritten per tile)."""
+    output channels), BN partial sums.  The last two have more tiles than resident workgroups
+    (several dispatch rounds, border tiles in every round)."""
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src
     g = torch.Generator().manual_seed(71 + H + Cout)

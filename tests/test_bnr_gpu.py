@@ -70,7 +70,7 @@ def test_dgrad_bnr_fp32(dev, kind, N, H, W, Cin, Cout):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 40, 64, 64, 64), (1, 33, 45, 128, 96), (2, 32, 32, 256, 128),
-                                            (32, 90, 70, 64, 64)])  # last: several tiles per persistent workgroup
+                                            (32, 90, 70, 64, 64)])  # last: more tiles than resident workgroups
 def test_dgrad_bnr_dma(dev, N, H, W, Cin, Cout):
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src, frame_to_bf16, pack_weights_dma

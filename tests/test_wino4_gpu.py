@@ -91,7 +91,7 @@ sys.path.insert(0, sys.argv[1])
 from pmu_hip import _lib as L
 from pmu_hip.engine import pack_weights_wino4
 N, H, W, Cin, Cout, split = 2, 40, 36, 160, 64, 96
-if len(sys.argv) > 2:  # several work items per persistent workgroup, each with several passes
+if len(sys.argv) > 2:  # many workgroups of several passes, border blocks
     N, H, W = 20, 100, 90
 g = torch.Generator().manual_seed(19)
 dz = torch.randn(N, H, W, Cout, generator=g).cuda()
@@ -130,9 +130,8 @@ def test_wino4_multipass(cpb, big):
     """Output-channel passes of the F(4x4) kernels (a workgroup walking cpb co-blocks of one spatial
     block, the next pass's first chunk fetched under this pass's MFMAs), forced through PMU_WINO4_CPB:
     input gradient with Cin = 160 (5 co-blocks, concat split inside a pass) and forward with
-    Cout = 160 (bias and BN partial sums per pass).  big: 720 work items for 256 persistent
-    workgroups, so a workgroup's flat pipeline crosses from a pass to the next pass and to the next
-    work item (new operand units, border blocks)."""
+    Cout = 160 (bias and BN partial sums per pass).  big: 720 workgroups of 2, 2 and 1 passes over
+    border and interior blocks, several dispatch rounds."""
     pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "probabilistic-multiplanar-unet_amd")
     from pmu_hip import _lib as L
     if not os.path.exists(L.EXP_LIB_PATH):
