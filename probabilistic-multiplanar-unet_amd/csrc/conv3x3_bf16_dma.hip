@@ -421,6 +421,15 @@ struct Shape {
   int wn, nwv, th;
 };
 static Shape dma_shape(int NOUT, int KC) {
+#ifdef PMU_EXPERIMENTS
+  // PMU_DMA_TALL=1 (A/B): the 64-channel workgroups as 8 waves over 32 tile rows (1024 pixels, one
+  // workgroup per CU: half the tiles, a 34-row halo per 32 output rows instead of 18 per 16)
+  static const int tall = [] {
+    const char* e = pmu_variant_env("PMU_DMA_TALL");
+    return e ? atoi(e) : 0;
+  }();
+  if (tall && dma_bn(NOUT, KC) == 64) return {1, 8, 32};
+#endif
   if (dma_bn(NOUT, KC) == 64) return {1, 4, 16};
   return {2, 8, 16};
 }
@@ -465,16 +474,23 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks), blk(64 * sh.nwv);
   const bool zb = zbf == 1;
+#ifdef PMU_EXPERIMENTS
+#define PMU_DMA_TALL_LAUNCH(D, Z, CSV) \
+  else if (sh.wn == 1 && sh.nwv == 8) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 8, 0, CSV>), grid, blk, 0, st, a);
+#else
+#define PMU_DMA_TALL_LAUNCH(D, Z, CSV)
+#endif
 #define PMU_DMA_LAUNCH(D, Z)                                                                              \
   {                                                                                                       \
-    if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 4>), grid, blk, 0, st, a);            \
+    if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 4>), grid, blk, 0, st, a); \
+    PMU_DMA_TALL_LAUNCH(D, Z, false)                                                                      \
     else hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 2, 8>), grid, blk, 0, st, a);                       \
   }
 #ifdef PMU_EXPERIMENTS
   {
     const char* e = pmu_variant_env("PMU_DMA_EXP");
     const int x = e ? atoi(e) : 0;
-    if (!dgrad && !zb && x >= 1 && x <= 3) {
+    if (!dgrad && !zb && x >= 1 && x <= 3 && !(sh.wn == 1 && sh.nwv == 8)) {
       if (sh.wn == 1) {
         if (x == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<false, false, 1, 4, 1>), grid, blk, 0, st, a);
         if (x == 2) hipLaunchKernelGGL((conv3x3_dma_kernel<false, false, 1, 4, 2>), grid, blk, 0, st, a);
@@ -490,7 +506,8 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   }
 #endif
   if (dgrad && part && !bz) {  // column sums (pmu_conv3x3_dgrad_dma_x1b_sum)
-    if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true>), grid, blk, 0, st, a);
+    if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true>), grid, blk, 0, st, a);
+    PMU_DMA_TALL_LAUNCH(true, false, true)
     else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, true>), grid, blk, 0, st, a);
   }
 #ifdef PMU_EXPERIMENTS
@@ -502,6 +519,7 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   else if (dgrad) PMU_DMA_LAUNCH(true, false)
   else PMU_DMA_LAUNCH(false, false)
 #undef PMU_DMA_LAUNCH
+#undef PMU_DMA_TALL_LAUNCH
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

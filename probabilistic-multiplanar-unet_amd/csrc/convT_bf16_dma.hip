@@ -36,6 +36,7 @@ struct GArgs {
   int nnb;
   int ldo;                    // fwd: output pixel stride (Cout, or the concat operand's width)
   unsigned short* outb;       // fwd, nullable: write bf16(u) here (pixel stride ldo) instead of out
+  int pair;                   // outb 4-byte aligned and ldo even: channel pairs stored as one 4-byte word
 };
 
 template <int WN>
@@ -230,19 +231,42 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
       const long long cbase = (long long)(ab >> 1) * 2 * g.W * ldo + (ab & 1) * ldo + co;
       float* outc = g.out + cbase;
       unsigned short* outcb = g.outb + cbase;
+      if (g.outb && g.pair) {
+        // bf16 output as 4-byte channel pairs: lanes 2k and 2k+1 hold adjacent channels of the same two
+        // rows (r, r + 1); one xor-1 shuffle gives the even lane row r's pair and the odd lane row
+        // r + 1's, so each stores 4 bytes (half the store instructions of 2-byte stores)
+        const int odd = lane & 1;
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
+        for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 128 + fm * 32 + acc_row(r, lane);
-          if (m < g.M) {
-            const unsigned t = (unsigned)m / (unsigned)g.W, j = (unsigned)m - t * (unsigned)g.W;
-            const unsigned n = t / (unsigned)g.H, i = t - n * (unsigned)g.H;
-            const long long o = ((long long)(n * 2 * g.H + 2 * i) * (2 * g.W) + 2 * j) * ldo;
-            if (g.outb) outcb[o] = __builtin_bit_cast(unsigned short, (__bf16)(acc[fm][fn][r] + b));
-            else outc[o] = acc[fm][fn][r] + b;
+          for (int r = 0; r < 16; r += 2) {
+            const unsigned b0 = __builtin_bit_cast(unsigned short, (__bf16)(acc[fm][fn][r] + b));
+            const unsigned b1 = __builtin_bit_cast(unsigned short, (__bf16)(acc[fm][fn][r + 1] + b));
+            const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);
+            const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
+            const int m = m0 + wm * 128 + fm * 32 + acc_row(r + odd, lane);
+            if (m < g.M) {
+              const unsigned t = (unsigned)m / (unsigned)g.W, j = (unsigned)m - t * (unsigned)g.W;
+              const unsigned n = t / (unsigned)g.H, i = t - n * (unsigned)g.H;
+              const long long o = ((long long)(n * 2 * g.H + 2 * i) * (2 * g.W) + 2 * j) * ldo - odd;
+              *reinterpret_cast<unsigned*>(outcb + o) = pair;
+            }
           }
-        }
+      } else {
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * 128 + fm * 32 + acc_row(r, lane);
+            if (m < g.M) {
+              const unsigned t = (unsigned)m / (unsigned)g.W, j = (unsigned)m - t * (unsigned)g.W;
+              const unsigned n = t / (unsigned)g.H, i = t - n * (unsigned)g.H;
+              const long long o = ((long long)(n * 2 * g.H + 2 * i) * (2 * g.W) + 2 * j) * ldo;
+              if (g.outb) outcb[o] = __builtin_bit_cast(unsigned short, (__bf16)(acc[fm][fn][r] + b));
+              else outc[o] = acc[fm][fn][r] + b;
+            }
+          }
+      }
     }
   }
 }
@@ -308,6 +332,7 @@ extern "C" int pmu_convT2x2_fwd_dma_ldb(const unsigned short* xt, int Cip, int N
   g.a = xt; g.bp = wp; g.bias = bias; g.out = nullptr; g.outb = ub;
   g.M = N * H * W; g.Ncols = 4 * Cout; g.K = Cin; g.lda = Cip;
   g.H = H; g.W = W; g.Cout = Cout; g.ldo = ldo;
+  g.pair = (ldo % 2 == 0 && (reinterpret_cast<uintptr_t>(ub) & 3) == 0) ? 1 : 0;
   return launch<false>(g, stream);
 }
 

@@ -62,7 +62,8 @@ def test_convT_fwd_dgrad_match_float64(N, H, W, Cin, Cout):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,H,W,Cin,Cup,Cskip", [(2, 16, 16, 128, 64, 64), (1, 8, 32, 256, 128, 128)])
+@pytest.mark.parametrize("N,H,W,Cin,Cup,Cskip", [(2, 16, 16, 128, 64, 64), (1, 8, 32, 256, 128, 128),
+                                                  (1, 7, 9, 128, 64, 64)])  # odd pixel count (pair stores)
 def test_concat_operand_built_in_place(N, H, W, Cin, Cup, Cskip):
     """The Up block's concat operand written in place (unet_parts.py:52,66): pmu_convT2x2_fwd_ld /
     pmu_convT2x2_fwd_dma_ldb fill channels [Cskip, Cskip + Cup) and pmu_frame_to_f32_ld /
