@@ -332,14 +332,32 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
   #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
         const int h = h0 + 4 * wm + fm;
+        if (dstb) {
+          // the bf16 copy as 4-byte channel pairs: lanes 2k, 2k+1 hold adjacent channels of the same
+          // pixels r, r + 1; one xor-1 shuffle gives the even lane pixel r's pair and the odd lane pixel
+          // r + 1's (half the store instructions of 2-byte stores; dstb is uniform per fragment, so the
+          // whole wave runs the shuffles; channel pairs never straddle NOUT: NOUT - split % 8 == 0)
+          const int odd = lane & 1;
+  #pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const unsigned b0 = bf16_bits(acc[fm][fn][r]), b1 = bf16_bits(acc[fm][fn][r + 1]);
+            const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);
+            const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
+            const int w = w0 + acc_row(r + odd, lane);
+            if (!jok || h >= a.H || w >= a.W) continue;
+            const long long pix = ((long long)n * a.H + h) * a.W + w;
+            PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+            *reinterpret_cast<unsigned*>(dstb + pix * ld - odd) = pair;
+          }
+        }
+        if (CS && !dstp) continue;  // (only the CS variant has a null out1: its dx1 is the bf16 copy alone)
   #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int w = w0 + acc_row(r, lane);
           if (!jok || h >= a.H || w >= a.W) continue;
           const long long pix = ((long long)n * a.H + h) * a.W + w;
           PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-          if (!CS || dstp) dstp[pix * ld] = acc[fm][fn][r];  // (only the CS variant has a null out1)
-          if (dstb) dstb[pix * ld] = bf16_bits(acc[fm][fn][r]);
+          dstp[pix * ld] = acc[fm][fn][r];
         }
       }
     }

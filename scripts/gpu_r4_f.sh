@@ -7,6 +7,9 @@ cd $R
 PMU_LIB=exp PMU_DMA_TALL=1 timeout -k 10 600 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu \
   tests/test_bf16_gpu.py tests/test_bnr_gpu.py -k "dma" > $O/tests_tall.log 2>&1 || { tail -30 $O/tests_tall.log; exit 1; }
 tail -2 $O/tests_tall.log
+timeout -k 10 600 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu \
+  tests/test_bf16_gpu.py tests/test_bnr_gpu.py -k "dma" > $O/tests_rel.log 2>&1 || { tail -30 $O/tests_rel.log; exit 1; }
+tail -1 $O/tests_rel.log
 for T in 0 1; do
   PMU_LIB=exp PMU_DMA_TALL=$T timeout -k 10 300 python tools/kbench.py --c5 --ops fwd_dma,dgrad_dma,dgrad_dmab --iters 5 > $O/kbench_c5_tall$T.txt 2>&1 || exit $?
   grep TOTAL $O/kbench_c5_tall$T.txt
