@@ -278,12 +278,41 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       bv[fn] = a.bias ? a.bias[jc] : 0.f;
       zov[fn] = (ZB && a.zoff) ? a.zoff[jc] : 0.f;
     }
+    // (ZB = false, NOUT even) z as 8-byte channel pairs: lanes 2k, 2k+1 hold adjacent channels of the
+    // same pixels r, r + 1; one xor-1 shuffle gives the even lane pixel r's pair and the odd lane pixel
+    // r + 1's — half the store instructions (the bf16 ConvT forward gained 23% from the same change)
+    const bool pairs = !ZB && (a.NOUT & 1) == 0;
+    const int odd = lane & 1;
   #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
       const int h = h0 + 4 * wm + fm;
       const long long rowpix = ((long long)n * a.H + (h < a.H ? h : a.H - 1)) * a.W;
       float* drow = a.out0 + rowpix * a.NOUT;
       unsigned short* drowb = reinterpret_cast<unsigned short*>(a.out0) + rowpix * a.NOUT;
+      if (pairs) {
+  #pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int j = j0 + wn * 64 + fn * 32 + li;
+  #pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const float v0 = acc[fm][fn][r] + bv[fn], v1 = acc[fm][fn][r + 1] + bv[fn];
+            const bool ok0 = jok[fn] && h < a.H && w0 + acc_row(r, lane) < a.W;
+            const bool ok1 = jok[fn] && h < a.H && w0 + acc_row(r + 1, lane) < a.W;
+            const float m0 = ok0 ? v0 : 0.f, m1 = ok1 ? v1 : 0.f;
+            s1[fn] += m0;
+            s2[fn] = fmaf(m0, m0, s2[fn]);
+            s1[fn] += m1;
+            s2[fn] = fmaf(m1, m1, s2[fn]);
+            const float recv = __shfl_xor(odd ? v0 : v1, 1, 64);
+            const float2 pv = odd ? make_float2(recv, v1) : make_float2(v0, recv);
+            const int w = w0 + acc_row(r + odd, lane);
+            if (!(jok[fn] && h < a.H && w < a.W) || (EXP & 1)) continue;
+            PMU_DCHECK(((long long)n * a.H + h) * a.W + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+            *reinterpret_cast<float2*>(drow + (unsigned)(w * a.NOUT + j - odd)) = pv;
+          }
+        }
+        continue;
+      }
   #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const int j = j0 + wn * 64 + fn * 32 + li;
@@ -351,6 +380,21 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
           }
         }
         if (CS && !dstp) continue;  // (only the CS variant has a null out1: its dx1 is the bf16 copy alone)
+        if ((ld & 1) == 0) {  // (uniform) fp32 dx as 8-byte channel pairs, as the bf16 copy above
+          const int odd = lane & 1;
+  #pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const float v0 = acc[fm][fn][r], v1 = acc[fm][fn][r + 1];
+            const float recv = __shfl_xor(odd ? v0 : v1, 1, 64);
+            const float2 pv = odd ? make_float2(recv, v1) : make_float2(v0, recv);
+            const int w = w0 + acc_row(r + odd, lane);
+            if (!jok || h >= a.H || w >= a.W) continue;
+            const long long pix = ((long long)n * a.H + h) * a.W + w;
+            PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+            *reinterpret_cast<float2*>(dstp + pix * ld - odd) = pv;
+          }
+          continue;
+        }
   #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int w = w0 + acc_row(r, lane);
