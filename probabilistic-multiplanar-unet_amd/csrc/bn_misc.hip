@@ -1051,18 +1051,13 @@ __global__ __launch_bounds__(256) void wgrad1x1_fast_kernel(const float* __restr
 }
 
 // out[o] = sum_r ws[r][o] for o < K*(C+1), split into dw[k][c] and db[k]; 64 outputs x 4 row phases
-__global__ __launch_bounds__(256) void rows_sum_split4_kernel(const float* __restrict__ ws, int R, int K, int C,
-                                                              float* dw, float* db) {
-  __shared__ double red[256];
+__global__ __launch_bounds__(1024) void rows_sum_split4_kernel(const float* __restrict__ ws, int R, int K, int C,
+                                                               float* dw, float* db) {
+  __shared__ double red[1024];
   const int CW = C + 1, Wd = K * CW;
-  const int o = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
-  double s = 0.0;
-  if (o < Wd)
-    for (int r = ph; r < R; r += 4) s += ws[(long long)r * Wd + o];
-  red[threadIdx.x] = s;
-  __syncthreads();
+  const int o = blockIdx.x * 64 + (threadIdx.x & 63);
+  const double t = pmu_colsum64x16(ws, R, Wd, o, red);
   if (threadIdx.x < 64 && o < Wd) {
-    const double t = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
     const int k = o / CW, c = o - k * CW;
     if (c < C) dw[k * C + c] = (float)t;
     else if (db) db[k] = (float)t;
@@ -1544,7 +1539,7 @@ extern "C" int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmo
     }
 #undef PMU_HEAD_FUSED
     PMU_CHECK_LAUNCH();
-    hipLaunchKernelGGL(rows_sum_split4_kernel, dim3((unsigned)pmu_cdiv(K * (C + 1), 64)), dim3(256), 0,
+    hipLaunchKernelGGL(rows_sum_split4_kernel, dim3((unsigned)pmu_cdiv(K * (C + 1), 64)), dim3(1024), 0,
                        (hipStream_t)stream, (const float*)ws, R, K, C, dw, db);
   } else {
     hipLaunchKernelGGL((head_bwd_fast_kernel<true, false>), dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dy, y,
@@ -1573,7 +1568,7 @@ extern "C" int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float*
   else
     hipLaunchKernelGGL(wgrad1x1_kernel, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dl, f, K, ws);
   PMU_CHECK_LAUNCH();
-  hipLaunchKernelGGL(rows_sum_split4_kernel, dim3((unsigned)pmu_cdiv(K * (f.C + 1), 64)), dim3(256), 0,
+  hipLaunchKernelGGL(rows_sum_split4_kernel, dim3((unsigned)pmu_cdiv(K * (f.C + 1), 64)), dim3(1024), 0,
                      (hipStream_t)stream, (const float*)ws, R, K, f.C, dw, db);
   PMU_CHECK_LAUNCH();
   return PMU_OK;

@@ -310,17 +310,12 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_tile_kernel(FirstWgArgs 
 }
 
 // out[o] = sum_r ws[r][o]: block = 64 outputs x 4 row phases (fixed order), fp64 accumulation
-__global__ __launch_bounds__(256) void rows_sum4_kernel(const float* __restrict__ ws, int R, int Wd,
-                                                        float* __restrict__ out) {
-  __shared__ double red[256];
-  const int o = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
-  double s = 0.0;
-  if (o < Wd)
-    for (int r = ph; r < R; r += 4) s += ws[(long long)r * Wd + o];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x < 64 && o < Wd) out[o] = (float)(red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] +
-                                                   red[threadIdx.x + 192]);
+__global__ __launch_bounds__(1024) void rows_sum4_kernel(const float* __restrict__ ws, int R, int Wd,
+                                                         float* __restrict__ out) {
+  __shared__ double red[1024];
+  const int o = blockIdx.x * 64 + (threadIdx.x & 63);
+  const double t = pmu_colsum64x16(ws, R, Wd, o, red);
+  if (threadIdx.x < 64 && o < Wd) out[o] = (float)t;
 }
 
 // dw[o] = sum_b ws[b][o]
@@ -406,7 +401,7 @@ extern "C" int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* pla
   }
   PMU_CHECK_LAUNCH();
   const int Wd = Cout * Cin * 9;
-  hipLaunchKernelGGL(rows_sum4_kernel, dim3((unsigned)pmu_cdiv(Wd, 64)), dim3(256), 0, st, (const float*)ws, nb, Wd,
+  hipLaunchKernelGGL(rows_sum4_kernel, dim3((unsigned)pmu_cdiv(Wd, 64)), dim3(1024), 0, st, (const float*)ws, nb, Wd,
                      dw);
   PMU_CHECK_LAUNCH();
   return PMU_OK;

@@ -17,6 +17,32 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
   } while (0)
 
 static inline int pmu_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+// Column sums of an fp32 slab ws[R][Wd] in fp64, in a fixed order, for the 1024-thread block that owns
+// columns [64 b, 64 b + 64): thread (column o, phase ph = tid >> 6 of 16) sums rows ph, ph + 16, ... in
+// four interleaved fp64 accumulators (four loads in flight; combined in order), then the 16 phases are
+// combined in order through red[1024].  Returns the total in threads tid < 64 (0 elsewhere).  (One
+// dependent fp64 add per row with 4 phases left 512-row reductions latency-bound at ~0.2 ms.)
+__device__ __forceinline__ double pmu_colsum64x16(const float* __restrict__ ws, int R, int Wd, int o, double* red) {
+  const int tid = threadIdx.x, ph = tid >> 6;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (o < Wd) {
+    int r = ph;
+    for (; r + 48 < R; r += 64) {
+      a0 += (double)ws[(long long)r * Wd + o];
+      a1 += (double)ws[(long long)(r + 16) * Wd + o];
+      a2 += (double)ws[(long long)(r + 32) * Wd + o];
+      a3 += (double)ws[(long long)(r + 48) * Wd + o];
+    }
+    for (; r < R; r += 16) a0 += (double)ws[(long long)r * Wd + o];
+  }
+  red[tid] = ((a0 + a1) + a2) + a3;
+  __syncthreads();
+  double t = 0.0;
+  if (tid < 64)
+    for (int p = 0; p < 16; ++p) t += red[p * 64 + tid];
+  return t;
+}
+
 // compute units of the current device (cached per process: one device per process)
 static inline int pmu_num_cus() {
   static const int cus = [] {
