@@ -267,10 +267,13 @@ int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* planes, int Ci
 int pmu_colsum_f64(const float* part, int R, int Wd, double* out, int G, void* stream);
 int pmu_colsum_groups(int R);
 /* From fp64 sums acc[G][2][C] (sum, sumsq) over count elements: mean, invstd, coef=[scale|shift];
- * update running stats (unbiased var, momentum) when running_mean != NULL. */
+ * update running stats (unbiased var, momentum) when running_mean != NULL, and add 1 to
+ * *num_batches_tracked when it is non-NULL (BatchNorm2d's counter, PMU/model/unet/unet_parts.py:16,19:
+ * one launch instead of a separate increment per layer). */
 int pmu_bn_fwd_finalize(const double* acc, int G, int C, double count, const float* gamma,
                         const float* beta, float eps, float momentum, float* running_mean,
-                        float* running_var, float* mean, float* invstd, float* coef, void* stream);
+                        float* running_var, long long* num_batches_tracked, float* mean, float* invstd,
+                        float* coef, void* stream);
 /* Eval mode: coef from running stats. */
 int pmu_bn_eval_coef(const float* running_mean, const float* running_var, const float* gamma,
                      const float* beta, float eps, int C, float* coef, void* stream);

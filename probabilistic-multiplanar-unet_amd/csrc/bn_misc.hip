@@ -56,8 +56,9 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const double* __re
                                                               double count, const float* __restrict__ gamma,
                                                               const float* __restrict__ beta, float eps,
                                                               float momentum, float* running_mean,
-                                                              float* running_var, float* mean_out,
+                                                              float* running_var, long long* nbt, float* mean_out,
                                                               float* invstd_out, float* coef) {
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] = nbt[0] + 1;  // (one lane, a vector store)
   double s1, s2;
   if (!group_sums(acc, G, C, s1, s2)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -1255,11 +1256,13 @@ extern "C" int pmu_colsum_f64(const float* part, int R, int Wd, double* out, int
 
 extern "C" int pmu_bn_fwd_finalize(const double* acc, int G, int C, double count, const float* gamma,
                                    const float* beta, float eps, float momentum, float* running_mean,
-                                   float* running_var, float* mean, float* invstd, float* coef, void* stream) {
+                                   float* running_var, long long* num_batches_tracked, float* mean,
+                                   float* invstd, float* coef, void* stream) {
   PMU_REQUIRE(acc && G > 0 && C > 0 && count > 0 && mean && invstd && coef);
   PMU_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((unsigned)pmu_cdiv(C, 64)), dim3(256), 0, (hipStream_t)stream,
-                     acc, G, C, count, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, coef);
+                     acc, G, C, count, gamma, beta, eps, momentum, running_mean, running_var,
+                     num_batches_tracked, mean, invstd, coef);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

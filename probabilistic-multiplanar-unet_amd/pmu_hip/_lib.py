@@ -110,7 +110,7 @@ SIGNATURES = {
     "pmu_colsum_f64": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
     "pmu_colsum_groups": (c_int, [c_int]),
     "pmu_bn_fwd_finalize": (c_int, [c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_float, c_float,
-                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_bn_eval_coef": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p, c_void_p]),
     "pmu_bn_bwd_reduce": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                   c_void_p]),

@@ -159,14 +159,19 @@ def bn_forward(part, R: int, C: int, count: int, bn: torch.nn.BatchNorm2d, train
     mean, invstd, coef = _empty(C, device=dev), _empty(C, device=dev), _empty(2 * C, device=dev)
     update = training and bn.track_running_stats and bn.running_mean is not None
     momentum = bn.momentum
+    nbt = None  # the finalize kernel adds 1 to num_batches_tracked (one launch fewer per layer)
     if update:
-        bn.num_batches_tracked.add_(1)
-        if momentum is None:  # cumulative moving average
+        if momentum is None:  # cumulative moving average: the host needs the count now
+            bn.num_batches_tracked.add_(1)
             momentum = 1.0 / float(bn.num_batches_tracked.item())
+        elif bn.num_batches_tracked.dtype == torch.int64 and bn.num_batches_tracked.device == dev:
+            nbt = bn.num_batches_tracked.data_ptr()
+        else:
+            bn.num_batches_tracked.add_(1)
     L.call("pmu_bn_fwd_finalize", acc.data_ptr(), G, C, float(count), L.ptr(bn.weight), L.ptr(bn.bias),
            float(bn.eps), float(momentum or 0.0),
            bn.running_mean.data_ptr() if update else None, bn.running_var.data_ptr() if update else None,
-           mean.data_ptr(), invstd.data_ptr(), coef.data_ptr(), s)
+           nbt, mean.data_ptr(), invstd.data_ptr(), coef.data_ptr(), s)
     return BNState(coef=coef, mean=mean, invstd=invstd, count=float(count))
 
 
