@@ -161,3 +161,65 @@ def test_data_write_needs_invalidate_packs(dev):
     assert not torch.equal(y1, y0)
     assert torch.equal(y1, y_ref)                         # after invalidate_packs(): the new weights
     assert torch.equal(y2, y0)                            # the load is seen without invalidate_packs()
+
+
+def _expected_dma(w, dgrad):
+    """The LDS-DMA bf16 layout (csrc/conv3x3_bf16_dma.hip, pack_dma_body): wp[jb][ch][tap][u][e], unit u =
+    2 co + (q XOR bit 3 of co) holding B[tap][k = 16 ch + 8 q + e][j = BN jb + co]; forward B[tap][ci][co] =
+    w[co][ci][tap], input gradient B[tap][co][ci] = w[co][ci][8 - tap]; zero padded, bf16 RNE."""
+    wf = w.float().cpu().reshape(w.shape[0], w.shape[1], 9)
+    B = wf.flip(2).permute(2, 0, 1) if dgrad else wf.permute(2, 1, 0)   # [tap][k][j]
+    KC, NOUT = B.shape[1], B.shape[2]
+    BN = 64 if (NOUT <= 64 or -(-KC // 16) * 16 <= 128) else 128
+    njb, nch = -(-NOUT // BN), -(-KC // 16)
+    full = torch.zeros(9, nch * 16, njb * BN)
+    full[:, :KC, :NOUT] = B
+    X = full.reshape(9, nch, 2, 8, njb, BN).permute(4, 1, 0, 5, 2, 3)   # [jb][ch][tap][co][q][e]
+    u = torch.arange(2 * BN)
+    co = u >> 1
+    q = (u & 1) ^ ((co >> 3) & 1)
+    return X[:, :, :, co, q, :].contiguous().reshape(-1).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("Cout,Cin", [(64, 64), (40, 24), (128, 72), (256, 160), (96, 8)])
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_pack_dma(dev, Cout, Cin, dgrad):
+    """The bf16 LDS-DMA pack (one 16-B unit per thread) equals the layout restatement bit for bit."""
+    from pmu_hip import _lib as L
+    g = torch.Generator().manual_seed(Cout * 3 + Cin + int(dgrad))
+    w = torch.randn(Cout, Cin, 3, 3, generator=g).to(dev)
+    n = L.lib().pmu_conv3x3_packed_size_dma(Cout, Cin, int(dgrad)) // 2
+    wp = torch.full((n,), -1, dtype=torch.int16, device=dev)
+    L.call("pmu_conv3x3_pack_dma", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = _expected_dma(w, dgrad)
+    assert ref.numel() == n
+    assert torch.equal(wp.cpu(), ref.view(torch.int16))
+
+
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_pack_dma_multi(dev, dgrad):
+    """One batched launch over ragged tensors (each job's blocks from pmu_conv3x3_pack_dma_blocks) equals
+    the single-tensor packs."""
+    from pmu_hip import _lib as L
+    shapes = [(64, 64), (40, 24), (256, 160), (96, 8), (512, 256)]
+    g = torch.Generator().manual_seed(11 + int(dgrad))
+    ws = [torch.randn(co, ci, 3, 3, generator=g).to(dev) for co, ci in shapes]
+    outs = [torch.full((L.lib().pmu_conv3x3_packed_size_dma(co, ci, int(dgrad)) // 2,), -1, dtype=torch.int16,
+                       device=dev) for co, ci in shapes]
+    jobs = (L.PmuPackJob * len(ws))()
+    b0 = 0
+    for i, (w, o) in enumerate(zip(ws, outs)):
+        nb = L.lib().pmu_conv3x3_pack_dma_blocks(w.shape[0], w.shape[1], int(dgrad))
+        jobs[i] = L.PmuPackJob(w.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], b0, nb)
+        b0 += nb
+    jt = torch.frombuffer(bytearray(bytes(jobs)), dtype=torch.uint8).to(dev)
+    L.call("pmu_conv3x3_pack_dma_multi", jt.data_ptr(), len(ws), b0, int(dgrad), L.stream())
+    torch.cuda.synchronize()
+    for w, o in zip(ws, outs):
+        single = torch.full_like(o, -1)
+        L.call("pmu_conv3x3_pack_dma", w.data_ptr(), w.shape[0], w.shape[1], int(dgrad), single.data_ptr(),
+               L.stream())
+        torch.cuda.synchronize()
+        assert torch.equal(o, single), tuple(w.shape)
+        assert torch.equal(o.cpu(), _expected_dma(w, dgrad).view(torch.int16))
