@@ -37,6 +37,7 @@ struct GArgs {
   int ldo;                    // fwd: output pixel stride (Cout, or the concat operand's width)
   unsigned short* outb;       // fwd, nullable: write bf16(u) here (pixel stride ldo) instead of out
   int pair;                   // outb 4-byte aligned and ldo even: channel pairs stored as one 4-byte word
+  int w32;                    // fwd: W % 32 == 0 (a 32-pixel fragment never wraps an image row)
 };
 
 template <int WN>
@@ -236,22 +237,42 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
         // rows (r, r + 1); one xor-1 shuffle gives the even lane row r's pair and the odd lane row
         // r + 1's, so each stores 4 bytes (half the store instructions of 2-byte stores)
         const int odd = lane & 1;
+#define PMU_CT_PAIR(FM_, R_)                                                                                \
+  const unsigned b0 = __builtin_bit_cast(unsigned short, (__bf16)(acc[FM_][fn][R_] + b));                   \
+  const unsigned b1 = __builtin_bit_cast(unsigned short, (__bf16)(acc[FM_][fn][(R_) + 1] + b));             \
+  const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);                                  \
+  const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
 #pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
+        for (int fm = 0; fm < FM; ++fm) {
+          const int mf = m0 + wm * 128 + fm * 32;  // (uniform) the fragment's first input pixel
+          if (g.w32) {
+            // W % 32 == 0: the fragment's 32 pixels lie in one image row (it starts at a multiple of
+            // 32), so (n, i, j0) is decoded once per fragment (scalar) and pixel mf + x lands 2x output
+            // pixels further along the same output row — no per-store integer division
+            const unsigned t = (unsigned)mf / (unsigned)g.W, j0 = (unsigned)mf - t * (unsigned)g.W;
+            const unsigned n = t / (unsigned)g.H, i = t - n * (unsigned)g.H;
+            unsigned short* fp = outcb + ((long long)(n * 2 * g.H + 2 * i) * (2 * g.W) + 2 * j0) * ldo - odd;
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            const unsigned b0 = __builtin_bit_cast(unsigned short, (__bf16)(acc[fm][fn][r] + b));
-            const unsigned b1 = __builtin_bit_cast(unsigned short, (__bf16)(acc[fm][fn][r + 1] + b));
-            const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);
-            const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
-            const int m = m0 + wm * 128 + fm * 32 + acc_row(r + odd, lane);
-            if (m < g.M) {
-              const unsigned t = (unsigned)m / (unsigned)g.W, j = (unsigned)m - t * (unsigned)g.W;
-              const unsigned n = t / (unsigned)g.H, i = t - n * (unsigned)g.H;
-              const long long o = ((long long)(n * 2 * g.H + 2 * i) * (2 * g.W) + 2 * j) * ldo - odd;
-              *reinterpret_cast<unsigned*>(outcb + o) = pair;
+            for (int r = 0; r < 16; r += 2) {
+              PMU_CT_PAIR(fm, r)
+              const int x = acc_row(r + odd, lane);
+              if (mf + x < g.M) *reinterpret_cast<unsigned*>(fp + (unsigned)(2 * x) * (unsigned)ldo) = pair;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              PMU_CT_PAIR(fm, r)
+              const int m = mf + acc_row(r + odd, lane);
+              if (m < g.M) {
+                const unsigned t = (unsigned)m / (unsigned)g.W, j = (unsigned)m - t * (unsigned)g.W;
+                const unsigned n = t / (unsigned)g.H, i = t - n * (unsigned)g.H;
+                const long long o = ((long long)(n * 2 * g.H + 2 * i) * (2 * g.W) + 2 * j) * ldo - odd;
+                *reinterpret_cast<unsigned*>(outcb + o) = pair;
+              }
             }
           }
+        }
+#undef PMU_CT_PAIR
       } else {
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
@@ -277,6 +298,7 @@ template <bool DGRAD>
 static int launch(GArgs& g, void* stream) {
   const int wn = dma_wn(g.Ncols);
   const int BM = 128 * (NWV / wn), BN = 64 * wn;
+  g.w32 = (!DGRAD && g.W % 32 == 0) ? 1 : 0;
   g.nnb = g.Ncols / BN;
   const long long blocks = (long long)pmu_cdiv(g.M, BM) * g.nnb;
   PMU_REQUIRE(blocks < (1LL << 31));
