@@ -77,35 +77,24 @@ __device__ __forceinline__ unsigned short bf16_bits(float v) { return __builtin_
 
 // wp[jb][ch][tap][u][e]: unit u = swz(co, q) holds B[tap][k = 16 ch + 8 q + e][j = BN jb + co], zero
 // padded, bf16 RNE.  Forward: B[tap][ci][co] = w[co][ci][tap]; dgrad: B[tap][co][ci] = w[co][ci][8 - tap].
-// A thread packs one 16-B unit (its 8 k values) and stores it whole (2-byte stores per element ran
-// the per-step re-pack of c5's weights at 2 TB/s).
 __device__ __forceinline__ void pack_dma_body(const float* __restrict__ w, int Cout, int Cin, int dgrad, int BN,
                                               unsigned short* __restrict__ wp, int bid, int nblk) {
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
   const int nch = (KC + BK - 1) / BK, njb = (NOUT + BN - 1) / BN;
-  const long long units = (long long)njb * nch * 9 * 2 * BN;
-  for (long long e = (long long)bid * blockDim.x + threadIdx.x; e < units; e += (long long)nblk * blockDim.x) {
-    long long r = e;
+  const long long total = (long long)njb * nch * 9 * 2 * BN * 8;
+  for (long long e = (long long)bid * blockDim.x + threadIdx.x; e < total; e += (long long)nblk * blockDim.x) {
+    const int el = (int)(e & 7);
+    long long r = e >> 3;
     const int u = (int)(r % (2 * BN)); r /= 2 * BN;
     const int tap = (int)(r % 9); r /= 9;
     const int ch = (int)(r % nch);
     const int jb = (int)(r / nch);
     const int co = u >> 1, q = (u & 1) ^ ((co >> 3) & 1);
-    const int j = jb * BN + co, k0 = ch * BK + 8 * q;
-    unsigned pk[4];
-#pragma unroll
-    for (int el = 0; el < 8; el += 2) {
-      float v[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int k = k0 + el + i;
-        v[i] = 0.f;
-        if (j < NOUT && k < KC)
-          v[i] = dgrad ? w[((long long)k * Cin + j) * 9 + (8 - tap)] : w[((long long)j * Cin + k) * 9 + tap];
-      }
-      pk[el >> 1] = (unsigned)bf16_bits(v[0]) | ((unsigned)bf16_bits(v[1]) << 16);
-    }
-    *reinterpret_cast<uint4*>(wp + 8 * e) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    const int j = jb * BN + co, k = ch * BK + 8 * q + el;
+    float v = 0.f;
+    if (j < NOUT && k < KC)
+      v = dgrad ? w[((long long)k * Cin + j) * 9 + (8 - tap)] : w[((long long)j * Cin + k) * 9 + tap];
+    wp[e] = bf16_bits(v);
   }
 }
 __global__ __launch_bounds__(256) void pack_dma_kernel(const float* __restrict__ w, int Cout, int Cin, int dgrad, int BN,
@@ -616,8 +605,8 @@ extern "C" size_t pmu_conv3x3_packed_size_dma(int Cout, int Cin, int dgrad) {
 extern "C" int pmu_conv3x3_pack_dma(const float* w, int Cout, int Cin, int dgrad, unsigned short* wp, void* stream) {
   PMU_REQUIRE(w && wp && Cout > 0 && Cin > 0);
   const int NOUT = dgrad ? Cin : Cout, KC = dgrad ? Cout : Cin;
-  const long long units = (long long)(pmu_conv3x3_packed_size_dma(Cout, Cin, dgrad) / 16);
-  long long g = (units + 255) / 256;
+  const long long total = (long long)(pmu_conv3x3_packed_size_dma(Cout, Cin, dgrad) / sizeof(unsigned short));
+  long long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(pack_dma_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, w, Cout, Cin, dgrad,
                      dma_bn(NOUT, KC), wp);
@@ -689,8 +678,8 @@ extern "C" int pmu_conv3x3_dgrad_dma_bnr_zb(const unsigned short* dzt, int Cp, i
 #endif  // PMU_EXPERIMENTS
 
 static int pack_dma_grid(int Cout, int Cin, int dgrad) {
-  const long long units = (long long)(pmu_conv3x3_packed_size_dma(Cout, Cin, dgrad) / 16);  // (a thread per unit)
-  const long long g = (units + 255) / 256;
+  const long long total = (long long)(pmu_conv3x3_packed_size_dma(Cout, Cin, dgrad) / sizeof(unsigned short));
+  const long long g = (total + 255) / 256;
   return (int)(g > 4096 ? 4096 : g);
 }
 
