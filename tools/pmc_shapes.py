@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Per-shape HBM traffic of one kernel family from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE)
+of `tools/kbench.py --ops OP --iters I` (every shape launches 2 warm-up + I timed dispatches, in
+kbench's SHAPES order), next to the algorithmic bytes of the F(4x4) BN-backward input gradient
+(dgrad_w4b): dz read + dx written + the producer's z read + the packed U (36/9 of the filters).
+
+    python tools/pmc_shapes.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR ITERS [--N 32] > out.txt
+
+Bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 correction, tools/pmc_traffic.py)."""
+import argparse
+import csv
+import glob
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kbench import SHAPES  # noqa: E402
+
+
+def per_dispatch(d, counter, sub):
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter and sub in r["Kernel_Name"]:
+                k = int(r["Dispatch_Id"])
+                vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
+    return [vals[k] for k in sorted(vals)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("kernel")
+    ap.add_argument("iters", type=int)
+    ap.add_argument("--N", type=int, default=32)
+    a = ap.parse_args()
+    fe, wr = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel), per_dispatch(a.write, "WRITE_SIZE", a.kernel)
+    per = 2 + a.iters
+    assert len(fe) == len(wr) == per * len(SHAPES), (len(fe), len(wr), per * len(SHAPES))
+    print(f"{'H':>4} {'Cin':>5} {'Cout':>5} {'PMC MB':>9} {'alg MB':>9} {'ratio':>6}")
+    for s, (H, Cin, Cout) in enumerate(SHAPES):
+        idx = range(s * per + 2, (s + 1) * per)
+        hbm = sum((2 * fe[i] + wr[i]) * 1024 for i in idx) / a.iters
+        px = a.N * H * H
+        alg = px * Cout * 4 + px * Cin * 4 + px * Cin * 4 + Cin * Cout * 36 * 4
+        print(f"{H:4d} {Cin:5d} {Cout:5d} {hbm / 1e6:9.1f} {alg / 1e6:9.1f} {hbm / alg:6.2f}")
+
+
+if __name__ == "__main__":
+    main()
