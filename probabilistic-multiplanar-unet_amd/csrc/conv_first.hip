@@ -52,8 +52,9 @@ __device__ __forceinline__ void first_patch_load(const float* const (&planes)[4]
   }
 }
 
+// (three waves per SIMD fit the 9 * CIN weight pairs up to CIN = 3; CIN = 4 at that cap spilled 267 registers)
 template <int CIN>
-__global__ __launch_bounds__(256, 3) void conv_first_fwd_tile_kernel(FirstArgs a, int tiles_w, int tiles_h, int ntiles) {
+__global__ __launch_bounds__(256, CIN >= 4 ? 2 : 3) void conv_first_fwd_tile_kernel(FirstArgs a, int tiles_w, int tiles_h, int ntiles) {
   constexpr int PE = CIN * FT_PH * FT_PW, NPE = (PE + 255) / 256;
   __shared__ float patch[PE];
   __shared__ float red[256 * 8];
