@@ -46,7 +46,8 @@ def test_conv_first_wgrad_bnbwd(dev, N, Cin, H, W, Cout):
     assert err <= 1e-5 * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("N,Cin,H,W,Cout", [(2, 3, 37, 45, 64), (1, 1, 16, 64, 32)])
+@pytest.mark.parametrize("N,Cin,H,W,Cout", [(2, 3, 37, 45, 64), (1, 1, 16, 64, 32), (3, 4, 9, 70, 16),
+                                             (2, 4, 40, 33, 64), (1, 2, 24, 40, 64)])
 def test_conv_first_fwd(dev, N, Cin, H, W, Cout):
     import ctypes
     from pmu_hip import _lib as L
