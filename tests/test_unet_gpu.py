@@ -174,3 +174,34 @@ def test_unet_applied_twice_in_one_graph(dev):
     buf = net.__dict__["_pmu_grad_flat"]
     lo, hi = buf.data_ptr(), buf.data_ptr() + 4 * buf.numel()
     assert all(lo <= p.grad.data_ptr() < hi for p in net.parameters())
+
+
+def test_bn_cumulative_average_momentum_none(dev):
+    """nn.BatchNorm2d(momentum=None) keeps a cumulative average of the batch statistics: two training
+    forwards of the same batch leave running_mean / running_var at that batch's statistics — what
+    momentum=1.0 gives after one — and num_batches_tracked at 2 (the engine's host-side path; the
+    default momentum's counter is advanced by the finalize kernel, test_unet_train_step_parity)."""
+    from model import UNet
+    torch.manual_seed(0)
+    x = torch.rand(2, 1, 48, 40, generator=torch.Generator().manual_seed(5)).to(dev)
+    stats = []
+    for mom, passes in ((None, 2), (1.0, 1)):
+        torch.manual_seed(0)
+        net = UNet(1, 1, [8, 16, 32]).to(dev).train()
+        for m in net.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.momentum = mom
+        with torch.no_grad():
+            for _ in range(passes):
+                net(x)
+        torch.cuda.synchronize()
+        stats.append({k: v.detach().clone() for k, v in net.state_dict().items()})
+    cum, one = stats
+    n = 0
+    for k, v in cum.items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            assert max_abs(v, one[k]) <= 1e-5 * max(1.0, float(one[k].abs().max())), k
+            n += 1
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == 2 and int(one[k]) == 1, k
+    assert n >= 8
