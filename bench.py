@@ -5,7 +5,8 @@ metric : "2D slices/sec fwd+bwd, 256x256x1 batch32 U-Net; Dice vs ref"  (BASELIN
 step   : one training step of PMU/train.py:85-110 on one batch of synthetic 256x256x1 slices:
          UNet(1,1,[64,128,256,512,1024]) forward -> BCELoss -> backward -> (all-reduce) ->
          clip_grad_value_(0.1) + SGD(momentum 0.9), all on the HIP path (model.UNet + FusedSGD).
-N GPUs : one process per GPU (torch.distributed.run), 32 slices per GPU (weak scaling), one
+N GPUs : one process per GPU (torch.distributed.run; `--gpus N` outside torchrun starts the N ranks
+         itself as a child process), 32 slices per GPU (weak scaling), one
          RCCL all-reduce of the flat gradient buffer per step.
 
 Prints ONE JSON line on rank 0.  `roofline` is the dominant MFMA kernel family timed with HIP
@@ -75,6 +76,8 @@ class KernelTimer:
         """The call family of a fused variant: the BN-backward epilogue (_bnr), bf16-z (_zb), concat-split
         bf16 copy / column-sum (_x1b, _x1b_sum) and in-place concat (_ld, _ldb) forms take the same
         leading arguments and do the same MFMA work as the plain call."""
+        if name.endswith("_dxb"):   # bf16-dx storage of the same GEMM
+            name = name[:-4]
         for suf in ("_bnr_zb", "_x1b_sum", "_x1b", "_bnr", "_zb", "_ldb", "_ld"):
             if name.endswith(suf):
                 return name[: -len(suf)]
@@ -302,7 +305,7 @@ def cpu_leg(args, step):
         dvr = dice_vs_ref_probunet(step.net, *step.batch())
     # c2: BASELINE.md's protocol (batch 32, median of 3); c4 / c5 at a bounded batch (a batch-32 c4 or
     # batch-16 c5 step takes 30-40 s on the box's 16 host threads)
-    cpu_batch = {"unet": 32, "probunet": 8, "c5": 2}[args.workload] if args.batch >= 8 else args.batch
+    cpu_batch = {"unet": 32, "probunet": 32, "c5": 2}[args.workload] if args.batch >= 8 else args.batch
     cpu = cpu_baseline(workload="probunet" if args.workload == "probunet" else "unet", size=args.size,
                        channels=args.channels, classes=3 if args.workload == "probunet" else args.classes,
                        batch=cpu_batch)
@@ -415,6 +418,9 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_dgrad_dma_bnr_zb": r"conv3x3_dma_kernel<true",
     "pmu_convT2x2_fwd_dma": r"convT_dma_kernel<false", "pmu_convT2x2_dgrad_dma": r"convT_dma_kernel<true",
     "pmu_conv3x3_dgrad_dma_x1b": r"conv3x3_dma_kernel<true", "pmu_conv3x3_dgrad_dma_x1b_sum": r"conv3x3_dma_kernel<true",
+    "pmu_conv3x3_dgrad_dma_dxb": r"conv3x3_dma_kernel<true", "pmu_conv3x3_dgrad_dma_bnr_dxb": r"conv3x3_dma_kernel<true",
+    "pmu_conv3x3_dgrad_dma_x1b_dxb": r"conv3x3_dma_kernel<true",
+    "pmu_conv3x3_dgrad_dma_x1b_sum_dxb": r"conv3x3_dma_kernel<true",
     "pmu_convT2x2_fwd_ld": r"convT_pipe_kernel<false", "pmu_convT2x2_fwd_dma_ldb": r"convT_dma_kernel<false",
 }
 
@@ -679,6 +685,34 @@ def build_probunet(args, dev, world, rank):
     return step, None, config, data
 
 
+def launch_plan(gpus, argv, env):
+    """How to run ``bench.py --gpus N`` (pure host logic, no GPU call).
+
+    Returns None when this process is the rank to run (N == 1 outside torchrun, or any N under
+    torchrun with WORLD_SIZE == N), or the command list of a ``torch.distributed.run`` child that
+    starts N ranks of this script on this node (N > 1 outside torchrun) — the driver's own N-GPU
+    launch, one process per GPU, so ``--gpus N`` always measures N GPUs.  Raises ValueError when
+    ``--gpus`` disagrees with a torchrun world size: a run that would time a different number of GPUs
+    than it reports.  The child gets the same argv (``--gpus`` kept, so each rank re-checks it)."""
+    if gpus < 1:
+        raise ValueError(f"--gpus must be >= 1, got {gpus}")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise ValueError(f"--gpus {gpus} but WORLD_SIZE={world}: launch with --nproc-per-node {gpus} "
+                             f"or drop --gpus")
+        return None
+    if gpus == 1:
+        return None
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -699,6 +733,17 @@ def main():
     ap.add_argument("--no-eval", action="store_true", help="c5: skip the 3-view volume-fusion evaluation")
     ap.add_argument("--eval-size", type=int, default=512, help="c5 evaluation volume edge (D^3 voxels)")
     args = ap.parse_args()
+    try:
+        cmd = launch_plan(args.gpus, sys.argv[1:], os.environ)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        return 2
+    if cmd is not None:
+        # N ranks outside torchrun: start them as a child process (nothing here has touched the GPU;
+        # an exec from a GPU-initialised process is not allowed) and pass its exit code on; rank 0's
+        # JSON line reaches stdout through the inherited descriptor.
+        import subprocess
+        return subprocess.call(cmd)
     c5 = args.workload == "c5"
     if args.channels is None:
         args.channels = 3 if c5 else 1
@@ -818,7 +863,8 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

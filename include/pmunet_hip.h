@@ -204,6 +204,22 @@ int pmu_convT2x2_dbias_rows(const float* part, int R, long long ld, int Cout, fl
 int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
                               int Cin, float* dx, const float* z, const float* coef, const float* mean,
                               const float* invstd, float* part, void* stream);
+/* bf16 activation gradients (config c5, unet_parts.py:15,18 backward under torch.autocast(bfloat16),
+ * whose conv backward returns dx in bf16): the four input gradients above with dx / dx0 stored as
+ * bf16 (RNE) and every other output (dx1 values, dx1b, column sums, BN-backward partials) formed from
+ * the rounded values.  Cin % 8 == 0, Csplit % 8 == 0.  Consumers: pmu_frame_to_bf16 (BN-backward
+ * frames with a bf16 da), pmu_maxpool2_bwd_bnr_dxb, pmu_bn_bwd_reduce_dxb, pmu_conv_first_wgrad. */
+int pmu_conv3x3_dgrad_dma_dxb(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                              int Cin, int Csplit, unsigned short* dx0, float* dx1, void* stream);
+int pmu_conv3x3_dgrad_dma_x1b_dxb(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                  int Cin, int Csplit, unsigned short* dx0, float* dx1, unsigned short* dx1b,
+                                  void* stream);
+int pmu_conv3x3_dgrad_dma_x1b_sum_dxb(const unsigned short* dzt, int Cp, int N, int H, int W,
+                                      const unsigned short* wp, int Cin, int Csplit, unsigned short* dx0,
+                                      unsigned short* dx1b, float* part, void* stream);
+int pmu_conv3x3_dgrad_dma_bnr_dxb(const unsigned short* dzt, int Cp, int N, int H, int W, const unsigned short* wp,
+                                  int Cin, unsigned short* dx, const float* z, const float* coef, const float* mean,
+                                  const float* invstd, float* part, void* stream);
 /* The bf16 operand of a frame, materialised: out[N][H][W][Cpad] = bf16(frame value) (channels
  * >= C zero; Cpad % 4 == 0) — the BN+ReLU(+pool)(+concat) activation or the BN+ReLU backward dz
  * that pmu_conv3x3_wgrad_bf16 multiplies. */
@@ -259,6 +275,7 @@ int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, int H, int W,
                        void* stream);
 int pmu_conv_first_tiles(int N, int H, int W);
 size_t pmu_conv_first_wgrad_ws(int N, int H, int W, int Cin, int Cout);
+/* dz: one BN-backward (or raw) source; its da may be bf16-stored (a *_dxb input gradient's dx) */
 int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* planes, int Cin, int Cout,
                          float* dw, float* ws, size_t ws_bytes, void* stream);
 
@@ -280,6 +297,9 @@ int pmu_bn_eval_coef(const float* running_mean, const float* running_var, const 
 /* BN+ReLU backward reduction over da (NHWC) and z: part[tile][2][C] = (sum g, sum g*xhat). */
 int pmu_bn_bwd_reduce(const float* da, const float* z, const float* coef, const float* mean,
                       const float* invstd, int P, int C, float* part, void* stream);
+/* the same with da stored as bf16 (a *_dxb input gradient's dx); C % 4 == 0 */
+int pmu_bn_bwd_reduce_dxb(const unsigned short* da, const float* z, const float* coef, const float* mean,
+                          const float* invstd, int P, int C, float* part, void* stream);
 int pmu_bn_bwd_tiles(int P, int C);
 /* From acc[G][2][C]: dgamma, dbeta, dbias(conv bias feeding BN) and the BNBWD coef block
  * [scale|shift|mean|kx|kc]. */
@@ -304,6 +324,12 @@ int pmu_maxpool2_bwd_bnr_tiles(int N, int H, int W, int C);
 int pmu_maxpool2_bwd_bnr(const float* dpool, const float* z, const float* coef, const float* mean,
                          const float* invstd, int N, int H, int W, int C, float* dx, int accumulate,
                          float* part, void* stream);
+/* the same with dpool and the skip gradient stored as bf16 (the *_dxb input gradients' dx; skip
+ * nullable = no accumulation): dx (fp32, a separate tensor) = skip + routed dpool, summed in fp32 as
+ * autograd accumulates the skip activation's two gradients (unet_parts.py:33,66) */
+int pmu_maxpool2_bwd_bnr_dxb(const unsigned short* dpool, const unsigned short* skip, const float* z,
+                             const float* coef, const float* mean, const float* invstd, int N, int H, int W, int C,
+                             float* dx, float* part, void* stream);
 /* AvgPool2d(2,2,ceil_mode=True) backward: dx = dpool/count(window), overwrite. */
 int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream);
 /* The same (bit-equal dx, here da: N x H x W x C at the pooled layer's resolution) fused with the BN+ReLU

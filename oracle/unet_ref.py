@@ -41,6 +41,20 @@ def _dma_zb(x, cin, cout):
     return BF16_Z and x.shape[3] >= 32 and ((cin + 7) // 8 * 8) % 16 == 0 and cout % 8 == 0
 
 
+# torch.autocast(bfloat16)'s conv backward returns the input gradient in bf16.  BF16_DX models the HIP
+# path's storage of it (include/pmunet_hip.h *_dxb entries, engine CFG.dx_bf16, on by default): the
+# convs whose input gradient runs on the LDS-DMA kernel (maps >= 32 wide, pad8(Cout) % 16 == 0,
+# Cin % 8 == 0, a concat split on a 32-channel boundary) round dx to bf16 once (RNE), and everything
+# downstream (BN backward, max-pool routing, the skip-gradient sum in fp32, the transposed conv's
+# input gradient and bias gradient) sees the rounded values.  False: fp32 dx (PMU_DX_BF16=0).
+BF16_DX = True
+
+
+def _dma_dxb(x, cin, cout, split):
+    return (BF16_DX and x.shape[3] >= 32 and ((cout + 7) // 8 * 8) % 16 == 0 and cin % 8 == 0
+            and (split is None or split == cin or split % 32 == 0))
+
+
 def _round_centered(y, off):
     """bf16(y - off) + off per channel, gradient passed straight through (autocast's cast)."""
     o = off.to(y.dtype).view(1, -1, 1, 1)
@@ -51,13 +65,15 @@ class Bf16Conv3x3(torch.autograd.Function):
     """conv3x3(pad 1) with torch.autocast(bfloat16) arithmetic as the HIP bf16 kernels implement it
     (include/pmunet_hip.h, bf16 section): the operand x and the weights are rounded to bf16, the
     exact products summed in the ambient dtype; backward rounds the incoming gradient dy to bf16
-    once and forms dx = conv2d_input(rb(w), rb(dy)), dw = conv2d_weight(rb(x), rb(dy)), db = sum dy."""
+    once and forms dx = conv2d_input(rb(w), rb(dy)), dw = conv2d_weight(rb(x), rb(dy)), db = sum dy; with
+    ``round_dx`` (BF16_DX, the HIP path's *_dxb input gradient) dx itself is rounded to bf16 once."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, round_dx=False):
         xr, wr = _rb(x), _rb(w)
         ctx.save_for_backward(xr, wr)
         ctx.has_b = b is not None
+        ctx.round_dx = round_dx
         return F.conv2d(xr, wr, b, padding=1)
 
     @staticmethod
@@ -65,9 +81,11 @@ class Bf16Conv3x3(torch.autograd.Function):
         xr, wr = ctx.saved_tensors
         dyr = _rb(dy)
         dx = torch.nn.grad.conv2d_input(xr.shape, wr, dyr, padding=1)
+        if ctx.round_dx:
+            dx = _rb(dx)
         dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dyr, padding=1)
         db = dy.sum((0, 2, 3)) if ctx.has_b else None
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class Bf16ConvT2x2(torch.autograd.Function):
@@ -92,19 +110,21 @@ class Bf16ConvT2x2(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
-def _conv3x3(x, w, b, bf16):
-    return Bf16Conv3x3.apply(x, w, b) if bf16 else F.conv2d(x, w, b, padding=1)
+def _conv3x3(x, w, b, bf16, round_dx=False):
+    return Bf16Conv3x3.apply(x, w, b, round_dx) if bf16 else F.conv2d(x, w, b, padding=1)
 
 
-def double_conv(x, sd, pre, training, bf16=False, first_fp32=False):
+def double_conv(x, sd, pre, training, bf16=False, first_fp32=False, split=None, dxb=False):
     """(conv3x3 pad1 -> BN -> ReLU) x 2  (unet_parts.py:14-21); Sequential indices 0,1,3,4.
     bf16: the autocast arithmetic of Bf16Conv3x3 (first_fp32 keeps the first conv in fp32, as the
-    HIP path's Cin <= 4 first-layer kernel)."""
+    HIP path's Cin <= 4 first-layer kernel).  dxb: the block sits inside the UNet's backward, where the
+    HIP path keeps bf16 activation gradients (BF16_DX); split: the first conv's concat split."""
     for i in (0, 3):
         use = bf16 and not (first_fp32 and i == 0)
         w = sd[f"{pre}double_conv.{i}.weight"]
         zb = use and _dma_zb(x, w.shape[1], w.shape[0])
-        x = _conv3x3(x, w, sd[f"{pre}double_conv.{i}.bias"], use)
+        rdx = use and dxb and _dma_dxb(x, w.shape[1], w.shape[0], split if i == 0 else None)
+        x = _conv3x3(x, w, sd[f"{pre}double_conv.{i}.bias"], use, rdx)
         if zb:
             x = _round_centered(x, sd[f"{pre}double_conv.{i + 1}.running_mean"].clone())
         x = F.relu(_bn(x, sd, f"{pre}double_conv.{i + 1}.", training))
@@ -119,9 +139,10 @@ def unet_forward(sd, x, n_levels, n_classes, apply_last_layer=True, training=Tru
     (unet_parts.py:52,58-66); up_blocks stored deepest-first (unet_model.py:29); skip of up
     block i is xs[-(2 + 2i)] (:39).  bf16: every 3x3 conv but a Cin <= 4 first one in Bf16Conv3x3
     arithmetic (the HIP path's autocast mode)."""
-    xs = [double_conv(x, sd, "inc.", training, bf16, first_fp32=x.shape[1] <= 4)]
+    xs = [double_conv(x, sd, "inc.", training, bf16, first_fp32=x.shape[1] <= 4, dxb=True)]
     for i in range(n_levels - 1):
-        xs.append(double_conv(F.max_pool2d(xs[-1], 2), sd, f"down_blocks.{i}.maxpool_conv.1.", training, bf16))
+        xs.append(double_conv(F.max_pool2d(xs[-1], 2), sd, f"down_blocks.{i}.maxpool_conv.1.", training, bf16,
+                              dxb=True))
     for i in range(n_levels - 1):
         x1, x2 = xs[-1], xs[-(2 + 2 * i)]
         pre = f"up_blocks.{i}."
@@ -134,7 +155,8 @@ def unet_forward(sd, x, n_levels, n_classes, apply_last_layer=True, training=Tru
             x1 = F.conv_transpose2d(x1, wt, sd[pre + "up.bias"], stride=2)
         dy, dx = x2.shape[2] - x1.shape[2], x2.shape[3] - x1.shape[3]
         x1 = F.pad(x1, [dx // 2, dx - dx // 2, dy // 2, dy - dy // 2])
-        xs.append(double_conv(torch.cat([x2, x1], dim=1), sd, pre + "conv.", training, bf16))
+        xs.append(double_conv(torch.cat([x2, x1], dim=1), sd, pre + "conv.", training, bf16, split=x2.shape[1],
+                              dxb=True))
     feat = xs[-1]
     if not apply_last_layer:
         return feat

@@ -94,8 +94,8 @@ __global__ void bn_eval_coef_kernel(const float* rm, const float* rv, const floa
 // ---------------- BN + ReLU backward reduction ----------------
 // part[tile][2][C] = (sum g, sum g*xhat), g = da * (z*scale+shift > 0), xhat = (z-mean)*invstd
 constexpr int BNR_BYTES = 65536;  // bytes of one tensor per block
-template <class ZT>  // z stored as float or bf16 (unsigned short)
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ da, const ZT* __restrict__ z,
+template <class ZT, class DT = float>  // z / da stored as float or bf16 (unsigned short)
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const DT* __restrict__ da, const ZT* __restrict__ z,
                                                             const float* __restrict__ coef, const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, long long P, int C,
                                                             int ppb, float* __restrict__ part) {
@@ -121,12 +121,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
       // the block's pixels of this thread, in order; unrolled so 8 loads are in flight per thread
       const long long pend = min(P, p0 + ppb);
       const int nit = pend > p0 + pg ? (int)((pend - p0 - pg + npg - 1) / npg) : 0;
-      const float* dp = da + (p0 + pg) * C + c;
+      const DT* dp = da + (p0 + pg) * C + c;
       const ZT* zp = z + (p0 + pg) * C + c;
       const long long step = (long long)npg * C;
 #pragma unroll 4
       for (int it = 0; it < nit; ++it) {
-        const float4 d = *reinterpret_cast<const float4*>(dp + it * step);
+        const float4 d = pmu_ld4(dp + it * step);
         const float4 zz = pmu_ld4(zp + it * step);
         const float dv[4] = {d.x, d.y, d.z, d.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
         const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
@@ -398,9 +398,12 @@ struct MpWin {
   float4 z[4], d[4], g;
 };
 
-template <bool ACC>
-__device__ __forceinline__ void mp_load(const float* __restrict__ dpool, const float* __restrict__ z,
-                                        const float* __restrict__ dx, long long wi, int H, int W, int C, int c,
+// DT: storage of dpool and of the accumulated skip gradient (float, or bf16 as unsigned short: the
+// *_dxb input gradients' dx; the sum is formed and written in fp32, torch.autocast's gradient
+// accumulation of the skip activation)
+template <bool ACC, class DT = float>
+__device__ __forceinline__ void mp_load(const DT* __restrict__ dpool, const float* __restrict__ z,
+                                        const DT* __restrict__ dx, long long wi, int H, int W, int C, int c,
                                         MpWin& m) {
   const int Hp = H / 2, Wp = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
   const int wc = (int)(wi % Wc);
@@ -412,10 +415,10 @@ __device__ __forceinline__ void mp_load(const float* __restrict__ dpool, const f
     const int h = min(2 * hc + (k >> 1), H - 1), w = min(2 * wc + (k & 1), W - 1);
     const long long off = (((long long)n * H + h) * W + w) * C + c;
     m.z[k] = *reinterpret_cast<const float4*>(z + off);
-    if (ACC) m.d[k] = *reinterpret_cast<const float4*>(dx + off);
+    if (ACC) m.d[k] = pmu_ld4(dx + off);
   }
   const long long po = (((long long)n * Hp + min(hc, Hp - 1)) * Wp + min(wc, Wp - 1)) * C + c;
-  m.g = *reinterpret_cast<const float4*>(dpool + po);
+  m.g = pmu_ld4(dpool + po);
 }
 
 template <bool ACC>
@@ -469,14 +472,15 @@ __device__ __forceinline__ void mp_route(const MpWin& m, long long wi, bool vali
   }
 }
 
-template <bool ACC>
-__global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __restrict__ dpool,
+// base: the skip gradient accumulated into (ACC; dx itself for fp32, a bf16 tensor for DT = bf16)
+template <bool ACC, class DT = float>
+__global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const DT* __restrict__ dpool,
                                                                const float* __restrict__ z,
                                                                const float* __restrict__ coef,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ invstd, int N, int H, int W,
                                                                int C, int wpb, float* __restrict__ dx,
-                                                               float* __restrict__ part) {
+                                                               float* __restrict__ part, const DT* __restrict__ base) {
   __shared__ float red[256 * 8];
   const int tid = threadIdx.x;
   const int CQ = C >> 2;
@@ -503,14 +507,14 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const float* __re
       const long long last = wend - 1;
       MpWin A, B;
       long long wi = w0 + pg;
-      mp_load<ACC>(dpool, z, dx, min(wi, last), H, W, C, c, A);
+      mp_load<ACC>(dpool, z, base, min(wi, last), H, W, C, c, A);
       for (; wi < wend; wi += 2 * npg) {
         const long long wb = wi + npg, wa = wi + 2 * npg;
-        mp_load<ACC>(dpool, z, dx, min(wb, last), H, W, C, c, B);
+        mp_load<ACC>(dpool, z, base, min(wb, last), H, W, C, c, B);
         __builtin_amdgcn_sched_barrier(0);
         mp_route<ACC>(A, wi, true, H, W, C, c, scv, shv, muv, isv, dx, sg, sgx);
         __builtin_amdgcn_sched_barrier(0);
-        mp_load<ACC>(dpool, z, dx, min(wa, last), H, W, C, c, A);
+        mp_load<ACC>(dpool, z, base, min(wa, last), H, W, C, c, A);
         __builtin_amdgcn_sched_barrier(0);
         mp_route<ACC>(B, min(wb, last), wb < wend, H, W, C, c, scv, shv, muv, isv, dx, sg, sgx);
         __builtin_amdgcn_sched_barrier(0);
@@ -1356,6 +1360,17 @@ extern "C" int pmu_bn_bwd_reduce(const float* da, const float* z, const float* c
   return PMU_OK;
 }
 
+// da stored as bf16 (the *_dxb input gradients' dx)
+extern "C" int pmu_bn_bwd_reduce_dxb(const unsigned short* da, const float* z, const float* coef, const float* mean,
+                                     const float* invstd, int P, int C, float* part, void* stream) {
+  PMU_REQUIRE(da && z && coef && mean && invstd && part && P > 0 && C > 0 && C % 4 == 0);
+  const int ppb = bn_bwd_ppb(C);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<float, unsigned short>), dim3((unsigned)pmu_cdiv(P, ppb)), dim3(256), 0,
+                     (hipStream_t)stream, da, z, coef, mean, invstd, (long long)P, C, ppb, part);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
 #ifdef PMU_EXPERIMENTS
 // bf16-stored z (experiments build only: it breaks the c5 Dice contract)
 extern "C" int pmu_bn_bwd_reduce_zb(const float* da, const unsigned short* z, const float* coef, const float* mean,
@@ -1438,10 +1453,29 @@ extern "C" int pmu_maxpool2_bwd_bnr(const float* dpool, const float* z, const fl
   const int R = pmu_maxpool2_bwd_bnr_tiles(N, H, W, C);
   if (accumulate)
     hipLaunchKernelGGL(maxpool2_bwd_bnr_kernel<true>, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dpool, z,
-                       coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part);
+                       coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part, (const float*)dx);
   else
     hipLaunchKernelGGL(maxpool2_bwd_bnr_kernel<false>, dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dpool, z,
-                       coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part);
+                       coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part, (const float*)nullptr);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+// As pmu_maxpool2_bwd_bnr with the pooled gradient and the skip gradient stored as bf16 (the *_dxb
+// input gradients' dx): da = skip + routed dpool formed in fp32 and written to dx (a separate fp32
+// tensor); skip null: da = the routed dpool alone.
+extern "C" int pmu_maxpool2_bwd_bnr_dxb(const unsigned short* dpool, const unsigned short* skip, const float* z,
+                                        const float* coef, const float* mean, const float* invstd, int N, int H,
+                                        int W, int C, float* dx, float* part, void* stream) {
+  PMU_REQUIRE(dpool && z && coef && mean && invstd && dx && part && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
+  const int R = pmu_maxpool2_bwd_bnr_tiles(N, H, W, C);
+  if (skip)
+    hipLaunchKernelGGL((maxpool2_bwd_bnr_kernel<true, unsigned short>), dim3((unsigned)R), dim3(256), 0,
+                       (hipStream_t)stream, dpool, z, coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part, skip);
+  else
+    hipLaunchKernelGGL((maxpool2_bwd_bnr_kernel<false, unsigned short>), dim3((unsigned)R), dim3(256), 0,
+                       (hipStream_t)stream, dpool, z, coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part,
+                       (const unsigned short*)nullptr);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -122,7 +122,13 @@ __global__ __launch_bounds__(256) void pack_dma_multi_kernel(const pmu_pack_job*
 // CS (input gradient): per-tile column sums of dx into a.part instead of the BN-backward partials
 // (pmu_conv3x3_dgrad_dma_x1b_sum; a compile-time variant: as a runtime branch beside the a.bz one it
 // spilled 89 VGPRs)
-template <bool DGRAD, bool ZB, int WN, int NWV, int EXP = 0, bool CS = false>
+// XB (input gradient, the *_dxb entries): dx rounded to bf16 (RNE) as torch.autocast's conv backward
+// returns it, before anything is formed from it — dx0 stored as bf16 (out0 holds 2-byte values), dx1
+// (fp32 storage, when requested) holding the rounded values, the bf16 copy, column sums and the
+// producer's BN-backward partials all taken from the rounded values.  Halves the bytes of the
+// activation-gradient stream its consumers (the BN-backward dz stream, the max-pool backward, the
+// first layer's weight gradient) read.
+template <bool DGRAD, bool ZB, int WN, int NWV, int EXP = 0, bool CS = false, bool XB = false>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs a) {
   using G = DG<WN, NWV>;
   constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH, NT = G::NT;
@@ -342,6 +348,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     // accumulators and the z under them, a row at a time.  z loads interleaved with the stores made
     // every consumption of a z value wait for all earlier stores (vmcnt counts both, in order); the
     // straight-line masked form of the forward above spilled 18-140 VGPRs here.
+    // (XB: each use rounds its accumulator, rb() below; rounding all 128 up front spilled 7 VGPRs)
+    auto rb = [](float v) { return XB ? pmu_round_bf16(v) : v; };
   #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       s1[fn] = 0.f;
@@ -352,8 +360,11 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       float* dstp;
       int ld;
       unsigned short* dstb = nullptr;  // (uniform per fragment)
-      if (jb < a.split) { dstp = a.out0 + j; ld = a.split; }
-      else {  // (out1 null: only the bf16 copy, pmu_conv3x3_dgrad_dma_x1b_sum)
+      if (jb < a.split) {
+        ld = a.split;
+        if constexpr (XB) { dstp = nullptr; dstb = reinterpret_cast<unsigned short*>(a.out0) + j; }
+        else dstp = a.out0 + j;
+      } else {  // (out1 null: only the bf16 copy, pmu_conv3x3_dgrad_dma_x1b_sum)
         dstp = a.out1 ? a.out1 + (j - a.split) : nullptr;
         ld = a.NOUT - a.split;
         if (a.out1b) dstb = a.out1b + (j - a.split);
@@ -379,12 +390,13 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
             *reinterpret_cast<unsigned*>(dstb + pix * ld - odd) = pair;
           }
         }
-        if (CS && !dstp) continue;  // (only the CS variant has a null out1: its dx1 is the bf16 copy alone)
+        // (only CS has a null out1, its dx1 the bf16 copy alone; XB's dx0 is the bf16 store above)
+        if ((CS || XB) && !dstp) continue;
         if ((ld & 1) == 0) {  // (uniform) fp32 dx as 8-byte channel pairs, as the bf16 copy above
           const int odd = lane & 1;
   #pragma unroll
           for (int r = 0; r < 16; r += 2) {
-            const float v0 = acc[fm][fn][r], v1 = acc[fm][fn][r + 1];
+            const float v0 = rb(acc[fm][fn][r]), v1 = rb(acc[fm][fn][r + 1]);
             const float recv = __shfl_xor(odd ? v0 : v1, 1, 64);
             const float2 pv = odd ? make_float2(recv, v1) : make_float2(v0, recv);
             const int w = w0 + acc_row(r + odd, lane);
@@ -401,7 +413,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
           if (!jok || h >= a.H || w >= a.W) continue;
           const long long pix = ((long long)n * a.H + h) * a.W + w;
           PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-          dstp[pix * ld] = acc[fm][fn][r];
+          dstp[pix * ld] = rb(acc[fm][fn][r]);
         }
       }
     }
@@ -426,7 +438,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
           for (int r = 0; r < 16; ++r) {
             const int w = w0 + acc_row(r, lane);
             const bool ok = jok && h < a.H && w < a.W;
-            const float gg = (ok && fmaf(zt[r], bsc, bsh) > 0.f) ? acc[fm][fn][r] : 0.f;
+            const float gg = (ok && fmaf(zt[r], bsc, bsh) > 0.f) ? rb(acc[fm][fn][r]) : 0.f;
             s1[fn] += gg;
             s2[fn] = fmaf(gg, (zt[r] - bmu) * bis, s2[fn]);
           }
@@ -442,7 +454,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
   #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const bool ok = jok && h < a.H && w0 + acc_row(r, lane) < a.W;
-            s1[fn] += ok ? acc[fm][fn][r] : 0.f;
+            s1[fn] += ok ? rb(acc[fm][fn][r]) : 0.f;
           }
         }
       }
@@ -500,9 +512,11 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
                       int NOUT, float* out0, float* out1, int split, float* part, bool dgrad, void* stream,
                       const float* bz = nullptr, const float* bcoef = nullptr, const float* bmean = nullptr,
                       const float* binv = nullptr, int zbf = 0, const float* zoff = nullptr,
-                      unsigned short* out1b = nullptr) {
+                      unsigned short* out1b = nullptr, bool xb = false) {
   PMU_REQUIRE(x && wp && out0 && N > 0 && H > 0 && W >= 32 && Cp > 0 && Cp % BK == 0 && NOUT > 0);
   PMU_REQUIRE(!out1b || dgrad);
+  // bf16 dx: its channel pairs never straddle the split or the end (4-byte pair stores)
+  PMU_REQUIRE(!xb || (dgrad && zbf == 0 && NOUT % 8 == 0 && split % 8 == 0));
   PMU_REQUIRE(!dgrad || split == NOUT || (split % 32 == 0 && split < NOUT && (out1 || out1b)));
   const Shape sh = dma_shape(NOUT, Cp);
   const long long img_bytes = (long long)H * W * Cp * 2;
@@ -512,13 +526,14 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
       const long long px = (long long)n0 * H * W;
       // bf16 z (forward output / input-gradient bz): element offsets of 2-byte values
       float* o0 = (!dgrad && zbf == 1) ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(out0) + px * NOUT)
-                                  : out0 + px * (dgrad ? split : NOUT);
+                  : xb ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(out0) + px * split)
+                       : out0 + px * (dgrad ? split : NOUT);
       const float* bzc = !bz ? nullptr
                              : zbf == 1 ? reinterpret_cast<const float*>(reinterpret_cast<const unsigned short*>(bz) + px * NOUT)
                                    : bz + px * NOUT;
       return launch_dma(x + px * Cp, Cp, nn, H, W, wp, bias, NOUT, o0, out1 ? out1 + px * (NOUT - split) : nullptr,
                         split, part ? part + (long long)n0 * tiles * 2 * NOUT : nullptr, dgrad, stream, bzc, bcoef,
-                        bmean, binv, zbf, zoff, out1b ? out1b + px * (NOUT - split) : nullptr);
+                        bmean, binv, zbf, zoff, out1b ? out1b + px * (NOUT - split) : nullptr, xb);
     });
   }
   DmaArgs a;
@@ -537,15 +552,15 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   const dim3 grid((unsigned)blocks), blk(64 * sh.nwv);
   const bool zb = zbf == 1;
 #ifdef PMU_EXPERIMENTS
-#define PMU_DMA_TALL_LAUNCH(D, Z, CSV) \
-  else if (sh.wn == 1 && sh.nwv == 8) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 8, 0, CSV>), grid, blk, 0, st, a);
+#define PMU_DMA_TALL_LAUNCH(D, Z, CSV, XBV) \
+  else if (sh.wn == 1 && sh.nwv == 8) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 8, 0, CSV, XBV>), grid, blk, 0, st, a);
 #else
-#define PMU_DMA_TALL_LAUNCH(D, Z, CSV)
+#define PMU_DMA_TALL_LAUNCH(D, Z, CSV, XBV)
 #endif
 #define PMU_DMA_LAUNCH(D, Z)                                                                              \
   {                                                                                                       \
     if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 4>), grid, blk, 0, st, a); \
-    PMU_DMA_TALL_LAUNCH(D, Z, false)                                                                      \
+    PMU_DMA_TALL_LAUNCH(D, Z, false, false)                                                               \
     else hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 2, 8>), grid, blk, 0, st, a);                       \
   }
 #ifdef PMU_EXPERIMENTS
@@ -568,9 +583,19 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   }
 #endif
   if (dgrad && part && !bz) {  // column sums (pmu_conv3x3_dgrad_dma_x1b_sum)
-    if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true>), grid, blk, 0, st, a);
-    PMU_DMA_TALL_LAUNCH(true, false, true)
-    else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, true>), grid, blk, 0, st, a);
+    if (xb) {
+      if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true, true>), grid, blk, 0, st, a);
+      PMU_DMA_TALL_LAUNCH(true, false, true, true)
+      else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, true, true>), grid, blk, 0, st, a);
+    } else {
+      if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true>), grid, blk, 0, st, a);
+      PMU_DMA_TALL_LAUNCH(true, false, true, false)
+      else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, true>), grid, blk, 0, st, a);
+    }
+  } else if (dgrad && xb) {  // bf16 dx (the *_dxb entries)
+    if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, false, true>), grid, blk, 0, st, a);
+    PMU_DMA_TALL_LAUNCH(true, false, false, true)
+    else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, false, true>), grid, blk, 0, st, a);
   }
 #ifdef PMU_EXPERIMENTS
   else if (dgrad && zb) PMU_DMA_LAUNCH(true, true)
@@ -652,6 +677,41 @@ extern "C" int pmu_conv3x3_dgrad_dma_bnr(const unsigned short* dzt, int Cp, int 
                                          const float* invstd, float* part, void* stream) {
   PMU_REQUIRE(z && coef && mean && invstd && part);
   return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, dx, nullptr, Cin, part, true, stream, z, coef, mean, invstd);
+}
+
+// bf16 dx (XB above): as the entries without the _dxb suffix, with dx / dx0 stored as bf16 (RNE, the
+// dtype torch.autocast's conv backward returns) and every other output formed from the rounded values.
+// Cin % 8 == 0, Csplit % 8 == 0.
+extern "C" int pmu_conv3x3_dgrad_dma_dxb(const unsigned short* dzt, int Cp, int N, int H, int W,
+                                         const unsigned short* wp, int Cin, int Csplit, unsigned short* dx0,
+                                         float* dx1, void* stream) {
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, reinterpret_cast<float*>(dx0), dx1, Csplit, nullptr, true,
+                    stream, nullptr, nullptr, nullptr, nullptr, 0, nullptr, nullptr, true);
+}
+
+extern "C" int pmu_conv3x3_dgrad_dma_x1b_dxb(const unsigned short* dzt, int Cp, int N, int H, int W,
+                                             const unsigned short* wp, int Cin, int Csplit, unsigned short* dx0,
+                                             float* dx1, unsigned short* dx1b, void* stream) {
+  PMU_REQUIRE(dx1 && dx1b && Csplit < Cin && (Cin - Csplit) % 8 == 0);
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, reinterpret_cast<float*>(dx0), dx1, Csplit, nullptr, true,
+                    stream, nullptr, nullptr, nullptr, nullptr, 0, nullptr, dx1b, true);
+}
+
+extern "C" int pmu_conv3x3_dgrad_dma_x1b_sum_dxb(const unsigned short* dzt, int Cp, int N, int H, int W,
+                                                 const unsigned short* wp, int Cin, int Csplit, unsigned short* dx0,
+                                                 unsigned short* dx1b, float* part, void* stream) {
+  PMU_REQUIRE(dx1b && part && Csplit < Cin && (Cin - Csplit) % 8 == 0);
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, reinterpret_cast<float*>(dx0), nullptr, Csplit, part, true,
+                    stream, nullptr, nullptr, nullptr, nullptr, 0, nullptr, dx1b, true);
+}
+
+extern "C" int pmu_conv3x3_dgrad_dma_bnr_dxb(const unsigned short* dzt, int Cp, int N, int H, int W,
+                                             const unsigned short* wp, int Cin, unsigned short* dx, const float* z,
+                                             const float* coef, const float* mean, const float* invstd, float* part,
+                                             void* stream) {
+  PMU_REQUIRE(z && coef && mean && invstd && part);
+  return launch_dma(dzt, Cp, N, H, W, wp, nullptr, Cin, reinterpret_cast<float*>(dx), nullptr, Cin, part, true, stream,
+                    z, coef, mean, invstd, 0, nullptr, nullptr, true);
 }
 
 #ifdef PMU_EXPERIMENTS

@@ -190,7 +190,8 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_kernel(FirstWgArgs a) {
 // float4 loads of da and z (BN-backward coefficients of the thread's channel quad in registers).
 constexpr int FW_TPB = 16;  // tiles per block
 
-template <int CIN>
+// XB: da stored as bf16 (the second conv's *_dxb input gradient)
+template <int CIN, bool XB = false>
 __global__ __launch_bounds__(256) void conv_first_wgrad_tile_kernel(FirstWgArgs a, int tiles_w, int tiles_h,
                                                                     int ntiles) {
   constexpr int K9 = CIN * 9, PE = CIN * FT_PH * FT_PW, NPE = (PE + 255) / 256;
@@ -236,7 +237,8 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_tile_kernel(FirstWgArgs 
   auto issue = [&](int j, int slot) {
     size_t p; int r, cc; bool ok;
     pixel_of(j, p, r, cc, ok);
-    dq[slot] = *reinterpret_cast<const float4*>(s.x + p * Cout + c);
+    dq[slot] = XB ? pmu_ld4(reinterpret_cast<const unsigned short*>(s.x) + p * Cout + c)
+                  : *reinterpret_cast<const float4*>(s.x + p * Cout + c);
     zq[slot] = *reinterpret_cast<const float4*>(s.z + p * Cout + c);
   };
   auto consume = [&](int j, int slot) {
@@ -375,7 +377,9 @@ extern "C" size_t pmu_conv_first_wgrad_ws(int N, int H, int W, int Cin, int Cout
 
 extern "C" int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* planes, int Cin, int Cout,
                                     float* dw, float* ws, size_t ws_bytes, void* stream) {
-  PMU_REQUIRE(valid_frame(dz) && dz->nsrc == 1 && dz->src[0].C == Cout && planes && dw && ws);
+  // (dz's da may be bf16-stored: the tiled kernel below takes it, the generic one reads through src_xform)
+  PMU_REQUIRE(valid_frame(dz, true) && dz->nsrc == 1 && dz->src[0].C == Cout && planes && dw && ws);
+  PMU_REQUIRE((dz->src[0].dtype & PMU_DT_Z_BF16) == 0);
   PMU_REQUIRE(Cin >= 1 && Cin <= 4 && Cout >= 1 && Cout <= 256 && 256 % Cout == 0);
   PMU_REQUIRE(ws_bytes >= pmu_conv_first_wgrad_ws(dz->N, dz->H, dz->W, Cin, Cout));
   FirstWgArgs a;
@@ -390,12 +394,16 @@ extern "C" int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* pla
     const int tw = pmu_cdiv(dz->W, FT_W), th = pmu_cdiv(dz->H, FT_H), nt = dz->N * tw * th;
     PMU_REQUIRE(P < (1LL << 31));
     nb = pmu_cdiv(nt, FW_TPB);
-    switch (Cin) {
-      case 1: hipLaunchKernelGGL(conv_first_wgrad_tile_kernel<1>, dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break;
-      case 2: hipLaunchKernelGGL(conv_first_wgrad_tile_kernel<2>, dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break;
-      case 3: hipLaunchKernelGGL(conv_first_wgrad_tile_kernel<3>, dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break;
-      default: hipLaunchKernelGGL(conv_first_wgrad_tile_kernel<4>, dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break;
-    }
+#define PMU_FW_LAUNCH(XBV)                                                                                         \
+  switch (Cin) {                                                                                                  \
+    case 1: hipLaunchKernelGGL((conv_first_wgrad_tile_kernel<1, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
+    case 2: hipLaunchKernelGGL((conv_first_wgrad_tile_kernel<2, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
+    case 3: hipLaunchKernelGGL((conv_first_wgrad_tile_kernel<3, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
+    default: hipLaunchKernelGGL((conv_first_wgrad_tile_kernel<4, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
+  }
+    if (dz->src[0].dtype & PMU_DT_X_BF16) PMU_FW_LAUNCH(true)
+    else PMU_FW_LAUNCH(false)
+#undef PMU_FW_LAUNCH
   } else {
     nb = pmu_cdiv(P, FWPIX);
     hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, a);

@@ -338,10 +338,13 @@ struct StreamArgs {
   int ldo2;
 };
 
-template <int MODE, bool POOL>
+// XB (BNBWD only): x (the activation gradient da) stored as bf16 — one 16-B load of its 8 channels
+// (xb), converted when the step is stored; v[0], v[1] then hold z
+template <int MODE, bool POOL, bool XB = false>
 struct StreamLd {
-  static constexpr int NV = POOL ? 8 : (MODE == PMU_SRC_BNBWD ? 4 : 2);
+  static constexpr int NV = POOL ? 8 : (MODE == PMU_SRC_BNBWD ? (XB ? 2 : 4) : 2);
   float4 v[NV];
+  uint4 xb;
 };
 
 typedef float stream_f4 __attribute__((ext_vector_type(4)));
@@ -355,9 +358,20 @@ __device__ __forceinline__ float4 stream_ld4(const float* p) {
   return pmu_ld4(p);
 }
 
-template <int MODE, bool POOL, int NT>
-__device__ __forceinline__ void stream_load(const StreamArgs& a, unsigned p, int c, StreamLd<MODE, POOL>& d) {
-  if (!POOL) {
+template <int MODE, bool POOL, int NT, bool XB = false>
+__device__ __forceinline__ void stream_load(const StreamArgs& a, unsigned p, int c, StreamLd<MODE, POOL, XB>& d) {
+  if (XB) {  // (BNBWD, unpooled)
+    const size_t o = (size_t)p * a.C + c;
+    const uint4* xp = reinterpret_cast<const uint4*>(reinterpret_cast<const unsigned short*>(a.x) + o);
+    if (NT & 1) {
+      const stream_u4 v = __builtin_nontemporal_load(reinterpret_cast<const stream_u4*>(xp));
+      d.xb = make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+      d.xb = *xp;
+    }
+    d.v[0] = stream_ld4<NT>(a.z + o);
+    d.v[1] = stream_ld4<NT>(a.z + o + 4);
+  } else if (!POOL) {
     const size_t o = (size_t)p * a.C + c;
     d.v[0] = stream_ld4<NT>(a.x + o);
     d.v[1] = stream_ld4<NT>(a.x + o + 4);
@@ -418,7 +432,7 @@ __device__ __forceinline__ void stream_st8(void* out, size_t e, float4 r0, float
 // SKIP (POOL only, even source dims): the four values of each window also written unpooled to out2 —
 // the skip half of the Up block's concat operand, made in the same pass as the max-pooled operand of
 // the next level's first conv (one read of the activation instead of two)
-template <int MODE, bool POOL, bool BF, int U, int NT, bool SKIP = false>
+template <int MODE, bool POOL, bool BF, int U, int NT, bool SKIP = false, bool XB = false>
 __global__ __launch_bounds__(256) void frame_stream_kernel(StreamArgs a) {
   const int tid = threadIdx.x;
   const int c = 8 * (tid & ((1 << a.lg) - 1));
@@ -443,12 +457,12 @@ __global__ __launch_bounds__(256) void frame_stream_kernel(StreamArgs a) {
   // loads of step s+1 are in flight while step s stores.  Loads are unconditional, the pixel clamped
   // to the last one (a load under a branch makes the compiler wait for every outstanding load before
   // the first store), and the loop runs on the block's uniform base.
-  StreamLd<MODE, POOL> A[U], B[U];
-  auto load = [&](StreamLd<MODE, POOL>* d, unsigned base) {
+  StreamLd<MODE, POOL, XB> A[U], B[U];
+  auto load = [&](StreamLd<MODE, POOL, XB>* d, unsigned base) {
 #pragma unroll
-    for (int j = 0; j < U; ++j) stream_load<MODE, POOL, NT>(a, min(base + pr + j * pb, plast), c, d[j]);
+    for (int j = 0; j < U; ++j) stream_load<MODE, POOL, NT, XB>(a, min(base + pr + j * pb, plast), c, d[j]);
   };
-  auto store = [&](const StreamLd<MODE, POOL>* d, unsigned base) {
+  auto store = [&](const StreamLd<MODE, POOL, XB>* d, unsigned base) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       // past the end: the clamped pixel's own value rewritten to it (identical bytes), so the stores
@@ -469,6 +483,11 @@ __global__ __launch_bounds__(256) void frame_stream_kernel(StreamArgs a) {
           r[k] = m;
         } else if (MODE == PMU_SRC_BNRELU) {
           r[k] = bnrelu4(d[j].v[k], sc[k], sh[k]);
+        } else if (MODE == PMU_SRC_BNBWD && XB) {
+          const unsigned u0 = k ? d[j].xb.z : d[j].xb.x, u1 = k ? d[j].xb.w : d[j].xb.y;
+          const float4 xv = make_float4(__uint_as_float(u0 << 16), __uint_as_float(u0 & 0xffff0000u),
+                                        __uint_as_float(u1 << 16), __uint_as_float(u1 & 0xffff0000u));
+          r[k] = bnbwd4(xv, d[j].v[k], sc[k], sh[k], mu[k], kx[k], kc[k]);
         } else if (MODE == PMU_SRC_BNBWD) {
           r[k] = bnbwd4(d[j].v[k], d[j].v[2 + k], sc[k], sh[k], mu[k], kx[k], kc[k]);
         } else {
@@ -507,7 +526,9 @@ __global__ __launch_bounds__(256) void frame_stream_kernel(StreamArgs a) {
 static bool stream_ok(const pmu_frame* f, int Cout) {
   if (f->nsrc != 1) return false;
   const pmu_src& s = f->src[0];
-  if (s.dtype != 0 || s.off_h != 0 || s.off_w != 0 || s.C != Cout || s.C % 8 != 0) return false;
+  // (bf16 storage: only the activation gradient of an unpooled BN-backward source, the *_dxb dx)
+  if (s.dtype != 0 && !(s.dtype == PMU_DT_X_BF16 && s.mode == PMU_SRC_BNBWD && s.pool == PMU_POOL_NONE)) return false;
+  if (s.off_h != 0 || s.off_w != 0 || s.C != Cout || s.C % 8 != 0) return false;
   const int nu = s.C / 8;
   if (nu > 256 || (nu & (nu - 1)) != 0) return false;
   if (s.pool == PMU_POOL_AVG2CEIL || (s.pool == PMU_POOL_MAX2 && s.mode == PMU_SRC_BNBWD)) return false;
@@ -527,6 +548,8 @@ static void launch_stream_nt(const pmu_src& s, dim3 grid, dim3 blk, hipStream_t 
     else hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_RAW, true, BF, U_POOL, NT>), grid, blk, 0, st, a);
   } else if (s.mode == PMU_SRC_BNRELU) {
     hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_BNRELU, false, BF, U_FLAT, NT>), grid, blk, 0, st, a);
+  } else if (s.mode == PMU_SRC_BNBWD && s.dtype == PMU_DT_X_BF16) {
+    hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_BNBWD, false, BF, U_BWD, NT, false, true>), grid, blk, 0, st, a);
   } else if (s.mode == PMU_SRC_BNBWD) {
     hipLaunchKernelGGL((frame_stream_kernel<PMU_SRC_BNBWD, false, BF, U_BWD, NT>), grid, blk, 0, st, a);
   } else {

@@ -206,6 +206,18 @@ SIGNATURES = {
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_dma_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_dxb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                          c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_x1b_dxb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                              c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_x1b_sum_dxb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                                  c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_dgrad_dma_bnr_dxb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_bn_bwd_reduce_dxb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                      c_void_p]),
+    "pmu_maxpool2_bwd_bnr_dxb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                         c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_pack_wino2h_blocks": (c_int, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_wino2h_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "pmu_conv3x3_pack_wino4_blocks": (c_int, [c_int, c_int, c_int]),
@@ -268,6 +280,8 @@ MFMA_ENTRY_POINTS = (
     "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw",
     "pmu_conv3x3_fwd_dma", "pmu_conv3x3_fwd_dma_zb", "pmu_conv3x3_dgrad_dma", "pmu_conv3x3_dgrad_dma_bnr",
     "pmu_conv3x3_dgrad_dma_bnr_zb", "pmu_conv3x3_dgrad_dma_x1b", "pmu_conv3x3_dgrad_dma_x1b_sum",
+    "pmu_conv3x3_dgrad_dma_dxb", "pmu_conv3x3_dgrad_dma_bnr_dxb", "pmu_conv3x3_dgrad_dma_x1b_dxb",
+    "pmu_conv3x3_dgrad_dma_x1b_sum_dxb",
     # transposed convs
     "pmu_convT2x2_fwd", "pmu_convT2x2_fwd_ld", "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad",
     "pmu_convT2x2_fwd_bf16", "pmu_convT2x2_dgrad_bf16", "pmu_convT2x2_wgrad_bf16",

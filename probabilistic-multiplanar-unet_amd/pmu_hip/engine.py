@@ -190,8 +190,12 @@ def bn_backward(da: torch.Tensor, z: torch.Tensor, st: BNState, bn: torch.nn.Bat
     else:
         R = lb.pmu_bn_bwd_tiles(P, C)
         part = _empty(R, 2 * C, device=dev)
-        L.call("pmu_bn_bwd_reduce_zb" if z.dtype == BF16S else "pmu_bn_bwd_reduce", da.data_ptr(), z.data_ptr(),
-               st.coef.data_ptr(), st.mean.data_ptr(), st.invstd.data_ptr(), P, C, part.data_ptr(), s)
+        if da.dtype == BF16S and (z.dtype != F32 or C % 4 != 0):
+            da = frame_to_f32([Src(da)], N, H, W)   # (the bf16-da reduce takes fp32 z, channel quads)
+        name = ("pmu_bn_bwd_reduce_dxb" if da.dtype == BF16S else
+                "pmu_bn_bwd_reduce_zb" if z.dtype == BF16S else "pmu_bn_bwd_reduce")
+        L.call(name, da.data_ptr(), z.data_ptr(), st.coef.data_ptr(), st.mean.data_ptr(), st.invstd.data_ptr(), P, C,
+               part.data_ptr(), s)
     G = lb.pmu_colsum_groups(R)
     acc = _empty(G, 2 * C, dtype=torch.float64, device=dev)
     L.call("pmu_colsum_f64", part.data_ptr(), R, 2 * C, acc.data_ptr(), G, s)
@@ -374,12 +378,15 @@ def tee32_ok(cin: int, cout: int) -> bool:
 
 
 def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, need_dx=True, split=None,
-                     x1_bf16_only=False):
-    """Backward of relu(bn(conv(operand))) given da (NHWC).  Writes conv/bn grads into ``grads``.
+                     x1_bf16_only=False, dx_bf16=False):
+    """Backward of relu(bn(conv(operand))) given da (NHWC; fp32, or bf16 bits from a *_dxb input
+    gradient).  Writes conv/bn grads into ``grads``.
 
     Returns the operand gradient(s): one NHWC tensor, or (dx0, dx1) when ``split`` is given
     (channel split of a concatenated operand).  x1_bf16_only (bf16 convs): the caller needs dx1 only as
-    the transposed conv's bf16 operand and its column sums (see _conv_backward_bf16)."""
+    the transposed conv's bf16 operand and its column sums (see _conv_backward_bf16).  dx_bf16 (bf16
+    convs, CFG.dx_bf16): the caller's consumers take dx / dx0 stored as bf16 (BF16S) — the LDS-DMA input
+    gradient then writes it so (autocast's dtype for a conv's input gradient)."""
     s = L.stream()
     z = out.z
     N, H, W, Cout = z.shape
@@ -395,7 +402,7 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     lb = L.lib()
     prod = _bnr_producer(out, need_dx, split)
     if out.bf16:
-        return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split, prod, x1_bf16_only)
+        return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split, prod, x1_bf16_only, dx_bf16)
     if out.xt32 is not None and need_dx:
         return _conv_backward_tee32(out, dz_src, conv, dw, split, prod)
     if out.planes is not None:
@@ -523,7 +530,8 @@ def raw_ok(N, H, W, Cp) -> bool:
     return N * H * W * Cp < 2 ** 31
 
 
-def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, prod=None, x1_bf16_only=False):
+def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, prod=None, x1_bf16_only=False,
+                        dx_bf16=False):
     """bf16-MFMA backward of one conv layer (torch.autocast(bfloat16) arithmetic).  dz after the
     BN+ReLU backward is written once in bf16 (dzt); the input gradient streams it (or, for a concat
     split that is not a multiple of 32, stages dz's frame in the fused kernel) and the weight
@@ -536,8 +544,12 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
     res = None
     if need_dx:
         sp = Cin if split is None else split
-        dx0 = _empty(N, H, W, sp, device=dev)
-        x1only = x1_bf16_only and sp < Cin and (Cin - sp) % 8 == 0 and dma_ok(H, W, dzt.shape[3], Cin, sp)
+        use_dma = dma_ok(H, W, dzt.shape[3], Cin, sp)
+        # bf16 dx0 (the *_dxb entries; every other output formed from the rounded values)
+        xb = dx_bf16 and CFG.dx_bf16 and use_dma and Cin % 8 == 0 and sp % 8 == 0
+        dx0 = _empty(N, H, W, sp, dtype=BF16S if xb else F32, device=dev)
+        sfx = "_dxb" if xb else ""
+        x1only = x1_bf16_only and sp < Cin and (Cin - sp) % 8 == 0 and use_dma
         dx1 = _empty(N, H, W, Cin - sp, device=dev) if sp < Cin and not x1only else None
         if x1only:
             # dx1 only in bf16 (the transposed conv's operand) with per-tile column sums (its bias gradient):
@@ -546,24 +558,28 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
             R = L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3])
             part = _empty(R, 2 * Cin, device=dev)
             dx1 = torch.empty(N, H, W, Cin - sp, dtype=BF16S, device=dev)
-            L.call("pmu_conv3x3_dgrad_dma_x1b_sum", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
-                   dx0.data_ptr(), dx1.data_ptr(), part.data_ptr(), s)
+            L.call("pmu_conv3x3_dgrad_dma_x1b_sum" + sfx, dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin,
+                   sp, dx0.data_ptr(), dx1.data_ptr(), part.data_ptr(), s)
             dx1._pmu_dbpart = (part, R, sp)
-        elif dma_ok(H, W, dzt.shape[3], Cin, sp):
+        elif use_dma:
             wp = pack_weights_dma(conv.weight, dgrad=True)
             if prod is not None:
-                _bnr_call("pmu_conv3x3_dgrad_dma_bnr_zb" if prod.z.dtype == BF16S else "pmu_conv3x3_dgrad_dma_bnr",
-                          prod, L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3]),
+                if prod.z.dtype == BF16S:   # (experiments build: bf16 z; its dx stays fp32)
+                    dx0 = _empty(N, H, W, sp, device=dev) if xb else dx0
+                    name = "pmu_conv3x3_dgrad_dma_bnr_zb"
+                else:
+                    name = "pmu_conv3x3_dgrad_dma_bnr" + sfx
+                _bnr_call(name, prod, L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, dzt.shape[3]),
                           (dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin), dx0, s)
             elif dx1 is not None and (Cin - sp) % 8 == 0:
                 # the up-sampled part's gradient also in bf16: the transposed conv's operand, kept on the
                 # fp32 tensor (unet_backward uses it instead of a pmu_frame_to_bf16 pass over dx1)
                 dx1b = torch.empty(N, H, W, Cin - sp, dtype=BF16S, device=dev)
-                L.call("pmu_conv3x3_dgrad_dma_x1b", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
-                       dx0.data_ptr(), dx1.data_ptr(), dx1b.data_ptr(), s)
+                L.call("pmu_conv3x3_dgrad_dma_x1b" + sfx, dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin,
+                       sp, dx0.data_ptr(), dx1.data_ptr(), dx1b.data_ptr(), s)
                 dx1._pmu_bf16 = dx1b
             else:
-                L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
+                L.call("pmu_conv3x3_dgrad_dma" + sfx, dzt.data_ptr(), dzt.shape[3], N, H, W, wp.data_ptr(), Cin, sp,
                        dx0.data_ptr(), L.ptr(dx1), s)
         elif raw_ok(N, H, W, dzt.shape[3]) and (sp == Cin or sp % 32 == 0):
             wp = pack_weights_raw(conv.weight, dgrad=True)
@@ -651,18 +667,22 @@ class EngineConfig:
         tests/test_bf16_gpu.py::test_c5_bf16_dice_gap_vs_fp32_oracle; DESIGN.md §3b), so PMU_BF16_Z=1
         is honoured only by an experiments build of the library, as PMU_WINO4=1;
     wgrad4: the fp32 weight gradient by Winograd F(4x4,3x3) where its shapes allow (PMU_WGRAD4=1; off by
-        default: measured equal to F(2x2) over the c2 shapes, 10.29 vs 10.29 ms — LDS-read bound)."""
+        default: measured equal to F(2x2) over the c2 shapes, 10.29 vs 10.29 ms — LDS-read bound);
+    dx_bf16: bf16 mode keeps the activation gradients the LDS-DMA input gradients produce inside the
+        UNet backward in bf16 (the *_dxb entries) — the dtype torch.autocast's conv backward returns
+        them in — and their consumers read them so (PMU_DX_BF16=0: fp32, the round-4 path)."""
     fp32_conv: str = "wino"
     wino2h: bool = True
     wino4: str = "dgrad"
     bf16_z: bool = False
     wgrad4: bool = False
+    dx_bf16: bool = True
 
     @classmethod
     def from_env(cls):
         return cls(fp32_conv=os.environ.get("PMU_FP32_CONV", "wino"), wino2h=os.environ.get("PMU_WINO2H", "1") != "0",
                    wino4=os.environ.get("PMU_WINO4", "dgrad"), bf16_z=os.environ.get("PMU_BF16_Z", "0") == "1",
-                   wgrad4=os.environ.get("PMU_WGRAD4", "0") == "1")
+                   wgrad4=os.environ.get("PMU_WGRAD4", "0") == "1", dx_bf16=os.environ.get("PMU_DX_BF16", "1") != "0")
 
 
 CFG = EngineConfig.from_env()
@@ -1031,7 +1051,7 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         up = net.up_blocks[j]
         us: UpState = st.ups[j]
         c1w, b1, c2w, b2 = _dc_layers(up.conv)
-        da1 = conv_bn_backward(us.c2, da, c2w, b2, grads)
+        da1 = conv_bn_backward(us.c2, da, c2w, b2, grads, dx_bf16=True)
         grads.flush()
         Cskip = us.cskip
         convT = up.up
@@ -1041,7 +1061,7 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         # bf16 with the LDS-DMA transposed-conv input gradient and no F.pad: dup is needed only in bf16 and
         # for the bias gradient's column sums, which the concat input gradient forms in its epilogue
         x1only = bool(us.bf16 and us.off == (0, 0) and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 1))
-        dsk, dup = conv_bn_backward(us.c1, da1, c1w, b1, grads, split=Cskip, x1_bf16_only=x1only)
+        dsk, dup = conv_bn_backward(us.c1, da1, c1w, b1, grads, split=Cskip, x1_bf16_only=x1only, dx_bf16=True)
         grads.flush()
         dskip[nlev - 2 - j] = dsk
         Hd, Wd = dup.shape[1], dup.shape[2]
@@ -1102,15 +1122,34 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             c1w, b1, c2w, b2 = _dc_layers(net.down_blocks[lev - 1].maxpool_conv[1])
         if lev != nlev - 1:
             da = dskip[lev]   # skip grad with the pooled path accumulated below
-        da1 = conv_bn_backward(o2, da, c2w, b2, grads)
+        da1 = conv_bn_backward(o2, da, c2w, b2, grads, dx_bf16=True)
         grads.flush()
-        dpool = conv_bn_backward(o1, da1, c1w, b1, grads, need_dx=(lev > 0))
+        dpool = conv_bn_backward(o1, da1, c1w, b1, grads, need_dx=(lev > 0), dx_bf16=True)
         grads.flush()
         if lev > 0:
             prev = st.enc[lev - 1][1]
             hp, wp = prev.z.shape[1], prev.z.shape[2]
             Cp = prev.z.shape[3]
-            if prev.z.dtype == F32 and prev.bn.mean is not None and Cp % 4 == 0:
+            dsk = dskip[lev - 1]
+            bn_ok = prev.z.dtype == F32 and prev.bn.mean is not None and Cp % 4 == 0
+            if bn_ok and dpool.dtype == BF16S and dsk.dtype == BF16S:
+                # bf16 pooled and skip gradients (*_dxb): their fp32 sum is the pooled layer's da, written
+                # to a new tensor with that layer's BN-backward partial sums
+                R = L.lib().pmu_maxpool2_bwd_bnr_tiles(N, hp, wp, Cp)
+                part = _empty(R, 2 * Cp, device=dev)
+                dsum = _empty(N, hp, wp, Cp, device=dev)
+                L.call("pmu_maxpool2_bwd_bnr_dxb", dpool.data_ptr(), dsk.data_ptr(), prev.z.data_ptr(),
+                       prev.bn.coef.data_ptr(), prev.bn.mean.data_ptr(), prev.bn.invstd.data_ptr(), N, hp, wp, Cp,
+                       dsum.data_ptr(), part.data_ptr(), s)
+                dskip[lev - 1] = dsum
+                prev.bnr = (dsum, part, R)
+                continue
+            # (mixed storage: the fp32 kernels below on fp32 copies)
+            if dpool.dtype == BF16S:
+                dpool = frame_to_f32([Src(dpool)], N, hp // 2, wp // 2)
+            if dsk.dtype == BF16S:
+                dskip[lev - 1] = frame_to_f32([Src(dsk)], N, hp, wp)
+            if bn_ok:
                 # routed into the skip gradient, which completes the pooled layer's da: the same pass
                 # forms that layer's BN-backward partial sums (no pmu_bn_bwd_reduce for it)
                 R = L.lib().pmu_maxpool2_bwd_bnr_tiles(N, hp, wp, Cp)

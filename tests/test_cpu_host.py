@@ -259,3 +259,33 @@ def test_debug_build_exports_and_identifies_itself():
         pytest.skip("debug library not built (make -C csrc DEBUG=1)")
     dbg = _lib.load_library(dbg_path)   # every SIGNATURES export must resolve
     assert dbg.pmu_build_flags() == _lib.BUILD_DEBUG
+
+
+def test_bench_gpus_launch_plan():
+    """bench.py --gpus N: outside torchrun N > 1 becomes a torch.distributed.run child
+    with N ranks on this node and the same argv; under torchrun --gpus must equal WORLD_SIZE."""
+    import bench
+    assert bench.launch_plan(1, [], {}) is None
+    cmd = bench.launch_plan(4, ["--gpus", "4", "--steps", "3"], {})
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    assert bench.launch_plan(2, [], {"WORLD_SIZE": "2"}) is None
+    assert bench.launch_plan(1, [], {"WORLD_SIZE": "1"}) is None
+    for gpus, world in ((1, "8"), (8, "1"), (2, "4")):
+        with pytest.raises(ValueError):
+            bench.launch_plan(gpus, [], {"WORLD_SIZE": world})
+    with pytest.raises(ValueError):
+        bench.launch_plan(0, [], {})
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    """The mismatch check runs before anything touches torch.cuda: rc 2 and a message, no JSON line."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "WORLD_SIZE=2" in r.stderr and r.stdout.strip() == ""

@@ -164,6 +164,83 @@ def test_fusion_512_edge_vs_restatement(dev, D0, D1, D2):
     assert bool(((top[:, 0] - top[:, 1])[flips] < 1e-5).all()), int(flips.sum())
 
 
+def _argmax_dim1(x):
+    """torch.argmax(x, 1) (first index of the maximum) as C-1 elementwise passes: torch's CPU
+    reduction over a short middle axis takes ~30 s per 512^3 x 3 volume, this ~1.5 s (no NaN here)."""
+    best = x[:, 0].clone()
+    idx = torch.zeros(best.shape, dtype=torch.long)
+    for c in range(1, x.shape[1]):
+        m = x[:, c] > best
+        idx[m] = c
+        best = torch.where(m, x[:, c], best)
+    return idx
+
+
+def test_fusion_512_cubed_vs_restatement(dev):
+    """Config c5's eval at full size (PMU/eval.py:157-203 on a 512^3 scan, 3 classes):
+    one pmu_fuse3view launch over three 512^3 x 3-class view stacks vs the restatement
+    (oracle/data_ref.fuse + eval.py:42-49's argmax Dice) on the CPU.  Predictions correlate with a nested-ellipsoid truth, so the Dice values are far from 0
+    and 1.  Probabilities in: average and label volume bit-exact, Dice counts exact, per-class Dice of
+    all four volumes within 1e-6 of eval.py's formula on the restated counts (contract: 1e-3).
+    Logits in (the predictor's path, softmax in the kernel): average within 1e-6, labels equal except
+    at fp32 near-ties of the top two classes."""
+    from oracle.data_ref import fuse
+    from pmu_hip.fusion import fuse_views
+    D, C = 512, 3
+    g = torch.Generator(device="cpu").manual_seed(512)
+    ax = torch.arange(D, dtype=torch.float32) - D / 2
+    r2 = ((ax[:, None, None] / (0.40 * D)) ** 2 + (ax[None, :, None] / (0.33 * D)) ** 2 +
+          (ax[None, None, :] / (0.28 * D)) ** 2)
+    truth = (r2 < 1.0).float() + (r2 < 0.35).float()
+    del r2
+    # per-view stacks in their own frames (the inverse of eval.py:176-188's permutes): evidence + noise
+    logits = []
+    for perm in ((0, 1, 2), (1, 0, 2), (2, 0, 1)):
+        t = truth.permute(*perm).unsqueeze(1)
+        lg = torch.randn(D, C, D, D, generator=g) * 1.5
+        lg += 2.0 * (t == torch.arange(C, dtype=torch.float32)[None, :, None, None]).float()
+        logits.append(lg)
+        del t
+    st = [torch.softmax(t, 1) for t in logits]
+    vols = fuse(*st)
+    truth_d = truth.to(dev)
+    r = fuse_views(*[t.to(dev) for t in st], truth_d)
+    r_avg, r_lab, r_cnt, r_dice = r["avg"].cpu(), r["label"].cpu(), r["counts"].cpu(), r["dice"].cpu()
+    del r
+    torch.cuda.empty_cache()
+    r2 = fuse_views(*[t.to(dev) for t in logits], truth_d, logits=True)
+    l_avg, l_lab = r2["avg"].cpu(), r2["label"].cpu()
+    del r2, truth_d
+    torch.cuda.empty_cache()
+    avg = vols[3]
+    lab = _argmax_dim1(avg).int()
+    assert torch.equal(lab[200:204], torch.argmax(avg[200:204], 1).int())   # the helper is torch.argmax
+    assert torch.equal(r_avg, avg)
+    assert torch.equal(r_lab, lab)
+    assert float((l_avg - avg).abs().max()) <= 1e-6
+    f = (l_lab != lab).nonzero(as_tuple=True)
+    top = torch.topk(avg[f[0], :, f[1], f[2]], 2, dim=1).values if f[0].numel() else torch.zeros(0, 2)
+    flips, near_tie_flips = int(f[0].numel()), int(((top[:, 0] - top[:, 1]) < 1e-5).sum())
+    # eval.py:42-49's argmax of each volume; views 1 and 2 argmax'ed in their own frame and the label
+    # volume permuted (the same per-voxel argmax, first index on ties, as argmax of the permuted view)
+    ams = [_argmax_dim1(st[0]), _argmax_dim1(st[1]).permute(1, 0, 2),
+           _argmax_dim1(st[2]).permute(1, 2, 0), lab.long()]
+    tl = truth.long()
+    counts = torch.zeros(4, C, 3, dtype=torch.float64)
+    for v in range(4):
+        conf = torch.bincount((ams[v] * C + tl).reshape(-1), minlength=C * C).reshape(C, C).double()
+        counts[v, :, 0] = conf.diagonal()
+        counts[v, :, 1] = conf.sum(1)
+        counts[v, :, 2] = conf.sum(0)
+    assert flips == near_tie_flips, (flips, near_tie_flips)
+    assert torch.equal(r_cnt, counts)
+    for v in range(4):   # eval.py:42-49's Dice (dice_coeff's 1e-6 smoothing) on the restated counts
+        for c in range(C):
+            ref = (2.0 * counts[v, c, 0] + 1e-6) / (counts[v, c, 1] + counts[v, c, 2] + 1e-6)
+            assert abs(float(r_dice[v, c]) - float(ref)) <= 1e-6, (v, c, float(r_dice[v, c]), float(ref))
+    assert 0.05 < float(r_dice[3, 1]) < 0.999 and 0.05 < float(r_dice[3, 2]) < 0.999, r_dice
+
+
 def _synthetic_scans(n, shape, seed):
     g = np.random.default_rng(seed)
     out = {}

@@ -27,3 +27,23 @@ def test_bucketed_allreduce_overlapped_with_hip_backward():
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "DP_CHECK OK" in out, out[-4000:]
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_launches_two_ranks():
+    """bench.py --gpus 2 outside torchrun starts 2 ranks itself and the line reports the
+    whole job: n_gpus 2, global batch 64, dp2.  Rehearsed on the 1-GPU box over gloo (both ranks on
+    cuda:0); the driver's N-GPU node runs the same path over RCCL."""
+    import json
+    env = dict(os.environ, PMU_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--no-kernel-timing"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 64 and res["config"]["parallelism"] == "dp2"
+    assert res["value"] > 0 and res["steps"] == 2

@@ -10,7 +10,13 @@ time from the same run's kernel trace).  The counter MFMA-busy fraction is then
 -- the share of SIMD-cycles the matrix cores were busy at the clock the chip actually held -- and the
 fraction of the 2.4 GHz dense peak is  flops / wall / peak.  The two differ by the clock ratio
 (f_eff / 2.4 GHz).  counter_defs.yaml's MfmaUtil (busy / (GRBM x SIMD_NUM)) omits the /8 and reads 8x low
-on gfx950."""
+on gfx950.
+
+Rows whose effective clock reads above 2.4 GHz (the chip's peak clock) are marked `excluded`: the
+counter window of such a dispatch is longer than the dispatch itself (GRBM / 8 > 2.4 GHz x wall), so
+neither f_eff nor the busy fraction derived from it is physical.  Short dispatches (batch 1, < 0.3 ms)
+fall under the same rule; one long dispatch does too (the first 512-channel bf16 weight-gradient
+launch of round 4, 0.40 ms at a read 2.88 GHz, its two repeats at 2.02-2.03 GHz)."""
 import csv
 import glob
 import os
@@ -18,6 +24,7 @@ import sys
 from collections import defaultdict
 
 SIMDS = 1024
+F_MAX_GHZ = 2.4        # gfx950 peak engine clock: a higher f_eff means the counter window overran
 PEAK = {"bf16": 2.5166e15, "f32": 157.3e12}     # dense MFMA peaks at 2.4 GHz (MI355X_MICROARCH.md)
 
 
@@ -42,7 +49,7 @@ def main(d):
             rows.append((run, did, k, c, dur.get(did)))
     rows.sort(key=lambda r: (r[0], r[1]))
     print(f"{'run':16s} {'kernel':44s} {'flops=MOPS*512':>14s} {'busy/inst':>9s} {'ms':>7s} {'f_eff GHz':>9s} "
-          f"{'busy_frac':>9s} {'peak_frac':>9s}")
+          f"{'busy_frac':>9s} {'peak_frac':>9s} use")
     for run, did, k, c, t in rows:
         mops_b = c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0)
         mops_f = c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0)
@@ -59,7 +66,7 @@ def main(d):
         pf = flops / t / peak if t else float("nan")
         print(f"{run:16s} {name:44s} {flops:14.4e} {busy / ninst if ninst else float('nan'):9.2f} "
               f"{(t or float('nan')) * 1e3:7.3f} {feff:9.2f} {busy / (SIMDS * cyc) if cyc else float('nan'):9.3f} "
-              f"{pf:9.3f}")
+              f"{pf:9.3f} {'yes' if feff <= F_MAX_GHZ else 'excluded'}")
 
 
 if __name__ == "__main__":
