@@ -127,7 +127,7 @@ class KernelTimer:
         if name == "pmu_conv3x3_dgrad_bf16":
             f = args[0]._obj
             return 2.0 * f.N * f.H * f.W * f.src[0].C * args[2] * 9
-        if name == "pmu_conv3x3_wgrad_bf16":
+        if name in ("pmu_conv3x3_wgrad_bf16", "pmu_conv3x3_wgrad_bf16_dma"):
             N, H, W, cout, cin = args[2], args[3], args[4], args[5], args[6]
             return 2.0 * N * H * W * cin * cout * 9
         if name in ("pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw"):
@@ -408,7 +408,7 @@ KERNEL_FAMILY = {
     "pmu_fcomb_bwd": r"fcomb_bwd_kernel",
     "pmu_conv3x3_fwd_bf16": r"conv3x3_bf16_pipe_kernel<false|conv3x3_bf16_kernel<\d, \d+, false>",
     "pmu_conv3x3_dgrad_bf16": r"conv3x3_bf16_pipe_kernel<true|conv3x3_bf16_kernel<\d, \d+, true>",
-    "pmu_conv3x3_wgrad_bf16": r"wgrad3x3_bf16_kernel<", "pmu_conv3x3_fwd_raw": r"conv3x3_raw_kernel<false",
+    "pmu_conv3x3_wgrad_bf16": r"wgrad3x3_bf16_kernel<", "pmu_conv3x3_wgrad_bf16_dma": r"wgrad3x3_bf16_dma_kernel<", "pmu_conv3x3_fwd_raw": r"conv3x3_raw_kernel<false",
     "pmu_conv3x3_dgrad_raw": r"conv3x3_raw_kernel<true", "pmu_convT2x2_fwd_bf16": r"convT_bf16_kernel<false>",
     "pmu_convT2x2_dgrad_bf16": r"convT_bf16_kernel<true>", "pmu_convT2x2_wgrad_bf16": r"convT_wgrad_bf16_kernel",
     "pmu_conv3x3_dgrad_wino4_bnr": r"conv3x3_wino4_kernel<true", "pmu_conv3x3_dgrad_wino2h_bnr": r"conv3x3_wino2h_kernel<true",

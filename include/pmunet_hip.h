@@ -245,6 +245,14 @@ int pmu_frame_to_f32_pool_skip(const pmu_frame* f, float* out, float* skip, int 
 size_t pmu_conv3x3_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);
 int pmu_conv3x3_wgrad_bf16(const unsigned short* dzt, const unsigned short* xt, int N, int H, int W,
                            int Cout, int Cin, float* dw, float* ws, size_t ws_bytes, void* stream);
+/* The same weight gradient with both operands staged by LDS-DMA (csrc/wgrad3x3_bf16_dma.hip): a wave
+ * owns a 32-co x 32-ci fragment pair and all nine taps, walks 16-pixel-wide image strips row by row
+ * and keeps the three activation rows of a step in registers (one new row per step).  Maps at least
+ * 16 wide (pmu_conv3x3_wgrad_dma_ok); ws holds pmu_conv3x3_wgrad_ws_bf16_dma() bytes. */
+int pmu_conv3x3_wgrad_dma_ok(int N, int H, int W, int Cin, int Cout);
+size_t pmu_conv3x3_wgrad_ws_bf16_dma(int N, int H, int W, int Cin, int Cout);
+int pmu_conv3x3_wgrad_bf16_dma(const unsigned short* dzt, const unsigned short* xt, int N, int H, int W,
+                               int Cout, int Cin, float* dw, float* ws, size_t ws_bytes, void* stream);
 
 /* Weight gradient from materialised bf16 operands: xt [N][H][W][pad8(Cin)] (the convT input after BN+ReLU)
  * and dut [N][Hd][Wd][pad8(Cout)] (du); dbias (nullable) sums the fp32 du over the output region. */

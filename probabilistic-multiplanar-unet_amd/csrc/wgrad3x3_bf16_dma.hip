@@ -1,0 +1,351 @@
+// Weight gradient of the 3x3 / pad 1 convolution on bf16 MFMA with both operands staged by LDS-DMA
+// (config c5: autograd of nn.Conv2d w.r.t. its weight, PMU/model/unet/unet_parts.py:15,18, under
+// torch.autocast(bfloat16): bf16 operands, fp32 sums, fp32 dw).
+//
+//   dw[co][ci][kh][kw] = sum_{n,y,x} dzt[n,y,x,co] * xt[n, y+kh-1, x+kw-1, ci]
+//
+// GEMM per wave: one 32-co x 32-ci fragment pair and ALL nine taps (9 accumulators of
+// v_mfma_f32_32x32x16_bf16, 144 registers); K = pixels, 16 per k-step = one 16-pixel row segment of a
+// vertical strip of the image.  A workgroup walks its strips down, row by row:
+//   * the dz row (A) of step y serves all nine taps;
+//   * the three activation rows y-1, y, y+1 (B, per kw a 16-pixel window of an 18-pixel halo row)
+//     are kept in registers and rotate: each step reads ONE new halo row (y+1), the rows for kh = 0, 1
+//     come from the two previous steps.
+// Per step and wave: 2 + 6 ds_read_b64_tr_b16 for 9 MFMAs (the register-staged kernel in
+// wgrad3x3_bf16.hip: 10 for 6).
+//
+// Staging: a ring of NS LDS stages filled by global_load_lds (16 B per lane, no staging registers, no
+// ds_write); a stage holds three consecutive steps (dz rows y..y+2, halo rows y+1..y+3) of every strip
+// lane of the workgroup; one barrier per stage (27 MFMAs per wave).  Units outside the image, the
+// channels or the segment are DMA'd from a zero page, so every wave issues the same number of DMA
+// instructions per stage and the ring waits are counted (s_waitcnt vmcnt(N)) with the next NS-2 stages
+// in flight.  LDS rows are unit permutations, not padded rows (LDS-DMA writes 1 KiB contiguous per
+// wave-instruction): 16-B unit u of pixel p sits at u ^ sw(p), chosen so the four pixel rows a 32-lane
+// group of a transposed read touches fall in four distinct 16-bank quarters (conflict-free).
+//
+// K split: the image is cut into segments (n, 16-wide strip, 3m consecutive rows); a segment starts
+// with a prologue stage (halo rows y0-1, y0 into the rotation registers).  Workgroup = (co block, ci
+// block, split); its WS strip lanes each walk SPB segments in lockstep; split-K slabs
+// ws[split*WS + lane][tap][co][ci], reduced in a fixed order (pmu_splitk_reduce9_kernel).
+#include <type_traits>
+
+#include "pmu_stage.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+static __device__ __attribute__((aligned(64))) unsigned g_wgd_zero[256];  // 1 KiB of zeros (DMA source)
+
+constexpr int SW = 16;  // strip width (pixels per k-step)
+
+// WCOF x WCIF x WS = 8 waves: co fragments x ci fragments x strip lanes
+template <int WCOF, int WCIF, int WS>
+struct WG {
+  static_assert(WCOF * WCIF * WS == 8, "8 waves");
+  static constexpr int NT = 512;
+  static constexpr int ARU = 4 * WCOF, XRU = 4 * WCIF;      // 16-B units per pixel row
+  static constexpr int A_ROW = SW * ARU, X_ROW = (SW + 2) * XRU;
+  static constexpr int A_UNITS = WS * 3 * A_ROW, X_UNITS = WS * 3 * X_ROW;
+  static constexpr int NI = (A_UNITS + X_UNITS + NT - 1) / NT;  // DMA instructions per wave per stage
+  static constexpr int STAGE = NI * NT * 16;                      // bytes
+  static constexpr int NS = (4 * STAGE <= 160 * 1024) ? 4 : 3;
+  static_assert(NS * STAGE <= 160 * 1024, "LDS");
+};
+
+// unit permutation of a pixel row of F 32-channel fragments (see top)
+template <int F>
+__device__ __forceinline__ int wgd_sw(int p) {
+  return F == 1 ? 0 : F == 2 ? 4 * ((p >> 1) & 1) : 4 * (p & 3);
+}
+
+struct WgdArgs {
+  const unsigned short* dzt;  // [N][H][W][Cop]
+  const unsigned short* xt;   // [N][H][W][Cip]
+  float* ws;
+  int N, H, W, Cout, Cin, Cop, Cip;
+  int strips_w, nseg_strip, m, spb, nsplit, nseg;  // segments: 3m rows; spb per lane; nseg in all
+};
+
+template <int OFF>
+__device__ __forceinline__ s16x4 wgd_tr(unsigned addr) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void wgd_wait_lgkm() {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt");
+  __builtin_amdgcn_s_waitcnt(0xC07F | (N << 8));
+}
+__device__ __forceinline__ bf16x8 wgd_frag(s16x4 lo, s16x4 hi) {
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int N>
+__device__ __forceinline__ void wgd_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  // gfx9 s_waitcnt: vmcnt[3:0] bits 3:0, vmcnt[5:4] bits 15:14; expcnt / lgkmcnt at their maxima
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+
+template <int WCOF, int WCIF, int WS>
+__global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
+  using G = WG<WCOF, WCIF, WS>;
+  constexpr int NS = G::NS, NI = G::NI;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * G::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ncb = pmu_cdiv_dev(a.Cout, 32 * WCOF), nib = pmu_cdiv_dev(a.Cin, 32 * WCIF);
+  // (channel block, split) in XCD order, channel blocks fastest: the blocks of one split walk the same
+  // pixels in step on one XCD, whose L2 then serves each row to all of them
+  const int nblk = ncb * nib;
+  const int lbk = pmu_xcd_block(blockIdx.x, gridDim.x);
+  const int blk = lbk % nblk, split = lbk / nblk;
+  const int co0 = (blk % ncb) * 32 * WCOF, ci0 = (blk / ncb) * 32 * WCIF;
+  PMU_DCHECK(split < a.nsplit, PMU_DBG_GRID);
+  // wave -> (co fragment, ci fragment, strip lane)
+  const int wco = wave % WCOF, wci = (wave / WCOF) % WCIF, wsl = wave / (WCOF * WCIF);
+
+  // segment (lane sl, k-th of the block) -> image n, strip column c0, first row y0 (invalid: past the end,
+  // y0 beyond the image so every unit reads the zero page)
+  auto seg_of = [&](int k, int sl, int& n, int& c0, int& y0) {
+    const int s = (split * a.spb + k) * WS + sl;
+    if (s >= a.nseg) { n = 0; c0 = 0; y0 = a.H + 1; return; }
+    const int ys = s % a.nseg_strip;
+    const int st = s / a.nseg_strip;
+    c0 = (st % a.strips_w) * SW;
+    n = st / a.strips_w;
+    y0 = ys * 3 * a.m;
+  };
+  // DMA of stage index s (segment s / (m+1), step t = s % (m+1)) into ring slot s % NS.  Stage t = 0:
+  // halo rows y0-1, y0, y0+1 (the prologue; dz rows unread); t >= 1: dz rows Y..Y+2 and halo rows
+  // Y+1..Y+3, Y = y0 + 3(t-1).  Lane unit U = (i * 8 + wave) * 64 + lane of the stage.
+  const char* zsrc = reinterpret_cast<const char*>(g_wgd_zero) + 16 * lane;
+  auto issue = [&](int s) {
+    const int k = s / (a.m + 1), t = s - k * (a.m + 1);
+    unsigned char* stg = smem + (s % NS) * G::STAGE;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int U = (i * 8 + wave) * 64 + lane;
+      const char* src = zsrc;
+      if (U < G::A_UNITS) {
+        const int sl = U / (3 * G::A_ROW);
+        const int r = U - sl * (3 * G::A_ROW);
+        const int j = r / G::A_ROW, pu = r - j * G::A_ROW;
+        const int px = pu / G::ARU, u = (pu % G::ARU) ^ wgd_sw<WCOF>(px);
+        int n, c0, y0;
+        seg_of(k, sl, n, c0, y0);
+        const int y = y0 + 3 * (t - 1) + j, x = c0 + px, c = co0 + 8 * u;
+        if (t > 0 && y < a.H && x < a.W && c < a.Cop)
+          src = reinterpret_cast<const char*>(a.dzt + ((((long long)n * a.H + y) * a.W + x) * a.Cop + c));
+      } else if (U < G::A_UNITS + G::X_UNITS) {
+        const int V = U - G::A_UNITS;
+        const int sl = V / (3 * G::X_ROW);
+        const int r = V - sl * (3 * G::X_ROW);
+        const int j = r / G::X_ROW, pu = r - j * G::X_ROW;
+        const int px = pu / G::XRU, u = (pu % G::XRU) ^ wgd_sw<WCIF>(px);
+        int n, c0, y0;
+        seg_of(k, sl, n, c0, y0);
+        const int y = (t == 0 ? y0 - 1 : y0 + 3 * t - 2) + j, x = c0 - 1 + px, c = ci0 + 8 * u;
+        if (y >= 0 && y < a.H && x >= 0 && x < a.W && c < a.Cip)
+          src = reinterpret_cast<const char*>(a.xt + ((((long long)n * a.H + y) * a.W + x) * a.Cip + c));
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
+                                       (__attribute__((address_space(3))) void*)(stg + (i * 8 + wave) * 1024), 16, 0,
+                                       0);
+    }
+  };
+
+  f32x16 acc[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // transposed-read lane roles: half h takes pixels 8h..8h+7 of the 16-pixel step, group g the column
+  // block 16g of the fragment, lane 4q+p supplies pixel row 4t+q (t = 0, 1: the two reads) and columns
+  // 4p..4p+3 (byte 8 (p & 1) of 16-B unit 2g + (p >> 1) of the fragment).  Byte offsets within a stage,
+  // per lane (row j of the stage adds the immediate offset j * row bytes).
+  const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
+  const int ua = wco * 4 + 2 * g + (p >> 1), ux = wci * 4 + 2 * g + (p >> 1), hb = 8 * (p & 1);
+  const int aoff = wsl * 3 * G::A_ROW, xoff = G::A_UNITS + wsl * 3 * G::X_ROW;
+  unsigned ra[2], rx[3][2];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    const int pa = 8 * h + 4 * t2 + q;
+    ra[t2] = 16u * (aoff + pa * G::ARU + (ua ^ wgd_sw<WCOF>(pa))) + hb;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int px = pa + kw;
+      rx[kw][t2] = 16u * (xoff + px * G::XRU + (ux ^ wgd_sw<WCIF>(px))) + hb;
+    }
+  }
+  const unsigned sbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)(smem);
+  // The LDS reads are inline asm: through the ds_read_tr intrinsic the compiler cannot tell them from
+  // the pending LDS-DMA writes and put an s_waitcnt vmcnt(0) before every stage's reads (the whole ring
+  // drained each stage).  Their results are waited for by hand (wgd_wait_lgkm) behind a scheduling
+  // barrier, so no MFMA moves above its wait.
+  auto rd_a = [&](unsigned st, auto J) {
+    constexpr int OFF = decltype(J)::value * G::A_ROW * 16;
+    return wgd_frag(wgd_tr<OFF>(st + ra[0]), wgd_tr<OFF>(st + ra[1]));
+  };
+  auto rd_x = [&](unsigned st, auto J, bf16x8 (&o)[3]) {
+    constexpr int OFF = decltype(J)::value * G::X_ROW * 16;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) o[kw] = wgd_frag(wgd_tr<OFF>(st + rx[kw][0]), wgd_tr<OFF>(st + rx[kw][1]));
+  };
+  auto mm = [&](const bf16x8& af, const bf16x8 (&k0)[3], const bf16x8 (&k1)[3], const bf16x8 (&k2)[3]) {
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      acc[0][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, k0[kw], acc[0][kw], 0, 0, 0);
+      acc[1][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, k1[kw], acc[1][kw], 0, 0, 0);
+      acc[2][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, k2[kw], acc[2][kw], 0, 0, 0);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+
+  // prologue: the first NS-1 stages in flight (stages past the end read the zero page or other segments
+  // into slots nobody reads, so every wave issues NI DMAs per stage index and the counted waits hold)
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue(s);
+  // (a segment's prologue and its triplets as nested loops: as the two arms of one per-stage branch,
+  // the merged rotation registers spilled 150+ VGPRs)
+  int s = 0;
+  auto begin_stage = [&]() {
+    // stage s landed (this wave's DMAs: all but the NS-2 younger stages'), then every wave's, and every
+    // read of stage s-1 — whose slot the next DMA overwrites — is done (its MFMAs consumed them)
+    wgd_wait_vm<(NS - 2) * NI>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue(s + NS - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    return sbase + (unsigned)((s % NS) * G::STAGE);
+  };
+  bf16x8 B0[3], B1[3];  // halo rows y-1, y of the next step (per kw)
+  for (int k = 0; k < a.spb; ++k) {
+    {  // prologue of a segment: halo rows y0-1, y0
+      const unsigned st = begin_stage();
+      rd_x(st, I0{}, B0);
+      rd_x(st, I1{}, B1);
+      wgd_wait_lgkm<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      ++s;
+    }
+    for (int t = 1; t <= a.m; ++t, ++s) {  // steps y, y+1, y+2: new halo rows y+1, y+2, y+3
+      const unsigned st = begin_stage();
+      bf16x8 x0[3], x1[3], x2[3];
+      const bf16x8 a0 = rd_a(st, I0{});
+      rd_x(st, I0{}, x0);
+      const bf16x8 a1 = rd_a(st, I1{});
+      rd_x(st, I1{}, x1);
+      wgd_wait_lgkm<8>();  // step y's 8 reads
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a0, B0, B1, x0);
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 a2 = rd_a(st, I2{});
+      rd_x(st, I2{}, x2);
+      wgd_wait_lgkm<8>();  // step y+1's
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a1, B1, x0, x1);
+      __builtin_amdgcn_sched_barrier(0);
+      wgd_wait_lgkm<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a2, x0, x1, x2);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) { B0[kw] = x1[kw]; B1[kw] = x2[kw]; }
+    }
+  }
+  wgd_wait_vm<0>();  // (the tail stages' DMAs: nothing of them is read; drained before the wave exits)
+
+  // slab write: ws[split * WS + lane][tap][co][ci]; accumulator rows = co, columns = ci (lanes)
+  const int sp = split * WS + wsl;
+  const int ci = ci0 + wci * 32 + (lane & 31);
+  if (ci < a.Cin) {
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kh * 3 + kw;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = co0 + wco * 32 + acc_row(r, lane);
+          PMU_DCHECK(sp < a.nsplit * WS, PMU_DBG_WORKSPACE);
+          if (co < a.Cout) a.ws[(((long long)sp * 9 + tap) * a.Cout + co) * a.Cin + ci] = acc[kh][kw][r];
+        }
+      }
+  }
+}
+
+struct WgdGeo {
+  int wcof, wcif, ws, nsplit, m, spb, nseg_strip, strips_w, nseg;
+};
+
+// Workgroup shape by channel counts, then the K split: about one workgroup per CU in all (256), whole
+// strips per segment when there are enough of them, else strips cut into equal row segments.
+static WgdGeo wgd_geometry(int N, int H, int W, int Cin, int Cout) {
+  WgdGeo g;
+  if (Cout <= 64 && Cin <= 64) { g.wcof = 2; g.wcif = 2; g.ws = 2; }
+  else if (Cout <= 64) { g.wcof = 2; g.wcif = 4; g.ws = 1; }
+  else { g.wcof = 4; g.wcif = 2; g.ws = 1; }
+  const int nb = pmu_cdiv(Cout, 32 * g.wcof) * pmu_cdiv(Cin, 32 * g.wcif);
+  g.nsplit = 256 / nb;
+  if (g.nsplit < 1) g.nsplit = 1;
+  g.strips_w = pmu_cdiv(W, SW);
+  const long long strips = (long long)N * g.strips_w;
+  const long long lanes = (long long)g.nsplit * g.ws;
+  g.nseg_strip = strips >= lanes ? 1 : (int)((lanes + strips - 1) / strips);
+  if (g.nseg_strip > pmu_cdiv(H, 3)) g.nseg_strip = pmu_cdiv(H, 3);
+  g.m = pmu_cdiv(pmu_cdiv(H, g.nseg_strip), 3);
+  g.nseg_strip = pmu_cdiv(H, 3 * g.m);
+  g.nseg = (int)(strips * g.nseg_strip);
+  if ((long long)g.nsplit * g.ws > g.nseg) g.nsplit = pmu_cdiv(g.nseg, g.ws);
+  g.spb = pmu_cdiv(g.nseg, g.nsplit * g.ws);
+  g.nsplit = pmu_cdiv(g.nseg, g.spb * g.ws);  // (no workgroup without a segment)
+  return g;
+}
+
+}  // namespace
+
+// Shapes the LDS-DMA weight gradient takes (the engine's default for bf16 maps at least 16 wide).
+extern "C" int pmu_conv3x3_wgrad_dma_ok(int N, int H, int W, int Cin, int Cout) {
+  return N > 0 && H > 0 && W >= SW && Cin > 0 && Cout > 0 && (long long)N * pmu_cdiv(W, SW) * H < (1LL << 30);
+}
+
+extern "C" size_t pmu_conv3x3_wgrad_ws_bf16_dma(int N, int H, int W, int Cin, int Cout) {
+  const WgdGeo g = wgd_geometry(N, H, W, Cin, Cout);
+  return (size_t)g.nsplit * g.ws * 9 * Cout * Cin * sizeof(float);
+}
+
+// dw[Cout][Cin][3][3] from dzt [N][H][W][pad8(Cout)] and xt [N][H][W][pad8(Cin)] (bf16), as
+// pmu_conv3x3_wgrad_bf16; ws holds pmu_conv3x3_wgrad_ws_bf16_dma() bytes.
+extern "C" int pmu_conv3x3_wgrad_bf16_dma(const unsigned short* dzt, const unsigned short* xt, int N, int H, int W,
+                                          int Cout, int Cin, float* dw, float* ws, size_t ws_bytes, void* stream) {
+  PMU_REQUIRE(dzt && xt && dw && ws && pmu_conv3x3_wgrad_dma_ok(N, H, W, Cin, Cout));
+  const WgdGeo g = wgd_geometry(N, H, W, Cin, Cout);
+  PMU_REQUIRE(ws_bytes >= (size_t)g.nsplit * g.ws * 9 * Cout * Cin * sizeof(float));
+  WgdArgs a;
+  a.dzt = dzt; a.xt = xt; a.ws = ws;
+  a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.Cin = Cin;
+  a.Cop = (Cout + 7) & ~7; a.Cip = (Cin + 7) & ~7;
+  a.strips_w = g.strips_w; a.nseg_strip = g.nseg_strip; a.m = g.m; a.spb = g.spb; a.nsplit = g.nsplit;
+  a.nseg = g.nseg;
+  const int nb = pmu_cdiv(Cout, 32 * g.wcof) * pmu_cdiv(Cin, 32 * g.wcif);
+  const dim3 grid((unsigned)(nb * g.nsplit)), blk(512);
+  hipStream_t st = (hipStream_t)stream;
+  if (g.ws == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 2, 2>), grid, blk, 0, st, a);
+  else if (g.wcof == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 4, 1>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<4, 2, 1>), grid, blk, 0, st, a);
+  PMU_CHECK_LAUNCH();
+  const long long E = 9LL * Cout * Cin;
+  hipLaunchKernelGGL(pmu_splitk_reduce9_kernel, dim3((unsigned)pmu_cdiv(E, 64)), dim3(256), 0, st, (const float*)ws,
+                     g.nsplit * g.ws, (long long)Cout * Cin, dw);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}

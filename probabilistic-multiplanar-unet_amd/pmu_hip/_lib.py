@@ -214,6 +214,10 @@ SIGNATURES = {
                                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_dma_bnr_dxb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pmu_conv3x3_wgrad_dma_ok": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_conv3x3_wgrad_ws_bf16_dma": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pmu_conv3x3_wgrad_bf16_dma": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                           c_size_t, c_void_p]),
     "pmu_bn_bwd_reduce_dxb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                       c_void_p]),
     "pmu_maxpool2_bwd_bnr_dxb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
@@ -276,7 +280,7 @@ MFMA_ENTRY_POINTS = (
     "pmu_conv3x3_fwd_wino2h", "pmu_conv3x3_dgrad_wino2h", "pmu_conv3x3_dgrad_wino2h_bnr",
     "pmu_conv3x3_fwd_wino4", "pmu_conv3x3_dgrad_wino4", "pmu_conv3x3_dgrad_wino4_bnr", "pmu_conv3x3_wgrad_wino4",
     # bf16 3x3 convs
-    "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16",
+    "pmu_conv3x3_fwd_bf16", "pmu_conv3x3_dgrad_bf16", "pmu_conv3x3_wgrad_bf16", "pmu_conv3x3_wgrad_bf16_dma",
     "pmu_conv3x3_fwd_raw", "pmu_conv3x3_dgrad_raw",
     "pmu_conv3x3_fwd_dma", "pmu_conv3x3_fwd_dma_zb", "pmu_conv3x3_dgrad_dma", "pmu_conv3x3_dgrad_dma_bnr",
     "pmu_conv3x3_dgrad_dma_bnr_zb", "pmu_conv3x3_dgrad_dma_x1b", "pmu_conv3x3_dgrad_dma_x1b_sum",

@@ -592,10 +592,12 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
         res = dx0 if split is None else (dx0, dx1)
     xt = out.xt if out.xt is not None else frame_to_bf16(out.srcs, N, H, W)
     out.xt = None
-    wsb = L.lib().pmu_conv3x3_wgrad_ws_bf16(N, H, W, Cin, Cout)
+    lb = L.lib()
+    sfx = "_dma" if CFG.wgrad_dma and lb.pmu_conv3x3_wgrad_dma_ok(N, H, W, Cin, Cout) else ""
+    wsb = getattr(lb, "pmu_conv3x3_wgrad_ws_bf16" + sfx)(N, H, W, Cin, Cout)
     ws = _empty(max(1, (wsb + 3) // 4), device=dev)
-    L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(), ws.data_ptr(),
-           wsb, s)
+    L.call("pmu_conv3x3_wgrad_bf16" + sfx, dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(),
+           ws.data_ptr(), wsb, s)
     return res
 
 
@@ -670,19 +672,23 @@ class EngineConfig:
         default: measured equal to F(2x2) over the c2 shapes, 10.29 vs 10.29 ms — LDS-read bound);
     dx_bf16: bf16 mode keeps the activation gradients the LDS-DMA input gradients produce inside the
         UNet backward in bf16 (the *_dxb entries) — the dtype torch.autocast's conv backward returns
-        them in — and their consumers read them so (PMU_DX_BF16=0: fp32, the round-4 path)."""
+        them in — and their consumers read them so (PMU_DX_BF16=0: fp32, the round-4 path);
+    wgrad_dma: the bf16 weight gradient on the LDS-DMA strip kernel (pmu_conv3x3_wgrad_bf16_dma) where
+        its shapes allow, else the register-staged one (PMU_WGRAD_DMA=0: always the latter)."""
     fp32_conv: str = "wino"
     wino2h: bool = True
     wino4: str = "dgrad"
     bf16_z: bool = False
     wgrad4: bool = False
     dx_bf16: bool = True
+    wgrad_dma: bool = True
 
     @classmethod
     def from_env(cls):
         return cls(fp32_conv=os.environ.get("PMU_FP32_CONV", "wino"), wino2h=os.environ.get("PMU_WINO2H", "1") != "0",
                    wino4=os.environ.get("PMU_WINO4", "dgrad"), bf16_z=os.environ.get("PMU_BF16_Z", "0") == "1",
-                   wgrad4=os.environ.get("PMU_WGRAD4", "0") == "1", dx_bf16=os.environ.get("PMU_DX_BF16", "1") != "0")
+                   wgrad4=os.environ.get("PMU_WGRAD4", "0") == "1", dx_bf16=os.environ.get("PMU_DX_BF16", "1") != "0",
+                   wgrad_dma=os.environ.get("PMU_WGRAD_DMA", "1") != "0")
 
 
 CFG = EngineConfig.from_env()

@@ -93,6 +93,8 @@ def main():
         L.call("pmu_frame_to_bf16", fin, cpi, xt.data_ptr(), s)
         wsbb = L.lib().pmu_conv3x3_wgrad_ws_bf16(N, H, W, Cin, Cout)
         wsb16 = torch.empty(wsbb // 4 + 1, device=dev)
+        wsbd = L.lib().pmu_conv3x3_wgrad_ws_bf16_dma(N, H, W, Cin, Cout)
+        wsd16 = torch.empty(wsbd // 4 + 1, device=dev)
         def packr(wt, dg):
             n = L.lib().pmu_conv3x3_packed_size_raw(wt.shape[0], wt.shape[1], int(dg)) // 2
             t = torch.empty(n, dtype=torch.int16, device=dev)
@@ -149,6 +151,8 @@ def main():
                                         dx.data_ptr(), None, s),
             "wgrad_bf16": lambda: L.call("pmu_conv3x3_wgrad_bf16", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin,
                                          dw.data_ptr(), wsb16.data_ptr(), wsbb, s),
+            "wgrad_bf16d": lambda: L.call("pmu_conv3x3_wgrad_bf16_dma", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout,
+                                          Cin, dw.data_ptr(), wsd16.data_ptr(), wsbd, s),
             "mat_bf16": lambda: (L.call("pmu_frame_to_bf16", fdz, cpo, dzt.data_ptr(), s),
                                  L.call("pmu_frame_to_bf16", fin, cpi, xt.data_ptr(), s)),
             "fwd_bf16": lambda: L.call("pmu_conv3x3_fwd_bf16", fin, wbf.data_ptr(), b.data_ptr(), Cout,
@@ -197,7 +201,7 @@ def main():
             tot.setdefault(op, [0.0, 0.0])
             tot[op][0] += ms
             tot[op][1] += flops
-            peak = 2516.0 if (op.endswith("bf16") or op.endswith("raw") or "dma" in op) else 157.3
+            peak = 2516.0 if (op.endswith("bf16") or op.endswith("bf16d") or op.endswith("raw") or "dma" in op) else 157.3
             print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / peak * 100:5.1f}%)",
                   flush=True)
     for op, (ms, fl) in tot.items():
