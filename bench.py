@@ -421,6 +421,7 @@ KERNEL_FAMILY = {
     "pmu_conv3x3_dgrad_dma_dxb": r"conv3x3_dma_kernel<true", "pmu_conv3x3_dgrad_dma_bnr_dxb": r"conv3x3_dma_kernel<true",
     "pmu_conv3x3_dgrad_dma_x1b_dxb": r"conv3x3_dma_kernel<true",
     "pmu_conv3x3_dgrad_dma_x1b_sum_dxb": r"conv3x3_dma_kernel<true",
+    "pmu_convT2x2_dgrad_dma_dxb": r"convT_dma_kernel<true",
     "pmu_convT2x2_fwd_ld": r"convT_pipe_kernel<false", "pmu_convT2x2_fwd_dma_ldb": r"convT_dma_kernel<false",
 }
 
@@ -494,7 +495,7 @@ def build_unet(args, dev, world, rank):
     crit = BCELoss() if args.classes == 1 else CrossEntropyLoss()
     batches = None
     if args.data == "phantom":
-        batches = phantom_batches(S, B, rank, world, dev)
+        batches, gather_rate = phantom_batches(S, B, rank, world, dev)
     else:
         x = torch.rand(B, args.channels, S, S, generator=g).to(dev)
         if args.classes == 1:
@@ -528,6 +529,7 @@ def build_unet(args, dev, world, rank):
 
     step.net = net
     step.batch = lambda: (x, tgt)
+    step.gather_rate = gather_rate if args.data == "phantom" else None
     flops = conv_flops_per_slice(S, S, FILTERS, args.channels, args.classes) * B
     lossn = "BCE" if args.classes == 1 else "CE"
     tag = "c5" if args.workload == "c5" else "c2"
@@ -569,7 +571,23 @@ def phantom_batches(S, B, rank, world, dev):
                 i = 0
             yield ds.get_batch(order[i:i + B])
             i += B
-    return gen()
+
+    def gather_rate(nb=50):
+        """The slicer's own rate (row a13 / f1): nb batches of B slices gathered back to back with no
+        training step, timed with HIP events on the launch stream (host index upload included)."""
+        it = gen()
+        next(it)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(nb):
+            next(it)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / nb
+        return {"slices_per_s": round(B / (ms * 1e-3), 1), "ms_per_batch": round(ms, 4), "batches": nb,
+                "batch": B, "note": "MRI_Dataset.get_batch alone: two pmu_gather_slices launches (image, mask)"}
+    return gen(), gather_rate
 
 
 def roofline_peak(kernel):
@@ -860,6 +878,8 @@ def main():
         }
         if evalres is not None:
             res["c5_volume_fusion_eval"] = evalres
+        if getattr(step, "gather_rate", None) is not None:
+            res["gather"] = step.gather_rate()
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

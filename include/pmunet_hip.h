@@ -272,6 +272,12 @@ int pmu_convT2x2_fwd_dma_ldb(const unsigned short* xt, int Cip, int N, int H, in
 int pmu_convT2x2_dgrad_dma(const unsigned short* dut, int Cop, int Hd, int Wd, int off_h, int off_w,
                            const unsigned short* wp, int N, int H, int W, int Cin, int Cout, float* dx,
                            void* stream);
+/* the same with dx stored as bf16 (RNE; autocast's dtype for ConvTranspose2d's input gradient,
+ * unet_parts.py:52 backward): its consumer's BN backward reads it (pmu_bn_bwd_reduce_dxb and the
+ * BN-backward frames) */
+int pmu_convT2x2_dgrad_dma_dxb(const unsigned short* dut, int Cop, int Hd, int Wd, int off_h, int off_w,
+                               const unsigned short* wp, int N, int H, int W, int Cin, int Cout, unsigned short* dx,
+                               void* stream);
 size_t pmu_convT2x2_wgrad_ws_bf16(int N, int H, int W, int Cin, int Cout);
 int pmu_convT2x2_wgrad_bf16(const unsigned short* xt, const unsigned short* dut, const float* du, int N, int H,
                             int W, int Hd, int Wd, int off_h, int off_w, int Cin, int Cout, float* dw,

@@ -44,7 +44,8 @@ def _dma_zb(x, cin, cout):
 # torch.autocast(bfloat16)'s conv backward returns the input gradient in bf16.  BF16_DX models the HIP
 # path's storage of it (include/pmunet_hip.h *_dxb entries, engine CFG.dx_bf16, on by default): the
 # convs whose input gradient runs on the LDS-DMA kernel (maps >= 32 wide, pad8(Cout) % 16 == 0,
-# Cin % 8 == 0, a concat split on a 32-channel boundary) round dx to bf16 once (RNE), and everything
+# Cin % 8 == 0, a concat split on a 32-channel boundary) and the transposed convs whose input gradient
+# does (Cin % 128 == 0, Cout % 32 == 0) round dx to bf16 once (RNE), and everything
 # downstream (BN backward, max-pool routing, the skip-gradient sum in fp32, the transposed conv's
 # input gradient and bias gradient) sees the rounded values.  False: fp32 dx (PMU_DX_BF16=0).
 BF16_DX = True
@@ -95,19 +96,21 @@ class Bf16ConvT2x2(torch.autograd.Function):
     the bias gradient sums the unrounded dy."""
 
     @staticmethod
-    def forward(ctx, x, w, b, fwd, dgrad):
+    def forward(ctx, x, w, b, fwd, dgrad, round_dx=False):
         ctx.save_for_backward(x, w)
-        ctx.dgrad, ctx.has_b = dgrad, b is not None
+        ctx.dgrad, ctx.has_b, ctx.round_dx = dgrad, b is not None, round_dx
         return F.conv_transpose2d(_rb(x) if fwd else x, _rb(w) if fwd else w, b, stride=2)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dx = F.conv2d(_rb(dy) if ctx.dgrad else dy, _rb(w) if ctx.dgrad else w, stride=2)
+        if ctx.round_dx:   # BF16_DX: pmu_convT2x2_dgrad_dma_dxb stores dx in bf16
+            dx = _rb(dx)
         n, k = dy.shape[0], dy.shape[1]
         dw = torch.einsum("ncij,nkiajb->ckab", _rb(x), _rb(dy).reshape(n, k, x.shape[2], 2, x.shape[3], 2))
         db = dy.sum((0, 2, 3)) if ctx.has_b else None
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def _conv3x3(x, w, b, bf16, round_dx=False):
@@ -150,7 +153,8 @@ def unet_forward(sd, x, n_levels, n_classes, apply_last_layer=True, training=Tru
         if bf16:  # the HIP path's bf16 convT where its kernels take the shapes (pmu_convT2x2_bf16_ok)
             cin, cout = wt.shape[0], wt.shape[1]
             fwd_b = cin % 32 == 0 and cout % 32 == 0 and (4 * cout) % 128 == 0
-            x1 = Bf16ConvT2x2.apply(x1, wt, sd[pre + "up.bias"], fwd_b, cin % 128 == 0 and cout % 32 == 0)
+            dma_d = cin % 128 == 0 and cout % 32 == 0   # pmu_convT2x2_dma_ok(cin, cout, 1)
+            x1 = Bf16ConvT2x2.apply(x1, wt, sd[pre + "up.bias"], fwd_b, dma_d, BF16_DX and dma_d)
         else:
             x1 = F.conv_transpose2d(x1, wt, sd[pre + "up.bias"], stride=2)
         dy, dx = x2.shape[2] - x1.shape[2], x2.shape[3] - x1.shape[3]

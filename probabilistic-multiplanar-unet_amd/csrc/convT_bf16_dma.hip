@@ -212,6 +212,26 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
   for (int fn = 0; fn < FN; ++fn) {
     const int col = n0 + bro[fn];
     if constexpr (DGRAD) {
+      if (g.outb) {
+        // bf16 dx (pmu_convT2x2_dgrad_dma_dxb; RNE) as 4-byte channel pairs, as the forward's bf16 output:
+        // the even lane stores row r's pair, the odd lane row r + 1's (Ncols % 128 == 0: pairs are aligned)
+        const int odd = lane & 1;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const unsigned b0 = __builtin_bit_cast(unsigned short, (__bf16)acc[fm][fn][r]);
+            const unsigned b1 = __builtin_bit_cast(unsigned short, (__bf16)acc[fm][fn][r + 1]);
+            const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);
+            const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
+            const int m = m0 + wm * 128 + fm * 32 + acc_row(r + odd, lane);
+            if (m < g.M) {
+              PMU_DCHECK(col < g.Ncols, PMU_DBG_OUTPUT);
+              *reinterpret_cast<unsigned*>(g.outb + (long long)m * g.Ncols + col - odd) = pair;
+            }
+          }
+        continue;
+      }
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
@@ -366,6 +386,21 @@ extern "C" int pmu_convT2x2_dgrad_dma(const unsigned short* dut, int Cop, int Hd
   PMU_REQUIRE(off_h >= 0 && off_w >= 0 && off_h + 2 * H <= Hd && off_w + 2 * W <= Wd);
   GArgs g{};
   g.a = dut; g.bp = wp; g.out = dx;
+  g.M = N * H * W; g.Ncols = Cin; g.K = 4 * Cout; g.lda = Cop;
+  g.H = H; g.W = W; g.Cout = Cout; g.Hd = Hd; g.Wd = Wd; g.oh = off_h; g.ow = off_w;
+  return launch<true>(g, stream);
+}
+
+// The input gradient stored as bf16 (RNE; the dtype torch.autocast's ConvTranspose2d backward returns it
+// in): the consumer's BN backward reads it (pmu_bn_bwd_reduce_dxb, the BN-backward frames).
+extern "C" int pmu_convT2x2_dgrad_dma_dxb(const unsigned short* dut, int Cop, int Hd, int Wd, int off_h, int off_w,
+                                          const unsigned short* wp, int N, int H, int W, int Cin, int Cout,
+                                          unsigned short* dx, void* stream) {
+  PMU_REQUIRE(dut && wp && dx && N > 0 && H > 0 && W > 0 && Cop >= Cout && Cop % 8 == 0);
+  PMU_REQUIRE(pmu_convT2x2_dma_ok(Cin, Cout, 1) && (long long)N * H * W < (1LL << 31));
+  PMU_REQUIRE(off_h >= 0 && off_w >= 0 && off_h + 2 * H <= Hd && off_w + 2 * W <= Wd);
+  GArgs g{};
+  g.a = dut; g.bp = wp; g.out = nullptr; g.outb = dx;
   g.M = N * H * W; g.Ncols = Cin; g.K = 4 * Cout; g.lda = Cop;
   g.H = H; g.W = W; g.Cout = Cout; g.Hd = Hd; g.Wd = Wd; g.oh = off_h; g.ow = off_w;
   return launch<true>(g, stream);

@@ -200,6 +200,8 @@ SIGNATURES = {
                                          c_void_p, c_int, c_void_p]),
     "pmu_convT2x2_dgrad_dma": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int,
                                        c_int, c_int, c_void_p, c_void_p]),
+    "pmu_convT2x2_dgrad_dma_dxb": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                           c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_wino2h_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pmu_conv3x3_dgrad_wino4_bnr": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
@@ -289,7 +291,7 @@ MFMA_ENTRY_POINTS = (
     # transposed convs
     "pmu_convT2x2_fwd", "pmu_convT2x2_fwd_ld", "pmu_convT2x2_dgrad", "pmu_convT2x2_wgrad",
     "pmu_convT2x2_fwd_bf16", "pmu_convT2x2_dgrad_bf16", "pmu_convT2x2_wgrad_bf16",
-    "pmu_convT2x2_fwd_dma", "pmu_convT2x2_fwd_dma_ldb", "pmu_convT2x2_dgrad_dma",
+    "pmu_convT2x2_fwd_dma", "pmu_convT2x2_fwd_dma_ldb", "pmu_convT2x2_dgrad_dma", "pmu_convT2x2_dgrad_dma_dxb",
     # the Probabilistic U-Net's Fcomb
     "pmu_fcomb_fwd", "pmu_fcomb_bwd",
 )

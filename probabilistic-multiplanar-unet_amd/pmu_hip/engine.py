@@ -1071,7 +1071,10 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         grads.flush()
         dskip[nlev - 2 - j] = dsk
         Hd, Wd = dup.shape[1], dup.shape[2]
-        dx = _empty(N, hi, wi, Cin_t, device=dev)
+        # bf16 dx from the LDS-DMA transposed-conv input gradient (CFG.dx_bf16): its consumer is the next
+        # layer's BN backward (pmu_bn_bwd_reduce_dxb, the BN-backward frames)
+        dxb = bool(us.bf16 and CFG.dx_bf16 and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 1))
+        dx = _empty(N, hi, wi, Cin_t, dtype=BF16S if dxb else F32, device=dev)
         dut = None
         dbpart = getattr(dup, "_pmu_dbpart", None)
         if dbpart is not None:
@@ -1081,8 +1084,8 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             dut = dut if dut is not None else frame_to_bf16([Src(dup)], N, Hd, Wd)
         if us.bf16 and L.lib().pmu_convT2x2_dma_ok(Cin_t, Cup, 1):
             wpt = pack_convT_weights_dma(convT.weight, dgrad=True)
-            L.call("pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd, Wd, us.off[0], us.off[1], wpt.data_ptr(),
-                   N, hi, wi, Cin_t, Cup, dx.data_ptr(), s)
+            L.call("pmu_convT2x2_dgrad_dma_dxb" if dxb else "pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd,
+                   Wd, us.off[0], us.off[1], wpt.data_ptr(), N, hi, wi, Cin_t, Cup, dx.data_ptr(), s)
         elif us.bf16 and Cin_t % 128 == 0 and Cup % 32 == 0 and L.experiments_build():
             wpt = pack_convT_weights_bf16(convT.weight, dgrad=True)
             L.call("pmu_convT2x2_dgrad_bf16", dup.data_ptr(), Hd, Wd, us.off[0], us.off[1], wpt.data_ptr(), N, hi, wi,

@@ -255,3 +255,26 @@ def test_unet_autocast_dx_storage(dev, dxb, filters, n_cls, N, H, W, C):
     named = dict(net.named_parameters())
     err, worst = grad_err({k: named[k].grad for k in keys}, gref)
     assert err <= tol_g, (err, worst, tol_g)
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,off", [(2, 32, 32, 128, 64, (0, 0)), (1, 16, 24, 256, 128, (1, 0)),
+                                                (2, 8, 8, 1024, 512, (0, 1))])
+def test_convT_dgrad_dma_dxb(dev, N, H, W, Cin, Cout, off):
+    """pmu_convT2x2_dgrad_dma_dxb: the bf16 (RNE) bits of pmu_convT2x2_dgrad_dma's dx (same kernel, same
+    sums), including an F.pad offset into du."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_to_bf16, pack_convT_weights_dma
+    g = torch.Generator().manual_seed(67 + H + Cin)
+    Hd, Wd = 2 * H + off[0] + 1, 2 * W + off[1]
+    du = torch.randn(N, Hd, Wd, Cout, generator=g).to(dev)
+    w = (torch.randn(Cin, Cout, 2, 2, generator=g) * 0.05).to(dev)
+    dut = frame_to_bf16([Src(du)], N, Hd, Wd)
+    wp = pack_convT_weights_dma(w, True)
+    ref = torch.empty(N, H, W, Cin, device=dev)
+    L.call("pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd, Wd, off[0], off[1], wp.data_ptr(), N, H, W, Cin,
+           Cout, ref.data_ptr(), L.stream())
+    got = torch.full((N, H, W, Cin), -1, dtype=torch.int16, device=dev)
+    L.call("pmu_convT2x2_dgrad_dma_dxb", dut.data_ptr(), dut.shape[3], Hd, Wd, off[0], off[1], wp.data_ptr(), N, H, W,
+           Cin, Cout, got.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(got, _bits(ref))
