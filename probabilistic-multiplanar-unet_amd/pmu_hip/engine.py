@@ -546,7 +546,7 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
         sp = Cin if split is None else split
         use_dma = dma_ok(H, W, dzt.shape[3], Cin, sp)
         # bf16 dx0 (the *_dxb entries; every other output formed from the rounded values)
-        xb = dx_bf16 and CFG.dx_bf16 and use_dma and Cin % 8 == 0 and sp % 8 == 0
+        xb = dx_bf16 and CFG.dx_bf16 and dxb_ok(H, W, Cout, Cin, sp)
         dx0 = _empty(N, H, W, sp, dtype=BF16S if xb else F32, device=dev)
         sfx = "_dxb" if xb else ""
         x1only = x1_bf16_only and sp < Cin and (Cin - sp) % 8 == 0 and use_dma
@@ -599,6 +599,13 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
     L.call("pmu_conv3x3_wgrad_bf16" + sfx, dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout, Cin, dw.data_ptr(),
            ws.data_ptr(), wsb, s)
     return res
+
+
+def dxb_ok(H, W, Cout, Cin, split) -> bool:
+    """The conv's input gradient runs on the LDS-DMA kernel and may store dx in bf16 (the *_dxb entries):
+    maps >= 32 wide, pad8(Cout) % 16 == 0, a concat split on a 32-channel boundary, Cin and the split
+    multiples of 8.  oracle/unet_ref.py's _dma_dxb models the same rule (tests/test_cpu_host.py)."""
+    return dma_ok(H, W, _pad8(Cout), Cin, split) and Cin % 8 == 0 and split % 8 == 0
 
 
 def dma_ok(H, W, Cp, NOUT, split) -> bool:

@@ -10,6 +10,8 @@ timeout -k 10 600 python -u -m pytest -v -p no:cacheprovider --timeout 300 --tim
 grep -E "PASSED|FAILED|Error" $O/new_tests.log | tail -60
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python tools/kbench.py --c5 --ops wgrad_bf16,wgrad_bf16d > $O/kbench_wgrad_c5.txt 2>&1 || exit $?
+timeout -k 10 300 python tools/kbench.py --ops dgrad_w4b,dgrad_w2hb > $O/kbench_dgrad_c2.txt 2>&1 || exit $?
+grep -E "TOTAL" $O/kbench_dgrad_c2.txt
 grep -E "TOTAL" $O/kbench_wgrad_c5.txt
 timeout -k 10 900 python -u -m pytest -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread tests > $O/tests_gpu.log 2>&1; rc=$?
 tail -5 $O/tests_gpu.log
@@ -21,4 +23,7 @@ for v in "PMU_DX_BF16=0 PMU_WGRAD_DMA=0" "PMU_DX_BF16=1 PMU_WGRAD_DMA=0" "PMU_DX
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o bench -- python3 $R/bench.py --workload c5 --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing --no-eval > $O/prof_c5.log 2>&1 || exit $?
+cd $R
+timeout -k 10 600 python bench.py --data phantom --no-cpu-baseline > $O/bench_c3_phantom.json 2> $O/bench_c3.err || exit $?
+python -c "import json;d=json.load(open('$O/bench_c3_phantom.json'));print('c3', d['value'], d.get('gather'))"
 echo r5b-done

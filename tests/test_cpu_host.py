@@ -289,3 +289,31 @@ def test_bench_refuses_gpus_world_mismatch():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2, r.stderr[-2000:]
     assert "WORLD_SIZE=2" in r.stderr and r.stdout.strip() == ""
+
+
+def test_oracle_bf16_dx_rule_matches_engine(monkeypatch):
+    """oracle/unet_ref.py models the HIP path's bf16 activation gradients (BF16_DX) by the same rule the
+    engine uses to pick the *_dxb input gradients (engine.dxb_ok, through the library's
+    pmu_conv3x3_dma_ok; the transposed conv: pmu_convT2x2_dma_ok) — checked here over a grid of shapes so
+    the parity tests compare like with like."""
+    import oracle.unet_ref as ur
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import dxb_ok
+    if not os.path.exists(L.LIB_PATH):
+        pytest.skip("library not built")
+    lb = L.load_library()   # host-side shape predicates only (no GPU call)
+    monkeypatch.setattr(L, "_LIB", lb)
+    assert ur.BF16_DX
+    x = torch.empty(1, 1, 1, 1)
+    for W in (16, 31, 32, 45, 64):
+        xx = x.expand(1, 1, 1, W)
+        for cin in (3, 8, 12, 32, 40, 64, 96, 128, 1024):
+            for cout in (8, 12, 16, 20, 32, 64, 1024):
+                for split in (None, 8, 16, 32, 64):
+                    if split is not None and split >= cin:
+                        continue
+                    want = dxb_ok(7, W, cout, cin, cin if split is None else split)
+                    assert ur._dma_dxb(xx, cin, cout, split) == want, (W, cin, cout, split)
+    for cin in (32, 64, 96, 128, 256, 1024):
+        for cout in (16, 32, 64, 512):
+            assert bool(lb.pmu_convT2x2_dma_ok(cin, cout, 1)) == (cin % 128 == 0 and cout % 32 == 0), (cin, cout)
