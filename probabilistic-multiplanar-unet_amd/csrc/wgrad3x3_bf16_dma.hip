@@ -40,14 +40,19 @@ static __device__ __attribute__((aligned(64))) unsigned g_wgd_zero[256];  // 1 K
 
 constexpr int SW = 16;  // strip width (pixels per k-step)
 
-// WCOF x WCIF x WS = 8 waves: co fragments x ci fragments x strip lanes
-template <int WCOF, int WCIF, int WS>
+// WCOF x WCIF x WS = 8 waves: co fragments x ci fragments x strip lanes; TPS step triplets per stage
+template <int WCOF, int WCIF, int WS, int TPS>
 struct WG {
   static_assert(WCOF * WCIF * WS == 8, "8 waves");
   static constexpr int NT = 512;
   static constexpr int ARU = 4 * WCOF, XRU = 4 * WCIF;      // 16-B units per pixel row
   static constexpr int A_ROW = SW * ARU, X_ROW = (SW + 2) * XRU;
-  static constexpr int A_UNITS = WS * 3 * A_ROW, X_UNITS = WS * 3 * X_ROW;
+  // a strip lane's three dz rows and three halo rows, each region rounded up to whole wave-instructions
+  // (64 units), so every DMA instruction moves one kind of one strip lane: its kind, lane and row step
+  // are uniform per (instruction, wave)
+  static constexpr int RPS = 3 * TPS;                        // rows per stage
+  static constexpr int A_LANE = (RPS * A_ROW + 63) / 64 * 64, X_LANE = (RPS * X_ROW + 63) / 64 * 64;
+  static constexpr int A_UNITS = WS * A_LANE, X_UNITS = WS * X_LANE;
   static constexpr int NI = (A_UNITS + X_UNITS + NT - 1) / NT;  // DMA instructions per wave per stage
   static constexpr int STAGE = NI * NT * 16;                      // bytes
   static constexpr int NS = (4 * STAGE <= 160 * 1024) ? 4 : 3;
@@ -90,9 +95,10 @@ __device__ __forceinline__ void wgd_wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
 }
 
-template <int WCOF, int WCIF, int WS>
+template <int WCOF, int WCIF, int WS, int TPS>
 __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
-  using G = WG<WCOF, WCIF, WS>;
+  using G = WG<WCOF, WCIF, WS, TPS>;
+  constexpr int RPS = G::RPS;
   constexpr int NS = G::NS, NI = G::NI;
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -110,51 +116,75 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
 
   // segment (lane sl, k-th of the block) -> image n, strip column c0, first row y0 (invalid: past the end,
   // y0 beyond the image so every unit reads the zero page)
-  auto seg_of = [&](int k, int sl, int& n, int& c0, int& y0) {
+  // segment (lane sl, k-th of the block) -> image n, strip column c0, first row y0 (none: k past the
+  // block's segments or the launch's — y0 beyond the image, so every unit reads the zero page)
+  auto seg_of = [&](int k, int sl, int& n, int& c0, int& y0) __attribute__((always_inline)) {
     const int s = (split * a.spb + k) * WS + sl;
-    if (s >= a.nseg) { n = 0; c0 = 0; y0 = a.H + 1; return; }
+    if (k >= a.spb || s >= a.nseg) { n = 0; c0 = 0; y0 = a.H + 1; return; }
     const int ys = s % a.nseg_strip;
     const int st = s / a.nseg_strip;
     c0 = (st % a.strips_w) * SW;
     n = st / a.strips_w;
-    y0 = ys * 3 * a.m;
+    y0 = ys * RPS * a.m;
   };
-  // DMA of stage index s (segment s / (m+1), step t = s % (m+1)) into ring slot s % NS.  Stage t = 0:
+  // DMA of stage index s (segment k = s / (m+1), step t = s % (m+1)) into ring slot s % NS.  Stage t = 0:
   // halo rows y0-1, y0, y0+1 (the prologue; dz rows unread); t >= 1: dz rows Y..Y+2 and halo rows
-  // Y+1..Y+3, Y = y0 + 3(t-1).  Lane unit U = (i * 8 + wave) * 64 + lane of the stage.
+  // Y+1..Y+3, Y = y0 + 3(t-1).  Lane unit U = (i * 8 + wave) * 64 + lane of the stage.  Stages are issued
+  // in order, so a cursor (dk, dt, slot) replaces the divisions; a segment's strip position is formed
+  // once per segment (uniform per strip lane), a unit's place in the stage (constant divisions) per stage
+  // — held across stages it cost the 64/64 layout 14 spilled registers.
   const char* zsrc = reinterpret_cast<const char*>(g_wgd_zero) + 16 * lane;
-  auto issue = [&](int s) {
-    const int k = s / (a.m + 1), t = s - k * (a.m + 1);
-    unsigned char* stg = smem + (s % NS) * G::STAGE;
+  // (element offsets in 32 bits: pmu_conv3x3_wgrad_dma_ok requires both operands below 2^31 elements)
+  const int rsA = a.W * a.Cop, rsX = a.W * a.Cip;
+  // A unit's source offset and row at step t = 1 are formed once per segment (ue, uy); a stage adds the
+  // uniform row step (recomputing the unit's place per stage cost ~25 VALU per unit: the kernel was
+  // issue-bound at ~10 non-MFMA instructions per MFMA).
+  // (re-deriving the row per stage from the unit index instead of holding uy measured 2-8% slower)
+  int ue[NI], uy[NI];
+  auto seg_setup = [&](int k) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int U = (i * 8 + wave) * 64 + lane;
-      const char* src = zsrc;
-      if (U < G::A_UNITS) {
-        const int sl = U / (3 * G::A_ROW);
-        const int r = U - sl * (3 * G::A_ROW);
-        const int j = r / G::A_ROW, pu = r - j * G::A_ROW;
-        const int px = pu / G::ARU, u = (pu % G::ARU) ^ wgd_sw<WCOF>(px);
-        int n, c0, y0;
-        seg_of(k, sl, n, c0, y0);
-        const int y = y0 + 3 * (t - 1) + j, x = c0 + px, c = co0 + 8 * u;
-        if (t > 0 && y < a.H && x < a.W && c < a.Cop)
-          src = reinterpret_cast<const char*>(a.dzt + ((((long long)n * a.H + y) * a.W + x) * a.Cop + c));
-      } else if (U < G::A_UNITS + G::X_UNITS) {
-        const int V = U - G::A_UNITS;
-        const int sl = V / (3 * G::X_ROW);
-        const int r = V - sl * (3 * G::X_ROW);
-        const int j = r / G::X_ROW, pu = r - j * G::X_ROW;
-        const int px = pu / G::XRU, u = (pu % G::XRU) ^ wgd_sw<WCIF>(px);
-        int n, c0, y0;
-        seg_of(k, sl, n, c0, y0);
-        const int y = (t == 0 ? y0 - 1 : y0 + 3 * t - 2) + j, x = c0 - 1 + px, c = ci0 + 8 * u;
-        if (y >= 0 && y < a.H && x >= 0 && x < a.W && c < a.Cip)
-          src = reinterpret_cast<const char*>(a.xt + ((((long long)n * a.H + y) * a.W + x) * a.Cip + c));
-      }
+      const int w = i * 8 + wave;                    // wave-instruction index of the stage (uniform)
+      const bool isA = w * 64 < G::A_UNITS;
+      const int sl = isA ? (w * 64) / G::A_LANE : (w * 64 - G::A_UNITS) / G::X_LANE;
+      const int r = isA ? w * 64 + lane - sl * G::A_LANE : w * 64 + lane - G::A_UNITS - sl * G::X_LANE;
+      const int j = isA ? r / G::A_ROW : r / G::X_ROW;
+      const int pu = r - j * (isA ? G::A_ROW : G::X_ROW);
+      const int px = isA ? pu / G::ARU : pu / G::XRU;
+      const int u = isA ? ((pu % G::ARU) ^ wgd_sw<WCOF>(px)) : ((pu % G::XRU) ^ wgd_sw<WCIF>(px));
+      int n, c0, y0;
+      seg_of(k, sl < WS ? sl : 0, n, c0, y0);
+      const int x = isA ? c0 + px : c0 - 1 + px;
+      const int c = 8 * u + (isA ? co0 : ci0);
+      const bool in = sl < WS && j < RPS && x >= 0 && x < a.W && c < (isA ? a.Cop : a.Cip);
+      const int y1 = y0 + j + (isA ? 0 : 1);         // the unit's row at stage t = 1
+      uy[i] = in ? y1 : -(1 << 28);                  // (outside: never inside [0, H))
+      ue[i] = ((n * a.H + y1) * a.W + x) * (isA ? a.Cop : a.Cip) + c;
+    }
+  };
+  int dk = 0, dt = 0, dslot = 0;
+  seg_setup(0);
+  auto issue = [&]() __attribute__((always_inline)) {
+    unsigned char* stg = smem + dslot * G::STAGE;
+    // rows relative to stage t = 1: dz RPS(t-1) (none at t = 0); halo RPS(t-1), at t = 0 -2 (y0-1, ..)
+    const int dyA = RPS * (dt - 1), dyX = dt == 0 ? -2 : RPS * (dt - 1);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const bool isA = (i * 8 + wave) * 64 < G::A_UNITS;   // (uniform)
+      const int dy = isA ? dyA : dyX;
+      const int y = uy[i] + dy;
+      const bool ok = (unsigned)y < (unsigned)a.H && (!isA || dt > 0);
+      const int e = ue[i] + dy * (isA ? rsA : rsX);
+      const char* src = !ok ? zsrc
+                            : isA ? reinterpret_cast<const char*>(a.dzt + e) : reinterpret_cast<const char*>(a.xt + e);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
                                        (__attribute__((address_space(3))) void*)(stg + (i * 8 + wave) * 1024), 16, 0,
                                        0);
+    }
+    dslot = dslot + 1 == NS ? 0 : dslot + 1;
+    if (++dt > a.m) {   // (uniform) the next stage starts a new segment
+      dt = 0;
+      seg_setup(++dk);
     }
   };
 
@@ -172,7 +202,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   // per lane (row j of the stage adds the immediate offset j * row bytes).
   const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane >> 2) & 3, p = lane & 3;
   const int ua = wco * 4 + 2 * g + (p >> 1), ux = wci * 4 + 2 * g + (p >> 1), hb = 8 * (p & 1);
-  const int aoff = wsl * 3 * G::A_ROW, xoff = G::A_UNITS + wsl * 3 * G::X_ROW;
+  const int aoff = wsl * G::A_LANE, xoff = G::A_UNITS + wsl * G::X_LANE;
   unsigned ra[2], rx[3][2];
 #pragma unroll
   for (int t2 = 0; t2 < 2; ++t2) {
@@ -189,16 +219,17 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   // the pending LDS-DMA writes and put an s_waitcnt vmcnt(0) before every stage's reads (the whole ring
   // drained each stage).  Their results are waited for by hand (wgd_wait_lgkm) behind a scheduling
   // barrier, so no MFMA moves above its wait.
-  auto rd_a = [&](unsigned st, auto J) {
+  auto rd_a = [&](unsigned st, auto J) __attribute__((always_inline)) {
     constexpr int OFF = decltype(J)::value * G::A_ROW * 16;
     return wgd_frag(wgd_tr<OFF>(st + ra[0]), wgd_tr<OFF>(st + ra[1]));
   };
-  auto rd_x = [&](unsigned st, auto J, bf16x8 (&o)[3]) {
+  auto rd_x = [&](unsigned st, auto J, bf16x8 (&o)[3]) __attribute__((always_inline)) {
     constexpr int OFF = decltype(J)::value * G::X_ROW * 16;
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) o[kw] = wgd_frag(wgd_tr<OFF>(st + rx[kw][0]), wgd_tr<OFF>(st + rx[kw][1]));
   };
-  auto mm = [&](const bf16x8& af, const bf16x8 (&k0)[3], const bf16x8 (&k1)[3], const bf16x8 (&k2)[3]) {
+  auto mm = [&](const bf16x8& af, const bf16x8 (&k0)[3], const bf16x8 (&k1)[3],
+                const bf16x8 (&k2)[3]) __attribute__((always_inline)) {
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       acc[0][kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, k0[kw], acc[0][kw], 0, 0, 0);
@@ -213,21 +244,48 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   // prologue: the first NS-1 stages in flight (stages past the end read the zero page or other segments
   // into slots nobody reads, so every wave issues NI DMAs per stage index and the counted waits hold)
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue(s);
+  for (int s = 0; s < NS - 1; ++s) issue();
   // (a segment's prologue and its triplets as nested loops: as the two arms of one per-stage branch,
   // the merged rotation registers spilled 150+ VGPRs)
-  int s = 0;
-  auto begin_stage = [&]() {
+  int rslot = 0;   // ring slot of stage s (s % NS)
+  auto begin_stage = [&]() __attribute__((always_inline)) {
     // stage s landed (this wave's DMAs: all but the NS-2 younger stages'), then every wave's, and every
     // read of stage s-1 — whose slot the next DMA overwrites — is done (its MFMAs consumed them)
     wgd_wait_vm<(NS - 2) * NI>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    issue(s + NS - 1);
+    issue();   // stage s + NS - 1, into the slot stage s - 1 used
     __builtin_amdgcn_sched_barrier(0);
-    return sbase + (unsigned)((s % NS) * G::STAGE);
+    const unsigned st = sbase + (unsigned)(rslot * G::STAGE);
+    rslot = rslot + 1 == NS ? 0 : rslot + 1;
+    return st;
   };
   bf16x8 B0[3], B1[3];  // halo rows y-1, y of the next step (per kw)
+  // triplet TT of a stage: steps on its rows 3TT .. 3TT+2 (read during the previous step's MFMAs)
+  auto triplets = [&](unsigned st, auto TT) __attribute__((always_inline)) {
+    constexpr int T0 = 3 * decltype(TT)::value;
+    bf16x8 x0[3], x1[3], x2[3];
+    const bf16x8 a0 = rd_a(st, std::integral_constant<int, T0>{});
+    rd_x(st, std::integral_constant<int, T0>{}, x0);
+    const bf16x8 a1 = rd_a(st, std::integral_constant<int, T0 + 1>{});
+    rd_x(st, std::integral_constant<int, T0 + 1>{}, x1);
+    wgd_wait_lgkm<8>();  // step y's 8 reads
+    __builtin_amdgcn_sched_barrier(0);
+    mm(a0, B0, B1, x0);
+    __builtin_amdgcn_sched_barrier(0);
+    const bf16x8 a2 = rd_a(st, std::integral_constant<int, T0 + 2>{});
+    rd_x(st, std::integral_constant<int, T0 + 2>{}, x2);
+    wgd_wait_lgkm<8>();  // step y+1's
+    __builtin_amdgcn_sched_barrier(0);
+    mm(a1, B1, x0, x1);
+    __builtin_amdgcn_sched_barrier(0);
+    wgd_wait_lgkm<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    mm(a2, x0, x1, x2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) { B0[kw] = x1[kw]; B1[kw] = x2[kw]; }
+  };
   for (int k = 0; k < a.spb; ++k) {
     {  // prologue of a segment: halo rows y0-1, y0
       const unsigned st = begin_stage();
@@ -235,31 +293,11 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
       rd_x(st, I1{}, B1);
       wgd_wait_lgkm<0>();
       __builtin_amdgcn_sched_barrier(0);
-      ++s;
     }
-    for (int t = 1; t <= a.m; ++t, ++s) {  // steps y, y+1, y+2: new halo rows y+1, y+2, y+3
+    for (int t = 1; t <= a.m; ++t) {  // TPS triplets of steps y, y+1, y+2: new halo rows y+1, y+2, y+3
       const unsigned st = begin_stage();
-      bf16x8 x0[3], x1[3], x2[3];
-      const bf16x8 a0 = rd_a(st, I0{});
-      rd_x(st, I0{}, x0);
-      const bf16x8 a1 = rd_a(st, I1{});
-      rd_x(st, I1{}, x1);
-      wgd_wait_lgkm<8>();  // step y's 8 reads
-      __builtin_amdgcn_sched_barrier(0);
-      mm(a0, B0, B1, x0);
-      __builtin_amdgcn_sched_barrier(0);
-      const bf16x8 a2 = rd_a(st, I2{});
-      rd_x(st, I2{}, x2);
-      wgd_wait_lgkm<8>();  // step y+1's
-      __builtin_amdgcn_sched_barrier(0);
-      mm(a1, B1, x0, x1);
-      __builtin_amdgcn_sched_barrier(0);
-      wgd_wait_lgkm<0>();
-      __builtin_amdgcn_sched_barrier(0);
-      mm(a2, x0, x1, x2);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) { B0[kw] = x1[kw]; B1[kw] = x2[kw]; }
+      triplets(st, std::integral_constant<int, 0>{});
+      if constexpr (TPS == 2) triplets(st, std::integral_constant<int, 1>{});
     }
   }
   wgd_wait_vm<0>();  // (the tail stages' DMAs: nothing of them is read; drained before the wave exits)
@@ -284,7 +322,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
 }
 
 struct WgdGeo {
-  int wcof, wcif, ws, nsplit, m, spb, nseg_strip, strips_w, nseg;
+  int wcof, wcif, ws, tps, nsplit, m, spb, nseg_strip, strips_w, nseg;
 };
 
 // Workgroup shape by channel counts, then the K split: about one workgroup per CU in all (256), whole
@@ -294,6 +332,9 @@ static WgdGeo wgd_geometry(int N, int H, int W, int Cin, int Cout) {
   if (Cout <= 64 && Cin <= 64) { g.wcof = 2; g.wcif = 2; g.ws = 2; }
   else if (Cout <= 64) { g.wcof = 2; g.wcif = 4; g.ws = 1; }
   else { g.wcof = 4; g.wcif = 2; g.ws = 1; }
+  // one step triplet per stage (TPS = 2, half the barriers per MFMA, spilled 26 VGPRs at its 160 KB ring)
+  g.tps = 1;
+  const int rps = 3 * g.tps;
   const int nb = pmu_cdiv(Cout, 32 * g.wcof) * pmu_cdiv(Cin, 32 * g.wcif);
   g.nsplit = 256 / nb;
   if (g.nsplit < 1) g.nsplit = 1;
@@ -301,9 +342,9 @@ static WgdGeo wgd_geometry(int N, int H, int W, int Cin, int Cout) {
   const long long strips = (long long)N * g.strips_w;
   const long long lanes = (long long)g.nsplit * g.ws;
   g.nseg_strip = strips >= lanes ? 1 : (int)((lanes + strips - 1) / strips);
-  if (g.nseg_strip > pmu_cdiv(H, 3)) g.nseg_strip = pmu_cdiv(H, 3);
-  g.m = pmu_cdiv(pmu_cdiv(H, g.nseg_strip), 3);
-  g.nseg_strip = pmu_cdiv(H, 3 * g.m);
+  if (g.nseg_strip > pmu_cdiv(H, rps)) g.nseg_strip = pmu_cdiv(H, rps);
+  g.m = pmu_cdiv(pmu_cdiv(H, g.nseg_strip), rps);
+  g.nseg_strip = pmu_cdiv(H, rps * g.m);
   g.nseg = (int)(strips * g.nseg_strip);
   if ((long long)g.nsplit * g.ws > g.nseg) g.nsplit = pmu_cdiv(g.nseg, g.ws);
   g.spb = pmu_cdiv(g.nseg, g.nsplit * g.ws);
@@ -315,7 +356,9 @@ static WgdGeo wgd_geometry(int N, int H, int W, int Cin, int Cout) {
 
 // Shapes the LDS-DMA weight gradient takes (the engine's default for bf16 maps at least 16 wide).
 extern "C" int pmu_conv3x3_wgrad_dma_ok(int N, int H, int W, int Cin, int Cout) {
-  return N > 0 && H > 0 && W >= SW && Cin > 0 && Cout > 0 && (long long)N * pmu_cdiv(W, SW) * H < (1LL << 30);
+  const long long px = (long long)N * H * W;
+  return N > 0 && H > 0 && W >= SW && Cin > 0 && Cout > 0 && px * ((Cin + 7) & ~7) < (1LL << 31) &&
+         px * ((Cout + 7) & ~7) < (1LL << 31);
 }
 
 extern "C" size_t pmu_conv3x3_wgrad_ws_bf16_dma(int N, int H, int W, int Cin, int Cout) {
@@ -339,9 +382,9 @@ extern "C" int pmu_conv3x3_wgrad_bf16_dma(const unsigned short* dzt, const unsig
   const int nb = pmu_cdiv(Cout, 32 * g.wcof) * pmu_cdiv(Cin, 32 * g.wcif);
   const dim3 grid((unsigned)(nb * g.nsplit)), blk(512);
   hipStream_t st = (hipStream_t)stream;
-  if (g.ws == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 2, 2>), grid, blk, 0, st, a);
-  else if (g.wcof == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 4, 1>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<4, 2, 1>), grid, blk, 0, st, a);
+  if (g.ws == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 2, 2, 1>), grid, blk, 0, st, a);
+  else if (g.wcof == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 4, 1, 1>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<4, 2, 1, 1>), grid, blk, 0, st, a);
   PMU_CHECK_LAUNCH();
   const long long E = 9LL * Cout * Cin;
   hipLaunchKernelGGL(pmu_splitk_reduce9_kernel, dim3((unsigned)pmu_cdiv(E, 64)), dim3(256), 0, st, (const float*)ws,
