@@ -344,6 +344,18 @@ int pmu_maxpool2_bwd_bnr(const float* dpool, const float* z, const float* coef, 
 int pmu_maxpool2_bwd_bnr_dxb(const unsigned short* dpool, const unsigned short* skip, const float* z,
                              const float* coef, const float* mean, const float* invstd, int N, int H, int W, int C,
                              float* dx, float* part, void* stream);
+/* The pooled layer's da = skip + routed dpool kept in registers instead of stored (config c5's skip
+ * levels): _stats_dxb forms only the partial sums above (bit-equal part); _bnbwd_dxb, given that
+ * layer's BN-backward coefficients (pmu_bn_bwd_finalize's bcoef) and its forward coef (the routing's
+ * argmax), writes dz = BN+ReLU backward of that da as the bf16 operand [N][H][W][ldo] of its input and
+ * weight gradients — bit-equal to pmu_frame_to_bf16 of Src(da, BNBWD) over the stored da.  ldo == C;
+ * C / 4 divides 256 or is a multiple of it. */
+int pmu_maxpool2_bwd_bnr_stats_dxb(const unsigned short* dpool, const unsigned short* skip, const float* z,
+                                   const float* coef, const float* mean, const float* invstd, int N, int H, int W,
+                                   int C, float* part, void* stream);
+int pmu_maxpool2_bwd_bnbwd_dxb(const unsigned short* dpool, const unsigned short* skip, const float* z,
+                               const float* coef, const float* bcoef, int N, int H, int W, int C, int ldo,
+                               unsigned short* dz, void* stream);
 /* AvgPool2d(2,2,ceil_mode=True) backward: dx = dpool/count(window), overwrite. */
 int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream);
 /* The same (bit-equal dx, here da: N x H x W x C at the pooled layer's resolution) fused with the BN+ReLU

@@ -91,6 +91,13 @@ int pmu_bn_bwd_reduce_zb(const float* da, const unsigned short* z, const float* 
 int pmu_maxpool2_bwd_zb(const float* dpool, const unsigned short* z, const float* coef, int N, int H, int W,
                         int C, float* dx, int accumulate, void* stream);
 
+/* ---- persistent tile schedule of the LDS-DMA convs (conv3x3_bf16_dma.hip PERS; PMU_DMA_PERS=1 turns
+ * it on for the pmu_conv3x3_*_dma entries of this library): 1 when a conv of this shape (NOUT outputs
+ * of a Cp-channel operand) would run it — one resident workgroup per slot walking a run of tiles, the
+ * next tile's first chunk fetched under the current one's last — else 0.  Bit-identical to the
+ * one-tile grid; measured slower. */
+int pmu_conv3x3_dma_persistent(int N, int H, int W, int NOUT, int Cp);
+
 /* ---- diagnostics of the direct-sum kernel */
 int pmu_occupancy_conv3x3_pipe(int* blocks_per_cu);
 

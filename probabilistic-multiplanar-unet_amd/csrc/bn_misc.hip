@@ -8,6 +8,8 @@
 //   clip_grad_value_ + SGD(momentum) (PMU/train.py:65,108-110)
 //   dice_coeff counts with argmax/one-hot (PMU/dice_loss.py:5-12, trainer/unet_trainer.py:39-58)
 // All reductions write per-block partial slabs that are summed in a fixed order (fp64).
+#include <algorithm>
+
 #include "pmu_stage.h"
 
 namespace {
@@ -421,7 +423,7 @@ __device__ __forceinline__ void mp_load(const DT* __restrict__ dpool, const floa
   m.g = pmu_ld4(dpool + po);
 }
 
-template <bool ACC>
+template <bool ACC, bool ST = true>
 __device__ __forceinline__ void mp_route(const MpWin& m, long long wi, bool valid, int H, int W, int C, int c,
                                          const float (&scv)[4], const float (&shv)[4], const float (&muv)[4],
                                          const float (&isv)[4], float* __restrict__ dx, float (&sg)[4], float (&sgx)[4]) {
@@ -462,6 +464,7 @@ __device__ __forceinline__ void mp_route(const MpWin& m, long long wi, bool vali
       sgx[e] = fmaf(gg, (zv[k][e] - muv[e]) * isv[e], sgx[e]);
     }
   }
+  if constexpr (!ST) return;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     if (!ok[k]) continue;
@@ -472,8 +475,62 @@ __device__ __forceinline__ void mp_route(const MpWin& m, long long wi, bool vali
   }
 }
 
+// The pooled layer's BN+ReLU backward applied to da = skip + routed dpool (bf16 inputs), written as the
+// bf16 operand dz of its input / weight gradients: the fp32 da maxpool2_bwd_bnr_kernel<.., ST> would
+// store, and pmu_frame_to_bf16 of Src(da, BNBWD) re-read, is formed in registers instead (same values:
+// the routing of mp_route, the formula of the frame streams, RNE), after the stats-only pass made the
+// coefficients.  A thread owns one channel quad of 2x2 windows, two windows in flight per step.
+__device__ __forceinline__ float mp_bnbwd1(float x, float z, float sc, float sh, float mu, float kx, float kc) {
+  return fmaf(sc, fmaf(z, sc, sh) > 0.f ? x : 0.f, fmaf(kx, z - mu, kc));
+}
+struct MpBwdCoef {
+  float sc[4], sh[4];                           // forward BN scale / shift (the max-pool's argmax)
+  float bsc[4], bsh[4], mu[4], kx[4], kc[4];    // backward coefficients (bcoef, 5 C)
+};
+__device__ __forceinline__ void mp_apply(const MpWin& m, long long wi, bool valid, int H, int W, int c, int ldo,
+                                         long long lim, const MpBwdCoef& k, unsigned short* __restrict__ out) {
+  const int Hp = H / 2, Wp = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
+  const int wc = (int)(wi % Wc);
+  const long long r = wi / Wc;
+  const int hc = (int)(r % Hc);
+  const int n = (int)(r / Hc);
+  const bool full = hc < Hp && wc < Wp;
+  float zv[4][4], dv[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    zv[q][0] = m.z[q].x; zv[q][1] = m.z[q].y; zv[q][2] = m.z[q].z; zv[q][3] = m.z[q].w;
+    dv[q][0] = m.d[q].x; dv[q][1] = m.d[q].y; dv[q][2] = m.d[q].z; dv[q][3] = m.d[q].w;
+  }
+  const float gv[4] = {full ? m.g.x : 0.f, full ? m.g.y : 0.f, full ? m.g.z : 0.f, full ? m.g.w : 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float best = fmaxf(0.f, fmaf(zv[0][e], k.sc[e], k.sh[e]));
+    int arg = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float a = fmaxf(0.f, fmaf(zv[q][e], k.sc[e], k.sh[e]));
+      if (a > best) { best = a; arg = q; }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dv[q][e] += arg == q ? gv[e] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int h = 2 * hc + (q >> 1), w = 2 * wc + (q & 1);
+    if (!valid || h >= H || w >= W) continue;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = mp_bnbwd1(dv[q][e], zv[q][e], k.bsc[e], k.bsh[e], k.mu[e], k.kx[e], k.kc[e]);
+    const long long off = (((long long)n * H + h) * W + w) * ldo + c;
+    PMU_DCHECK(off + 4 <= lim, PMU_DBG_OUTPUT);
+    (void)lim;
+    *reinterpret_cast<uint2*>(out + off) = make_uint2(pmu_pk_bf16(o[0], o[1]), pmu_pk_bf16(o[2], o[3]));
+  }
+}
+
 // base: the skip gradient accumulated into (ACC; dx itself for fp32, a bf16 tensor for DT = bf16)
-template <bool ACC, class DT = float>
+// ST = false: the partial sums only (da not stored: maxpool2_bwd_bnbwd_kernel re-forms it)
+template <bool ACC, class DT = float, bool ST = true>
 __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const DT* __restrict__ dpool,
                                                                const float* __restrict__ z,
                                                                const float* __restrict__ coef,
@@ -512,11 +569,11 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const DT* __restr
         const long long wb = wi + npg, wa = wi + 2 * npg;
         mp_load<ACC>(dpool, z, base, min(wb, last), H, W, C, c, B);
         __builtin_amdgcn_sched_barrier(0);
-        mp_route<ACC>(A, wi, true, H, W, C, c, scv, shv, muv, isv, dx, sg, sgx);
+        mp_route<ACC, ST>(A, wi, true, H, W, C, c, scv, shv, muv, isv, dx, sg, sgx);
         __builtin_amdgcn_sched_barrier(0);
         mp_load<ACC>(dpool, z, base, min(wa, last), H, W, C, c, A);
         __builtin_amdgcn_sched_barrier(0);
-        mp_route<ACC>(B, min(wb, last), wb < wend, H, W, C, c, scv, shv, muv, isv, dx, sg, sgx);
+        mp_route<ACC, ST>(B, min(wb, last), wb < wend, H, W, C, c, scv, shv, muv, isv, dx, sg, sgx);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -537,6 +594,41 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const DT* __restr
       }
     }
     __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool2_bwd_bnbwd_kernel(const unsigned short* __restrict__ dpool,
+                                                                 const unsigned short* __restrict__ skip,
+                                                                 const float* __restrict__ z,
+                                                                 const float* __restrict__ coef,
+                                                                 const float* __restrict__ bcoef, int N, int H, int W,
+                                                                 int C, int ldo, unsigned short* __restrict__ out) {
+  const int CQ = C >> 2, qs = CQ < 256 ? CQ : 256, wpt = 256 / qs;  // windows per block step
+  const int q0 = threadIdx.x % qs, wl = threadIdx.x / qs;
+  const long long nwin = (long long)N * ((H + 1) / 2) * ((W + 1) / 2), last = nwin - 1;
+  const long long lim = (long long)N * H * W * ldo;
+  const long long step = (long long)gridDim.x * wpt;
+  for (int qb = 0; qb < CQ; qb += qs) {  // (qs divides CQ: C % 4 == 0 and CQ < 256 or CQ % 256 == 0)
+    const int c = 4 * (qb + q0);
+    MpBwdCoef k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      k.sc[e] = coef[c + e];
+      k.sh[e] = coef[C + c + e];
+      k.bsc[e] = bcoef[c + e];
+      k.bsh[e] = bcoef[C + c + e];
+      k.mu[e] = bcoef[2 * C + c + e];
+      k.kx[e] = bcoef[3 * C + c + e];
+      k.kc[e] = bcoef[4 * C + c + e];
+    }
+    for (long long wi = (long long)blockIdx.x * wpt + wl; wi < nwin; wi += 2 * step) {
+      const long long wj = wi + step;
+      MpWin A, B;
+      mp_load<true, unsigned short>(dpool, z, skip, wi, H, W, C, c, A);
+      mp_load<true, unsigned short>(dpool, z, skip, min(wj, last), H, W, C, c, B);
+      mp_apply(A, wi, true, H, W, c, ldo, lim, k, out);
+      mp_apply(B, min(wj, last), wj < nwin, H, W, c, ldo, lim, k, out);
+    }
   }
 }
 
@@ -1476,6 +1568,35 @@ extern "C" int pmu_maxpool2_bwd_bnr_dxb(const unsigned short* dpool, const unsig
     hipLaunchKernelGGL((maxpool2_bwd_bnr_kernel<false, unsigned short>), dim3((unsigned)R), dim3(256), 0,
                        (hipStream_t)stream, dpool, z, coef, mean, invstd, N, H, W, C, mpb_wpb(C), dx, part,
                        (const unsigned short*)nullptr);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+// The stats-only form of pmu_maxpool2_bwd_bnr_dxb (da not stored) and the pass that turns the same da
+// into the pooled layer's bf16 dz (see maxpool2_bwd_bnbwd_kernel).
+extern "C" int pmu_maxpool2_bwd_bnr_stats_dxb(const unsigned short* dpool, const unsigned short* skip, const float* z,
+                                              const float* coef, const float* mean, const float* invstd, int N,
+                                              int H, int W, int C, float* part, void* stream) {
+  PMU_REQUIRE(dpool && skip && z && coef && mean && invstd && part && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
+  const int R = pmu_maxpool2_bwd_bnr_tiles(N, H, W, C);
+  hipLaunchKernelGGL((maxpool2_bwd_bnr_kernel<true, unsigned short, false>), dim3((unsigned)R), dim3(256), 0,
+                     (hipStream_t)stream, dpool, z, coef, mean, invstd, N, H, W, C, mpb_wpb(C), (float*)nullptr, part,
+                     skip);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_maxpool2_bwd_bnbwd_dxb(const unsigned short* dpool, const unsigned short* skip, const float* z,
+                                          const float* coef, const float* bcoef, int N, int H, int W, int C, int ldo,
+                                          unsigned short* dz, void* stream) {
+  PMU_REQUIRE(dpool && skip && z && coef && bcoef && dz && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0 && ldo == C);
+  const int CQ = C / 4;
+  PMU_REQUIRE(CQ < 256 ? 256 % CQ == 0 : CQ % 256 == 0);
+  const int wpt = 256 / (CQ < 256 ? CQ : 256);
+  const long long nwin = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);
+  const long long blocks = std::min<long long>(pmu_cdiv(nwin, 2LL * wpt), 1LL << 20);
+  hipLaunchKernelGGL(maxpool2_bwd_bnbwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dpool, skip,
+                     z, coef, bcoef, N, H, W, C, ldo, dz);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

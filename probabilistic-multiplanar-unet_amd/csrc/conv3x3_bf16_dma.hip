@@ -18,6 +18,7 @@
 // bit 3 of p).  A 32-lane fragment read (32 consecutive pixels, one half) then hits 16 distinct
 // 4-bank groups in each ds_read_b128 lane group, for any starting pixel (every tap).  The weights are
 // packed in the same order (channel co in place of the pixel), so their DMA is a straight copy.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -73,6 +74,17 @@ struct DmaArgs {
 };
 
 __device__ __forceinline__ int swz(int p, int q) { return 2 * p + (q ^ ((p >> 3) & 1)); }
+
+// Output stores that do not stay in the XCD's L2 (relaxed agent-scope atomic stores: `sc1`, written
+// through and dropped): z / dx are next read by another kernel, long after they would have left L2,
+// and kept lines evict the operand halo that the next chunks of the resident tiles re-read.
+__device__ __forceinline__ void st_drop(float* p, float2 v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_drop(unsigned short* p, unsigned v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ unsigned short bf16_bits(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
 
 // wp[jb][ch][tap][u][e]: unit u = swz(co, q) holds B[tap][k = 16 ch + 8 q + e][j = BN jb + co], zero
@@ -128,47 +140,95 @@ __global__ __launch_bounds__(256) void pack_dma_multi_kernel(const pmu_pack_job*
 // producer's BN-backward partials all taken from the rounded values.  Halves the bytes of the
 // activation-gradient stream its consumers (the BN-backward dz stream, the max-pool backward, the
 // first layer's weight gradient) read.
-template <bool DGRAD, bool ZB, int WN, int NWV, int EXP = 0, bool CS = false, bool XB = false>
+// PERS (persistent): one resident workgroup per slot walks a run of tiles of one channel block (its
+// XCD's share of the tiles, interleaved with the other slots of that XCD): the next tile's chunk 0 is
+// fetched during the last chunk of the current one, so no tile pays the DMA round trip of its first
+// chunk or a workgroup launch, and the 2 workgroups of a CU drift out of phase (one's epilogue
+// stores under the other's MFMAs).  Needs an even chunk count (the operand-buffer parity restarts at
+// every tile) and a slot count per XCD divisible by the channel blocks (launch_dma).  Experiments
+// build only (PMU_DMA_PERS=1): bit-identical to the one-tile grid (tests/test_dma_pers_gpu.py) but
+// SLOWER on every c5 shape — kbench --c5 fwd 4.92 vs 4.37 ms, dgrad 6.45 vs 4.73 (profiles/r05/pers):
+// state carried across the tile loop spills 60-80 VGPRs, and a scratch reload in the chunk loop waits
+// (in-order vmcnt) for the DMA issued before it, serialising the fetch pipeline.
+template <bool DGRAD, bool ZB, int WN, int NWV, int EXP = 0, bool CS = false, bool XB = false, bool PERS = false>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs a) {
   using G = DG<WN, NWV>;
   constexpr int FM = 4, FN = 2, BN = G::BN, WM = G::WM, TH = G::TH, NT = G::NT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE];
+  // (PERS: the epilogue's reduction area apart from the stages, which hold the next tile's chunk 0)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::STAGE + (PERS ? NT * 8 : 0)];
   // the wave index as a uniform (SGPR) value: the epilogue's row pointers derive from it
   const int tid = threadIdx.x, lane = tid & 63, wave = DGRAD ? tid >> 6 : __builtin_amdgcn_readfirstlane(tid >> 6);
   // (spatial tile, channel block), channel blocks fastest in XCD order: the channel blocks of one
   // tile share its halo image through their XCD's L2
-  const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
-  const int cb = lb % a.ncb;
-  int t = lb / a.ncb;
-  const int tsp = t;
-  const int tw = t % a.tiles_w;
-  t /= a.tiles_w;
-  const int th = t % a.tiles_h;
-  const int n = t / a.tiles_h;
-  const int h0 = th * TH, w0 = tw * TW, j0 = cb * BN;
+  int cb, tcur, tend = 0, tstride = 0;
+  if constexpr (PERS) {
+    // slot s of XCD x (workgroups are dispatched round-robin over the 8 XCDs): channel block s % ncb,
+    // tiles start + s / ncb, + nsl / ncb, ... of the XCD's contiguous share [start, tend)
+    const int x = blockIdx.x & 7, s = blockIdx.x >> 3, nsl = gridDim.x >> 3;
+    const int T = a.N * a.tiles_h * a.tiles_w, q = T >> 3, r = T & 7;
+    const int start = x * q + (x < r ? x : r);
+    cb = s % a.ncb;
+    tend = start + q + (x < r ? 1 : 0);
+    tstride = nsl / a.ncb;
+    tcur = start + s / a.ncb;
+    if (tcur >= tend) return;
+  } else {
+    const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
+    cb = lb % a.ncb;
+    tcur = lb / a.ncb;
+  }
+  const int j0 = cb * BN;
+  int tsp, n, h0, w0;
+  auto coords = [&](int t, int& tn, int& th0, int& tw0) {
+    const int tw = t % a.tiles_w;
+    t /= a.tiles_w;
+    th0 = (t % a.tiles_h) * TH;
+    tn = t / a.tiles_h;
+    tw0 = tw * TW;
+  };
+  tsp = tcur;
+  coords(tcur, n, h0, w0);
   PMU_DCHECK(n < a.N && j0 < a.NOUT, PMU_DBG_GRID);
 
+  f32x16 acc[FM][FN];
+  bf16x8 op[2][FM + FN];
+  bool first = true;
+  for (;;) {  // tiles (one unless PERS)
+  // (PERS: the lane is opaque per tile, so every lane-derived address is formed inside the tile
+  // instead of hoisted out of the tile loop and held through the epilogue: 100-200 VGPRs spilled)
+  int tl = lane;
+  if constexpr (PERS) asm volatile("" : "+v"(tl));
   // operand units of this thread (DMA round r: unit (r * 8 + wave) * 64 + lane): 32-bit byte offset
   // of chunk 0 and whether the unit is inside the image; units outside it are zero in both stages
   unsigned goff[G::NGA];
   unsigned gin = 0u;
+  auto offsets = [&](int tn, int th0, int tw0) {
+    gin = 0u;
 #pragma unroll
-  for (int r = 0; r < G::NGA; ++r) {
-    const int u = (r * NWV + wave) * 64 + lane;
-    const bool data = u < G::A_UNITS;
-    const int hp = u >> 1, q = (u & 1) ^ ((hp >> 3) & 1);
-    const int hr = hp / HW2, hc = hp - hr * HW2;
-    const int h = h0 - 1 + hr, w = w0 - 1 + hc;
-    const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
-    goff[r] = in ? (unsigned)(((((long long)n * a.H + h) * a.W + w) * a.Cp + 8 * q) * 2) : 0u;
-    PMU_DCHECK(!in || (((long long)n * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
-    gin |= in ? (1u << r) : 0u;
-    if (data && !in) {
-      *reinterpret_cast<uint4*>(smem + 16 * u) = make_uint4(0u, 0u, 0u, 0u);
-      *reinterpret_cast<uint4*>(smem + G::STAGE + 16 * u) = make_uint4(0u, 0u, 0u, 0u);
+    for (int r = 0; r < G::NGA; ++r) {
+      const int u = (r * NWV + wave) * 64 + tl;
+      const bool data = u < G::A_UNITS;
+      const int hp = u >> 1, q = (u & 1) ^ ((hp >> 3) & 1);
+      const int hr = hp / HW2, hc = hp - hr * HW2;
+      const int h = th0 - 1 + hr, w = tw0 - 1 + hc;
+      const bool in = data && h >= 0 && w >= 0 && h < a.H && w < a.W;
+      // (32-bit: the operand is under 4 GB, launch_dma; every partial product is at most the offset)
+      goff[r] = in ? ((((unsigned)tn * a.H + h) * a.W + w) * a.Cp + 8 * q) * 2u : 0u;
+      PMU_DCHECK(!in || (((long long)tn * a.H + h) * a.W + w) < (long long)a.N * a.H * a.W, PMU_DBG_OPERAND);
+      gin |= in ? (1u << r) : 0u;
     }
-  }
-  const char* wsrc = reinterpret_cast<const char*>(a.wp) + (long long)cb * a.nch * G::B_UNITS * 16 + 16 * lane;
+  };
+  // zero the units outside the image in one stage (the DMA skips them); PERS: before each tile's
+  // first two fetches, the stages' previous contents being another tile's
+  auto zero_stage = [&](unsigned char* st) {
+#pragma unroll
+    for (int r = 0; r < G::NGA; ++r) {
+      const int u = (r * NWV + wave) * 64 + tl;
+      if (u < G::A_UNITS && !((gin >> r) & 1u)) *reinterpret_cast<uint4*>(st + 16 * u) = make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  offsets(n, h0, w0);
+  const char* wsrc = reinterpret_cast<const char*>(a.wp) + (long long)cb * a.nch * G::B_UNITS * 16 + 16 * tl;
 
 #define PMU_GLDS(S, D)                                                                                      \
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S),                     \
@@ -182,34 +242,33 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       if ((gin >> r) & 1u) PMU_GLDS(xa_ + goff[r], st_ + (r * NWV + wave) * 1024)                         \
     const char* wb_ = wsrc + (long long)(CH) * G::B_UNITS * 16;                                            \
     _Pragma("unroll") for (int r = 0; r < G::NGB; ++r)                                                     \
-      if ((r + 1) * NT <= G::B_UNITS || (r * NWV + wave) * 64 + lane < G::B_UNITS)                          \
+      if ((r + 1) * NT <= G::B_UNITS || (r * NWV + wave) * 64 + tl < G::B_UNITS)                            \
         PMU_GLDS(wb_ + (r * NWV + wave) * 1024, st_ + G::A_BYTES + (r * NWV + wave) * 1024)               \
   }
 
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-  const int q = lane >> 5, li = lane & 31;
+  const int q = tl >> 5, li = tl & 31;
   const int hpb = 4 * wm * HW2 + li;           // halo pixel of fragment 0, tap (0, 0)
   int ub[FN];
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) ub[fn] = G::A_BYTES + 16 * swz(wn * 64 + fn * 32 + li, q);
 
-  f32x16 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  PMU_FETCH(0, smem)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (!PERS || first) {
+    if constexpr (PERS) {
+      zero_stage(smem);
+    } else {
+      zero_stage(smem);
+      zero_stage(smem + G::STAGE);
+    }
+    PMU_FETCH(0, smem)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }  // (PERS, later tiles: chunk 0 fetched, landed and past the barrier in the last tile's last chunk)
   // One operand set per tap in two register buffers; tap t+1's reads are issued during tap t's MFMAs,
   // and the next chunk's tap 0 during this chunk's tap 8: the chunk barrier (its DMA landed, every
   // wave done reading the stage the following fetch overwrites) sits between two taps' MFMA groups,
   // not between a barrier and the first LDS round trip of a chunk.  9 taps per chunk flip the buffer
   // parity every chunk, so chunks run in compile-time-parity pairs.
-  bf16x8 op[2][FM + FN];
   auto load_tap = [&](const unsigned char* cur, int tap, bf16x8 (&o)[FM + FN]) {
     const int dy = tap / 3, dx = tap - 3 * (tap / 3);
 #pragma unroll
@@ -220,12 +279,27 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) o[FM + fn] = *reinterpret_cast<const bf16x8*>(cur + ub[fn] + tap * (32 * BN));
   };
+  // (PERS) the next tile of this slot: tnext, at (nn, nh0, nw0)
+  int tnext = 0, nn = 0, nh0 = 0, nw0 = 0;
+  bool has_next = false;
+  if constexpr (PERS) {
+    tnext = tcur + tstride;
+    has_next = tnext < tend;
+    if (has_next) coords(tnext, nn, nh0, nw0);
+  }
   auto run_chunk = [&](int ch, auto par) {
     constexpr int P = decltype(par)::value;
     const unsigned char* cur = smem + (ch & 1) * G::STAGE;
     const unsigned char* nxt = smem + ((ch + 1) & 1) * G::STAGE;
-    const bool more = ch + 1 < a.nch;
-    if (more) PMU_FETCH(ch + 1, smem + ((ch + 1) & 1) * G::STAGE)
+    const bool more = ch + 1 < a.nch || has_next;
+    if (ch + 1 < a.nch) {
+      if (PERS && ch == 0) zero_stage(smem + G::STAGE);
+      PMU_FETCH(ch + 1, smem + ((ch + 1) & 1) * G::STAGE)
+    } else if (PERS && has_next) {  // the next tile's chunk 0 (into stage 0: nch is even)
+      offsets(nn, nh0, nw0);
+      zero_stage(smem);
+      PMU_FETCH(0, smem)
+    }
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       // this tap's operands (read during the previous tap's MFMAs) have landed: wait for them BEFORE
@@ -239,7 +313,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's share of chunk ch + 1 landed
         __builtin_amdgcn_s_barrier();                      // everyone's, and every read of chunk ch - 1 done
         __builtin_amdgcn_sched_barrier(0);
-        load_tap(nxt, 0, op[(9 + P) & 1]);
+        // (PERS, last chunk: the next tile's tap 0 is read at that tile's start, not held through the
+        // epilogue)
+        if (!PERS || ch + 1 < a.nch) load_tap(nxt, 0, op[(9 + P) & 1]);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -253,19 +329,26 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     }
   };
   load_tap(smem, 0, op[0]);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   int ch = 0;
   for (; ch + 1 < a.nch; ch += 2) {
     run_chunk(ch, std::integral_constant<int, 0>{});
     run_chunk(ch + 1, std::integral_constant<int, 1>{});
   }
-  if (ch < a.nch) run_chunk(ch, std::integral_constant<int, 0>{});
-  __syncthreads();  // every wave's last reads are done before the epilogue reuses the stages
-#undef PMU_FETCH
-#undef PMU_GLDS
+  if (!PERS && ch < a.nch) run_chunk(ch, std::integral_constant<int, 0>{});
+  if constexpr (!PERS) __syncthreads();  // every wave's last reads are done before the epilogue reuses the stages
 
-  // epilogue: accumulator (fm, fn, r) = output pixel (tile row 4 wm + fm, column acc_row(r, lane)),
-  // channel j0 + 64 wn + 32 fn + (lane & 31); a 32-channel destination is uniform (split % 32 == 0).
-  float* red = reinterpret_cast<float*>(smem);  // [NWV waves][64][2] (the stages are free now)
+  const int elane = tl, ej0 = j0;
+  const int eli = elane & 31;
+  // epilogue: accumulator (fm, fn, r) = output pixel (tile row 4 wm + fm, column acc_row(r, elane)),
+  // channel ej0 + 64 wn + 32 fn + (elane & 31); a 32-channel destination is uniform (split % 32 == 0).
+  // [NWV waves][64][2] (non-PERS: in the stages, free now)
+  float* red = reinterpret_cast<float*>(smem + (PERS ? 2 * G::STAGE : 0));
   float s1[FN], s2[FN];
   if constexpr (!DGRAD) {
     // Forward: values and BN sums formed unconditionally (masked), only the stores predicated.  With the
@@ -278,17 +361,17 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     for (int fn = 0; fn < FN; ++fn) {
       s1[fn] = 0.f;
       s2[fn] = 0.f;
-      const int j = j0 + wn * 64 + fn * 32 + li;
+      const int j = ej0 + wn * 64 + fn * 32 + eli;
       jok[fn] = j < a.NOUT;
       const int jc = jok[fn] ? j : a.NOUT - 1;
       bv[fn] = a.bias ? a.bias[jc] : 0.f;
       zov[fn] = (ZB && a.zoff) ? a.zoff[jc] : 0.f;
     }
     // (ZB = false, NOUT even) z as 8-byte channel pairs: lanes 2k, 2k+1 hold adjacent channels of the
-    // same pixels r, r + 1; one xor-1 shuffle gives the even lane pixel r's pair and the odd lane pixel
+    // same pixels r, r + 1; one xor-1 shuffle gives the even elane pixel r's pair and the odd elane pixel
     // r + 1's — half the store instructions (the bf16 ConvT forward gained 23% from the same change)
     const bool pairs = !ZB && (a.NOUT & 1) == 0;
-    const int odd = lane & 1;
+    const int odd = elane & 1;
   #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
       const int h = h0 + 4 * wm + fm;
@@ -298,12 +381,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       if (pairs) {
   #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
-          const int j = j0 + wn * 64 + fn * 32 + li;
+          const int j = ej0 + wn * 64 + fn * 32 + eli;
   #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const float v0 = acc[fm][fn][r] + bv[fn], v1 = acc[fm][fn][r + 1] + bv[fn];
-            const bool ok0 = jok[fn] && h < a.H && w0 + acc_row(r, lane) < a.W;
-            const bool ok1 = jok[fn] && h < a.H && w0 + acc_row(r + 1, lane) < a.W;
+            const bool ok0 = jok[fn] && h < a.H && w0 + acc_row(r, elane) < a.W;
+            const bool ok1 = jok[fn] && h < a.H && w0 + acc_row(r + 1, elane) < a.W;
             const float m0 = ok0 ? v0 : 0.f, m1 = ok1 ? v1 : 0.f;
             s1[fn] += m0;
             s2[fn] = fmaf(m0, m0, s2[fn]);
@@ -311,20 +394,20 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
             s2[fn] = fmaf(m1, m1, s2[fn]);
             const float recv = __shfl_xor(odd ? v0 : v1, 1, 64);
             const float2 pv = odd ? make_float2(recv, v1) : make_float2(v0, recv);
-            const int w = w0 + acc_row(r + odd, lane);
+            const int w = w0 + acc_row(r + odd, elane);
             if (!(jok[fn] && h < a.H && w < a.W) || (EXP & 1)) continue;
             PMU_DCHECK(((long long)n * a.H + h) * a.W + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-            *reinterpret_cast<float2*>(drow + (unsigned)(w * a.NOUT + j - odd)) = pv;
+            st_drop(drow + (unsigned)(w * a.NOUT + j - odd), pv);
           }
         }
         continue;
       }
   #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        const int j = j0 + wn * 64 + fn * 32 + li;
+        const int j = ej0 + wn * 64 + fn * 32 + eli;
   #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int w = w0 + acc_row(r, lane);
+          const int w = w0 + acc_row(r, elane);
           const bool ok = jok[fn] && h < a.H && w < a.W;
           float v = acc[fm][fn][r] + bv[fn];
           unsigned short vb = 0;
@@ -354,8 +437,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     for (int fn = 0; fn < FN; ++fn) {
       s1[fn] = 0.f;
       s2[fn] = 0.f;
-      const int jb = j0 + wn * 64 + fn * 32;
-      const int j = jb + li;
+      const int jb = ej0 + wn * 64 + fn * 32;
+      const int j = jb + eli;
       const bool jok = j < a.NOUT;
       float* dstp;
       int ld;
@@ -374,42 +457,42 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
         const int h = h0 + 4 * wm + fm;
         if (dstb) {
           // the bf16 copy as 4-byte channel pairs: lanes 2k, 2k+1 hold adjacent channels of the same
-          // pixels r, r + 1; one xor-1 shuffle gives the even lane pixel r's pair and the odd lane pixel
+          // pixels r, r + 1; one xor-1 shuffle gives the even elane pixel r's pair and the odd elane pixel
           // r + 1's (half the store instructions of 2-byte stores; dstb is uniform per fragment, so the
           // whole wave runs the shuffles; channel pairs never straddle NOUT: NOUT - split % 8 == 0)
-          const int odd = lane & 1;
+          const int odd = elane & 1;
   #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const unsigned b0 = bf16_bits(acc[fm][fn][r]), b1 = bf16_bits(acc[fm][fn][r + 1]);
             const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);
             const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
-            const int w = w0 + acc_row(r + odd, lane);
+            const int w = w0 + acc_row(r + odd, elane);
             if (!jok || h >= a.H || w >= a.W) continue;
             const long long pix = ((long long)n * a.H + h) * a.W + w;
             PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-            *reinterpret_cast<unsigned*>(dstb + pix * ld - odd) = pair;
+            st_drop(dstb + pix * ld - odd, pair);
           }
         }
         // (only CS has a null out1, its dx1 the bf16 copy alone; XB's dx0 is the bf16 store above)
         if ((CS || XB) && !dstp) continue;
         if ((ld & 1) == 0) {  // (uniform) fp32 dx as 8-byte channel pairs, as the bf16 copy above
-          const int odd = lane & 1;
+          const int odd = elane & 1;
   #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const float v0 = rb(acc[fm][fn][r]), v1 = rb(acc[fm][fn][r + 1]);
             const float recv = __shfl_xor(odd ? v0 : v1, 1, 64);
             const float2 pv = odd ? make_float2(recv, v1) : make_float2(v0, recv);
-            const int w = w0 + acc_row(r + odd, lane);
+            const int w = w0 + acc_row(r + odd, elane);
             if (!jok || h >= a.H || w >= a.W) continue;
             const long long pix = ((long long)n * a.H + h) * a.W + w;
             PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-            *reinterpret_cast<float2*>(dstp + pix * ld - odd) = pv;
+            st_drop(dstp + pix * ld - odd, pv);
           }
           continue;
         }
   #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int w = w0 + acc_row(r, lane);
+          const int w = w0 + acc_row(r, elane);
           if (!jok || h >= a.H || w >= a.W) continue;
           const long long pix = ((long long)n * a.H + h) * a.W + w;
           PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
@@ -420,7 +503,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     if (!CS && a.bz) {
   #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        const int j = j0 + wn * 64 + fn * 32 + li;
+        const int j = ej0 + wn * 64 + fn * 32 + eli;
         const bool jok = j < a.NOUT;
         const int jc = jok ? j : a.NOUT - 1;
         const float bsc = a.bcoef[jc], bsh = a.bcoef[a.NOUT + jc], bmu = a.bmean[jc], bis = a.binv[jc];
@@ -430,13 +513,13 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
           const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
           float zt[16];
   #pragma unroll
-          for (int r = 0; r < 16; ++r) {  // clamped addresses: every lane loads, masked values ignored
-            const long long zi = (row + min(w0 + acc_row(r, lane), a.W - 1)) * a.NOUT + jc;
+          for (int r = 0; r < 16; ++r) {  // clamped addresses: every elane loads, masked values ignored
+            const long long zi = (row + min(w0 + acc_row(r, elane), a.W - 1)) * a.NOUT + jc;
             zt[r] = ZB ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
           }
   #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int w = w0 + acc_row(r, lane);
+            const int w = w0 + acc_row(r, elane);
             const bool ok = jok && h < a.H && w < a.W;
             const float gg = (ok && fmaf(zt[r], bsc, bsh) > 0.f) ? rb(acc[fm][fn][r]) : 0.f;
             s1[fn] += gg;
@@ -447,13 +530,13 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     } else if (CS) {  // per-tile column sums of dx (x1b_sum: the transposed conv's bias gradient)
   #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        const bool jok = j0 + wn * 64 + fn * 32 + li < a.NOUT;
+        const bool jok = ej0 + wn * 64 + fn * 32 + eli < a.NOUT;
   #pragma unroll
         for (int fm = 0; fm < FM; ++fm) {
           const int h = h0 + 4 * wm + fm;
   #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const bool ok = jok && h < a.H && w0 + acc_row(r, lane) < a.W;
+            const bool ok = jok && h < a.H && w0 + acc_row(r, elane) < a.W;
             s1[fn] += ok ? rb(acc[fm][fn][r]) : 0.f;
           }
         }
@@ -465,14 +548,19 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     for (int fn = 0; fn < FN; ++fn) {
       s1[fn] += __shfl_xor(s1[fn], 32, 64);
       s2[fn] += __shfl_xor(s2[fn], 32, 64);
-      if (lane < 32) {
-        red[(wave * 64 + fn * 32 + lane) * 2 + 0] = s1[fn];
-        red[(wave * 64 + fn * 32 + lane) * 2 + 1] = s2[fn];
+      if (elane < 32) {
+        red[(wave * 64 + fn * 32 + elane) * 2 + 0] = s1[fn];
+        red[(wave * 64 + fn * 32 + elane) * 2 + 1] = s2[fn];
       }
     }
-    __syncthreads();
+    if constexpr (PERS) {  // (__syncthreads' vmcnt(0) would wait for every store of the epilogue)
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();
+    }
     if (tid < BN) {  // channel tid = 64 wn + c: summed over the WM waves of column group wn, in order
-      const int j = j0 + tid, wnn = tid >> 6, c = tid & 63;
+      const int j = ej0 + tid, wnn = tid >> 6, c = tid & 63;
       if (j < a.NOUT) {
         float t1 = 0.f, t2 = 0.f;
 #pragma unroll
@@ -486,6 +574,19 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
       }
     }
   }
+  if constexpr (!PERS) {
+    break;
+  } else {
+    if (!has_next) break;
+    tcur = tsp = tnext;
+    n = nn;
+    h0 = nh0;
+    w0 = nw0;
+    first = false;
+  }
+  }  // tiles
+#undef PMU_FETCH
+#undef PMU_GLDS
 }
 
 // Workgroup shape: 64 output channels x 512 pixels in 4 waves (two workgroups per CU) for <= 64
@@ -506,6 +607,40 @@ static Shape dma_shape(int NOUT, int KC) {
 #endif
   if (dma_bn(NOUT, KC) == 64) return {1, 4, 16};
   return {2, 8, 16};
+}
+
+// persistent tiles (PERS above; experiments build, PMU_DMA_PERS=1) when every slot gets two or more:
+// the resident workgroups per CU follow from the LDS (78 KB for the 4-wave shape, 117 KB for the
+// 8-wave one)
+static long long dma_slots(const Shape& sh) { return (long long)pmu_num_cus() * (sh.nwv == 4 ? 2 : 1); }
+static bool dma_pers(const Shape& sh, int nch, int ncb, long long blocks) {
+  const char* pe = pmu_variant_env("PMU_DMA_PERS");
+  const long long slots = dma_slots(sh);
+  return pe && atoi(pe) != 0 && sh.th == 16 && nch % 2 == 0 && slots % 8 == 0 && (slots / 8) % ncb == 0 &&
+         blocks >= 2 * slots;
+}
+
+// one kernel variant by workgroup shape and tile schedule (pers: `slots` resident workgroups)
+template <bool D, bool Z, bool CSV, bool XBV>
+static void launch_variant(const Shape& sh, bool pers, dim3 grid, unsigned slots, hipStream_t st, const DmaArgs& a) {
+  const dim3 blk(64 * sh.nwv);
+#ifdef PMU_EXPERIMENTS
+  if constexpr (!Z) {
+    if (pers) {
+      if (sh.wn == 1) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 4, 0, CSV, XBV, true>), dim3(slots), blk, 0, st, a);
+      else hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 2, 8, 0, CSV, XBV, true>), dim3(slots), blk, 0, st, a);
+      return;
+    }
+  }
+#else
+  (void)pers;
+  (void)slots;
+#endif
+  if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 4, 0, CSV, XBV>), grid, blk, 0, st, a);
+#ifdef PMU_EXPERIMENTS
+  else if (sh.wn == 1 && sh.nwv == 8) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 8, 0, CSV, XBV>), grid, blk, 0, st, a);
+#endif
+  else hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 2, 8, 0, CSV, XBV>), grid, blk, 0, st, a);
 }
 
 static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, const unsigned short* wp, const float* bias,
@@ -551,18 +686,8 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks), blk(64 * sh.nwv);
   const bool zb = zbf == 1;
-#ifdef PMU_EXPERIMENTS
-#define PMU_DMA_TALL_LAUNCH(D, Z, CSV, XBV) \
-  else if (sh.wn == 1 && sh.nwv == 8) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 8, 0, CSV, XBV>), grid, blk, 0, st, a);
-#else
-#define PMU_DMA_TALL_LAUNCH(D, Z, CSV, XBV)
-#endif
-#define PMU_DMA_LAUNCH(D, Z)                                                                              \
-  {                                                                                                       \
-    if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 1, 4>), grid, blk, 0, st, a); \
-    PMU_DMA_TALL_LAUNCH(D, Z, false, false)                                                               \
-    else hipLaunchKernelGGL((conv3x3_dma_kernel<D, Z, 2, 8>), grid, blk, 0, st, a);                       \
-  }
+  const long long slots = dma_slots(sh);
+  const bool pers = !zb && dma_pers(sh, a.nch, a.ncb, blocks);
 #ifdef PMU_EXPERIMENTS
   {
     const char* e = pmu_variant_env("PMU_DMA_EXP");
@@ -582,31 +707,21 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
     }
   }
 #endif
+  const unsigned ns = (unsigned)slots;
   if (dgrad && part && !bz) {  // column sums (pmu_conv3x3_dgrad_dma_x1b_sum)
-    if (xb) {
-      if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true, true>), grid, blk, 0, st, a);
-      PMU_DMA_TALL_LAUNCH(true, false, true, true)
-      else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, true, true>), grid, blk, 0, st, a);
-    } else {
-      if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, true>), grid, blk, 0, st, a);
-      PMU_DMA_TALL_LAUNCH(true, false, true, false)
-      else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, true>), grid, blk, 0, st, a);
-    }
+    if (xb) launch_variant<true, false, true, true>(sh, pers, grid, ns, st, a);
+    else launch_variant<true, false, true, false>(sh, pers, grid, ns, st, a);
   } else if (dgrad && xb) {  // bf16 dx (the *_dxb entries)
-    if (sh.wn == 1 && sh.nwv == 4) hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 1, 4, 0, false, true>), grid, blk, 0, st, a);
-    PMU_DMA_TALL_LAUNCH(true, false, false, true)
-    else hipLaunchKernelGGL((conv3x3_dma_kernel<true, false, 2, 8, 0, false, true>), grid, blk, 0, st, a);
+    launch_variant<true, false, false, true>(sh, pers, grid, ns, st, a);
   }
 #ifdef PMU_EXPERIMENTS
-  else if (dgrad && zb) PMU_DMA_LAUNCH(true, true)
-  else if (zb) PMU_DMA_LAUNCH(false, true)
+  else if (dgrad && zb) launch_variant<true, true, false, false>(sh, false, grid, ns, st, a);
+  else if (zb) launch_variant<false, true, false, false>(sh, false, grid, ns, st, a);
 #else
   else if (zb) return PMU_ERR_ARG;  // bf16-stored z: experiments build only
 #endif
-  else if (dgrad) PMU_DMA_LAUNCH(true, false)
-  else PMU_DMA_LAUNCH(false, false)
-#undef PMU_DMA_LAUNCH
-#undef PMU_DMA_TALL_LAUNCH
+  else if (dgrad) launch_variant<true, false, false, false>(sh, pers, grid, ns, st, a);
+  else launch_variant<false, false, false, false>(sh, pers, grid, ns, st, a);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }
@@ -616,6 +731,20 @@ static int launch_dma(const unsigned short* x, int Cp, int N, int H, int W, cons
 extern "C" int pmu_conv3x3_dma_ok(int H, int W, int Cp, int NOUT, int split) {
   return W >= 32 && H >= 1 && Cp % BK == 0 && NOUT > 0 && (split == NOUT || split % 32 == 0);
 }
+
+#ifdef PMU_EXPERIMENTS
+extern "C" int pmu_conv3x3_dma_persistent(int N, int H, int W, int NOUT, int Cp) {
+  if (N <= 0 || H <= 0 || W < 32 || Cp <= 0 || Cp % BK || NOUT <= 0) return 0;
+  const Shape sh = dma_shape(NOUT, Cp);
+  const int ncb = pmu_cdiv(NOUT, 64 * sh.wn);
+  const long long img_bytes = (long long)H * W * Cp * 2;
+  // (an operand over 4 GB runs per image group: its first group's grid decides, as launch_dma does)
+  long long n = N;
+  if (n * img_bytes >= (1LL << 32)) n = std::max(1LL, ((1LL << 32) - 1) / img_bytes);
+  const long long blocks = (long long)pmu_cdiv(W, TW) * pmu_cdiv(H, sh.th) * n * ncb;
+  return dma_pers(sh, Cp / BK, ncb, blocks) ? 1 : 0;
+}
+#endif
 
 extern "C" int pmu_conv3x3_tiles_dma(int N, int H, int W, int Cout, int Cp) {
   return N * pmu_cdiv(H, dma_shape(Cout, Cp).th) * pmu_cdiv(W, TW);

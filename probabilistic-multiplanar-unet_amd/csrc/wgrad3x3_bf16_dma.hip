@@ -239,7 +239,6 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
 
   // prologue: the first NS-1 stages in flight (stages past the end read the zero page or other segments
   // into slots nobody reads, so every wave issues NI DMAs per stage index and the counted waits hold)

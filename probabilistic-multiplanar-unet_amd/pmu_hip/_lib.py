@@ -224,6 +224,10 @@ SIGNATURES = {
                                       c_void_p]),
     "pmu_maxpool2_bwd_bnr_dxb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                          c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "pmu_maxpool2_bwd_bnr_stats_dxb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                               c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_maxpool2_bwd_bnbwd_dxb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                           c_int, c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_pack_wino2h_blocks": (c_int, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_wino2h_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "pmu_conv3x3_pack_wino4_blocks": (c_int, [c_int, c_int, c_int]),
@@ -257,6 +261,7 @@ EXP_SIGNATURES = {
     "pmu_convT2x2_dgrad_bf16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                         c_int, c_void_p, c_void_p]),
     "pmu_occupancy_conv3x3_pipe": (c_int, [POINTER(c_int)]),
+    "pmu_conv3x3_dma_persistent": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "pmu_bn_bwd_reduce_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p,
                                      c_void_p]),
     "pmu_maxpool2_bwd_zb": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,

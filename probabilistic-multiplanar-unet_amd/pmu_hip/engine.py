@@ -360,6 +360,50 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
                      xt32=None if (bf16 or planes is not None) else xt32)
 
 
+class PoolSumDa:
+    """The gradient of a pooled layer's activation, da = dsk + routed dpool (MaxPool2d(2) backward,
+    unet_parts.py:33, plus the skip path, unet_parts.py:66; both parts bf16 from *_dxb input gradients),
+    left unstored: pmu_maxpool2_bwd_bnr_stats_dxb formed its BN-backward partial sums (prod.bnr) and
+    dz_bf16 turns it into that layer's bf16 dz in one pass (pmu_maxpool2_bwd_bnbwd_dxb) — the fp32 da
+    is neither written nor re-read.  materialise() stores it (fp32) for the paths that read da itself."""
+
+    def __init__(self, dpool: torch.Tensor, dsk: torch.Tensor, prod: ConvBNOut):
+        self.dpool, self.dsk, self.prod = dpool, dsk, prod
+        self.shape = prod.z.shape
+        self.dtype = F32
+        self.device = prod.z.device
+
+    def dz_bf16(self, bcoef: torch.Tensor) -> torch.Tensor:
+        N, H, W, C = self.shape
+        dz = torch.empty(N, H, W, C, dtype=BF16S, device=self.device)
+        L.call("pmu_maxpool2_bwd_bnbwd_dxb", self.dpool.data_ptr(), self.dsk.data_ptr(), self.prod.z.data_ptr(),
+               self.prod.bn.coef.data_ptr(), bcoef.data_ptr(), N, H, W, C, C, dz.data_ptr(), L.stream())
+        return dz
+
+    def materialise(self) -> torch.Tensor:
+        N, H, W, C = self.shape
+        p = self.prod
+        part = _empty(L.lib().pmu_maxpool2_bwd_bnr_tiles(N, H, W, C), 2 * C, device=self.device)
+        da = _empty(N, H, W, C, device=self.device)
+        L.call("pmu_maxpool2_bwd_bnr_dxb", self.dpool.data_ptr(), self.dsk.data_ptr(), p.z.data_ptr(),
+               p.bn.coef.data_ptr(), p.bn.mean.data_ptr(), p.bn.invstd.data_ptr(), N, H, W, C, da.data_ptr(),
+               part.data_ptr(), L.stream())
+        return da
+
+
+def pool_fuse_ok(C: int) -> bool:
+    """Channel counts pmu_maxpool2_bwd_bnbwd_dxb takes: C % 4 == 0, C / 4 dividing 256 or a multiple of it."""
+    q = C // 4
+    return C % 4 == 0 and q > 0 and (256 % q == 0 if q < 256 else q % 256 == 0)
+
+
+def _concrete(src: Src) -> Src:
+    """src with a stored da (PoolSumDa materialised) for the kernels that read da itself."""
+    if isinstance(src.x, PoolSumDa):
+        return Src(src.x.materialise(), src.mode, src.coef, z=src.z, pool=src.pool, off=src.off, prod=src.prod)
+    return src
+
+
 def _bnr_producer(out: ConvBNOut, need_dx: bool, split):
     """The ConvBNOut whose BatchNorm+ReLU backward partial sums this conv's input gradient can form in
     its epilogue: the operand is that layer's unpooled activation alone and its batch statistics exist."""
@@ -395,14 +439,17 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     if out.bnr is not None and out.bnr[0] is da:
         pre = out.bnr[1:]
     out.bnr = None
+    if pre is None and isinstance(da, PoolSumDa):
+        da = da.materialise()
     bcoef, _, _, _ = bn_backward(da, z, out.bn, bn, grads, conv.bias, pre=pre)
     dz_src = Src(da, L.SRC_BNBWD, bcoef, z=z)
-    dzf = frame_of([dz_src], N, H, W)
     dw = grads.new(conv.weight)
     lb = L.lib()
     prod = _bnr_producer(out, need_dx, split)
     if out.bf16:
         return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split, prod, x1_bf16_only, dx_bf16)
+    dz_src = _concrete(dz_src)
+    dzf = frame_of([dz_src], N, H, W)
     if out.xt32 is not None and need_dx:
         return _conv_backward_tee32(out, dz_src, conv, dw, split, prod)
     if out.planes is not None:
@@ -540,7 +587,10 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
     N, H, W, Cout = out.z.shape
     dev = out.z.device
     Cin = conv.in_channels
-    dzt = frame_to_bf16([dz_src], N, H, W)
+    if isinstance(dz_src.x, PoolSumDa):
+        dzt = dz_src.x.dz_bf16(dz_src.coef)
+    else:
+        dzt = frame_to_bf16([dz_src], N, H, W)
     res = None
     if need_dx:
         sp = Cin if split is None else split
@@ -587,6 +637,7 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
                    dx0.data_ptr(), L.ptr(dx1), s)
         else:
             wp = pack_weights_bf16(conv.weight, dgrad=True)
+            dz_src = _concrete(dz_src)
             L.call("pmu_conv3x3_dgrad_bf16", frame_of(_f32_srcs([dz_src], N, H, W), N, H, W), wp.data_ptr(), Cin,
                    sp, dx0.data_ptr(), L.ptr(dx1), None, s)
         res = dx0 if split is None else (dx0, dx1)
@@ -681,7 +732,10 @@ class EngineConfig:
         UNet backward in bf16 (the *_dxb entries) — the dtype torch.autocast's conv backward returns
         them in — and their consumers read them so (PMU_DX_BF16=0: fp32, the round-4 path);
     wgrad_dma: the bf16 weight gradient on the LDS-DMA strip kernel (pmu_conv3x3_wgrad_bf16_dma) where
-        its shapes allow, else the register-staged one (PMU_WGRAD_DMA=0: always the latter)."""
+        its shapes allow, else the register-staged one (PMU_WGRAD_DMA=0: always the latter);
+    pool_fuse: a pooled layer's da (skip + routed pooled gradient, both bf16) is not stored: a
+        stats-only pass forms its BN-backward partials and its bf16 dz is made from the two parts
+        directly (PoolSumDa; PMU_POOL_FUSE=0: stored in fp32 and streamed, the round-5 path)."""
     fp32_conv: str = "wino"
     wino2h: bool = True
     wino4: str = "dgrad"
@@ -689,13 +743,15 @@ class EngineConfig:
     wgrad4: bool = False
     dx_bf16: bool = True
     wgrad_dma: bool = True
+    pool_fuse: bool = True
 
     @classmethod
     def from_env(cls):
         return cls(fp32_conv=os.environ.get("PMU_FP32_CONV", "wino"), wino2h=os.environ.get("PMU_WINO2H", "1") != "0",
                    wino4=os.environ.get("PMU_WINO4", "dgrad"), bf16_z=os.environ.get("PMU_BF16_Z", "0") == "1",
                    wgrad4=os.environ.get("PMU_WGRAD4", "0") == "1", dx_bf16=os.environ.get("PMU_DX_BF16", "1") != "0",
-                   wgrad_dma=os.environ.get("PMU_WGRAD_DMA", "1") != "0")
+                   wgrad_dma=os.environ.get("PMU_WGRAD_DMA", "1") != "0",
+                   pool_fuse=os.environ.get("PMU_POOL_FUSE", "1") != "0")
 
 
 CFG = EngineConfig.from_env()
@@ -1148,6 +1204,20 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             Cp = prev.z.shape[3]
             dsk = dskip[lev - 1]
             bn_ok = prev.z.dtype == F32 and prev.bn.mean is not None and Cp % 4 == 0
+            if bn_ok and dpool.dtype == BF16S and dsk.dtype == BF16S and CFG.pool_fuse and prev.bf16 \
+                    and pool_fuse_ok(Cp):
+                # bf16 pooled and skip gradients (*_dxb): the pooled layer's da = their fp32 sum stays
+                # unstored (PoolSumDa) — its BN-backward partial sums here, its bf16 dz in that layer's
+                # backward
+                R = L.lib().pmu_maxpool2_bwd_bnr_tiles(N, hp, wp, Cp)
+                part = _empty(R, 2 * Cp, device=dev)
+                L.call("pmu_maxpool2_bwd_bnr_stats_dxb", dpool.data_ptr(), dsk.data_ptr(), prev.z.data_ptr(),
+                       prev.bn.coef.data_ptr(), prev.bn.mean.data_ptr(), prev.bn.invstd.data_ptr(), N, hp, wp, Cp,
+                       part.data_ptr(), s)
+                dsum = PoolSumDa(dpool, dsk, prev)
+                dskip[lev - 1] = dsum
+                prev.bnr = (dsum, part, R)
+                continue
             if bn_ok and dpool.dtype == BF16S and dsk.dtype == BF16S:
                 # bf16 pooled and skip gradients (*_dxb): their fp32 sum is the pooled layer's da, written
                 # to a new tensor with that layer's BN-backward partial sums
