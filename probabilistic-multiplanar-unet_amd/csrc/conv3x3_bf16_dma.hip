@@ -129,8 +129,12 @@ __global__ __launch_bounds__(256) void pack_dma_multi_kernel(const pmu_pack_job*
 // epilogue output stores, bit 1 = no MFMAs.  512^2 x 64 -> 64 (c5, tools/kbench.py --c5): 0.52 ms; no
 // stores 0.33; no MFMAs 0.36; neither 0.17 — the z stores (1.07 GB fp32) and the MFMAs add up instead
 // of overlapping.  Measured and dropped: a phase offset between the two workgroups of a CU (s_sleep
-// before the first round: no change) and 16-B stores through an LDS transpose (-2..5% on K <= 128
-// only).
+// before the first round: no change), 16-B stores through an LDS transpose (-2..5% on K <= 128
+// only), and the transposed accumulator layout (MFMA operands swapped: a pixel per lane, four
+// consecutive channels per register group, so every z / dx store and the BN-backward z loads are
+// 16 B and bf16 dx leaves in permlane32-swapped 16-B vectors — a quarter of the store instructions;
+// BN sums through LDS): kbench --c5 fwd 4.57 vs 4.42 ms, dgrad_bnr 6.44 vs 5.92 (profiles/r05/
+// transposed_epilogue) — the store tail here is not issue-bound.
 // CS (input gradient): per-tile column sums of dx into a.part instead of the BN-backward partials
 // (pmu_conv3x3_dgrad_dma_x1b_sum; a compile-time variant: as a runtime branch beside the a.bz one it
 // spilled 89 VGPRs)

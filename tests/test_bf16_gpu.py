@@ -448,7 +448,11 @@ def test_c5_bf16_dice_gap_vs_fp32_oracle(dev):
         assert res["fp32"][f"argmax_agreement_vs_oracle_{m}"] >= 0.999, m
         assert max(res["fp32"][f"dice_gap_{m}"]) <= 1e-3, m
         # the north star's Dice contract holds for the bf16 mode too (measured: agreement 0.99988,
-        # Dice gap <= 1.7e-4; profiles/r02/c5_bf16_dice_gap.json)
+        # Dice gap <= 1.7e-4; profiles/r02/c5_bf16_dice_gap.json).  Its seed spread (tools/
+        # dice_gap_seeds.py, 6 init seeds, profiles/r05/transposed_epilogue/dice_gap_seeds_prev.json):
+        # train-mode gap <= 2.6e-4 on every seed, but the eval-mode gap (BN running statistics after 12
+        # steps) 0 .. 4.7e-3, mean 1.6e-3 — the eval gate at 1e-3 holds at this seed, the train-mode
+        # gap is the seed-robust statistic; any change of the bf16 summation order moves the eval one.
         assert res["bf16"][f"argmax_agreement_vs_oracle_{m}"] >= 0.99, m
         assert max(res["bf16"][f"dice_gap_{m}"]) <= 1e-3, m
     # the phantom is learnable: the reference itself segments it after 12 steps
