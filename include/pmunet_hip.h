@@ -406,6 +406,14 @@ int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmoid, const f
                         int N, int H, int W, float* dl, float* da, const float* z, const float* coef,
                         const float* mean, const float* invstd, float* part, float* dw, float* db, float* ws,
                         size_t ws_bytes, void* stream);
+/* With dw non-NULL, da may be NULL too (not stored): pmu_head1x1_bwd_dz then writes the last layer's
+ * dz straight from dy — da = sum_k g_k w[k] formed as the pass above forms it — as that layer's
+ * BN+ReLU backward over bcoef (pmu_bn_bwd_finalize's 5 C coefficients): bf16 bits (out_bf16, C % 8
+ * == 0; the bf16 convs' operand) or fp32, [N][H][W][C]; bit-equal to pmu_frame_to_bf16 / _f32 of
+ * Src(stored da, BNBWD, bcoef, z).  Shapes as pmu_head1x1_bwd_bnr_ok, K <= 8. */
+int pmu_head1x1_bwd_dz(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
+                       int N, int H, int W, const float* z, const float* bcoef, int out_bf16, void* dz,
+                       void* stream);
 size_t pmu_wgrad1x1_ws(int P, int K, int C);
 /* dw[K][C] = sum_p dl[p][k] act[p][c], db[k] = sum_p dl[p][k]; dl NCHW [N][K][H][W]. */
 int pmu_wgrad1x1(const float* dl, const pmu_frame* act, int K, float* dw, float* db, float* ws,

@@ -990,10 +990,14 @@ __global__ __launch_bounds__(256) void head_bwd_fast_kernel(const float* __restr
 // iteration made each iteration's loads wait for the previous iteration's store (vmcnt counts loads
 // and stores in order): 2.2 TB/s.  Same per-thread summation order as head_bwd_fast_kernel /
 // wgrad1x1_fast_kernel (masked terms add exact zeros), so the results are bit-identical.
-template <int KT, bool SIG>
+// STDA = false: da not stored (head_dz_kernel re-forms it for the last layer's dz, engine.HeadDa)
+template <int KT, bool SIG, bool STDA = true>
 __global__ __launch_bounds__(256) void head_bwd_fused_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                                                              const float* __restrict__ w, int C, long long HW,
                                                              long long P, float* __restrict__ da, HeadBnr bn) {
+  // (no fp contraction: without the da store hipcc fused g = dy * y(1-y) into the bias sum's add, an
+  // FMA where pmu_wgrad1x1 adds the rounded g — db then differed in the last bit)
+#pragma clang fp contract(off)
   constexpr int B = 4;
   __shared__ float red[4 * 2 * 256];
   __shared__ float redw[4 * KT * 260];
@@ -1052,7 +1056,7 @@ __global__ __launch_bounds__(256) void head_bwd_fused_kernel(const float* __rest
         s1[e] += gg;
         s2[e] = fmaf(gg, (zv[e] - muv[e]) * isv[e], s2[e]);
       }
-      if (ok) *reinterpret_cast<float4*>(da + (size_t)p * C + 4 * cq) = o;
+      if (STDA && ok) *reinterpret_cast<float4*>(da + (size_t)p * C + 4 * cq) = o;
     }
   }
 #pragma unroll
@@ -1093,6 +1097,71 @@ __global__ __launch_bounds__(256) void head_bwd_fused_kernel(const float* __rest
     float t = 0.f;
     for (int wv = 0; wv < 4; ++wv) t += redw[(wv * KT + k) * 260 + c];
     bn.ws[(long long)blockIdx.x * KT * CW + o] = t;
+  }
+}
+
+// The last layer's BN+ReLU backward dz from the head's gradient without a stored da (engine.HeadDa):
+// da = sum_k g_k w_k formed as head_bwd_fused_kernel forms it (same g, same fmaf order, so the same
+// fp32 values), then dz = fmaf(sc, (z*sc+sh > 0) ? da : 0, fmaf(kx, z - mu, kc)) — the frame streams'
+// BN-backward formula over bcoef (5 C) — written as bf16 (RNE, the bf16 convs' operand) or fp32 (the
+// Winograd input gradient's).  Thread mapping and 4-pixel load batches as head_bwd_fused_kernel.
+template <int KT, bool SIG, bool BF>
+__global__ __launch_bounds__(256) void head_dz_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                      const float* __restrict__ w, int C, long long HW, long long P,
+                                                      const float* __restrict__ z, const float* __restrict__ bcoef,
+                                                      void* __restrict__ out) {
+#pragma clang fp contract(off)
+  constexpr int B = 4;
+  const int tid = threadIdx.x;
+  const int CQ = C >> 2, PG = 256 / CQ;
+  const int cq = tid & (CQ - 1), pg = tid / CQ;
+  float4 wq[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) wq[k] = *reinterpret_cast<const float4*>(w + k * C + 4 * cq);
+  const float4 sc = *reinterpret_cast<const float4*>(bcoef + 4 * cq);
+  const float4 sh = *reinterpret_cast<const float4*>(bcoef + C + 4 * cq);
+  const float4 mu = *reinterpret_cast<const float4*>(bcoef + 2 * C + 4 * cq);
+  const float4 kx = *reinterpret_cast<const float4*>(bcoef + 3 * C + 4 * cq);
+  const float4 kc = *reinterpret_cast<const float4*>(bcoef + 4 * C + 4 * cq);
+  const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+  const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, kxv[4] = {kx.x, kx.y, kx.z, kx.w}, kcv[4] = {kc.x, kc.y, kc.z, kc.w};
+  const unsigned HWu = (unsigned)HW, pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
+  for (unsigned p0 = blockIdx.x * HPPB + pg; p0 < pend; p0 += B * PG) {
+    float4 zz[B];
+    float g[B][KT];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const unsigned p = min(p0 + b * PG, pend - 1);
+      const unsigned n = p / HWu, pix = p - n * HWu;
+      zz[b] = *reinterpret_cast<const float4*>(z + (size_t)p * C + 4 * cq);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        const size_t i = (size_t)(n * KT + k) * HWu + pix;
+        g[b][k] = dy[i];
+        if (SIG) { const float sg = y[i]; g[b][k] = g[b][k] * (sg * (1.f - sg)); }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const unsigned p = p0 + b * PG;
+      if (p >= pend) continue;
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        o.x = fmaf(g[b][k], wq[k].x, o.x); o.y = fmaf(g[b][k], wq[k].y, o.y);
+        o.z = fmaf(g[b][k], wq[k].z, o.z); o.w = fmaf(g[b][k], wq[k].w, o.w);
+      }
+      const float ov[4] = {o.x, o.y, o.z, o.w}, zv[4] = {zz[b].x, zz[b].y, zz[b].z, zz[b].w};
+      float r[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        r[e] = fmaf(scv[e], fmaf(zv[e], scv[e], shv[e]) > 0.f ? ov[e] : 0.f, fmaf(kxv[e], zv[e] - muv[e], kcv[e]));
+      if (BF)
+        *reinterpret_cast<uint2*>(static_cast<unsigned short*>(out) + (size_t)p * C + 4 * cq) =
+            make_uint2(pmu_pk_bf16(r[0], r[1]), pmu_pk_bf16(r[2], r[3]));
+      else
+        *reinterpret_cast<float4*>(static_cast<float*>(out) + (size_t)p * C + 4 * cq) = make_float4(r[0], r[1], r[2], r[3]);
+    }
   }
 }
 
@@ -1673,9 +1742,9 @@ extern "C" int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmo
                                    int N, int H, int W, float* dl, float* da, const float* z, const float* coef,
                                    const float* mean, const float* invstd, float* part, float* dw, float* db,
                                    float* ws, size_t ws_bytes, void* stream) {
-  PMU_REQUIRE(dy && w && da && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y) && N > 0 && H > 0 &&
+  PMU_REQUIRE(dy && w && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y) && N > 0 && H > 0 &&
               W > 0 && z && coef && mean && invstd && part && pmu_head1x1_bwd_bnr_ok(N, H, W, C));
-  PMU_REQUIRE(dw ? (ws != nullptr) : (dl != nullptr));
+  PMU_REQUIRE(dw ? (ws != nullptr) : (dl != nullptr && da != nullptr));  // (da null: not stored, dw path only)
   const long long P = (long long)N * H * W;
   const int R = pmu_cdiv(P, HPPB);
   const HeadBnr bn{z, coef, mean, invstd, part, ws};
@@ -1685,10 +1754,14 @@ extern "C" int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmo
     const long long HW = (long long)H * W;
 #define PMU_HEAD_FUSED(KV)                                                                                   \
   case KV:                                                                                                  \
-    if (do_sigmoid) hipLaunchKernelGGL((head_bwd_fused_kernel<KV, true>), dim3((unsigned)R), dim3(256), 0, st,  \
-                                       dy, y, w, C, HW, P, da, bn);                                         \
-    else hipLaunchKernelGGL((head_bwd_fused_kernel<KV, false>), dim3((unsigned)R), dim3(256), 0, st, dy, y, w, \
-                            C, HW, P, da, bn);                                                              \
+    if (do_sigmoid && da) hipLaunchKernelGGL((head_bwd_fused_kernel<KV, true>), dim3((unsigned)R), dim3(256), 0, \
+                                             st, dy, y, w, C, HW, P, da, bn);                               \
+    else if (do_sigmoid) hipLaunchKernelGGL((head_bwd_fused_kernel<KV, true, false>), dim3((unsigned)R),       \
+                                            dim3(256), 0, st, dy, y, w, C, HW, P, da, bn);                   \
+    else if (da) hipLaunchKernelGGL((head_bwd_fused_kernel<KV, false>), dim3((unsigned)R), dim3(256), 0, st, dy, \
+                                    y, w, C, HW, P, da, bn);                                                \
+    else hipLaunchKernelGGL((head_bwd_fused_kernel<KV, false, false>), dim3((unsigned)R), dim3(256), 0, st, dy, \
+                            y, w, C, HW, P, da, bn);                                                        \
     break;
     switch (K) {
       PMU_HEAD_FUSED(1) PMU_HEAD_FUSED(2) PMU_HEAD_FUSED(3) PMU_HEAD_FUSED(4)
@@ -1703,6 +1776,36 @@ extern "C" int pmu_head1x1_bwd_bnr(const float* dy, const float* y, int do_sigmo
     hipLaunchKernelGGL((head_bwd_fast_kernel<true, false>), dim3((unsigned)R), dim3(256), 0, (hipStream_t)stream, dy, y,
                        do_sigmoid, w, K, C, (long long)H * W, P, dl, da, bn);
   }
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_head1x1_bwd_dz(const float* dy, const float* y, int do_sigmoid, const float* w, int K, int C,
+                                  int N, int H, int W, const float* z, const float* bcoef, int out_bf16, void* dz,
+                                  void* stream) {
+  PMU_REQUIRE(dy && w && K >= 1 && K <= HEAD_KMAX && C > 0 && (!do_sigmoid || y) && N > 0 && H > 0 && W > 0 && z &&
+              bcoef && dz && pmu_head1x1_bwd_bnr_ok(N, H, W, C) && (!out_bf16 || C % 8 == 0));
+  const long long P = (long long)N * H * W;
+  const long long HW = (long long)H * W;
+  const int R = pmu_cdiv(P, HPPB);
+  hipStream_t st = (hipStream_t)stream;
+#define PMU_HEAD_DZ(KV)                                                                                       \
+  case KV:                                                                                                    \
+    if (do_sigmoid && out_bf16) hipLaunchKernelGGL((head_dz_kernel<KV, true, true>), dim3((unsigned)R), dim3(256), \
+                                                   0, st, dy, y, w, C, HW, P, z, bcoef, dz);                 \
+    else if (do_sigmoid) hipLaunchKernelGGL((head_dz_kernel<KV, true, false>), dim3((unsigned)R), dim3(256), 0,  \
+                                            st, dy, y, w, C, HW, P, z, bcoef, dz);                           \
+    else if (out_bf16) hipLaunchKernelGGL((head_dz_kernel<KV, false, true>), dim3((unsigned)R), dim3(256), 0, st, \
+                                          dy, y, w, C, HW, P, z, bcoef, dz);                                 \
+    else hipLaunchKernelGGL((head_dz_kernel<KV, false, false>), dim3((unsigned)R), dim3(256), 0, st, dy, y, w, C, \
+                            HW, P, z, bcoef, dz);                                                            \
+    break;
+  switch (K) {
+    PMU_HEAD_DZ(1) PMU_HEAD_DZ(2) PMU_HEAD_DZ(3) PMU_HEAD_DZ(4)
+    PMU_HEAD_DZ(5) PMU_HEAD_DZ(6) PMU_HEAD_DZ(7) PMU_HEAD_DZ(8)
+    default: return PMU_ERR_ARG;
+  }
+#undef PMU_HEAD_DZ
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -391,6 +391,38 @@ class PoolSumDa:
         return da
 
 
+class HeadDa:
+    """The last layer's activation gradient da = OutConv's input gradient (unet_parts.py:70-76 backward:
+    sum over classes of dy_k w_k, through the sigmoid for one class) left unstored: the head backward
+    (pmu_head1x1_bwd_bnr with da NULL) formed the layer's BN-backward partials and the head's weight
+    gradient, and dz(bcoef, bf16) writes the layer's dz straight from dy (pmu_head1x1_bwd_dz) — the
+    fp32 da is neither written nor re-read.  materialise() stores it for the paths that read da."""
+
+    def __init__(self, dy: torch.Tensor, y: torch.Tensor, sigmoid: bool, w: torch.Tensor, K: int, prod: ConvBNOut):
+        self.dy, self.y, self.sigmoid, self.w, self.K, self.prod = dy, y, sigmoid, w, K, prod
+        self.shape = prod.z.shape
+        self.dtype = F32
+        self.device = prod.z.device
+
+    def dz(self, bcoef: torch.Tensor, bf16: bool) -> torch.Tensor:
+        N, H, W, C = self.shape
+        out = torch.empty(N, H, W, C, dtype=BF16S if bf16 else F32, device=self.device)
+        L.call("pmu_head1x1_bwd_dz", self.dy.data_ptr(), self.y.data_ptr(), int(self.sigmoid), self.w.data_ptr(),
+               self.K, C, N, H, W, self.prod.z.data_ptr(), bcoef.data_ptr(), int(bf16), out.data_ptr(), L.stream())
+        return out
+
+    def dz_bf16(self, bcoef: torch.Tensor) -> torch.Tensor:
+        return self.dz(bcoef, True)
+
+    def materialise(self) -> torch.Tensor:
+        N, H, W, C = self.shape
+        da = _empty(N, H, W, C, device=self.device)
+        dl = _empty(N, self.K, H, W, device=self.device)
+        L.call("pmu_head1x1_bwd", self.dy.data_ptr(), self.y.data_ptr(), int(self.sigmoid), self.w.data_ptr(),
+               self.K, C, N, H, W, dl.data_ptr(), da.data_ptr(), L.stream())
+        return da
+
+
 def pool_fuse_ok(C: int) -> bool:
     """Channel counts pmu_maxpool2_bwd_bnbwd_dxb takes: C % 4 == 0, C / 4 dividing 256 or a multiple of it."""
     q = C // 4
@@ -398,8 +430,8 @@ def pool_fuse_ok(C: int) -> bool:
 
 
 def _concrete(src: Src) -> Src:
-    """src with a stored da (PoolSumDa materialised) for the kernels that read da itself."""
-    if isinstance(src.x, PoolSumDa):
+    """src with a stored da (PoolSumDa / HeadDa materialised) for the kernels that read da itself."""
+    if isinstance(src.x, (PoolSumDa, HeadDa)):
         return Src(src.x.materialise(), src.mode, src.coef, z=src.z, pool=src.pool, off=src.off, prod=src.prod)
     return src
 
@@ -439,7 +471,7 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     if out.bnr is not None and out.bnr[0] is da:
         pre = out.bnr[1:]
     out.bnr = None
-    if pre is None and isinstance(da, PoolSumDa):
+    if pre is None and isinstance(da, (PoolSumDa, HeadDa)):
         da = da.materialise()
     bcoef, _, _, _ = bn_backward(da, z, out.bn, bn, grads, conv.bias, pre=pre)
     dz_src = Src(da, L.SRC_BNBWD, bcoef, z=z)
@@ -448,7 +480,8 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     prod = _bnr_producer(out, need_dx, split)
     if out.bf16:
         return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split, prod, x1_bf16_only, dx_bf16)
-    dz_src = _concrete(dz_src)
+    # (an unstored head gradient gives dz itself, fp32: a RAW source of the same values)
+    dz_src = Src(da.dz(bcoef, False)) if isinstance(da, HeadDa) else _concrete(dz_src)
     dzf = frame_of([dz_src], N, H, W)
     if out.xt32 is not None and need_dx:
         return _conv_backward_tee32(out, dz_src, conv, dw, split, prod)
@@ -587,7 +620,7 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
     N, H, W, Cout = out.z.shape
     dev = out.z.device
     Cin = conv.in_channels
-    if isinstance(dz_src.x, PoolSumDa):
+    if isinstance(dz_src.x, (PoolSumDa, HeadDa)):
         dzt = dz_src.x.dz_bf16(dz_src.coef)
     else:
         dzt = frame_to_bf16([dz_src], N, H, W)
@@ -735,7 +768,10 @@ class EngineConfig:
         its shapes allow, else the register-staged one (PMU_WGRAD_DMA=0: always the latter);
     pool_fuse: a pooled layer's da (skip + routed pooled gradient, both bf16) is not stored: a
         stats-only pass forms its BN-backward partials and its bf16 dz is made from the two parts
-        directly (PoolSumDa; PMU_POOL_FUSE=0: stored in fp32 and streamed, the round-5 path)."""
+        directly (PoolSumDa; PMU_POOL_FUSE=0: stored in fp32 and streamed, the round-5 path);
+    head_fuse: the head's input gradient (the last layer's da) is not stored: the head backward forms
+        the last layer's BN-backward partials and the head's weight gradient, and that layer's dz (bf16 or
+        fp32) is made from dy directly (HeadDa; PMU_HEAD_FUSE=0: da stored, then streamed)."""
     fp32_conv: str = "wino"
     wino2h: bool = True
     wino4: str = "dgrad"
@@ -744,6 +780,7 @@ class EngineConfig:
     dx_bf16: bool = True
     wgrad_dma: bool = True
     pool_fuse: bool = True
+    head_fuse: bool = True
 
     @classmethod
     def from_env(cls):
@@ -751,7 +788,8 @@ class EngineConfig:
                    wino4=os.environ.get("PMU_WINO4", "dgrad"), bf16_z=os.environ.get("PMU_BF16_Z", "0") == "1",
                    wgrad4=os.environ.get("PMU_WGRAD4", "0") == "1", dx_bf16=os.environ.get("PMU_DX_BF16", "1") != "0",
                    wgrad_dma=os.environ.get("PMU_WGRAD_DMA", "1") != "0",
-                   pool_fuse=os.environ.get("PMU_POOL_FUSE", "1") != "0")
+                   pool_fuse=os.environ.get("PMU_POOL_FUSE", "1") != "0",
+                   head_fuse=os.environ.get("PMU_HEAD_FUSE", "1") != "0")
 
 
 CFG = EngineConfig.from_env()
@@ -1087,9 +1125,11 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
         K = net.outc.conv.out_channels
         C = last.z.shape[3]
         dyc = dy.contiguous()
-        dl = _empty(N, K, H, W, device=dev)
-        da = _empty(N, H, W, C, device=dev)
         lb = L.lib()
+        head_fuse = (CFG.head_fuse and K <= 8 and last.z.dtype == F32 and last.bn.mean is not None
+                     and lb.pmu_head1x1_bwd_bnr_ok(N, H, W, C) and (not last.bf16 or C % 8 == 0))
+        dl = None if head_fuse else _empty(N, K, H, W, device=dev)
+        da = None if head_fuse else _empty(N, H, W, C, device=dev)
         dwo = grads.new(net.outc.conv.weight)
         dbo = grads.new(net.outc.conv.bias) if net.outc.conv.bias is not None else _empty(K, device=dev)
         wsb = lb.pmu_wgrad1x1_ws(N * H * W, K, C)
@@ -1100,9 +1140,11 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
             R = lb.pmu_head1x1_bwd_tiles(N, H, W)
             part = _empty(R, 2 * C, device=dev)
             L.call("pmu_head1x1_bwd_bnr", dyc.data_ptr(), st.y.data_ptr(), int(net.n_classes == 1),
-                   net.outc.conv.weight.data_ptr(), K, C, N, H, W, None, da.data_ptr(), last.z.data_ptr(),
+                   net.outc.conv.weight.data_ptr(), K, C, N, H, W, None, L.ptr(da), last.z.data_ptr(),
                    last.bn.coef.data_ptr(), last.bn.mean.data_ptr(), last.bn.invstd.data_ptr(), part.data_ptr(),
                    dwo.data_ptr(), dbo.data_ptr(), ws.data_ptr(), wsb, s)
+            if head_fuse:   # da unstored: the last layer's dz comes from dy (HeadDa)
+                da = HeadDa(dyc, st.y, net.n_classes == 1, net.outc.conv.weight, K, last)
             last.bnr = (da, part, R)
         else:
             L.call("pmu_head1x1_bwd", dyc.data_ptr(), st.y.data_ptr(), int(net.n_classes == 1),
