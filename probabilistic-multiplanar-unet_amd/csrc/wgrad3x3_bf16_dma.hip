@@ -16,7 +16,8 @@
 //
 // Staging: a ring of NS LDS stages filled by global_load_lds (16 B per lane, no staging registers, no
 // ds_write); a stage holds three consecutive steps (dz rows y..y+2, halo rows y+1..y+3) of every strip
-// lane of the workgroup; one barrier per stage (27 MFMAs per wave).  Units outside the image, the
+// lane of the workgroup; one barrier per two stages (54 MFMAs per wave; a ring of 5: kbench over the
+// c5 shapes 4.21 vs 4.29 ms with one barrier per stage and a ring of 4, profiles/r05/wgrad_pair).  Units outside the image, the
 // channels or the segment are DMA'd from a zero page, so every wave issues the same number of DMA
 // instructions per stage and the ring waits are counted (s_waitcnt vmcnt(N)) with the next NS-2 stages
 // in flight.  LDS rows are unit permutations, not padded rows (LDS-DMA writes 1 KiB contiguous per
@@ -55,7 +56,10 @@ struct WG {
   static constexpr int A_UNITS = WS * A_LANE, X_UNITS = WS * X_LANE;
   static constexpr int NI = (A_UNITS + X_UNITS + NT - 1) / NT;  // DMA instructions per wave per stage
   static constexpr int STAGE = NI * NT * 16;                      // bytes
-  static constexpr int NS = (4 * STAGE <= 160 * 1024) ? 4 : 3;
+  // PAIR: one barrier per two stages (a ring of 5: the barrier at an even stage s waits for s and
+  // s + 1 and refills the two slots s - 2, s - 1 free by then); else one per stage, a ring of 4 / 3
+  static constexpr bool PAIR = 5 * STAGE <= 160 * 1024;
+  static constexpr int NS = PAIR ? 5 : (4 * STAGE <= 160 * 1024) ? 4 : 3;
   static_assert(NS * STAGE <= 160 * 1024, "LDS");
 };
 
@@ -243,47 +247,66 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   // prologue: the first NS-1 stages in flight (stages past the end read the zero page or other segments
   // into slots nobody reads, so every wave issues NI DMAs per stage index and the counted waits hold)
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue();
+  for (int s = 0; s < NS - (G::PAIR ? 2 : 1); ++s) issue();
   // (a segment's prologue and its triplets as nested loops: as the two arms of one per-stage branch,
   // the merged rotation registers spilled 150+ VGPRs)
   int rslot = 0;   // ring slot of stage s (s % NS)
+  int sg = 0;      // stage index s (PAIR: its parity)
   auto begin_stage = [&]() __attribute__((always_inline)) {
-    // stage s landed (this wave's DMAs: all but the NS-2 younger stages'), then every wave's, and every
-    // read of stage s-1 — whose slot the next DMA overwrites — is done (its MFMAs consumed them)
-    wgd_wait_vm<(NS - 2) * NI>();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    issue();   // stage s + NS - 1, into the slot stage s - 1 used
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (G::PAIR) {
+      // even s: stages s and s + 1 landed (this wave's DMAs: all but the NS-4 younger stages'), then
+      // every wave's, and every read of stage s - 1 done; then stages s + NS - 2, s + NS - 1 into the
+      // slots of s - 2, s - 1.  Odd s: nothing (covered by the even barrier before it)
+      if ((sg & 1) == 0) {
+        wgd_wait_vm<(NS - 4) * NI>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue();
+        issue();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      ++sg;
+    } else {
+      // stage s landed (this wave's DMAs: all but the NS-2 younger stages'), then every wave's, and every
+      // read of stage s-1 — whose slot the next DMA overwrites — is done (its MFMAs consumed them)
+      wgd_wait_vm<(NS - 2) * NI>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      issue();   // stage s + NS - 1, into the slot stage s - 1 used
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const unsigned st = sbase + (unsigned)(rslot * G::STAGE);
     rslot = rslot + 1 == NS ? 0 : rslot + 1;
     return st;
   };
-  bf16x8 B0[3], B1[3];  // halo rows y-1, y of the next step (per kw)
+  // halo rows y-1, y of the next step (per kw) in two register sets that alternate per triplet: a
+  // triplet reads (P0, P1) and leaves its last two halo rows in (Q0, Q1), the next triplet the other
+  // way round — no rotation copies (12 bf16x8 moves per triplet, ~0.9 VALU per MFMA, in a kernel that
+  // is instruction-issue-bound)
+  bf16x8 B0[3], B1[3], C0[3], C1[3];
   // triplet TT of a stage: steps on its rows 3TT .. 3TT+2 (read during the previous step's MFMAs)
-  auto triplets = [&](unsigned st, auto TT) __attribute__((always_inline)) {
+  auto triplet = [&](unsigned st, auto TT, const bf16x8 (&P0)[3], const bf16x8 (&P1)[3], bf16x8 (&Q0)[3],
+                     bf16x8 (&Q1)[3]) __attribute__((always_inline)) {
     constexpr int T0 = 3 * decltype(TT)::value;
-    bf16x8 x0[3], x1[3], x2[3];
+    bf16x8 x0[3];
     const bf16x8 a0 = rd_a(st, std::integral_constant<int, T0>{});
     rd_x(st, std::integral_constant<int, T0>{}, x0);
     const bf16x8 a1 = rd_a(st, std::integral_constant<int, T0 + 1>{});
-    rd_x(st, std::integral_constant<int, T0 + 1>{}, x1);
+    rd_x(st, std::integral_constant<int, T0 + 1>{}, Q0);
     wgd_wait_lgkm<8>();  // step y's 8 reads
     __builtin_amdgcn_sched_barrier(0);
-    mm(a0, B0, B1, x0);
+    mm(a0, P0, P1, x0);
     __builtin_amdgcn_sched_barrier(0);
     const bf16x8 a2 = rd_a(st, std::integral_constant<int, T0 + 2>{});
-    rd_x(st, std::integral_constant<int, T0 + 2>{}, x2);
+    rd_x(st, std::integral_constant<int, T0 + 2>{}, Q1);
     wgd_wait_lgkm<8>();  // step y+1's
     __builtin_amdgcn_sched_barrier(0);
-    mm(a1, B1, x0, x1);
+    mm(a1, P1, x0, Q0);
     __builtin_amdgcn_sched_barrier(0);
     wgd_wait_lgkm<0>();
     __builtin_amdgcn_sched_barrier(0);
-    mm(a2, x0, x1, x2);
+    mm(a2, x0, Q0, Q1);
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) { B0[kw] = x1[kw]; B1[kw] = x2[kw]; }
   };
   for (int k = 0; k < a.spb; ++k) {
     {  // prologue of a segment: halo rows y0-1, y0
@@ -293,10 +316,24 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
       wgd_wait_lgkm<0>();
       __builtin_amdgcn_sched_barrier(0);
     }
-    for (int t = 1; t <= a.m; ++t) {  // TPS triplets of steps y, y+1, y+2: new halo rows y+1, y+2, y+3
-      const unsigned st = begin_stage();
-      triplets(st, std::integral_constant<int, 0>{});
-      if constexpr (TPS == 2) triplets(st, std::integral_constant<int, 1>{});
+    // TPS triplets per stage of steps y, y+1, y+2 (new halo rows y+1, y+2, y+3); the register sets
+    // alternate B -> C -> B, so stages run in pairs (TPS = 1) and a segment's odd last one alone (its
+    // C rows are not read: the next segment's prologue reloads B)
+    if constexpr (TPS == 2) {
+      for (int t = 1; t <= a.m; ++t) {
+        const unsigned st = begin_stage();
+        triplet(st, I0{}, B0, B1, C0, C1);
+        triplet(st, I1{}, C0, C1, B0, B1);
+      }
+    } else {
+      int t = 1;
+      for (; t + 1 <= a.m; t += 2) {
+        unsigned st = begin_stage();
+        triplet(st, I0{}, B0, B1, C0, C1);
+        st = begin_stage();
+        triplet(st, I0{}, C0, C1, B0, B1);
+      }
+      if (t <= a.m) triplet(begin_stage(), I0{}, B0, B1, C0, C1);
     }
   }
   wgd_wait_vm<0>();  // (the tail stages' DMAs: nothing of them is read; drained before the wave exits)
