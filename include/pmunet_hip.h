@@ -356,6 +356,13 @@ int pmu_maxpool2_bwd_bnr_stats_dxb(const unsigned short* dpool, const unsigned s
 int pmu_maxpool2_bwd_bnbwd_dxb(const unsigned short* dpool, const unsigned short* skip, const float* z,
                                const float* coef, const float* bcoef, int N, int H, int W, int C, int ldo,
                                unsigned short* dz, void* stream);
+/* The same for fp32 dpool / skip gradients (config c2) with an fp32 dz: bit-equal to pmu_maxpool2_bwd_bnr
+ * accumulating into skip and to pmu_frame_to_f32 of Src(that da, BNBWD, bcoef, z). */
+int pmu_maxpool2_bwd_bnr_stats(const float* dpool, const float* skip, const float* z, const float* coef,
+                               const float* mean, const float* invstd, int N, int H, int W, int C, float* part,
+                               void* stream);
+int pmu_maxpool2_bwd_bnbwd(const float* dpool, const float* skip, const float* z, const float* coef,
+                           const float* bcoef, int N, int H, int W, int C, int ldo, float* dz, void* stream);
 /* AvgPool2d(2,2,ceil_mode=True) backward: dx = dpool/count(window), overwrite. */
 int pmu_avgpool2_bwd(const float* dpool, int N, int H, int W, int C, float* dx, void* stream);
 /* The same (bit-equal dx, here da: N x H x W x C at the pooled layer's resolution) fused with the BN+ReLU

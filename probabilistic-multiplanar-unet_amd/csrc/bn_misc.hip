@@ -487,8 +487,9 @@ struct MpBwdCoef {
   float sc[4], sh[4];                           // forward BN scale / shift (the max-pool's argmax)
   float bsc[4], bsh[4], mu[4], kx[4], kc[4];    // backward coefficients (bcoef, 5 C)
 };
+template <bool BF>
 __device__ __forceinline__ void mp_apply(const MpWin& m, long long wi, bool valid, int H, int W, int c, int ldo,
-                                         long long lim, const MpBwdCoef& k, unsigned short* __restrict__ out) {
+                                         long long lim, const MpBwdCoef& k, void* __restrict__ out) {
   const int Hp = H / 2, Wp = W / 2, Hc = (H + 1) / 2, Wc = (W + 1) / 2;
   const int wc = (int)(wi % Wc);
   const long long r = wi / Wc;
@@ -524,7 +525,11 @@ __device__ __forceinline__ void mp_apply(const MpWin& m, long long wi, bool vali
     const long long off = (((long long)n * H + h) * W + w) * ldo + c;
     PMU_DCHECK(off + 4 <= lim, PMU_DBG_OUTPUT);
     (void)lim;
-    *reinterpret_cast<uint2*>(out + off) = make_uint2(pmu_pk_bf16(o[0], o[1]), pmu_pk_bf16(o[2], o[3]));
+    if (BF)
+      *reinterpret_cast<uint2*>(static_cast<unsigned short*>(out) + off) =
+          make_uint2(pmu_pk_bf16(o[0], o[1]), pmu_pk_bf16(o[2], o[3]));
+    else
+      *reinterpret_cast<float4*>(static_cast<float*>(out) + off) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -597,12 +602,15 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const DT* __restr
   }
 }
 
-__global__ __launch_bounds__(256) void maxpool2_bwd_bnbwd_kernel(const unsigned short* __restrict__ dpool,
-                                                                 const unsigned short* __restrict__ skip,
+// DT: storage of dpool and skip (bf16 bits: the *_dxb gradients; float: the fp32 path); BF: dz as bf16
+// bits (the bf16 convs' operand) or fp32 (the Winograd input gradient's)
+template <class DT, bool BF>
+__global__ __launch_bounds__(256) void maxpool2_bwd_bnbwd_kernel(const DT* __restrict__ dpool,
+                                                                 const DT* __restrict__ skip,
                                                                  const float* __restrict__ z,
                                                                  const float* __restrict__ coef,
                                                                  const float* __restrict__ bcoef, int N, int H, int W,
-                                                                 int C, int ldo, unsigned short* __restrict__ out) {
+                                                                 int C, int ldo, void* __restrict__ out) {
   const int CQ = C >> 2, qs = CQ < 256 ? CQ : 256, wpt = 256 / qs;  // windows per block step
   const int q0 = threadIdx.x % qs, wl = threadIdx.x / qs;
   const long long nwin = (long long)N * ((H + 1) / 2) * ((W + 1) / 2), last = nwin - 1;
@@ -624,10 +632,10 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnbwd_kernel(const unsigned 
     for (long long wi = (long long)blockIdx.x * wpt + wl; wi < nwin; wi += 2 * step) {
       const long long wj = wi + step;
       MpWin A, B;
-      mp_load<true, unsigned short>(dpool, z, skip, wi, H, W, C, c, A);
-      mp_load<true, unsigned short>(dpool, z, skip, min(wj, last), H, W, C, c, B);
-      mp_apply(A, wi, true, H, W, c, ldo, lim, k, out);
-      mp_apply(B, min(wj, last), wj < nwin, H, W, c, ldo, lim, k, out);
+      mp_load<true, DT>(dpool, z, skip, wi, H, W, C, c, A);
+      mp_load<true, DT>(dpool, z, skip, min(wj, last), H, W, C, c, B);
+      mp_apply<BF>(A, wi, true, H, W, c, ldo, lim, k, out);
+      mp_apply<BF>(B, min(wj, last), wj < nwin, H, W, c, ldo, lim, k, out);
     }
   }
 }
@@ -1664,8 +1672,37 @@ extern "C" int pmu_maxpool2_bwd_bnbwd_dxb(const unsigned short* dpool, const uns
   const int wpt = 256 / (CQ < 256 ? CQ : 256);
   const long long nwin = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);
   const long long blocks = std::min<long long>(pmu_cdiv(nwin, 2LL * wpt), 1LL << 20);
-  hipLaunchKernelGGL(maxpool2_bwd_bnbwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dpool, skip,
-                     z, coef, bcoef, N, H, W, C, ldo, dz);
+  hipLaunchKernelGGL((maxpool2_bwd_bnbwd_kernel<unsigned short, true>), dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, dpool, skip, z, coef, bcoef, N, H, W, C, ldo, (void*)dz);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+// The fp32 forms (config c2's skip levels): dpool and skip fp32, dz fp32 — bit-equal to pmu_maxpool2_bwd_bnr
+// accumulating into skip and to pmu_frame_to_f32 of Src(that da, BNBWD, bcoef, z).
+extern "C" int pmu_maxpool2_bwd_bnr_stats(const float* dpool, const float* skip, const float* z, const float* coef,
+                                          const float* mean, const float* invstd, int N, int H, int W, int C,
+                                          float* part, void* stream) {
+  PMU_REQUIRE(dpool && skip && z && coef && mean && invstd && part && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0);
+  const int R = pmu_maxpool2_bwd_bnr_tiles(N, H, W, C);
+  hipLaunchKernelGGL((maxpool2_bwd_bnr_kernel<true, float, false>), dim3((unsigned)R), dim3(256), 0,
+                     (hipStream_t)stream, dpool, z, coef, mean, invstd, N, H, W, C, mpb_wpb(C), (float*)nullptr, part,
+                     skip);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_maxpool2_bwd_bnbwd(const float* dpool, const float* skip, const float* z, const float* coef,
+                                      const float* bcoef, int N, int H, int W, int C, int ldo, float* dz,
+                                      void* stream) {
+  PMU_REQUIRE(dpool && skip && z && coef && bcoef && dz && N > 0 && H > 1 && W > 1 && C > 0 && C % 4 == 0 && ldo == C);
+  const int CQ = C / 4;
+  PMU_REQUIRE(CQ < 256 ? 256 % CQ == 0 : CQ % 256 == 0);
+  const int wpt = 256 / (CQ < 256 ? CQ : 256);
+  const long long nwin = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);
+  const long long blocks = std::min<long long>(pmu_cdiv(nwin, 2LL * wpt), 1LL << 20);
+  hipLaunchKernelGGL((maxpool2_bwd_bnbwd_kernel<float, false>), dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, dpool, skip, z, coef, bcoef, N, H, W, C, ldo, (void*)dz);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -230,6 +230,10 @@ SIGNATURES = {
                                                c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_maxpool2_bwd_bnbwd_dxb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                            c_int, c_int, c_void_p, c_void_p]),
+    "pmu_maxpool2_bwd_bnr_stats": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                           c_int, c_int, c_void_p, c_void_p]),
+    "pmu_maxpool2_bwd_bnbwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                       c_int, c_void_p, c_void_p]),
     "pmu_conv3x3_pack_wino2h_blocks": (c_int, [c_int, c_int, c_int]),
     "pmu_conv3x3_pack_wino2h_multi": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
     "pmu_conv3x3_pack_wino4_blocks": (c_int, [c_int, c_int, c_int]),

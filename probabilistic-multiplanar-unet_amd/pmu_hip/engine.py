@@ -362,32 +362,47 @@ def conv_bn_forward(srcs, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, N, H,
 
 class PoolSumDa:
     """The gradient of a pooled layer's activation, da = dsk + routed dpool (MaxPool2d(2) backward,
-    unet_parts.py:33, plus the skip path, unet_parts.py:66; both parts bf16 from *_dxb input gradients),
-    left unstored: pmu_maxpool2_bwd_bnr_stats_dxb formed its BN-backward partial sums (prod.bnr) and
-    dz_bf16 turns it into that layer's bf16 dz in one pass (pmu_maxpool2_bwd_bnbwd_dxb) — the fp32 da
-    is neither written nor re-read.  materialise() stores it (fp32) for the paths that read da itself."""
+    unet_parts.py:33, plus the skip path, unet_parts.py:66; both parts bf16 from *_dxb input gradients,
+    or both fp32), left unstored: a stats-only max-pool pass (pmu_maxpool2_bwd_bnr_stats{_dxb,}) formed
+    its BN-backward partial sums (prod.bnr) and dz() turns it into that layer's dz in one pass
+    (pmu_maxpool2_bwd_bnbwd{_dxb,}: bf16 dz from bf16 parts, fp32 from fp32 ones) — the fp32 da is
+    neither written nor re-read.  materialise() stores it (fp32) for the paths that read da itself."""
 
     def __init__(self, dpool: torch.Tensor, dsk: torch.Tensor, prod: ConvBNOut):
         self.dpool, self.dsk, self.prod = dpool, dsk, prod
+        self.bf16_parts = dpool.dtype == BF16S
         self.shape = prod.z.shape
         self.dtype = F32
         self.device = prod.z.device
 
-    def dz_bf16(self, bcoef: torch.Tensor) -> torch.Tensor:
+    def dz(self, bcoef: torch.Tensor, bf16: bool):
+        """The layer's dz (bf16 bits or fp32), or None when the parts' storage does not match."""
+        if bf16 != self.bf16_parts:
+            return None
         N, H, W, C = self.shape
-        dz = torch.empty(N, H, W, C, dtype=BF16S, device=self.device)
-        L.call("pmu_maxpool2_bwd_bnbwd_dxb", self.dpool.data_ptr(), self.dsk.data_ptr(), self.prod.z.data_ptr(),
-               self.prod.bn.coef.data_ptr(), bcoef.data_ptr(), N, H, W, C, C, dz.data_ptr(), L.stream())
+        dz = torch.empty(N, H, W, C, dtype=BF16S if bf16 else F32, device=self.device)
+        L.call("pmu_maxpool2_bwd_bnbwd_dxb" if bf16 else "pmu_maxpool2_bwd_bnbwd", self.dpool.data_ptr(),
+               self.dsk.data_ptr(), self.prod.z.data_ptr(), self.prod.bn.coef.data_ptr(), bcoef.data_ptr(), N, H, W, C,
+               C, dz.data_ptr(), L.stream())
         return dz
+
+    def dz_bf16(self, bcoef: torch.Tensor):
+        return self.dz(bcoef, True)
 
     def materialise(self) -> torch.Tensor:
         N, H, W, C = self.shape
         p = self.prod
         part = _empty(L.lib().pmu_maxpool2_bwd_bnr_tiles(N, H, W, C), 2 * C, device=self.device)
-        da = _empty(N, H, W, C, device=self.device)
-        L.call("pmu_maxpool2_bwd_bnr_dxb", self.dpool.data_ptr(), self.dsk.data_ptr(), p.z.data_ptr(),
-               p.bn.coef.data_ptr(), p.bn.mean.data_ptr(), p.bn.invstd.data_ptr(), N, H, W, C, da.data_ptr(),
-               part.data_ptr(), L.stream())
+        if self.bf16_parts:
+            da = _empty(N, H, W, C, device=self.device)
+            L.call("pmu_maxpool2_bwd_bnr_dxb", self.dpool.data_ptr(), self.dsk.data_ptr(), p.z.data_ptr(),
+                   p.bn.coef.data_ptr(), p.bn.mean.data_ptr(), p.bn.invstd.data_ptr(), N, H, W, C, da.data_ptr(),
+                   part.data_ptr(), L.stream())
+        else:   # (the fp32 form accumulates in place: into a copy of the skip gradient)
+            da = self.dsk.clone()
+            L.call("pmu_maxpool2_bwd_bnr", self.dpool.data_ptr(), p.z.data_ptr(), p.bn.coef.data_ptr(),
+                   p.bn.mean.data_ptr(), p.bn.invstd.data_ptr(), N, H, W, C, da.data_ptr(), 1, part.data_ptr(),
+                   L.stream())
         return da
 
 
@@ -480,8 +495,9 @@ def conv_bn_backward(out: ConvBNOut, da: torch.Tensor, conv, bn, grads: dict, ne
     prod = _bnr_producer(out, need_dx, split)
     if out.bf16:
         return _conv_backward_bf16(out, dz_src, conv, dw, need_dx, split, prod, x1_bf16_only, dx_bf16)
-    # (an unstored head gradient gives dz itself, fp32: a RAW source of the same values)
-    dz_src = Src(da.dz(bcoef, False)) if isinstance(da, HeadDa) else _concrete(dz_src)
+    # (an unstored head / pooled gradient gives dz itself, fp32: a RAW source of the same values)
+    dzt = da.dz(bcoef, False) if isinstance(da, (HeadDa, PoolSumDa)) else None
+    dz_src = Src(dzt) if dzt is not None else _concrete(dz_src)
     dzf = frame_of([dz_src], N, H, W)
     if out.xt32 is not None and need_dx:
         return _conv_backward_tee32(out, dz_src, conv, dw, split, prod)
@@ -526,9 +542,17 @@ def _dgrad32(dz_src, conv, N, H, W, split, tee, prod=None):
     dz_src = _f32_srcs([dz_src], N, H, W)[0]
     dzf = frame_of([dz_src], N, H, W)
     lb = L.lib()
-    if use_wino() and wino4_ok(Cout, H, W, "dgrad"):
+    # dz already stored in fp32 (an unstored head / pooled gradient's dz pass): read in place, no copy
+    ready = _materialised([dz_src], F32)
+
+    def dz_tensor():
+        if ready is not None and (tee is None or tee is ready):
+            return ready
         dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
         L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
+        return dzt
+    if use_wino() and wino4_ok(Cout, H, W, "dgrad"):
+        dzt = dz_tensor()
         wp = pack_weights_wino4(conv.weight, dgrad=True)
         if prod is not None:
             _bnr_call("pmu_conv3x3_dgrad_wino4_bnr", prod, lb.pmu_conv3x3_tiles_wino4(N, H, W),
@@ -537,8 +561,7 @@ def _dgrad32(dz_src, conv, N, H, W, split, tee, prod=None):
             L.call("pmu_conv3x3_dgrad_wino4", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
                    L.ptr(dx1), s)
     elif use_wino() and wino_raw_ok(Cout) and wino2h_ok(Cout):
-        dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
-        L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
+        dzt = dz_tensor()
         wp = pack_weights_wino2h(conv.weight, dgrad=True)
         if prod is not None:
             _bnr_call("pmu_conv3x3_dgrad_wino2h_bnr", prod, lb.pmu_conv3x3_tiles_wino2h(N, H, W),
@@ -547,18 +570,19 @@ def _dgrad32(dz_src, conv, N, H, W, split, tee, prod=None):
             L.call("pmu_conv3x3_dgrad_wino2h", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
                    L.ptr(dx1), s)
     elif use_wino() and wino_raw_ok(Cout):
-        dzt = tee if tee is not None else _empty(N, H, W, Cout, device=dev)
-        L.call("pmu_frame_to_f32", dzf, dzt.data_ptr(), s)
+        dzt = dz_tensor()
         wp = pack_weights_wino(conv.weight, dgrad=True)
         L.call("pmu_conv3x3_dgrad_wino_raw", dzt.data_ptr(), Cout, N, H, W, wp.data_ptr(), Cin, sp, dx0.data_ptr(),
                L.ptr(dx1), s)
-    elif use_wino():
-        wp = pack_weights_wino(conv.weight, dgrad=True)
-        L.call("pmu_conv3x3_dgrad_wino", dzf, wp.data_ptr(), Cin, sp, dx0.data_ptr(), L.ptr(dx1), L.ptr(tee), s)
     else:
-        wp = pack_weights(conv.weight, dgrad=True)
-        L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, sp, dx0.data_ptr(),
-               L.ptr(dx1), L.ptr(tee), s)
+        tee = None if (ready is not None and tee is ready) else tee   # (the tee would be the source itself)
+        if use_wino():
+            wp = pack_weights_wino(conv.weight, dgrad=True)
+            L.call("pmu_conv3x3_dgrad_wino", dzf, wp.data_ptr(), Cin, sp, dx0.data_ptr(), L.ptr(dx1), L.ptr(tee), s)
+        else:
+            wp = pack_weights(conv.weight, dgrad=True)
+            L.call("pmu_conv3x3_dgrad", dzf, conv.weight.data_ptr(), wp.data_ptr(), Cin, sp, dx0.data_ptr(),
+                   L.ptr(dx1), L.ptr(tee), s)
     return dx0 if split is None else (dx0, dx1)
 
 
@@ -571,7 +595,9 @@ def _conv_backward_tee32(out: ConvBNOut, dz_src, conv, dw, split, prod=None):
     N, H, W, Cout = out.z.shape
     dev = out.z.device
     Cin = conv.in_channels
-    dzt = _empty(N, H, W, Cout, device=dev)
+    # (a dz already stored in fp32 is the tee itself)
+    dzt = _materialised([dz_src], F32)
+    dzt = dzt if dzt is not None else _empty(N, H, W, Cout, device=dev)
     res = _dgrad32(dz_src, conv, N, H, W, split, dzt, prod)
     wsb4 = (lb.pmu_conv3x3_wgrad_ws_wino4(N, H, W, Cin, Cout)
             if (use_wino() and CFG.wgrad4 and L.experiments_build()) else 0)
@@ -620,9 +646,9 @@ def _conv_backward_bf16(out: ConvBNOut, dz_src: Src, conv, dw, need_dx, split, p
     N, H, W, Cout = out.z.shape
     dev = out.z.device
     Cin = conv.in_channels
-    if isinstance(dz_src.x, (PoolSumDa, HeadDa)):
-        dzt = dz_src.x.dz_bf16(dz_src.coef)
-    else:
+    dzt = dz_src.x.dz_bf16(dz_src.coef) if isinstance(dz_src.x, (PoolSumDa, HeadDa)) else None
+    if dzt is None:
+        dz_src = _concrete(dz_src)
         dzt = frame_to_bf16([dz_src], N, H, W)
     res = None
     if need_dx:
@@ -1277,6 +1303,18 @@ def unet_backward(net, st: UNetState, dy: torch.Tensor, grads: GradSink | None =
                 dpool = frame_to_f32([Src(dpool)], N, hp // 2, wp // 2)
             if dsk.dtype == BF16S:
                 dskip[lev - 1] = frame_to_f32([Src(dsk)], N, hp, wp)
+            if bn_ok and CFG.pool_fuse and pool_fuse_ok(Cp) and dpool.dtype == F32 and dskip[lev - 1].dtype == F32:
+                # fp32 parts (config c2): the pooled layer's da stays unstored as above (fp32 dz)
+                dsk = dskip[lev - 1]
+                R = L.lib().pmu_maxpool2_bwd_bnr_tiles(N, hp, wp, Cp)
+                part = _empty(R, 2 * Cp, device=dev)
+                L.call("pmu_maxpool2_bwd_bnr_stats", dpool.data_ptr(), dsk.data_ptr(), prev.z.data_ptr(),
+                       prev.bn.coef.data_ptr(), prev.bn.mean.data_ptr(), prev.bn.invstd.data_ptr(), N, hp, wp, Cp,
+                       part.data_ptr(), s)
+                dsum = PoolSumDa(dpool, dsk, prev)
+                dskip[lev - 1] = dsum
+                prev.bnr = (dsum, part, R)
+                continue
             if bn_ok:
                 # routed into the skip gradient, which completes the pooled layer's da: the same pass
                 # forms that layer's BN-backward partial sums (no pmu_bn_bwd_reduce for it)

@@ -1,6 +1,7 @@
 """The pooled layer's activation gradient left unstored (engine.PoolSumDa, CFG.pool_fuse; config c5's
 skip levels): da = skip + routed dpool (MaxPool2d(2) backward, PMU/model/unet/unet_parts.py:33, plus the
-skip path, unet_parts.py:66) is formed twice in registers instead of written in fp32 and re-read —
+skip path, unet_parts.py:66) is formed twice in registers instead of written in fp32 and re-read (bf16
+parts with a bf16 dz, or — config c2 — fp32 parts with an fp32 dz) —
   * pmu_maxpool2_bwd_bnr_stats_dxb: the BN-backward partial sums alone, bit-equal to those of
     pmu_maxpool2_bwd_bnr_dxb;
   * pmu_maxpool2_bwd_bnbwd_dxb: the layer's bf16 dz, bit-equal to pmu_frame_to_bf16 of the BN-backward
@@ -46,6 +47,36 @@ def test_stats_and_dz_match_stored_da(dev, N, H, W, C):
     assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("N,H,W,C", [(2, 64, 64, 64), (1, 33, 45, 32), (2, 16, 16, 512), (32, 64, 64, 128)])
+def test_fp32_stats_and_dz_match_stored_da(dev, N, H, W, C):
+    """fp32 parts (config c2): the partials bit-equal to pmu_maxpool2_bwd_bnr accumulating into the skip
+    gradient, dz bit-equal to pmu_frame_to_f32 of the BN-backward frame over that stored da."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_to_f32
+    from test_bnr_gpu import _bn_inputs
+    g = torch.Generator().manual_seed(73 + H + C)
+    z, coef, mean, invstd = _bn_inputs(N, H, W, C, g, dev)
+    dp = torch.randn(N, H // 2, W // 2, C, generator=g).to(dev)
+    sk = torch.randn(N, H, W, C, generator=g).to(dev)
+    bcoef = torch.cat([coef[:C].cpu(), coef[C:].cpu(), torch.randn(C, generator=g) * 0.2,
+                       torch.randn(C, generator=g), torch.randn(C, generator=g)]).to(dev)
+    R = L.lib().pmu_maxpool2_bwd_bnr_tiles(N, H, W, C)
+    da = sk.clone()
+    part = torch.full((R, 2 * C), float("nan"), device=dev)
+    L.call("pmu_maxpool2_bwd_bnr", dp.data_ptr(), z.data_ptr(), coef.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+           N, H, W, C, da.data_ptr(), 1, part.data_ptr(), L.stream())
+    ps = torch.full((R, 2 * C), float("nan"), device=dev)
+    L.call("pmu_maxpool2_bwd_bnr_stats", dp.data_ptr(), sk.data_ptr(), z.data_ptr(), coef.data_ptr(),
+           mean.data_ptr(), invstd.data_ptr(), N, H, W, C, ps.data_ptr(), L.stream())
+    want = frame_to_f32([Src(da, L.SRC_BNBWD, bcoef, z=z)], N, H, W)
+    got = torch.full((N, H, W, C), float("nan"), device=dev)
+    L.call("pmu_maxpool2_bwd_bnbwd", dp.data_ptr(), sk.data_ptr(), z.data_ptr(), coef.data_ptr(), bcoef.data_ptr(),
+           N, H, W, C, C, got.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ps, part)
+    assert torch.equal(got, want)
+
+
 def test_bnbwd_refuses_unsupported_channels(dev):
     from pmu_hip import _lib as L
     from pmu_hip.engine import pool_fuse_ok
@@ -56,18 +87,21 @@ def test_bnbwd_refuses_unsupported_channels(dev):
     assert rc == L.PMU_ERR_ARG
 
 
-@pytest.mark.parametrize("filters,N,H", [([16, 32, 64, 128], 2, 128), ([64, 128, 256, 512, 1024], 2, 64)])
-def test_unet_backward_bit_identical(dev, filters, N, H):
-    """model.UNet under autocast: every gradient bit-identical with CFG.pool_fuse on and off."""
+@pytest.mark.parametrize("bf16,channels,classes,filters,N,H", [(True, 3, 3, [16, 32, 64, 128], 2, 128),
+                                                               (True, 3, 3, [64, 128, 256, 512, 1024], 2, 64),
+                                                               (False, 1, 1, [16, 32, 64, 128], 2, 64),
+                                                               (False, 1, 1, [64, 128, 256, 512, 1024], 4, 64)])
+def test_unet_backward_bit_identical(dev, bf16, channels, classes, filters, N, H):
+    """model.UNet (under autocast: bf16 parts; fp32: c2's path): every gradient bit-identical with
+    CFG.pool_fuse on and off."""
     from model import UNet
     from pmu_hip import engine
-    import oracle.unet_ref as ur
     torch.manual_seed(0)
-    net = UNet(3, 3, filters).to(dev).train()
+    net = UNet(channels, classes, filters).to(dev).train()
     sd = {k: v.clone() for k, v in net.state_dict().items()}
     g = torch.Generator().manual_seed(8)
-    x = torch.rand(N, 3, H, H, generator=g).to(dev)
-    tgt = torch.randint(0, 3, (N, 1, H, H), generator=g).to(dev)
+    x = torch.rand(N, channels, H, H, generator=g).to(dev)
+    r = torch.randn(N, classes, H, H, generator=g).to(dev)
     grads = []
     old = engine.CFG.pool_fuse
     try:
@@ -75,9 +109,9 @@ def test_unet_backward_bit_identical(dev, filters, N, H):
             engine.CFG.pool_fuse = fuse
             net.load_state_dict(sd)
             net.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
                 out = net(x)
-            ur.unet_loss(out, tgt, 3).backward()
+            (out.float() * r).sum().backward()
             torch.cuda.synchronize()
             grads.append({k: p.grad.clone() for k, p in net.named_parameters()})
     finally:
