@@ -13,3 +13,10 @@ for wl in unet c5 probunet; do
   head -1 $O/summary_$wl.txt
 done
 echo round-b-done
+# c4 A/B of the pooled-gradient fusion (fp32 parts)
+cd $R
+for f in 0 1 0 1; do
+  PMU_POOL_FUSE=$f timeout -k 10 600 python bench.py --workload probunet --no-cpu-baseline > $O/bench_c4_fuse$f.json 2> $O/bench_c4_fuse$f.err || exit $?
+  python -c "import json;d=json.load(open('$O/bench_c4_fuse$f.json'));print('c4 pool_fuse=$f', d['value'], d['ms_per_step'])"
+done
+echo round-b2-done
