@@ -363,36 +363,42 @@ __global__ __launch_bounds__(16 * WCO_, 1) void wgrad3x3_wino32_kernel(WgwArgs a
 }
 
 // dw[co][ci][3][3] = G^T (sum over splits of M) G, G = [1 0 0; 1/2 1/2 1/2; 1/2 -1/2 1/2; 0 0 1].
-// Block = 16 consecutive (co, ci) elements x 16 components: thread (comp = t >> 4, e = t & 15) sums
-// its slab column over the splits (4 independent partial sums, combined in a fixed order:
-// deterministic), the 16 sums meet in LDS and 16 threads apply the output transform.  (One thread
-// per element walking 16 x nsplit loads left the small-channel layers latency-bound: 16 blocks for
-// a 64 x 64 layer.)
-__global__ __launch_bounds__(256) void wgrad_wino_reduce_kernel(const float* __restrict__ ws, int nsplit, int Cout,
-                                                                int Cin, float* __restrict__ dw) {
-  __shared__ float mm[16][17];
-  const long long CC = (long long)Cout * Cin;
-  const int c = threadIdx.x >> 4, el = threadIdx.x & 15;
-  const long long e = (long long)blockIdx.x * 16 + el;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (e < CC) {
-    const float* p = ws + (long long)c * CC + e;
-    const long long st = 16 * CC;
-    int sp = 0;
-    for (; sp + 3 < nsplit; sp += 4) {
-      s0 += p[(long long)sp * st];
-      s1 += p[(long long)(sp + 1) * st];
-      s2 += p[(long long)(sp + 2) * st];
-      s3 += p[(long long)(sp + 3) * st];
-    }
-    for (; sp < nsplit; ++sp) s0 += p[(long long)sp * st];
+// Block = 64 consecutive (co, ci) elements x 16 components x 4 split residues (1024 threads): thread
+// (q = t >> 8, comp = (t >> 4) & 15, four elements (t & 15) * 4 ...) sums splits q, q + 4, ... of its
+// float4 slab column (residue 0 also the tail past the last full group of 4), the four partial sums meet
+// in LDS in the fixed order (s0 + s1) + (s2 + s3) — deterministic — and 64 threads apply the output
+// transform.  (16 B per load: the 4-B loads of one thread per (element, residue) kept ~1/4 of the
+// bytes in flight and left the reduction latency-bound at ~21 us whatever the layer.)
+__global__ __launch_bounds__(1024) void wgrad_wino_reduce_kernel(const float* __restrict__ ws, int nsplit, int Cout,
+                                                                 int Cin, float* __restrict__ dw) {
+  __shared__ float red[4][16][65];
+  const long long CC = (long long)Cout * Cin;  // a multiple of 64 (pmu_conv3x3_wgrad_wino)
+  const int q = threadIdx.x >> 8, c = (threadIdx.x >> 4) & 15, e4 = (threadIdx.x & 15) * 4;
+  const long long e = (long long)blockIdx.x * 64 + e4;
+  const float* p = ws + (long long)c * CC + e;
+  const long long st = 16 * CC;
+  const int full = nsplit >> 2;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+  for (int k = 0; k < full; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(p + (long long)(4 * k + q) * st);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
-  mm[c][el] = (s0 + s1) + (s2 + s3);
+  if (q == 0)
+    for (int sp = 4 * full; sp < nsplit; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(p + (long long)sp * st);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  red[q][c][e4 + 0] = s.x;
+  red[q][c][e4 + 1] = s.y;
+  red[q][c][e4 + 2] = s.z;
+  red[q][c][e4 + 3] = s.w;
   __syncthreads();
-  if (threadIdx.x >= 16 || e >= CC) return;
+  if (threadIdx.x >= 64) return;
+  const int el = threadIdx.x;
   float m[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) m[k] = mm[k][el];
+  for (int k = 0; k < 16; ++k) m[k] = (red[0][k][el] + red[1][k][el]) + (red[2][k][el] + red[3][k][el]);
   float t[3][4];  // G^T M
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -401,7 +407,7 @@ __global__ __launch_bounds__(256) void wgrad_wino_reduce_kernel(const float* __r
     t[1][k] = 0.5f * (m[4 + k] - m[8 + k]);
     t[2][k] = h + m[12 + k];
   }
-  float* o = dw + e * 9;
+  float* o = dw + ((long long)blockIdx.x * 64 + el) * 9;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float h = 0.5f * (t[i][1] + t[i][2]);
@@ -499,8 +505,8 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
   else
     hipLaunchKernelGGL((wgrad3x3_wino32_kernel<0>), grid, dim3(NT), 0, st, a);
   PMU_CHECK_LAUNCH();
-  const long long CC = (long long)Cout * Cin;
-  hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3((unsigned)((CC + 15) / 16)), dim3(256), 0, st, (const float*)ws,
+  const long long CC = (long long)Cout * Cin;  // Cout % WCO, Cin % WCI: a multiple of 64
+  hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3((unsigned)(CC / 64)), dim3(1024), 0, st, (const float*)ws,
                      a.nsplit, Cout, Cin, dw);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
