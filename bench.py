@@ -652,7 +652,7 @@ def build_probunet(args, dev, world, rank):
     Fcomb in one fused pass + per-class Dice counts of every sample."""
     from model import ProbabilisticUnet
     from pmu_hip.functions import flat_grad_buffer
-    from pmu_hip.metrics import dice_counts
+    from pmu_hip.metrics import dice_counts_many
     from pmu_hip.optim import FusedSGD
     import torch.distributed as dist
     torch.manual_seed(0)
@@ -689,8 +689,7 @@ def build_probunet(args, dev, world, rank):
         opt.step(grad_scale=1.0 / world)
         with torch.no_grad():
             ys = net.sample_many(n_samples)                  # (16, B, 3, S, S)
-            for s_ in range(n_samples):
-                dice_counts(ys[s_], segm, n_cls)
+            dice_counts_many(ys, segm, n_cls)                # every sample's counts, one launch
         return loss
 
     config = {"workload": "c4: ProbabilisticUnet(1, 3, %s, latent_dim=6, no_convs_fcomb=4, beta=10), %dx%dx1 "

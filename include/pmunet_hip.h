@@ -466,6 +466,11 @@ int pmu_ce_bwd(const float* x, const long long* tgt, int N, int K, long long HW,
  * y NCHW [N][K][H][W], mask [N][H][W]. */
 int pmu_dice_counts(const float* y, const float* mask, int N, int K, int H, int W,
                     double* counts, void* stream);
+/* pmu_dice_counts of S predictions y[S][N][K][H][W] against one mask in one launch: counts[S][K][3],
+ * the same integers as S pmu_dice_counts calls (the eval over several prior samples,
+ * PMU/trainer/probunet_trainer.py:41-60). */
+int pmu_dice_counts_many(const float* y, const float* mask, int S, int N, int K, int H, int W, double* counts,
+                         void* stream);
 
 /* (sum a*b, sum a, sum b) over n elements into out[3] (fp64): dice_coeff's three sums
  * (PMU/dice_loss.py:5-12) for arbitrary pred/target tensors. */

@@ -1314,9 +1314,12 @@ __global__ __launch_bounds__(256) void sgd_clip_kernel(const pmu_sgd_chunk* __re
 // and fp64 adds per pixel, and the per-counter LDS tree with 9 barriers each, made the previous
 // version ~140 us per call for a 32 x 256^2 batch.
 constexpr int DICE_T = 256, DICE_MAXB = 512;
+// blockIdx.y: the prediction (sample) of a batched call — y + y * N K H W, its counters out + y * 3 K
 __global__ __launch_bounds__(DICE_T) void dice_counts_kernel(const float* __restrict__ y, const float* __restrict__ mask,
                                                              int N, int K, int H, int W, double* __restrict__ out) {
   __shared__ unsigned red[DICE_T / 64][3 * HEAD_KMAX];
+  y += (size_t)blockIdx.y * N * K * H * W;
+  out += (size_t)blockIdx.y * 3 * K;
   const unsigned HW = (unsigned)H * (unsigned)W;
   const unsigned P = (unsigned)N * HW;  // < 2^31, host-checked
   const int KK = K == 1 ? 1 : K;
@@ -1890,6 +1893,20 @@ extern "C" int pmu_dice_counts(const float* y, const float* mask, int N, int K, 
   unsigned g = (unsigned)pmu_cdiv(P, DICE_T * 8);
   if (g > DICE_MAXB) g = DICE_MAXB;
   hipLaunchKernelGGL(dice_counts_kernel, dim3(g), dim3(DICE_T), 0, (hipStream_t)stream, y, mask, N, K, H, W, counts);
+  PMU_CHECK_LAUNCH();
+  return PMU_OK;
+}
+
+extern "C" int pmu_dice_counts_many(const float* y, const float* mask, int S, int N, int K, int H, int W,
+                                    double* counts, void* stream) {
+  PMU_REQUIRE(y && mask && counts && S > 0 && S <= 65535 && N > 0 && K >= 1 && K <= HEAD_KMAX && H > 0 && W > 0);
+  if (hipMemsetAsync(counts, 0, sizeof(double) * 3 * K * S, (hipStream_t)stream) != hipSuccess) return PMU_ERR_ARG;
+  const long long P = (long long)N * H * W;
+  PMU_REQUIRE(P < (1LL << 31));
+  unsigned g = (unsigned)pmu_cdiv(P, DICE_T * 8);
+  if (g > DICE_MAXB) g = DICE_MAXB;
+  hipLaunchKernelGGL(dice_counts_kernel, dim3(g, (unsigned)S), dim3(DICE_T), 0, (hipStream_t)stream, y, mask, N, K,
+                     H, W, counts);
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -159,6 +159,7 @@ SIGNATURES = {
     "pmu_ce_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_longlong, c_int, c_longlong, c_void_p, c_void_p,
                            c_void_p, c_void_p]),
     "pmu_dice_counts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "pmu_dice_counts_many": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pmu_dice_sums": (c_int, [c_void_p, c_void_p, c_longlong, c_void_p, c_void_p]),
     "pmu_slice_view_layout": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                       c_void_p]),

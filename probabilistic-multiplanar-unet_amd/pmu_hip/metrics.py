@@ -31,6 +31,22 @@ def dice_counts(y: torch.Tensor, mask: torch.Tensor, n_classes: int) -> torch.Te
     return counts
 
 
+def dice_counts_many(ys: torch.Tensor, mask: torch.Tensor, n_classes: int) -> torch.Tensor:
+    """(S, K, 3) float64 counts of S predictions ys (S,N,K,H,W) against one mask, in one launch
+    (pmu_dice_counts_many) — the same integers as S dice_counts calls (the trainers' eval over
+    several samples, probunet_trainer.py:41-60)."""
+    if not ys.is_cuda:
+        raise RuntimeError("dice_counts runs on the MI355X HIP path only (there is no CPU fallback)")
+    S, N, K, H, W = ys.shape
+    if K != n_classes:
+        raise ValueError(f"prediction has {K} channels, expected n_classes={n_classes}")
+    yc = ys.detach().float().contiguous()
+    mc = mask.detach().to(device=ys.device, dtype=torch.float32).reshape(N, H, W).contiguous()
+    counts = torch.empty(S, K, 3, dtype=torch.float64, device=ys.device)
+    L.call("pmu_dice_counts_many", yc.data_ptr(), mc.data_ptr(), S, N, K, H, W, counts.data_ptr(), L.stream())
+    return counts
+
+
 def dice_from_counts(c: torch.Tensor) -> torch.Tensor:
     """fp32 (2 I + s) / (P + T + s), the reference's arithmetic on its fp32 sums."""
     c = c.float()

@@ -323,3 +323,20 @@ def test_dice_counts_multiblock_exact(K):
         want = torch.tensor([[((am == k) & (t == k)).sum(), (am == k).sum(), (t == k).sum()] for k in range(K)],
                             dtype=torch.float64)
     assert torch.equal(got, want), (got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,S", [(1, 3), (3, 16), (4, 5)])
+def test_dice_counts_many_equals_per_sample(K, S):
+    """pmu_dice_counts_many (the c4 eval's 16 prior samples in one launch): every sample's counts equal
+    its own pmu_dice_counts call exactly."""
+    from pmu_hip.metrics import dice_counts, dice_counts_many
+    g = torch.Generator().manual_seed(11 + K + S)
+    N, H, W = 4, 96, 80
+    ys = torch.randn(S, N, K, H, W, generator=g) if K > 1 else torch.rand(S, N, 1, H, W, generator=g)
+    mask = torch.randint(0, max(K, 2), (N, 1, H, W), generator=g).float().cuda()
+    ys = ys.cuda()
+    got = dice_counts_many(ys, mask, K).cpu()
+    assert got.shape == (S, K, 3)
+    for s in range(S):
+        assert torch.equal(got[s], dice_counts(ys[s], mask, K).cpu()), s
