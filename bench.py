@@ -702,6 +702,77 @@ def build_probunet(args, dev, world, rank):
     return step, None, config, data
 
 
+def mfma_families(per):
+    """Group the instrumented step's MFMA C-ABI entries into kernel families (KernelTimer._base: a fused
+    variant — BN-backward epilogue _bnr, bf16 dx _dxb, concat copies _x1b(_sum), in-place concat _ld(b) —
+    is the same GEMM as its plain entry) and rank them by their summed launch time.  Returns
+    [(family, [launches, executed FLOPs, seconds, direct-sum FLOPs], [member entries])], longest first:
+    c5's input gradient, split over _bnr_dxb / _x1b_sum_dxb / _dxb entries, is one family."""
+    fam = {}
+    for k, v in per.items():
+        if k not in KernelTimer.MFMA:
+            continue
+        b = KernelTimer._base(k)
+        d, members = fam.setdefault(b, ([0, 0.0, 0.0, 0.0], []))
+        for i in range(4):
+            d[i] += v[i]
+        members.append(k)
+    return sorted(((b, d, sorted(m)) for b, (d, m) in fam.items()), key=lambda e: -e[1][2])
+
+
+def roofline_entry(workload, family, d, members):
+    """The roofline object of one MFMA kernel family: executed FLOPs / its HIP-event time vs the dtype
+    peak, PMC traffic per launch from the newest committed summary."""
+    n, fl, t, dfl = d
+    ach = fl / t / 1e12
+    traffic, tsrc = pmc_traffic(workload, family)
+    peak = roofline_peak(family)
+    roof = {"kernel": family, "members": members, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+            "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "bytes/launch (HBM)",
+            "traffic_source": tsrc, "launches": n, "avg_launch_ms": round(t / n * 1e3, 4),
+            "family_ms": round(t * 1e3, 3), "flops_per_launch": fl / n,
+            "flops_basis": "MFMA products the kernel executes"}
+    if "_wino" in family:  # Winograd executes 16 of the direct sum's 36 products per 2x2 tile
+        roof["flops_basis"] = ("executed Winograd F(2x2,3x3) MFMA products (16 per 2x2 output tile per "
+                               "channel pair); frac is MFMA utilisation")
+        if family.endswith("_wino4"):
+            roof["flops_basis"] = ("executed Winograd F(4x4,3x3) MFMA products (36 per 4x4 output tile per "
+                                   "channel pair); frac is MFMA utilisation")
+        roof["direct_sum_flops_per_launch"] = dfl / n
+        roof["direct_sum_equiv_tflops"] = round(dfl / t / 1e12, 2)
+        roof["direct_sum_equiv_frac"] = round(dfl / t / 1e12 / peak, 4)
+        roof["direct_sum_note"] = ("SURVEY.md §8(d) basis (9 MACs per pixel per channel pair): >1 is possible "
+                                   "because Winograd executes 16/36 (F(2x2)) or 36/144 (F(4x4)) of those "
+                                   "products; not a utilisation")
+    return roof
+
+
+def check_layout(backend, world, ndev):
+    """Refuse a rank layout that would not time ``world`` distinct GPUs (pure host logic): under RCCL
+    (backend nccl) every rank needs its own device, so world > the visible device count is an error;
+    gloo may rehearse N ranks on fewer GPUs.  Returns an error message or None."""
+    if world > 1 and backend == "nccl" and world > ndev:
+        return (f"{world} RCCL ranks but {ndev} visible GPU(s): each rank needs its own device "
+                f"(PMU_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
+    return None
+
+
+def check_devices(backend, devices):
+    """Refuse an RCCL run whose ranks report the same GPU (devices: one PCI identity per rank, gathered
+    to every rank).  Returns an error message or None."""
+    if backend == "nccl" and len(set(devices)) != len(devices):
+        return f"RCCL ranks share a GPU: {devices}"
+    return None
+
+
+def device_identity(dev):
+    """PCI domain:bus:device of a GPU (and its uuid): one string per physical device."""
+    p = torch.cuda.get_device_properties(dev)
+    return "%04x:%02x:%02x.0 %s" % (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                                    getattr(p, "pci_device_id", 0), str(getattr(p, "uuid", "")))
+
+
 def launch_plan(gpus, argv, env):
     """How to run ``bench.py --gpus N`` (pure host logic, no GPU call).
 
@@ -781,14 +852,29 @@ def main():
     # rehearsed on fewer GPUs (PMU_DIST_BACKEND=gloo: RCCL needs distinct devices per rank)
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(1, ndev))
+    backend = os.environ.get("PMU_DIST_BACKEND", "nccl") if world > 1 else None
+    err = check_layout(backend, world, ndev)
+    if err:
+        print(f"bench.py: {err}", file=sys.stderr)
+        return 2
+    dist_info = {"backend": backend, "world": world, "visible_devices": ndev}
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(dev)
-        backend = os.environ.get("PMU_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        devices = [None] * world
+        dist.all_gather_object(devices, device_identity(dev))
+        dist_info["devices"] = devices
+        err = check_devices(backend, devices)
+        if err:
+            print(f"bench.py: {err}", file=sys.stderr)
+            dist.destroy_process_group()
+            return 2
+    else:
+        dist_info["devices"] = [device_identity(dev)]
 
     from pmu_hip import _lib as L
 
@@ -817,7 +903,7 @@ def main():
     ms = dt / args.steps * 1e3
     value = world * B * args.steps / dt
 
-    roof = kernels = mfma_busy = None
+    roof = roof_next = kernels = mfma_busy = None
     if not args.no_kernel_timing:
         timer = KernelTimer()
         L.set_call_observer(timer)
@@ -825,28 +911,10 @@ def main():
         L.set_call_observer(None)
         per = timer.summary()
         mf = {k: v for k, v in per.items() if k in KernelTimer.MFMA}
-        dom = max(mf, key=lambda k: mf[k][2])
-        n, fl, t, dfl = mf[dom]
-        ach = fl / t / 1e12
-        traffic, tsrc = pmc_traffic(args.workload, dom)
-        peak = roofline_peak(dom)
-        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                "traffic": round(traffic) if traffic is not None else None, "traffic_unit": "bytes/launch (HBM)",
-                "traffic_source": tsrc, "launches": n, "avg_launch_ms": round(t / n * 1e3, 4),
-                "flops_per_launch": fl / n, "flops_basis": "MFMA products the kernel executes"}
-        if "_wino" in dom:  # Winograd executes 16 of the direct sum's 36 products per 2x2 tile
-            roof["flops_basis"] = ("executed Winograd F(2x2,3x3) MFMA products (16 per 2x2 output tile per "
-                                   "channel pair); frac is MFMA utilisation")
-            if dom.endswith("_wino4"):
-                roof["flops_basis"] = ("executed Winograd F(4x4,3x3) MFMA products (36 per 4x4 output tile per "
-                                       "channel pair); frac is MFMA utilisation")
-            roof["direct_sum_flops_per_launch"] = dfl / n
-            roof["direct_sum_equiv_tflops"] = round(dfl / t / 1e12, 2)
-            roof["direct_sum_equiv_frac"] = round(dfl / t / 1e12 / peak, 4)
-            roof["direct_sum_note"] = ("SURVEY.md §8(d) basis (9 MACs per pixel per channel pair): >1 is possible "
-                                       "because Winograd executes 16/36 (F(2x2)) or 36/144 (F(4x4)) of those "
-                                       "products; not a utilisation")
+        fams = mfma_families(per)
+        # the dominant MFMA kernel family (summed over its fused entry variants) and the runner-up
+        roof = roofline_entry(args.workload, *fams[0])
+        roof_next = roofline_entry(args.workload, *fams[1]) if len(fams) > 1 else None
         kernels = {k: {"launches": v[0], "ms": round(v[2] * 1e3, 3),
                        "tflops": (round(v[1] / v[2] / 1e12, 2) if v[1] else None)} for k, v in sorted(per.items())}
         # executed MFMA work of the step at each kernel's own peak, over the step time: the MFMA-busy
@@ -872,7 +940,7 @@ def main():
             "step_mfma_busy_frac": round(mfma_busy, 4) if mfma_busy is not None else None,
             "step_mfma_busy_basis": ("sum over MFMA kernels of executed FLOPs / that kernel's dtype peak, over the "
                                      "step time (HIP events of one instrumented step)"),
-            "roofline": roof, "cpu_baseline": cpu, "dice_vs_ref": dvr, "kernels": kernels,
+            "roofline": roof, "roofline_next": roof_next, "dist": dist_info, "cpu_baseline": cpu, "dice_vs_ref": dvr, "kernels": kernels,
             "loss": float(loss.detach()),
         }
         if evalres is not None:

@@ -51,7 +51,17 @@ def _dma_zb(x, cin, cout):
 BF16_DX = True
 
 
+# AUTOCAST_ALL: torch.autocast(bfloat16)'s own semantics instead of the HIP path's shape rules — every
+# conv and transposed conv (the Cin <= 4 first layer included) rounds its operands, weights, incoming
+# gradient and input gradient to bf16, whatever its shape.  Used to measure what autocast itself does to
+# the reference's trajectory (tools/dice_gap_seeds.py) and how far the HIP path's fp32 exceptions (the
+# first layer, input gradients of maps < 32 wide, ConvT shapes off the LDS-DMA kernel) sit from it.
+AUTOCAST_ALL = False
+
+
 def _dma_dxb(x, cin, cout, split):
+    if AUTOCAST_ALL:
+        return BF16_DX
     return (BF16_DX and x.shape[3] >= 32 and ((cout + 7) // 8 * 8) % 16 == 0 and cin % 8 == 0
             and (split is None or split == cin or split % 32 == 0))
 
@@ -123,7 +133,7 @@ def double_conv(x, sd, pre, training, bf16=False, first_fp32=False, split=None, 
     HIP path's Cin <= 4 first-layer kernel).  dxb: the block sits inside the UNet's backward, where the
     HIP path keeps bf16 activation gradients (BF16_DX); split: the first conv's concat split."""
     for i in (0, 3):
-        use = bf16 and not (first_fp32 and i == 0)
+        use = bf16 and (AUTOCAST_ALL or not (first_fp32 and i == 0))
         w = sd[f"{pre}double_conv.{i}.weight"]
         zb = use and _dma_zb(x, w.shape[1], w.shape[0])
         rdx = use and dxb and _dma_dxb(x, w.shape[1], w.shape[0], split if i == 0 else None)
@@ -152,8 +162,8 @@ def unet_forward(sd, x, n_levels, n_classes, apply_last_layer=True, training=Tru
         wt = sd[pre + "up.weight"]
         if bf16:  # the HIP path's bf16 convT where its kernels take the shapes (pmu_convT2x2_bf16_ok)
             cin, cout = wt.shape[0], wt.shape[1]
-            fwd_b = cin % 32 == 0 and cout % 32 == 0 and (4 * cout) % 128 == 0
-            dma_d = cin % 128 == 0 and cout % 32 == 0   # pmu_convT2x2_dma_ok(cin, cout, 1)
+            fwd_b = AUTOCAST_ALL or (cin % 32 == 0 and cout % 32 == 0 and (4 * cout) % 128 == 0)
+            dma_d = AUTOCAST_ALL or (cin % 128 == 0 and cout % 32 == 0)   # pmu_convT2x2_dma_ok(cin, cout, 1)
             x1 = Bf16ConvT2x2.apply(x1, wt, sd[pre + "up.bias"], fwd_b, dma_d, BF16_DX and dma_d)
         else:
             x1 = F.conv_transpose2d(x1, wt, sd[pre + "up.bias"], stride=2)
@@ -214,14 +224,15 @@ def unet_param_keys(sd):
                                   or k.endswith("num_batches_tracked"))]
 
 
-def unet_train_step(sd, x, target, n_levels, n_classes, lr=None, bufs=None):
+def unet_train_step(sd, x, target, n_levels, n_classes, lr=None, bufs=None, bf16=False):
     """One reference training step on CPU: forward, loss, backward (+ optional clip/SGD).
-    Returns (out, loss, grads) and updates sd's running stats (and params if lr)."""
+    Returns (out, loss, grads) and updates sd's running stats (and params if lr).  bf16: the forward in
+    the HIP path's torch.autocast(bfloat16) arithmetic (unet_forward's bf16)."""
     keys = unet_param_keys(sd)
     params = {k: sd[k].detach().clone().requires_grad_(True) for k in keys}
     work = dict(sd)
     work.update(params)
-    out = unet_forward(work, x, n_levels, n_classes)
+    out = unet_forward(work, x, n_levels, n_classes, bf16=bf16)
     loss = unet_loss(out, target, n_classes)
     loss.backward()
     grads = {k: params[k].grad.detach().clone() for k in keys}

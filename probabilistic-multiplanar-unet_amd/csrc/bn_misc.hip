@@ -533,7 +533,9 @@ __device__ __forceinline__ void mp_apply(const MpWin& m, long long wi, bool vali
   }
 }
 
-// base: the skip gradient accumulated into (ACC; dx itself for fp32, a bf16 tensor for DT = bf16)
+// base: the skip gradient accumulated into (ACC; dx itself for fp32, a bf16 tensor for DT = bf16).
+// dx and base may alias (pmu_maxpool2_bwd_bnr accumulates in place), so neither is __restrict__: each
+// element's store follows its own load in the same thread, and no other thread touches that element.
 // ST = false: the partial sums only (da not stored: maxpool2_bwd_bnbwd_kernel re-forms it)
 template <bool ACC, class DT = float, bool ST = true>
 __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const DT* __restrict__ dpool,
@@ -541,8 +543,8 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_bnr_kernel(const DT* __restr
                                                                const float* __restrict__ coef,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ invstd, int N, int H, int W,
-                                                               int C, int wpb, float* __restrict__ dx,
-                                                               float* __restrict__ part, const DT* __restrict__ base) {
+                                                               int C, int wpb, float* dx,
+                                                               float* __restrict__ part, const DT* base) {
   __shared__ float red[256 * 8];
   const int tid = threadIdx.x;
   const int CQ = C >> 2;

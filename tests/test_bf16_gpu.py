@@ -543,6 +543,12 @@ def _c5_step_vs_oracle(dev, N, say=print, odev="cpu"):
     res.update(grad_err=err, tol_grad=tol_g)
     lab, lab_ref = out.detach().argmax(1).cpu(), ref.argmax(1)
     res["argmax_agreement"] = float((lab == lab_ref).float().mean())
+    # by location: every flipped label lies where the fp64 oracle's top-2 margin is within twice the
+    # output tolerance (a flip elsewhere would need an output error above the contract)
+    top = ref.topk(2, dim=1).values
+    mg = top[:, 0] - top[:, 1]
+    res["max_margin_at_flip"] = float(mg[lab != lab_ref].max()) if bool((lab != lab_ref).any()) else 0.0
+    res["margin_bound"] = 2 * tol_out * float(ref.abs().max())
     dh, dr = trainer_dice(out.detach().cpu(), tgt, 3), trainer_dice(ref, tgt, 3)
     res["dice_gap"] = max(abs(a - b) for a, b in zip(dh, dr))
     say("C5_STEP " + str(res))
@@ -550,6 +556,7 @@ def _c5_step_vs_oracle(dev, N, say=print, odev="cpu"):
     assert res["loss_rel"] <= tol_loss, res
     assert err <= tol_g, (err, worst, tol_g)
     assert res["argmax_agreement"] >= 0.99, res
+    assert res["max_margin_at_flip"] <= res["margin_bound"], res
     assert res["dice_gap"] <= 1e-3, (dh, dr)
     for k, v in net.state_dict().items():
         if k.endswith("running_mean") or k.endswith("running_var"):

@@ -291,6 +291,63 @@ def test_bench_refuses_gpus_world_mismatch():
     assert "WORLD_SIZE=2" in r.stderr and r.stdout.strip() == ""
 
 
+def test_bench_roofline_by_kernel_family():
+    """bench.py groups the MFMA entries into kernel families before picking the dominant one (VERDICT r5
+    #3): c5's input gradient runs as three entries (_bnr_dxb, _x1b_sum_dxb, _dxb) whose summed time beats
+    the forward's, so the line names the input gradient, with the forward as the runner-up."""
+    import bench
+    per = {  # name: [launches, executed FLOPs, seconds, direct-sum FLOPs] (c5-like proportions)
+        "pmu_conv3x3_dgrad_dma_bnr_dxb": [9, 2.7e12, 3.4e-3, 2.7e12],
+        "pmu_conv3x3_dgrad_dma_x1b_sum_dxb": [4, 1.6e12, 2.1e-3, 1.6e12],
+        "pmu_conv3x3_dgrad_dma_dxb": [3, 0.8e12, 1.0e-3, 0.8e12],
+        "pmu_conv3x3_fwd_dma": [17, 5.9e12, 5.4e-3, 5.9e12],
+        "pmu_conv3x3_wgrad_bf16_dma": [17, 5.5e12, 4.7e-3, 5.5e12],
+        "pmu_frame_to_bf16": [30, 0.0, 2.8e-3, 0.0],   # not an MFMA entry: never a family
+    }
+    fams = bench.mfma_families(per)
+    assert [f[0] for f in fams] == ["pmu_conv3x3_dgrad_dma", "pmu_conv3x3_fwd_dma", "pmu_conv3x3_wgrad_bf16_dma"]
+    fam, d, members = fams[0]
+    assert members == sorted(["pmu_conv3x3_dgrad_dma_bnr_dxb", "pmu_conv3x3_dgrad_dma_x1b_sum_dxb",
+                              "pmu_conv3x3_dgrad_dma_dxb"])
+    assert d[0] == 16 and abs(d[2] - 6.5e-3) < 1e-12
+    roof = bench.roofline_entry("c5", *fams[0])
+    assert roof["kernel"] == "pmu_conv3x3_dgrad_dma" and roof["launches"] == 16
+    assert roof["peak"] == bench.BF16_MFMA_PEAK_TF
+    assert abs(roof["frac"] - 5.1e12 / 6.5e-3 / 1e12 / bench.BF16_MFMA_PEAK_TF) < 1e-4
+    # a Winograd family carries its direct-sum figure beside the executed-product utilisation
+    w = bench.roofline_entry("unet", "pmu_conv3x3_dgrad_wino4", [15, 1.0e12, 9.8e-3, 2.25e12],
+                             ["pmu_conv3x3_dgrad_wino4", "pmu_conv3x3_dgrad_wino4_bnr"])
+    assert w["peak"] == bench.FP32_MFMA_PEAK_TF and w["direct_sum_equiv_frac"] > w["frac"]
+
+
+def test_bench_refuses_bad_rank_layouts():
+    """Under RCCL every rank needs its own GPU: world > visible devices, or two ranks reporting the same
+    PCI identity, is refused (exit 2); gloo may rehearse N ranks on one device."""
+    import bench
+    assert bench.check_layout("nccl", 8, 8) is None
+    assert bench.check_layout(None, 1, 1) is None and bench.check_layout(None, 1, 0) is None
+    assert bench.check_layout("gloo", 2, 1) is None
+    assert "2 RCCL ranks but 1" in bench.check_layout("nccl", 2, 1)
+    assert bench.check_layout("nccl", 4, 0)
+    assert bench.check_devices("nccl", ["0000:05:00.0 a", "0000:15:00.0 b"]) is None
+    assert bench.check_devices("gloo", ["0000:05:00.0 a", "0000:05:00.0 a"]) is None
+    assert "share a GPU" in bench.check_devices("nccl", ["0000:05:00.0 a", "0000:05:00.0 a"])
+
+
+def test_bench_refuses_rccl_ranks_beyond_devices():
+    """End to end: a rank of a 2-rank RCCL run on a host with fewer GPUs exits 2 with the reason before
+    any process group is formed (here: no GPU at all), and prints no JSON line."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT="29599", PMU_DIST_BACKEND="nccl")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "RCCL ranks but" in r.stderr and r.stdout.strip() == ""
+
+
 def test_oracle_bf16_dx_rule_matches_engine(monkeypatch):
     """oracle/unet_ref.py models the HIP path's bf16 activation gradients (BF16_DX) by the same rule the
     engine uses to pick the *_dxb input gradients (engine.dxb_ok, through the library's

@@ -47,3 +47,24 @@ def test_bench_gpus_2_launches_two_ranks():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 64 and res["config"]["parallelism"] == "dp2"
     assert res["value"] > 0 and res["steps"] == 2
+    # the line records its topology: gloo, 2 ranks, each rank's GPU identity (both cuda:0 on this box)
+    d = res["dist"]
+    assert d["backend"] == "gloo" and d["world"] == 2 and len(d["devices"]) == 2, d
+
+
+@pytest.mark.gpu
+def test_bench_refuses_two_rccl_ranks_on_one_gpu():
+    """The same launch over RCCL on a box with one GPU: each rank exits 2 before forming a process group
+    (two RCCL ranks on one device would time one GPU as two), and no JSON line is printed."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    env = dict(os.environ, PMU_DIST_BACKEND="nccl")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--no-cpu-baseline", "--no-kernel-timing"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0, (r.stdout + r.stderr)[-4000:]
+    assert "RCCL ranks but 1 visible GPU" in r.stderr, r.stderr[-4000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

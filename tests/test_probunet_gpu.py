@@ -232,6 +232,10 @@ def test_probunet_c4_geometry_vs_oracle(dev):
     for s in range(S):
         yr = fcomb_forward(fsd, res["feat"], zs[s], 4)
         assert max_abs(ys[s], yr) <= ACT_TOL, s
+        # argmax label map bit-exact away from fp32 ties: flips only where the oracle's top-2 margin < 1e-5
+        top = yr.topk(2, dim=1).values
+        flip = ys[s].argmax(1).cpu() != yr.argmax(1)
+        assert not bool((flip & ((top[:, 0] - top[:, 1]) >= 1e-5)).any()), (s, int(flip.sum()))
         got = dice_from_counts(dice_counts(ys[s], segm.to(dev), 3)).cpu()[1:].tolist()
         want = trainer_dice(yr, segm, 3)
         assert max(abs(a - b) for a, b in zip(got, want)) <= 1e-3, (s, got, want)
