@@ -906,9 +906,14 @@ def main():
     roof = roof_next = kernels = mfma_busy = None
     if not args.no_kernel_timing:
         timer = KernelTimer()
+        # the instrumented step runs on one stream: events bracketing a launch on a stream that other
+        # streams' kernels overlap would time their work too (c4's concurrent parts, engine CFG.prob_streams)
+        from pmu_hip.engine import CFG
+        prev_streams, CFG.prob_streams = CFG.prob_streams, False
         L.set_call_observer(timer)
         step()
         L.set_call_observer(None)
+        CFG.prob_streams = prev_streams
         per = timer.summary()
         mf = {k: v for k, v in per.items() if k in KernelTimer.MFMA}
         fams = mfma_families(per)

@@ -175,7 +175,19 @@ class ProbabilisticUnet(nn.Module):
         self.unet_features = None
 
     def forward(self, patch, segm, training=True):
-        """Prior latent space and UNet features for ``patch``; the posterior too when training (:215-223)."""
+        """Prior latent space and UNet features for ``patch``; the posterior too when training (:215-223).
+        The three parts are independent: on the HIP path they run on concurrent streams
+        (pmu_hip.functions.run_concurrent; PMU_PROB_STREAMS=0 runs them in the reference's order)."""
+        from pmu_hip.engine import CFG
+        if CFG.prob_streams and isinstance(patch, torch.Tensor) and patch.is_cuda:
+            parts = [lambda: self.unet.forward(patch), lambda: self.prior.forward(patch)]
+            if training:
+                parts.append(lambda: self.posterior.forward(patch, segm))
+            res = _fns().run_concurrent(patch.device, parts)
+            self.unet_features, self.prior_latent_space = res[0], res[1]
+            if training:
+                self.posterior_latent_space = res[2]
+            return
         if training:
             self.posterior_latent_space = self.posterior.forward(patch, segm)
         self.prior_latent_space = self.prior.forward(patch)

@@ -797,7 +797,10 @@ class EngineConfig:
         directly (PoolSumDa; PMU_POOL_FUSE=0: stored in fp32 and streamed, the round-5 path);
     head_fuse: the head's input gradient (the last layer's da) is not stored: the head backward forms
         the last layer's BN-backward partials and the head's weight gradient, and that layer's dz (bf16 or
-        fp32) is made from dy directly (HeadDa; PMU_HEAD_FUSE=0: da stored, then streamed)."""
+        fp32) is made from dy directly (HeadDa; PMU_HEAD_FUSE=0: da stored, then streamed);
+    prob_streams: the Probabilistic U-Net's forward runs its UNet, prior and posterior on three HIP
+        streams (functions.run_concurrent; their backwards follow autograd's stream of the forward), so
+        the parts' tile-starved deep layers and small launches overlap (PMU_PROB_STREAMS=0: one stream)."""
     fp32_conv: str = "wino"
     wino2h: bool = True
     wino4: str = "dgrad"
@@ -807,6 +810,7 @@ class EngineConfig:
     wgrad_dma: bool = True
     pool_fuse: bool = True
     head_fuse: bool = True
+    prob_streams: bool = True
 
     @classmethod
     def from_env(cls):
@@ -815,7 +819,8 @@ class EngineConfig:
                    wgrad4=os.environ.get("PMU_WGRAD4", "0") == "1", dx_bf16=os.environ.get("PMU_DX_BF16", "1") != "0",
                    wgrad_dma=os.environ.get("PMU_WGRAD_DMA", "1") != "0",
                    pool_fuse=os.environ.get("PMU_POOL_FUSE", "1") != "0",
-                   head_fuse=os.environ.get("PMU_HEAD_FUSE", "1") != "0")
+                   head_fuse=os.environ.get("PMU_HEAD_FUSE", "1") != "0",
+                   prob_streams=os.environ.get("PMU_PROB_STREAMS", "1") != "0")
 
 
 CFG = EngineConfig.from_env()

@@ -140,6 +140,59 @@ def grad_sink_for(module, params) -> GradSink:
 
 
 # ----------------------------------------------------------------------------------------
+# independent network parts on concurrent HIP streams
+# ----------------------------------------------------------------------------------------
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(dev, i):
+    key = (dev.index, i)
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _record(obj, stream):
+    """Mark every tensor reachable from a part's result (tensors, distributions' loc/scale, tuples)
+    as used on ``stream``, so the caching allocator does not hand its memory back to the producing side
+    stream while ``stream`` may still read it."""
+    if isinstance(obj, torch.Tensor):
+        obj.record_stream(stream)
+    elif isinstance(obj, (tuple, list)):
+        for o in obj:
+            _record(o, stream)
+    elif hasattr(obj, "base_dist"):
+        _record(obj.base_dist, stream)
+    elif hasattr(obj, "loc") and hasattr(obj, "scale"):
+        _record((obj.loc, obj.scale), stream)
+
+
+def run_concurrent(dev, parts):
+    """Run independent network parts (callables) with part 0 on the current stream and part i on side
+    stream i, each side stream starting behind everything already queued on the current one; the current
+    stream then waits for all of them.  The HIP executors launch on torch's current stream
+    (pmu_hip._lib.stream), so a part's kernels — and, through autograd's stream semantics, its backward,
+    which runs on the stream of its forward — overlap the other parts'.  Used by the Probabilistic U-Net's
+    forward for its UNet, prior and posterior (PMU/model/probabilistic_unet/probabilistic_unet.py:215-223),
+    whose deep 32^2 / 16^2 layers alone do not fill the chip.  Returns the parts' results in order."""
+    main = torch.cuda.current_stream(dev)
+    res = [None] * len(parts)
+    sides = []
+    for i in range(1, len(parts)):
+        s = _side_stream(dev, i)
+        s.wait_stream(main)
+        with torch.cuda.stream(s):
+            res[i] = parts[i]()
+        sides.append((i, s))
+    res[0] = parts[0]()
+    for i, s in sides:
+        main.wait_stream(s)
+        _record(res[i], main)
+    return res
+
+
+# ----------------------------------------------------------------------------------------
 # U-Net
 # ----------------------------------------------------------------------------------------
 def use_bf16(net) -> bool:

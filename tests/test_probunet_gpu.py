@@ -311,3 +311,48 @@ def test_fcomb_applied_twice_in_one_graph(dev):
     named = dict(fc.named_parameters())
     err, key = grad_err({k: named[k].grad for k in sd}, {k: sd[k].grad for k in sd})
     assert err <= GRAD_TOL, (err, key)
+
+
+def test_probunet_concurrent_streams_bit_identical(dev):
+    """ProbabilisticUnet.forward runs the UNet, prior and posterior on three HIP streams (engine CFG
+    .prob_streams, functions.run_concurrent), their backwards on the same streams: 3 training steps
+    (forward, injected posterior sample, -elbo, backward, clip+SGD, then the 16-sample sweep) at the c4
+    filters, 256x256, batch 8, give bit-identical losses, parameters, BN statistics and samples with the
+    streams on and off — the parts are independent and every kernel's summation order is fixed."""
+    from pmu_hip import engine
+    from pmu_hip.optim import FusedSGD
+    g = torch.Generator().manual_seed(3)
+    N, S = 8, 256
+    x = torch.rand(N, 1, S, S, generator=g).to(dev)
+    segm = torch.randint(0, 3, (N, 1, S, S), generator=g).float().to(dev)
+    eps = [torch.randn(N, 6, generator=g).to(dev) for _ in range(3)]
+    eps_prior = torch.randn(16, N, 6, generator=g).to(dev)
+    runs = []
+    prev = engine.CFG.prob_streams
+    try:
+        for on in (False, True):
+            engine.CFG.prob_streams = on
+            net = _net(dev, num_filters=(64, 128, 256, 512, 1024)).train()
+            opt = FusedSGD(net.parameters(), lr=1e-3, momentum=0.9, clip=0.1)
+            losses = []
+            for k in range(3):
+                opt.zero_grad()
+                net.forward(x, segm, training=True)
+                _inject(net.posterior_latent_space, eps[k], "rsample")
+                loss = -net.elbo(segm)
+                loss.backward()
+                opt.step()
+                losses.append(float(loss))
+            d = net.prior_latent_space
+            d.sample = lambda shape=torch.Size(): d.base_dist.loc + d.base_dist.scale * eps_prior
+            with torch.no_grad():
+                ys = net.sample_many(16)
+            torch.cuda.synchronize()
+            runs.append((losses, {k: v.detach().clone() for k, v in net.state_dict().items()}, ys.clone()))
+    finally:
+        engine.CFG.prob_streams = prev
+    (l0, sd0, y0), (l1, sd1, y1) = runs
+    assert l0 == l1, (l0, l1)
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+    assert torch.equal(y0, y1)

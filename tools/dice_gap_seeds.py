@@ -45,7 +45,8 @@ def margin(out):
 
 def oracle_run(sd0, x, t, device, dtype, autocast=False):
     import oracle.unet_ref as U
-    sd = {k: (v.to(device, dtype) if v.is_floating_point() else v.to(device)) for k, v in sd0.items()}
+    # (a copy: the oracle's BatchNorm updates the running statistics in place)
+    sd = {k: (v.to(device, dtype) if v.is_floating_point() else v.to(device)).clone() for k, v in sd0.items()}
     bufs = {k: torch.zeros_like(sd[k]) for k in U.unet_param_keys(sd)}
     xo, to = x.to(device, dtype), t.to(device)
     prev = U.AUTOCAST_ALL
