@@ -57,6 +57,10 @@ BF16_DX = True
 # the reference's trajectory (tools/dice_gap_seeds.py) and how far the HIP path's fp32 exceptions (the
 # first layer, input gradients of maps < 32 wide, ConvT shapes off the LDS-DMA kernel) sit from it.
 AUTOCAST_ALL = False
+# Which halves of the bf16 arithmetic Bf16Conv3x3 / Bf16ConvT2x2 apply (attribution experiments,
+# tools/dice_gap_seeds.py): "fwd" rounds the forward's operand and weights, "bwd" the backward's dy,
+# weights, saved operand and dx.  Both by default (the autocast / HIP arithmetic).
+ROUND_PARTS = ("fwd", "bwd")
 
 
 def _dma_dxb(x, cin, cout, split):
@@ -82,15 +86,18 @@ class Bf16Conv3x3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, round_dx=False):
         xr, wr = _rb(x), _rb(w)
-        ctx.save_for_backward(xr, wr)
+        ctx.save_for_backward(xr if "bwd" in ROUND_PARTS else x, wr if "bwd" in ROUND_PARTS else w)
         ctx.has_b = b is not None
-        ctx.round_dx = round_dx
+        ctx.round_dx = round_dx and "bwd" in ROUND_PARTS
+        ctx.rdy = "bwd" in ROUND_PARTS
+        if "fwd" not in ROUND_PARTS:
+            return F.conv2d(x, w, b, padding=1)
         return F.conv2d(xr, wr, b, padding=1)
 
     @staticmethod
     def backward(ctx, dy):
         xr, wr = ctx.saved_tensors
-        dyr = _rb(dy)
+        dyr = _rb(dy) if ctx.rdy else dy
         dx = torch.nn.grad.conv2d_input(xr.shape, wr, dyr, padding=1)
         if ctx.round_dx:
             dx = _rb(dx)
@@ -108,7 +115,9 @@ class Bf16ConvT2x2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, fwd, dgrad, round_dx=False):
         ctx.save_for_backward(x, w)
-        ctx.dgrad, ctx.has_b, ctx.round_dx = dgrad, b is not None, round_dx
+        bwd = "bwd" in ROUND_PARTS
+        ctx.dgrad, ctx.has_b, ctx.round_dx, ctx.rw = dgrad and bwd, b is not None, round_dx and bwd, bwd
+        fwd = fwd and "fwd" in ROUND_PARTS
         return F.conv_transpose2d(_rb(x) if fwd else x, _rb(w) if fwd else w, b, stride=2)
 
     @staticmethod
@@ -118,7 +127,8 @@ class Bf16ConvT2x2(torch.autograd.Function):
         if ctx.round_dx:   # BF16_DX: pmu_convT2x2_dgrad_dma_dxb stores dx in bf16
             dx = _rb(dx)
         n, k = dy.shape[0], dy.shape[1]
-        dw = torch.einsum("ncij,nkiajb->ckab", _rb(x), _rb(dy).reshape(n, k, x.shape[2], 2, x.shape[3], 2))
+        rb = _rb if ctx.rw else (lambda t: t)
+        dw = torch.einsum("ncij,nkiajb->ckab", rb(x), rb(dy).reshape(n, k, x.shape[2], 2, x.shape[3], 2))
         db = dy.sum((0, 2, 3)) if ctx.has_b else None
         return dx, dw, db, None, None, None
 

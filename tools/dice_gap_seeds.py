@@ -10,6 +10,9 @@ config c5's UNet(3, 3, [64..1024]) trained 12 identical steps (CE + clip + SGD, 
   oac      the oracle under torch.autocast(bfloat16)'s own semantics (oracle.unet_ref.AUTOCAST_ALL: every
            conv's operands, weights, dy and dx rounded to bf16), fp32 sums on the GPU — what autocast does to
            the reference itself;
+  oacf     oac with the forward rounding only (operands and weights), oacb with the backward's only;
+  tac      the oracle's fp32 code under torch.autocast(bfloat16) itself, on the GPU (PyTorch's bf16
+           convolutions: bf16 conv outputs, BN in fp32), the reference as autocast would run it;
   hip32    the HIP path in fp32;
   hip16    the HIP path under torch.autocast(bfloat16) (the shipped c5 arithmetic);
   hip16dx  the same with fp32 activation gradients (engine CFG.dx_bf16 off, oracle BF16_DX off).
@@ -43,16 +46,21 @@ def margin(out):
     return v[:, 0] - v[:, 1]
 
 
-def oracle_run(sd0, x, t, device, dtype, autocast=False):
+def oracle_run(sd0, x, t, device, dtype, autocast=False, parts=("fwd", "bwd"), torch_autocast=False):
+    """12 oracle steps from sd0, then the eval / train outputs.  autocast: the oracle's restatement of
+    torch.autocast(bfloat16) (AUTOCAST_ALL; ``parts`` picks the forward and / or backward rounding);
+    torch_autocast: the oracle's fp32 code run under torch.autocast itself on the GPU (PyTorch's own bf16
+    convolutions, cudnn off: im2col + rocBLAS)."""
     import oracle.unet_ref as U
     # (a copy: the oracle's BatchNorm updates the running statistics in place)
     sd = {k: (v.to(device, dtype) if v.is_floating_point() else v.to(device)).clone() for k, v in sd0.items()}
     bufs = {k: torch.zeros_like(sd[k]) for k in U.unet_param_keys(sd)}
     xo, to = x.to(device, dtype), t.to(device)
-    prev = U.AUTOCAST_ALL
-    U.AUTOCAST_ALL = autocast
+    prev = U.AUTOCAST_ALL, U.ROUND_PARTS
+    U.AUTOCAST_ALL, U.ROUND_PARTS = autocast, tuple(parts)
     try:
-        with torch.backends.cudnn.flags(enabled=False):
+        with torch.backends.cudnn.flags(enabled=False), \
+                torch.autocast("cuda", dtype=torch.bfloat16, enabled=torch_autocast):
             for _ in range(STEPS):
                 U.unet_train_step(sd, xo, to, len(FILTERS), 3, lr=LR, bufs=bufs, bf16=autocast)
             outs = {}
@@ -61,7 +69,7 @@ def oracle_run(sd0, x, t, device, dtype, autocast=False):
                     outs[m] = U.unet_forward({k: v.clone() for k, v in sd.items()}, xo, len(FILTERS), 3,
                                              training=m == "train", bf16=autocast).float().cpu()
     finally:
-        U.AUTOCAST_ALL = prev
+        U.AUTOCAST_ALL, U.ROUND_PARTS = prev
     return outs
 
 
@@ -140,6 +148,9 @@ def main():
         runs = {"o32gpu": lambda: oracle_run(sd0, x, t, dev, torch.float32),
                 "o64": lambda: oracle_run(sd0, x, t, dev, torch.float64),
                 "oac": lambda: oracle_run(sd0, x, t, dev, torch.float32, autocast=True),
+                "oacf": lambda: oracle_run(sd0, x, t, dev, torch.float32, autocast=True, parts=("fwd",)),
+                "oacb": lambda: oracle_run(sd0, x, t, dev, torch.float32, autocast=True, parts=("bwd",)),
+                "tac": lambda: oracle_run(sd0, x, t, dev, torch.float32, torch_autocast=True),
                 "hip32": lambda: hip_run(sd0, x, y, dev, False),
                 "hip16": lambda: hip_run(sd0, x, y, dev, True),
                 "hip16dx": lambda: hip_run(sd0, x, y, dev, True, dx_bf16=False)}
