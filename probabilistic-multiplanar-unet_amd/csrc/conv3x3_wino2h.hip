@@ -26,7 +26,9 @@ constexpr int OW = 2 * TX, OH = 2 * TY;       // 16 x 16 output pixels
 constexpr int HW = OW + 2, HH = OH + 2;       // 18 x 18 halo
 constexpr int BK = 8;                         // input channels per chunk
 constexpr int GP = 20;                        // floats per group of 2 halo pixels (2 x 8 ch + 1 pad unit)
-constexpr int ROWF = 184;                     // floats per halo row (9 groups = 180, padded)
+constexpr int ROWF = 208;                     // floats per halo row (9 groups = 180, padded to 16 mod 32:
+                                              // the wave's two tile rows 2 ROWF = 32 mod 64 floats apart,
+                                              // conflict-free ds_read_b64 patch pairs, see w2_pair)
 constexpr int ROWU = ROWF / 4;
 constexpr int A_FLOATS = HH * ROWF;
 [[maybe_unused]] constexpr int NC = 16;       // Winograd components
@@ -167,6 +169,12 @@ __global__ __launch_bounds__(256) void pack_wino2h_multi_kernel(const pmu_pack_j
 }
 
 template <int OFF>
+__device__ __forceinline__ float2 lds_b64(unsigned addr) {
+  float2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int OFF>
 __device__ __forceinline__ float lds_b32(unsigned addr) {
   float v;
   asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
@@ -246,6 +254,98 @@ __device__ __forceinline__ void w2_step(unsigned pa, unsigned ua, f32x4 (&acc)[2
   acc[0][7] = mfma16(v[7], u01.w, acc[0][7]);
   acc[1][7] = mfma16(v[7], u11.w, acc[1][7]);
   __builtin_amdgcn_sched_barrier(0);
+}
+
+// half CH of B^T d B from the column-pass halves t[a][j] (a = 0, 1): v[4a + b]
+__device__ __forceinline__ void w2_rows(const float (&t)[2][4], float (&v)[8]) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    v[4 * a + 0] = t[a][0] - t[a][2];
+    v[4 * a + 1] = t[a][1] + t[a][2];
+    v[4 * a + 2] = t[a][2] - t[a][1];
+    v[4 * a + 3] = t[a][1] - t[a][3];
+  }
+}
+
+// 16 MFMAs of one step on v with U groups (u00, u10) and (u01, u11); the second group waited for here
+// (W: lgkmcnt allowing the reads issued after it)
+template <int W>
+__device__ __forceinline__ void w2_mfma(const float (&v)[8], float4 u00, float4 u10, float4 u01, float4 u11,
+                                        f32x4 (&acc)[2][8]) {
+  acc[0][0] = mfma16(v[0], u00.x, acc[0][0]);
+  acc[1][0] = mfma16(v[0], u10.x, acc[1][0]);
+  acc[0][1] = mfma16(v[1], u00.y, acc[0][1]);
+  acc[1][1] = mfma16(v[1], u10.y, acc[1][1]);
+  acc[0][2] = mfma16(v[2], u00.z, acc[0][2]);
+  acc[1][2] = mfma16(v[2], u10.z, acc[1][2]);
+  acc[0][3] = mfma16(v[3], u00.w, acc[0][3]);
+  acc[1][3] = mfma16(v[3], u10.w, acc[1][3]);
+  __builtin_amdgcn_sched_barrier(0);
+  wait_lgkm<W>();
+  __builtin_amdgcn_sched_barrier(0);
+  acc[0][4] = mfma16(v[4], u01.x, acc[0][4]);
+  acc[1][4] = mfma16(v[4], u11.x, acc[1][4]);
+  acc[0][5] = mfma16(v[5], u01.y, acc[0][5]);
+  acc[1][5] = mfma16(v[5], u11.y, acc[1][5]);
+  acc[0][6] = mfma16(v[6], u01.z, acc[0][6]);
+  acc[1][6] = mfma16(v[6], u11.z, acc[1][6]);
+  acc[0][7] = mfma16(v[7], u01.w, acc[0][7]);
+  acc[1][7] = mfma16(v[7], u11.w, acc[1][7]);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Both MFMA steps of a chunk (channels 2kk, 2kk + 1 of k-slot kk) with the patch read as ds_read_b64
+// channel pairs, and only the three patch rows this component half uses (rows CH .. CH + 2): 12 b64 reads
+// per chunk instead of 2 x 16 b32.  Bank map of a 32-lane group (b64: dword banks mod 64): tile columns
+// GP = 20 floats apart, the wave's two tile rows 2 ROWF = 32 (mod 64) apart, the k-slot pair 2 floats:
+// the 16 tiles x 2 k-slots cover the 64 banks once (the b32 reads of one channel were 2-way: tile rows
+// 368 = 16 (mod 32) apart put both rows of tiles on the same 8 bank quads).
+template <int CH, int CO>
+__device__ __forceinline__ void w2_pair(unsigned pa, unsigned ua, f32x4 (&acc)[2][8]) {
+  float2 c[3][4];
+#define PMU_RD2(I, J) c[I][J] = lds_b64<PMU_W2P(CH + (I), J)>(pa);
+  PMU_RD2(0, 0) PMU_RD2(0, 1) PMU_RD2(0, 2) PMU_RD2(0, 3) PMU_RD2(1, 0) PMU_RD2(1, 1) PMU_RD2(1, 2) PMU_RD2(1, 3)
+  PMU_RD2(2, 0) PMU_RD2(2, 1) PMU_RD2(2, 2) PMU_RD2(2, 3)
+#undef PMU_RD2
+  wait_lgkm<0>();  // the patch
+  __builtin_amdgcn_sched_barrier(0);
+  // column pass (rows CH .. CH+2 of d as c[0..2]): CH 0: (d0 - d2, d1 + d2); CH 1: (d2 - d1, d1 - d3)
+  float t0[2][4], t1[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (CH == 0) {
+      t0[0][j] = c[0][j].x - c[2][j].x;
+      t0[1][j] = c[1][j].x + c[2][j].x;
+      t1[0][j] = c[0][j].y - c[2][j].y;
+      t1[1][j] = c[1][j].y + c[2][j].y;
+    } else {
+      t0[0][j] = c[1][j].x - c[0][j].x;
+      t0[1][j] = c[0][j].x - c[2][j].x;
+      t1[0][j] = c[1][j].y - c[0][j].y;
+      t1[1][j] = c[0][j].y - c[2][j].y;
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // U after the patch is consumed (at the 128-register cap of four waves per SIMD the patch pairs and U
+  // together spilled; the SIMD's other waves cover the U read latency)
+  float4 u00 = lds_b128<(8 * CH) * 4>(ua);
+  float4 u10 = lds_b128<(16 * NCP + 8 * CH) * 4>(ua);
+  float4 u01 = lds_b128<(8 * CH + 4) * 4>(ua);
+  float4 u11 = lds_b128<(16 * NCP + 8 * CH + 4) * 4>(ua);
+  float v[8];
+  w2_rows(t0, v);
+  wait_lgkm<2>();  // U group 0
+  __builtin_amdgcn_sched_barrier(0);
+  w2_mfma<0>(v, u00, u10, u01, u11, acc);
+  const unsigned ua1 = ua + CO * NCP * 4;
+  u00 = lds_b128<(8 * CH) * 4>(ua1);
+  u10 = lds_b128<(16 * NCP + 8 * CH) * 4>(ua1);
+  u01 = lds_b128<(8 * CH + 4) * 4>(ua1);
+  u11 = lds_b128<(16 * NCP + 8 * CH + 4) * 4>(ua1);
+  w2_rows(t1, v);
+  wait_lgkm<2>();  // step 1's U group 0
+  __builtin_amdgcn_sched_barrier(0);
+  w2_mfma<0>(v, u00, u10, u01, u11, acc);
 }
 
 // this half's share of Y = A^T M A (A^T = [1 1 1 0; 0 1 -1 -1]) for tile r of co half h:
@@ -395,7 +495,7 @@ struct W2Block {
   unsigned gin, gzero;
 };
 
-template <bool DGRAD, bool BNR, int CH, int CO_>
+template <bool DGRAD, bool BNR, int CH, int CO_, bool P64>
 __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, const unsigned (&goff)[W2Cfg<CO_>::NGL],
                                             float* smem) {
   using C = W2Cfg<CO_>;
@@ -449,8 +549,12 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
       float* cur = smem + (gi & 1) * STAGE;
       if (gi + 1 < total) PMU_FETCH2(gi + 1, smem + ((gi + 1) & 1) * STAGE)
       const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
-      w2_step<CH>(pa, ua, acc);                          // channel 2*kk
-      w2_step<CH>(pa + 4, ua + CO * NCP * 4, acc);       // channel 2*kk + 1
+      if constexpr (P64) {
+        w2_pair<CH, CO>(pa, ua, acc);                    // channels 2*kk, 2*kk + 1
+      } else {
+        w2_step<CH>(pa, ua, acc);                        // channel 2*kk
+        w2_step<CH>(pa + 4, ua + CO * NCP * 4, acc);     // channel 2*kk + 1
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
       __syncthreads();
     }
@@ -475,7 +579,7 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
 
 // BNR (input gradient only): the producer's BN-backward partial sums in the epilogue (a.bz set) — a
 // compile-time choice, so the z loads and their uses sit in straight-line code
-template <bool DGRAD, bool BNR, int CO_>
+template <bool DGRAD, bool BNR, int CO_, bool P64 = true>
 // 64 channels: 1024 threads = four waves per SIMD (<= 128 VGPRs implied); 32 channels: 512 threads,
 // capped at 128 VGPRs (four waves per SIMD) so two workgroups share a CU (at 132 VGPRs only one fit)
 __global__ __launch_bounds__(16 * CO_, CO_ == 32 ? 4 : 1) void conv3x3_wino2h_kernel(W2Args a) {
@@ -520,8 +624,8 @@ __global__ __launch_bounds__(16 * CO_, CO_ == 32 ? 4 : 1) void conv3x3_wino2h_ke
   }
   B.gin = gin;
   B.gzero = gzero;
-  if ((tid >> 8) & 1) wino2h_main<DGRAD, BNR, 1, CO_>(a, B, goff, smem);
-  else wino2h_main<DGRAD, BNR, 0, CO_>(a, B, goff, smem);
+  if ((tid >> 8) & 1) wino2h_main<DGRAD, BNR, 1, CO_, P64>(a, B, goff, smem);
+  else wino2h_main<DGRAD, BNR, 0, CO_, P64>(a, B, goff, smem);
 }
 
 // output channels per block (PMU_WINO2H_CO=32: 512-thread blocks, two per CU; A/B)
@@ -580,9 +684,23 @@ int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, 
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks);
   const bool bnr = dgrad && bz;
-  if (CO == 32 && bnr) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, true, 32>), grid, dim3(512), 0, st, a);
-  else if (CO == 32 && dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, false, 32>), grid, dim3(512), 0, st, a);
-  else if (CO == 32) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 32>), grid, dim3(512), 0, st, a);
+#ifdef PMU_EXPERIMENTS
+  // PMU_WINO2H_B32=1 (A/B): the patch read per channel as ds_read_b32 (w2_step), the round-5 kernel
+  static const int b32 = [] {
+    const char* e = pmu_variant_env("PMU_WINO2H_B32");
+    return e ? atoi(e) : 0;
+  }();
+  if (b32 && CO == 64) {
+    if (bnr) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, true, 64, false>), grid, dim3(1024), 0, st, a);
+    else if (dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, false, 64, false>), grid, dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, false>), grid, dim3(1024), 0, st, a);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
+#endif
+  if (CO == 32 && bnr) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, true, 32, false>), grid, dim3(512), 0, st, a);
+  else if (CO == 32 && dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, false, 32, false>), grid, dim3(512), 0, st, a);
+  else if (CO == 32) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 32, false>), grid, dim3(512), 0, st, a);
   else if (bnr) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, true, 64>), grid, dim3(1024), 0, st, a);
   else if (dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, false, 64>), grid, dim3(1024), 0, st, a);
   else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64>), grid, dim3(1024), 0, st, a);

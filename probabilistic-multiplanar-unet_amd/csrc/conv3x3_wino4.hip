@@ -332,6 +332,121 @@ __device__ __forceinline__ void w4_chunk(unsigned pa, unsigned ua, f32x4 (&acc)[
   w4_group<CH, 4, false>(ua1, v, ur, ut, acc, pa1, d);
 }
 
+// column j of the half-CH column pass of B^T d B (input_transform_half's first loop) for one channel
+template <int CH>
+__device__ __forceinline__ void w4_col_half(float d0, float d1, float d2, float d3, float d4, float d5, float& r0,
+                                            float& r1, float& r2) {
+  if (CH == 0) {
+    r0 = fmaf(-5.f, d2, fmaf(4.f, d0, d4));
+    const float a = fmaf(-4.f, d2, d4), b = fmaf(-4.f, d1, d3);
+    r1 = a + b;
+    r2 = a - b;
+  } else {
+    const float c = d4 - d2, e = d3 - d1;
+    r0 = fmaf(2.f, e, c);
+    r1 = fmaf(-2.f, e, c);
+    r2 = fmaf(-5.f, d3, fmaf(4.f, d1, d5));
+  }
+}
+// column J of this lane's 6x6 patch for both channels of its k-slot (2kk, 2kk + 1) as ds_read_b64: the
+// five rows half CH uses (0-4 for CH 0, 1-5 for CH 1) — an asm read whose result is never used would let
+// the compiler hand its register to a live value that the late LDS return then overwrites
+template <int CH, int J>
+__device__ __forceinline__ void w4_col_read(unsigned pa, float2 (&c)[5]) {
+  c[0] = lds_b64<PatchOff<6 * CH + J>::value>(pa);
+  c[1] = lds_b64<PatchOff<6 * CH + 6 + J>::value>(pa);
+  c[2] = lds_b64<PatchOff<6 * CH + 12 + J>::value>(pa);
+  c[3] = lds_b64<PatchOff<6 * CH + 18 + J>::value>(pa);
+  c[4] = lds_b64<PatchOff<6 * CH + 24 + J>::value>(pa);
+}
+template <int CH, int J>
+__device__ __forceinline__ void w4_col_tf(const float2 (&c)[5], float (&t0)[18], float (&t1)[18]) {
+  if (CH == 0) {  // rows 0-4 (w4_col_half<0> does not read d5)
+    w4_col_half<0>(c[0].x, c[1].x, c[2].x, c[3].x, c[4].x, 0.f, t0[J], t0[6 + J], t0[12 + J]);
+    w4_col_half<0>(c[0].y, c[1].y, c[2].y, c[3].y, c[4].y, 0.f, t1[J], t1[6 + J], t1[12 + J]);
+  } else {        // rows 1-5 (w4_col_half<1> does not read d0)
+    w4_col_half<1>(0.f, c[0].x, c[1].x, c[2].x, c[3].x, c[4].x, t0[J], t0[6 + J], t0[12 + J]);
+    w4_col_half<1>(0.f, c[0].y, c[1].y, c[2].y, c[3].y, c[4].y, t1[J], t1[6 + J], t1[12 + J]);
+  }
+}
+template <int CH>
+__device__ __forceinline__ void w4_row_pass(const float (&t)[18], float (&v)[18]) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    bt6(t[6 * a], t[6 * a + 1], t[6 * a + 2], t[6 * a + 3], t[6 * a + 4], t[6 * a + 5], v[6 * a], v[6 * a + 1],
+        v[6 * a + 2], v[6 * a + 3], v[6 * a + 4], v[6 * a + 5]);
+}
+
+// One chunk with the patch read as ds_read_b64 channel pairs: both steps' patches (channels 2kk, 2kk + 1)
+// arrive together, 30 b64 reads (the 5 x 6 elements this half uses) instead of 72 b32.  In a 32-lane group the 16 tiles x 2 k-slots cover
+// all 64 banks once (tile columns 36 floats apart, tile rows 4 x 312 = 32 mod 64 floats, k-slots 2
+// floats): conflict-free, where the b32 reads of one channel are 2-way (16 tiles x 2 channels on 32
+// banks of 4-float DMA units).  The patch streams column by column through two 6-read register sets; each
+// column's half column-pass runs for both channels as it lands, so the live state is the two channels'
+// column-pass halves (t0, t1: 36 floats, as d[36] before), not 72 patch values.
+template <int CH>
+__device__ __forceinline__ void w4_chunk64(unsigned pa, unsigned ua, f32x4 (&acc)[2][18]) {
+  float t0[18], t1[18], v[18];
+  float2 cA[5], cB[5];
+  float4 ur[3][2];
+  float2 ut[2];
+  w4_col_read<CH, 0>(pa, cA);
+  w4_col_read<CH, 1>(pa, cB);
+  wait_lgkm<5>();  // column 0 (reads complete in order)
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_tf<CH, 0>(cA, t0, t1);
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_read<CH, 2>(pa, cA);
+  wait_lgkm<5>();
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_tf<CH, 1>(cB, t0, t1);
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_read<CH, 3>(pa, cB);
+  wait_lgkm<5>();
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_tf<CH, 2>(cA, t0, t1);
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_read<CH, 4>(pa, cA);
+  wait_lgkm<5>();
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_tf<CH, 3>(cB, t0, t1);
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_read<CH, 5>(pa, cB);
+  // step 0's U groups 0-2 behind the last column (their registers are free until here)
+  w4_uread<CH, 0>(ua, ur, ut);
+  w4_uread<CH, 1>(ua, ur, ut);
+  w4_uread<CH, 2>(ua, ur, ut);
+  wait_lgkm<11>();  // column 4
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_tf<CH, 4>(cA, t0, t1);
+  __builtin_amdgcn_sched_barrier(0);
+  wait_lgkm<6>();   // column 5
+  __builtin_amdgcn_sched_barrier(0);
+  w4_col_tf<CH, 5>(cB, t0, t1);
+  w4_row_pass<CH>(t0, v);
+  __builtin_amdgcn_sched_barrier(0);
+  wait_lgkm<4>();   // U group 0
+  __builtin_amdgcn_sched_barrier(0);
+  float dn[36];   // (unused: no patch prefetch in this form)
+  w4_group<CH, 0, false>(ua, v, ur, ut, acc, 0u, dn);
+  w4_group<CH, 1, false>(ua, v, ur, ut, acc, 0u, dn);
+  w4_group<CH, 2, false>(ua, v, ur, ut, acc, 0u, dn);
+  w4_group<CH, 3, false>(ua, v, ur, ut, acc, 0u, dn);
+  w4_group<CH, 4, false>(ua, v, ur, ut, acc, 0u, dn);
+  const unsigned ua1 = ua + CO * NC * 4;
+  w4_uread<CH, 0>(ua1, ur, ut);
+  w4_uread<CH, 1>(ua1, ur, ut);
+  w4_uread<CH, 2>(ua1, ur, ut);
+  w4_row_pass<CH>(t1, v);
+  wait_lgkm<4>();  // step 1's U group 0
+  __builtin_amdgcn_sched_barrier(0);
+  w4_group<CH, 0, false>(ua1, v, ur, ut, acc, 0u, dn);
+  w4_group<CH, 1, false>(ua1, v, ur, ut, acc, 0u, dn);
+  w4_group<CH, 2, false>(ua1, v, ur, ut, acc, 0u, dn);
+  w4_group<CH, 3, false>(ua1, v, ur, ut, acc, 0u, dn);
+  w4_group<CH, 4, false>(ua1, v, ur, ut, acc, 0u, dn);
+}
+
 // this half's share of Y = A^T M A for tile r of co half h: P[4p + q] = sum over the half's rows a of
 // A^T[p][a] (M[a][:] A)[q]
 template <int CH>
@@ -486,8 +601,9 @@ struct W4Block {
   unsigned gzero;  // image units outside it (zero, written once; restored after an exchange in their stage)
 };
 
-// the pass / chunk pipeline of a wave of component half CH (waves 4 CH .. 4 CH + 3)
-template <bool DGRAD, bool BNR, int CH, bool PF>
+// the pass / chunk pipeline of a wave of component half CH (waves 4 CH .. 4 CH + 3); PM: the patch read —
+// 0 b32 per channel, 1 b32 with step 1's patch read under step 0's MFMAs, 2 b64 channel pairs (default)
+template <bool DGRAD, bool BNR, int CH, int PM>
 __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, const unsigned (&goff)[NGL],
                                            float* smem) {
   float* red = smem + 2 * STAGE;
@@ -542,7 +658,8 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
       float* cur = smem + (gi & 1) * STAGE;
       if (gi + 1 < total) PMU_FETCH4(gi + 1, smem + ((gi + 1) & 1) * STAGE)
       const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
-      w4_chunk<CH, PF>(pa, ua, acc);
+      if constexpr (PM == 2) w4_chunk64<CH>(pa, ua, acc);
+      else w4_chunk<CH, PM == 1>(pa, ua, acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
       __syncthreads();
     }
@@ -575,7 +692,7 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
 // rest, each for its tile group's 16 tiles x all 32 output channels.
 // BNR (input gradient only): the producer's BN-backward partial sums in the epilogue (a.bz set) — a
 // compile-time choice, so the z loads and their uses sit in straight-line code
-template <bool DGRAD, bool BNR, bool PF>
+template <bool DGRAD, bool BNR, int PM>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
   const int tid = threadIdx.x;
@@ -632,8 +749,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   B.gin = gin;
   B.gzero = gzero;
   if (a.prio && (tid >> 8)) __builtin_amdgcn_s_setprio(1);
-  if (tid >> 8) wino4_main<DGRAD, BNR, 1, PF>(a, B, goff, smem);
-  else wino4_main<DGRAD, BNR, 0, PF>(a, B, goff, smem);
+  if (tid >> 8) wino4_main<DGRAD, BNR, 1, PM>(a, B, goff, smem);
+  else wino4_main<DGRAD, BNR, 0, PM>(a, B, goff, smem);
 }
 
 int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
@@ -679,10 +796,16 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
     while (cpb * 2 <= a.nco && spatial * pmu_cdiv(a.nco, cpb * 2) >= min_wg) cpb *= 2;
   }
   a.cpb = cpb;
+  // patch read (A/B, experiments build): PMU_WINO4_PF=1 b32 with prefetch, PMU_WINO4_B32=1 b32; default b64 pairs
   static const int pf = [] {
     const char* e = pmu_variant_env("PMU_WINO4_PF");
     return e ? atoi(e) : 0;
   }();
+  static const int b32 = [] {
+    const char* e = pmu_variant_env("PMU_WINO4_B32");
+    return e ? atoi(e) : 0;
+  }();
+  const int pm = pf ? 1 : b32 ? 0 : 2;
   static const int prio = [] {  // PMU_WINO4_PRIO=1: waves of component half 1 at s_setprio 1 (A/B)
     const char* e = pmu_variant_env("PMU_WINO4_PRIO");
     return e ? atoi(e) : 0;
@@ -704,13 +827,19 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
   PMU_REQUIRE(blocks < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks);
-  if (dgrad && bz) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, false>), grid, dim3(NT), 0, st, a);
-  else if (dgrad && pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, true>), grid, dim3(NT), 0, st, a);
-  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, false>), grid, dim3(NT), 0, st, a);
 #ifdef PMU_EXPERIMENTS
-  else if (pf) hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, true>), grid, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, false>), grid, dim3(NT), 0, st, a);
+  if (dgrad && bz && pm == 0) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, 0>), grid, dim3(NT), 0, st, a);
+  else if (dgrad && bz) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, 2>), grid, dim3(NT), 0, st, a);
+  else if (dgrad && pm == 1) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, 1>), grid, dim3(NT), 0, st, a);
+  else if (dgrad && pm == 0) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, 0>), grid, dim3(NT), 0, st, a);
+  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, 2>), grid, dim3(NT), 0, st, a);
+  else if (pm == 1) hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, 1>), grid, dim3(NT), 0, st, a);
+  else if (pm == 0) hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, 0>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv3x3_wino4_kernel<false, false, 2>), grid, dim3(NT), 0, st, a);
 #else
+  (void)pm;
+  if (dgrad && bz) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, 2>), grid, dim3(NT), 0, st, a);
+  else if (dgrad) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, 2>), grid, dim3(NT), 0, st, a);
   else return PMU_ERR_ARG;  // the F(4x4) forward is an experiments-build kernel (see pmu_conv3x3_fwd_wino4)
 #endif
   PMU_CHECK_LAUNCH();

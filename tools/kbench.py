@@ -134,6 +134,7 @@ def main():
         bnr4 = bnr(L.lib().pmu_conv3x3_tiles_wino4(N, H, W))
         bnr2 = bnr(L.lib().pmu_conv3x3_tiles_wino2h(N, H, W))
         bnrd = bnr(L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, cpo))
+        dxb = torch.empty(N, H, W, Cin, dtype=torch.int16, device=dev)
         ops = {
             "dgrad_w4b": lambda: L.call("pmu_conv3x3_dgrad_wino4_bnr", dzt32.data_ptr(), Cout, N, H, W, w4d.data_ptr(),
                                         Cin, *bnr4),
@@ -141,6 +142,11 @@ def main():
                                          w2d.data_ptr(), Cin, *bnr2),
             "dgrad_dmab": lambda: L.call("pmu_conv3x3_dgrad_dma_bnr", dzt.data_ptr(), cpo, N, H, W, wdd.data_ptr(), Cin,
                                          *bnrd),
+            # c5's shipped forms: bf16 dx (the *_dxb entries), with and without the producer's BN partials
+            "dgrad_dmabx": lambda: L.call("pmu_conv3x3_dgrad_dma_bnr_dxb", dzt.data_ptr(), cpo, N, H, W, wdd.data_ptr(),
+                                          Cin, dxb.data_ptr(), *bnrd[1:]),
+            "dgrad_dmax": lambda: L.call("pmu_conv3x3_dgrad_dma_dxb", dzt.data_ptr(), cpo, N, H, W, wdd.data_ptr(), Cin,
+                                         Cin, dxb.data_ptr(), None, s),
             "fwd_dma": lambda: L.call("pmu_conv3x3_fwd_dma", xt.data_ptr(), cpi, N, H, W, wdf.data_ptr(), b.data_ptr(),
                                       Cout, out.data_ptr(), partd.data_ptr(), s),
             "dgrad_dma": lambda: L.call("pmu_conv3x3_dgrad_dma", dzt.data_ptr(), cpo, N, H, W, wdd.data_ptr(), Cin, Cin,

@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """Per-shape HBM traffic of one kernel family from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE)
 of `tools/kbench.py --ops OP --iters I` (every shape launches 2 warm-up + I timed dispatches, in
-kbench's SHAPES order), next to the algorithmic bytes of the F(4x4) BN-backward input gradient
-(dgrad_w4b): dz read + dx written + the producer's z read + the packed U (36/9 of the filters).
+kbench's SHAPES order), next to the op's algorithmic bytes:
+  dgrad_w4b   F(4x4) BN-backward input gradient: dz + dx (fp32) + the producer's z + the packed U (36/9)
+  dgrad_dmabx c5 LDS-DMA BN-backward input gradient: dz (bf16) + dx (bf16) + the producer's z (fp32) + w
+  dgrad_dmax  c5 LDS-DMA input gradient: dz (bf16) + dx (bf16) + w
+  fwd_dma     c5 LDS-DMA forward: x (bf16) + z (fp32) + w
 
-    python tools/pmc_shapes.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR ITERS [--N 32] > out.txt
+    python tools/pmc_shapes.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR ITERS [--N 32] [--op dgrad_w4b] [--c5]
 
 Bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 correction, tools/pmc_traffic.py)."""
 import argparse
@@ -34,17 +37,29 @@ def main():
     ap.add_argument("kernel")
     ap.add_argument("iters", type=int)
     ap.add_argument("--N", type=int, default=32)
+    ap.add_argument("--op", default="dgrad_w4b")
+    ap.add_argument("--c5", action="store_true", help="kbench --c5 shapes (512x512 input)")
     a = ap.parse_args()
+    shapes = [(2 * h, ci, co) for (h, ci, co) in SHAPES] if a.c5 else SHAPES
     fe, wr = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel), per_dispatch(a.write, "WRITE_SIZE", a.kernel)
     per = 2 + a.iters
-    assert len(fe) == len(wr) == per * len(SHAPES), (len(fe), len(wr), per * len(SHAPES))
+    assert len(fe) == len(wr) == per * len(shapes), (len(fe), len(wr), per * len(shapes))
+    print(f"op {a.op} N {a.N}; bytes per dispatch = (2 FETCH_SIZE + WRITE_SIZE) x 1024")
     print(f"{'H':>4} {'Cin':>5} {'Cout':>5} {'PMC MB':>9} {'alg MB':>9} {'ratio':>6}")
-    for s, (H, Cin, Cout) in enumerate(SHAPES):
+    tp = ta = 0.0
+    for s, (H, Cin, Cout) in enumerate(shapes):
         idx = range(s * per + 2, (s + 1) * per)
         hbm = sum((2 * fe[i] + wr[i]) * 1024 for i in idx) / a.iters
         px = a.N * H * H
-        alg = px * Cout * 4 + px * Cin * 4 + px * Cin * 4 + Cin * Cout * 36 * 4
+        cpi, cpo = (Cin + 7) // 8 * 8, (Cout + 7) // 8 * 8
+        alg = {"dgrad_w4b": px * Cout * 4 + px * Cin * 4 + px * Cin * 4 + Cin * Cout * 36 * 4,
+               "dgrad_dmabx": px * cpo * 2 + px * Cin * 2 + px * Cin * 4 + Cin * Cout * 9 * 2,
+               "dgrad_dmax": px * cpo * 2 + px * Cin * 2 + Cin * Cout * 9 * 2,
+               "fwd_dma": px * cpi * 2 + px * Cout * 4 + Cin * Cout * 9 * 2}[a.op]
+        tp += hbm
+        ta += alg
         print(f"{H:4d} {Cin:5d} {Cout:5d} {hbm / 1e6:9.1f} {alg / 1e6:9.1f} {hbm / alg:6.2f}")
+    print(f"{'all':>16} {tp / 1e6:9.1f} {ta / 1e6:9.1f} {tp / ta:6.2f}")
 
 
 if __name__ == "__main__":
