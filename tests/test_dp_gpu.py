@@ -26,7 +26,21 @@ def test_bucketed_allreduce_overlapped_with_hip_backward():
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tools", "dp_check.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     out = r.stdout + r.stderr
-    assert r.returncode == 0 and "DP_CHECK OK" in out, out[-4000:]
+    assert r.returncode == 0 and "DP_CHECK gloo world 2 OK" in out, out[-4000:]
+
+
+@pytest.mark.gpu
+def test_bucketed_allreduce_over_rccl_one_rank():
+    """The same check over RCCL (backend nccl) with the one rank this box's single GPU allows: the RCCL
+    communicator, the bucket all-reduces issued from inside the HIP backward on RCCL's stream behind the
+    compute stream's events, and the learned bucket layout; the synchronised gradient equals the local one
+    bit for bit."""
+    env = dict(os.environ, PMU_DIST_BACKEND="nccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tools", "dp_check.py")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "DP_CHECK nccl world 1 OK" in out, out[-4000:]
 
 
 @pytest.mark.gpu

@@ -23,7 +23,14 @@ def main():
     rank = int(os.environ["RANK"])
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # gloo: N ranks sharing cuda:0; nccl (RCCL): one rank per device, so on a 1-GPU box world 1 — the
+    # real RCCL communicator and collectives under the overlapped buckets
+    backend = os.environ.get("PMU_DIST_BACKEND", "gloo")
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    cdev = dev if backend == "nccl" else torch.device("cpu")   # RCCL collectives take device tensors
     from model import UNet
     from pmu_hip.dp import BucketAllReduce
     torch.manual_seed(0)
@@ -41,12 +48,13 @@ def main():
 
     # local gradient (BN running stats move; the weights do not, so both passes see the same net)
     backward()
-    local = torch.cat([p.grad.reshape(-1) for p in plist]).cpu()
+    local = torch.cat([p.grad.reshape(-1) for p in plist]).to(cdev)
     allg = [torch.empty_like(local) for _ in range(world)]
     dist.all_gather(allg, local)
     want = allg[0].clone()
     for a in allg[1:]:
         want += a
+    want = want.cpu()
     from pmu_hip.engine import unet_report_order
     sync = BucketAllReduce(net, bucket_bytes=64 << 10)
     # the backward's real report order, seen through the reducer's flush callback
@@ -74,10 +82,10 @@ def main():
         ok = ok and err == 0.0 and adopted and order_ok
         if it > 0:   # the learned layout: every bucket from inside the backward, bucket 0 early
             ok = ok and issued == nb and nb > 2 and first is not None and first < flushes // 2
-    flag = torch.tensor([1 if ok else 0])
+    flag = torch.tensor([1 if ok else 0], device=cdev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if rank == 0:
-        print("DP_CHECK", "OK" if flag.item() == 1 else "FAIL", flush=True)
+        print("DP_CHECK", backend, "world", world, "OK" if flag.item() == 1 else "FAIL", flush=True)
     dist.destroy_process_group()
     sys.exit(0 if flag.item() == 1 else 1)
 
