@@ -1,17 +1,17 @@
-# (CPU side) copy the evidence of a finished `gpu_round.sh` call from gpurun_out/ into profiles/<round>/
+# (CPU side) copy the evidence of finished `scripts/gpu_round.sh` calls (parts A and B) from gpurun_out/round
+# into profiles/<round>/round/
 set -eu
-R=${1:?round dir, e.g. r02}
-P=profiles/$R; G=gpurun_out/round; B=gpurun_out/pmc_bench
+R=${1:?round dir, e.g. r06}
+P=profiles/$R/round; G=gpurun_out/round
 mkdir -p $P
-cp $G/bench.json $P/bench_c2.json
-cp $G/bench_c4.json $P/bench_c4_probunet.json
-cp $G/bench_c5.json $P/bench_c5.json
-cp $G/tests_gpu.log $P/tests_gpu.log
-cp $G/smoke.log $P/smoke.log
-cp $G/prof/bench_kernel_stats.csv $P/rocprof_kernel_stats_c2.csv
-cp $G/prof_c4/bench_kernel_stats.csv $P/rocprof_kernel_stats_c4.csv
-cp $G/prof_c5/bench_kernel_stats.csv $P/rocprof_kernel_stats_c5.csv
+for f in tests_gpu.log smoke.log bench_c2.json bench_c4.json bench_c5.json bench_c3_phantom.json; do
+  [ -f $G/$f ] && cp $G/$f $P/
+done
+for d in prof:c2 prof_c4:c4 prof_c5:c5; do
+  src=${d%%:*}; tag=${d##*:}
+  [ -f $G/$src/bench_kernel_stats.csv ] && cp $G/$src/bench_kernel_stats.csv $P/rocprof_kernel_stats_$tag.csv
+done
 for W in unet c5 probunet; do
-  if [ -f $B/pmc_traffic_$W.json ]; then cp $B/pmc_traffic_$W.json $P/; cp $B/summary_$W.txt $P/pmc_traffic_${W}_summary.txt; fi
+  if [ -f $G/pmc_traffic_$W.json ]; then cp $G/pmc_traffic_$W.json $G/summary_$W.txt $P/; fi
 done
 ls -la $P
