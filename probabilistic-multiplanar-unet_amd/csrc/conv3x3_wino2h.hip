@@ -495,7 +495,11 @@ struct W2Block {
   unsigned gin, gzero;
 };
 
-template <bool DGRAD, bool BNR, int CH, int CO_, bool P64>
+// EXP (timing experiments, experiments build, PMU_WINO2H_EXP; wrong results on purpose): 1 = no restaging
+// (every chunk reads stage 0, no DMA after the first; the chunk barrier kept), 2 = that without the barrier,
+// 3 = the DMA issued as usual but never waited for (a bare s_barrier per chunk), 4 = only the operand image
+// restaged (U DMA'd for the first chunk only), 5 = only U restaged
+template <bool DGRAD, bool BNR, int CH, int CO_, bool P64, int EXP = 0>
 __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, const unsigned (&goff)[W2Cfg<CO_>::NGL],
                                             float* smem) {
   using C = W2Cfg<CO_>;
@@ -522,11 +526,11 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
     float* b_ = (BUF);                                                                                     \
     const char* xb_ = reinterpret_cast<const char*>(a.x + k0_);                                            \
     _Pragma("unroll") for (int r = 0; r < NGL; ++r)                                                        \
-      if ((gin >> r) & 1u) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)                           \
+      if (EXP != 5 && ((gin >> r) & 1u)) PMU_GLDS(xb_ + goff[r], b_ + 4 * (r * NT) + wave_off)             \
     const char* s_ = reinterpret_cast<const char*>(wsrc + ((long long)p_ * nchunks + cs_) * U_FLOATS) + uoff; \
     float* d_ = b_ + A_FLOATS + wave_off;                                                                  \
     _Pragma("unroll") for (int r = 0; r < UGL; ++r)                                                        \
-      if (r * NT * 4 + (wave + 1) * 256 <= U_FLOATS) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r)          \
+      if (EXP != 4 && r * NT * 4 + (wave + 1) * 256 <= U_FLOATS) PMU_GLDS(s_ + 16 * NT * r, d_ + 4 * NT * r) \
   }
   const int t = lane & 15, kk = lane >> 4, tg = wave & 3, cg = wave >> 3;
   const int pbase = 2 * (2 * tg + (t >> 3)) * ROWF + GP * (t & 7) + 2 * kk;
@@ -546,8 +550,8 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
     const float bias = (!DGRAD && a.bias && jb < a.NOUT) ? a.bias[jb] : 0.f;
     int gi = p * nchunks;
     for (int ch = 0; ch < nchunks; ++ch, ++gi) {
-      float* cur = smem + (gi & 1) * STAGE;
-      if (gi + 1 < total) PMU_FETCH2(gi + 1, smem + ((gi + 1) & 1) * STAGE)
+      float* cur = smem + ((EXP == 1 || EXP == 2) ? 0 : (gi & 1) * STAGE);
+      if (gi + 1 < total && EXP != 1 && EXP != 2) PMU_FETCH2(gi + 1, smem + ((gi + 1) & 1) * STAGE)
       const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
       if constexpr (P64) {
         w2_pair<CH, CO>(pa, ua, acc);                    // channels 2*kk, 2*kk + 1
@@ -555,8 +559,12 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
         w2_step<CH>(pa, ua, acc);                        // channel 2*kk
         w2_step<CH>(pa + 4, ua + CO * NCP * 4, acc);     // channel 2*kk + 1
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
-      __syncthreads();
+      if (EXP == 3) {  // timing experiment: the DMA issued but never waited for (a bare barrier)
+        __builtin_amdgcn_s_barrier();
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
+        if (EXP != 2) __syncthreads();
+      }
     }
     int ne = B.n, h0e = B.h0, w0e = B.w0;
     asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
@@ -579,7 +587,7 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
 
 // BNR (input gradient only): the producer's BN-backward partial sums in the epilogue (a.bz set) — a
 // compile-time choice, so the z loads and their uses sit in straight-line code
-template <bool DGRAD, bool BNR, int CO_, bool P64 = true>
+template <bool DGRAD, bool BNR, int CO_, bool P64 = true, int EXP = 0>
 // 64 channels: 1024 threads = four waves per SIMD (<= 128 VGPRs implied); 32 channels: 512 threads,
 // capped at 128 VGPRs (four waves per SIMD) so two workgroups share a CU (at 132 VGPRs only one fit)
 __global__ __launch_bounds__(16 * CO_, CO_ == 32 ? 4 : 1) void conv3x3_wino2h_kernel(W2Args a) {
@@ -624,8 +632,8 @@ __global__ __launch_bounds__(16 * CO_, CO_ == 32 ? 4 : 1) void conv3x3_wino2h_ke
   }
   B.gin = gin;
   B.gzero = gzero;
-  if ((tid >> 8) & 1) wino2h_main<DGRAD, BNR, 1, CO_, P64>(a, B, goff, smem);
-  else wino2h_main<DGRAD, BNR, 0, CO_, P64>(a, B, goff, smem);
+  if ((tid >> 8) & 1) wino2h_main<DGRAD, BNR, 1, CO_, P64, EXP>(a, B, goff, smem);
+  else wino2h_main<DGRAD, BNR, 0, CO_, P64, EXP>(a, B, goff, smem);
 }
 
 // output channels per block (PMU_WINO2H_CO=32: 512-thread blocks, two per CU; A/B)
@@ -690,6 +698,19 @@ int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, 
     const char* e = pmu_variant_env("PMU_WINO2H_B32");
     return e ? atoi(e) : 0;
   }();
+  static const int exp_v = [] {
+    const char* e = pmu_variant_env("PMU_WINO2H_EXP");
+    return e ? atoi(e) : 0;
+  }();
+  if (exp_v && CO == 64 && !dgrad) {
+    if (exp_v == 1) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 1>), grid, dim3(1024), 0, st, a);
+    else if (exp_v == 2) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 2>), grid, dim3(1024), 0, st, a);
+    else if (exp_v == 4) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 4>), grid, dim3(1024), 0, st, a);
+    else if (exp_v == 5) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 5>), grid, dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 3>), grid, dim3(1024), 0, st, a);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   if (b32 && CO == 64) {
     if (bnr) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, true, 64, false>), grid, dim3(1024), 0, st, a);
     else if (dgrad) hipLaunchKernelGGL((conv3x3_wino2h_kernel<true, false, 64, false>), grid, dim3(1024), 0, st, a);
