@@ -32,9 +32,16 @@ constexpr int ROWF = 208;                     // floats per halo row (9 groups =
 constexpr int ROWU = ROWF / 4;
 constexpr int A_FLOATS = HH * ROWF;
 [[maybe_unused]] constexpr int NC = 16;       // Winograd components
-constexpr int NCP = 20;                       // floats per U row: 16 components + a pad unit (odd unit stride:
-                                              // the lanes' b128 U reads are conflict-free; 16 banked 4-way)
+constexpr int NCP = 16;                       // floats per U row: the 16 components as four 16-B units, unit q
+                                              // of row r stored at q ^ u_swz(r) (the lanes' b128 U reads
+                                              // conflict-free without a pad unit, see u_swz)
 constexpr int A_UNITS = A_FLOATS / 4;
+
+// U row r = kl * CO + co (channel in chunk, output channel in block) keeps its 16-B unit q at q ^ u_swz(r):
+// 16 lanes reading rows r .. r + 15 (one b128 phase) then cover the 64 banks once — rows 4 apart, 256 B
+// = 64 banks apart, land on different units.  Every lane's row is 32 cg + 16 h + t (+ CO per channel, CO a
+// multiple of 16), so u_swz(row) = (t >> 2) & 3 for the lane's t = lane & 15.
+__host__ __device__ constexpr int u_swz(int row) { return (row >> 2) & 3; }
 
 // block geometry by output channels per block: 64 (1024 threads, 16 waves, one block per CU) or 32
 // (512 threads, 8 waves, 67 KB of LDS: two blocks per CU, PMU_WINO2H_CO=32)
@@ -43,7 +50,7 @@ struct W2Cfg {
   static constexpr int CO = CO_;
   static constexpr int NT = 16 * CO_;
   static constexpr int NW = NT / 64;
-  static constexpr int U_FLOATS = BK * CO_ * NCP;          // [ch 8][co][comp 16 + 4 pad]
+  static constexpr int U_FLOATS = BK * CO_ * NCP;          // [ch 8][co][comp 16, units swizzled]
   static constexpr int STAGE = A_FLOATS + U_FLOATS;
   static constexpr int NGL = (A_UNITS + NT - 1) / NT;
   static constexpr int UGL = (U_FLOATS / 4 + NT - 1) / NT;  // U DMA rounds (the last one by the first waves)
@@ -56,7 +63,7 @@ struct W2Cfg {
 
 struct W2Args {
   const float* x;     // [N][H][W][KC]
-  const float* wp;    // packed U [co block][chunk][ch 8][co 64][comp 16 + 4 pad]
+  const float* wp;    // packed U [co block][chunk][ch 8][co 64][comp 16, units swizzled by u_swz]
   const float* bias;
   float* out0;
   float* out1;
@@ -119,9 +126,9 @@ __device__ __forceinline__ void pack_wino2h_body(const float* __restrict__ w, in
     float u[16];
     wino2_u(g, u);
     float* dst = wp + (((long long)jb * nch + ch) * BK + kl) * (CO * NCP) + col * NCP;
+    const int sw = u_swz(kl * CO + col);
     for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
-    *reinterpret_cast<float4*>(dst + 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(dst + 4 * (q ^ sw)) = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
   }
 }
 template <int CO>
@@ -148,8 +155,8 @@ __device__ __forceinline__ void pack_wino2h_fwd_body(const float* __restrict__ w
     float u[16];
     wino2_u(g, u);
     float4* d = seg4 + (kl * CO + col) * (NCP / 4);
-    for (int q = 0; q < 4; ++q) d[q] = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
-    d[4] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int sw = u_swz(kl * CO + col);
+    for (int q = 0; q < 4; ++q) d[q ^ sw] = make_float4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
   }
   __syncthreads();
   float4* dst = reinterpret_cast<float4*>(wp + (long long)bid * SEG);
@@ -201,17 +208,18 @@ __device__ __forceinline__ void wait_lgkm() {
 // one MFMA step (channel 2*kk + ks in k-slot kk): patch (16 x b32), U (2 groups x 2 co halves x b128),
 // half CH of B^T d B (rows 2CH, 2CH+1; B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]), 16 MFMAs
 template <int CH>
-__device__ __forceinline__ void w2_step(unsigned pa, unsigned ua, f32x4 (&acc)[2][8]) {
+__device__ __forceinline__ void w2_step(unsigned pa, unsigned ua0, unsigned ua1, f32x4 (&acc)[2][8]) {
   float d[16];
 #define PMU_RD(I, J) d[4 * (I) + (J)] = lds_b32<PMU_W2P(I, J)>(pa);
   PMU_RD(0, 0) PMU_RD(0, 1) PMU_RD(0, 2) PMU_RD(0, 3) PMU_RD(1, 0) PMU_RD(1, 1) PMU_RD(1, 2) PMU_RD(1, 3)
   PMU_RD(2, 0) PMU_RD(2, 1) PMU_RD(2, 2) PMU_RD(2, 3) PMU_RD(3, 0) PMU_RD(3, 1) PMU_RD(3, 2) PMU_RD(3, 3)
 #undef PMU_RD
-  // U of this half: components 8CH .. 8CH+7 of co half h at row offset 16*NCP*h
-  const float4 u00 = lds_b128<(8 * CH) * 4>(ua);
-  const float4 u10 = lds_b128<(16 * NCP + 8 * CH) * 4>(ua);
-  const float4 u01 = lds_b128<(8 * CH + 4) * 4>(ua);
-  const float4 u11 = lds_b128<(16 * NCP + 8 * CH + 4) * 4>(ua);
+  // U of this half: components 8CH .. 8CH+7 (units 2CH at ua0, 2CH + 1 at ua1) of co half h at row
+  // offset 16*NCP*h
+  const float4 u00 = lds_b128<0>(ua0);
+  const float4 u10 = lds_b128<16 * NCP * 4>(ua0);
+  const float4 u01 = lds_b128<0>(ua1);
+  const float4 u11 = lds_b128<16 * NCP * 4>(ua1);
   wait_lgkm<2>();  // the patch and U group 0
   __builtin_amdgcn_sched_barrier(0);
   float t[2][4];
@@ -301,7 +309,7 @@ __device__ __forceinline__ void w2_mfma(const float (&v)[8], float4 u00, float4 
 // the 16 tiles x 2 k-slots cover the 64 banks once (the b32 reads of one channel were 2-way: tile rows
 // 368 = 16 (mod 32) apart put both rows of tiles on the same 8 bank quads).
 template <int CH, int CO>
-__device__ __forceinline__ void w2_pair(unsigned pa, unsigned ua, f32x4 (&acc)[2][8]) {
+__device__ __forceinline__ void w2_pair(unsigned pa, unsigned ua0, f32x4 (&acc)[2][8]) {
   float2 c[3][4];
 #define PMU_RD2(I, J) c[I][J] = lds_b64<PMU_W2P(CH + (I), J)>(pa);
   PMU_RD2(0, 0) PMU_RD2(0, 1) PMU_RD2(0, 2) PMU_RD2(0, 3) PMU_RD2(1, 0) PMU_RD2(1, 1) PMU_RD2(1, 2) PMU_RD2(1, 3)
@@ -328,20 +336,21 @@ __device__ __forceinline__ void w2_pair(unsigned pa, unsigned ua, f32x4 (&acc)[2
   __builtin_amdgcn_sched_barrier(0);
   // U after the patch is consumed (at the 128-register cap of four waves per SIMD the patch pairs and U
   // together spilled; the SIMD's other waves cover the U read latency)
-  float4 u00 = lds_b128<(8 * CH) * 4>(ua);
-  float4 u10 = lds_b128<(16 * NCP + 8 * CH) * 4>(ua);
-  float4 u01 = lds_b128<(8 * CH + 4) * 4>(ua);
-  float4 u11 = lds_b128<(16 * NCP + 8 * CH + 4) * 4>(ua);
+  // (unit 2CH + 1 at ua0 ^ 16, formed at each use: one register fewer live across the MFMAs)
+  float4 u00 = lds_b128<0>(ua0);
+  float4 u10 = lds_b128<16 * NCP * 4>(ua0);
+  float4 u01 = lds_b128<0>(ua0 ^ 16u);
+  float4 u11 = lds_b128<16 * NCP * 4>(ua0 ^ 16u);
   float v[8];
   w2_rows(t0, v);
   wait_lgkm<2>();  // U group 0
   __builtin_amdgcn_sched_barrier(0);
   w2_mfma<0>(v, u00, u10, u01, u11, acc);
-  const unsigned ua1 = ua + CO * NCP * 4;
-  u00 = lds_b128<(8 * CH) * 4>(ua1);
-  u10 = lds_b128<(16 * NCP + 8 * CH) * 4>(ua1);
-  u01 = lds_b128<(8 * CH + 4) * 4>(ua1);
-  u11 = lds_b128<(16 * NCP + 8 * CH + 4) * 4>(ua1);
+  const unsigned ub = ua0 + CO * NCP * 4;  // step 1: the next channel's rows, CO rows on (same swizzle)
+  u00 = lds_b128<0>(ub);
+  u10 = lds_b128<16 * NCP * 4>(ub);
+  u01 = lds_b128<0>(ub ^ 16u);
+  u11 = lds_b128<16 * NCP * 4>(ub ^ 16u);
   w2_rows(t1, v);
   wait_lgkm<2>();  // step 1's U group 0
   __builtin_amdgcn_sched_barrier(0);
@@ -535,6 +544,10 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
   const int t = lane & 15, kk = lane >> 4, tg = wave & 3, cg = wave >> 3;
   const int pbase = 2 * (2 * tg + (t >> 3)) * ROWF + GP * (t & 7) + 2 * kk;
   const int ubase = A_FLOATS + (2 * kk * CO + 32 * cg + t) * NCP;
+  static_assert(CO % 16 == 0, "u_swz of every row a lane reads is (t >> 2) & 3");
+  // byte offset of unit 2CH of the lane's row in a stage; unit 2CH + 1 is at that ^ 16 (rows 64-B aligned:
+  // smem aligned to 64, A_FLOATS and STAGE multiples of 16 floats)
+  const unsigned uoff0 = 4u * ubase + 16u * ((2 * CH) ^ ((t >> 2) & 3));
   f32x4 acc[2][8];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -552,12 +565,12 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
     for (int ch = 0; ch < nchunks; ++ch, ++gi) {
       float* cur = smem + ((EXP == 1 || EXP == 2) ? 0 : (gi & 1) * STAGE);
       if (gi + 1 < total && EXP != 1 && EXP != 2) PMU_FETCH2(gi + 1, smem + ((gi + 1) & 1) * STAGE)
-      const unsigned pa = lds_addr(cur + pbase), ua = lds_addr(cur + ubase);
+      const unsigned pa = lds_addr(cur + pbase), ua0 = lds_addr(cur) + uoff0, ua1 = ua0 ^ 16u;
       if constexpr (P64) {
-        w2_pair<CH, CO>(pa, ua, acc);                    // channels 2*kk, 2*kk + 1
+        w2_pair<CH, CO>(pa, ua0, acc);                   // channels 2*kk, 2*kk + 1
       } else {
-        w2_step<CH>(pa, ua, acc);                        // channel 2*kk
-        w2_step<CH>(pa + 4, ua + CO * NCP * 4, acc);     // channel 2*kk + 1
+        w2_step<CH>(pa, ua0, ua1, acc);                  // channel 2*kk
+        w2_step<CH>(pa + 4, ua0 + CO * NCP * 4, ua1 + CO * NCP * 4, acc);  // channel 2*kk + 1
       }
       if (EXP == 3) {  // timing experiment: the DMA issued but never waited for (a bare barrier)
         __builtin_amdgcn_s_barrier();
@@ -593,7 +606,8 @@ template <bool DGRAD, bool BNR, int CO_, bool P64 = true, int EXP = 0>
 __global__ __launch_bounds__(16 * CO_, CO_ == 32 ? 4 : 1) void conv3x3_wino2h_kernel(W2Args a) {
   using C = W2Cfg<CO_>;
   constexpr int NT = C::NT, NGL = C::NGL, STAGE = C::STAGE;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + C::RED_FLOATS];
+  __shared__ __attribute__((aligned(64))) float smem[2 * STAGE + C::RED_FLOATS];
+  static_assert(A_FLOATS % 16 == 0 && STAGE % 16 == 0, "U rows 64-B aligned (ua1 = ua0 ^ 16)");
   const int tid = threadIdx.x;
   const int lb = pmu_xcd_block(blockIdx.x, gridDim.x);
   const int ncog = (a.nco + a.cpb - 1) / a.cpb;

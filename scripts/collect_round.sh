@@ -4,7 +4,7 @@ set -eu
 R=${1:?round dir, e.g. r06}
 P=profiles/$R/round; G=gpurun_out/round
 mkdir -p $P
-for f in tests_gpu.log smoke.log bench_c2.json bench_c4.json bench_c5.json bench_c3_phantom.json; do
+for f in tests_gpu.log tests_gpu_debug.log smoke.log bench_c2.json bench_c4.json bench_c5.json bench_c3_phantom.json; do
   [ -f $G/$f ] && cp $G/$f $P/
 done
 for d in prof:c2 prof_c4:c4 prof_c5:c5; do

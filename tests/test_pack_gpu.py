@@ -2,7 +2,8 @@
 restatement of the packed layout, on ragged channel counts (partial co blocks and chunks are zero).
 
 Layouts (csrc/conv3x3_wino2h.hip, csrc/conv3x3_wino4.hip): [co block][chunk of 8][ci in chunk][co in
-block][components]; F(2x2): 64 co per block, components 4a+b of G g G^T plus 4 zero pad; F(4x4): 32 co
+block][components]; F(2x2): 64 co per block, components 4a+b of G g G^T as four 16-B units, unit q of row
+r = ci_in_chunk * 64 + co_in_block stored at q ^ ((r >> 2) & 3) (round 6's unpadded swizzle); F(4x4): 32 co
 per block, the 36 components 6a+b of G g G^T in component-half order (upos).  The input-gradient
 packs transform w[co][ci] rotated by 180 degrees, with ci as the output channel.
 """
@@ -20,7 +21,7 @@ def _upos(half, cl):
     return 16 * half + cl if cl < 16 else 32 + 2 * half + (cl - 16)
 
 
-def _expected(w, dgrad, G, CO, ncp, order=None):
+def _expected(w, dgrad, G, CO, ncp, order=None, swz=False):
     w = w.double().cpu()
     if dgrad:  # filters indexed [out = ci][reduction = co], rotated
         w = w.flip(2, 3).transpose(0, 1)
@@ -35,7 +36,13 @@ def _expected(w, dgrad, G, CO, ncp, order=None):
     if ncp > ncomp:
         full = torch.cat([full, torch.zeros(full.shape[0], full.shape[1], ncp - ncomp, dtype=torch.float64)], 2)
     # [co block][col][chunk][kl][comp] -> [co block][chunk][kl][col][comp]
-    return full.reshape(nco, CO, nch, 8, ncp).permute(0, 2, 3, 1, 4).contiguous().reshape(-1)
+    out = full.reshape(nco, CO, nch, 8, ncp).permute(0, 2, 3, 1, 4).contiguous()
+    if swz:  # position p of row r holds unit p ^ ((r >> 2) & 3) (XOR is its own inverse)
+        out = out.reshape(nco, nch, 8 * CO, ncp // 4, 4)
+        r = torch.arange(8 * CO)
+        src = torch.arange(ncp // 4)[None, :] ^ ((r[:, None] >> 2) & 3)
+        out = torch.gather(out, 3, src[None, None, :, :, None].expand(nco, nch, -1, -1, 4))
+    return out.reshape(-1)
 
 
 _ORDER4 = [0] * 36
@@ -53,7 +60,7 @@ def test_pack_wino2h(dev, Cout, Cin, dgrad):
     wp = torch.full((n,), float("nan"), device=dev)
     L.call("pmu_conv3x3_pack_wino2h", w.data_ptr(), Cout, Cin, int(dgrad), wp.data_ptr(), L.stream())
     torch.cuda.synchronize()
-    ref = _expected(w, dgrad, G2, 64, 20)
+    ref = _expected(w, dgrad, G2, 64, 16, swz=True)
     assert ref.numel() == n
     assert float((wp.double().cpu() - ref).abs().max()) <= 1e-6 * float(ref.abs().max())
 
