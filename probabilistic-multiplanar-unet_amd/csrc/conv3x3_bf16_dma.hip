@@ -396,7 +396,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
             s2[fn] = fmaf(m0, m0, s2[fn]);
             s1[fn] += m1;
             s2[fn] = fmaf(m1, m1, s2[fn]);
-            const float recv = __shfl_xor(odd ? v0 : v1, 1, 64);
+            const float recv = pmu_swap1(odd ? v0 : v1);
             const float2 pv = odd ? make_float2(recv, v1) : make_float2(v0, recv);
             const int w = w0 + acc_row(r + odd, elane);
             if (!(jok[fn] && h < a.H && w < a.W) || (EXP & 1)) continue;
@@ -437,6 +437,38 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
     // straight-line masked form of the forward above spilled 18-140 VGPRs here.
     // (XB: each use rounds its accumulator, rb() below; rounding all 128 up front spilled 7 VGPRs)
     auto rb = [](float v) { return XB ? pmu_round_bf16(v) : v; };
+    // (a.bz) z under the accumulators, a fragment row (fn, fm) of 16 values per lane at a time, the next
+    // row's loads issued before this row's are consumed (one HBM round trip per wave instead of one per
+    // row), the first row's before the dx stores (its consumption then waits for no store); clamped
+    // addresses: every elane loads, masked values ignored
+    float zt[2][16];
+    auto zload = [&](int g, float (&z)[16]) __attribute__((always_inline)) {
+      const int fn = g / FM, fm = g - (g / FM) * FM;
+      const int j = ej0 + wn * 64 + fn * 32 + eli;
+      const int jc = j < a.NOUT ? j : a.NOUT - 1;
+      const int h = h0 + 4 * wm + fm;
+      const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
+  #pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned zo = (unsigned)(min(w0 + acc_row(r, elane), a.W - 1) * a.NOUT);
+        if constexpr (ZB) z[r] = pmu_bf16_f32((reinterpret_cast<const unsigned short*>(a.bz) + row * a.NOUT + jc)[zo]);
+        else z[r] = (a.bz + row * a.NOUT + jc)[zo];
+      }
+    };
+    const bool bnr = !CS && a.bz;
+    float bsc[FN], bsh[FN], bmu[FN], bis[FN];  // the producer's BN coefficients of the lane's channels
+    if (bnr) {
+      zload(0, zt[0]);
+  #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int j = ej0 + wn * 64 + fn * 32 + eli;
+        const int jc = j < a.NOUT ? j : a.NOUT - 1;
+        bsc[fn] = a.bcoef[jc];
+        bsh[fn] = a.bcoef[a.NOUT + jc];
+        bmu[fn] = a.bmean[jc];
+        bis[fn] = a.binv[jc];
+      }
+    }
   #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       s1[fn] = 0.f;
@@ -459,6 +491,9 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
   #pragma unroll
       for (int fm = 0; fm < FM; ++fm) {
         const int h = h0 + 4 * wm + fm;
+        // the fragment row's first pixel (rows past the image clamped, their stores masked): one 64-bit
+        // row base per (fm, fn), 32-bit offsets within the row
+        const long long rowpix = ((long long)n * a.H + (h < a.H ? h : a.H - 1)) * a.W;
         if (dstb) {
           // the bf16 copy as 4-byte channel pairs: lanes 2k, 2k+1 hold adjacent channels of the same
           // pixels r, r + 1; one xor-1 shuffle gives the even elane pixel r's pair and the odd elane pixel
@@ -468,13 +503,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
   #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const unsigned b0 = bf16_bits(acc[fm][fn][r]), b1 = bf16_bits(acc[fm][fn][r + 1]);
-            const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);
+            const unsigned recv = pmu_swap1(odd ? b0 : b1);
             const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
             const int w = w0 + acc_row(r + odd, elane);
             if (!jok || h >= a.H || w >= a.W) continue;
-            const long long pix = ((long long)n * a.H + h) * a.W + w;
-            PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-            st_drop(dstb + pix * ld - odd, pair);
+            PMU_DCHECK(rowpix + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+            st_drop(dstb + rowpix * ld + (unsigned)(w * ld - odd), pair);
           }
         }
         // (only CS has a null out1, its dx1 the bf16 copy alone; XB's dx0 is the bf16 store above)
@@ -484,13 +518,12 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
   #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const float v0 = rb(acc[fm][fn][r]), v1 = rb(acc[fm][fn][r + 1]);
-            const float recv = __shfl_xor(odd ? v0 : v1, 1, 64);
+            const float recv = pmu_swap1(odd ? v0 : v1);
             const float2 pv = odd ? make_float2(recv, v1) : make_float2(v0, recv);
             const int w = w0 + acc_row(r + odd, elane);
             if (!jok || h >= a.H || w >= a.W) continue;
-            const long long pix = ((long long)n * a.H + h) * a.W + w;
-            PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-            st_drop(dstp + pix * ld - odd, pv);
+            PMU_DCHECK(rowpix + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+            st_drop(dstp + rowpix * ld + (unsigned)(w * ld - odd), pv);
           }
           continue;
         }
@@ -498,36 +531,28 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void conv3x3_dma_kernel(DmaArgs 
         for (int r = 0; r < 16; ++r) {
           const int w = w0 + acc_row(r, elane);
           if (!jok || h >= a.H || w >= a.W) continue;
-          const long long pix = ((long long)n * a.H + h) * a.W + w;
-          PMU_DCHECK(pix < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
-          dstp[pix * ld] = rb(acc[fm][fn][r]);
+          PMU_DCHECK(rowpix + w < (long long)a.N * a.H * a.W, PMU_DBG_OUTPUT);
+          dstp[rowpix * ld + (unsigned)(w * ld)] = rb(acc[fm][fn][r]);
         }
       }
     }
-    if (!CS && a.bz) {
+    if (bnr) {
   #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        const int j = ej0 + wn * 64 + fn * 32 + eli;
-        const bool jok = j < a.NOUT;
-        const int jc = jok ? j : a.NOUT - 1;
-        const float bsc = a.bcoef[jc], bsh = a.bcoef[a.NOUT + jc], bmu = a.bmean[jc], bis = a.binv[jc];
+        const bool jok = ej0 + wn * 64 + fn * 32 + eli < a.NOUT;
   #pragma unroll
         for (int fm = 0; fm < FM; ++fm) {
+          const int g = fn * FM + fm;
+          if (g + 1 < FN * FM) zload(g + 1, zt[(g + 1) & 1]);
+          const float (&z)[16] = zt[g & 1];
           const int h = h0 + 4 * wm + fm;
-          const long long row = ((long long)n * a.H + min(h, a.H - 1)) * a.W;
-          float zt[16];
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) {  // clamped addresses: every elane loads, masked values ignored
-            const long long zi = (row + min(w0 + acc_row(r, elane), a.W - 1)) * a.NOUT + jc;
-            zt[r] = ZB ? pmu_bf16_f32(reinterpret_cast<const unsigned short*>(a.bz)[zi]) : a.bz[zi];
-          }
   #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int w = w0 + acc_row(r, elane);
             const bool ok = jok && h < a.H && w < a.W;
-            const float gg = (ok && fmaf(zt[r], bsc, bsh) > 0.f) ? rb(acc[fm][fn][r]) : 0.f;
+            const float gg = (ok && fmaf(z[r], bsc[fn], bsh[fn]) > 0.f) ? rb(acc[fm][fn][r]) : 0.f;
             s1[fn] += gg;
-            s2[fn] = fmaf(gg, (zt[r] - bmu) * bis, s2[fn]);
+            s2[fn] = fmaf(gg, (z[r] - bmu[fn]) * bis[fn], s2[fn]);
           }
         }
       }

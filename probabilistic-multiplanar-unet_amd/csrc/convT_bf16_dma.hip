@@ -222,7 +222,7 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
           for (int r = 0; r < 16; r += 2) {
             const unsigned b0 = __builtin_bit_cast(unsigned short, (__bf16)acc[fm][fn][r]);
             const unsigned b1 = __builtin_bit_cast(unsigned short, (__bf16)acc[fm][fn][r + 1]);
-            const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);
+            const unsigned recv = pmu_swap1(odd ? b0 : b1);
             const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
             const int m = m0 + wm * 128 + fm * 32 + acc_row(r + odd, lane);
             if (m < g.M) {
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(NT, 1) void convT_dma_kernel(GArgs g) {
 #define PMU_CT_PAIR(FM_, R_)                                                                                \
   const unsigned b0 = __builtin_bit_cast(unsigned short, (__bf16)(acc[FM_][fn][R_] + b));                   \
   const unsigned b1 = __builtin_bit_cast(unsigned short, (__bf16)(acc[FM_][fn][(R_) + 1] + b));             \
-  const unsigned recv = (unsigned)__shfl_xor((int)(odd ? b0 : b1), 1, 64);                                  \
+  const unsigned recv = pmu_swap1(odd ? b0 : b1);                                                         \
   const unsigned pair = odd ? (recv | (b1 << 16)) : (b0 | (recv << 16));
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) {

@@ -119,6 +119,15 @@ __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (
 __device__ __forceinline__ float pmu_bf16_f32(unsigned short u) { return __uint_as_float((unsigned)u << 16); }
 __device__ __forceinline__ unsigned short pmu_f32_bf16(float v) { return __builtin_bit_cast(unsigned short, (__bf16)v); }
 __device__ __forceinline__ float pmu_round_bf16(float v) { return pmu_bf16_f32(pmu_f32_bf16(v)); }
+
+// The value of lane l ^ 1 (adjacent-lane swap) as a DPP quad permutation [1, 0, 3, 2]: a VALU move, where
+// __shfl_xor(v, 1) is a ds_bpermute whose LDS round trip each use waits for (lgkmcnt(0) per swap in the
+// store epilogues).  Every lane of the wave must be active.
+__device__ __forceinline__ int pmu_swap1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true); }
+__device__ __forceinline__ unsigned pmu_swap1(unsigned v) { return (unsigned)pmu_swap1((int)v); }
+__device__ __forceinline__ float pmu_swap1(float v) {
+  return __builtin_bit_cast(float, pmu_swap1(__builtin_bit_cast(int, v)));
+}
 __device__ __forceinline__ float4 pmu_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float4 pmu_ld4(const unsigned short* p) {
   const uint2 u = *reinterpret_cast<const uint2*>(p);

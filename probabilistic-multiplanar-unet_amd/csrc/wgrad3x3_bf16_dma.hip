@@ -99,7 +99,11 @@ __device__ __forceinline__ void wgd_wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
 }
 
-template <int WCOF, int WCIF, int WS, int TPS>
+// EXP (timing experiments, experiments build, PMU_WGD_EXP; wrong results on purpose): 1 = no DMA at all
+// (the stage bookkeeping and barriers kept), 2 = the DMA issued from the zero page for every unit (no
+// per-stage source address work), 3 = the DMA as shipped without the stage barrier, 4 = the source
+// addresses formed as shipped (kept live) but the DMA issued from the zero page
+template <int WCOF, int WCIF, int WS, int TPS, int EXP = 0>
 __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   using G = WG<WCOF, WCIF, WS, TPS>;
   constexpr int RPS = G::RPS;
@@ -174,13 +178,18 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
     const int dyA = RPS * (dt - 1), dyX = dt == 0 ? -2 : RPS * (dt - 1);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
+      if constexpr (EXP == 1) continue;
       const bool isA = (i * 8 + wave) * 64 < G::A_UNITS;   // (uniform)
       const int dy = isA ? dyA : dyX;
       const int y = uy[i] + dy;
       const bool ok = (unsigned)y < (unsigned)a.H && (!isA || dt > 0);
       const int e = ue[i] + dy * (isA ? rsA : rsX);
-      const char* src = !ok ? zsrc
+      const char* src = (!ok || EXP == 2) ? zsrc
                             : isA ? reinterpret_cast<const char*>(a.dzt + e) : reinterpret_cast<const char*>(a.xt + e);
+      if constexpr (EXP == 4) {
+        asm volatile("" ::"v"(src));
+        src = zsrc;
+      }
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
                                        (__attribute__((address_space(3))) void*)(stg + (i * 8 + wave) * 1024), 16, 0,
                                        0);
@@ -259,7 +268,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
       // slots of s - 2, s - 1.  Odd s: nothing (covered by the even barrier before it)
       if ((sg & 1) == 0) {
         wgd_wait_vm<(NS - 4) * NI>();
-        __builtin_amdgcn_s_barrier();
+        if constexpr (EXP != 3) __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         issue();
         issue();
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
       // stage s landed (this wave's DMAs: all but the NS-2 younger stages'), then every wave's, and every
       // read of stage s-1 — whose slot the next DMA overwrites — is done (its MFMAs consumed them)
       wgd_wait_vm<(NS - 2) * NI>();
-      __builtin_amdgcn_s_barrier();
+      if constexpr (EXP != 3) __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       issue();   // stage s + NS - 1, into the slot stage s - 1 used
       __builtin_amdgcn_sched_barrier(0);
@@ -418,6 +427,21 @@ extern "C" int pmu_conv3x3_wgrad_bf16_dma(const unsigned short* dzt, const unsig
   const int nb = pmu_cdiv(Cout, 32 * g.wcof) * pmu_cdiv(Cin, 32 * g.wcif);
   const dim3 grid((unsigned)(nb * g.nsplit)), blk(512);
   hipStream_t st = (hipStream_t)stream;
+#ifdef PMU_EXPERIMENTS
+  static const int exp_v = [] {
+    const char* e = pmu_variant_env("PMU_WGD_EXP");
+    return e ? atoi(e) : 0;
+  }();
+  if (exp_v >= 1 && exp_v <= 4) {
+#define PMU_WGD_LAUNCH(E)                                                                                   \
+    if (g.ws == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 2, 2, 1, E>), grid, blk, 0, st, a);      \
+    else if (g.wcof == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 4, 1, 1, E>), grid, blk, 0, st, a); \
+    else hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<4, 2, 1, 1, E>), grid, blk, 0, st, a);
+    if (exp_v == 1) { PMU_WGD_LAUNCH(1) } else if (exp_v == 2) { PMU_WGD_LAUNCH(2) }
+    else if (exp_v == 3) { PMU_WGD_LAUNCH(3) } else { PMU_WGD_LAUNCH(4) }
+#undef PMU_WGD_LAUNCH
+  } else
+#endif
   if (g.ws == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 2, 2, 1>), grid, blk, 0, st, a);
   else if (g.wcof == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 4, 1, 1>), grid, blk, 0, st, a);
   else hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<4, 2, 1, 1>), grid, blk, 0, st, a);
