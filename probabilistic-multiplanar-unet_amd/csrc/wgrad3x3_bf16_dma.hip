@@ -18,9 +18,9 @@
 // ds_write); a stage holds three consecutive steps (dz rows y..y+2, halo rows y+1..y+3) of every strip
 // lane of the workgroup; one barrier per two stages (54 MFMAs per wave; a ring of 5: kbench over the
 // c5 shapes 4.21 vs 4.29 ms with one barrier per stage and a ring of 4, profiles/r05/wgrad_pair).  Units outside the image, the
-// channels or the segment are DMA'd from a zero page, so every wave issues the same number of DMA
-// instructions per stage and the ring waits are counted (s_waitcnt vmcnt(N)) with the next NS-2 stages
-// in flight.  LDS rows are unit permutations, not padded rows (LDS-DMA writes 1 KiB contiguous per
+// channels or the segment read zeros through the buffer descriptors' range check, so every wave issues
+// the same number of DMA instructions per stage and the ring waits are counted (s_waitcnt vmcnt(N)) with
+// the next NS-2 stages in flight.  LDS rows are unit permutations, not padded rows (LDS-DMA writes 1 KiB contiguous per
 // wave-instruction): 16-B unit u of pixel p sits at u ^ sw(p), chosen so the four pixel rows a 32-lane
 // group of a transposed read touches fall in four distinct 16-bank quarters (conflict-free).
 //
@@ -37,7 +37,6 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
-static __device__ __attribute__((aligned(64))) unsigned g_wgd_zero[256];  // 1 KiB of zeros (DMA source)
 
 constexpr int SW = 16;  // strip width (pixels per k-step)
 
@@ -47,7 +46,12 @@ struct WG {
   static_assert(WCOF * WCIF * WS == 8, "8 waves");
   static constexpr int NT = 512;
   static constexpr int ARU = 4 * WCOF, XRU = 4 * WCIF;      // 16-B units per pixel row
-  static constexpr int A_ROW = SW * ARU, X_ROW = (SW + 2) * XRU;
+  // LDS rows of whole wave-instructions (64 units): every DMA instruction moves units of ONE image row,
+  // so its row, and whether that row lies in the image, are uniform (SGPR) per instruction and stage; the
+  // halo row's 18 pixels are padded (144 -> 192 units at 8 per pixel, 288 -> 320 at 16; the pad reads
+  // zeros and is never read back)
+  static constexpr int A_ROW = SW * ARU, X_ROW = ((SW + 2) * XRU + 63) / 64 * 64;
+  static_assert(A_ROW % 64 == 0, "dz rows of whole wave-instructions");
   // a strip lane's three dz rows and three halo rows, each region rounded up to whole wave-instructions
   // (64 units), so every DMA instruction moves one kind of one strip lane: its kind, lane and row step
   // are uniform per (instruction, wave)
@@ -74,6 +78,7 @@ struct WgdArgs {
   const unsigned short* xt;   // [N][H][W][Cip]
   float* ws;
   int N, H, W, Cout, Cin, Cop, Cip;
+  unsigned bytesA, bytesX;    // dzt / xt bytes (< 2^31: buffer-descriptor range, see the kernel)
   int strips_w, nseg_strip, m, spb, nsplit, nseg;  // segments: 3m rows; spb per lane; nseg in all
 };
 
@@ -100,9 +105,8 @@ __device__ __forceinline__ void wgd_wait_vm() {
 }
 
 // EXP (timing experiments, experiments build, PMU_WGD_EXP; wrong results on purpose): 1 = no DMA at all
-// (the stage bookkeeping and barriers kept), 2 = the DMA issued from the zero page for every unit (no
-// per-stage source address work), 3 = the DMA as shipped without the stage barrier, 4 = the source
-// addresses formed as shipped (kept live) but the DMA issued from the zero page
+// (the stage bookkeeping and barriers kept), 2 = every DMA through the zero-record descriptor (addresses
+// formed, nothing fetched), 3 = the DMA as shipped without the stage barrier
 template <int WCOF, int WCIF, int WS, int TPS, int EXP = 0>
 __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   using G = WG<WCOF, WCIF, WS, TPS>;
@@ -122,10 +126,8 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   // wave -> (co fragment, ci fragment, strip lane)
   const int wco = wave % WCOF, wci = (wave / WCOF) % WCIF, wsl = wave / (WCOF * WCIF);
 
-  // segment (lane sl, k-th of the block) -> image n, strip column c0, first row y0 (invalid: past the end,
-  // y0 beyond the image so every unit reads the zero page)
   // segment (lane sl, k-th of the block) -> image n, strip column c0, first row y0 (none: k past the
-  // block's segments or the launch's — y0 beyond the image, so every unit reads the zero page)
+  // block's segments or the launch's — y0 beyond the image, so every unit reads zeros)
   auto seg_of = [&](int k, int sl, int& n, int& c0, int& y0) __attribute__((always_inline)) {
     const int s = (split * a.spb + k) * WS + sl;
     if (k >= a.spb || s >= a.nseg) { n = 0; c0 = 0; y0 = a.H + 1; return; }
@@ -138,36 +140,46 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
   // DMA of stage index s (segment k = s / (m+1), step t = s % (m+1)) into ring slot s % NS.  Stage t = 0:
   // halo rows y0-1, y0, y0+1 (the prologue; dz rows unread); t >= 1: dz rows Y..Y+2 and halo rows
   // Y+1..Y+3, Y = y0 + 3(t-1).  Lane unit U = (i * 8 + wave) * 64 + lane of the stage.  Stages are issued
-  // in order, so a cursor (dk, dt, slot) replaces the divisions; a segment's strip position is formed
-  // once per segment (uniform per strip lane), a unit's place in the stage (constant divisions) per stage
-  // — held across stages it cost the 64/64 layout 14 spilled registers.
-  const char* zsrc = reinterpret_cast<const char*>(g_wgd_zero) + 16 * lane;
-  // (element offsets in 32 bits: pmu_conv3x3_wgrad_dma_ok requires both operands below 2^31 elements)
-  const int rsA = a.W * a.Cop, rsX = a.W * a.Cip;
-  // A unit's source offset and row at step t = 1 are formed once per segment (ue, uy); a stage adds the
-  // uniform row step (recomputing the unit's place per stage cost ~25 VALU per unit: the kernel was
-  // issue-bound at ~10 non-MFMA instructions per MFMA).
-  // (re-deriving the row per stage from the unit index instead of holding uy measured 2-8% slower)
-  int ue[NI], uy[NI];
+  // in order, so a cursor (dk, dt, slot) replaces the divisions.
+  // Sources are buffer loads to LDS (buffer_load_dwordx4 ... lds) through SGPR descriptors: the byte
+  // address = descriptor base + soffset (SGPR: the instruction's image row, uniform) + voffset (VGPR: the
+  // lane's pixel and channel within the row, fixed per segment).  Units outside the image or the
+  // channels read zeros through the range check: a lane outside the row carries voffset 0x80000000
+  // (>= every descriptor's size, tensors < 2^31 bytes: pmu_conv3x3_wgrad_dma_ok), an instruction whose
+  // row is outside the image (or whose segment is none) goes through the zero-record descriptor.  A
+  // stage's DMA issue is SALU work plus the DMA instructions — no per-lane address arithmetic (the 64-bit
+  // global_load_lds addresses and their in-image selects were ~10 VALU per DMA: kbench over the c5 shapes
+  // 3.53 ms with them formed but unused vs 3.07 without, EXP 4 / 2 of round 6).
+  // (every descriptor input and soffset is made provably wave-uniform with readfirstlane: otherwise hipcc
+  // wraps each buffer op in a waterfall loop, and a select between whole descriptors went through scratch)
+  const unsigned rbA = 2u * a.W * a.Cop, rbX = 2u * a.W * a.Cip;   // bytes per image row
+  // per instruction i, for the current segment: yr = n*H + y (image row index) and yl = y (row in the
+  // image, range check) at stage t = 1 — uniform; vo = the lane's byte offset within the row
+  int yr[NI], yl[NI];
+  unsigned vo[NI];
   auto seg_setup = [&](int k) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int w = i * 8 + wave;                    // wave-instruction index of the stage (uniform)
       const bool isA = w * 64 < G::A_UNITS;
       const int sl = isA ? (w * 64) / G::A_LANE : (w * 64 - G::A_UNITS) / G::X_LANE;
-      const int r = isA ? w * 64 + lane - sl * G::A_LANE : w * 64 + lane - G::A_UNITS - sl * G::X_LANE;
-      const int j = isA ? r / G::A_ROW : r / G::X_ROW;
-      const int pu = r - j * (isA ? G::A_ROW : G::X_ROW);
+      const int ROW = isA ? G::A_ROW : G::X_ROW;
+      const int rb = isA ? w * 64 - sl * G::A_LANE : w * 64 - G::A_UNITS - sl * G::X_LANE;  // (uniform)
+      const int j = rb / ROW;                                                              // (uniform)
+      const int pu = rb - j * ROW + lane;
       const int px = isA ? pu / G::ARU : pu / G::XRU;
       const int u = isA ? ((pu % G::ARU) ^ wgd_sw<WCOF>(px)) : ((pu % G::XRU) ^ wgd_sw<WCIF>(px));
       int n, c0, y0;
       seg_of(k, sl < WS ? sl : 0, n, c0, y0);
       const int x = isA ? c0 + px : c0 - 1 + px;
       const int c = 8 * u + (isA ? co0 : ci0);
-      const bool in = sl < WS && j < RPS && x >= 0 && x < a.W && c < (isA ? a.Cop : a.Cip);
-      const int y1 = y0 + j + (isA ? 0 : 1);         // the unit's row at stage t = 1
-      uy[i] = in ? y1 : -(1 << 28);                  // (outside: never inside [0, H))
-      ue[i] = ((n * a.H + y1) * a.W + x) * (isA ? a.Cop : a.Cip) + c;
+      const int Cp = isA ? a.Cop : a.Cip;
+      const bool in = px < (isA ? SW : SW + 2) && x >= 0 && x < a.W && c < Cp;
+      vo[i] = in ? (unsigned)(x * Cp + c) * 2u : 0x80000000u;
+      const bool rowok = sl < WS && j < RPS;
+      const int y1 = y0 + j + (isA ? 0 : 1);         // the instruction's row at stage t = 1
+      yl[i] = __builtin_amdgcn_readfirstlane(rowok ? y1 : -(1 << 28));  // (outside: never inside [0, H))
+      yr[i] = __builtin_amdgcn_readfirstlane(n * a.H + y1);
     }
   };
   int dk = 0, dt = 0, dslot = 0;
@@ -181,18 +193,18 @@ __global__ __launch_bounds__(512, 2) void wgrad3x3_bf16_dma_kernel(WgdArgs a) {
       if constexpr (EXP == 1) continue;
       const bool isA = (i * 8 + wave) * 64 < G::A_UNITS;   // (uniform)
       const int dy = isA ? dyA : dyX;
-      const int y = uy[i] + dy;
-      const bool ok = (unsigned)y < (unsigned)a.H && (!isA || dt > 0);
-      const int e = ue[i] + dy * (isA ? rsA : rsX);
-      const char* src = (!ok || EXP == 2) ? zsrc
-                            : isA ? reinterpret_cast<const char*>(a.dzt + e) : reinterpret_cast<const char*>(a.xt + e);
-      if constexpr (EXP == 4) {
-        asm volatile("" ::"v"(src));
-        src = zsrc;
-      }
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src),
-                                       (__attribute__((address_space(3))) void*)(stg + (i * 8 + wave) * 1024), 16, 0,
-                                       0);
+      const bool ok = EXP != 2 && (unsigned)(yl[i] + dy) < (unsigned)a.H && (!isA || dt > 0);
+      const int soff = __builtin_amdgcn_readfirstlane((int)((unsigned)(yr[i] + dy) * (isA ? rbA : rbX)));
+      const int nrec = __builtin_amdgcn_readfirstlane(ok ? (int)(isA ? a.bytesA : a.bytesX) : 0);
+#if defined(__HIP_DEVICE_COMPILE__)  // (the descriptor type and builtins exist for the device pass only; a
+                                     // template body using them in the host pass lost the kernel's stub)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<unsigned short*>(isA ? a.dzt : a.xt), 0, nrec, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(stg + (i * 8 + wave) * 1024),
+                                               16, vo[i], soff, 0, 0);
+#else
+      (void)soff; (void)nrec; (void)stg;
+#endif
     }
     dslot = dslot + 1 == NS ? 0 : dslot + 1;
     if (++dt > a.m) {   // (uniform) the next stage starts a new segment
@@ -402,8 +414,9 @@ static WgdGeo wgd_geometry(int N, int H, int W, int Cin, int Cout) {
 // Shapes the LDS-DMA weight gradient takes (the engine's default for bf16 maps at least 16 wide).
 extern "C" int pmu_conv3x3_wgrad_dma_ok(int N, int H, int W, int Cin, int Cout) {
   const long long px = (long long)N * H * W;
-  return N > 0 && H > 0 && W >= SW && Cin > 0 && Cout > 0 && px * ((Cin + 7) & ~7) < (1LL << 31) &&
-         px * ((Cout + 7) & ~7) < (1LL << 31);
+  // (buffer descriptors: each operand below 2^31 bytes, so offsets and the out-of-range marker fit)
+  return N > 0 && H > 0 && W >= SW && Cin > 0 && Cout > 0 && 2 * px * ((Cin + 7) & ~7) < (1LL << 31) &&
+         2 * px * ((Cout + 7) & ~7) < (1LL << 31);
 }
 
 extern "C" size_t pmu_conv3x3_wgrad_ws_bf16_dma(int N, int H, int W, int Cin, int Cout) {
@@ -422,6 +435,8 @@ extern "C" int pmu_conv3x3_wgrad_bf16_dma(const unsigned short* dzt, const unsig
   a.dzt = dzt; a.xt = xt; a.ws = ws;
   a.N = N; a.H = H; a.W = W; a.Cout = Cout; a.Cin = Cin;
   a.Cop = (Cout + 7) & ~7; a.Cip = (Cin + 7) & ~7;
+  a.bytesA = (unsigned)(2LL * N * H * W * a.Cop);
+  a.bytesX = (unsigned)(2LL * N * H * W * a.Cip);
   a.strips_w = g.strips_w; a.nseg_strip = g.nseg_strip; a.m = g.m; a.spb = g.spb; a.nsplit = g.nsplit;
   a.nseg = g.nseg;
   const int nb = pmu_cdiv(Cout, 32 * g.wcof) * pmu_cdiv(Cin, 32 * g.wcif);
@@ -432,13 +447,12 @@ extern "C" int pmu_conv3x3_wgrad_bf16_dma(const unsigned short* dzt, const unsig
     const char* e = pmu_variant_env("PMU_WGD_EXP");
     return e ? atoi(e) : 0;
   }();
-  if (exp_v >= 1 && exp_v <= 4) {
+  if (exp_v >= 1 && exp_v <= 3) {
 #define PMU_WGD_LAUNCH(E)                                                                                   \
     if (g.ws == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 2, 2, 1, E>), grid, blk, 0, st, a);      \
     else if (g.wcof == 2) hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<2, 4, 1, 1, E>), grid, blk, 0, st, a); \
     else hipLaunchKernelGGL((wgrad3x3_bf16_dma_kernel<4, 2, 1, 1, E>), grid, blk, 0, st, a);
-    if (exp_v == 1) { PMU_WGD_LAUNCH(1) } else if (exp_v == 2) { PMU_WGD_LAUNCH(2) }
-    else if (exp_v == 3) { PMU_WGD_LAUNCH(3) } else { PMU_WGD_LAUNCH(4) }
+    if (exp_v == 1) { PMU_WGD_LAUNCH(1) } else if (exp_v == 2) { PMU_WGD_LAUNCH(2) } else { PMU_WGD_LAUNCH(3) }
 #undef PMU_WGD_LAUNCH
   } else
 #endif
