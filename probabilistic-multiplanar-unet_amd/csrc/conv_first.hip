@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256, CIN >= 4 ? 2 : 3) void conv_first_fwd_tile_ker
     red[tid * 8 + 0] = s1lo.x; red[tid * 8 + 1] = s1lo.y; red[tid * 8 + 2] = s1hi.x; red[tid * 8 + 3] = s1hi.y;
     red[tid * 8 + 4] = s2lo.x; red[tid * 8 + 5] = s2lo.y; red[tid * 8 + 6] = s2hi.x; red[tid * 8 + 7] = s2hi.y;
     __syncthreads();
+    // (one thread per (channel quad, value) instead, the same sums in the same order: 406 vs 382 us at c5)
     if (tid < CQ) {
       float t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
       for (int l = 0; l < npl; ++l) {
@@ -312,6 +313,171 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_tile_kernel(FirstWgArgs 
   }
 }
 
+// MFMA form of the tiled weight gradient (Cout = 16 MT, MT = 1, 2, 4; the engine's first layers): per
+// output channel and tap dw[c][k] = sum over pixels g[px][c] * patch[px][k], i.e. a GEMM with M = Cout,
+// N = 9 CIN taps (padded to 16 NN), K = pixels, on v_mfma_f32_16x16x4f32 (fp32, as the first layer runs
+// under autocast).  Lane (i, k) = (lane & 15, lane >> 4) supplies the A element g[px_k][MT i + m] of M tile
+// m (so its MT channels are consecutive: one 4 MT-byte z load and one da load per pixel, 256 / 128 B per
+// 16 lanes) and the B element patch[px_k][tap i + 16 nt].  A wave takes 64 of a tile's 256 pixels, four at
+// a time, with the loads of the next DEPTH groups in flight; accumulators MT x NN x 4 registers instead
+// of the VALU kernel's 4 x 27 per thread (at 210 VGPRs, two waves per SIMD and two pixels in flight:
+// 0.54 ms for c5's 2.1 GB, latency-bound).  Same per-block rows (ws) and row sum as the VALU kernel.
+typedef float pmu_f32x4 __attribute__((ext_vector_type(4)));
+
+template <int CIN, int MT, bool XB>
+__global__ __launch_bounds__(256) void conv_first_wgrad_mfma_kernel(FirstWgArgs a, int tiles_w, int tiles_h,
+                                                                    int ntiles) {
+  constexpr int K9 = CIN * 9, NN = (K9 + 15) / 16, PE = CIN * FT_PH * FT_PW, NPE = (PE + 255) / 256;
+  // (DEPTH 8 at c5: 446 vs 380 us)
+  constexpr int COUT = 16 * MT, DEPTH = 4, ITS = FT_H * FT_W / 16;  // 4-pixel groups per wave and tile
+  static_assert(ITS % DEPTH == 0, "groups per tile");
+  __shared__ float patch[PE];
+  __shared__ float red[4 * COUT * K9];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const DevSrc& s = a.dz.s0;
+  const int H = a.dz.H, W = a.dz.W;
+  const unsigned HW = (unsigned)H * (unsigned)W;
+  float sc[MT], sh[MT], mu[MT], kx[MT], kc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int c = MT * li + m;
+    sc[m] = s.coef[c];
+    sh[m] = s.coef[COUT + c];
+    mu[m] = s.coef[2 * COUT + c];
+    kx[m] = s.coef[3 * COUT + c];
+    kc[m] = s.coef[4 * COUT + c];
+  }
+  int toff[NN];  // the lane's tap of N tile nt: its offset in the patch (-1: padding tap)
+#pragma unroll
+  for (int nt = 0; nt < NN; ++nt) {
+    const int j = li + 16 * nt, ci = j / 9, t = j - 9 * (j / 9);
+    toff[nt] = j < K9 ? (ci * FT_PH + t / 3) * FT_PW + t % 3 : -1;
+  }
+  pmu_f32x4 acc[MT][NN];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt) acc[m][nt] = pmu_f32x4{0.f, 0.f, 0.f, 0.f};
+  const int t_beg = blockIdx.x * FW_TPB, t_end = min(ntiles, t_beg + FW_TPB);
+  const int nj = (t_end - t_beg) * ITS;
+  float pv[NPE];
+  auto load_patch = [&](int tile) { first_patch_load<CIN>(a.planes, tile, tiles_w, tiles_h, H, W, pv); };
+  // group j (flat over the block's tiles): the lane's pixel (clamped past the end: a valid address)
+  auto pixel_of = [&](int j, unsigned& p, int& r, int& c, bool& ok) __attribute__((always_inline)) {
+    const int jj = j < nj ? j : nj - 1;
+    int t = t_beg + jj / ITS;
+    const int q = wave * (FT_H * FT_W / 4) + (jj - (jj / ITS) * ITS) * 4 + lk;
+    r = q / FT_W;
+    c = q - r * FT_W;
+    const int tw = t % tiles_w; t /= tiles_w;
+    const int th = t % tiles_h;
+    const int n = t / tiles_h;
+    const int h = th * FT_H + r, w = tw * FT_W + c;
+    ok = j < nj && h < H && w < W;
+    p = (unsigned)n * HW + (unsigned)(min(h, H - 1) * W + min(w, W - 1));
+  };
+  float zq[DEPTH][MT], dq[DEPTH][MT];
+  unsigned dqb[DEPTH][(MT + 1) / 2];  // (XB) raw bf16 pairs
+  auto issue = [&](int j, int slot) __attribute__((always_inline)) {
+    unsigned p; int r, c; bool ok;
+    pixel_of(j, p, r, c, ok);
+    const size_t e = (size_t)p * COUT + MT * li;
+    const float* zp = s.z + e;
+    if constexpr (MT == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(zp);
+      zq[slot][0] = v.x; zq[slot][1] = v.y; zq[slot][2] = v.z; zq[slot][3] = v.w;
+    } else if constexpr (MT == 2) {
+      const float2 v = *reinterpret_cast<const float2*>(zp);
+      zq[slot][0] = v.x; zq[slot][1] = v.y;
+    } else {
+      zq[slot][0] = *zp;
+    }
+    if constexpr (XB) {
+      const unsigned short* dp = reinterpret_cast<const unsigned short*>(s.x) + e;
+      if constexpr (MT == 4) {
+        const uint2 v = *reinterpret_cast<const uint2*>(dp);
+        dqb[slot][0] = v.x; dqb[slot][1] = v.y;
+      } else if constexpr (MT == 2) {
+        dqb[slot][0] = *reinterpret_cast<const unsigned*>(dp);
+      } else {
+        dqb[slot][0] = *dp;
+      }
+    } else {
+      const float* dp = s.x + e;
+      if constexpr (MT == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(dp);
+        dq[slot][0] = v.x; dq[slot][1] = v.y; dq[slot][2] = v.z; dq[slot][3] = v.w;
+      } else if constexpr (MT == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(dp);
+        dq[slot][0] = v.x; dq[slot][1] = v.y;
+      } else {
+        dq[slot][0] = *dp;
+      }
+    }
+  };
+  auto consume = [&](int j, int slot) __attribute__((always_inline)) {
+    unsigned p; int r, c; bool ok;
+    pixel_of(j, p, r, c, ok);
+    float g[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float d;
+      if constexpr (XB) d = pmu_bf16_f32((unsigned short)(dqb[slot][m >> 1] >> (16 * (m & 1))));
+      else d = dq[slot][m];
+      g[m] = ok ? pmu_bnbwd1(d, zq[slot][m], sc[m], sh[m], mu[m], kx[m], kc[m]) : 0.f;
+    }
+    float b[NN];
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt) {
+      const float v = patch[(toff[nt] < 0 ? 0 : toff[nt]) + r * FT_PW + c];
+      b[nt] = toff[nt] < 0 ? 0.f : v;
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int nt = 0; nt < NN; ++nt) acc[m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(g[m], b[nt], acc[m][nt], 0, 0, 0);
+  };
+  if (t_beg < t_end) {
+    load_patch(t_beg);
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) issue(d, d);
+  }
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    __syncthreads();  // the previous tile's patch reads are done
+#pragma unroll
+    for (int q = 0; q < NPE; ++q)
+      if (tid + 256 * q < PE) patch[tid + 256 * q] = pv[q];
+    __syncthreads();
+    if (tile + 1 < t_end) load_patch(tile + 1);  // in flight under this tile's MFMAs
+    const int j0 = (tile - t_beg) * ITS;
+    for (int ii = 0; ii < ITS; ii += DEPTH) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        consume(j0 + ii + d, d);
+        issue(j0 + ii + d + DEPTH, d);
+      }
+    }
+  }
+  // accumulator element e of (m, nt): channel MT (4 lk + e) + m, tap li + 16 nt; the 4 waves' sums in order
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int nt = 0; nt < NN; ++nt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = li + 16 * nt;
+        if (j < K9) red[(wave * COUT + MT * (4 * lk + e) + m) * K9 + j] = acc[m][nt][e];
+      }
+  __syncthreads();
+  for (int o = tid; o < COUT * K9; o += 256) {
+    float v = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) v += red[wv * COUT * K9 + o];
+    a.ws[(long long)blockIdx.x * COUT * K9 + o] = v;
+  }
+}
+
 // out[o] = sum_r ws[r][o]: block = 64 outputs x 4 row phases (fixed order), fp64 accumulation
 __global__ __launch_bounds__(1024) void rows_sum4_kernel(const float* __restrict__ ws, int R, int Wd,
                                                          float* __restrict__ out) {
@@ -401,9 +567,21 @@ extern "C" int pmu_conv_first_wgrad(const pmu_frame* dz, const float* const* pla
     case 3: hipLaunchKernelGGL((conv_first_wgrad_tile_kernel<3, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
     default: hipLaunchKernelGGL((conv_first_wgrad_tile_kernel<4, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
   }
-    if (dz->src[0].dtype & PMU_DT_X_BF16) PMU_FW_LAUNCH(true)
+#define PMU_FWM_LAUNCH(MTV, XBV)                                                                                  \
+  switch (Cin) {                                                                                                  \
+    case 1: hipLaunchKernelGGL((conv_first_wgrad_mfma_kernel<1, MTV, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
+    case 2: hipLaunchKernelGGL((conv_first_wgrad_mfma_kernel<2, MTV, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
+    case 3: hipLaunchKernelGGL((conv_first_wgrad_mfma_kernel<3, MTV, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
+    default: hipLaunchKernelGGL((conv_first_wgrad_mfma_kernel<4, MTV, XBV>), dim3((unsigned)nb), dim3(256), 0, st, a, tw, th, nt); break; \
+  }
+    const bool xb = dz->src[0].dtype & PMU_DT_X_BF16;
+    if (Cout == 64) { if (xb) PMU_FWM_LAUNCH(4, true) else PMU_FWM_LAUNCH(4, false) }
+    else if (Cout == 32) { if (xb) PMU_FWM_LAUNCH(2, true) else PMU_FWM_LAUNCH(2, false) }
+    else if (Cout == 16) { if (xb) PMU_FWM_LAUNCH(1, true) else PMU_FWM_LAUNCH(1, false) }
+    else if (xb) PMU_FW_LAUNCH(true)
     else PMU_FW_LAUNCH(false)
 #undef PMU_FW_LAUNCH
+#undef PMU_FWM_LAUNCH
   } else {
     nb = pmu_cdiv(P, FWPIX);
     hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, st, a);
