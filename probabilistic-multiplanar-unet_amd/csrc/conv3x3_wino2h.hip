@@ -404,8 +404,27 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
     bmu = a.bmean[j];
     bis = a.binv[j];
   }
+  // (BNR) the producer's z under a round's two tiles (4 outputs each), loaded at the start of the round,
+  // before its stores: loaded per tile between the stores, each tile's z waited (in-order vmcnt) for
+  // every earlier store of the epilogue — four HBM round trips per wave behind the stores, now one (the
+  // second round's).  All four tiles' z up front spilled 18 VGPRs.  Clamped addresses: every lane loads,
+  // unused values are ignored.
+  float zt2[2][4];
 #pragma unroll
   for (int rho = 0; rho < 2; ++rho) {
+    if (BNR) {
+      const int jc = min(j, a.NOUT - 1);
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int t = 4 * kk + 2 * rho + rr;
+        const int oh = h0 + 2 * (2 * tg + (t >> 3)), ow = w0 + 2 * (t & 7);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const long long pix = ((long long)n * a.H + min(oh + (e >> 1), a.H - 1)) * a.W + min(ow + (e & 1), a.W - 1);
+          zt2[rr][e] = a.bz[pix * a.NOUT + jc];
+        }
+      }
+    }
     if (rho) __syncthreads();
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
@@ -420,17 +439,7 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
       const int r = 2 * rho + rr;
       const int t = 4 * kk + r;
       const int oh = h0 + 2 * (2 * tg + (t >> 3)), ow = w0 + 2 * (t & 7);
-      // the producer's z under this tile's 4 outputs, loaded together ahead of the output transform
-      // (clamped addresses: every lane loads, no branch per load; unused values are ignored)
-      float zt[4];
-      if (BNR) {
-        const int jc = min(j, a.NOUT - 1);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const long long pix = ((long long)n * a.H + min(oh + (e >> 1), a.H - 1)) * a.W + min(ow + (e & 1), a.W - 1);
-          zt[e] = a.bz[pix * a.NOUT + jc];
-        }
-      }
+      const float (&zt)[4] = zt2[rr];
       float P[4];
       w2_partial<CH>(acc, CH, r, P);
       // the partner's partial outputs read together and held in registers before any store branch (read
