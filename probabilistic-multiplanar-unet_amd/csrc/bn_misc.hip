@@ -822,7 +822,9 @@ constexpr int HPPB = 2048;  // pixels per block in the fast head kernels
 // waited for on its own).  HU pixels per thread per round, their loads issued together (address
 // clamped to the block's last pixel, only the stores predicated): one pixel per round left a global
 // round trip exposed per pixel for one class (c2: 0.19 -> 0.14 ms); with three classes the batch of
-// four measured slower (c5: 0.31 -> 0.37 ms), so HU = 1 there
+// four measured slower (c5: 0.31 -> 0.37 ms; with the DPP class sums 0.32 vs 0.26), so HU = 1 there.
+// The per-class sum over a pixel's CQ lanes is pmu_group_sum: DPP moves instead of xor shuffles (one
+// ds_bpermute round trip per step): c5 0.286 -> 0.260 ms, c2 0.142 -> 0.138 ms, bit-identical
 template <bool XBF, int HU>
 __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const float* __restrict__ w,
                                                             const float* __restrict__ b, int K, int do_sigmoid,
@@ -860,7 +862,7 @@ __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const fl
       for (int k = 0; k < HEAD_KMAX; ++k) {
         if (k >= K) break;
         float v = fmaf(a.x, wq[k].x, fmaf(a.y, wq[k].y, fmaf(a.z, wq[k].z, a.w * wq[k].w)));
-        for (int o = 1; o < CQ; o <<= 1) v += __shfl_xor(v, o, 64);
+        v = pmu_group_sum(v, CQ);  // (bit-identical to the xor-shuffle butterfly it replaces)
         v += bk[k];
         if (do_sigmoid) v = 1.f / (1.f + expf(-v));
         if (cq == 0 && p < pend) y[(size_t)(n * K + k) * HWu + pix] = v;

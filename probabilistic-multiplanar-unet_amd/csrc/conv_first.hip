@@ -28,6 +28,7 @@ constexpr int FT_H = 8, FT_W = 32, FT_PH = FT_H + 2, FT_PW = FT_W + 2;
 constexpr int FT_TPB = 4;  // tiles per forward block (one block per tile exposed each patch load: 0.35 ms at c5)
 
 typedef float pmu_f2 __attribute__((ext_vector_type(2)));
+typedef float pmu_f32x4 __attribute__((ext_vector_type(4)));
 
 // the (8+2) x (32+2) x CIN patch values of one tile this thread stages (zero outside the image)
 template <int CIN>
@@ -127,6 +128,117 @@ __global__ __launch_bounds__(256, CIN >= 4 ? 2 : 3) void conv_first_fwd_tile_ker
         a.part[((long long)tile * 2 + 0) * a.Cout + 4 * tid + e] = t1[e];
         a.part[((long long)tile * 2 + 1) * a.Cout + 4 * tid + e] = t2[e];
       }
+    }
+  }
+}
+
+// MFMA form of the tiled forward (Cout = 16 MT, MT = 1, 2, 4; the engine's first layers): z[px][c] =
+// bias[c] + sum over k = 9 ci + tap of w[c][k] * patch[px][k], as D[c][px] on v_mfma_f32_16x16x4f32 with
+// K = 9 CIN taps in steps of 4 (zero-padded).  A = w (lane (i, kk): w[16 m + i][4 s + kk], held in
+// registers), B = patch (lane (j, kk): pixel j's tap 4 s + kk, from the tile's LDS patch), so each lane
+// ends with 4 consecutive channels of one pixel: one 16-B z store per M tile.  A wave takes 16 pixels
+// of its tile at a time (4 groups per tile); the per-tile BN partial sums are summed over a group's 16
+// pixel lanes by DPP row sums, then over the 4 waves in order.  The fp32 sums of the VALU kernel come in
+// another order (z equal to within its rounding); one part row per tile as before.
+template <int CIN, int MT>
+__global__ __launch_bounds__(256) void conv_first_fwd_mfma_kernel(FirstArgs a, int tiles_w, int tiles_h, int ntiles) {
+  constexpr int K9 = CIN * 9, KS = (K9 + 3) / 4, PE = CIN * FT_PH * FT_PW, NPE = (PE + 255) / 256;
+  constexpr int COUT = 16 * MT, GPT = FT_H * FT_W / 64;  // 16-pixel groups per wave and tile
+  __shared__ float patch[PE];
+  __shared__ float red[4 * 2 * COUT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const unsigned HW = (unsigned)a.H * (unsigned)a.W;
+  float wa[MT][KS];  // A operand: w[16 m + li][4 s + lk]
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int k = 4 * st + lk;
+      wa[m][st] = k < K9 ? a.w[(16 * m + li) * K9 + k] : 0.f;
+    }
+  int koff[KS];  // B operand: the lane's tap 4 s + lk as a patch offset (-1: padding)
+#pragma unroll
+  for (int st = 0; st < KS; ++st) {
+    const int k = 4 * st + lk, ci = k / 9, t = k - 9 * (k / 9);
+    koff[st] = k < K9 ? (ci * FT_PH + t / 3) * FT_PW + t % 3 : -1;
+  }
+  float4 bq[MT];  // bias of the lane's output channels 16 m + 4 lk .. + 3
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+    bq[m] = a.bias ? *reinterpret_cast<const float4*>(a.bias + 16 * m + 4 * lk) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int t_beg = blockIdx.x * FT_TPB, t_end = min(ntiles, t_beg + FT_TPB);
+  float pv[NPE];
+  first_patch_load<CIN>(a.planes, t_beg, tiles_w, tiles_h, a.H, a.W, pv);
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    __syncthreads();  // the previous tile's patch and partial-sum reads are done
+#pragma unroll
+    for (int q = 0; q < NPE; ++q)
+      if (tid + 256 * q < PE) patch[tid + 256 * q] = pv[q];
+    __syncthreads();
+    if (tile + 1 < t_end) first_patch_load<CIN>(a.planes, tile + 1, tiles_w, tiles_h, a.H, a.W, pv);
+    int t = tile;
+    const int tw = t % tiles_w; t /= tiles_w;
+    const int th = t % tiles_h;
+    const int n = t / tiles_h;
+    const int h0 = th * FT_H, w0 = tw * FT_W;
+    float s1[MT][4], s2[MT][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { s1[m][e] = 0.f; s2[m][e] = 0.f; }
+#pragma unroll 1
+    for (int gi = 0; gi < GPT; ++gi) {
+      const int q0 = (wave * GPT + gi) * 16;  // the group's first pixel in the tile (16 in one tile row)
+      const int r = q0 / FT_W, c = q0 - r * FT_W + li;
+      float b[KS];
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        const float v = patch[(koff[st] < 0 ? 0 : koff[st]) + r * FT_PW + c];
+        b[st] = koff[st] < 0 ? 0.f : v;
+      }
+      pmu_f32x4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m] = pmu_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < KS; ++st) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[m][st], b[st], acc[m], 0, 0, 0);
+      }
+      const int h = h0 + r, w = w0 + c;
+      const bool ok = h < a.H && w < a.W;
+      const unsigned p = (unsigned)n * HW + (unsigned)(min(h, a.H - 1) * a.W + min(w, a.W - 1));
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const float4 zv = make_float4(acc[m][0] + bq[m].x, acc[m][1] + bq[m].y, acc[m][2] + bq[m].z, acc[m][3] + bq[m].w);
+        const float zz[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = ok ? zz[e] : 0.f;
+          s1[m][e] += v;
+          s2[m][e] = fmaf(v, v, s2[m][e]);
+        }
+        if (ok) *reinterpret_cast<float4*>(a.z + (size_t)p * COUT + 16 * m + 4 * lk) = zv;
+      }
+    }
+    if (!a.part) continue;  // (block-uniform)
+    // over the 16 pixel lanes of each channel quad (a DPP row), then over the 4 waves in order
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float t1 = pmu_group_sum(s1[m][e], 16), t2 = pmu_group_sum(s2[m][e], 16);
+        if (li == 0) {
+          red[(wave * 2 + 0) * COUT + 16 * m + 4 * lk + e] = t1;
+          red[(wave * 2 + 1) * COUT + 16 * m + 4 * lk + e] = t2;
+        }
+      }
+    __syncthreads();
+    for (int o = tid; o < 2 * COUT; o += 256) {
+      const int rr = o / COUT, cc = o - rr * COUT;
+      float v = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv) v += red[(wv * 2 + rr) * COUT + cc];
+      a.part[((long long)tile * 2 + rr) * a.Cout + cc] = v;
     }
   }
 }
@@ -322,8 +434,6 @@ __global__ __launch_bounds__(256) void conv_first_wgrad_tile_kernel(FirstWgArgs 
 // a time, with the loads of the next DEPTH groups in flight; accumulators MT x NN x 4 registers instead
 // of the VALU kernel's 4 x 27 per thread (at 210 VGPRs, two waves per SIMD and two pixels in flight:
 // 0.54 ms for c5's 2.1 GB, latency-bound).  Same per-block rows (ws) and row sum as the VALU kernel.
-typedef float pmu_f32x4 __attribute__((ext_vector_type(4)));
-
 template <int CIN, int MT, bool XB>
 __global__ __launch_bounds__(256) void conv_first_wgrad_mfma_kernel(FirstWgArgs a, int tiles_w, int tiles_h,
                                                                     int ntiles) {
@@ -516,12 +626,25 @@ extern "C" int pmu_conv_first_fwd(const float* const* planes, int Cin, int N, in
   const int tw = pmu_cdiv(W, FT_W), th = pmu_cdiv(H, FT_H), nt = N * tw * th;
   const dim3 grid((unsigned)pmu_cdiv(nt, FT_TPB));
   hipStream_t st = (hipStream_t)stream;
-  switch (Cin) {
+#define PMU_FFM_LAUNCH(MTV)                                                                                       \
+  switch (Cin) {                                                                                                  \
+    case 1: hipLaunchKernelGGL((conv_first_fwd_mfma_kernel<1, MTV>), grid, dim3(256), 0, st, a, tw, th, nt); break; \
+    case 2: hipLaunchKernelGGL((conv_first_fwd_mfma_kernel<2, MTV>), grid, dim3(256), 0, st, a, tw, th, nt); break; \
+    case 3: hipLaunchKernelGGL((conv_first_fwd_mfma_kernel<3, MTV>), grid, dim3(256), 0, st, a, tw, th, nt); break; \
+    default: hipLaunchKernelGGL((conv_first_fwd_mfma_kernel<4, MTV>), grid, dim3(256), 0, st, a, tw, th, nt); break; \
+  }
+  // MFMA form for three or four planes (c5: 382 -> 348 us); with one plane the VALU kernel is faster
+  // (c2: 110 vs 124 us; 9 taps are three MFMA steps of the padded K)
+  if (Cin >= 3 && Cout == 64) { PMU_FFM_LAUNCH(4) }
+  else if (Cin >= 3 && Cout == 32) { PMU_FFM_LAUNCH(2) }
+  else if (Cin >= 3 && Cout == 16) { PMU_FFM_LAUNCH(1) }
+  else switch (Cin) {
     case 1: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<1>, grid, dim3(256), 0, st, a, tw, th, nt); break;
     case 2: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<2>, grid, dim3(256), 0, st, a, tw, th, nt); break;
     case 3: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<3>, grid, dim3(256), 0, st, a, tw, th, nt); break;
     default: hipLaunchKernelGGL(conv_first_fwd_tile_kernel<4>, grid, dim3(256), 0, st, a, tw, th, nt); break;
   }
+#undef PMU_FFM_LAUNCH
   PMU_CHECK_LAUNCH();
   return PMU_OK;
 }

@@ -128,6 +128,25 @@ __device__ __forceinline__ unsigned pmu_swap1(unsigned v) { return (unsigned)pmu
 __device__ __forceinline__ float pmu_swap1(float v) {
   return __builtin_bit_cast(float, pmu_swap1(__builtin_bit_cast(int, v)));
 }
+
+// Sum over each group of CQ consecutive lanes (CQ a power of two <= 64, wave-uniform; every lane of the
+// group gets the total) by DPP moves within 16-lane rows — quad permutations [1,0,3,2], [2,3,0,1], then
+// the half-row and row mirrors — and xor shuffles only across rows.  The same operands meet in the same
+// order as the xor butterfly (v += v^1, v^2, v^4, v^8, ...): after each step the lanes being combined hold
+// equal values, so a mirror partner and an xor partner are interchangeable — bit-identical to it, without
+// an LDS round trip (ds_bpermute + lgkmcnt(0)) per step.  Every lane of the wave must be active.
+template <int CTRL>
+__device__ __forceinline__ float pmu_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float pmu_group_sum(float v, int CQ) {
+  if (CQ >= 2) v += pmu_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (CQ >= 4) v += pmu_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (CQ >= 8) v += pmu_dpp<0x141>(v);  // row_half_mirror
+  if (CQ >= 16) v += pmu_dpp<0x140>(v); // row_mirror
+  for (int o = 16; o < CQ; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 __device__ __forceinline__ float4 pmu_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float4 pmu_ld4(const unsigned short* p) {
   const uint2 u = *reinterpret_cast<const uint2*>(p);
