@@ -189,6 +189,22 @@ def test_library_rejects_bad_arguments_without_gpu():
     assert cdll.pmu_conv3x3_tiles(32, 256, 256) == 32 * 32 * 8
 
 
+def test_wgrad_dma_shape_rule_without_gpu():
+    """The bf16 weight gradient's buffer descriptors need each operand below 2^31 bytes (their
+    out-of-range marker is voffset 0x80000000) and 16-wide maps: pmu_conv3x3_wgrad_dma_ok, a host
+    function, admits c5's largest shapes and refuses what would overflow (the engine then takes the
+    register-staged kernel)."""
+    from pmu_hip._lib import LIB_PATH, load_library
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("library not built")
+    cdll = load_library()
+    ok = cdll.pmu_conv3x3_wgrad_dma_ok
+    assert ok(16, 512, 512, 128, 64) and ok(16, 512, 512, 64, 64)       # c5's 512^2 layers: 1.07 GB operands
+    assert not ok(32, 512, 512, 128, 64)                                  # x at 2.1 GB
+    assert not ok(64, 512, 512, 64, 128)                                  # dz at 4.3 GB
+    assert not ok(2, 64, 15, 64, 64)                                      # narrower than a strip
+
+
 def test_bench_roofline_peak_by_kernel_family():
     """bench.py prices the dominant kernel against the MFMA peak of the dtype it computes in."""
     import bench

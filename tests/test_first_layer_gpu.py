@@ -19,14 +19,19 @@ def _planes(N, Cin, H, W, g, dev):
     return x, [x[:, c].contiguous().to(dev) for c in range(Cin)]
 
 
+@pytest.mark.parametrize("xb", [False, True])
 @pytest.mark.parametrize("N,Cin,H,W,Cout", [(2, 3, 37, 45, 64), (1, 1, 16, 64, 32), (3, 4, 9, 70, 16)])
-def test_conv_first_wgrad_bnbwd(dev, N, Cin, H, W, Cout):
+def test_conv_first_wgrad_bnbwd(dev, N, Cin, H, W, Cout, xb):
+    """xb: da stored as bf16 (the c5 path: the second conv's *_dxb input gradient), the reference on the
+    same bf16-rounded values."""
     import ctypes
     from pmu_hip import _lib as L
     from pmu_hip.engine import Src, frame_of
     g = torch.Generator().manual_seed(H * 7 + Cin)
     x, planes = _planes(N, Cin, H, W, g, dev)
     da = torch.randn(N, H, W, Cout, generator=g)
+    if xb:
+        da = da.to(torch.bfloat16).float()
     z = torch.randn(N, H, W, Cout, generator=g)
     coef = torch.cat([torch.rand(Cout, generator=g) + 0.5, torch.randn(Cout, generator=g) * 0.3,
                       torch.randn(Cout, generator=g) * 0.1, torch.randn(Cout, generator=g) * 0.1,
@@ -38,7 +43,8 @@ def test_conv_first_wgrad_bnbwd(dev, N, Cin, H, W, Cout):
     ws = torch.empty(wsb // 4 + 1, device=dev)
     dw = torch.empty(Cout, Cin, 3, 3, device=dev)
     arr = (ctypes.c_void_p * Cin)(*[p.data_ptr() for p in planes])
-    src = Src(da.to(dev), L.SRC_BNBWD, coef.to(dev), z=z.to(dev))   # (kept alive over the call)
+    dax = da.to(torch.bfloat16).view(torch.int16).to(dev) if xb else da.to(dev)
+    src = Src(dax, L.SRC_BNBWD, coef.to(dev), z=z.to(dev))   # (kept alive over the call)
     f = frame_of([src], N, H, W)
     L.call("pmu_conv_first_wgrad", f, arr, Cin, Cout, dw.data_ptr(), ws.data_ptr(), wsb, L.stream())
     torch.cuda.synchronize()
