@@ -428,9 +428,6 @@ static bool wgw_v16() {  // PMU_WGRAD_WINO=16x16: the 16x16x4 layout (all compon
 static int wgw_wco(int Cout) {
   static const bool w64 = [] {
     const char* e = pmu_variant_env("PMU_WGW64");
-#ifdef PMU_EXPERIMENTS
-    if (pmu_variant_env("PMU_WINO_EXP")) return false;  // the timing experiments are 32-channel kernels
-#endif
     return !(e && atoi(e) == 0);
   }();
   return (w64 && !wgw_v16() && Cout % 64 == 0) ? 64 : 32;
@@ -492,8 +489,11 @@ extern "C" int pmu_conv3x3_wgrad_wino(const float* dzt, const float* xt, int N, 
     return e ? atoi(e) : 0;
   }();
   if (exp_ == 1 || exp_ == 3) {
+    const bool w64 = wgw_wco(Cout) == 64;  // (the shipped 1024-thread layout when it applies)
     if (v16 && exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino_kernel<1>), grid, dim3(NT), 0, st, a);
     else if (v16) hipLaunchKernelGGL((wgrad3x3_wino_kernel<3>), grid, dim3(NT), 0, st, a);
+    else if (exp_ == 1 && w64) hipLaunchKernelGGL((wgrad3x3_wino32_kernel<1, 64>), grid, dim3(1024), 0, st, a);
+    else if (w64) hipLaunchKernelGGL((wgrad3x3_wino32_kernel<3, 64>), grid, dim3(1024), 0, st, a);
     else if (exp_ == 1) hipLaunchKernelGGL((wgrad3x3_wino32_kernel<1>), grid, dim3(NT), 0, st, a);
     else hipLaunchKernelGGL((wgrad3x3_wino32_kernel<3>), grid, dim3(NT), 0, st, a);
   } else
