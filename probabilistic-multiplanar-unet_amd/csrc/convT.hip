@@ -521,7 +521,10 @@ __device__ __forceinline__ unsigned ct_lds_addr(const float* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(p);
 }
 
-template <bool DGRAD, int EXP = 0>
+// PF2: the operands of chunk c + 2 are loaded while chunk c's MFMAs run (two register sets in
+// alternation), so a chunk's global loads have two chunks' MFMAs (2 x 2048 cycles per wave) to land
+// before their LDS store instead of one
+template <bool DGRAD, int EXP = 0, bool PF2 = false>
 __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
   __shared__ __attribute__((aligned(16))) float As[2][PM * PLS];
   __shared__ __attribute__((aligned(16))) float Bs[2][PN * PLS];
@@ -570,9 +573,11 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // staging as macros over plain locals (captured by a lambda, the DGRAD registers went to scratch)
-  float4 ra0, ra1, rb0, rb1, rsc, rsh;
-#define PMU_TLOAD(K0)                                                                                       \
+  // staging as macros over plain locals (captured by a lambda, the DGRAD registers went to scratch);
+  // set S (0, or 1 for PF2's second set)
+  float4 ra0_0, ra1_0, rb0_0, rb1_0, rsc_0, rsh_0;
+  float4 ra0_1, ra1_1, rb0_1, rb1_1, rsc_1, rsh_1;
+#define PMU_TLOAD(K0, S)                                                                                    \
   {                                                                                                        \
     const int k0_ = (K0);                                                                                  \
     long long off_ = k0_ + kq;                                                                             \
@@ -580,39 +585,35 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
       const int ab_ = k0_ / p.Cout;                                                                        \
       off_ = ((long long)(ab_ >> 1) * p.Wd + (ab_ & 1)) * p.Cout + (k0_ - ab_ * p.Cout) + kq;              \
     } else { /* the chunk's BN coefficients travel with its operand (loaded under the MFMAs too) */       \
-      rsc = *reinterpret_cast<const float4*>(p.coef + k0_ + kq);                                           \
-      rsh = *reinterpret_cast<const float4*>(p.coef + p.Cin + k0_ + kq);                                   \
+      rsc_##S = *reinterpret_cast<const float4*>(p.coef + k0_ + kq);                                       \
+      rsh_##S = *reinterpret_cast<const float4*>(p.coef + p.Cin + k0_ + kq);                               \
     }                                                                                                      \
     /* unconditional: rows past M read row 0 (row_base) and are zeroed at the store; a guarded */        \
     /* load became 4 branchy dword loads per row */                                                        \
-    ra0 = *reinterpret_cast<const float4*>(p.a + ab0 + off_);                                              \
-    ra1 = *reinterpret_cast<const float4*>(p.a + ab1 + off_);                                              \
-    rb0 = *reinterpret_cast<const float4*>(br0 + k0_);                                                     \
-    rb1 = *reinterpret_cast<const float4*>(br1 + k0_);                                                     \
+    ra0_##S = *reinterpret_cast<const float4*>(p.a + ab0 + off_);                                          \
+    ra1_##S = *reinterpret_cast<const float4*>(p.a + ab1 + off_);                                          \
+    rb0_##S = *reinterpret_cast<const float4*>(br0 + k0_);                                                 \
+    rb1_##S = *reinterpret_cast<const float4*>(br1 + k0_);                                                 \
   }
-#define PMU_TBN(V) make_float4(fmaxf(0.f, fmaf((V).x, rsc.x, rsh.x)), fmaxf(0.f, fmaf((V).y, rsc.y, rsh.y)), \
-                               fmaxf(0.f, fmaf((V).z, rsc.z, rsh.z)), fmaxf(0.f, fmaf((V).w, rsc.w, rsh.w)))
-#define PMU_TSTORE(BUF)                                                                                     \
+#define PMU_TBN(V, S) make_float4(fmaxf(0.f, fmaf((V).x, rsc_##S.x, rsh_##S.x)), fmaxf(0.f, fmaf((V).y, rsc_##S.y, rsh_##S.y)), \
+                                  fmaxf(0.f, fmaf((V).z, rsc_##S.z, rsh_##S.z)), fmaxf(0.f, fmaf((V).w, rsc_##S.w, rsh_##S.w)))
+#define PMU_TSTORE(BUF, S)                                                                                  \
   {                                                                                                        \
     if constexpr (!DGRAD && EXP != 2) { /* BN + ReLU of the producer, in registers */                     \
-      ra0 = PMU_TBN(ra0);                                                                                  \
-      ra1 = PMU_TBN(ra1);                                                                                  \
+      ra0_##S = PMU_TBN(ra0_##S, S);                                                                       \
+      ra1_##S = PMU_TBN(ra1_##S, S);                                                                       \
     }                                                                                                      \
-    if (!rok0) ra0 = make_float4(0.f, 0.f, 0.f, 0.f); /* rows past M stay zero */                          \
-    if (!rok1) ra1 = make_float4(0.f, 0.f, 0.f, 0.f);                                                      \
-    *reinterpret_cast<float4*>(&As[BUF][rl0 * PLS + kq]) = ra0;                                            \
-    *reinterpret_cast<float4*>(&As[BUF][rl1 * PLS + kq]) = ra1;                                            \
-    *reinterpret_cast<float4*>(&Bs[BUF][rl0 * PLS + kq]) = rb0;                                            \
-    *reinterpret_cast<float4*>(&Bs[BUF][rl1 * PLS + kq]) = rb1;                                            \
+    if (!rok0) ra0_##S = make_float4(0.f, 0.f, 0.f, 0.f); /* rows past M stay zero */                      \
+    if (!rok1) ra1_##S = make_float4(0.f, 0.f, 0.f, 0.f);                                                  \
+    *reinterpret_cast<float4*>(&As[BUF][rl0 * PLS + kq]) = ra0_##S;                                        \
+    *reinterpret_cast<float4*>(&As[BUF][rl1 * PLS + kq]) = ra1_##S;                                        \
+    *reinterpret_cast<float4*>(&Bs[BUF][rl0 * PLS + kq]) = rb0_##S;                                        \
+    *reinterpret_cast<float4*>(&Bs[BUF][rl1 * PLS + kq]) = rb1_##S;                                        \
   }
 
   const int nch = p.K / PK;
-  PMU_TLOAD(0)
-  PMU_TSTORE(0)
-  __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    const int cur = c & 1;
-    if (c + 1 < nch) PMU_TLOAD((c + 1) * PK)
+  // one chunk's MFMAs on LDS buffer CUR
+  auto chunk_mfma = [&](int cur) __attribute__((always_inline)) {
     // the chunk's operands in two halves (k-steps 0-3, then 4-7), the second half's reads in flight
     // under the first half's 16 MFMAs (one wait for all eight reads exposed the LDS latency)
     // (explicit ds_read_b128 + waits: the compiler's own wait was one lgkmcnt(0) for all eight)
@@ -647,8 +648,32 @@ __global__ __launch_bounds__(256, 2) void convT_pipe_kernel(PipeArgs p) {
           }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < nch) PMU_TSTORE(cur ^ 1)
-    __syncthreads();
+  };
+  PMU_TLOAD(0, 0)
+  PMU_TSTORE(0, 0)
+  __syncthreads();
+  if constexpr (!PF2) {
+    for (int c = 0; c < nch; ++c) {
+      const int cur = c & 1;
+      if (c + 1 < nch) PMU_TLOAD((c + 1) * PK, 0)
+      chunk_mfma(cur);
+      if (c + 1 < nch) PMU_TSTORE(cur ^ 1, 0)
+      __syncthreads();
+    }
+  } else {
+    // set 1 holds chunk c + 1 at even c, set 0 at odd c: chunk c + 2 goes into the set chunk c came in
+    if (nch > 1) PMU_TLOAD(PK, 1)
+    for (int c = 0; c < nch; c += 2) {
+      if (c + 2 < nch) PMU_TLOAD((c + 2) * PK, 0)
+      chunk_mfma(0);
+      if (c + 1 < nch) PMU_TSTORE(1, 1)
+      __syncthreads();
+      if (c + 1 >= nch) break;
+      if (c + 3 < nch) PMU_TLOAD((c + 3) * PK, 1)
+      chunk_mfma(1);
+      if (c + 2 < nch) PMU_TSTORE(0, 0)
+      __syncthreads();
+    }
   }
 #undef PMU_TLOAD
 #undef PMU_TBN
@@ -800,11 +825,17 @@ static int convT_fwd(const pmu_frame* in, const float* w, const float* wp, const
       const char* e = pmu_variant_env("PMU_CONVT_EXP");
       return e ? atoi(e) : 0;
     }();
+    static const int pf1 = [] {  // PMU_CONVT_PF2=0: one chunk of prefetch (the round-5 kernel; A/B)
+      const char* e = pmu_variant_env("PMU_CONVT_PF2");
+      return e ? atoi(e) == 0 : 0;
+    }();
     if (exp == 1) hipLaunchKernelGGL((convT_pipe_kernel<false, 1>), grid, dim3(256), 0, (hipStream_t)stream, p);
     else if (exp == 2) hipLaunchKernelGGL((convT_pipe_kernel<false, 2>), grid, dim3(256), 0, (hipStream_t)stream, p);
+    else if (pf1) hipLaunchKernelGGL((convT_pipe_kernel<false>), grid, dim3(256), 0, (hipStream_t)stream, p);
     else
 #endif
-    hipLaunchKernelGGL(convT_pipe_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, p);
+    // two chunks of prefetch: kbench over the c2 shapes 1.56 -> 1.42 ms (the K = 1024 layer -22%)
+    hipLaunchKernelGGL((convT_pipe_kernel<false, 0, true>), grid, dim3(256), 0, (hipStream_t)stream, p);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
   }
@@ -852,6 +883,15 @@ extern "C" int pmu_convT2x2_dgrad(const float* du, int Hd, int Wd, int off_h, in
     p.Hd = Hd; p.Wd = Wd; p.off_h = off_h; p.off_w = off_w;
     pipe_grid(p, Cin / PN);
     const dim3 grid = p.xcd ? dim3((unsigned)(pmu_cdiv(M, PM) * p.nnb)) : dim3((unsigned)pmu_cdiv(M, PM), (unsigned)p.nnb);
+#ifdef PMU_EXPERIMENTS
+    static const int pf2 = [] {
+      const char* e = pmu_variant_env("PMU_CONVT_PF2");
+      return e ? atoi(e) : 0;
+    }();
+    if (pf2) hipLaunchKernelGGL((convT_pipe_kernel<true, 0, true>), grid, dim3(256), 0, (hipStream_t)stream, p);
+    else
+#endif
+    // (two chunks of prefetch measured equal here: 1.249 vs 1.244 ms over the c2 shapes)
     hipLaunchKernelGGL(convT_pipe_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, p);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
