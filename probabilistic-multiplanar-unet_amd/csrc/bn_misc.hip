@@ -844,13 +844,25 @@ __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const fl
     bk[k] = (k < K && b) ? b[k] : 0.f;
   }
   const unsigned pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
-  for (unsigned p0 = blockIdx.x * HPPB + pg; p0 < pend; p0 += HU * PG) {  // 32-bit decode (P < 2^31)
-    float4 zx[HU];
+  // a round's loads; with HU > 1 the next round's are issued before this round's stores (waiting for
+  // them then does not wait, in-order vmcnt, for those stores: c2 138 -> 134 us); with HU = 1 that
+  // measured slower (c5 260 -> 349 us), so a round loads its own pixel there
+  auto load_round = [&](unsigned q0, float4 (&zo)[HU]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < HU; ++u) {
-      const unsigned p = min(p0 + u * PG, pend - 1);
+      const unsigned p = min(q0 + u * PG, pend - 1);
       const long long i = (long long)p * C + 4 * cq;
-      zx[u] = XBF ? pmu_ld4(reinterpret_cast<const unsigned short*>(f.s0.x) + i) : pmu_ld4(f.s0.x + i);
+      zo[u] = XBF ? pmu_ld4(reinterpret_cast<const unsigned short*>(f.s0.x) + i) : pmu_ld4(f.s0.x + i);
+    }
+  };
+  float4 zx[HU], zn[HU];
+  const unsigned pfirst = blockIdx.x * HPPB + pg;
+  if (HU > 1 && pfirst < pend) load_round(pfirst, zx);
+  for (unsigned p0 = pfirst; p0 < pend; p0 += HU * PG) {  // 32-bit decode (P < 2^31)
+    if constexpr (HU > 1) {
+      if (p0 + HU * PG < pend) load_round(p0 + HU * PG, zn);
+    } else {
+      load_round(p0, zx);
     }
 #pragma unroll
     for (int u = 0; u < HU; ++u) {
@@ -867,6 +879,10 @@ __global__ __launch_bounds__(256) void head_fwd_fast_kernel(DevFrame f, const fl
         if (do_sigmoid) v = 1.f / (1.f + expf(-v));
         if (cq == 0 && p < pend) y[(size_t)(n * K + k) * HWu + pix] = v;
       }
+    }
+    if constexpr (HU > 1) {
+#pragma unroll
+      for (int u = 0; u < HU; ++u) zx[u] = zn[u];
     }
   }
 }
@@ -1138,21 +1154,37 @@ __global__ __launch_bounds__(256) void head_dz_kernel(const float* __restrict__ 
   const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
   const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, kxv[4] = {kx.x, kx.y, kx.z, kx.w}, kcv[4] = {kc.x, kc.y, kc.z, kc.w};
   const unsigned HWu = (unsigned)HW, pend = (unsigned)min(P, (long long)(blockIdx.x + 1) * HPPB);
-  for (unsigned p0 = blockIdx.x * HPPB + pg; p0 < pend; p0 += B * PG) {
-    float4 zz[B];
-    float g[B][KT];
+  // a batch's raw loads (z, dy, and y when SIG), clamped to the block's last pixel; the next batch's are
+  // issued before this batch's stores, so waiting for them does not wait (in-order vmcnt) for those stores
+  float4 zz[B], zn[B];
+  float dyv[B][KT], yv[B][KT], dyn[B][KT], yn[B][KT];
+  auto load_batch = [&](unsigned q0, float4 (&zo)[B], float (&dyo)[B][KT], float (&yo)[B][KT])
+      __attribute__((always_inline)) {
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-      const unsigned p = min(p0 + b * PG, pend - 1);
+      const unsigned p = min(q0 + b * PG, pend - 1);
       const unsigned n = p / HWu, pix = p - n * HWu;
-      zz[b] = *reinterpret_cast<const float4*>(z + (size_t)p * C + 4 * cq);
+      zo[b] = *reinterpret_cast<const float4*>(z + (size_t)p * C + 4 * cq);
 #pragma unroll
       for (int k = 0; k < KT; ++k) {
         const size_t i = (size_t)(n * KT + k) * HWu + pix;
-        g[b][k] = dy[i];
-        if (SIG) { const float sg = y[i]; g[b][k] = g[b][k] * (sg * (1.f - sg)); }
+        dyo[b][k] = dy[i];
+        if (SIG) yo[b][k] = y[i];
       }
     }
+  };
+  const unsigned pfirst = blockIdx.x * HPPB + pg;
+  if (pfirst < pend) load_batch(pfirst, zz, dyv, yv);
+  for (unsigned p0 = pfirst; p0 < pend; p0 += B * PG) {
+    if (p0 + B * PG < pend) load_batch(p0 + B * PG, zn, dyn, yn);
+    float g[B][KT];
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        g[b][k] = dyv[b][k];
+        if (SIG) { const float sg = yv[b][k]; g[b][k] = g[b][k] * (sg * (1.f - sg)); }
+      }
 #pragma unroll
     for (int b = 0; b < B; ++b) {
       const unsigned p = p0 + b * PG;
@@ -1173,6 +1205,12 @@ __global__ __launch_bounds__(256) void head_dz_kernel(const float* __restrict__ 
             make_uint2(pmu_pk_bf16(r[0], r[1]), pmu_pk_bf16(r[2], r[3]));
       else
         *reinterpret_cast<float4*>(static_cast<float*>(out) + (size_t)p * C + 4 * cq) = make_float4(r[0], r[1], r[2], r[3]);
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      zz[b] = zn[b];
+#pragma unroll
+      for (int k = 0; k < KT; ++k) { dyv[b][k] = dyn[b][k]; yv[b][k] = yn[b][k]; }
     }
   }
 }
