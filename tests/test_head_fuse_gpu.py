@@ -83,3 +83,36 @@ def test_unet_backward_bit_identical(dev, bf16, channels, classes, filters, N, H
         engine.CFG.head_fuse = old
     for k in grads[0]:
         assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+@pytest.mark.parametrize("K,C,sig", [(1, 8, True), (3, 16, False), (3, 64, False), (1, 64, True), (2, 128, False),
+                                     (4, 256, True)])
+@pytest.mark.parametrize("xbf", [False, True])
+def test_head_fwd_fast_vs_fp64(dev, K, C, sig, xbf):
+    """pmu_head1x1_fwd's channel-quad fast path (OutConv on the last layer's BN+ReLU, unet_parts.py:70-76):
+    the per-class sum over a pixel's C/4 quad lanes by DPP row moves (pmu_group_sum, plus xor shuffles
+    across rows for C/4 = 32, 64) against the fp64 sum of the same products; the source's x in fp32 or
+    bf16 (autocast's activations)."""
+    from pmu_hip import _lib as L
+    from pmu_hip.engine import Src, frame_of
+    N, H, W = 2, 37, 45
+    g = torch.Generator().manual_seed(13 + K + C)
+    z = torch.randn(N, H, W, C, generator=g)
+    if xbf:
+        z = z.to(torch.bfloat16).float()
+    coef = torch.cat([torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.3])
+    w = torch.randn(K, C, generator=g) * 0.3
+    b = torch.randn(K, generator=g)
+    a = torch.relu(z.double() * coef[:C].double() + coef[C:].double())
+    ref = torch.einsum("nhwc,kc->nkhw", a, w.double()) + b.double().view(1, K, 1, 1)
+    if sig:
+        ref = torch.sigmoid(ref)
+    zx = z.to(torch.bfloat16).view(torch.int16).to(dev) if xbf else z.to(dev)
+    src = Src(zx, L.SRC_BNRELU, coef.to(dev))
+    f = frame_of([src], N, H, W)
+    y = torch.full((N, K, H, W), float("nan"), device=dev)
+    wd, bd = w.to(dev), b.to(dev)
+    L.call("pmu_head1x1_fwd", f, wd.data_ptr(), bd.data_ptr(), K, int(sig), y.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert not torch.isnan(y).any()
+    assert (y.double().cpu() - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
