@@ -135,6 +135,27 @@ def main():
         bnr2 = bnr(L.lib().pmu_conv3x3_tiles_wino2h(N, H, W))
         bnrd = bnr(L.lib().pmu_conv3x3_tiles_dma(N, H, W, Cin, cpo))
         dxb = torch.empty(N, H, W, Cin, dtype=torch.int16, device=dev)
+        # the c5 operand streams (frame_stream_kernel): BN-backward dz from a bf16 activation gradient (the
+        # *_dxb dx), and the max-pooled BN+ReLU operand with its unpooled skip half written in the same pass
+        dab = torch.randn(N, H, W, Cout, device=dev).to(torch.bfloat16).view(torch.int16)
+        fdzb = frame_of([Src(dab, L.SRC_BNBWD, bco, z=zz)], N, H, W)
+        fpool = frame_of([Src(z, L.SRC_BNRELU, coef, pool=L.POOL_MAX2)], N, H // 2, W // 2)
+        pool_ok = bool(L.lib().pmu_frame_pool_skip_ok(fpool)) and H % 2 == 0
+        pooled = torch.empty(N, H // 2, W // 2, Cin, dtype=torch.int16, device=dev) if pool_ok else None
+        xcat = torch.empty(N, H, W, 2 * Cin, dtype=torch.int16, device=dev) if pool_ok else None
+        # the max-pool backward of a skip level (c5, bf16 parts): C = Cout channels at H x W, the pooled
+        # gradient at H/2 x W/2 — the stats-only pass (BN-backward partials) and the dz pass
+        dpb = torch.randn(N, H // 2, W // 2, Cout, device=dev).to(torch.bfloat16).view(torch.int16)
+        dskb = torch.randn(N, H, W, Cout, device=dev).to(torch.bfloat16).view(torch.int16)
+        mpm, mpi = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+        mpc = bco[:2 * Cout].contiguous()
+        mpart = torch.empty(L.lib().pmu_maxpool2_bwd_bnr_tiles(N, H, W, Cout), 2 * Cout, device=dev)
+        mdz = torch.empty(N, H, W, Cout, dtype=torch.int16, device=dev)
+        px = N * H * W
+        hbm = {"mp_stats_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4),
+               "mp_bnbwd_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4) + px * Cout * 2,"mat_bnrelu": px * Cin * 4 + px * cpi * 2,
+               "mat_bnbwd_xb": px * Cout * (2 + 4) + px * cpo * 2,
+               "mat_pool_skip": px * Cin * 4 + px // 4 * Cin * 2 + px * Cin * 2}
         ops = {
             "dgrad_w4b": lambda: L.call("pmu_conv3x3_dgrad_wino4_bnr", dzt32.data_ptr(), Cout, N, H, W, w4d.data_ptr(),
                                         Cin, *bnr4),
@@ -159,6 +180,15 @@ def main():
                                          dw.data_ptr(), wsb16.data_ptr(), wsbb, s),
             "wgrad_bf16d": lambda: L.call("pmu_conv3x3_wgrad_bf16_dma", dzt.data_ptr(), xt.data_ptr(), N, H, W, Cout,
                                           Cin, dw.data_ptr(), wsd16.data_ptr(), wsbd, s),
+            "mat_bnrelu": lambda: L.call("pmu_frame_to_bf16", fin, cpi, xt.data_ptr(), s),
+            "mat_bnbwd_xb": lambda: L.call("pmu_frame_to_bf16", fdzb, cpo, dzt.data_ptr(), s),
+            "mat_pool_skip": (lambda: L.call("pmu_frame_to_bf16_pool_skip", fpool, pooled.data_ptr(), xcat.data_ptr(),
+                                             2 * Cin, s)) if pool_ok else None,
+            "mp_stats_xb": lambda: L.call("pmu_maxpool2_bwd_bnr_stats_dxb", dpb.data_ptr(), dskb.data_ptr(), zz.data_ptr(),
+                                          mpc.data_ptr(), mpm.data_ptr(), mpi.data_ptr(), N, H, W, Cout,
+                                          mpart.data_ptr(), s),
+            "mp_bnbwd_xb": lambda: L.call("pmu_maxpool2_bwd_bnbwd_dxb", dpb.data_ptr(), dskb.data_ptr(), zz.data_ptr(),
+                                          mpc.data_ptr(), bco.data_ptr(), N, H, W, Cout, Cout, mdz.data_ptr(), s),
             "mat_bf16": lambda: (L.call("pmu_frame_to_bf16", fdz, cpo, dzt.data_ptr(), s),
                                  L.call("pmu_frame_to_bf16", fin, cpi, xt.data_ptr(), s)),
             "fwd_bf16": lambda: L.call("pmu_conv3x3_fwd_bf16", fin, wbf.data_ptr(), b.data_ptr(), Cout,
@@ -200,9 +230,16 @@ def main():
             "wgrad": lambda: L.call("pmu_conv3x3_wgrad", fdz, fin, Cout, dw.data_ptr(), ws.data_ptr(), wsb, s),
         }
         for op in args.ops.split(","):
-            if op not in ops:
+            if ops.get(op) is None:
                 continue
             ms = timeit(ops[op], args.iters)
+            if op in hbm:
+                tot.setdefault(op, [0.0, 0.0])
+                tot[op][0] += ms
+                tot[op][1] += hbm[op]
+                print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  "
+                      f"{hbm[op] / (ms * 1e-3) / 1e9:7.1f} GB/s  ({hbm[op] / 1e6:8.1f} MB algorithmic)", flush=True)
+                continue
             tf = flops / (ms * 1e-3) / 1e12
             tot.setdefault(op, [0.0, 0.0])
             tot[op][0] += ms
@@ -211,7 +248,10 @@ def main():
             print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {ms:8.3f} ms  {tf:7.2f} TF  ({tf / peak * 100:5.1f}%)",
                   flush=True)
     for op, (ms, fl) in tot.items():
-        print(f"TOTAL {op:6s} {ms:8.3f} ms  {fl / (ms * 1e-3) / 1e12:7.2f} TF")
+        if op in hbm:
+            print(f"TOTAL {op:6s} {ms:8.3f} ms  {fl / (ms * 1e-3) / 1e9:7.1f} GB/s")
+        else:
+            print(f"TOTAL {op:6s} {ms:8.3f} ms  {fl / (ms * 1e-3) / 1e12:7.2f} TF")
 
 
 if __name__ == "__main__":

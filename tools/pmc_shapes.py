@@ -6,6 +6,11 @@ kbench's SHAPES order), next to the op's algorithmic bytes:
   dgrad_dmabx c5 LDS-DMA BN-backward input gradient: dz (bf16) + dx (bf16) + the producer's z (fp32) + w
   dgrad_dmax  c5 LDS-DMA input gradient: dz (bf16) + dx (bf16) + w
   fwd_dma     c5 LDS-DMA forward: x (bf16) + z (fp32) + w
+  mat_bnrelu  BN+ReLU bf16 operand: z (fp32) in, x (bf16) out
+  mat_bnbwd_xb BN-backward bf16 dz from the bf16 dx: dx (bf16) + z (fp32) in, dz (bf16) out
+  mat_pool_skip max-pooled BN+ReLU operand + unpooled skip half: z (fp32) in, pooled + skip (bf16) out
+  mp_stats_xb max-pool backward, BN-backward partials only: pooled + skip gradients (bf16) + z (fp32) in
+  mp_bnbwd_xb max-pool backward to the layer's bf16 dz: the same in, dz (bf16) out
 
     python tools/pmc_shapes.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR ITERS [--N 32] [--op dgrad_w4b] [--c5]
 
@@ -42,20 +47,27 @@ def main():
     a = ap.parse_args()
     shapes = [(2 * h, ci, co) for (h, ci, co) in SHAPES] if a.c5 else SHAPES
     fe, wr = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel), per_dispatch(a.write, "WRITE_SIZE", a.kernel)
-    per = 2 + a.iters
+    # kbench's own setup streams the dz and x operands of every shape: two frame_stream dispatches first
+    lead = 2 if a.op.startswith("mat_") else 0
+    per = lead + 2 + a.iters
     assert len(fe) == len(wr) == per * len(shapes), (len(fe), len(wr), per * len(shapes))
     print(f"op {a.op} N {a.N}; bytes per dispatch = (2 FETCH_SIZE + WRITE_SIZE) x 1024")
     print(f"{'H':>4} {'Cin':>5} {'Cout':>5} {'PMC MB':>9} {'alg MB':>9} {'ratio':>6}")
     tp = ta = 0.0
     for s, (H, Cin, Cout) in enumerate(shapes):
-        idx = range(s * per + 2, (s + 1) * per)
+        idx = range(s * per + lead + 2, (s + 1) * per)
         hbm = sum((2 * fe[i] + wr[i]) * 1024 for i in idx) / a.iters
         px = a.N * H * H
         cpi, cpo = (Cin + 7) // 8 * 8, (Cout + 7) // 8 * 8
         alg = {"dgrad_w4b": px * Cout * 4 + px * Cin * 4 + px * Cin * 4 + Cin * Cout * 36 * 4,
                "dgrad_dmabx": px * cpo * 2 + px * Cin * 2 + px * Cin * 4 + Cin * Cout * 9 * 2,
                "dgrad_dmax": px * cpo * 2 + px * Cin * 2 + Cin * Cout * 9 * 2,
-               "fwd_dma": px * cpi * 2 + px * Cout * 4 + Cin * Cout * 9 * 2}[a.op]
+               "fwd_dma": px * cpi * 2 + px * Cout * 4 + Cin * Cout * 9 * 2,
+               "mat_bnrelu": px * Cin * 4 + px * cpi * 2,
+               "mat_bnbwd_xb": px * Cout * (2 + 4) + px * cpo * 2,
+               "mat_pool_skip": px * Cin * 4 + px // 4 * Cin * 2 + px * Cin * 2,
+               "mp_stats_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4),
+               "mp_bnbwd_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4) + px * Cout * 2}[a.op]
         tp += hbm
         ta += alg
         print(f"{H:4d} {Cin:5d} {Cout:5d} {hbm / 1e6:9.1f} {alg / 1e6:9.1f} {hbm / alg:6.2f}")
