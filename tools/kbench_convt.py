@@ -60,12 +60,15 @@ def main():
         wdf, wdd = pack_convT_weights_dma(w, False), pack_convT_weights_dma(w, True)
         wsbb = L.lib().pmu_convT2x2_wgrad_ws_bf16(N, H, W, Cin, Cout)
         wsb16 = torch.empty(max(1, (wsbb + 3) // 4), device=dev)
+        ucat = torch.empty(N, Hd, Wd, 2 * Cout, dtype=torch.int16, device=dev)   # c5: bf16 into the concat operand
         ops = {
             "fwd_bf16": lambda: L.call("pmu_convT2x2_fwd_bf16", fin, wbf.data_ptr(), b.data_ptr(), Cout, u.data_ptr(), s),
             "fwd_dma": lambda: L.call("pmu_convT2x2_fwd_dma", xt.data_ptr(), xt.shape[3], N, H, W, wdf.data_ptr(),
                                       b.data_ptr(), Cin, Cout, u.data_ptr(), s),
             "dgrad_bf16": lambda: L.call("pmu_convT2x2_dgrad_bf16", du.data_ptr(), Hd, Wd, 0, 0, wbd.data_ptr(), N, H, W,
                                          Cin, Cout, dx.data_ptr(), s),
+            "fwd_ldb": lambda: L.call("pmu_convT2x2_fwd_dma_ldb", xt.data_ptr(), xt.shape[3], N, H, W, wdf.data_ptr(),
+                                      b.data_ptr(), Cin, Cout, ucat.data_ptr(), 2 * Cout, s),
             "dgrad_dma": lambda: L.call("pmu_convT2x2_dgrad_dma", dut.data_ptr(), dut.shape[3], Hd, Wd, 0, 0,
                                         wdd.data_ptr(), N, H, W, Cin, Cout, dx.data_ptr(), s),
             "wgrad_bf16": lambda: L.call("pmu_convT2x2_wgrad_bf16", xt.data_ptr(), dut.data_ptr(), du.data_ptr(), N, H, W,
@@ -77,10 +80,20 @@ def main():
             "wgrad": lambda: L.call("pmu_convT2x2_wgrad", du.data_ptr(), Hd, Wd, 0, 0, fin, Cout, dw.data_ptr(),
                                     db.data_ptr(), ws.data_ptr(), wsb, s),
         }
+        # algorithmic HBM bytes of the LDS-DMA / bf16 kernels as kbench calls them (fp32 u / dx here; c5's
+        # *_ldb / *_dxb forms store bf16): the pass is bound by these, not by its MFMAs (2 FLOP per 4-6 B)
+        pin = N * H * W
+        hbm = {"fwd_dma": pin * Cin * 2 + 4 * pin * Cout * 4 + Cin * Cout * 4 * 2,
+               "fwd_ldb": pin * Cin * 2 + 4 * pin * Cout * 2 + Cin * Cout * 4 * 2,
+               "dgrad_dma": 4 * pin * Cout * 2 + pin * Cin * 4 + Cin * Cout * 4 * 2,
+               "wgrad_bf16": pin * Cin * 2 + 4 * pin * Cout * (2 + 4) + Cin * Cout * 4 * 4}
         for op in args.ops.split(","):
             if op not in ops:
                 continue
             ms = timeit(ops[op], args.iters)
+            if op in hbm:
+                print(f"{op:6s} H={H:4d} Cin={Cin:5d} Cout={Cout:5d}  {hbm[op] / 1e6:8.1f} MB algorithmic  "
+                      f"{hbm[op] / (ms * 1e-3) / 1e9:7.1f} GB/s", flush=True)
             tf = flops / (ms * 1e-3) / 1e12
             tot.setdefault(op, [0.0, 0.0])
             tot[op][0] += ms
