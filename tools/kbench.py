@@ -152,7 +152,9 @@ def main():
         mpart = torch.empty(L.lib().pmu_maxpool2_bwd_bnr_tiles(N, H, W, Cout), 2 * Cout, device=dev)
         mdz = torch.empty(N, H, W, Cout, dtype=torch.int16, device=dev)
         px = N * H * W
-        hbm = {"mp_stats_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4),
+        hbm = {"mat32": px * Cin * 4 * 2,
+               "mat32_bnbwd": px * Cout * 4 * 3,
+               "mp_stats_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4),
                "mp_bnbwd_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4) + px * Cout * 2,"mat_bnrelu": px * Cin * 4 + px * cpi * 2,
                "mat_bnbwd_xb": px * Cout * (2 + 4) + px * cpo * 2,
                "mat_pool_skip": px * Cin * 4 + px // 4 * Cin * 2 + px * Cin * 2}
@@ -218,6 +220,7 @@ def main():
             "dgrad_w2h": lambda: L.call("pmu_conv3x3_dgrad_wino2h", dzt32.data_ptr(), Cout, N, H, W, w2d.data_ptr(),
                                         Cin, Cin, dx.data_ptr(), None, s),
             "mat32": lambda: L.call("pmu_frame_to_f32", fin, xt32.data_ptr(), s),
+            "mat32_bnbwd": lambda: L.call("pmu_frame_to_f32", fdz, dzt32.data_ptr(), s),
             "fwd_wino": lambda: L.call("pmu_conv3x3_fwd_wino", fin, wwf.data_ptr(), b.data_ptr(), Cout,
                                        out.data_ptr(), partw.data_ptr(), None, s),
             "dgrad_wino": lambda: L.call("pmu_conv3x3_dgrad_wino", fdz, wwd.data_ptr(), Cin, Cin, dx.data_ptr(),

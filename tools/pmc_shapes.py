@@ -9,6 +9,8 @@ kbench's SHAPES order), next to the op's algorithmic bytes:
   mat_bnrelu  BN+ReLU bf16 operand: z (fp32) in, x (bf16) out
   mat_bnbwd_xb BN-backward bf16 dz from the bf16 dx: dx (bf16) + z (fp32) in, dz (bf16) out
   mat_pool_skip max-pooled BN+ReLU operand + unpooled skip half: z (fp32) in, pooled + skip (bf16) out
+  mat32       BN+ReLU fp32 operand (config c2): z in, x out, fp32
+  mat32_bnbwd BN-backward fp32 dz (config c2): da + z in, dz out, fp32
   mp_stats_xb max-pool backward, BN-backward partials only: pooled + skip gradients (bf16) + z (fp32) in
   mp_bnbwd_xb max-pool backward to the layer's bf16 dz: the same in, dz (bf16) out
 
@@ -48,7 +50,7 @@ def main():
     shapes = [(2 * h, ci, co) for (h, ci, co) in SHAPES] if a.c5 else SHAPES
     fe, wr = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel), per_dispatch(a.write, "WRITE_SIZE", a.kernel)
     # kbench's own setup streams the dz and x operands of every shape: two frame_stream dispatches first
-    lead = 2 if a.op.startswith("mat_") else 0
+    lead = 2 if a.op.startswith("mat") else 0
     per = lead + 2 + a.iters
     assert len(fe) == len(wr) == per * len(shapes), (len(fe), len(wr), per * len(shapes))
     print(f"op {a.op} N {a.N}; bytes per dispatch = (2 FETCH_SIZE + WRITE_SIZE) x 1024")
@@ -66,6 +68,8 @@ def main():
                "mat_bnrelu": px * Cin * 4 + px * cpi * 2,
                "mat_bnbwd_xb": px * Cout * (2 + 4) + px * cpo * 2,
                "mat_pool_skip": px * Cin * 4 + px // 4 * Cin * 2 + px * Cin * 2,
+               "mat32": px * Cin * 4 * 2,
+               "mat32_bnbwd": px * Cout * 4 * 3,
                "mp_stats_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4),
                "mp_bnbwd_xb": px // 4 * Cout * 2 + px * Cout * (2 + 4) + px * Cout * 2}[a.op]
         tp += hbm
