@@ -383,7 +383,7 @@ __device__ __forceinline__ void w2_partial(const f32x4 (&acc)[2][8], int h, int 
 // epilogue: lane holds M[comp (half CH)][tile 4*kk + r of the group][co j0 + 32 cg + 16 h + (lane & 15)];
 // the two component halves of (tg, cg) swap the partial outputs of the co half the other finishes
 // through xb (a free LDS stage), in two rounds of two tiles per lane
-template <bool DGRAD, bool BNR, int CH, int CO>
+template <bool DGRAD, bool BNR, int CH, int CO, bool NOST = false>
 __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, int w0, int j0, int spatial,
                                                 const f32x4 (&acc)[2][8], float* xb, float* red, float bias) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kk = lane >> 4;
@@ -472,7 +472,7 @@ __device__ __forceinline__ void wino2h_epilogue(const W2Args& a, int n, int h0, 
             s1 += g;
             s2 = fmaf(g, (zz - bmu) * bis, s2);
           }
-          if (!ok) continue;
+          if (!ok || NOST) continue;
           PMU_DCHECK((((long long)n * a.H + hh) * a.W + ww) < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
           rowp[(unsigned)(ww * ld)] = v;
         }
@@ -516,7 +516,8 @@ struct W2Block {
 // EXP (timing experiments, experiments build, PMU_WINO2H_EXP; wrong results on purpose): 1 = no restaging
 // (every chunk reads stage 0, no DMA after the first; the chunk barrier kept), 2 = that without the barrier,
 // 3 = the DMA issued as usual but never waited for (a bare s_barrier per chunk), 4 = only the operand image
-// restaged (U DMA'd for the first chunk only), 5 = only U restaged
+// restaged (U DMA'd for the first chunk only), 5 = only U restaged, 6 = no z stores, 7 = 3 in the first chunk
+// of every pass after the first only
 template <bool DGRAD, bool BNR, int CH, int CO_, bool P64, int EXP = 0>
 __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, const unsigned (&goff)[W2Cfg<CO_>::NGL],
                                             float* smem) {
@@ -581,7 +582,9 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
         w2_step<CH>(pa, ua0, ua1, acc);                  // channel 2*kk
         w2_step<CH>(pa + 4, ua0 + CO * NCP * 4, ua1 + CO * NCP * 4, acc);  // channel 2*kk + 1
       }
-      if (EXP == 3) {  // timing experiment: the DMA issued but never waited for (a bare barrier)
+      if (EXP == 3 || (EXP == 7 && ch == 0 && p > 0)) {  // timing experiment: the DMA issued but never
+        // waited for (a bare barrier); 7: only in a pass's first chunk, where the wait also covers the previous
+        // pass's epilogue stores (in-order vmcnt)
         __builtin_amdgcn_s_barrier();
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next chunk's DMA has landed
@@ -591,7 +594,7 @@ __device__ __forceinline__ void wino2h_main(const W2Args& a, const W2Block& B, c
     int ne = B.n, h0e = B.h0, w0e = B.w0;
     asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
     float* xb = smem + ((gi - 1) & 1) * STAGE;
-    wino2h_epilogue<DGRAD, BNR, CH, CO>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    wino2h_epilogue<DGRAD, BNR, CH, CO, EXP == 6>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
     if (p + 1 < B.npass) {  // block-uniform: restore the zero units the exchange overwrote
 #pragma unroll
       for (int r = 0; r < NGL; ++r)
@@ -730,6 +733,8 @@ int launch_wino2h(const float* x, int KC, int N, int H, int W, const float* wp, 
     else if (exp_v == 2) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 2>), grid, dim3(1024), 0, st, a);
     else if (exp_v == 4) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 4>), grid, dim3(1024), 0, st, a);
     else if (exp_v == 5) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 5>), grid, dim3(1024), 0, st, a);
+    else if (exp_v == 6) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 6>), grid, dim3(1024), 0, st, a);
+    else if (exp_v == 7) hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 7>), grid, dim3(1024), 0, st, a);
     else hipLaunchKernelGGL((conv3x3_wino2h_kernel<false, false, 64, true, 3>), grid, dim3(1024), 0, st, a);
     PMU_CHECK_LAUNCH();
     return PMU_OK;
