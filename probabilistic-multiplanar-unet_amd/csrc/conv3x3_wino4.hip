@@ -478,7 +478,7 @@ __device__ __forceinline__ void w4_partial(const f32x4 (&acc)[2][18], int h, int
 // in acc[h][cl][r].  The two waves of a tile group (halves 0 and 1) swap the partial outputs of the
 // co half the other one finishes through xb (a free LDS stage), in two rounds of two tiles per lane;
 // wave (tg, CH) then finishes co half CH: bias, store, BN partial sums.
-template <bool DGRAD, bool BNR, int CH>
+template <bool DGRAD, bool BNR, int CH, int EXP = 0>
 __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, int w0, int j0, int spatial,
                                                const f32x4 (&acc)[2][18], float* xb, float* red, float bias) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kk = lane >> 4;
@@ -491,7 +491,7 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
   if (!DGRAD) { dst = a.out0 + j; ld = a.NOUT; }
   else if (j < a.split) { dst = a.out0 + j; ld = a.split; }
   else { dst = a.out1 + (j - a.split); ld = a.NOUT - a.split; }
-  float s1 = 0.f, s2 = 0.f;
+  float s1 = 0.f, s2 = 0.f, sink = 0.f;
   float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
   if (BNR && jok) {
     bsc = a.bcoef[j];
@@ -518,7 +518,11 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
       // the producer's z under this tile's 16 outputs, loaded before the output transform so the
       // loads are in flight together (issued one per store, each waited for on its own)
       float zt[16];
-      if (BNR) {
+      if (BNR && EXP == 8) {  // timing experiment: one z load (the column's first pixel) for all 16
+        const float z0 = a.bz[min(j, a.NOUT - 1)];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) zt[e] = z0;
+      } else if (BNR) {
         const int jc = min(j, a.NOUT - 1);  // clamped: every lane loads (no branch per load), unused ones ignored
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -560,6 +564,10 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
             s1 += g;
             s2 = fmaf(g, (zz - bmu) * bis, s2);
           }
+          if (EXP == 6) {  // timing experiment: no stores (the values kept live through one sum)
+            sink += ok ? v : 0.f;
+            continue;
+          }
           if (!ok) continue;
           PMU_DCHECK((((long long)n * a.H + hh2) * a.W + ww) < (long long)a.N * a.H * a.W && j < a.NOUT, PMU_DBG_OUTPUT);
           rowp[(unsigned)(ww * ld)] = v;
@@ -567,6 +575,7 @@ __device__ __forceinline__ void wino4_epilogue(const W4Args& a, int n, int h0, i
       }
     }
   }
+  if (EXP == 6 && a.N < 0) dst[0] = sink;  // (never true: keeps the experiment's values live)
   if (a.part) {  // forward: BN partial sums of the output; input gradient: of the producer's BN backward
     s1 += __shfl_xor(s1, 16, 64);
     s2 += __shfl_xor(s2, 16, 64);
@@ -603,7 +612,7 @@ struct W4Block {
 
 // the pass / chunk pipeline of a wave of component half CH (waves 4 CH .. 4 CH + 3); PM: the patch read —
 // 0 b32 per channel, 1 b32 with step 1's patch read under step 0's MFMAs, 2 b64 channel pairs (default)
-template <bool DGRAD, bool BNR, int CH, int PM>
+template <bool DGRAD, bool BNR, int CH, int PM, int EXP = 0>
 __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, const unsigned (&goff)[NGL],
                                            float* smem) {
   float* red = smem + 2 * STAGE;
@@ -668,7 +677,7 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
     int ne = B.n, h0e = B.h0, w0e = B.w0;
     asm volatile("" : "+s"(ne), "+s"(h0e), "+s"(w0e));
     float* xb = smem + ((gi - 1) & 1) * STAGE;
-    wino4_epilogue<DGRAD, BNR, CH>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
+    wino4_epilogue<DGRAD, BNR, CH, EXP>(a, ne, h0e, w0e, j0, B.spatial, acc, xb, red, bias);
     if (p + 1 < B.npass) {  // block-uniform: every wave takes the barrier
       // the exchange overwrote xb's stage: restore its zero units (each thread its own) before the
       // next pass reads it
@@ -692,7 +701,9 @@ __device__ __forceinline__ void wino4_main(const W4Args& a, const W4Block& B, co
 // rest, each for its tile group's 16 tiles x all 32 output channels.
 // BNR (input gradient only): the producer's BN-backward partial sums in the epilogue (a.bz set) — a
 // compile-time choice, so the z loads and their uses sit in straight-line code
-template <bool DGRAD, bool BNR, int PM>
+// EXP (timing experiments, experiments build, PMU_WINO4_EXP; wrong results on purpose): 6 = no output
+// stores, 8 = no z loads in the BN-backward epilogue
+template <bool DGRAD, bool BNR, int PM, int EXP = 0>
 __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE + RED_FLOATS];
   const int tid = threadIdx.x;
@@ -749,8 +760,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_wino4_kernel(W4Args a) {
   B.gin = gin;
   B.gzero = gzero;
   if (a.prio && (tid >> 8)) __builtin_amdgcn_s_setprio(1);
-  if (tid >> 8) wino4_main<DGRAD, BNR, 1, PM>(a, B, goff, smem);
-  else wino4_main<DGRAD, BNR, 0, PM>(a, B, goff, smem);
+  if (tid >> 8) wino4_main<DGRAD, BNR, 1, PM, EXP>(a, B, goff, smem);
+  else wino4_main<DGRAD, BNR, 0, PM, EXP>(a, B, goff, smem);
 }
 
 int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, const float* bias, int NOUT,
@@ -828,6 +839,18 @@ int launch_wino4(const float* x, int KC, int N, int H, int W, const float* wp, c
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)blocks);
 #ifdef PMU_EXPERIMENTS
+  static const int exp_v = [] {
+    const char* e = pmu_variant_env("PMU_WINO4_EXP");
+    return e ? atoi(e) : 0;
+  }();
+  if (dgrad && pm == 2 && (exp_v == 6 || exp_v == 8)) {
+    if (bz && exp_v == 6) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, 2, 6>), grid, dim3(NT), 0, st, a);
+    else if (bz) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, 2, 8>), grid, dim3(NT), 0, st, a);
+    else if (exp_v == 6) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, 2, 6>), grid, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, 2>), grid, dim3(NT), 0, st, a);
+    PMU_CHECK_LAUNCH();
+    return PMU_OK;
+  }
   if (dgrad && bz && pm == 0) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, 0>), grid, dim3(NT), 0, st, a);
   else if (dgrad && bz) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, true, 2>), grid, dim3(NT), 0, st, a);
   else if (dgrad && pm == 1) hipLaunchKernelGGL((conv3x3_wino4_kernel<true, false, 1>), grid, dim3(NT), 0, st, a);
